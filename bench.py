@@ -1,0 +1,281 @@
+#!/usr/bin/env python3
+"""Headline benchmark: device-resident 4+2 EC encode + reconstruct of batched
+1 MiB objects on MI355X (BASELINE.json metric, configs[1] + configs[2]).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+        --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
+
+One step = one pass of the hot path over one batch held in HBM:
+  1. Encoder.Encode   of 4096 objects x 1 MiB  (4 data shards read, 2 parity written)
+  2. Encoder.Reconstruct of the same 4096 objects with shards {0,1} erased
+     (survivors 2,3,P0,P1 read, the 2 data shards written)
+Per object the algorithmic traffic of each op is k*S read + 2*S written =
+1.5 MiB, 12 GiB per step per GPU.  `value` = algorithmic bytes
+of all ranks / max-over-ranks time, in GiB/s.  Objects are partitioned across
+ranks (rank r owns global objects [r*4096, (r+1)*4096)): weak scaling, no
+data-path collective; torch.distributed carries only the barrier and the
+max-time reduction.
+
+Extra objects on the JSON line: `roofline` (dominant kernel = the
+gf_apply_vec<4,2> kernel that both ops launch; achieved = algorithmic bytes per
+launch / its HIP-event-timed average launch duration on the launch stream;
+traffic = PMC HBM bytes per launch from the committed rocprofv3 summary,
+profiles/*_pmc.json) and `cpu_baseline` (oracle/gf_oracle.c's AVX2 port of
+klauspost's algorithm over the host cores on a bounded sample, rank 0 at N=1).
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import torch
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+from hummingbird_amd import batch as B  # noqa: E402
+from hummingbird_amd import reedsolomon as RS  # noqa: E402
+
+METRIC = "GiB/s device-resident EC encode+reconstruct, 4+2 @ 1 MiB; % HBM roofline"
+GiB = float(1 << 30)
+MiB = 1 << 20
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+KERNEL_NAME = "gf_apply_vec<4, 2>"
+
+
+def dist_env():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return world, rank, local
+
+
+def partition(n_per_rank: int, rank: int) -> tuple[int, int]:
+    """Global object range [first, first+n) owned by `rank` (weak scaling)."""
+    return rank * n_per_rank, n_per_rank
+
+
+def load_pmc(prefix_glob="profiles/*_pmc.json"):
+    files = sorted(glob.glob(str(ROOT / prefix_glob)))
+    if not files:
+        return None, None
+    data = json.loads(Path(files[-1]).read_text())
+    return data, os.path.relpath(files[-1], ROOT)
+
+
+class Workload:
+    """4+2 batch resident in HBM: objs [n, 1 MiB], parity [n, 512 KiB],
+    rebuilt [n, 512 KiB] (reconstruct target for the erased shards 0,1)."""
+
+    def __init__(self, k, m, n, obj_len, first, erased):
+        self.k, self.m, self.n, self.obj_len = k, m, n, obj_len
+        self.s = obj_len // k
+        self.erased = list(erased)
+        self.enc = RS.New(k, m)
+        self.objs = torch.empty((n, obj_len), dtype=torch.uint8, device="cuda")
+        self.parity = torch.empty((n, m * self.s), dtype=torch.uint8, device="cuda")
+        self.rebuilt = torch.empty((n, len(self.erased) * self.s), dtype=torch.uint8, device="cuda")
+        B.fill_splitmix(self.objs, obj_len, first=first)
+        self.enc_views = B.shard_views(self.objs, k, self.s) + B.shard_views(self.parity, m, self.s)
+        rv = list(self.enc_views)
+        for slot, i in enumerate(self.erased):
+            rv[i] = (self.rebuilt.data_ptr() + slot * self.s, self.rebuilt.stride(0))
+        self.rec_views = rv
+        self.present = [0 if i in self.erased else 1 for i in range(k + m)]
+        # algorithmic bytes per launch: k*S read + (m | e)*S written per object
+        self.enc_bytes = n * (k + m) * self.s
+        self.rec_bytes = n * (k + len(self.erased)) * self.s
+
+    def encode(self):
+        B.encode_views(self.enc, self.enc_views, self.n, self.s)
+
+    def reconstruct(self):
+        B.reconstruct_views(self.enc, self.rec_views, self.present, self.n, self.s)
+
+    def verify(self) -> bool:
+        torch.cuda.synchronize()
+        want = torch.cat([self.objs[:, i * self.s:(i + 1) * self.s] for i in self.erased], dim=1)
+        return bool(torch.equal(self.rebuilt, want))
+
+
+def cpu_baseline(k, m, obj_len, erased, budget_s=12.0, sample_objs=512):
+    """Oracle AVX2 port over the host threads, bounded sample, same two ops."""
+    import numpy as np
+
+    from oracle import coracle as CO
+    from oracle import oracle as O
+
+    threads = CO.cpu_threads()
+    s = obj_len // k
+    objs = CO.fill_objects(0, sample_objs, obj_len)
+    parity = np.empty((sample_objs, m * s), dtype=np.uint8)
+    rebuilt = np.empty((sample_objs, len(erased) * s), dtype=np.uint8)
+    mat = CO.build_matrix(k, m)
+    enc_in = [(objs.ctypes.data + j * s, obj_len) for j in range(k)]
+    enc_out = [(parity.ctypes.data + r * s, m * s) for r in range(m)]
+    present = [0 if i in erased else 1 for i in range(k + m)]
+    surv, inv = O.Encoder(k, m).decode_matrix(present)
+    rows = [inv[i] for i in erased]
+    all_views = enc_in + enc_out
+    rec_in = [all_views[i] for i in surv]
+    rec_out = [(rebuilt.ctypes.data + e * s, len(erased) * s) for e in range(len(erased))]
+    t_total, passes = 0.0, 0
+    while t_total < budget_s or passes == 0:
+        t_total += CO.apply_batch(mat[k:], enc_in, enc_out, sample_objs, s, threads)
+        t_total += CO.apply_batch(rows, rec_in, rec_out, sample_objs, s, threads)
+        passes += 1
+        if passes >= 200:
+            break
+    assert np.array_equal(rebuilt, np.concatenate([objs[:, i * s:(i + 1) * s] for i in erased], axis=1))
+    nbytes = passes * sample_objs * ((k + m) * s + (k + len(erased)) * s)
+    # config 1: one object through an ecSplit-shaped call, single thread
+    one = objs[0].copy()
+    reps = [CO.ecsplit_once(k, m, one, MiB, CO.AVX2, True) for _ in range(100)]
+    reps.sort()
+    return {
+        "value": round(nbytes / t_total / GiB, 3),
+        "unit": "GiB/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{passes} passes x {sample_objs} x 1 MiB objects, encode + reconstruct{{{','.join(map(str, erased))}}}, "
+                  f"{t_total:.1f} s wall, AVX2 nibble-table port of klauspost galMulAVX2Xor "
+                  f"(oracle/gf_oracle.c), {threads} threads, {cpu_model()}",
+        "config1_ecsplit_1mib_single_thread_ms": round(reps[len(reps) // 2] * 1e3, 4),
+    }
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown cpu"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--objects", type=int, default=4096, help="objects per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    args = ap.parse_args()
+
+    world, rank, local = dist_env()
+    torch.cuda.set_device(local)
+    pg = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        pg = dist
+
+    k, m, obj_len, erased = 4, 2, MiB, (0, 1)
+    first, n = partition(args.objects, rank)
+    w = Workload(k, m, n, obj_len, first, erased)
+    stream = torch.cuda.current_stream()
+
+    for _ in range(args.warmup):
+        w.encode()
+        w.reconstruct()
+    ok = w.verify()
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+           torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if pg:
+        pg.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        e0, e1, e2 = ev[i]
+        e0.record(stream)
+        w.encode()
+        e1.record(stream)
+        w.reconstruct()
+        e2.record(stream)
+    torch.cuda.synchronize()
+    if pg:
+        pg.barrier()
+    elapsed = time.perf_counter() - t0
+
+    enc_ms = sum(e0.elapsed_time(e1) for e0, e1, _ in ev) / args.steps
+    rec_ms = sum(e1.elapsed_time(e2) for _, e1, e2 in ev) / args.steps
+    if pg:
+        t = torch.tensor([elapsed, enc_ms, rec_ms, 0.0 if ok else 1.0], dtype=torch.float64, device="cuda")
+        pg.all_reduce(t, op=pg.ReduceOp.MAX)
+        elapsed, enc_ms, rec_ms, bad = t.tolist()
+        ok = bad == 0.0
+
+    step_bytes = w.enc_bytes + w.rec_bytes
+    total_bytes = step_bytes * args.steps * world
+    value = total_bytes / elapsed / GiB
+    ms_per_step = elapsed / args.steps * 1e3
+
+    if rank == 0:
+        launch_bytes = w.enc_bytes  # == rec_bytes for 2 erasures
+        avg_launch_ms = (enc_ms + rec_ms) / 2
+        achieved = launch_bytes / (avg_launch_ms * 1e-3) / 1e9
+        pmc, pmc_file = load_pmc()
+        traffic = None
+        if pmc and KERNEL_NAME in pmc.get("kernels", {}):
+            traffic = pmc["kernels"][KERNEL_NAME].get("hbm_bytes_per_launch")
+        info = B.kernel_info(k, m)
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic: splitmix64 objects (SURVEY.md §8d), generated in HBM",
+            "config": {
+                "workload": "4+2 Encode + Reconstruct{0,1} of 4096 x 1 MiB objects per GPU, device-resident "
+                            "(BASELINE configs[1]+[2])",
+                "k": k, "m": m, "object_bytes": obj_len, "shard_bytes": w.s,
+                "objects_per_gpu": n, "global_objects": n * world,
+                "parallelism": f"object-partition x{world}",
+                "bytes_per_step_per_gpu": step_bytes,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "kernel": KERNEL_NAME,
+                "bytes_per_launch": launch_bytes,
+                "encode_ms_per_launch": round(enc_ms, 4),
+                "reconstruct_ms_per_launch": round(rec_ms, 4),
+                "traffic_source": pmc_file,
+                "tile_bytes": info["tile_bytes"], "blocks_per_cu": info["blocks_per_cu"],
+            },
+            "object_data_gib_s": round(value * k / (k + m), 2),
+            "parity_ok": ok,
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(k, m, obj_len, erased, budget_s=args.cpu_budget)
+        print(json.dumps(line), flush=True)
+    if pg:
+        pg.destroy_process_group()
+    if not ok:
+        sys.exit(3)
+
+
+if __name__ == "__main__":
+    main()

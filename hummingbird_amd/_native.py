@@ -1,0 +1,108 @@
+"""ctypes binding of libhbec.so (include/hbec.h).
+
+There is deliberately no fallback: if the native library is missing or fails
+to load, every entry point raises.  The GF arithmetic runs only in the HIP
+kernels of libhbec.so.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+_PKG = Path(__file__).resolve().parent
+LIB_PATH = Path(os.environ.get("HBEC_LIB", _PKG / "libhbec.so"))
+
+HBEC_OK = 0
+ERR_INV_SHARD_NUM = -1
+ERR_MAX_SHARD_NUM = -2
+ERR_TOO_FEW_SHARDS = -3
+ERR_SHARD_NO_DATA = -4
+ERR_SHARD_SIZE = -5
+ERR_SINGULAR = -6
+ERR_INVALID_ARG = -7
+ERR_DEVICE = -8
+ERR_NOMEM = -9
+ERR_UNEXPECTED_EOF = -10
+ERR_IO = -11
+ERR_SCHEME = -12
+
+
+class View(C.Structure):
+    _fields_ = [("base", C.c_void_p), ("obj_stride", C.c_uint64)]
+
+
+READ_FN = C.CFUNCTYPE(C.c_int64, C.c_void_p, C.POINTER(C.c_uint8), C.c_size_t)
+WRITE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint8), C.c_size_t)
+
+# every symbol include/hbec.h declares: (name, restype, argtypes)
+_P = C.c_void_p
+_U8P = C.POINTER(C.c_uint8)
+_SIG = [
+    ("hbec_strerror", C.c_char_p, [C.c_int]),
+    ("hbec_last_error", C.c_char_p, []),
+    ("hbec_version", C.c_int, []),
+    ("hbec_new", C.c_int, [C.c_int, C.c_int, C.POINTER(_P)]),
+    ("hbec_free", None, [_P]),
+    ("hbec_data_shards", C.c_int, [_P]),
+    ("hbec_parity_shards", C.c_int, [_P]),
+    ("hbec_matrix", C.c_int, [_P, _U8P]),
+    ("hbec_encode", C.c_int, [_P, C.POINTER(_P), C.POINTER(C.c_size_t), C.c_int]),
+    ("hbec_reconstruct", C.c_int, [_P, C.POINTER(_P), C.POINTER(C.c_size_t), C.c_int, C.c_int]),
+    ("hbec_encode_batch", C.c_int, [_P, C.POINTER(View), C.c_uint64, C.c_uint64, _P]),
+    ("hbec_reconstruct_batch", C.c_int,
+     [_P, C.POINTER(View), _U8P, C.c_uint64, C.c_uint64, C.c_int, _P]),
+    ("hbec_decode_rows", C.c_int,
+     [_P, _U8P, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int), _U8P]),
+    ("hbec_apply_batch", C.c_int,
+     [C.c_int, C.c_int, _U8P, C.POINTER(View), C.POINTER(View), C.c_uint64, C.c_uint64, _P]),
+    ("hbec_fill_splitmix", C.c_int, [_P, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, _P]),
+    ("hbec_set_force_stream", C.c_int, [C.c_int]),
+    ("hbec_kernel_info", C.c_int, [C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    ("hbec_ec_shard_length", C.c_int64, [C.c_int64, C.c_int]),
+    ("hbec_ec_split", C.c_int, [C.c_int, C.c_int, READ_FN, _P, C.c_int, C.c_int64, WRITE_FN, C.POINTER(_P)]),
+    ("hbec_ec_reconstruct", C.c_int,
+     [C.c_int, C.c_int, READ_FN, C.POINTER(_P), C.c_int, C.c_int64, WRITE_FN, C.POINTER(_P),
+      C.POINTER(C.c_int), C.c_int]),
+    ("hbec_ec_glue", C.c_int,
+     [C.c_int, C.c_int, READ_FN, C.POINTER(_P), C.c_int, C.c_int64, WRITE_FN, C.POINTER(_P), C.c_int]),
+    ("hbec_parse_ec_scheme", C.c_int,
+     [C.c_char_p, C.c_char_p, C.c_size_t, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    ("hbec_range_chunk_align", None,
+     [C.c_int64, C.c_int64, C.c_int64, C.c_int, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
+]
+SYMBOLS = [s[0] for s in _SIG]
+
+_lib = None
+
+
+class NativeLibraryError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libhbec.so once; raise NativeLibraryError if it is absent."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise NativeLibraryError(
+                f"{LIB_PATH} not found: build it with `python -m hummingbird_amd.build` "
+                "(there is no CPU fallback)")
+        try:
+            h = C.CDLL(str(LIB_PATH))
+        except OSError as e:  # pragma: no cover - depends on the host
+            raise NativeLibraryError(f"cannot load {LIB_PATH}: {e}") from e
+        for name, res, args in _SIG:
+            fn = getattr(h, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = h
+    return _lib
+
+
+def last_error() -> str:
+    return lib().hbec_last_error().decode(errors="replace")
+
+
+def strerror(code: int) -> str:
+    return lib().hbec_strerror(code).decode()

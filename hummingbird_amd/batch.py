@@ -1,0 +1,97 @@
+"""Device-resident batches of objects (the GPU hot path) on torch tensors.
+
+torch supplies device memory and streams only; the arithmetic is libhbec's
+HIP kernels, called through the C ABI (``hbec_encode_batch`` /
+``hbec_reconstruct_batch``).  Layout of a batch of n one-stripe objects with
+shard length S (the ecSplit layout, objectserver/ecutils.go:55-58):
+
+    objs   : uint8 [n, k*S]  — object o's data shard j = objs[o, j*S:(j+1)*S]
+    parity : uint8 [n, m*S]  — object o's parity shard r = parity[o, r*S:(r+1)*S]
+
+Shards are never copied: the kernels read the data shards in place.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+from . import _native as N
+from .reedsolomon import Encoder, check
+
+HBEC_SEED = 0x48424543
+
+
+def _stream_ptr(stream):
+    import torch
+
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return C.c_void_p(stream.cuda_stream)
+
+
+def shard_views(t, n_shards: int, shard_len: int):
+    """Views of the n_shards consecutive shards stored in each row of a 2-D tensor."""
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise ValueError("expected a 2-D row-contiguous tensor")
+    if t.shape[1] < n_shards * shard_len:
+        raise ValueError("tensor rows shorter than n_shards * shard_len")
+    base = t.data_ptr()
+    row = t.stride(0) * t.element_size()
+    return [(base + i * shard_len, row) for i in range(n_shards)]
+
+
+def _views(pairs):
+    arr = (N.View * len(pairs))()
+    for i, (b, s) in enumerate(pairs):
+        arr[i].base = b
+        arr[i].obj_stride = s
+    return arr
+
+
+def encode_views(enc: Encoder, views, n_objects: int, shard_len: int, stream=None) -> None:
+    v = _views(views)
+    check(N.lib().hbec_encode_batch(enc.handle, v, int(n_objects), int(shard_len), _stream_ptr(stream)))
+
+
+def reconstruct_views(enc: Encoder, views, present, n_objects: int, shard_len: int, data_only: bool = False,
+                      stream=None) -> None:
+    v = _views(views)
+    p = (C.c_uint8 * len(present))(*[1 if x else 0 for x in present])
+    check(N.lib().hbec_reconstruct_batch(enc.handle, v, p, int(n_objects), int(shard_len), int(data_only),
+                                         _stream_ptr(stream)))
+
+
+def encode_objects(enc: Encoder, objs, parity, shard_len: int, stream=None) -> None:
+    """Encode every row of ``objs`` [n, k*S] into ``parity`` [n, m*S]."""
+    n = objs.shape[0]
+    if parity.shape[0] != n:
+        raise ValueError("objs and parity disagree on the batch size")
+    views = shard_views(objs, enc.DataShards, shard_len) + shard_views(parity, enc.ParityShards, shard_len)
+    encode_views(enc, views, n, shard_len, stream)
+
+
+def fill_splitmix(t, obj_len: int, base_seed: int = HBEC_SEED, first: int = 0, stream=None) -> None:
+    """Fill row o of a 2-D uint8 tensor with synthetic object (first + o)."""
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise ValueError("expected a 2-D row-contiguous tensor")
+    check(N.lib().hbec_fill_splitmix(C.c_void_p(t.data_ptr()), t.shape[0], int(obj_len),
+                                     t.stride(0) * t.element_size(), int(base_seed), int(first),
+                                     _stream_ptr(stream)))
+
+
+def apply_views(rows: int, cols: int, coeffs, in_views, out_views, n_objects: int, shard_len: int,
+                stream=None) -> None:
+    """Generic GF(2^8) matrix apply: out[r] = XOR_c coeffs[r][c] * in[c]."""
+    flat = bytes(int(x) for row in coeffs for x in row)
+    cbuf = (C.c_uint8 * len(flat)).from_buffer_copy(flat)
+    check(N.lib().hbec_apply_batch(int(rows), int(cols), cbuf, _views(in_views), _views(out_views),
+                                   int(n_objects), int(shard_len), _stream_ptr(stream)))
+
+
+def kernel_info(k: int, r: int):
+    tb, st, bpc = C.c_int(), C.c_int(), C.c_int()
+    check(N.lib().hbec_kernel_info(k, r, C.byref(tb), C.byref(st), C.byref(bpc)))
+    return {"tile_bytes": tb.value, "streaming": bool(st.value), "blocks_per_cu": bpc.value}
+
+
+def set_force_stream(on: bool) -> None:
+    N.lib().hbec_set_force_stream(1 if on else 0)

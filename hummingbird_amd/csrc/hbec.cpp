@@ -1,0 +1,508 @@
+// hbec.cpp — the codec (klauspost Encoder mirror) and the device batch API
+// behind include/hbec.h.
+//
+// Reference semantics restated here (klauspost/reedsolomon, reached from
+// objectserver/ecutils.go:27,59,77,111,135,168):
+//   New:            k <= 0 || m < 0 -> ErrInvShardNum; k+m > 256 -> ErrMaxShardNum
+//   Encode:         len(shards) != k+m -> ErrTooFewShards; checkShards(nilok=false)
+//   Reconstruct(*): checkShards(nilok=true); nothing to do if all present (or all
+//                   data present for ReconstructData); < k present -> ErrTooFewShards;
+//                   survivors = first k present shards; missing data = inv(sub) rows;
+//                   missing parity = M_p x data.  Parity rows are fused with the
+//                   inverse (M_p x inv(sub)), which is the same linear map for
+//                   every input (DESIGN.md "Reconstruct").
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/hbec.h"
+#include "gf256.h"
+#include "internal.h"
+#include "kernels.h"
+
+namespace hbec {
+
+static thread_local std::string t_last_error;
+
+int fail(int code, const std::string& msg) {
+    t_last_error = msg;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    std::string m = std::string(what) + ": " + hipGetErrorString(e);
+    return fail(HBEC_ERR_DEVICE, m);
+}
+
+static std::atomic<int> g_force_stream{0};
+
+// ---------------------------------------------------------------------------
+// Per-device facts (CU count, occupancy per kernel shape)
+// ---------------------------------------------------------------------------
+struct DeviceInfo {
+    int cus = 0;
+    std::map<std::pair<int, int>, int> blocks_per_cu;
+};
+
+static std::mutex g_dev_mu;
+static std::map<int, DeviceInfo> g_devs;
+
+static int current_device(int* dev) {
+    hipError_t e = hipGetDevice(dev);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+    return HBEC_OK;
+}
+
+static int device_blocks(int dev, int k, int r, int force_stream, int* cus, int* per_cu) {
+    std::lock_guard<std::mutex> g(g_dev_mu);
+    DeviceInfo& d = g_devs[dev];
+    if (d.cus == 0) {
+        hipDeviceProp_t p;
+        hipError_t e = hipGetDeviceProperties(&p, dev);
+        if (e != hipSuccess) return hip_fail(e, "hipGetDeviceProperties");
+        d.cus = p.multiProcessorCount;
+    }
+    const int key_k = force_stream ? -k : k;
+    auto it = d.blocks_per_cu.find({key_k, r});
+    if (it == d.blocks_per_cu.end()) {
+        int b = 0;
+        hipError_t e = vec_occupancy(k, r, force_stream, &b);
+        if (e != hipSuccess) return hip_fail(e, "occupancy query");
+        if (b < 1) b = 1;
+        it = d.blocks_per_cu.emplace(std::make_pair(key_k, r), b).first;
+    }
+    *cus = d.cus;
+    *per_cu = it->second;
+    return HBEC_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Generic pass planner: out[R] (^)= C[R][K] x in[K] over strided views
+// ---------------------------------------------------------------------------
+static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+int apply_views(int rows, int cols, const uint8_t* coeffs, const hbec_view* in, const hbec_view* out,
+                uint64_t n_obj, uint64_t shard_len, hipStream_t stream) {
+    if (rows <= 0 || n_obj == 0 || shard_len == 0) return HBEC_OK;
+    if (cols <= 0 || !coeffs || !in || !out) return fail(HBEC_ERR_INVALID_ARG, "apply: bad arguments");
+    bool vec = (shard_len % 16) == 0;
+    for (int c = 0; c < cols && vec; ++c) vec = aligned16(in[c].base) && (in[c].obj_stride % 16) == 0;
+    for (int r = 0; r < rows && vec; ++r) vec = aligned16(out[r].base) && (out[r].obj_stride % 16) == 0;
+    for (int c = 0; c < cols; ++c)
+        if (!in[c].base) return fail(HBEC_ERR_INVALID_ARG, "apply: null input view");
+    for (int r = 0; r < rows; ++r)
+        if (!out[r].base) return fail(HBEC_ERR_INVALID_ARG, "apply: null output view");
+    int dev = 0;
+    int rc = current_device(&dev);
+    if (rc) return rc;
+    const int force_stream = g_force_stream.load();
+
+    for (int r0 = 0; r0 < rows; r0 += kMaxR) {
+        const int R = std::min(kMaxR, rows - r0);
+        for (int c0 = 0; c0 < cols; c0 += kMaxK) {
+            const int K = std::min(kMaxK, cols - c0);
+            PassArgs a;
+            std::memset(&a, 0, sizeof(a));
+            for (int j = 0; j < K; ++j) {
+                a.in[j] = static_cast<const uint8_t*>(in[c0 + j].base);
+                a.in_stride[j] = in[c0 + j].obj_stride;
+            }
+            for (int r = 0; r < R; ++r) {
+                a.out[r] = static_cast<uint8_t*>(out[r0 + r].base);
+                a.out_stride[r] = out[r0 + r].obj_stride;
+                for (int j = 0; j < K; ++j) perm_table(coeffs[(size_t)(r0 + r) * cols + c0 + j], a.tab[r][j]);
+            }
+            a.shard_len = shard_len;
+            a.accumulate = c0 > 0 ? 1u : 0u;
+            if (vec) {
+                int cus = 0, per_cu = 0;
+                rc = device_blocks(dev, K, R, force_stream, &cus, &per_cu);
+                if (rc) return rc;
+                const uint64_t tile = (uint64_t)vec_tile_bytes(K, R, force_stream);
+                const uint64_t tpo = (shard_len + tile - 1) / tile;
+                // keep n_tiles < 2^31 per launch: split the batch by objects
+                const uint64_t max_obj = std::max<uint64_t>(1, (1ull << 31) / tpo);
+                for (uint64_t o0 = 0; o0 < n_obj; o0 += max_obj) {
+                    const uint64_t no = std::min(max_obj, n_obj - o0);
+                    PassArgs b = a;
+                    for (int j = 0; j < K; ++j) b.in[j] = a.in[j] + o0 * a.in_stride[j];
+                    for (int r = 0; r < R; ++r) b.out[r] = a.out[r] + o0 * a.out_stride[r];
+                    b.n_obj = no;
+                    b.tiles_per_obj = (uint32_t)tpo;
+                    b.n_tiles = (uint32_t)(no * tpo);
+                    const uint64_t want_blocks = (b.n_tiles + (kBlockThreads / 64) - 1) / (kBlockThreads / 64);
+                    const uint64_t cap = (uint64_t)cus * (uint64_t)per_cu;
+                    const int grid = (int)std::max<uint64_t>(1, std::min(want_blocks, cap));
+                    hipError_t e = launch_vec(K, R, b, grid, stream, force_stream);
+                    if (e != hipSuccess) return hip_fail(e, "launch gf_apply_vec");
+                }
+            } else {
+                a.n_obj = n_obj;
+                const uint64_t words = ((shard_len + 3) / 4) * n_obj;
+                const uint64_t want = (words + kBlockThreads - 1) / kBlockThreads;
+                const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, 8192));
+                hipError_t e = launch_bytes(K, R, a, grid, stream);
+                if (e != hipSuccess) return hip_fail(e, "launch gf_apply_bytes");
+            }
+        }
+    }
+    return HBEC_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Staging pool for the host-memory API (one stream + device buffer each)
+// ---------------------------------------------------------------------------
+struct Staging {
+    int dev = 0;
+    hipStream_t stream = nullptr;
+    uint8_t* dbuf = nullptr;
+    size_t dcap = 0;
+};
+
+static std::mutex g_pool_mu;
+static std::vector<Staging*> g_pool;
+
+static int staging_acquire(size_t bytes, Staging** out) {
+    int dev = 0;
+    int rc = current_device(&dev);
+    if (rc) return rc;
+    Staging* s = nullptr;
+    {
+        std::lock_guard<std::mutex> g(g_pool_mu);
+        for (size_t i = 0; i < g_pool.size(); ++i)
+            if (g_pool[i]->dev == dev) {
+                s = g_pool[i];
+                g_pool.erase(g_pool.begin() + i);
+                break;
+            }
+    }
+    if (!s) {
+        s = new Staging();
+        s->dev = dev;
+        hipError_t e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
+        if (e != hipSuccess) {
+            delete s;
+            return hip_fail(e, "hipStreamCreate");
+        }
+    }
+    if (s->dcap < bytes) {
+        if (s->dbuf) (void)hipFree(s->dbuf);
+        s->dbuf = nullptr;
+        s->dcap = 0;
+        size_t cap = std::max<size_t>(bytes, 1 << 20);
+        hipError_t e = hipMalloc(&s->dbuf, cap);
+        if (e != hipSuccess) {
+            std::lock_guard<std::mutex> g(g_pool_mu);
+            g_pool.push_back(s);
+            return hip_fail(e, "hipMalloc staging");
+        }
+        s->dcap = cap;
+    }
+    *out = s;
+    return HBEC_OK;
+}
+
+static void staging_release(Staging* s) {
+    std::lock_guard<std::mutex> g(g_pool_mu);
+    g_pool.push_back(s);
+}
+
+}  // namespace hbec
+
+// ---------------------------------------------------------------------------
+// Codec
+// ---------------------------------------------------------------------------
+struct hbec_codec {
+    int k = 0, m = 0;
+    std::vector<uint8_t> matrix;  // (k+m) x k
+    std::mutex mu;
+    std::map<std::vector<int>, std::vector<uint8_t>> inv_cache;  // survivors -> inv(sub)
+};
+
+namespace hbec {
+
+// Decode rows for a present mask: survivors = first k present shards.
+static int decode_rows(hbec_codec* c, const std::vector<uint8_t>& present, bool data_only,
+                       std::vector<int>& survivors, std::vector<int>& outputs, std::vector<uint8_t>& rows) {
+    const int k = c->k, n = c->k + c->m;
+    survivors.clear();
+    for (int i = 0; i < n && (int)survivors.size() < k; ++i)
+        if (present[i]) survivors.push_back(i);
+    if ((int)survivors.size() < k) return fail(HBEC_ERR_TOO_FEW_SHARDS, "too few shards given");
+    outputs.clear();
+    for (int i = 0; i < n; ++i)
+        if (!present[i] && (i < k || !data_only)) outputs.push_back(i);
+    std::vector<uint8_t> inv;
+    {
+        std::lock_guard<std::mutex> g(c->mu);
+        auto it = c->inv_cache.find(survivors);
+        if (it != c->inv_cache.end()) {
+            inv = it->second;
+        } else {
+            std::vector<uint8_t> sub((size_t)k * k);
+            for (int r = 0; r < k; ++r)
+                std::memcpy(&sub[(size_t)r * k], &c->matrix[(size_t)survivors[r] * k], k);
+            inv.resize((size_t)k * k);
+            if (!invert(k, sub.data(), inv.data())) return fail(HBEC_ERR_SINGULAR, "matrix is singular");
+            c->inv_cache.emplace(survivors, inv);
+        }
+    }
+    const Field& F = field();
+    rows.assign(outputs.size() * (size_t)k, 0);
+    for (size_t o = 0; o < outputs.size(); ++o) {
+        const int i = outputs[o];
+        uint8_t* row = &rows[o * k];
+        if (i < k) {
+            std::memcpy(row, &inv[(size_t)i * k], k);
+        } else {  // parity row fused with the inverse: M[i] x inv
+            for (int t = 0; t < k; ++t) {
+                const uint8_t mc = c->matrix[(size_t)i * k + t];
+                if (!mc) continue;
+                for (int j = 0; j < k; ++j) row[j] ^= F.mul(mc, inv[(size_t)t * k + j]);
+            }
+        }
+    }
+    return HBEC_OK;
+}
+
+// klauspost checkShards: size of first non-empty shard, then equality.
+static int check_shards(const size_t* lens, int n, bool nilok, size_t* size) {
+    size_t s = 0;
+    for (int i = 0; i < n; ++i)
+        if (lens[i] != 0) {
+            s = lens[i];
+            break;
+        }
+    if (s == 0) return fail(HBEC_ERR_SHARD_NO_DATA, "no shard data");
+    for (int i = 0; i < n; ++i)
+        if (lens[i] != s && (lens[i] != 0 || !nilok)) return fail(HBEC_ERR_SHARD_SIZE, "shard sizes do not match");
+    *size = s;
+    return HBEC_OK;
+}
+
+static uint64_t round16(uint64_t v) { return (v + 15) & ~uint64_t(15); }
+
+// Host-memory apply: copy inputs in, run one object, copy outputs back.
+static int host_apply(int rows, int cols, const uint8_t* coeffs, const uint8_t* const* in, uint8_t* const* out,
+                      size_t len) {
+    if (rows == 0) return HBEC_OK;
+    const uint64_t pad = round16(len);
+    Staging* s = nullptr;
+    int rc = staging_acquire((size_t)pad * (cols + rows), &s);
+    if (rc) return rc;
+    std::vector<hbec_view> vin(cols), vout(rows);
+    hipError_t e = hipSuccess;
+    for (int j = 0; j < cols && e == hipSuccess; ++j) {
+        vin[j] = {s->dbuf + (size_t)j * pad, 0};
+        e = hipMemcpyAsync(vin[j].base, in[j], len, hipMemcpyHostToDevice, s->stream);
+    }
+    for (int r = 0; r < rows; ++r) vout[r] = {s->dbuf + (size_t)(cols + r) * pad, 0};
+    if (e != hipSuccess) {
+        staging_release(s);
+        return hip_fail(e, "hipMemcpyAsync H2D");
+    }
+    // process the padded length: bytes past len are don't-care in, don't-care out
+    rc = apply_views(rows, cols, coeffs, vin.data(), vout.data(), 1, pad, s->stream);
+    for (int r = 0; r < rows && rc == HBEC_OK && e == hipSuccess; ++r)
+        e = hipMemcpyAsync(out[r], vout[r].base, len, hipMemcpyDeviceToHost, s->stream);
+    hipError_t e2 = hipStreamSynchronize(s->stream);
+    staging_release(s);
+    if (rc) return rc;
+    if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync D2H");
+    if (e2 != hipSuccess) return hip_fail(e2, "hipStreamSynchronize");
+    return HBEC_OK;
+}
+
+}  // namespace hbec
+
+using namespace hbec;
+
+extern "C" {
+
+const char* hbec_strerror(int code) {
+    switch (code) {
+        case HBEC_OK: return "ok";
+        case HBEC_ERR_INV_SHARD_NUM: return "cannot create Encoder with zero or less data/parity shards";
+        case HBEC_ERR_MAX_SHARD_NUM: return "cannot create Encoder with more than 256 data+parity shards";
+        case HBEC_ERR_TOO_FEW_SHARDS: return "too few shards given";
+        case HBEC_ERR_SHARD_NO_DATA: return "no shard data";
+        case HBEC_ERR_SHARD_SIZE: return "shard sizes do not match";
+        case HBEC_ERR_SINGULAR: return "matrix is singular";
+        case HBEC_ERR_INVALID_ARG: return "invalid argument";
+        case HBEC_ERR_DEVICE: return "device error";
+        case HBEC_ERR_NOMEM: return "out of memory";
+        case HBEC_ERR_UNEXPECTED_EOF: return "unexpected EOF";
+        case HBEC_ERR_IO: return "i/o error";
+        case HBEC_ERR_SCHEME: return "invalid EC scheme";
+    }
+    return "unknown error";
+}
+
+const char* hbec_last_error(void) { return t_last_error.c_str(); }
+
+int hbec_version(void) { return HBEC_VERSION; }
+
+int hbec_new(int data_shards, int parity_shards, hbec_codec** out) {
+    if (!out) return fail(HBEC_ERR_INVALID_ARG, "out is NULL");
+    *out = nullptr;
+    if (data_shards <= 0 || parity_shards < 0)
+        return fail(HBEC_ERR_INV_SHARD_NUM, "cannot create Encoder with zero or less data/parity shards");
+    if (data_shards + parity_shards > 256)
+        return fail(HBEC_ERR_MAX_SHARD_NUM, "cannot create Encoder with more than 256 data+parity shards");
+    std::unique_ptr<hbec_codec> c(new (std::nothrow) hbec_codec());
+    if (!c) return fail(HBEC_ERR_NOMEM, "codec allocation");
+    c->k = data_shards;
+    c->m = parity_shards;
+    if (!build_matrix(c->k, c->m, c->matrix)) return fail(HBEC_ERR_SINGULAR, "matrix is singular");
+    *out = c.release();
+    return HBEC_OK;
+}
+
+void hbec_free(hbec_codec* codec) { delete codec; }
+
+int hbec_data_shards(const hbec_codec* c) { return c ? c->k : HBEC_ERR_INVALID_ARG; }
+int hbec_parity_shards(const hbec_codec* c) { return c ? c->m : HBEC_ERR_INVALID_ARG; }
+
+int hbec_matrix(const hbec_codec* c, uint8_t* out) {
+    if (!c || !out) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+    std::memcpy(out, c->matrix.data(), c->matrix.size());
+    return HBEC_OK;
+}
+
+int hbec_encode(hbec_codec* c, uint8_t* const* shards, const size_t* lens, int n_shards) {
+    if (!c || !shards || !lens) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+    if (n_shards != c->k + c->m) return fail(HBEC_ERR_TOO_FEW_SHARDS, "too few shards given");
+    size_t s = 0;
+    int rc = check_shards(lens, n_shards, false, &s);
+    if (rc) return rc;
+    for (int i = 0; i < n_shards; ++i)
+        if (!shards[i]) return fail(HBEC_ERR_INVALID_ARG, "null shard pointer");
+    return host_apply(c->m, c->k, c->matrix.data() + (size_t)c->k * c->k, shards, shards + c->k, s);
+}
+
+int hbec_reconstruct(hbec_codec* c, uint8_t* const* shards, size_t* lens, int n_shards, int data_only) {
+    if (!c || !shards || !lens) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+    if (n_shards != c->k + c->m) return fail(HBEC_ERR_TOO_FEW_SHARDS, "too few shards given");
+    size_t s = 0;
+    int rc = check_shards(lens, n_shards, true, &s);
+    if (rc) return rc;
+    std::vector<uint8_t> present(n_shards);
+    int n_present = 0, data_present = 0;
+    for (int i = 0; i < n_shards; ++i) {
+        present[i] = lens[i] != 0;
+        n_present += present[i];
+        if (i < c->k) data_present += present[i];
+    }
+    if (n_present == n_shards || (data_only && data_present == c->k)) return HBEC_OK;
+    if (n_present < c->k) return fail(HBEC_ERR_TOO_FEW_SHARDS, "too few shards given");
+    std::vector<int> surv, outs;
+    std::vector<uint8_t> rows;
+    rc = decode_rows(c, present, data_only != 0, surv, outs, rows);
+    if (rc) return rc;
+    std::vector<const uint8_t*> in(surv.size());
+    std::vector<uint8_t*> out(outs.size());
+    for (size_t j = 0; j < surv.size(); ++j) in[j] = shards[surv[j]];
+    for (size_t o = 0; o < outs.size(); ++o) {
+        if (!shards[outs[o]]) return fail(HBEC_ERR_INVALID_ARG, "missing shard has no buffer");
+        out[o] = shards[outs[o]];
+    }
+    rc = host_apply((int)outs.size(), c->k, rows.data(), in.data(), out.data(), s);
+    if (rc) return rc;
+    for (int i : outs) lens[i] = s;
+    return HBEC_OK;
+}
+
+int hbec_encode_batch(hbec_codec* c, const hbec_view* views, uint64_t n_objects, uint64_t shard_len,
+                      void* hip_stream) {
+    if (!c || !views) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+    return apply_views(c->m, c->k, c->matrix.data() + (size_t)c->k * c->k, views, views + c->k, n_objects,
+                       shard_len, static_cast<hipStream_t>(hip_stream));
+}
+
+int hbec_decode_rows(hbec_codec* c, const uint8_t* present, int data_only, int* survivors, int* outputs,
+                     int* n_outputs, uint8_t* rows) {
+    if (!c || !present || !survivors || !outputs || !n_outputs || !rows)
+        return fail(HBEC_ERR_INVALID_ARG, "null argument");
+    std::vector<uint8_t> p(present, present + c->k + c->m);
+    for (auto& v : p) v = v ? 1 : 0;
+    std::vector<int> surv, outs;
+    std::vector<uint8_t> r;
+    int rc = decode_rows(c, p, data_only != 0, surv, outs, r);
+    if (rc) return rc;
+    std::copy(surv.begin(), surv.end(), survivors);
+    std::copy(outs.begin(), outs.end(), outputs);
+    *n_outputs = (int)outs.size();
+    std::copy(r.begin(), r.end(), rows);
+    return HBEC_OK;
+}
+
+int hbec_reconstruct_batch(hbec_codec* c, const hbec_view* views, const uint8_t* present, uint64_t n_objects,
+                           uint64_t shard_len, int data_only, void* hip_stream) {
+    if (!c || !views || !present) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+    const int n = c->k + c->m;
+    std::vector<uint8_t> p(present, present + n);
+    int n_present = 0, data_present = 0;
+    for (int i = 0; i < n; ++i) {
+        p[i] = p[i] ? 1 : 0;
+        n_present += p[i];
+        if (i < c->k) data_present += p[i];
+    }
+    if (n_present == n || (data_only && data_present == c->k)) return HBEC_OK;
+    if (n_present < c->k) return fail(HBEC_ERR_TOO_FEW_SHARDS, "too few shards given");
+    std::vector<int> surv, outs;
+    std::vector<uint8_t> rows;
+    int rc = decode_rows(c, p, data_only != 0, surv, outs, rows);
+    if (rc) return rc;
+    std::vector<hbec_view> vin(surv.size()), vout(outs.size());
+    for (size_t j = 0; j < surv.size(); ++j) vin[j] = views[surv[j]];
+    for (size_t o = 0; o < outs.size(); ++o) vout[o] = views[outs[o]];
+    return apply_views((int)outs.size(), c->k, rows.data(), vin.data(), vout.data(), n_objects, shard_len,
+                       static_cast<hipStream_t>(hip_stream));
+}
+
+int hbec_apply_batch(int rows, int cols, const uint8_t* coeffs, const hbec_view* in, const hbec_view* out,
+                     uint64_t n_objects, uint64_t shard_len, void* hip_stream) {
+    return apply_views(rows, cols, coeffs, in, out, n_objects, shard_len, static_cast<hipStream_t>(hip_stream));
+}
+
+int hbec_fill_splitmix(void* dst, uint64_t n_objects, uint64_t obj_len, uint64_t obj_stride, uint64_t base_seed,
+                       uint64_t first, void* hip_stream) {
+    if (!dst) return fail(HBEC_ERR_INVALID_ARG, "null dst");
+    if (n_objects == 0 || obj_len == 0) return HBEC_OK;
+    const uint64_t words = ((obj_len + 7) / 8) * n_objects;
+    const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((words + kBlockThreads - 1) / kBlockThreads, 16384));
+    hipError_t e = launch_fill(static_cast<uint8_t*>(dst), n_objects, obj_len, obj_stride, base_seed, first, grid,
+                               static_cast<hipStream_t>(hip_stream));
+    if (e != hipSuccess) return hip_fail(e, "launch fill_splitmix");
+    return HBEC_OK;
+}
+
+int hbec_set_force_stream(int on) {
+    g_force_stream.store(on ? 1 : 0);
+    return HBEC_OK;
+}
+
+int hbec_kernel_info(int k, int r, int* tile_bytes, int* streaming, int* blocks_per_cu) {
+    if (k < 1 || k > kMaxK || r < 1 || r > kMaxR) return fail(HBEC_ERR_INVALID_ARG, "shape out of range");
+    const int fs = g_force_stream.load();
+    if (tile_bytes) *tile_bytes = vec_tile_bytes(k, r, fs);
+    if (streaming) *streaming = is_streaming_shape(k, r, fs);
+    if (blocks_per_cu) {
+        int dev = 0, cus = 0;
+        int rc = current_device(&dev);
+        if (rc) return rc;
+        rc = device_blocks(dev, k, r, fs, &cus, blocks_per_cu);
+        if (rc) return rc;
+    }
+    return HBEC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,364 @@
+// kernels.hip — gfx950 (CDNA4) GF(2^8) shard kernels for the Hummingbird EC path.
+//
+// One kernel body serves both hot operations of objectserver/ecutils.go:
+//   * Encode       (ecSplit      -> Encoder.Encode,      ecutils.go:59)
+//       out[r] = XOR_j M[k+r][j] * data[j]
+//   * Reconstruct  (ecReconstruct-> Encoder.Reconstruct, ecutils.go:111;
+//                   ecGlue       -> ReconstructData,     ecutils.go:168)
+//       out[e] = XOR_j D[e][j] * survivor[j]   (D = decode rows built on host)
+//
+// Field multiply without tables in memory: a byte x is split into bit fields
+// x[2:0], x[5:3], x[7:6]; c*x = c*x[2:0] ^ c*(x[5:3]<<3) ^ c*(x[7:6]<<6)
+// (GF multiply is linear over XOR).  Each field indexes an 8-entry (or
+// 4-entry) byte table held in two (one) registers, and v_perm_b32 performs
+// that lookup for all 4 bytes of a dword at once.  So one coefficient costs 3
+// v_perm_b32 per input dword plus XORs, and the selector extraction (5 VALU
+// ops) is shared by every output row.  No LDS, no MFMA: the kernel is an HBM
+// stream (k inputs read once, R outputs written once, coalesced 16 B/lane).
+//
+// Work decomposition: a "wave tile" is U x 1 KiB of one shard column
+// (64 lanes x 16 B per KiB) across all K inputs of one object.  Waves walk
+// tiles grid-stride; tile -> (object, offset) is one scalar division per tile.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kernels.h"
+
+namespace hbec {
+
+__device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
+    // v_perm_b32: byte i of result = byte sel.u8[i] of the 64-bit {hi, lo}
+    // (selector 0-3 -> lo, 4-7 -> hi).
+    return __builtin_amdgcn_perm(hi, lo, sel);
+}
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+#ifndef HBEC_NT_LOADS
+#define HBEC_NT_LOADS 1
+#endif
+#ifndef HBEC_NT_STORES
+#define HBEC_NT_STORES 1
+#endif
+
+__device__ __forceinline__ u32x4 ld16(const uint8_t* p) {
+#if HBEC_NT_LOADS
+    return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+#else
+    return *reinterpret_cast<const u32x4*>(p);
+#endif
+}
+
+__device__ __forceinline__ void st16(uint8_t* p, u32x4 v) {
+#if HBEC_NT_STORES
+    __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+#else
+    *reinterpret_cast<u32x4*>(p) = v;
+#endif
+}
+
+struct Sel {
+    uint32_t s0, s1, s2;
+};
+
+__device__ __forceinline__ Sel selectors(uint32_t x) {
+    Sel s;
+    s.s0 = x & 0x07070707u;
+    s.s1 = (x >> 3) & 0x07070707u;
+    s.s2 = (x >> 6) & 0x03030303u;
+    return s;
+}
+
+__device__ __forceinline__ uint32_t gf_mul_sel(const Sel& s, uint32_t t0, uint32_t t1, uint32_t t2,
+                                               uint32_t t3, uint32_t t4) {
+    return perm(t1, t0, s.s0) ^ perm(t3, t2, s.s1) ^ perm(t4, t4, s.s2);
+}
+
+template <int K, int R, int U>
+__device__ __forceinline__ void process_tile(const PassArgs& a, uint64_t obj, uint64_t off0, bool full,
+                                             bool accumulate) {
+    // Issue every load of the tile first (K x U x 16 B per lane in flight),
+    // then retire one 1 KiB sub-tile at a time so only its accumulators and
+    // selectors are live.
+    u32x4 x[U][K];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint64_t off = off0 + (uint64_t)u * 1024u;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            if (full || off < a.shard_len) {
+                x[u][j] = ld16(a.in[j] + obj * a.in_stride[j] + off);
+            } else {
+                x[u][j] = u32x4{0, 0, 0, 0};
+            }
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint64_t off = off0 + (uint64_t)u * 1024u;
+        const bool live = full || off < a.shard_len;
+        u32x4 acc[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            acc[r] = u32x4{0, 0, 0, 0};
+            if (accumulate && live) acc[r] = *reinterpret_cast<const u32x4*>(a.out[r] + obj * a.out_stride[r] + off);
+        }
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const Sel sx = selectors(x[u][j][e]);
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const uint32_t* t = a.tab[r][j];
+                    acc[r][e] ^= gf_mul_sel(sx, t[0], t[1], t[2], t[3], t[4]);
+                }
+            }
+        }
+        if (live) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) st16(a.out[r] + obj * a.out_stride[r] + off, acc[r]);
+        }
+    }
+}
+
+// Sub-tiles (1 KiB each) per wave tile: keeps K*U*4 load VGPRs <= 32.
+__host__ __device__ constexpr int tile_kib(int k) { return k <= 2 ? 4 : (k <= 4 ? 2 : 1); }
+
+// Vector path: every base 16-B aligned, every stride and shard_len % 16 == 0.
+template <int K, int R>
+__global__ __launch_bounds__(kBlockThreads, kVecWavesPerSimd) void gf_apply_vec(PassArgs a) {
+    constexpr int U = tile_kib(K);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave =
+        __builtin_amdgcn_readfirstlane(blockIdx.x * (kBlockThreads / 64) + (threadIdx.x >> 6));
+    const uint32_t nwaves = gridDim.x * (kBlockThreads / 64);
+    const uint32_t tpo = a.tiles_per_obj;
+    const bool accumulate = a.accumulate != 0;
+    for (uint32_t t = wave; t < a.n_tiles; t += nwaves) {
+        const uint32_t obj = t / tpo;
+        const uint32_t tile = t - obj * tpo;
+        const uint64_t tile_base = (uint64_t)tile * (uint64_t)(U * 1024);
+        const uint64_t off0 = tile_base + lane * 16u;
+        if (tile_base + (uint64_t)(U * 1024) <= a.shard_len) {
+            process_tile<K, R, U>(a, obj, off0, true, accumulate);
+        } else {
+            process_tile<K, R, U>(a, obj, off0, false, accumulate);
+        }
+    }
+}
+
+// Streaming vec path (runtime K): one input shard at a time with the next
+// input's loads in flight, coefficient tables fetched per input by scalar
+// loads, so registers stay at R x 4 KiB accumulators + 2 x 4 KiB buffers for
+// any K.  Used for shapes whose fully unrolled form would spill.
+template <int R>
+__global__ __launch_bounds__(kBlockThreads, kVecWavesPerSimd) void gf_apply_vec_stream(PassArgs a, int K) {
+    constexpr int U = 4;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave =
+        __builtin_amdgcn_readfirstlane(blockIdx.x * (kBlockThreads / 64) + (threadIdx.x >> 6));
+    const uint32_t nwaves = gridDim.x * (kBlockThreads / 64);
+    const uint32_t tpo = a.tiles_per_obj;
+    for (uint32_t t = wave; t < a.n_tiles; t += nwaves) {
+        const uint32_t obj = t / tpo;
+        const uint32_t tile = t - obj * tpo;
+        const uint64_t off0 = (uint64_t)tile * (uint64_t)(U * 1024) + lane * 16u;
+        bool live[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) live[u] = off0 + (uint64_t)u * 1024u < a.shard_len;
+        u32x4 acc[R][U];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                acc[r][u] = u32x4{0, 0, 0, 0};
+                if (a.accumulate && live[u])
+                    acc[r][u] = *reinterpret_cast<const u32x4*>(a.out[r] + obj * a.out_stride[r] + off0 + u * 1024u);
+            }
+        u32x4 cur[U];
+        {
+            const uint8_t* src = a.in[0] + obj * a.in_stride[0] + off0;
+#pragma unroll
+            for (int u = 0; u < U; ++u) cur[u] = live[u] ? ld16(src + u * 1024u) : u32x4{0, 0, 0, 0};
+        }
+#pragma unroll 1
+        for (int j = 0; j < K; ++j) {
+            u32x4 nxt[U];
+            if (j + 1 < K) {
+                const uint8_t* src = a.in[j + 1] + obj * a.in_stride[j + 1] + off0;
+#pragma unroll
+                for (int u = 0; u < U; ++u) nxt[u] = live[u] ? ld16(src + u * 1024u) : u32x4{0, 0, 0, 0};
+            }
+            uint32_t tb[R][5];
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+#pragma unroll
+                for (int q = 0; q < 5; ++q) tb[r][q] = a.tab[r][j][q];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const Sel sx = selectors(cur[u][e]);
+#pragma unroll
+                    for (int r = 0; r < R; ++r)
+                        acc[r][u][e] ^= gf_mul_sel(sx, tb[r][0], tb[r][1], tb[r][2], tb[r][3], tb[r][4]);
+                }
+#pragma unroll
+            for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (live[u]) st16(a.out[r] + obj * a.out_stride[r] + off0 + u * 1024u, acc[r][u]);
+    }
+}
+
+// Byte path: any alignment / length (small or odd shards).  Each thread owns
+// 4 consecutive bytes of one shard column.
+__global__ __launch_bounds__(kBlockThreads) void gf_apply_bytes(PassArgs a, int K, int R) {
+    const uint64_t words = (a.shard_len + 3) / 4;
+    const uint64_t total = words * a.n_obj;
+    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < total;
+         v += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t obj = v / words;
+        const uint64_t off = (v - obj * words) * 4;
+        const int nb = (a.shard_len - off) >= 4 ? 4 : (int)(a.shard_len - off);
+        uint32_t acc[kMaxR] = {0, 0, 0, 0};
+        if (a.accumulate) {
+            for (int r = 0; r < R; ++r) {
+                const uint8_t* d = a.out[r] + obj * a.out_stride[r] + off;
+                uint32_t w = 0;
+                for (int b = 0; b < nb; ++b) w |= (uint32_t)d[b] << (8 * b);
+                acc[r] = w;
+            }
+        }
+        for (int j = 0; j < K; ++j) {
+            const uint8_t* s = a.in[j] + obj * a.in_stride[j] + off;
+            uint32_t w = 0;
+            for (int b = 0; b < nb; ++b) w |= (uint32_t)s[b] << (8 * b);
+            const Sel sx = selectors(w);
+            for (int r = 0; r < R; ++r) {
+                const uint32_t* t = a.tab[r][j];
+                acc[r] ^= gf_mul_sel(sx, t[0], t[1], t[2], t[3], t[4]);
+            }
+        }
+        for (int r = 0; r < R; ++r) {
+            uint8_t* d = a.out[r] + obj * a.out_stride[r] + off;
+            for (int b = 0; b < nb; ++b) d[b] = (uint8_t)(acc[r] >> (8 * b));
+        }
+    }
+}
+
+// Synthetic objects: object i's bytes are the little-endian
+// splitmix64 stream seeded with base_seed ^ (i * golden).  splitmix64 is
+// counter based, so each 8-byte word is computed independently.
+__global__ __launch_bounds__(kBlockThreads) void fill_splitmix(uint8_t* dst, uint64_t n_obj, uint64_t obj_len,
+                                                             uint64_t obj_stride, uint64_t base_seed,
+                                                             uint64_t first) {
+    const uint64_t words = (obj_len + 7) / 8;
+    const uint64_t total = words * n_obj;
+    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < total;
+         v += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t obj = v / words;
+        const uint64_t w = v - obj * words;
+        const uint64_t seed = base_seed ^ ((first + obj) * 0x9E3779B97F4A7C15ull);
+        uint64_t z = seed + (w + 1) * 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        z = z ^ (z >> 31);
+        uint8_t* d = dst + obj * obj_stride + w * 8;
+        const uint64_t rem = obj_len - w * 8;
+        if (rem >= 8 && (reinterpret_cast<uintptr_t>(d) & 7u) == 0) {
+            *reinterpret_cast<uint64_t*>(d) = z;
+        } else {
+            const int nb = rem >= 8 ? 8 : (int)rem;
+            for (int b = 0; b < nb; ++b) d[b] = (uint8_t)(z >> (8 * b));
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Host-side launch table
+// ---------------------------------------------------------------------------
+template <int K, int R>
+static const void* vec_kernel_ptr() {
+    return reinterpret_cast<const void*>(&gf_apply_vec<K, R>);
+}
+
+// Fully unrolled instantiations that compile spill-free (checked with
+// -Rpass-analysis=kernel-resource-usage); other shapes use the streaming kernel.
+template <int K>
+static const void* vec_kernel_for_r(int r) {
+    switch (r) {
+        case 1: return vec_kernel_ptr<K, 1>();
+        case 2: return vec_kernel_ptr<K, 2>();
+        case 3: return vec_kernel_ptr<K, 3>();
+    }
+    return nullptr;
+}
+
+static const void* unrolled_kernel(int k, int r) {
+    switch (k) {
+        case 1: return vec_kernel_for_r<1>(r);
+        case 2: return vec_kernel_for_r<2>(r);
+        case 3: return vec_kernel_for_r<3>(r);
+        case 4: return vec_kernel_for_r<4>(r);
+        case 5: return vec_kernel_for_r<5>(r);
+        case 6: return vec_kernel_for_r<6>(r);
+        case 7: return vec_kernel_for_r<7>(r);
+        case 8: return vec_kernel_for_r<8>(r);
+    }
+    return nullptr;
+}
+
+static const void* stream_kernel(int r) {
+    switch (r) {
+        case 1: return reinterpret_cast<const void*>(&gf_apply_vec_stream<1>);
+        case 2: return reinterpret_cast<const void*>(&gf_apply_vec_stream<2>);
+        case 3: return reinterpret_cast<const void*>(&gf_apply_vec_stream<3>);
+        case 4: return reinterpret_cast<const void*>(&gf_apply_vec_stream<4>);
+    }
+    return nullptr;
+}
+
+int is_streaming_shape(int k, int r, int force_stream) { return (force_stream || !unrolled_kernel(k, r)) ? 1 : 0; }
+
+int vec_tile_bytes(int k, int r, int force_stream) {
+    if (!force_stream && unrolled_kernel(k, r)) return tile_kib(k) * 1024;
+    return 4 * 1024;
+}
+
+hipError_t launch_vec(int k, int r, const PassArgs& a, int grid, hipStream_t stream, int force_stream) {
+    const void* fn = force_stream ? nullptr : unrolled_kernel(k, r);
+    if (fn) {
+        void* args[] = {const_cast<PassArgs*>(&a)};
+        return hipLaunchKernel(fn, dim3(grid), dim3(kBlockThreads), args, 0, stream);
+    }
+    fn = stream_kernel(r);
+    if (!fn || k < 1 || k > kMaxK) return hipErrorInvalidValue;
+    void* args[] = {const_cast<PassArgs*>(&a), &k};
+    return hipLaunchKernel(fn, dim3(grid), dim3(kBlockThreads), args, 0, stream);
+}
+
+hipError_t launch_bytes(int k, int r, const PassArgs& a, int grid, hipStream_t stream) {
+    hipLaunchKernelGGL(gf_apply_bytes, dim3(grid), dim3(kBlockThreads), 0, stream, a, k, r);
+    return hipGetLastError();
+}
+
+hipError_t launch_fill(uint8_t* dst, uint64_t n_obj, uint64_t obj_len, uint64_t obj_stride, uint64_t base_seed,
+                       uint64_t first, int grid, hipStream_t stream) {
+    hipLaunchKernelGGL(fill_splitmix, dim3(grid), dim3(kBlockThreads), 0, stream, dst, n_obj, obj_len, obj_stride,
+                       base_seed, first);
+    return hipGetLastError();
+}
+
+hipError_t vec_occupancy(int k, int r, int force_stream, int* blocks_per_cu) {
+    const void* fn = force_stream ? nullptr : unrolled_kernel(k, r);
+    if (!fn) fn = stream_kernel(r);
+    if (!fn) return hipErrorInvalidValue;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, kBlockThreads, 0);
+}
+
+}  // namespace hbec

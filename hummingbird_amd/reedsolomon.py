@@ -1,0 +1,171 @@
+"""The klauspost/reedsolomon ``Encoder`` surface that objectserver/ecutils.go
+uses, backed by libhbec's gfx950 kernels.
+
+Reference call sites: ``reedsolomon.New`` (ecutils.go:27,77,135),
+``enc.Encode`` (:59), ``enc.Reconstruct`` (:111), ``enc.ReconstructData``
+(:168).  Names, argument meaning and errors follow that API:
+
+    enc = New(4, 2)
+    enc.Encode(shards)            # shards: k+m equal-length buffers, parity in place
+    enc.Reconstruct(shards)       # missing = None / len 0, filled in place
+    enc.ReconstructData(shards)   # data shards only
+
+Shards are writable byte buffers (``bytearray``, ``numpy.uint8`` arrays,
+``memoryview``).  Missing shards are refilled with new ``numpy`` arrays, the
+way Go allocates when the slice has no capacity.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _native as N
+
+
+class ReedSolomonError(Exception):
+    code = None
+
+
+class ErrInvShardNum(ReedSolomonError):
+    code = N.ERR_INV_SHARD_NUM
+
+
+class ErrMaxShardNum(ReedSolomonError):
+    code = N.ERR_MAX_SHARD_NUM
+
+
+class ErrTooFewShards(ReedSolomonError):
+    code = N.ERR_TOO_FEW_SHARDS
+
+
+class ErrShardNoData(ReedSolomonError):
+    code = N.ERR_SHARD_NO_DATA
+
+
+class ErrShardSize(ReedSolomonError):
+    code = N.ERR_SHARD_SIZE
+
+
+class ErrSingular(ReedSolomonError):
+    code = N.ERR_SINGULAR
+
+
+class ErrDevice(ReedSolomonError):
+    code = N.ERR_DEVICE
+
+
+class ErrInvalidArg(ReedSolomonError):
+    code = N.ERR_INVALID_ARG
+
+
+class ErrUnexpectedEOF(ReedSolomonError):
+    code = N.ERR_UNEXPECTED_EOF
+
+
+class ErrIO(ReedSolomonError):
+    code = N.ERR_IO
+
+
+class ErrScheme(ReedSolomonError):
+    code = N.ERR_SCHEME
+
+
+_BY_CODE = {c.code: c for c in (ErrInvShardNum, ErrMaxShardNum, ErrTooFewShards, ErrShardNoData, ErrShardSize,
+                                ErrSingular, ErrDevice, ErrInvalidArg, ErrUnexpectedEOF, ErrIO, ErrScheme)}
+
+
+def check(rc: int) -> None:
+    if rc != N.HBEC_OK:
+        cls = _BY_CODE.get(rc, ReedSolomonError)
+        raise cls(f"{N.strerror(rc)}: {N.last_error()}")
+
+
+def _as_array(buf) -> np.ndarray:
+    if buf is None:
+        return np.zeros(0, dtype=np.uint8)
+    if isinstance(buf, np.ndarray):
+        if buf.dtype != np.uint8 or buf.ndim != 1 or not buf.flags.c_contiguous:
+            raise TypeError("shards must be 1-D contiguous uint8 arrays")
+        return buf
+    return np.frombuffer(buf, dtype=np.uint8)
+
+
+class Encoder:
+    """reedsolomon.Encoder over the GPU codec (one matrix per (k, m))."""
+
+    def __init__(self, data_shards: int, parity_shards: int):
+        self._h = C.c_void_p()
+        check(N.lib().hbec_new(int(data_shards), int(parity_shards), C.byref(self._h)))
+        self.DataShards = int(data_shards)
+        self.ParityShards = int(parity_shards)
+        self.Shards = self.DataShards + self.ParityShards
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h and N._lib is not None:
+            N._lib.hbec_free(h)
+            self._h = None
+
+    @property
+    def handle(self):
+        return self._h
+
+    def matrix(self) -> np.ndarray:
+        out = np.zeros((self.Shards, self.DataShards), dtype=np.uint8)
+        check(N.lib().hbec_matrix(self._h, out.ctypes.data_as(C.POINTER(C.c_uint8))))
+        return out
+
+    def _ptrs(self, arrs):
+        n = len(arrs)
+        ptrs = (C.c_void_p * n)(*[a.ctypes.data if a.size else 0 for a in arrs])
+        lens = (C.c_size_t * n)(*[a.size for a in arrs])
+        return ptrs, lens
+
+    def Encode(self, shards) -> None:
+        arrs = [_as_array(s) for s in shards]
+        for a in arrs:
+            if a.size and not a.flags.writeable:
+                raise ValueError("shards must be writable")
+        ptrs, lens = self._ptrs(arrs)
+        check(N.lib().hbec_encode(self._h, ptrs, lens, len(arrs)))
+
+    def _reconstruct(self, shards, data_only: int) -> None:
+        arrs = [_as_array(s) for s in shards]
+        size = next((a.size for a in arrs if a.size), 0)
+        if len(arrs) == self.Shards and size:
+            # give every missing shard a buffer of the shard size (Go: reuse or allocate)
+            for i, a in enumerate(arrs):
+                if a.size == 0 and (i < self.DataShards or not data_only):
+                    arrs[i] = np.zeros(size, dtype=np.uint8)
+        n = len(arrs)
+        ptrs = (C.c_void_p * n)(*[a.ctypes.data if a.size else 0 for a in arrs])
+        lens = (C.c_size_t * n)(*[(a.size if (shards[i] is not None and len(shards[i])) else 0)
+                                  for i, a in enumerate(arrs)])
+        check(N.lib().hbec_reconstruct(self._h, ptrs, lens, n, data_only))
+        for i in range(n):
+            if lens[i] and (shards[i] is None or len(shards[i]) == 0):
+                shards[i] = arrs[i]
+
+    def Reconstruct(self, shards) -> None:
+        self._reconstruct(shards, 0)
+
+    def ReconstructData(self, shards) -> None:
+        self._reconstruct(shards, 1)
+
+    def DecodeRows(self, present, data_only: bool = False):
+        """(survivors, outputs, rows) the reconstruct kernels apply."""
+        n = self.Shards
+        p = (C.c_uint8 * n)(*[1 if x else 0 for x in present])
+        surv = (C.c_int * self.DataShards)()
+        outs = (C.c_int * n)()
+        nout = C.c_int()
+        rows = (C.c_uint8 * (n * self.DataShards))()
+        check(N.lib().hbec_decode_rows(self._h, p, int(data_only), surv, outs, C.byref(nout), rows))
+        r = np.frombuffer(bytes(rows), dtype=np.uint8)[: nout.value * self.DataShards]
+        return list(surv), list(outs)[: nout.value], r.reshape(nout.value, self.DataShards)
+
+
+def New(data_shards: int, parity_shards: int) -> Encoder:
+    """reedsolomon.New (ecutils.go:27,77,135)."""
+    return Encoder(data_shards, parity_shards)

@@ -1,0 +1,160 @@
+/*
+ * hbec.h — C ABI of libhbec, the MI355X (gfx950) erasure-coding engine for
+ * Hummingbird's `hec` EC storage policy.
+ *
+ * Drop-in boundary.  In the reference the EC arithmetic is reached only
+ * through github.com/klauspost/reedsolomon at six call sites in
+ * objectserver/ecutils.go (:27,:59,:77,:111,:135,:168).  The plugin surface
+ * above it — RegisterObjectEngine("hec", ecEngineConstructor)
+ * (objectserver/ecengine.go:734-736) and the Object/ObjectStabilizer/
+ * ObjectEngine interfaces (objectserver/objengine.go:35-95) — is untouched.
+ * A cgo shim binds these entry points in place of the
+ * klauspost Encoder (hbec_new/encode/reconstruct) and, optionally, of the
+ * whole stripe loops of ecutils.go (hbec_ec_split/_reconstruct/_glue).
+ *
+ * Conventions: plain pointers and sizes only; 0 = success, negative = error
+ * (codes map 1:1 onto the klauspost sentinels).  All entry points are
+ * thread-safe (cgo calls arrive on arbitrary OS threads).  The library never
+ * keeps a caller pointer after a call returns (batch calls: after the work
+ * queued on the caller's stream completes).  There is NO CPU fallback inside
+ * the library: a GPU failure returns HBEC_ERR_DEVICE and the caller decides.
+ */
+#ifndef HBEC_H
+#define HBEC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HBEC_VERSION 1
+
+enum {
+    HBEC_OK = 0,
+    HBEC_ERR_INV_SHARD_NUM = -1,   /* reedsolomon.ErrInvShardNum  (k <= 0 or m < 0)          */
+    HBEC_ERR_MAX_SHARD_NUM = -2,   /* reedsolomon.ErrMaxShardNum  (k + m > 256)              */
+    HBEC_ERR_TOO_FEW_SHARDS = -3,  /* reedsolomon.ErrTooFewShards                            */
+    HBEC_ERR_SHARD_NO_DATA = -4,   /* reedsolomon.ErrShardNoData                             */
+    HBEC_ERR_SHARD_SIZE = -5,      /* reedsolomon.ErrShardSize                               */
+    HBEC_ERR_SINGULAR = -6,        /* reedsolomon errSingular (matrix.go)                    */
+    HBEC_ERR_INVALID_ARG = -7,     /* bad pointer / size / flag                              */
+    HBEC_ERR_DEVICE = -8,          /* HIP failure or no GPU: caller may use its own CPU codec */
+    HBEC_ERR_NOMEM = -9,           /* host or device allocation failed                       */
+    HBEC_ERR_UNEXPECTED_EOF = -10, /* io.ErrUnexpectedEOF (ecSplit short read)               */
+    HBEC_ERR_IO = -11,             /* a reader/writer callback returned an error             */
+    HBEC_ERR_SCHEME = -12          /* parseECScheme error                                    */
+};
+
+/* Human-readable name of a code; thread-local detail of this thread's last failure. */
+const char* hbec_strerror(int code);
+const char* hbec_last_error(void);
+int hbec_version(void);
+
+/* ---------------------------------------------------------------------------
+ * Codec — replaces reedsolomon.New / Encoder (klauspost reedsolomon.go),
+ * called at objectserver/ecutils.go:27,77,135.
+ * ------------------------------------------------------------------------- */
+typedef struct hbec_codec hbec_codec;
+
+/* reedsolomon.New(dataShards, parityShards): builds the (k+m) x k systematic
+ * matrix (Vandermonde x inv(top)).  Needs no GPU. */
+int hbec_new(int data_shards, int parity_shards, hbec_codec** out);
+void hbec_free(hbec_codec* codec);
+int hbec_data_shards(const hbec_codec* codec);
+int hbec_parity_shards(const hbec_codec* codec);
+/* Copies the (k+m) x k coding matrix, row-major. */
+int hbec_matrix(const hbec_codec* codec, uint8_t* out);
+
+/* Encoder.Encode(shards) — ecutils.go:59.  shards[0..k) data, [k..k+m)
+ * parity, every lens[i] equal and non-zero (else ErrShardSize /
+ * ErrShardNoData); n_shards must be k+m (else ErrTooFewShards).  Parity is
+ * written in place.  Host memory, synchronous. */
+int hbec_encode(hbec_codec* codec, uint8_t* const* shards, const size_t* lens, int n_shards);
+
+/* Encoder.Reconstruct (data_only = 0; ecutils.go:111) and
+ * Encoder.ReconstructData (data_only = 1; ecutils.go:168).  lens[i] == 0
+ * marks shard i missing; shards[i] must then point at >= S writable bytes
+ * (the Go side resolves "reuse capacity or allocate").  Present shards must
+ * share one length S.  On success lens[i] = S for every shard filled in. */
+int hbec_reconstruct(hbec_codec* codec, uint8_t* const* shards, size_t* lens, int n_shards, int data_only);
+
+/* ---------------------------------------------------------------------------
+ * Device-resident batches (the GPU hot path).  A view places shard i of
+ * object o at base + o * obj_stride in device memory.  Work is queued on
+ * hip_stream (a hipStream_t; NULL = default stream) and not waited for.
+ * ------------------------------------------------------------------------- */
+typedef struct {
+    void* base;
+    uint64_t obj_stride;
+} hbec_view;
+
+/* Encode n_objects objects at once: views[0..k) data, views[k..k+m) parity. */
+int hbec_encode_batch(hbec_codec* codec, const hbec_view* views, uint64_t n_objects, uint64_t shard_len,
+                      void* hip_stream);
+
+/* Reconstruct with one erasure pattern for the whole batch: present[i] != 0
+ * for surviving shards (read), 0 for missing ones (written).  Same row
+ * selection as Encoder.Reconstruct: the first k present shards in index
+ * order are the survivors.  data_only = 1 leaves missing parity untouched. */
+int hbec_reconstruct_batch(hbec_codec* codec, const hbec_view* views, const uint8_t* present, uint64_t n_objects,
+                           uint64_t shard_len, int data_only, void* hip_stream);
+
+/* The decode rows a reconstruct applies: survivors[0..k) (shard indices read),
+ * outputs[0..*n_outputs) (shard indices written), rows[*n_outputs][k]. */
+int hbec_decode_rows(hbec_codec* codec, const uint8_t* present, int data_only, int* survivors, int* outputs,
+                     int* n_outputs, uint8_t* rows);
+
+/* Generic GF(2^8) matrix apply on the GPU: out[r] = XOR_c coeffs[r*cols+c] * in[c]. */
+int hbec_apply_batch(int rows, int cols, const uint8_t* coeffs, const hbec_view* in, const hbec_view* out,
+                     uint64_t n_objects, uint64_t shard_len, void* hip_stream);
+
+/* Synthetic objects on the GPU (bench/test inputs): object o = the
+ * little-endian splitmix64 stream seeded base_seed ^ ((first+o) * 0x9E3779B97F4A7C15). */
+int hbec_fill_splitmix(void* dst, uint64_t n_objects, uint64_t obj_len, uint64_t obj_stride, uint64_t base_seed,
+                       uint64_t first, void* hip_stream);
+
+/* Tuning / introspection: force the runtime-K streaming kernel (0/1) and
+ * report the kernel shape a (k, r) pass uses. */
+int hbec_set_force_stream(int on);
+int hbec_kernel_info(int k, int r, int* tile_bytes, int* streaming, int* blocks_per_cu);
+
+/* ---------------------------------------------------------------------------
+ * ecutils.go stripe loops over io callbacks (objectserver/ecutils.go:14-186,
+ * objectserver/ecobj.go:82-98, :814-824).
+ * ------------------------------------------------------------------------- */
+/* io.Reader.Read: returns bytes read (> 0), 0 at EOF, < 0 on error. */
+typedef int64_t (*hbec_read_fn)(void* ctx, uint8_t* buf, size_t n);
+/* io.Writer.Write: returns 0 when all n bytes were written, non-zero on error. */
+typedef int (*hbec_write_fn)(void* ctx, const uint8_t* buf, size_t n);
+
+/* ecShardLength (ecutils.go:14-24): ceil(length / k), 0 for length < 0. */
+int64_t hbec_ec_shard_length(int64_t length, int data_shards);
+
+/* ecSplit (ecutils.go:26-72).  writers: k+m contexts, NULL = nil writer.  A
+ * failing writer is dropped for the rest of the object, as in Go. */
+int hbec_ec_split(int data_shards, int parity_shards, hbec_read_fn read, void* fp, int chunk_size,
+                  int64_t content_length, hbec_write_fn write, void* const* writers);
+
+/* ecReconstruct (ecutils.go:74-132).  bodies: k+m reader contexts, NULL = nil. */
+int hbec_ec_reconstruct(int data_shards, int parity_shards, hbec_read_fn read, void* const* bodies, int chunk_size,
+                        int64_t content_length, hbec_write_fn write, void* const* dsts, const int* dst_chunk_num,
+                        int n_dsts);
+
+/* ecGlue (ecutils.go:134-186). */
+int hbec_ec_glue(int data_shards, int parity_shards, hbec_read_fn read, void* const* bodies, int chunk_size,
+                 int64_t content_length, hbec_write_fn write, void* const* dsts, int n_dsts);
+
+/* parseECScheme (ecobj.go:82-98): "reedsolomon/<k>/<m>/<chunk>". */
+int hbec_parse_ec_scheme(const char* scheme, char* algo, size_t algo_cap, int* data_shards, int* parity_shards,
+                         int* chunk_size);
+
+/* rangeChunkAlign (ecobj.go:814-824). */
+void hbec_range_chunk_align(int64_t start, int64_t end, int64_t chunk_size, int data_shards, int64_t* out_start,
+                            int64_t* out_end);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HBEC_H */

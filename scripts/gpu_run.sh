@@ -1,0 +1,44 @@
+#!/bin/bash
+# GPU-box runner: each step under its own time limit; stop at the first step
+# that ends in anything but success / ordinary test failure (rc 0 or 1).
+# usage: scripts/gpu_run.sh STEP [STEP ...]   (steps: tests smoke bench prof pmc)
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+ROOT=$(pwd)
+OUT=$ROOT/gpurun_out
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+step() {
+  local name=$1 t=$2; shift 2
+  echo "[$(date +%T)] start $name" | tee -a "$OUT/status.log"
+  timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "[$(date +%T)] $name rc=$rc" | tee -a "$OUT/status.log"
+  tail -5 "$OUT/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
+    echo "stopping after $name (rc=$rc)" | tee -a "$OUT/status.log"
+    exit $rc
+  fi
+}
+for s in "$@"; do
+  case $s in
+    build) step build 600 python -c "import __graft_entry__ as g; g.build()" ;;
+    tests) step tests 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
+    testsall) step testsall 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench 600 python bench.py --steps 20 --warmup 5 ;;
+    prof)
+      mkdir -p "$OUT/prof"
+      (cd /tmp && step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline) || exit $?
+      ;;
+    pmcfetch)
+      mkdir -p "$OUT/pmc_fetch"
+      (cd /tmp && step pmcfetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline) || exit $?
+      ;;
+    pmcwrite)
+      mkdir -p "$OUT/pmc_write"
+      (cd /tmp && step pmcwrite 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o run -- python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline) || exit $?
+      ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done

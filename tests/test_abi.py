@@ -1,0 +1,164 @@
+"""C-ABI boundary checks that need no GPU: the library loads, exports exactly
+what include/hbec.h declares, and its host-side logic (matrix build, decode
+rows, argument validation, ecutils helpers) matches the oracle / reference
+tests.  No GF compute call here (that needs the GPU: test_gpu_parity.py)."""
+import ctypes as C
+import itertools
+import re
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from hummingbird_amd import _native as N
+from hummingbird_amd import ecutils as E
+from hummingbird_amd import reedsolomon as RS
+from oracle import oracle as O
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def header_symbols():
+    text = (ROOT / "include" / "hbec.h").read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(hbec_[a-z0-9_]+)\s*\(", text)) - {"hbec_read_fn", "hbec_write_fn"})
+
+
+def test_library_exports_every_header_symbol():
+    N.lib()
+    out = subprocess.run(["nm", "-D", "--defined-only", str(N.LIB_PATH)], capture_output=True, text=True,
+                         check=True).stdout
+    exported = set(re.findall(r" T (hbec_[a-z0-9_]+)$", out, flags=re.M))
+    declared = set(header_symbols())
+    assert declared, "no symbols parsed from include/hbec.h"
+    assert declared <= exported, sorted(declared - exported)
+    assert declared == set(N.SYMBOLS)
+
+
+def test_version_and_strerror():
+    assert N.lib().hbec_version() == 1
+    assert N.strerror(N.ERR_TOO_FEW_SHARDS) == "too few shards given"
+    assert N.strerror(N.ERR_SHARD_SIZE) == "shard sizes do not match"
+
+
+@pytest.mark.parametrize("k,m,exc", [(0, 2, RS.ErrInvShardNum), (-1, 2, RS.ErrInvShardNum),
+                                     (4, -1, RS.ErrInvShardNum), (200, 57, RS.ErrMaxShardNum)])
+def test_new_errors(k, m, exc):
+    with pytest.raises(exc):
+        RS.New(k, m)
+
+
+@pytest.mark.parametrize("k,m", [(1, 0), (2, 1), (3, 2), (4, 2), (8, 3), (10, 4), (17, 3), (200, 56)])
+def test_matrix_matches_oracle(k, m):
+    enc = RS.New(k, m)
+    want = O.build_matrix(k, k + m) if k + m <= 20 else None
+    got = enc.matrix()
+    assert np.array_equal(got[:k], np.eye(k, dtype=np.uint8))
+    if want is not None:
+        assert got.tolist() == want
+
+
+@pytest.mark.parametrize("k,m", [(4, 2), (8, 3)])
+def test_decode_rows_match_oracle(k, m):
+    enc = RS.New(k, m)
+    oenc = O.Encoder(k, m)
+    for e in range(1, m + 1):
+        for missing in itertools.combinations(range(k + m), e):
+            present = [0 if i in missing else 1 for i in range(k + m)]
+            surv, outs, rows = enc.DecodeRows(present)
+            osurv, inv = oenc.decode_matrix(present)
+            assert surv == osurv
+            assert outs == list(missing)
+            for o, row in zip(outs, rows):
+                if o < k:
+                    want = inv[o]
+                else:  # parity rows fused with the inverse
+                    want = O.mat_mul([oenc.m[o]], inv)[0]
+                assert row.tolist() == want
+            surv_d, outs_d, _ = enc.DecodeRows(present, data_only=True)
+            assert outs_d == [i for i in missing if i < k]
+
+
+def test_encode_validation_before_device():
+    enc = RS.New(4, 2)
+    good = [np.ones(8, np.uint8) for _ in range(6)]
+    with pytest.raises(RS.ErrTooFewShards):
+        enc.Encode(good[:5])
+    with pytest.raises(RS.ErrShardSize):
+        enc.Encode(good[:5] + [np.ones(7, np.uint8)])
+    with pytest.raises(RS.ErrShardSize):
+        enc.Encode(good[:5] + [np.zeros(0, np.uint8)])
+    with pytest.raises(RS.ErrShardNoData):
+        enc.Encode([np.zeros(0, np.uint8)] * 6)
+
+
+def test_reconstruct_validation_before_device():
+    enc = RS.New(4, 2)
+    z = np.zeros(0, np.uint8)
+    with pytest.raises(RS.ErrShardNoData):
+        enc.Reconstruct([z] * 6)
+    with pytest.raises(RS.ErrShardSize):
+        enc.Reconstruct([np.ones(4, np.uint8)] * 5 + [np.ones(3, np.uint8)])
+    with pytest.raises(RS.ErrTooFewShards):
+        enc.Reconstruct([z, z, z] + [np.ones(4, np.uint8)] * 3)
+    with pytest.raises(RS.ErrTooFewShards):
+        enc.Reconstruct([np.ones(4, np.uint8)] * 5)
+    # nothing missing / all data present with ReconstructData: no work, no error, no GPU
+    full = [np.ones(4, np.uint8)] * 6
+    enc.Reconstruct(full)
+    enc.ReconstructData([np.ones(4, np.uint8)] * 4 + [z, z])
+
+
+def test_product_path_has_no_cpu_fallback():
+    torch = pytest.importorskip("torch")
+    if torch.cuda.is_available():
+        pytest.skip("GPU present: covered by test_gpu_parity")
+    enc = RS.New(4, 2)
+    with pytest.raises(RS.ErrDevice):
+        enc.Encode([np.ones(8, np.uint8) for _ in range(6)])
+
+
+def test_missing_library_fails_loudly(tmp_path, monkeypatch):
+    monkeypatch.setattr(N, "LIB_PATH", tmp_path / "nope.so")
+    monkeypatch.setattr(N, "_lib", None)
+    with pytest.raises(N.NativeLibraryError):
+        N.lib()
+
+
+def test_ecutils_host_kats(kats):
+    for length, k, want in kats["shard_length"]:
+        assert E.ec_shard_length(length, k) == want
+    for s, e, cs, k, ws, we in kats["range_chunk_align"]:
+        assert E.range_chunk_align(s, e, cs, k) == (ws, we)
+    for scheme, algo, k, m, c in kats["parse_ec_scheme"]["ok"]:
+        assert E.parse_ec_scheme(scheme) == (algo, k, m, c)
+    for scheme in kats["parse_ec_scheme"]["err"] + ["", "a/b", "reedsolomon/1/2/3/4", "reedsolomon/ 1/2/3",
+                                                    "reedsolomon/1/2/", "reedsolomon/1/+/3"]:
+        with pytest.raises(RS.ErrScheme):
+            E.parse_ec_scheme(scheme)
+    assert E.parse_ec_scheme("reedsolomon/+4/-2/0") == ("reedsolomon", 4, -2, 0)
+    assert E.parse_ec_scheme("xor/4/2/1048576") == ("xor", 4, 2, 1048576)
+
+
+def test_ec_split_zero_length_needs_no_device():
+    out = []
+
+    class W:
+        def write(self, b):
+            out.append(b)
+
+    E.ec_split(4, 2, None, 1 << 20, 0, [W() for _ in range(6)])
+    assert out == []
+
+
+def test_ec_split_short_read_is_unexpected_eof():
+    import io
+    with pytest.raises(RS.ErrUnexpectedEOF):
+        E.ec_split(4, 2, io.BytesIO(b""), 1 << 20, 10, [None] * 6)
+
+
+def test_header_has_c_linkage():
+    text = (ROOT / "include" / "hbec.h").read_text()
+    assert 'extern "C"' in text
+    assert "torch" not in text.lower()

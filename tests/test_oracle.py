@@ -1,0 +1,165 @@
+"""Pin the CPU oracle before trusting it (CPU only).
+
+The reference's codec (klauspost/reedsolomon) is not in /root/reference and
+no Go toolchain exists, so the oracle is pinned by (a) the upstream
+klauspost/Backblaze KATs and (b) the reference's own ecutils/ecobj tests,
+both in tests/golden/kats.json; then the C restatement (gf_oracle.c, scalar
+and AVX2) is checked against the Python one, and both against the committed
+vectors.
+"""
+import hashlib
+import io
+
+import numpy as np
+import pytest
+
+from oracle import coracle as CO
+from oracle import oracle as O
+
+
+def sha(b):
+    return hashlib.sha256(bytes(b)).hexdigest()
+
+
+def test_gal_mul_exp_kats(kats):
+    for a, b, want in kats["gal_mul"]:
+        assert O.gal_mul(a, b) == want
+        assert CO.lib().orc_gal_mul(a, b) == want
+    for a, n, want in kats["gal_exp"]:
+        assert O.gal_exp(a, n) == want
+        assert CO.lib().orc_gal_exp(a, n) == want
+
+
+def test_invert_kats(kats):
+    for case in kats["invert"]:
+        assert O.mat_invert(case["in"]) == case["out"]
+        assert CO.invert(case["in"]).tolist() == case["out"]
+
+
+def test_one_encode_kat(kats):
+    c = kats["one_encode"]
+    shards = [np.array(d, np.uint8) for d in c["data"]] + [np.zeros(2, np.uint8) for _ in range(c["m"])]
+    O.Encoder(c["k"], c["m"]).encode(shards)
+    assert [s.tolist() for s in shards[c["k"]:]] == c["parity"]
+    for impl in (CO.SCALAR, CO.AVX2):
+        mat = CO.build_matrix(c["k"], c["m"])
+        outs = CO.apply(mat[c["k"]:], [np.array(d, np.uint8) for d in c["data"]], impl)
+        assert [o.tolist() for o in outs] == c["parity"]
+
+
+def test_reference_ecutils_kats(kats):
+    for length, k, want in kats["shard_length"]:
+        assert O.ec_shard_length(length, k) == want
+    for s, e, cs, k, ws, we in kats["range_chunk_align"]:
+        assert O.range_chunk_align(s, e, cs, k) == (ws, we)
+    for scheme, algo, k, m, c in kats["parse_ec_scheme"]["ok"]:
+        assert O.parse_ec_scheme(scheme) == (algo, k, m, c)
+    for scheme in kats["parse_ec_scheme"]["err"]:
+        with pytest.raises(ValueError):
+            O.parse_ec_scheme(scheme)
+    st = kats["stabilize_lengths"]
+    files = O.ec_split(st["k"], st["m"], st["body"].encode(), st["chunk"])
+    assert [len(f) for f in files] == [st["shard_len"]] * (st["k"] + st["m"])
+
+
+@pytest.mark.parametrize("k,m", [(2, 1), (3, 2), (4, 2), (5, 5), (8, 3), (10, 4), (17, 3)])
+def test_c_matrix_matches_python(k, m):
+    assert CO.build_matrix(k, m).tolist() == O.build_matrix(k, k + m)
+
+
+def test_parity_rows_vectors(vectors):
+    for key, rows in vectors["parity_rows"].items():
+        k, m = map(int, key.split("+"))
+        assert O.Encoder(k, m).parity == rows
+        assert CO.build_matrix(k, m)[k:].tolist() == rows
+
+
+@pytest.mark.parametrize("k,m,n", [(4, 2, 4096), (8, 3, 1000), (5, 5, 33), (17, 3, 257)])
+def test_c_scalar_avx2_python_agree(k, m, n):
+    rng = np.random.default_rng(k * 100 + m)
+    data = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)]
+    mat = CO.build_matrix(k, m)[k:]
+    want = O.gf_apply(mat.tolist(), data)
+    for impl in (CO.SCALAR, CO.AVX2):
+        got = CO.apply(mat, data, impl)
+        assert all(np.array_equal(a, b) for a, b in zip(got, want))
+
+
+def test_splitmix_python_matches_c():
+    for idx, n in [(0, 1), (3, 7), (4095, 100), (12, 4096)]:
+        assert np.array_equal(O.object_bytes(idx, n), CO.fill_objects(idx, 1, n)[0])
+
+
+def test_seeded_vectors(vectors):
+    for case in vectors["seeded"]:
+        k, m, size = case["k"], case["m"], case["size"]
+        obj = CO.fill_objects(case["index"], 1, size)
+        assert sha(obj[0]) == case["object_sha256"]
+        par, _ = CO.encode_batch(k, m, obj)
+        s = size // k
+        got = [sha(obj[0][j * s:(j + 1) * s]) for j in range(k)] + [sha(par[0][r * s:(r + 1) * s]) for r in range(m)]
+        assert got == case["shard_sha256"]
+
+
+def test_erasure_vectors(vectors):
+    for case in vectors["erasures"]:
+        k, m = case["k"], case["m"]
+        enc = O.Encoder(k, m)
+        obj = O.object_bytes(case["index"], case["size"])
+        s = case["size"] // k
+        full = [obj[j * s:(j + 1) * s].copy() for j in range(k)] + [np.zeros(s, np.uint8) for _ in range(m)]
+        enc.encode(full)
+        assert [sha(x) for x in full] == case["shard_sha256"]
+        for p in case["patterns"][:: max(1, len(case["patterns"]) // 25)]:
+            sh = [x.copy() if i not in p["missing"] else np.zeros(0, np.uint8) for i, x in enumerate(full)]
+            enc.reconstruct(sh)
+            assert [sha(x) for x in sh] == case["shard_sha256"]
+            present = [0 if i in p["missing"] else 1 for i in range(k + m)]
+            surv, inv = enc.decode_matrix(present)
+            assert surv == p["survivors"]
+            assert [inv[i] for i in p["missing"] if i < k] == p["data_rows"]
+
+
+def test_ec_split_vectors(vectors):
+    for case in vectors["ec_split"]:
+        obj = O.object_bytes(case["object_seed_index"], case["size"]).tobytes()
+        files = O.ec_split(case["k"], case["m"], obj, case["chunk"])
+        assert [len(f) for f in files] == case["file_len"]
+        assert [sha(f) for f in files] == case["file_sha256"]
+        # every shard file is ecShardLength long (ecutils.go:14-24 / auditor.go size rule)
+        assert all(len(f) == O.ec_shard_length(case["size"], case["k"]) for f in files)
+        assert O.ec_glue(case["k"], case["m"], files, case["chunk"], case["size"]) == obj
+
+
+def test_testing_3_2_vector(vectors):
+    files = O.ec_split(3, 2, b"TESTING", 100)
+    assert [list(f) for f in files] == vectors["testing_3_2"]["files"]
+    assert files[3] == bytes([71, 12, 29]) and files[4] == bytes([62, 166, 76])
+
+
+def test_oracle_reconstruct_errors():
+    enc = O.Encoder(4, 2)
+    with pytest.raises(O.ErrTooFewShards):
+        enc.reconstruct([np.zeros(0, np.uint8)] * 3 + [np.ones(4, np.uint8)] * 3)
+    with pytest.raises(O.ErrShardNoData):
+        enc.reconstruct([np.zeros(0, np.uint8)] * 6)
+    with pytest.raises(O.ErrShardSize):
+        enc.reconstruct([np.ones(4, np.uint8)] * 5 + [np.ones(3, np.uint8)])
+    with pytest.raises(O.ErrTooFewShards):
+        enc.encode([np.ones(4, np.uint8)] * 5)
+    with pytest.raises(O.ErrInvShardNum):
+        O.Encoder(0, 2)
+    with pytest.raises(O.ErrMaxShardNum):
+        O.Encoder(200, 57)
+
+
+def test_ec_reconstruct_oracle_roundtrip():
+    obj = O.object_bytes(5, 10000).tobytes()
+    files = O.ec_split(4, 2, obj, 1024)
+    damaged = list(files)
+    damaged[1] = None
+    damaged[5] = None
+    out = O.ec_reconstruct(4, 2, damaged, 1024, len(obj), [1, 5])
+    assert out == [files[1], files[5]]
+    assert O.ec_glue(4, 2, damaged, 1024, len(obj)) == obj
+    assert io.BytesIO(obj).read() == obj
