@@ -46,15 +46,20 @@ def _stale(target: Path, deps: list[Path]) -> bool:
     return any(d.stat().st_mtime > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = True, defs=()) -> Path:
-    OBJ.mkdir(exist_ok=True)
+def build(force: bool = False, verbose: bool = True, defs=(), lib: Path | None = None,
+          objdir: Path | None = None) -> Path:
+    """Build libhbec.so (or, for tuning experiments, a variant with extra -D
+    definitions into `lib` / `objdir`)."""
+    lib = Path(lib) if lib else LIB
+    objdir = Path(objdir) if objdir else OBJ
+    objdir.mkdir(parents=True, exist_ok=True)
     hipcc = _hipcc()
     hdrs = [CSRC / h for h in HEADERS] + [INCLUDE / "hbec.h"]
     jobs = []
     objs = []
     for src in SOURCES:
         s = CSRC / src
-        o = OBJ / (src.rsplit(".", 1)[0] + ".o")
+        o = objdir / (src.rsplit(".", 1)[0] + ".o")
         objs.append(o)
         if force or _stale(o, [s] + hdrs):
             lang = ["-x", "hip"] if src.endswith(".hip") else []
@@ -69,10 +74,10 @@ def build(force: bool = False, verbose: bool = True, defs=()) -> Path:
 
     with ThreadPoolExecutor(max_workers=min(4, max(1, len(jobs)))) as ex:
         list(ex.map(run, jobs))
-    if force or jobs or _stale(LIB, objs):
-        run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(LIB), *map(str, objs),
+    if force or jobs or _stale(lib, objs):
+        run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(lib), *map(str, objs),
              "-lpthread"])
-    return LIB
+    return lib
 
 
 if __name__ == "__main__":

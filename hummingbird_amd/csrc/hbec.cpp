@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -43,6 +44,12 @@ int hip_fail(hipError_t e, const char* what) {
 }
 
 static std::atomic<int> g_force_stream{0};
+// Tuning knob: cap on resident blocks per CU used to size vec-kernel grids
+// (0 = the occupancy the compiler's register allocation allows).
+static const int g_blocks_per_cu_override = [] {
+    const char* e = std::getenv("HBEC_BLOCKS_PER_CU");
+    return e ? std::atoi(e) : 0;
+}();
 
 // ---------------------------------------------------------------------------
 // Per-device facts (CU count, occupancy per kernel shape)
@@ -139,7 +146,9 @@ int apply_views(int rows, int cols, const uint8_t* coeffs, const hbec_view* in, 
                     b.tiles_per_obj = (uint32_t)tpo;
                     b.n_tiles = (uint32_t)(no * tpo);
                     const uint64_t want_blocks = (b.n_tiles + (kBlockThreads / 64) - 1) / (kBlockThreads / 64);
-                    const uint64_t cap = (uint64_t)cus * (uint64_t)per_cu;
+                    const uint64_t cap = (uint64_t)cus * (uint64_t)(g_blocks_per_cu_override > 0
+                                                                         ? g_blocks_per_cu_override
+                                                                         : per_cu);
                     const int grid = (int)std::max<uint64_t>(1, std::min(want_blocks, cap));
                     hipError_t e = launch_vec(K, R, b, grid, stream, force_stream);
                     if (e != hipSuccess) return hip_fail(e, "launch gf_apply_vec");

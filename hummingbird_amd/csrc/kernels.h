@@ -8,7 +8,10 @@ namespace hbec {
 constexpr int kMaxK = 16;         // inputs per kernel pass
 constexpr int kMaxR = 4;          // outputs per kernel pass
 constexpr int kBlockThreads = 256;
-constexpr int kVecWavesPerSimd = 4;  // occupancy floor for the vec kernels (<=128 VGPRs)
+#ifndef HBEC_WAVES_PER_SIMD
+#define HBEC_WAVES_PER_SIMD 4
+#endif
+constexpr int kVecWavesPerSimd = HBEC_WAVES_PER_SIMD;  // occupancy floor for the vec kernels
 
 // One pass: out[r] (^)= XOR_{j<K} C[r][j] * in[j] over n_obj objects.
 // Input j of object o starts at in[j] + o*in_stride[j]; likewise outputs.

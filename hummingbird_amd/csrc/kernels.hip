@@ -69,14 +69,65 @@ __device__ __forceinline__ Sel selectors(uint32_t x) {
     return s;
 }
 
+#ifndef HBEC_XOR3
+#define HBEC_XOR3 1
+#endif
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // v_bitop3_b32: a ^ b ^ c
+}
+
+// acc ^ c*x as 3 perms folded by two 3-input XORs.
+__device__ __forceinline__ uint32_t gf_fma_sel(uint32_t acc, const Sel& s, uint32_t t0, uint32_t t1, uint32_t t2,
+                                               uint32_t t3, uint32_t t4) {
+    const uint32_t p0 = perm(t1, t0, s.s0), p1 = perm(t3, t2, s.s1), p2 = perm(t4, t4, s.s2);
+    return xor3(xor3(acc, p0, p1), p2, 0u);
+}
+
 __device__ __forceinline__ uint32_t gf_mul_sel(const Sel& s, uint32_t t0, uint32_t t1, uint32_t t2,
                                                uint32_t t3, uint32_t t4) {
     return perm(t1, t0, s.s0) ^ perm(t3, t2, s.s1) ^ perm(t4, t4, s.s2);
 }
 
+#ifndef HBEC_VGPR_TABLES
+#define HBEC_VGPR_TABLES 1
+#endif
+
+// Coefficient tables of one pass.  v_perm_b32 may read only one SGPR (GFX9
+// constant-bus limit), so the low halves t[0] and t[2] are copied to VGPRs
+// once per kernel instead of by a v_mov before every perm.
+template <int K, int R>
+struct Tables {
+    uint32_t lo0[R][K];
+    uint32_t lo2[R][K];
+};
+
+__device__ __forceinline__ uint32_t to_vgpr(uint32_t x) {
+#if HBEC_VGPR_TABLES
+    uint32_t r;
+    asm("v_mov_b32 %0, %1" : "=v"(r) : "s"(x));
+    return r;
+#else
+    return x;
+#endif
+}
+
+template <int K, int R>
+__device__ __forceinline__ Tables<K, R> load_tables(const PassArgs& a) {
+    Tables<K, R> t;
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            t.lo0[r][j] = to_vgpr(a.tab[r][j][0]);
+            t.lo2[r][j] = to_vgpr(a.tab[r][j][2]);
+        }
+    return t;
+}
+
 template <int K, int R, int U>
-__device__ __forceinline__ void process_tile(const PassArgs& a, uint64_t obj, uint64_t off0, bool full,
-                                             bool accumulate) {
+__device__ __forceinline__ void process_tile(const PassArgs& a, const Tables<K, R>& tb, uint64_t obj,
+                                             uint64_t off0, bool full, bool accumulate) {
     // Issue every load of the tile first (K x U x 16 B per lane in flight),
     // then retire one 1 KiB sub-tile at a time so only its accumulators and
     // selectors are live.
@@ -103,6 +154,38 @@ __device__ __forceinline__ void process_tile(const PassArgs& a, uint64_t obj, ui
             acc[r] = u32x4{0, 0, 0, 0};
             if (accumulate && live) acc[r] = *reinterpret_cast<const u32x4*>(a.out[r] + obj * a.out_stride[r] + off);
         }
+#if HBEC_XOR3
+        // 3K perm terms per (row, dword) folded into acc by v_bitop3 XOR3s:
+        // a pending odd term is carried so every XOR3 retires two terms.
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            uint32_t pend[R];
+            bool has = false;
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                const Sel sx = selectors(x[u][j][e]);
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const uint32_t* t = a.tab[r][j];
+                    const uint32_t p0 = perm(t[1], tb.lo0[r][j], sx.s0);
+                    const uint32_t p1 = perm(t[3], tb.lo2[r][j], sx.s1);
+                    const uint32_t p2 = perm(t[4], t[4], sx.s2);
+                    if (!has) {
+                        acc[r][e] = xor3(acc[r][e], p0, p1);
+                        pend[r] = p2;
+                    } else {
+                        acc[r][e] = xor3(acc[r][e], pend[r], p0);
+                        acc[r][e] = xor3(acc[r][e], p1, p2);
+                    }
+                }
+                has = !has;
+            }
+            if (has) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) acc[r][e] ^= pend[r];
+            }
+        }
+#else
 #pragma unroll
         for (int j = 0; j < K; ++j) {
 #pragma unroll
@@ -111,10 +194,11 @@ __device__ __forceinline__ void process_tile(const PassArgs& a, uint64_t obj, ui
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     const uint32_t* t = a.tab[r][j];
-                    acc[r][e] ^= gf_mul_sel(sx, t[0], t[1], t[2], t[3], t[4]);
+                    acc[r][e] ^= gf_mul_sel(sx, tb.lo0[r][j], t[1], tb.lo2[r][j], t[3], t[4]);
                 }
             }
         }
+#endif
         if (live) {
 #pragma unroll
             for (int r = 0; r < R; ++r) st16(a.out[r] + obj * a.out_stride[r] + off, acc[r]);
@@ -123,7 +207,18 @@ __device__ __forceinline__ void process_tile(const PassArgs& a, uint64_t obj, ui
 }
 
 // Sub-tiles (1 KiB each) per wave tile: keeps K*U*4 load VGPRs <= 32.
-__host__ __device__ constexpr int tile_kib(int k) { return k <= 2 ? 4 : (k <= 4 ? 2 : 1); }
+#ifndef HBEC_TILE_SMALL
+#define HBEC_TILE_SMALL 4
+#endif
+#ifndef HBEC_TILE_MID
+#define HBEC_TILE_MID 1
+#endif
+#ifndef HBEC_TILE_BIG
+#define HBEC_TILE_BIG 1
+#endif
+__host__ __device__ constexpr int tile_kib(int k) {
+    return k <= 2 ? HBEC_TILE_SMALL : (k <= 4 ? HBEC_TILE_MID : HBEC_TILE_BIG);
+}
 
 // Vector path: every base 16-B aligned, every stride and shard_len % 16 == 0.
 template <int K, int R>
@@ -135,15 +230,16 @@ __global__ __launch_bounds__(kBlockThreads, kVecWavesPerSimd) void gf_apply_vec(
     const uint32_t nwaves = gridDim.x * (kBlockThreads / 64);
     const uint32_t tpo = a.tiles_per_obj;
     const bool accumulate = a.accumulate != 0;
+    const Tables<K, R> tb = load_tables<K, R>(a);
     for (uint32_t t = wave; t < a.n_tiles; t += nwaves) {
         const uint32_t obj = t / tpo;
         const uint32_t tile = t - obj * tpo;
         const uint64_t tile_base = (uint64_t)tile * (uint64_t)(U * 1024);
         const uint64_t off0 = tile_base + lane * 16u;
         if (tile_base + (uint64_t)(U * 1024) <= a.shard_len) {
-            process_tile<K, R, U>(a, obj, off0, true, accumulate);
+            process_tile<K, R, U>(a, tb, obj, off0, true, accumulate);
         } else {
-            process_tile<K, R, U>(a, obj, off0, false, accumulate);
+            process_tile<K, R, U>(a, tb, obj, off0, false, accumulate);
         }
     }
 }

@@ -1,0 +1,248 @@
+#!/usr/bin/env python3
+"""A/B kernel variants of libhbec in ONE process, interleaved rounds.
+
+    python scripts/tune.py build            # on the CPU container: compile variants
+    python scripts/tune.py run [--rounds R] # on the GPU: time + cross-check
+
+Each variant = extra -D definitions (kernel shape) and/or env (grid sizing),
+built into tune_build/<name>/libhbec.so.  The run loads every variant with
+ctypes, runs the 4+2 @ 1 MiB x 4096 workload (encode + reconstruct{0,1}),
+checks every variant's parity and rebuilt bytes against the first variant's,
+and prints per-variant median / min kernel time and achieved GB/s.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+import os
+import statistics
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+OUTDIR = ROOT / "tune_build"
+
+BASE = ["HBEC_VGPR_TABLES=1", "HBEC_XOR3=1"]
+T1 = BASE + ["HBEC_TILE_MID=1"]
+VARIANTS = {
+    "t1": (T1, {}),
+    "t1_w8": (T1 + ["HBEC_WAVES_PER_SIMD=8"], {}),
+    "t1_b4": (T1, {"HBEC_BLOCKS_PER_CU": "4"}),
+    "t1_b6": (T1, {"HBEC_BLOCKS_PER_CU": "6"}),
+    "t1_b16": (T1, {"HBEC_BLOCKS_PER_CU": "16"}),
+    "t1_b64": (T1, {"HBEC_BLOCKS_PER_CU": "64"}),
+    "t1_w8_b16": (T1 + ["HBEC_WAVES_PER_SIMD=8"], {"HBEC_BLOCKS_PER_CU": "16"}),
+    "t1_ldplain": (T1 + ["HBEC_NT_LOADS=0"], {}),
+    "t1_stplain": (T1 + ["HBEC_NT_STORES=0"], {}),
+    "v0_orig": ([], {}),
+    "vt": (["HBEC_VGPR_TABLES=1"], {}),
+    "vt_x3": (BASE, {}),
+    "x3_ldplain": (BASE + ["HBEC_NT_LOADS=0"], {}),
+    "x3_stplain": (BASE + ["HBEC_NT_STORES=0"], {}),
+    "x3_plain": (BASE + ["HBEC_NT_LOADS=0", "HBEC_NT_STORES=0"], {}),
+    "x3_t1": (BASE + ["HBEC_TILE_MID=1"], {}),
+    "x3_t4": (BASE + ["HBEC_TILE_MID=4"], {}),
+    "x3_b2": (BASE, {"HBEC_BLOCKS_PER_CU": "2"}),
+    "x3_b8": (BASE + ["HBEC_WAVES_PER_SIMD=8"], {"HBEC_BLOCKS_PER_CU": "8"}),
+    "x3_w8": (BASE + ["HBEC_WAVES_PER_SIMD=8"], {}),
+}
+
+
+def build(names):
+    from hummingbird_amd import build as hb
+
+    for n in names:
+        defs, _ = VARIANTS[n]
+        d = OUTDIR / n
+        hb.build(defs=defs, lib=d / "libhbec.so", objdir=d / "obj", verbose=False)
+        print("built", n, flush=True)
+
+
+def run(names, rounds, n_obj, launches):
+    import torch
+
+    from hummingbird_amd import _native as N
+
+    torch.cuda.set_device(0)
+    k, m, s = 4, 2, (1 << 20) // 4
+    libs = {}
+    for n in names:
+        _, env = VARIANTS[n]
+        old = {e: os.environ.get(e) for e in env}
+        os.environ.update(env)
+        h = C.CDLL(str(OUTDIR / n / "libhbec.so"))
+        for e, v in old.items():
+            if v is None:
+                os.environ.pop(e, None)
+            else:
+                os.environ[e] = v
+        for name, res, args in N._SIG:
+            f = getattr(h, name)
+            f.restype, f.argtypes = res, args
+        codec = C.c_void_p()
+        assert h.hbec_new(k, m, C.byref(codec)) == 0
+        libs[n] = (h, codec)
+
+    objs = torch.empty((n_obj, 4 * s), dtype=torch.uint8, device="cuda")
+    h0 = libs[names[0]][0]
+    stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    assert h0.hbec_fill_splitmix(C.c_void_p(objs.data_ptr()), n_obj, 4 * s, 4 * s, 0x48424543, 0, stream) == 0
+    shared_p = torch.zeros((n_obj, 2 * s), dtype=torch.uint8, device="cuda")
+    shared_r = torch.zeros((n_obj, 2 * s), dtype=torch.uint8, device="cuda")
+    parity = {n: shared_p for n in names}
+    rebuilt = {n: shared_r for n in names}
+    ok = {n: [True, True] for n in names}
+    ref_p = None
+
+    def views(n):
+        enc = [(objs.data_ptr() + j * s, 4 * s) for j in range(4)] + \
+              [(parity[n].data_ptr() + r * s, 2 * s) for r in range(2)]
+        rec = list(enc)
+        rec[0] = (rebuilt[n].data_ptr(), 2 * s)
+        rec[1] = (rebuilt[n].data_ptr() + s, 2 * s)
+        mk = lambda vs: (N.View * 6)(*[N.View(b, st) for b, st in vs])  # noqa: E731
+        return mk(enc), mk(rec)
+
+    vv = {n: views(n) for n in names}
+    present = (C.c_uint8 * 6)(0, 0, 1, 1, 1, 1)
+    times = {n: {"enc": [], "rec": []} for n in names}
+    for rnd in range(rounds):
+        for n in names:
+            h, codec = libs[n]
+            ve, vr = vv[n]
+            evs = [torch.cuda.Event(enable_timing=True) for _ in range(2 * launches + 1)]
+            torch.cuda.synchronize()
+            evs[0].record()
+            for i in range(launches):
+                assert h.hbec_encode_batch(codec, ve, n_obj, s, stream) == 0
+                evs[2 * i + 1].record()
+                assert h.hbec_reconstruct_batch(codec, vr, present, n_obj, s, 0, stream) == 0
+                evs[2 * i + 2].record()
+            torch.cuda.synchronize()
+            if ref_p is None:
+                ref_p = shared_p.clone()
+            if rnd == rounds - 1:
+                ok[n] = [bool(torch.equal(shared_p, ref_p)), bool(torch.equal(shared_r, objs[:, :2 * s]))]
+                shared_p.zero_()
+                shared_r.zero_()
+            if rnd > 0:  # round 0 = warmup
+                for i in range(launches):
+                    times[n]["enc"].append(evs[2 * i].elapsed_time(evs[2 * i + 1]))
+                    times[n]["rec"].append(evs[2 * i + 1].elapsed_time(evs[2 * i + 2]))
+    bytes_per_launch = n_obj * 6 * s
+    res = []
+    for n in names:
+        okp, okr = ok[n]
+        h = libs[n][0]
+        tb, st, bpc = C.c_int(), C.c_int(), C.c_int()
+        h.hbec_kernel_info(4, 2, C.byref(tb), C.byref(st), C.byref(bpc))
+        e = statistics.median(times[n]["enc"])
+        r = statistics.median(times[n]["rec"])
+        row = {"variant": n, "enc_ms_med": round(e, 4), "rec_ms_med": round(r, 4),
+               "enc_ms_min": round(min(times[n]["enc"]), 4), "rec_ms_min": round(min(times[n]["rec"]), 4),
+               "enc_GBs": round(bytes_per_launch / e / 1e6, 1), "rec_GBs": round(bytes_per_launch / r / 1e6, 1),
+               "frac": round(2 * bytes_per_launch / (e + r) / 1e6 / 8000, 4), "parity_ok": okp, "rebuilt_ok": okr,
+               "tile": tb.value, "blocks_per_cu": bpc.value}
+        res.append(row)
+        print(json.dumps(row), flush=True)
+    return res
+
+
+def build_probe():
+    import subprocess
+    OUTDIR.mkdir(exist_ok=True)
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+                    "-x", "hip", str(ROOT / "scripts" / "hbm_probe.hip"), "-o", str(OUTDIR / "probe.so")],
+                   check=True)
+    print("built probe")
+
+
+def run_probe(reps=10):
+    import torch
+
+    torch.cuda.set_device(0)
+    h = C.CDLL(str(OUTDIR / "probe.so"))
+    h.probe_launch.restype = C.c_int
+    h.probe_launch.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32,
+                               C.c_int, C.c_void_p]
+    n_obj, S = 4096, 1 << 18
+    objs = torch.randint(0, 255, (n_obj, 4 * S), dtype=torch.uint8, device="cuda")
+    out = torch.empty((n_obj, 2 * S), dtype=torch.uint8, device="cuda")
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    cases = []
+    for grid in (1024, 2048, 4096, 8192):
+        cases += [("read4G", 0, objs, out, 4 << 30, 4 << 30, 0, grid),
+                  ("write2G", 1, objs, out, 2 << 30, 2 << 30, 0, grid),
+                  ("copy2G", 2, objs, out, 2 << 30, 4 << 30, 0, grid),
+                  ("xor42_objmajor", 3, objs, out, 0, 6 << 30, 0, grid),
+                  ("xor42_offmajor", 3, objs, out, 0, 6 << 30, 1, grid),
+                  ("xor40_read", 4, objs, out, 0, 4 << 30, 0, grid)]
+    for name, which, a, b, n, traffic, mode, grid in cases:
+        ts = []
+        for r in range(reps + 1):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            assert h.probe_launch(which, a.data_ptr(), b.data_ptr(), n, n_obj, S, mode, grid, st) == 0
+            e1.record()
+            torch.cuda.synchronize()
+            if r:
+                ts.append(e0.elapsed_time(e1))
+        med = statistics.median(ts)
+        print(json.dumps({"probe": name, "grid": grid, "ms": round(med, 4),
+                          "GBs": round(traffic / med / 1e6, 1), "frac": round(traffic / med / 1e6 / 8000, 4)}),
+              flush=True)
+    h.probe_write_variant.restype = C.c_int
+    h.probe_write_variant.argtypes = [C.c_int, C.c_void_p, C.c_uint64, C.c_int, C.c_void_p]
+    names = ["flat_plain", "flat_nt", "flat_plain_u4", "flat_nt_u4", "buf_aux0", "buf_nt", "buf_sc1", "buf_sc0sc1",
+             "buf_ntsc1", "buf_sc0", "flat_nt_u8"]
+    for grid in (512, 1024, 2048, 4096):
+        for v, nm in enumerate(names):
+            ts = []
+            for r in range(reps + 1):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                assert h.probe_write_variant(v, out.data_ptr(), 2 << 30, grid, st) == 0
+                e1.record()
+                torch.cuda.synchronize()
+                if r:
+                    ts.append(e0.elapsed_time(e1))
+            med = statistics.median(ts)
+            print(json.dumps({"probe": "w_" + nm, "grid": grid, "ms": round(med, 4),
+                              "GBs": round((2 << 30) / med / 1e6, 1), "frac": round((2 << 30) / med / 1e6 / 8000, 4)}),
+                  flush=True)
+    # torch / runtime references
+    for name, fn, traffic in [("torch_copy2G", lambda: out.view(-1).copy_(objs.view(-1)[: 2 << 30]), 4 << 30)]:
+        ts = []
+        for r in range(reps + 1):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            torch.cuda.synchronize()
+            if r:
+                ts.append(e0.elapsed_time(e1))
+        med = statistics.median(ts)
+        print(json.dumps({"probe": name, "ms": round(med, 4), "GBs": round(traffic / med / 1e6, 1),
+                          "frac": round(traffic / med / 1e6 / 8000, 4)}), flush=True)
+
+
+if __name__ == "__main__":
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("cmd", choices=["build", "run", "probe", "build_probe"])
+    ap.add_argument("--variants", default=",".join(VARIANTS))
+    ap.add_argument("--rounds", type=int, default=12)
+    ap.add_argument("--objects", type=int, default=4096)
+    ap.add_argument("--launches", type=int, default=5)
+    a = ap.parse_args()
+    names = a.variants.split(",")
+    if a.cmd == "build":
+        build(names)
+    elif a.cmd == "build_probe":
+        build_probe()
+    elif a.cmd == "probe":
+        run_probe()
+    else:
+        run(names, a.rounds, a.objects, a.launches)
