@@ -46,7 +46,7 @@ METRIC = "GiB/s device-resident EC encode+reconstruct, 4+2 @ 1 MiB; % HBM roofli
 GiB = float(1 << 30)
 MiB = 1 << 20
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
-KERNEL_NAME = "gf_apply_vec<4, 2>"
+KERNEL_NAME = "gf_apply_vec_pipe<4, 2>"
 
 
 def dist_env():
@@ -228,7 +228,7 @@ def main():
         traffic = None
         if pmc and KERNEL_NAME in pmc.get("kernels", {}):
             traffic = pmc["kernels"][KERNEL_NAME].get("hbm_bytes_per_launch")
-        info = B.kernel_info(k, m)
+        info = B.kernel_info(k, m, w.s)
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -262,7 +262,8 @@ def main():
                 "encode_ms_per_launch": round(enc_ms, 4),
                 "reconstruct_ms_per_launch": round(rec_ms, 4),
                 "traffic_source": pmc_file,
-                "tile_bytes": info["tile_bytes"], "blocks_per_cu": info["blocks_per_cu"],
+                "tile_bytes": info["tile_bytes"], "kernel_kind": info["kind"],
+                "blocks_per_cu": info["blocks_per_cu"],
             },
             "object_data_gib_s": round(value * k / (k + m), 2),
             "parity_ok": ok,

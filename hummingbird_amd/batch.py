@@ -87,10 +87,13 @@ def apply_views(rows: int, cols: int, coeffs, in_views, out_views, n_objects: in
                                    int(n_objects), int(shard_len), _stream_ptr(stream)))
 
 
-def kernel_info(k: int, r: int):
-    tb, st, bpc = C.c_int(), C.c_int(), C.c_int()
-    check(N.lib().hbec_kernel_info(k, r, C.byref(tb), C.byref(st), C.byref(bpc)))
-    return {"tile_bytes": tb.value, "streaming": bool(st.value), "blocks_per_cu": bpc.value}
+KERNEL_KINDS = {0: "unrolled", 1: "pipelined", 2: "streaming"}
+
+
+def kernel_info(k: int, r: int, shard_len: int):
+    tb, kind, bpc = C.c_int(), C.c_int(), C.c_int()
+    check(N.lib().hbec_kernel_info(k, r, int(shard_len), C.byref(tb), C.byref(kind), C.byref(bpc)))
+    return {"tile_bytes": tb.value, "kind": KERNEL_KINDS[kind.value], "blocks_per_cu": bpc.value}
 
 
 def set_force_stream(on: bool) -> None:

@@ -68,7 +68,7 @@ static int current_device(int* dev) {
     return HBEC_OK;
 }
 
-static int device_blocks(int dev, int k, int r, int force_stream, int* cus, int* per_cu) {
+static int device_blocks(int dev, int k, int r, int pipe, int force_stream, int* cus, int* per_cu) {
     std::lock_guard<std::mutex> g(g_dev_mu);
     DeviceInfo& d = g_devs[dev];
     if (d.cus == 0) {
@@ -77,11 +77,11 @@ static int device_blocks(int dev, int k, int r, int force_stream, int* cus, int*
         if (e != hipSuccess) return hip_fail(e, "hipGetDeviceProperties");
         d.cus = p.multiProcessorCount;
     }
-    const int key_k = force_stream ? -k : k;
+    const int key_k = force_stream ? -k : (pipe ? 1000 + k : k);
     auto it = d.blocks_per_cu.find({key_k, r});
     if (it == d.blocks_per_cu.end()) {
         int b = 0;
-        hipError_t e = vec_occupancy(k, r, force_stream, &b);
+        hipError_t e = vec_occupancy(k, r, pipe, force_stream, &b);
         if (e != hipSuccess) return hip_fail(e, "occupancy query");
         if (b < 1) b = 1;
         it = d.blocks_per_cu.emplace(std::make_pair(key_k, r), b).first;
@@ -131,9 +131,10 @@ int apply_views(int rows, int cols, const uint8_t* coeffs, const hbec_view* in, 
             a.accumulate = c0 > 0 ? 1u : 0u;
             if (vec) {
                 int cus = 0, per_cu = 0;
-                rc = device_blocks(dev, K, R, force_stream, &cus, &per_cu);
+                rc = device_blocks(dev, K, R, is_pipe_shape(K, R, shard_len, force_stream) && c0 == 0, force_stream,
+                                   &cus, &per_cu);
                 if (rc) return rc;
-                const uint64_t tile = (uint64_t)vec_tile_bytes(K, R, force_stream);
+                const uint64_t tile = (uint64_t)vec_tile_bytes(K, R, shard_len, c0 > 0, force_stream);
                 const uint64_t tpo = (shard_len + tile - 1) / tile;
                 // keep n_tiles < 2^31 per launch: split the batch by objects
                 const uint64_t max_obj = std::max<uint64_t>(1, (1ull << 31) / tpo);
@@ -499,17 +500,19 @@ int hbec_set_force_stream(int on) {
     return HBEC_OK;
 }
 
-int hbec_kernel_info(int k, int r, int* tile_bytes, int* streaming, int* blocks_per_cu) {
+int hbec_kernel_info(int k, int r, uint64_t shard_len, int* tile_bytes, int* kind, int* blocks_per_cu) {
     if (k < 1 || k > kMaxK || r < 1 || r > kMaxR) return fail(HBEC_ERR_INVALID_ARG, "shape out of range");
     const int fs = g_force_stream.load();
-    if (tile_bytes) *tile_bytes = vec_tile_bytes(k, r, fs);
-    if (streaming) *streaming = is_streaming_shape(k, r, fs);
+    const int pipe = is_pipe_shape(k, r, shard_len, fs);
+    if (tile_bytes) *tile_bytes = vec_tile_bytes(k, r, shard_len, 0, fs);
+    if (kind) *kind = is_streaming_shape(k, r, fs) ? 2 : (pipe ? 1 : 0);
     if (blocks_per_cu) {
         int dev = 0, cus = 0;
         int rc = current_device(&dev);
         if (rc) return rc;
-        rc = device_blocks(dev, k, r, fs, &cus, blocks_per_cu);
+        rc = device_blocks(dev, k, r, pipe, fs, &cus, blocks_per_cu);
         if (rc) return rc;
+        if (g_blocks_per_cu_override > 0) *blocks_per_cu = g_blocks_per_cu_override;
     }
     return HBEC_OK;
 }

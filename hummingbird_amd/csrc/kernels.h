@@ -30,12 +30,13 @@ struct PassArgs {
 };
 
 // Vec path launch: fully unrolled kernel for small shapes, streaming otherwise.
-int vec_tile_bytes(int k, int r, int force_stream);
+int vec_tile_bytes(int k, int r, uint64_t shard_len, int accumulate, int force_stream);
 int is_streaming_shape(int k, int r, int force_stream);
+int is_pipe_shape(int k, int r, uint64_t shard_len, int force_stream);
 hipError_t launch_vec(int k, int r, const PassArgs& a, int grid, hipStream_t stream, int force_stream);
 hipError_t launch_bytes(int k, int r, const PassArgs& a, int grid, hipStream_t stream);
 hipError_t launch_fill(uint8_t* dst, uint64_t n_obj, uint64_t obj_len, uint64_t obj_stride, uint64_t base_seed,
                        uint64_t first, int grid, hipStream_t stream);
-hipError_t vec_occupancy(int k, int r, int force_stream, int* blocks_per_cu);
+hipError_t vec_occupancy(int k, int r, int pipe, int force_stream, int* blocks_per_cu);
 
 }  // namespace hbec

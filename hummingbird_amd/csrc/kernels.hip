@@ -244,6 +244,122 @@ __global__ __launch_bounds__(kBlockThreads, kVecWavesPerSimd) void gf_apply_vec(
     }
 }
 
+// Pipelined vec path: few waves per CU (HBM works best with ~16-64 KiB of
+// loads in flight per CU, hbm_probe copy/xor sweeps), each wave keeping the
+// NEXT tile's loads in flight while it computes and stores the current one.
+// Tile = U x 1 KiB of each of the K inputs, U = 16 / K (K*U = 16 loads).
+__host__ __device__ constexpr int pipe_u(int k) { return k >= 16 ? 1 : (16 / k > 4 ? 4 : 16 / k); }
+
+// Branch-free tile load: lanes past the end of a partial tile read the last
+// 16 B of the shard instead (always in bounds); their results are never
+// stored.  No per-load exec branches, so the compiler keeps counted waits.
+template <int K, int R, int U>
+__device__ __forceinline__ void load_tile(u32x4 (&x)[U][K], const PassArgs& a, uint64_t obj, uint64_t off0) {
+    const uint64_t last = a.shard_len - 16u;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        uint64_t off = off0 + (uint64_t)u * 1024u;
+        off = off < last ? off : last;
+#pragma unroll
+        for (int j = 0; j < K; ++j) x[u][j] = ld16(a.in[j] + obj * a.in_stride[j] + off);
+    }
+}
+
+template <int K, int R, int U>
+__device__ __forceinline__ void compute_store_tile(const u32x4 (&x)[U][K], const PassArgs& a, const Tables<K, R>& tb,
+                                                   uint64_t obj, uint64_t off0, bool full, bool accumulate) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint64_t off = off0 + (uint64_t)u * 1024u;
+        const bool live = full || off < a.shard_len;
+        u32x4 acc[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            acc[r] = u32x4{0, 0, 0, 0};
+            if (accumulate && live) acc[r] = *reinterpret_cast<const u32x4*>(a.out[r] + obj * a.out_stride[r] + off);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            uint32_t pend[R];
+            bool has = false;
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                const Sel sx = selectors(x[u][j][e]);
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const uint32_t* t = a.tab[r][j];
+                    const uint32_t p0 = perm(t[1], tb.lo0[r][j], sx.s0);
+                    const uint32_t p1 = perm(t[3], tb.lo2[r][j], sx.s1);
+                    const uint32_t p2 = perm(t[4], t[4], sx.s2);
+                    if (!has) {
+                        acc[r][e] = xor3(acc[r][e], p0, p1);
+                        pend[r] = p2;
+                    } else {
+                        acc[r][e] = xor3(acc[r][e], pend[r], p0);
+                        acc[r][e] = xor3(acc[r][e], p1, p2);
+                    }
+                }
+                has = !has;
+            }
+            if (has) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) acc[r][e] ^= pend[r];
+            }
+        }
+        if (live) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) st16(a.out[r] + obj * a.out_stride[r] + off, acc[r]);
+        }
+    }
+}
+
+#ifndef HBEC_USE_PIPE
+#define HBEC_USE_PIPE 1
+#endif
+#ifndef HBEC_PIPE_WAVES_PER_SIMD
+#define HBEC_PIPE_WAVES_PER_SIMD 1
+#endif
+
+template <int K, int R>
+__global__ __launch_bounds__(kBlockThreads, HBEC_PIPE_WAVES_PER_SIMD) void gf_apply_vec_pipe(PassArgs a) {
+    // never launched with a.accumulate (launch_vec routes those to gf_apply_vec)
+    constexpr int U = pipe_u(K);
+    constexpr uint64_t TILE = (uint64_t)U * 1024u;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave =
+        __builtin_amdgcn_readfirstlane(blockIdx.x * (kBlockThreads / 64) + (threadIdx.x >> 6));
+    const uint32_t nwaves = gridDim.x * (kBlockThreads / 64);
+    const uint32_t tpo = a.tiles_per_obj;
+    const Tables<K, R> tb = load_tables<K, R>(a);
+    uint32_t t = wave;
+    if (t >= a.n_tiles) return;
+    u32x4 cur[U][K];
+    uint32_t obj = t / tpo;
+    uint64_t base = (uint64_t)(t - obj * tpo) * TILE;
+    load_tile<K, R, U>(cur, a, obj, base + lane * 16u);
+    // steady state: next tile's loads in flight while this tile computes
+    for (uint32_t tn = t + nwaves; tn < a.n_tiles; tn += nwaves) {
+        u32x4 nxt[U][K];
+        const uint32_t obj_n = tn / tpo;
+        const uint64_t base_n = (uint64_t)(tn - obj_n * tpo) * TILE;
+        load_tile<K, R, U>(nxt, a, obj_n, base_n + lane * 16u);
+        if (base + TILE <= a.shard_len)
+            compute_store_tile<K, R, U>(cur, a, tb, obj, base + lane * 16u, true, false);
+        else
+            compute_store_tile<K, R, U>(cur, a, tb, obj, base + lane * 16u, false, false);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int j = 0; j < K; ++j) cur[u][j] = nxt[u][j];
+        obj = obj_n;
+        base = base_n;
+    }
+    if (base + TILE <= a.shard_len)
+        compute_store_tile<K, R, U>(cur, a, tb, obj, base + lane * 16u, true, false);
+    else
+        compute_store_tile<K, R, U>(cur, a, tb, obj, base + lane * 16u, false, false);
+}
+
 // Streaming vec path (runtime K): one input shard at a time with the next
 // input's loads in flight, coefficient tables fetched per input by scalar
 // loads, so registers stay at R x 4 KiB accumulators + 2 x 4 KiB buffers for
@@ -379,32 +495,33 @@ __global__ __launch_bounds__(kBlockThreads) void fill_splitmix(uint8_t* dst, uin
 // Host-side launch table
 // ---------------------------------------------------------------------------
 template <int K, int R>
-static const void* vec_kernel_ptr() {
+static const void* vec_kernel_ptr(bool pipe) {
+    if (pipe) return reinterpret_cast<const void*>(&gf_apply_vec_pipe<K, R>);
     return reinterpret_cast<const void*>(&gf_apply_vec<K, R>);
 }
 
 // Fully unrolled instantiations that compile spill-free (checked with
 // -Rpass-analysis=kernel-resource-usage); other shapes use the streaming kernel.
 template <int K>
-static const void* vec_kernel_for_r(int r) {
+static const void* vec_kernel_for_r(int r, bool pipe) {
     switch (r) {
-        case 1: return vec_kernel_ptr<K, 1>();
-        case 2: return vec_kernel_ptr<K, 2>();
-        case 3: return vec_kernel_ptr<K, 3>();
+        case 1: return vec_kernel_ptr<K, 1>(pipe);
+        case 2: return vec_kernel_ptr<K, 2>(pipe);
+        case 3: return vec_kernel_ptr<K, 3>(pipe);
     }
     return nullptr;
 }
 
-static const void* unrolled_kernel(int k, int r) {
+static const void* unrolled_kernel(int k, int r, bool pipe) {
     switch (k) {
-        case 1: return vec_kernel_for_r<1>(r);
-        case 2: return vec_kernel_for_r<2>(r);
-        case 3: return vec_kernel_for_r<3>(r);
-        case 4: return vec_kernel_for_r<4>(r);
-        case 5: return vec_kernel_for_r<5>(r);
-        case 6: return vec_kernel_for_r<6>(r);
-        case 7: return vec_kernel_for_r<7>(r);
-        case 8: return vec_kernel_for_r<8>(r);
+        case 1: return vec_kernel_for_r<1>(r, pipe);
+        case 2: return vec_kernel_for_r<2>(r, pipe);
+        case 3: return vec_kernel_for_r<3>(r, pipe);
+        case 4: return vec_kernel_for_r<4>(r, pipe);
+        case 5: return vec_kernel_for_r<5>(r, pipe);
+        case 6: return vec_kernel_for_r<6>(r, pipe);
+        case 7: return vec_kernel_for_r<7>(r, pipe);
+        case 8: return vec_kernel_for_r<8>(r, pipe);
     }
     return nullptr;
 }
@@ -419,15 +536,31 @@ static const void* stream_kernel(int r) {
     return nullptr;
 }
 
-int is_streaming_shape(int k, int r, int force_stream) { return (force_stream || !unrolled_kernel(k, r)) ? 1 : 0; }
+int is_streaming_shape(int k, int r, int force_stream) {
+    return (force_stream || !unrolled_kernel(k, r, false)) ? 1 : 0;
+}
 
-int vec_tile_bytes(int k, int r, int force_stream) {
-    if (!force_stream && unrolled_kernel(k, r)) return tile_kib(k) * 1024;
+// The pipelined kernel wants whole tiles; short shards (e.g. 8+3 of a 4 KiB
+// object: 512 B) take the 1 KiB-tile kernel so fewer lanes idle.
+static bool use_pipe(int k, uint64_t shard_len, bool accumulate) {
+    return HBEC_USE_PIPE && !accumulate && shard_len >= (uint64_t)pipe_u(k) * 1024u;
+}
+
+int is_pipe_shape(int k, int r, uint64_t shard_len, int force_stream) {
+    return (!is_streaming_shape(k, r, force_stream) && use_pipe(k, shard_len, false)) ? 1 : 0;
+}
+
+int vec_tile_bytes(int k, int r, uint64_t shard_len, int accumulate, int force_stream) {
+    if (!force_stream && unrolled_kernel(k, r, false))
+        return (use_pipe(k, shard_len, accumulate != 0) ? pipe_u(k) : tile_kib(k)) * 1024;
     return 4 * 1024;
 }
 
 hipError_t launch_vec(int k, int r, const PassArgs& a, int grid, hipStream_t stream, int force_stream) {
-    const void* fn = force_stream ? nullptr : unrolled_kernel(k, r);
+    // accumulate passes (inputs beyond kMaxK) need the output read-back, which
+    // the pipelined kernel does not do: they take the plain unrolled kernel.
+    const bool pipe = use_pipe(k, a.shard_len, a.accumulate != 0);
+    const void* fn = force_stream ? nullptr : unrolled_kernel(k, r, pipe);
     if (fn) {
         void* args[] = {const_cast<PassArgs*>(&a)};
         return hipLaunchKernel(fn, dim3(grid), dim3(kBlockThreads), args, 0, stream);
@@ -450,8 +583,8 @@ hipError_t launch_fill(uint8_t* dst, uint64_t n_obj, uint64_t obj_len, uint64_t 
     return hipGetLastError();
 }
 
-hipError_t vec_occupancy(int k, int r, int force_stream, int* blocks_per_cu) {
-    const void* fn = force_stream ? nullptr : unrolled_kernel(k, r);
+hipError_t vec_occupancy(int k, int r, int pipe, int force_stream, int* blocks_per_cu) {
+    const void* fn = force_stream ? nullptr : unrolled_kernel(k, r, pipe != 0);
     if (!fn) fn = stream_kernel(r);
     if (!fn) return hipErrorInvalidValue;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, kBlockThreads, 0);

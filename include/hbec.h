@@ -115,10 +115,12 @@ int hbec_apply_batch(int rows, int cols, const uint8_t* coeffs, const hbec_view*
 int hbec_fill_splitmix(void* dst, uint64_t n_objects, uint64_t obj_len, uint64_t obj_stride, uint64_t base_seed,
                        uint64_t first, void* hip_stream);
 
-/* Tuning / introspection: force the runtime-K streaming kernel (0/1) and
- * report the kernel shape a (k, r) pass uses. */
+/* Tuning / introspection: force the runtime-K streaming kernel (0/1), and
+ * report what a pass of k inputs -> r outputs over shard_len bytes launches:
+ * tile bytes per wave, kind (0 = unrolled, 1 = pipelined, 2 = streaming) and
+ * resident blocks per CU used to size the grid. */
 int hbec_set_force_stream(int on);
-int hbec_kernel_info(int k, int r, int* tile_bytes, int* streaming, int* blocks_per_cu);
+int hbec_kernel_info(int k, int r, uint64_t shard_len, int* tile_bytes, int* kind, int* blocks_per_cu);
 
 /* ---------------------------------------------------------------------------
  * ecutils.go stripe loops over io callbacks (objectserver/ecutils.go:14-186,

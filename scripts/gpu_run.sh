@@ -39,6 +39,9 @@ for s in "$@"; do
       mkdir -p "$OUT/pmc_write"
       (cd /tmp && step pmcwrite 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o run -- python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline) || exit $?
       ;;
+    xorsweep) step xorsweep 600 python scripts/tune.py xorsweep ;;
+    copysweep) step copysweep 600 python scripts/tune.py copysweep ;;
+    layout) step layout 600 python scripts/tune.py layout ;;
     probe) step probe 600 python scripts/tune.py probe ;;
     tune) step tune 900 python scripts/tune.py run ${TUNE_ARGS:-} ;;
     *) echo "unknown step $s"; exit 2 ;;

@@ -85,6 +85,36 @@ __global__ __launch_bounds__(256) void probe_xor40(const uint8_t* objs, uint8_t*
 
 }  // extern "C"
 
+// 6-stream xor probe with U consecutive 1 KiB tiles per wave iteration
+template <int U>
+__global__ __launch_bounds__(256) void probe_xor42u(const uint8_t* objs, uint8_t* out, uint32_t n_obj, uint32_t S) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    const uint32_t nw = gridDim.x * 4;
+    const uint32_t tpo = S / (1024 * U);
+    const uint32_t nt = n_obj * tpo;
+    for (uint32_t t = wave; t < nt; t += nw) {
+        const uint32_t o = t / tpo, tile = t - o * tpo;
+        const uint64_t off = (uint64_t)tile * 1024 * U + lane * 16;
+        u32x4 x[U][4];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                x[u][j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(
+                    objs + (uint64_t)o * 4 * S + (uint64_t)j * S + off + u * 1024));
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                u32x4 a = {(uint32_t)r, 0, 0, 0};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) a ^= x[u][j];
+                __builtin_nontemporal_store(a, reinterpret_cast<u32x4*>(out + (uint64_t)o * 2 * S + (uint64_t)r * S + off + u * 1024));
+            }
+    }
+}
+
 // store-flavour probes: aux bits of the buffer store (1 = sc0, 2 = nt, 16 = sc1)
 template <int AUX, int UNR>
 __global__ __launch_bounds__(256) void probe_write_buf(uint8_t* dst, uint64_t n16) {
@@ -117,7 +147,50 @@ __global__ __launch_bounds__(256) void probe_write_flat(uint8_t* dst, uint64_t n
     }
 }
 
+// copy sweep: block-contiguous chunk of U x blockDim float4 per iteration,
+// all U loads issued before the U stores.
+template <int U, int NT>
+__global__ void probe_copy_u(const uint8_t* src, uint8_t* dst, uint64_t n16) {
+    const u32x4* s = reinterpret_cast<const u32x4*>(src);
+    u32x4* d = reinterpret_cast<u32x4*>(dst);
+    const uint64_t chunk = (uint64_t)U * blockDim.x;
+    for (uint64_t base = (uint64_t)blockIdx.x * chunk; base < n16; base += (uint64_t)gridDim.x * chunk) {
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = base + (uint64_t)u * blockDim.x + threadIdx.x;
+            if (NT) v[u] = __builtin_nontemporal_load(s + i); else v[u] = s[i];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = base + (uint64_t)u * blockDim.x + threadIdx.x;
+            if (NT) __builtin_nontemporal_store(v[u], d + i); else d[i] = v[u];
+        }
+    }
+}
+
 extern "C" {
+int probe_xor_variant(int u, const void* src, void* dst, uint32_t n_obj, uint32_t S, int grid, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    const uint8_t* a = (const uint8_t*)src;
+    uint8_t* b = (uint8_t*)dst;
+    if (u == 1) hipLaunchKernelGGL((probe_xor42u<1>), dim3(grid), dim3(256), 0, st, a, b, n_obj, S);
+    else if (u == 2) hipLaunchKernelGGL((probe_xor42u<2>), dim3(grid), dim3(256), 0, st, a, b, n_obj, S);
+    else if (u == 4) hipLaunchKernelGGL((probe_xor42u<4>), dim3(grid), dim3(256), 0, st, a, b, n_obj, S);
+    else return -1;
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+int probe_copy_variant(int u, int nt, const void* src, void* dst, uint64_t n, int grid, int block, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    const uint8_t* a = (const uint8_t*)src;
+    uint8_t* b = (uint8_t*)dst;
+    const uint64_t n16 = n / 16;
+    if (n16 % ((uint64_t)u * block)) return -3;
+#define CASE(U, NT) if (u == U && nt == NT) hipLaunchKernelGGL((probe_copy_u<U, NT>), dim3(grid), dim3(block), 0, st, a, b, n16);
+    CASE(1, 0) CASE(2, 0) CASE(4, 0) CASE(8, 0) CASE(1, 1) CASE(2, 1) CASE(4, 1) CASE(8, 1)
+#undef CASE
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
 static int grid_for(int blocks) { return blocks; }
 
 int probe_write_variant(int v, void* dst, uint64_t n, int grid, void* stream) {

@@ -25,7 +25,23 @@ OUTDIR = ROOT / "tune_build"
 
 BASE = ["HBEC_VGPR_TABLES=1", "HBEC_XOR3=1"]
 T1 = BASE + ["HBEC_TILE_MID=1"]
+T2 = BASE + ["HBEC_TILE_MID=2"]
+T4 = BASE + ["HBEC_TILE_MID=4"]
+P = T1 + ["HBEC_USE_PIPE=1"]
 VARIANTS = {
+    "pipe": (P, {}),
+    "pipe_b1": (P, {"HBEC_BLOCKS_PER_CU": "1"}),
+    "pipe_b2": (P, {"HBEC_BLOCKS_PER_CU": "2"}),
+    "pipe_b3": (P, {"HBEC_BLOCKS_PER_CU": "3"}),
+    "pipe_ldplain_b1": (P + ["HBEC_NT_LOADS=0"], {"HBEC_BLOCKS_PER_CU": "1"}),
+    "pipe_stplain_b1": (P + ["HBEC_NT_STORES=0"], {"HBEC_BLOCKS_PER_CU": "1"}),
+    "t1_b1": (T1, {"HBEC_BLOCKS_PER_CU": "1"}),
+    "t1_b2": (T1, {"HBEC_BLOCKS_PER_CU": "2"}),
+    "t1_b3": (T1, {"HBEC_BLOCKS_PER_CU": "3"}),
+    "t2_b1": (T2, {"HBEC_BLOCKS_PER_CU": "1"}),
+    "t2_b2": (T2, {"HBEC_BLOCKS_PER_CU": "2"}),
+    "t4_b1": (T4, {"HBEC_BLOCKS_PER_CU": "1"}),
+    "t4_b2": (T4, {"HBEC_BLOCKS_PER_CU": "2"}),
     "t1": (T1, {}),
     "t1_w8": (T1 + ["HBEC_WAVES_PER_SIMD=8"], {}),
     "t1_b4": (T1, {"HBEC_BLOCKS_PER_CU": "4"}),
@@ -136,7 +152,7 @@ def run(names, rounds, n_obj, launches):
         okp, okr = ok[n]
         h = libs[n][0]
         tb, st, bpc = C.c_int(), C.c_int(), C.c_int()
-        h.hbec_kernel_info(4, 2, C.byref(tb), C.byref(st), C.byref(bpc))
+        h.hbec_kernel_info(4, 2, s, C.byref(tb), C.byref(st), C.byref(bpc))
         e = statistics.median(times[n]["enc"])
         r = statistics.median(times[n]["rec"])
         row = {"variant": n, "enc_ms_med": round(e, 4), "rec_ms_med": round(r, 4),
@@ -147,6 +163,125 @@ def run(names, rounds, n_obj, launches):
         res.append(row)
         print(json.dumps(row), flush=True)
     return res
+
+
+def run_layout(reps=8):
+    """Encode/reconstruct time vs. buffer placement (default lib)."""
+    import torch
+
+    from hummingbird_amd import _native as N
+    from hummingbird_amd import batch as B
+    from hummingbird_amd import reedsolomon as RS
+
+    torch.cuda.set_device(0)
+    n_obj, S = 4096, 1 << 18
+    enc = RS.New(4, 2)
+    pool_bytes = (4 * S + 64 * 1024) * n_obj + 2 * (2 * S + 64 * 1024) * n_obj + (64 << 20)
+    pool = torch.empty(pool_bytes, dtype=torch.uint8, device="cuda")
+    base = pool.data_ptr()
+    present = [0, 0, 1, 1, 1, 1]
+    results = []
+    for obj_pad in (0, 4096, 16384, 65536):
+        for par_off in (0, 4096, 1 << 20, (32 << 20) + 4096):
+            ostride = 4 * S + obj_pad
+            pstride = 2 * S + obj_pad
+            obase = base
+            pbase = base + ostride * n_obj + par_off
+            pbase = (pbase + 4095) // 4096 * 4096 + (par_off % 4096)
+            rbase = pbase + pstride * n_obj + 4096
+            # every byte any kernel touches must lie inside the pool
+            assert obase + ostride * n_obj <= base + pool_bytes
+            assert rbase + pstride * (n_obj - 1) + 2 * S <= base + pool_bytes, "layout exceeds pool"
+            assert pbase + pstride * (n_obj - 1) + 2 * S <= rbase
+            assert N.lib().hbec_fill_splitmix(C.c_void_p(obase), n_obj, 4 * S, ostride, 0x48424543, 0,
+                                               C.c_void_p(torch.cuda.current_stream().cuda_stream)) == 0
+            ev = [(obase + j * S, ostride) for j in range(4)] + [(pbase + r * S, pstride) for r in range(2)]
+            rv = [(rbase, pstride), (rbase + S, pstride)] + ev[2:]
+            te, tr = [], []
+            for r in range(reps + 1):
+                e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+                e0.record()
+                B.encode_views(enc, ev, n_obj, S)
+                e1.record()
+                B.reconstruct_views(enc, rv, present, n_obj, S)
+                e2.record()
+                torch.cuda.synchronize()
+                if r:
+                    te.append(e0.elapsed_time(e1))
+                    tr.append(e1.elapsed_time(e2))
+            e, rr = statistics.median(te), statistics.median(tr)
+            row = {"obj_pad": obj_pad, "par_off": par_off, "enc_ms": round(e, 4), "rec_ms": round(rr, 4),
+                   "frac": round(2 * n_obj * 6 * S / (e + rr) / 1e6 / 8000, 4)}
+            results.append(row)
+            print(json.dumps(row), flush=True)
+    return results
+
+
+def run_copy_sweep(reps=8):
+    import torch
+
+    torch.cuda.set_device(0)
+    h = C.CDLL(str(OUTDIR / "probe.so"))
+    h.probe_copy_variant.restype = C.c_int
+    h.probe_copy_variant.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_int, C.c_int,
+                                     C.c_void_p]
+    n = 2 << 30
+    src = torch.empty(n, dtype=torch.uint8, device="cuda")
+    dst = torch.empty(n, dtype=torch.uint8, device="cuda")
+    src.random_(0, 255)
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    best = []
+    for block in (256, 512, 1024):
+        for u in (1, 2, 4, 8):
+            for nt in (0, 1):
+                for grid in (256, 512, 1024, 2048, 4096, 16384):
+                    ts = []
+                    for r in range(reps + 1):
+                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        e0.record()
+                        rc = h.probe_copy_variant(u, nt, src.data_ptr(), dst.data_ptr(), n, grid, block, st)
+                        assert rc == 0, rc
+                        e1.record()
+                        torch.cuda.synchronize()
+                        if r:
+                            ts.append(e0.elapsed_time(e1))
+                    med = statistics.median(ts)
+                    row = {"block": block, "u": u, "nt": nt, "grid": grid, "ms": round(med, 4),
+                           "GBs": round(2 * n / med / 1e6, 1)}
+                    best.append(row)
+                    print(json.dumps(row), flush=True)
+    assert torch.equal(src, dst)
+    best.sort(key=lambda r: -r["GBs"])
+    print("TOP", json.dumps(best[:8]))
+
+
+def run_xor_sweep(reps=8):
+    import torch
+
+    torch.cuda.set_device(0)
+    h = C.CDLL(str(OUTDIR / "probe.so"))
+    h.probe_xor_variant.restype = C.c_int
+    h.probe_xor_variant.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.c_void_p]
+    n_obj, S = 4096, 1 << 18
+    objs = torch.empty((n_obj, 4 * S), dtype=torch.uint8, device="cuda")
+    out = torch.empty((n_obj, 2 * S), dtype=torch.uint8, device="cuda")
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    rows = []
+    for u in (1, 2, 4):
+        for grid in (256, 512, 768, 1024, 1792, 2048, 4096):
+            ts = []
+            for r in range(reps + 1):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                assert h.probe_xor_variant(u, objs.data_ptr(), out.data_ptr(), n_obj, S, grid, st) == 0
+                e1.record()
+                torch.cuda.synchronize()
+                if r:
+                    ts.append(e0.elapsed_time(e1))
+            med = statistics.median(ts)
+            row = {"u": u, "grid": grid, "ms": round(med, 4), "GBs": round(n_obj * 6 * S / med / 1e6, 1)}
+            rows.append(row)
+            print(json.dumps(row), flush=True)
 
 
 def build_probe():
@@ -231,7 +366,7 @@ if __name__ == "__main__":
     import argparse
 
     ap = argparse.ArgumentParser()
-    ap.add_argument("cmd", choices=["build", "run", "probe", "build_probe"])
+    ap.add_argument("cmd", choices=["build", "run", "probe", "build_probe", "layout", "copysweep", "xorsweep"])
     ap.add_argument("--variants", default=",".join(VARIANTS))
     ap.add_argument("--rounds", type=int, default=12)
     ap.add_argument("--objects", type=int, default=4096)
@@ -244,5 +379,11 @@ if __name__ == "__main__":
         build_probe()
     elif a.cmd == "probe":
         run_probe()
+    elif a.cmd == "xorsweep":
+        run_xor_sweep()
+    elif a.cmd == "copysweep":
+        run_copy_sweep()
+    elif a.cmd == "layout":
+        run_layout()
     else:
         run(names, a.rounds, a.objects, a.launches)

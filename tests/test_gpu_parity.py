@@ -358,3 +358,23 @@ def test_baseline_size_4096x1mib_roundtrip():
     sample = list(range(0, n, 64))
     want, _ = CO.encode_batch(k, m, objs[sample].cpu().numpy(), threads=CO.cpu_threads())
     assert np.array_equal(parity[sample].cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("k,m,s,n", [(4, 2, 5 * 4096 + 48, 7), (8, 3, 3 * 2048 + 16, 5), (2, 2, 4096 * 2 + 1024, 3),
+                                     (4, 2, 4096, 1), (6, 3, 16 * 1024, 300), (4, 1, 256 * 1024, 9)])
+def test_batch_pipelined_partial_tiles(k, m, s, n):
+    """Shard lengths that are not a multiple of the pipelined kernel's tile,
+    and grids with fewer tiles than waves."""
+    objs = torch.empty((n, k * s), dtype=torch.uint8, device="cuda")
+    B.fill_splitmix(objs, k * s, first=s)
+    parity = torch.full((n, m * s + 64), 0x5A, dtype=torch.uint8, device="cuda")
+    enc = RS.New(k, m)
+    B.encode_views(enc, B.shard_views(objs, k, s) + [(parity.data_ptr() + r * s, parity.stride(0))
+                                                     for r in range(m)], n, s)
+    torch.cuda.synchronize()
+    want, _ = CO.encode_batch(k, m, objs.cpu().numpy(), threads=CO.cpu_threads())
+    got = parity.cpu().numpy()
+    assert np.array_equal(got[:, :m * s], want)
+    assert (got[:, m * s:] == 0x5A).all()  # nothing written past the last shard
+    info = B.kernel_info(k, m, s)
+    assert info["tile_bytes"] > 0
