@@ -61,6 +61,16 @@ def partition(n_per_rank: int, rank: int) -> tuple[int, int]:
     return rank * n_per_rank, n_per_rank
 
 
+def max_over_ranks(pg, values, device):
+    """Element-wise max of a list of floats over all ranks (the only
+    collective in the bench: control, not data path)."""
+    if pg is None:
+        return list(values)
+    t = torch.tensor(list(values), dtype=torch.float64, device=device)
+    pg.all_reduce(t, op=pg.ReduceOp.MAX)
+    return t.tolist()
+
+
 def load_pmc(prefix_glob="profiles/*_pmc.json"):
     files = sorted(glob.glob(str(ROOT / prefix_glob)))
     if not files:
@@ -130,7 +140,7 @@ def cpu_baseline(k, m, obj_len, erased, budget_s=12.0, sample_objs=512):
         t_total += CO.apply_batch(mat[k:], enc_in, enc_out, sample_objs, s, threads)
         t_total += CO.apply_batch(rows, rec_in, rec_out, sample_objs, s, threads)
         passes += 1
-        if passes >= 200:
+        if passes >= 20000:
             break
     assert np.array_equal(rebuilt, np.concatenate([objs[:, i * s:(i + 1) * s] for i in erased], axis=1))
     nbytes = passes * sample_objs * ((k + m) * s + (k + len(erased)) * s)
@@ -171,12 +181,20 @@ def main():
     args = ap.parse_args()
 
     world, rank, local = dist_env()
-    torch.cuda.set_device(local)
+    # one rank per GPU; HBEC_DIST_BACKEND=gloo lets several ranks share one
+    # GPU to rehearse the N>1 path on a 1-GPU box (control traffic only)
+    backend = os.environ.get("HBEC_DIST_BACKEND", "nccl")
+    dev = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev)
     pg = None
+    ctl_device = "cuda" if backend == "nccl" else "cpu"
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
         pg = dist
 
     k, m, obj_len, erased = 4, 2, MiB, (0, 1)
@@ -209,11 +227,8 @@ def main():
 
     enc_ms = sum(e0.elapsed_time(e1) for e0, e1, _ in ev) / args.steps
     rec_ms = sum(e1.elapsed_time(e2) for _, e1, e2 in ev) / args.steps
-    if pg:
-        t = torch.tensor([elapsed, enc_ms, rec_ms, 0.0 if ok else 1.0], dtype=torch.float64, device="cuda")
-        pg.all_reduce(t, op=pg.ReduceOp.MAX)
-        elapsed, enc_ms, rec_ms, bad = t.tolist()
-        ok = bad == 0.0
+    elapsed, enc_ms, rec_ms, bad = max_over_ranks(pg, [elapsed, enc_ms, rec_ms, 0.0 if ok else 1.0], ctl_device)
+    ok = bad == 0.0
 
     step_bytes = w.enc_bytes + w.rec_bytes
     total_bytes = step_bytes * args.steps * world

@@ -1,0 +1,129 @@
+#!/usr/bin/env python3
+"""Host-path (PCIe-inclusive) rates for DESIGN.md — not the headline metric.
+
+The reference path starts and ends in host memory (nursery file / HTTP body
+in, shard PUT bodies out: objectserver/ecobj.go:689-811, ecutils.go:26-72).
+Two measurements:
+
+ 1. pipelined batch: objects in pinned host memory -> H2D (k*S per object) ->
+    encode kernel -> D2H (m*S per object), chunked and double-buffered on three
+    HIP streams (copy-in / compute / copy-out), for 4+2 @ 1 MiB; same for a
+    reconstruct{0,1} (survivors in, 2 rebuilt shards out).
+ 2. per-call Encoder.Encode through the C ABI on pageable host buffers (what a
+    drop-in ecSplit call does per stripe), 1 MiB objects, sequential.
+
+Prints one JSON object per measurement.
+"""
+from __future__ import annotations
+
+import json
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+from hummingbird_amd import batch as B  # noqa: E402
+from hummingbird_amd import reedsolomon as RS  # noqa: E402
+
+MiB = 1 << 20
+GiB = float(1 << 30)
+
+
+def pipelined(op: str, n_obj=4096, chunk=256, reps=3):
+    k, m, S = 4, 2, MiB // 4
+    enc = RS.New(k, m)
+    n_in = 4 if op == "encode" else 4  # survivors read per object
+    n_out = 2
+    host_in = torch.empty((n_obj, n_in * S), dtype=torch.uint8).pin_memory()
+    host_out = torch.empty((n_obj, n_out * S), dtype=torch.uint8).pin_memory()
+    dev_objs = torch.empty((n_obj, k * S), dtype=torch.uint8, device="cuda")
+    B.fill_splitmix(dev_objs, k * S)
+    dev_par = torch.empty((n_obj, m * S), dtype=torch.uint8, device="cuda")
+    B.encode_objects(enc, dev_objs, dev_par, S)
+    torch.cuda.synchronize()
+    if op == "encode":
+        host_in.copy_(dev_objs.cpu())
+        want = dev_par.cpu()
+    else:  # survivors 2,3,P0,P1 -> rebuild 0,1
+        host_in.copy_(torch.cat([dev_objs[:, 2 * S:], dev_par], dim=1).cpu())
+        want = dev_objs[:, :2 * S].cpu()
+    del dev_objs, dev_par
+    d_in = [torch.empty((chunk, n_in * S), dtype=torch.uint8, device="cuda") for _ in range(2)]
+    d_out = [torch.empty((chunk, n_out * S), dtype=torch.uint8, device="cuda") for _ in range(2)]
+    s_in, s_cmp, s_out = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
+    present = [0, 0, 1, 1, 1, 1]
+
+    def run():
+        done_out = [None, None]
+        for c in range(n_obj // chunk):
+            b = c % 2
+            lo, hi = c * chunk, (c + 1) * chunk
+            with torch.cuda.stream(s_in):
+                if done_out[b] is not None:
+                    s_in.wait_event(done_out[b])  # buffer b's previous D2H has finished
+                d_in[b].copy_(host_in[lo:hi], non_blocking=True)
+                e_in = torch.cuda.Event()
+                e_in.record(s_in)
+            with torch.cuda.stream(s_cmp):
+                s_cmp.wait_event(e_in)
+                if op == "encode":
+                    views = B.shard_views(d_in[b], 4, S) + B.shard_views(d_out[b], 2, S)
+                    B.encode_views(enc, views, chunk, S, stream=s_cmp)
+                else:
+                    views = B.shard_views(d_out[b], 2, S) + B.shard_views(d_in[b], 4, S)
+                    B.reconstruct_views(enc, views, present, chunk, S, stream=s_cmp)
+                e_cmp = torch.cuda.Event()
+                e_cmp.record(s_cmp)
+            with torch.cuda.stream(s_out):
+                s_out.wait_event(e_cmp)
+                host_out[lo:hi].copy_(d_out[b], non_blocking=True)
+                e_out = torch.cuda.Event()
+                e_out.record(s_out)
+                done_out[b] = e_out
+        torch.cuda.synchronize()
+
+    run()
+    assert torch.equal(host_out, want), "host-path output differs"
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        run()
+        ts.append(time.perf_counter() - t0)
+    t = min(ts)
+    obj_bytes = n_obj * k * S
+    return {"measure": f"host_path_pipelined_{op}", "objects": n_obj, "chunk_objects": chunk,
+            "seconds": round(t, 4),
+            "object_data_GiB_s": round(obj_bytes / t / GiB, 2),
+            "algorithmic_GiB_s": round(n_obj * (n_in + n_out) * S / t / GiB, 2),
+            "pcie_GB_s_h2d_plus_d2h": round(n_obj * (n_in + n_out) * S / t / 1e9, 2),
+            "objects_per_s": round(n_obj / t, 1)}
+
+
+def per_call(n_calls=200):
+    k, m, S = 4, 2, MiB // 4
+    enc = RS.New(k, m)
+    rng = np.random.default_rng(0)
+    obj = rng.integers(0, 256, k * S, dtype=np.uint8)
+    shards = [obj[j * S:(j + 1) * S].copy() for j in range(k)] + [np.zeros(S, np.uint8) for _ in range(m)]
+    enc.Encode(shards)
+    t0 = time.perf_counter()
+    for _ in range(n_calls):
+        enc.Encode(shards)
+    t = time.perf_counter() - t0
+    return {"measure": "per_call_Encode_pageable_1MiB", "calls": n_calls, "us_per_call": round(t / n_calls * 1e6, 1),
+            "object_data_GiB_s": round(n_calls * k * S / t / GiB, 3)}
+
+
+def main():
+    torch.cuda.set_device(0)
+    for r in (pipelined("encode"), pipelined("reconstruct"), per_call()):
+        print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -284,6 +284,46 @@ def run_xor_sweep(reps=8):
             print(json.dumps(row), flush=True)
 
 
+def run_seq(reps=6):
+    """Encode-only and reconstruct-only back-to-back sequences (default lib)."""
+    import torch
+
+    from hummingbird_amd import batch as B
+    from hummingbird_amd import reedsolomon as RS
+
+    torch.cuda.set_device(0)
+    n, S = 4096, 1 << 18
+    enc = RS.New(4, 2)
+    objs = torch.empty((n, 4 * S), dtype=torch.uint8, device="cuda")
+    par = torch.empty((n, 2 * S), dtype=torch.uint8, device="cuda")
+    reb = torch.empty((n, 2 * S), dtype=torch.uint8, device="cuda")
+    B.fill_splitmix(objs, 4 * S)
+    ev = B.shard_views(objs, 4, S) + B.shard_views(par, 2, S)
+    rv = B.shard_views(reb, 2, S) + ev[2:]
+    pres = [0, 0, 1, 1, 1, 1]
+    # reconstruct of the PARITY shards only (inputs = 4 data shards, like encode, other decode rows)
+    rv_p = ev[:4] + B.shard_views(reb, 2, S)
+    seqs = {
+        "enc": lambda: B.encode_views(enc, ev, n, S),
+        "rec01": lambda: B.reconstruct_views(enc, rv, pres, n, S),
+        "rec45": lambda: B.reconstruct_views(enc, rv_p, [1, 1, 1, 1, 0, 0], n, S),
+    }
+    for rnd in range(3):
+        for name, fn in seqs.items():
+            evs = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
+            torch.cuda.synchronize()
+            evs[0].record()
+            for i in range(reps):
+                fn()
+                evs[i + 1].record()
+            torch.cuda.synchronize()
+            ts = [evs[i].elapsed_time(evs[i + 1]) for i in range(reps)]
+            print(json.dumps({"seq": name, "round": rnd, "ms": [round(t, 4) for t in ts],
+                              "med": round(statistics.median(ts[1:]), 4)}), flush=True)
+    torch.cuda.synchronize()
+    assert torch.equal(reb, par)  # rec45 regenerates the parity
+
+
 def build_probe():
     import subprocess
     OUTDIR.mkdir(exist_ok=True)
@@ -366,7 +406,7 @@ if __name__ == "__main__":
     import argparse
 
     ap = argparse.ArgumentParser()
-    ap.add_argument("cmd", choices=["build", "run", "probe", "build_probe", "layout", "copysweep", "xorsweep"])
+    ap.add_argument("cmd", choices=["build", "run", "probe", "build_probe", "layout", "copysweep", "xorsweep", "seq"])
     ap.add_argument("--variants", default=",".join(VARIANTS))
     ap.add_argument("--rounds", type=int, default=12)
     ap.add_argument("--objects", type=int, default=4096)
@@ -379,6 +419,8 @@ if __name__ == "__main__":
         build_probe()
     elif a.cmd == "probe":
         run_probe()
+    elif a.cmd == "seq":
+        run_seq()
     elif a.cmd == "xorsweep":
         run_xor_sweep()
     elif a.cmd == "copysweep":
