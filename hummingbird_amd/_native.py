@@ -32,6 +32,10 @@ class View(C.Structure):
     _fields_ = [("base", C.c_void_p), ("obj_stride", C.c_uint64)]
 
 
+class Stripe(C.Structure):
+    _fields_ = [("base", C.c_void_p), ("shard_len", C.c_uint64)]
+
+
 READ_FN = C.CFUNCTYPE(C.c_int64, C.c_void_p, C.POINTER(C.c_uint8), C.c_size_t)
 WRITE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint8), C.c_size_t)
 
@@ -57,6 +61,12 @@ _SIG = [
     ("hbec_apply_batch", C.c_int,
      [C.c_int, C.c_int, _U8P, C.POINTER(View), C.POINTER(View), C.c_uint64, C.c_uint64, _P]),
     ("hbec_fill_splitmix", C.c_int, [_P, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, _P]),
+    ("hbec_plan_stripes", C.c_int, [_P, C.POINTER(Stripe), C.c_uint64, C.POINTER(_P)]),
+    ("hbec_plan_free", None, [_P]),
+    ("hbec_plan_info", C.c_int,
+     [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_int), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    ("hbec_encode_plan", C.c_int, [_P, _P, _P]),
+    ("hbec_reconstruct_plan", C.c_int, [_P, _P, _U8P, C.c_int, _P]),
     ("hbec_set_force_stream", C.c_int, [C.c_int]),
     ("hbec_kernel_info", C.c_int,
      [C.c_int, C.c_int, C.c_uint64, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),

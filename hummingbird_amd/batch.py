@@ -87,6 +87,41 @@ def apply_views(rows: int, cols: int, coeffs, in_views, out_views, n_objects: in
                                    int(n_objects), int(shard_len), _stream_ptr(stream)))
 
 
+class StripePlan:
+    """A device-side plan over stripes of mixed shard lengths (hbec_plan_*).
+    `stripes` = [(device address, shard_len)], each stripe being k+m shards
+    back to back (ecSplit's databuf layout).  Buffers must outlive the plan's
+    queued work."""
+
+    def __init__(self, enc: Encoder, stripes):
+        self.enc = enc
+        arr = (N.Stripe * max(1, len(stripes)))()
+        for i, (b, s) in enumerate(stripes):
+            arr[i].base = b
+            arr[i].shard_len = s
+        self._h = C.c_void_p()
+        check(N.lib().hbec_plan_stripes(enc.handle, arr, len(stripes), C.byref(self._h)))
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h and N._lib is not None:
+            N._lib.hbec_plan_free(h)
+            self._h = None
+
+    def info(self):
+        nt, fb, sb = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        tb = C.c_int()
+        check(N.lib().hbec_plan_info(self._h, C.byref(nt), C.byref(tb), C.byref(fb), C.byref(sb)))
+        return {"n_tiles": nt.value, "tile_bytes": tb.value, "n_fallback": fb.value, "shard_bytes": sb.value}
+
+    def encode(self, stream=None):
+        check(N.lib().hbec_encode_plan(self.enc.handle, self._h, _stream_ptr(stream)))
+
+    def reconstruct(self, present, data_only=False, stream=None):
+        p = (C.c_uint8 * len(present))(*[1 if x else 0 for x in present])
+        check(N.lib().hbec_reconstruct_plan(self.enc.handle, self._h, p, int(data_only), _stream_ptr(stream)))
+
+
 KERNEL_KINDS = {0: "unrolled", 1: "pipelined", 2: "streaming"}
 
 

@@ -20,8 +20,8 @@ LIB = PKG / "libhbec.so"
 ROOT = PKG.parent
 INCLUDE = ROOT / "include"
 
-SOURCES = ["kernels.hip", "hbec.cpp", "ecutils.cpp"]
-HEADERS = ["kernels.h", "gf256.h", "internal.h"]
+SOURCES = ["kernels.hip", "stripes.hip", "hbec.cpp", "ecutils.cpp", "plan.cpp"]
+HEADERS = ["kernels.h", "gf256.h", "internal.h", "gf_device.h"]
 ARCH = os.environ.get("HBEC_OFFLOAD_ARCH", "gfx950")
 
 

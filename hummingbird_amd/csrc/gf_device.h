@@ -1,0 +1,166 @@
+// gf_device.h — device-side GF(2^8) building blocks shared by the gfx950
+// kernels (kernels.hip, stripes.hip): 16-B streaming loads/stores, the
+// v_perm_b32 field multiply (3-bit/3-bit/2-bit split of each byte) and the
+// v_bitop3 XOR3 folding.  See kernels.hip for the scheme.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kernels.h"
+
+namespace hbec {
+
+__device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
+    // v_perm_b32: byte i of result = byte sel.u8[i] of the 64-bit {hi, lo}
+    // (selector 0-3 -> lo, 4-7 -> hi).
+    return __builtin_amdgcn_perm(hi, lo, sel);
+}
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+#ifndef HBEC_NT_LOADS
+#define HBEC_NT_LOADS 1
+#endif
+#ifndef HBEC_NT_STORES
+#define HBEC_NT_STORES 1
+#endif
+
+__device__ __forceinline__ u32x4 ld16(const uint8_t* p) {
+#if HBEC_NT_LOADS
+    return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+#else
+    return *reinterpret_cast<const u32x4*>(p);
+#endif
+}
+
+__device__ __forceinline__ void st16(uint8_t* p, u32x4 v) {
+#if HBEC_NT_STORES
+    __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+#else
+    *reinterpret_cast<u32x4*>(p) = v;
+#endif
+}
+
+// Global-address-space (addrspace 1) views for addresses built from integers
+// (tile records): without them hipcc emits flat_* ops, which complete out of
+// order and force vmcnt(0)/lgkmcnt(0) waits.
+typedef __attribute__((address_space(1))) const u32x4 gu32x4_c;
+typedef __attribute__((address_space(1))) u32x4 gu32x4;
+
+__device__ __forceinline__ u32x4 ld16_addr(uint64_t addr) {
+#if HBEC_NT_LOADS
+    return __builtin_nontemporal_load(reinterpret_cast<gu32x4_c*>(addr));
+#else
+    return *reinterpret_cast<gu32x4_c*>(addr);
+#endif
+}
+
+__device__ __forceinline__ void st16_addr(uint64_t addr, u32x4 v) {
+#if HBEC_NT_STORES
+    __builtin_nontemporal_store(v, reinterpret_cast<gu32x4*>(addr));
+#else
+    *reinterpret_cast<gu32x4*>(addr) = v;
+#endif
+}
+
+struct Sel {
+    uint32_t s0, s1, s2;
+};
+
+__device__ __forceinline__ Sel selectors(uint32_t x) {
+    Sel s;
+    s.s0 = x & 0x07070707u;
+    s.s1 = (x >> 3) & 0x07070707u;
+    s.s2 = (x >> 6) & 0x03030303u;
+    return s;
+}
+
+#ifndef HBEC_XOR3
+#define HBEC_XOR3 1
+#endif
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // v_bitop3_b32: a ^ b ^ c
+}
+
+__device__ __forceinline__ uint32_t gf_mul_sel(const Sel& s, uint32_t t0, uint32_t t1, uint32_t t2,
+                                               uint32_t t3, uint32_t t4) {
+    return perm(t1, t0, s.s0) ^ perm(t3, t2, s.s1) ^ perm(t4, t4, s.s2);
+}
+
+#ifndef HBEC_VGPR_TABLES
+#define HBEC_VGPR_TABLES 1
+#endif
+
+// Coefficient tables of one pass.  v_perm_b32 may read only one SGPR (GFX9
+// constant-bus limit), so the low halves t[0] and t[2] are copied to VGPRs
+// once per kernel instead of by a v_mov before every perm.
+template <int K, int R>
+struct Tables {
+    uint32_t lo0[R][K];
+    uint32_t lo2[R][K];
+};
+
+__device__ __forceinline__ uint32_t to_vgpr(uint32_t x) {
+#if HBEC_VGPR_TABLES
+    uint32_t r;
+    asm("v_mov_b32 %0, %1" : "=v"(r) : "s"(x));
+    return r;
+#else
+    return x;
+#endif
+}
+
+typedef uint32_t TabArray[kMaxR][kMaxK][5];
+
+template <int K, int R>
+__device__ __forceinline__ Tables<K, R> load_tables(const TabArray& tab) {
+    Tables<K, R> t;
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            t.lo0[r][j] = to_vgpr(tab[r][j][0]);
+            t.lo2[r][j] = to_vgpr(tab[r][j][2]);
+        }
+    return t;
+}
+
+// acc[r] ^= XOR_j C[r][j] * x[j] for one 16-B column of K inputs.  The 3K
+// perm terms per (row, dword) are folded by v_bitop3 XOR3s; a pending odd
+// term is carried so every XOR3 retires two terms.
+template <int K, int R>
+__device__ __forceinline__ void gf_dot(u32x4 (&acc)[R], const u32x4 (&x)[K], const TabArray& tab,
+                                       const Tables<K, R>& tb) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        uint32_t pend[R];
+        bool has = false;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const Sel sx = selectors(x[j][e]);
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const uint32_t* t = tab[r][j];
+                const uint32_t p0 = perm(t[1], tb.lo0[r][j], sx.s0);
+                const uint32_t p1 = perm(t[3], tb.lo2[r][j], sx.s1);
+                const uint32_t p2 = perm(t[4], t[4], sx.s2);
+                if (!has) {
+                    acc[r][e] = xor3(acc[r][e], p0, p1);
+                    pend[r] = p2;
+                } else {
+                    acc[r][e] = xor3(acc[r][e], pend[r], p0);
+                    acc[r][e] = xor3(acc[r][e], p1, p2);
+                }
+            }
+            has = !has;
+        }
+        if (has) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) acc[r][e] ^= pend[r];
+        }
+    }
+}
+
+
+}  // namespace hbec

@@ -22,108 +22,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "gf_device.h"
 #include "kernels.h"
 
 namespace hbec {
-
-__device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
-    // v_perm_b32: byte i of result = byte sel.u8[i] of the 64-bit {hi, lo}
-    // (selector 0-3 -> lo, 4-7 -> hi).
-    return __builtin_amdgcn_perm(hi, lo, sel);
-}
-
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-#ifndef HBEC_NT_LOADS
-#define HBEC_NT_LOADS 1
-#endif
-#ifndef HBEC_NT_STORES
-#define HBEC_NT_STORES 1
-#endif
-
-__device__ __forceinline__ u32x4 ld16(const uint8_t* p) {
-#if HBEC_NT_LOADS
-    return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
-#else
-    return *reinterpret_cast<const u32x4*>(p);
-#endif
-}
-
-__device__ __forceinline__ void st16(uint8_t* p, u32x4 v) {
-#if HBEC_NT_STORES
-    __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
-#else
-    *reinterpret_cast<u32x4*>(p) = v;
-#endif
-}
-
-struct Sel {
-    uint32_t s0, s1, s2;
-};
-
-__device__ __forceinline__ Sel selectors(uint32_t x) {
-    Sel s;
-    s.s0 = x & 0x07070707u;
-    s.s1 = (x >> 3) & 0x07070707u;
-    s.s2 = (x >> 6) & 0x03030303u;
-    return s;
-}
-
-#ifndef HBEC_XOR3
-#define HBEC_XOR3 1
-#endif
-
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
-    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // v_bitop3_b32: a ^ b ^ c
-}
-
-// acc ^ c*x as 3 perms folded by two 3-input XORs.
-__device__ __forceinline__ uint32_t gf_fma_sel(uint32_t acc, const Sel& s, uint32_t t0, uint32_t t1, uint32_t t2,
-                                               uint32_t t3, uint32_t t4) {
-    const uint32_t p0 = perm(t1, t0, s.s0), p1 = perm(t3, t2, s.s1), p2 = perm(t4, t4, s.s2);
-    return xor3(xor3(acc, p0, p1), p2, 0u);
-}
-
-__device__ __forceinline__ uint32_t gf_mul_sel(const Sel& s, uint32_t t0, uint32_t t1, uint32_t t2,
-                                               uint32_t t3, uint32_t t4) {
-    return perm(t1, t0, s.s0) ^ perm(t3, t2, s.s1) ^ perm(t4, t4, s.s2);
-}
-
-#ifndef HBEC_VGPR_TABLES
-#define HBEC_VGPR_TABLES 1
-#endif
-
-// Coefficient tables of one pass.  v_perm_b32 may read only one SGPR (GFX9
-// constant-bus limit), so the low halves t[0] and t[2] are copied to VGPRs
-// once per kernel instead of by a v_mov before every perm.
-template <int K, int R>
-struct Tables {
-    uint32_t lo0[R][K];
-    uint32_t lo2[R][K];
-};
-
-__device__ __forceinline__ uint32_t to_vgpr(uint32_t x) {
-#if HBEC_VGPR_TABLES
-    uint32_t r;
-    asm("v_mov_b32 %0, %1" : "=v"(r) : "s"(x));
-    return r;
-#else
-    return x;
-#endif
-}
-
-template <int K, int R>
-__device__ __forceinline__ Tables<K, R> load_tables(const PassArgs& a) {
-    Tables<K, R> t;
-#pragma unroll
-    for (int r = 0; r < R; ++r)
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-            t.lo0[r][j] = to_vgpr(a.tab[r][j][0]);
-            t.lo2[r][j] = to_vgpr(a.tab[r][j][2]);
-        }
-    return t;
-}
 
 template <int K, int R, int U>
 __device__ __forceinline__ void process_tile(const PassArgs& a, const Tables<K, R>& tb, uint64_t obj,
@@ -155,35 +57,11 @@ __device__ __forceinline__ void process_tile(const PassArgs& a, const Tables<K, 
             if (accumulate && live) acc[r] = *reinterpret_cast<const u32x4*>(a.out[r] + obj * a.out_stride[r] + off);
         }
 #if HBEC_XOR3
-        // 3K perm terms per (row, dword) folded into acc by v_bitop3 XOR3s:
-        // a pending odd term is carried so every XOR3 retires two terms.
+        {
+            u32x4 xs[K];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            uint32_t pend[R];
-            bool has = false;
-#pragma unroll
-            for (int j = 0; j < K; ++j) {
-                const Sel sx = selectors(x[u][j][e]);
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    const uint32_t* t = a.tab[r][j];
-                    const uint32_t p0 = perm(t[1], tb.lo0[r][j], sx.s0);
-                    const uint32_t p1 = perm(t[3], tb.lo2[r][j], sx.s1);
-                    const uint32_t p2 = perm(t[4], t[4], sx.s2);
-                    if (!has) {
-                        acc[r][e] = xor3(acc[r][e], p0, p1);
-                        pend[r] = p2;
-                    } else {
-                        acc[r][e] = xor3(acc[r][e], pend[r], p0);
-                        acc[r][e] = xor3(acc[r][e], p1, p2);
-                    }
-                }
-                has = !has;
-            }
-            if (has) {
-#pragma unroll
-                for (int r = 0; r < R; ++r) acc[r][e] ^= pend[r];
-            }
+            for (int j = 0; j < K; ++j) xs[j] = x[u][j];
+            gf_dot<K, R>(acc, xs, a.tab, tb);
         }
 #else
 #pragma unroll
@@ -230,7 +108,7 @@ __global__ __launch_bounds__(kBlockThreads, kVecWavesPerSimd) void gf_apply_vec(
     const uint32_t nwaves = gridDim.x * (kBlockThreads / 64);
     const uint32_t tpo = a.tiles_per_obj;
     const bool accumulate = a.accumulate != 0;
-    const Tables<K, R> tb = load_tables<K, R>(a);
+    const Tables<K, R> tb = load_tables<K, R>(a.tab);
     for (uint32_t t = wave; t < a.n_tiles; t += nwaves) {
         const uint32_t obj = t / tpo;
         const uint32_t tile = t - obj * tpo;
@@ -248,7 +126,6 @@ __global__ __launch_bounds__(kBlockThreads, kVecWavesPerSimd) void gf_apply_vec(
 // loads in flight per CU, hbm_probe copy/xor sweeps), each wave keeping the
 // NEXT tile's loads in flight while it computes and stores the current one.
 // Tile = U x 1 KiB of each of the K inputs, U = 16 / K (K*U = 16 loads).
-__host__ __device__ constexpr int pipe_u(int k) { return k >= 16 ? 1 : (16 / k > 4 ? 4 : 16 / k); }
 
 // Branch-free tile load: lanes past the end of a partial tile read the last
 // 16 B of the shard instead (always in bounds); their results are never
@@ -267,46 +144,15 @@ __device__ __forceinline__ void load_tile(u32x4 (&x)[U][K], const PassArgs& a, u
 
 template <int K, int R, int U>
 __device__ __forceinline__ void compute_store_tile(const u32x4 (&x)[U][K], const PassArgs& a, const Tables<K, R>& tb,
-                                                   uint64_t obj, uint64_t off0, bool full, bool accumulate) {
+                                                   uint64_t obj, uint64_t off0, bool full) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const uint64_t off = off0 + (uint64_t)u * 1024u;
-        const bool live = full || off < a.shard_len;
         u32x4 acc[R];
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-            acc[r] = u32x4{0, 0, 0, 0};
-            if (accumulate && live) acc[r] = *reinterpret_cast<const u32x4*>(a.out[r] + obj * a.out_stride[r] + off);
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            uint32_t pend[R];
-            bool has = false;
-#pragma unroll
-            for (int j = 0; j < K; ++j) {
-                const Sel sx = selectors(x[u][j][e]);
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    const uint32_t* t = a.tab[r][j];
-                    const uint32_t p0 = perm(t[1], tb.lo0[r][j], sx.s0);
-                    const uint32_t p1 = perm(t[3], tb.lo2[r][j], sx.s1);
-                    const uint32_t p2 = perm(t[4], t[4], sx.s2);
-                    if (!has) {
-                        acc[r][e] = xor3(acc[r][e], p0, p1);
-                        pend[r] = p2;
-                    } else {
-                        acc[r][e] = xor3(acc[r][e], pend[r], p0);
-                        acc[r][e] = xor3(acc[r][e], p1, p2);
-                    }
-                }
-                has = !has;
-            }
-            if (has) {
-#pragma unroll
-                for (int r = 0; r < R; ++r) acc[r][e] ^= pend[r];
-            }
-        }
-        if (live) {
+        for (int r = 0; r < R; ++r) acc[r] = u32x4{0, 0, 0, 0};
+        gf_dot<K, R>(acc, x[u], a.tab, tb);
+        if (full || off < a.shard_len) {
 #pragma unroll
             for (int r = 0; r < R; ++r) st16(a.out[r] + obj * a.out_stride[r] + off, acc[r]);
         }
@@ -330,7 +176,7 @@ __global__ __launch_bounds__(kBlockThreads, HBEC_PIPE_WAVES_PER_SIMD) void gf_ap
         __builtin_amdgcn_readfirstlane(blockIdx.x * (kBlockThreads / 64) + (threadIdx.x >> 6));
     const uint32_t nwaves = gridDim.x * (kBlockThreads / 64);
     const uint32_t tpo = a.tiles_per_obj;
-    const Tables<K, R> tb = load_tables<K, R>(a);
+    const Tables<K, R> tb = load_tables<K, R>(a.tab);
     uint32_t t = wave;
     if (t >= a.n_tiles) return;
     u32x4 cur[U][K];
@@ -344,9 +190,9 @@ __global__ __launch_bounds__(kBlockThreads, HBEC_PIPE_WAVES_PER_SIMD) void gf_ap
         const uint64_t base_n = (uint64_t)(tn - obj_n * tpo) * TILE;
         load_tile<K, R, U>(nxt, a, obj_n, base_n + lane * 16u);
         if (base + TILE <= a.shard_len)
-            compute_store_tile<K, R, U>(cur, a, tb, obj, base + lane * 16u, true, false);
+            compute_store_tile<K, R, U>(cur, a, tb, obj, base + lane * 16u, true);
         else
-            compute_store_tile<K, R, U>(cur, a, tb, obj, base + lane * 16u, false, false);
+            compute_store_tile<K, R, U>(cur, a, tb, obj, base + lane * 16u, false);
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -355,9 +201,9 @@ __global__ __launch_bounds__(kBlockThreads, HBEC_PIPE_WAVES_PER_SIMD) void gf_ap
         base = base_n;
     }
     if (base + TILE <= a.shard_len)
-        compute_store_tile<K, R, U>(cur, a, tb, obj, base + lane * 16u, true, false);
+        compute_store_tile<K, R, U>(cur, a, tb, obj, base + lane * 16u, true);
     else
-        compute_store_tile<K, R, U>(cur, a, tb, obj, base + lane * 16u, false, false);
+        compute_store_tile<K, R, U>(cur, a, tb, obj, base + lane * 16u, false);
 }
 
 // Streaming vec path (runtime K): one input shard at a time with the next

@@ -1,0 +1,219 @@
+// plan.cpp — stripe plans: a batch of stripes of mixed shard lengths coded in
+// one launch (stripes.hip).  A stripe is ecSplit's databuf layout
+// (objectserver/ecutils.go:31-35,55-58): k+m shards of shard_len bytes back
+// to back, data first.  Stripes the tiled kernel cannot take (unaligned, or
+// shapes beyond K <= 8 inputs) go through the generic strided path one by one.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "../../include/hbec.h"
+#include "gf256.h"
+#include "internal.h"
+#include "kernels.h"
+
+using hbec::fail;
+using hbec::hip_fail;
+
+struct hbec_plan {
+    int k = 0, m = 0;
+    int tile_bytes = 0;
+    hbec::TileRec* d_tiles = nullptr;
+    uint64_t n_tiles = 0;
+    std::vector<hbec_stripe> tiled;     // stripes covered by d_tiles
+    std::vector<hbec_stripe> fallback;  // stripes coded one by one
+    uint64_t shard_bytes = 0;           // sum of shard_len over all stripes
+};
+
+namespace {
+
+bool aligned_stripe(const hbec_stripe& s) {
+    return (reinterpret_cast<uintptr_t>(s.base) & 15u) == 0 && (s.shard_len % 16) == 0 &&
+           s.shard_len < (1ull << 32);
+}
+
+std::mutex g_occ_mu;
+
+int stripes_grid(int k, int r, uint64_t n_tiles, int* grid) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+    static int cus[64] = {0};
+    static int occ[64][9][4] = {};
+    std::lock_guard<std::mutex> g(g_occ_mu);
+    if (dev < 0 || dev >= 64) return fail(HBEC_ERR_DEVICE, "device index out of range");
+    if (cus[dev] == 0) {
+        hipDeviceProp_t p;
+        e = hipGetDeviceProperties(&p, dev);
+        if (e != hipSuccess) return hip_fail(e, "hipGetDeviceProperties");
+        cus[dev] = p.multiProcessorCount;
+    }
+    if (occ[dev][k][r] == 0) {
+        int b = 0;
+        e = hbec::stripes_occupancy(k, r, &b);
+        if (e != hipSuccess) return hip_fail(e, "stripes occupancy");
+        occ[dev][k][r] = std::max(1, b);
+    }
+    const uint64_t want = (n_tiles + 3) / 4;  // 4 waves per block
+    const uint64_t cap = (uint64_t)cus[dev] * (uint64_t)occ[dev][k][r];
+    *grid = (int)std::max<uint64_t>(1, std::min(want, cap));
+    return HBEC_OK;
+}
+
+// Codes one stripe through the generic strided path (any alignment / shape).
+int apply_one(const hbec_stripe& s, int n_shards, const std::vector<int>& in_idx, const std::vector<int>& out_idx,
+              const uint8_t* rows, hipStream_t stream) {
+    std::vector<hbec_view> vin(in_idx.size()), vout(out_idx.size());
+    uint8_t* base = static_cast<uint8_t*>(s.base);
+    for (size_t j = 0; j < in_idx.size(); ++j) vin[j] = {base + (uint64_t)in_idx[j] * s.shard_len, 0};
+    for (size_t r = 0; r < out_idx.size(); ++r) vout[r] = {base + (uint64_t)out_idx[r] * s.shard_len, 0};
+    (void)n_shards;
+    return hbec::apply_views((int)out_idx.size(), (int)in_idx.size(), rows, vin.data(), vout.data(), 1, s.shard_len,
+                             stream);
+}
+
+// out rows (given as shard indices + coefficient rows over in_idx) for every stripe
+int run_plan(const hbec_plan* p, const std::vector<int>& in_idx, const std::vector<int>& out_idx,
+             const std::vector<uint8_t>& rows, hipStream_t stream) {
+    const int K = (int)in_idx.size();
+    const int R_all = (int)out_idx.size();
+    if (R_all == 0 || p->shard_bytes == 0) return HBEC_OK;
+    const bool tiled_ok = K <= 8 && hbec::stripes_supported(K, 1);
+    if (tiled_ok && p->n_tiles > 0) {
+        for (int r0 = 0; r0 < R_all; r0 += 3) {
+            const int R = std::min(3, R_all - r0);
+            hbec::StripeArgs a;
+            std::memset(&a, 0, sizeof(a));
+            a.tiles = p->d_tiles;
+            a.n_tiles = (uint32_t)p->n_tiles;
+            for (int j = 0; j < K; ++j) a.in_idx[j] = (uint32_t)in_idx[j];
+            for (int r = 0; r < R; ++r) {
+                a.out_idx[r] = (uint32_t)out_idx[r0 + r];
+                for (int j = 0; j < K; ++j) hbec::perm_table(rows[(size_t)(r0 + r) * K + j], a.tab[r][j]);
+            }
+            int grid = 0;
+            int rc = stripes_grid(K, R, p->n_tiles, &grid);
+            if (rc) return rc;
+            hipError_t e = hbec::launch_stripes(K, R, a, grid, stream);
+            if (e != hipSuccess) return hip_fail(e, "launch gf_apply_stripes");
+        }
+    }
+    const auto& singles = tiled_ok ? p->fallback : p->tiled;
+    for (const auto& s : singles) {
+        int rc = apply_one(s, p->k + p->m, in_idx, out_idx, rows.data(), stream);
+        if (rc) return rc;
+    }
+    if (!tiled_ok) {
+        for (const auto& s : p->fallback) {
+            int rc = apply_one(s, p->k + p->m, in_idx, out_idx, rows.data(), stream);
+            if (rc) return rc;
+        }
+    }
+    return HBEC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hbec_plan_stripes(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n, hbec_plan** out) {
+    if (!codec || !out || (n && !stripes)) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+    *out = nullptr;
+    const int k = hbec_data_shards(codec), m = hbec_parity_shards(codec);
+    std::unique_ptr<hbec_plan> p(new (std::nothrow) hbec_plan());
+    if (!p) return fail(HBEC_ERR_NOMEM, "plan allocation");
+    p->k = k;
+    p->m = m;
+    p->tile_bytes = hbec::stripes_tile_bytes(std::min(k, 8));
+    std::vector<hbec::TileRec> recs;
+    for (uint64_t i = 0; i < n; ++i) {
+        const hbec_stripe& s = stripes[i];
+        if (s.shard_len == 0) continue;
+        if (!s.base) return fail(HBEC_ERR_INVALID_ARG, "stripe with null base");
+        p->shard_bytes += s.shard_len;
+        if (!aligned_stripe(s)) {
+            p->fallback.push_back(s);
+            continue;
+        }
+        p->tiled.push_back(s);
+        for (uint64_t off = 0; off < s.shard_len; off += (uint64_t)p->tile_bytes) {
+            hbec::TileRec r;
+            r.addr = reinterpret_cast<uint64_t>(s.base) + off;
+            r.shard_len = (uint32_t)s.shard_len;
+            r.valid = (uint32_t)std::min<uint64_t>((uint64_t)p->tile_bytes, s.shard_len - off);
+            recs.push_back(r);
+        }
+    }
+    if (recs.size() >= (1ull << 31)) return fail(HBEC_ERR_INVALID_ARG, "plan too large (>= 2^31 tiles)");
+    p->n_tiles = recs.size();
+    if (!recs.empty()) {
+        hipError_t e = hipMalloc(&p->d_tiles, recs.size() * sizeof(hbec::TileRec));
+        if (e != hipSuccess) return hip_fail(e, "hipMalloc plan tiles");
+        e = hipMemcpy(p->d_tiles, recs.data(), recs.size() * sizeof(hbec::TileRec), hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            (void)hipFree(p->d_tiles);
+            p->d_tiles = nullptr;
+            return hip_fail(e, "hipMemcpy plan tiles");
+        }
+    }
+    *out = p.release();
+    return HBEC_OK;
+}
+
+void hbec_plan_free(hbec_plan* plan) {
+    if (!plan) return;
+    if (plan->d_tiles) (void)hipFree(plan->d_tiles);
+    delete plan;
+}
+
+int hbec_plan_info(const hbec_plan* plan, uint64_t* n_tiles, int* tile_bytes, uint64_t* n_fallback,
+                   uint64_t* shard_bytes) {
+    if (!plan) return fail(HBEC_ERR_INVALID_ARG, "null plan");
+    if (n_tiles) *n_tiles = plan->n_tiles;
+    if (tile_bytes) *tile_bytes = plan->tile_bytes;
+    if (n_fallback) *n_fallback = plan->fallback.size();
+    if (shard_bytes) *shard_bytes = plan->shard_bytes;
+    return HBEC_OK;
+}
+
+int hbec_encode_plan(hbec_codec* codec, const hbec_plan* plan, void* hip_stream) {
+    if (!codec || !plan) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+    const int k = hbec_data_shards(codec), m = hbec_parity_shards(codec);
+    if (k != plan->k || m != plan->m) return fail(HBEC_ERR_INVALID_ARG, "plan built for another (k, m)");
+    if (m == 0) return HBEC_OK;
+    std::vector<uint8_t> mat((size_t)(k + m) * k);
+    hbec_matrix(codec, mat.data());
+    std::vector<uint8_t> rows(mat.begin() + (size_t)k * k, mat.end());
+    std::vector<int> in_idx(k), out_idx(m);
+    for (int j = 0; j < k; ++j) in_idx[j] = j;
+    for (int r = 0; r < m; ++r) out_idx[r] = k + r;
+    return run_plan(plan, in_idx, out_idx, rows, static_cast<hipStream_t>(hip_stream));
+}
+
+int hbec_reconstruct_plan(hbec_codec* codec, const hbec_plan* plan, const uint8_t* present, int data_only,
+                          void* hip_stream) {
+    if (!codec || !plan || !present) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+    const int k = hbec_data_shards(codec), m = hbec_parity_shards(codec), n = k + m;
+    if (k != plan->k || m != plan->m) return fail(HBEC_ERR_INVALID_ARG, "plan built for another (k, m)");
+    int n_present = 0, data_present = 0;
+    for (int i = 0; i < n; ++i) {
+        n_present += present[i] ? 1 : 0;
+        if (i < k) data_present += present[i] ? 1 : 0;
+    }
+    if (n_present == n || (data_only && data_present == k)) return HBEC_OK;
+    if (n_present < k) return fail(HBEC_ERR_TOO_FEW_SHARDS, "too few shards given");
+    std::vector<int> surv(k), outs(n);
+    std::vector<uint8_t> rows((size_t)n * k);
+    int n_out = 0;
+    int rc = hbec_decode_rows(codec, present, data_only, surv.data(), outs.data(), &n_out, rows.data());
+    if (rc) return rc;
+    outs.resize(n_out);
+    rows.resize((size_t)n_out * k);
+    return run_plan(plan, surv, outs, rows, static_cast<hipStream_t>(hip_stream));
+}
+
+}  // extern "C"

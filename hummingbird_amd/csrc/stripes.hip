@@ -1,0 +1,143 @@
+// stripes.hip — one-launch GF(2^8) apply over a batch of stripes of MIXED
+// shard lengths (BASELINE config 4: 8+3 over 4 KiB and 1 MiB objects; and
+// the batching unit for many concurrent ecSplit stripes, ecutils.go:38-70).
+//
+// A stripe is ecSplit's databuf layout (ecutils.go:31-35,55-58): k+m shards of
+// shard_len bytes back to back at `base`, data first.  The host plan cuts
+// every stripe into tiles of TILE = pipe_u(k) KiB of shard column and writes
+// one 16-B record per tile: {address of the tile in shard 0, shard_len, valid
+// bytes}.  Shard i of the tile then starts at addr + i*shard_len.  Waves walk
+// the tile list grid-stride with the same pipeline as gf_apply_vec_pipe: the
+// NEXT tile's data loads and the tile record after that are in flight while
+// the current tile computes and stores.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gf_device.h"
+#include "kernels.h"
+
+namespace hbec {
+
+template <int K, int U>
+__device__ __forceinline__ void load_stripe_tile(u32x4 (&x)[U][K], const StripeArgs& a, const TileRec& t,
+                                                 uint32_t lane) {
+    const uint64_t last = (uint64_t)t.valid - 16u;  // valid >= 16, multiple of 16
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        uint64_t off = (uint64_t)lane * 16u + (uint64_t)u * 1024u;
+        off = off < last ? off : last;
+#pragma unroll
+        for (int j = 0; j < K; ++j) x[u][j] = ld16_addr(t.addr + (uint64_t)a.in_idx[j] * t.shard_len + off);
+    }
+}
+
+template <int K, int R, int U, bool FULL>
+__device__ __forceinline__ void store_stripe_tile_(const u32x4 (&x)[U][K], const StripeArgs& a,
+                                                   const Tables<K, R>& tb, const TileRec& t, uint32_t lane) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint64_t off = (uint64_t)lane * 16u + (uint64_t)u * 1024u;
+        u32x4 acc[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r] = u32x4{0, 0, 0, 0};
+        gf_dot<K, R>(acc, x[u], a.tab, tb);
+        if (FULL || off < t.valid) {
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                st16_addr(t.addr + (uint64_t)a.out_idx[r] * t.shard_len + off, acc[r]);
+        }
+    }
+}
+
+template <int K, int R, int U>
+__device__ __forceinline__ void store_stripe_tile(const u32x4 (&x)[U][K], const StripeArgs& a, const Tables<K, R>& tb,
+                                                  const TileRec& t, uint32_t lane) {
+    if (t.valid >= (uint32_t)U * 1024u)  // wave-uniform: whole tile live
+        store_stripe_tile_<K, R, U, true>(x, a, tb, t, lane);
+    else
+        store_stripe_tile_<K, R, U, false>(x, a, tb, t, lane);
+}
+
+// Tile records are read-only for the whole launch and passed as a separate
+// __restrict__ argument, so the wave-uniform loads below become scalar loads.
+__device__ __forceinline__ TileRec load_rec(const TileRec* __restrict__ recs, uint32_t i) {
+    return recs[i];
+}
+
+template <int K, int R>
+__global__ __launch_bounds__(kBlockThreads, 1) void gf_apply_stripes(StripeArgs a,
+                                                                     const TileRec* __restrict__ tiles) {
+    constexpr int U = pipe_u(K);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave =
+        __builtin_amdgcn_readfirstlane(blockIdx.x * (kBlockThreads / 64) + (threadIdx.x >> 6));
+    const uint32_t nw = gridDim.x * (kBlockThreads / 64);
+    const uint32_t n = a.n_tiles;
+    if (wave >= n) return;
+    const Tables<K, R> tb = load_tables<K, R>(a.tab);
+    TileRec cur = load_rec(tiles, wave);
+    u32x4 x[U][K];
+    load_stripe_tile<K, U>(x, a, cur, lane);
+    uint32_t tn = wave + nw;
+    TileRec nxt = load_rec(tiles, tn < n ? tn : wave);
+    for (; tn < n; tn += nw) {
+        u32x4 y[U][K];
+        load_stripe_tile<K, U>(y, a, nxt, lane);  // data one tile ahead
+        // record two tiles ahead, issued after the data loads: scalar loads
+        // return out of order, so waiting for `nxt` is an lgkmcnt(0)
+        const uint32_t t2 = tn + nw;
+        const TileRec after = load_rec(tiles, t2 < n ? t2 : tn);
+        store_stripe_tile<K, R, U>(x, a, tb, cur, lane);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int j = 0; j < K; ++j) x[u][j] = y[u][j];
+        cur = nxt;
+        nxt = after;
+    }
+    store_stripe_tile<K, R, U>(x, a, tb, cur, lane);
+}
+
+template <int K>
+static const void* stripes_for_r(int r) {
+    switch (r) {
+        case 1: return reinterpret_cast<const void*>(&gf_apply_stripes<K, 1>);
+        case 2: return reinterpret_cast<const void*>(&gf_apply_stripes<K, 2>);
+        case 3: return reinterpret_cast<const void*>(&gf_apply_stripes<K, 3>);
+    }
+    return nullptr;
+}
+
+static const void* stripes_kernel(int k, int r) {
+    switch (k) {
+        case 1: return stripes_for_r<1>(r);
+        case 2: return stripes_for_r<2>(r);
+        case 3: return stripes_for_r<3>(r);
+        case 4: return stripes_for_r<4>(r);
+        case 5: return stripes_for_r<5>(r);
+        case 6: return stripes_for_r<6>(r);
+        case 7: return stripes_for_r<7>(r);
+        case 8: return stripes_for_r<8>(r);
+    }
+    return nullptr;
+}
+
+int stripes_tile_bytes(int k) { return pipe_u(k) * 1024; }
+
+bool stripes_supported(int k, int r) { return stripes_kernel(k, r) != nullptr; }
+
+hipError_t launch_stripes(int k, int r, const StripeArgs& a, int grid, hipStream_t stream) {
+    const void* fn = stripes_kernel(k, r);
+    if (!fn) return hipErrorInvalidValue;
+    const TileRec* tiles = a.tiles;
+    void* args[] = {const_cast<StripeArgs*>(&a), &tiles};
+    return hipLaunchKernel(fn, dim3(grid), dim3(kBlockThreads), args, 0, stream);
+}
+
+hipError_t stripes_occupancy(int k, int r, int* blocks_per_cu) {
+    const void* fn = stripes_kernel(k, r);
+    if (!fn) return hipErrorInvalidValue;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, kBlockThreads, 0);
+}
+
+}  // namespace hbec

@@ -115,6 +115,31 @@ int hbec_apply_batch(int rows, int cols, const uint8_t* coeffs, const hbec_view*
 int hbec_fill_splitmix(void* dst, uint64_t n_objects, uint64_t obj_len, uint64_t obj_stride, uint64_t base_seed,
                        uint64_t first, void* hip_stream);
 
+/* ---------------------------------------------------------------------------
+ * Stripe plans: many stripes of MIXED shard lengths in one launch.  A stripe
+ * is ecSplit's databuf layout (ecutils.go:31-35,55-58): k+m shards of
+ * shard_len bytes back to back at base, data first.  The plan (built
+ * synchronously, device memory) records the stripes' addresses: the buffers
+ * must stay allocated while work queued with the plan runs.  Stripes whose
+ * base or shard_len is not 16-B aligned are coded one by one.
+ * ------------------------------------------------------------------------- */
+typedef struct {
+    void* base;
+    uint64_t shard_len;
+} hbec_stripe;
+
+typedef struct hbec_plan hbec_plan;
+
+int hbec_plan_stripes(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n_stripes, hbec_plan** out);
+void hbec_plan_free(hbec_plan* plan);
+int hbec_plan_info(const hbec_plan* plan, uint64_t* n_tiles, int* tile_bytes, uint64_t* n_fallback,
+                   uint64_t* shard_bytes);
+/* Encode every stripe of the plan (parity shards k..k+m-1 written). */
+int hbec_encode_plan(hbec_codec* codec, const hbec_plan* plan, void* hip_stream);
+/* Reconstruct every stripe with one erasure pattern (as hbec_reconstruct_batch). */
+int hbec_reconstruct_plan(hbec_codec* codec, const hbec_plan* plan, const uint8_t* present, int data_only,
+                          void* hip_stream);
+
 /* Tuning / introspection: force the runtime-K streaming kernel (0/1), and
  * report what a pass of k inputs -> r outputs over shard_len bytes launches:
  * tile bytes per wave, kind (0 = unrolled, 1 = pipelined, 2 = streaming) and

@@ -162,3 +162,16 @@ def test_header_has_c_linkage():
     text = (ROOT / "include" / "hbec.h").read_text()
     assert 'extern "C"' in text
     assert "torch" not in text.lower()
+
+
+def test_plan_build_needs_no_kernel_launch_for_empty():
+    # an empty plan allocates nothing on the device
+    enc = RS.New(4, 2)
+    import ctypes as C
+    h = C.c_void_p()
+    arr = (N.Stripe * 1)()
+    assert N.lib().hbec_plan_stripes(enc.handle, arr, 0, C.byref(h)) == 0
+    nt, fb, sb, tb = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_int()
+    assert N.lib().hbec_plan_info(h, C.byref(nt), C.byref(tb), C.byref(fb), C.byref(sb)) == 0
+    assert (nt.value, fb.value, sb.value, tb.value) == (0, 0, 0, 4096)
+    N.lib().hbec_plan_free(h)

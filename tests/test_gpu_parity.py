@@ -378,3 +378,90 @@ def test_batch_pipelined_partial_tiles(k, m, s, n):
     assert (got[:, m * s:] == 0x5A).all()  # nothing written past the last shard
     info = B.kernel_info(k, m, s)
     assert info["tile_bytes"] > 0
+
+
+# ------------------------------------------------------------------ stripe plans
+def _stripe_pool(k, m, sizes, align=16, misalign=()):
+    """Host pool of ecSplit databufs: stripe i = object i (k*S data bytes, zero
+    padded) followed by m*S parity bytes.  Returns (pool, [(offset, S)])."""
+    layout, off = [], 0
+    for i, size in enumerate(sizes):
+        s = O.ec_shard_length(size, k)
+        off = (off + align - 1) // align * align + (3 if i in misalign else 0)
+        layout.append((off, s, size))
+        off += (k + m) * s
+    pool = np.zeros(off + 64, dtype=np.uint8)
+    for i, (o, s, size) in enumerate(layout):
+        pool[o:o + size] = CO.fill_objects(1000 + i, 1, size)[0]
+    return pool, layout
+
+
+def _expected_pool(k, m, pool, layout):
+    want = pool.copy()
+    mat = CO.build_matrix(k, m)[k:]
+    for o, s, _ in layout:
+        data = [want[o + j * s:o + (j + 1) * s] for j in range(k)]
+        for r, p in enumerate(CO.apply(mat, data)):
+            want[o + (k + r) * s:o + (k + r + 1) * s] = p
+    return want
+
+
+@pytest.mark.parametrize("k,m,sizes,misalign", [
+    (8, 3, [4096, MiB, 4096, 4096, MiB, 4096, MiB, 4096] * 3, ()),
+    (4, 2, [MiB, 7, 4096, 1001, MiB + 16, 64, 4097], (1, 3)),
+    (10, 4, [4096, 40960, 160], ()),
+    (5, 5, [5 * 4096, 5 * 100000, 80], ()),
+])
+def test_plan_encode_reconstruct_mixed(k, m, sizes, misalign):
+    pool, layout = _stripe_pool(k, m, sizes, misalign=misalign)
+    want = _expected_pool(k, m, pool, layout)
+    dev = torch.from_numpy(pool).cuda()
+    enc = RS.New(k, m)
+    plan = B.StripePlan(enc, [(dev.data_ptr() + o, s) for o, s, _ in layout])
+    info = plan.info()
+    assert info["shard_bytes"] == sum(s for _, s, _ in layout)
+    plan.encode()
+    torch.cuda.synchronize()
+    assert np.array_equal(dev.cpu().numpy(), want)
+    # erase up to m shards of every stripe (data first), rebuild in place
+    for missing in [tuple(range(min(m, 3))), (0, k), (k - 1,), tuple(range(k, k + m))]:
+        damaged = torch.from_numpy(want.copy()).cuda()
+        for o, s, _ in layout:
+            for i in missing:
+                damaged[o + i * s:o + (i + 1) * s] = 0xEE
+        dplan = B.StripePlan(enc, [(damaged.data_ptr() + o, s) for o, s, _ in layout])
+        dplan.reconstruct([0 if i in missing else 1 for i in range(k + m)])
+        torch.cuda.synchronize()
+        assert np.array_equal(damaged.cpu().numpy(), want), missing
+
+
+def test_plan_config4_shape_counts():
+    """Config 4 plan: 8+3, 4 KiB and 1 MiB objects drawn p=0.5 by splitmix64."""
+    k, m = 8, 3
+    flags = O.splitmix_bytes(O.HBEC_SEED, 64)
+    sizes = [MiB if b & 1 else 4096 for b in flags]
+    pool, layout = _stripe_pool(k, m, sizes)
+    dev = torch.from_numpy(pool).cuda()
+    plan = B.StripePlan(RS.New(k, m), [(dev.data_ptr() + o, s) for o, s, _ in layout])
+    info = plan.info()
+    tile = info["tile_bytes"]
+    assert info["n_tiles"] == sum((s + tile - 1) // tile for _, s, _ in layout)
+    assert info["n_fallback"] == 0
+    plan.encode()
+    torch.cuda.synchronize()
+    assert np.array_equal(dev.cpu().numpy(), _expected_pool(k, m, pool, layout))
+
+
+def test_plan_empty_and_zero_length():
+    enc = RS.New(4, 2)
+    B.StripePlan(enc, []).encode()
+    B.StripePlan(enc, [(0x1000, 0)]).encode()
+    torch.cuda.synchronize()
+
+
+def test_plan_rejects_other_codec_shape():
+    buf = torch.zeros(6 * 4096, dtype=torch.uint8, device="cuda")
+    plan = B.StripePlan(RS.New(4, 2), [(buf.data_ptr(), 4096)])
+    with pytest.raises(RS.ErrInvalidArg):
+        N_plan_encode = __import__("hummingbird_amd._native", fromlist=["lib"]).lib().hbec_encode_plan
+        RS.check(N_plan_encode(RS.New(8, 3).handle, plan._h, None))
