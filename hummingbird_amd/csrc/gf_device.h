@@ -95,10 +95,15 @@ __device__ __forceinline__ uint32_t gf_mul_sel(const Sel& s, uint32_t t0, uint32
 // Coefficient tables of one pass.  v_perm_b32 may read only one SGPR (GFX9
 // constant-bus limit), so the low halves t[0] and t[2] are copied to VGPRs
 // once per kernel instead of by a v_mov before every perm.
+#ifndef HBEC_ALLVGPR_MIN
+#define HBEC_ALLVGPR_MIN 16  // K*R at or above which all 5 table words live in VGPRs (SGPR spills otherwise)
+#endif
+
 template <int K, int R>
 struct Tables {
     uint32_t lo0[R][K];
     uint32_t lo2[R][K];
+    uint32_t hi[K * R >= HBEC_ALLVGPR_MIN ? R : 1][K * R >= HBEC_ALLVGPR_MIN ? K : 1][3];
 };
 
 __device__ __forceinline__ uint32_t to_vgpr(uint32_t x) {
@@ -122,6 +127,11 @@ __device__ __forceinline__ Tables<K, R> load_tables(const TabArray& tab) {
         for (int j = 0; j < K; ++j) {
             t.lo0[r][j] = to_vgpr(tab[r][j][0]);
             t.lo2[r][j] = to_vgpr(tab[r][j][2]);
+            if constexpr (K * R >= HBEC_ALLVGPR_MIN) {
+                t.hi[r][j][0] = to_vgpr(tab[r][j][1]);
+                t.hi[r][j][1] = to_vgpr(tab[r][j][3]);
+                t.hi[r][j][2] = to_vgpr(tab[r][j][4]);
+            }
         }
     return t;
 }
@@ -141,10 +151,19 @@ __device__ __forceinline__ void gf_dot(u32x4 (&acc)[R], const u32x4 (&x)[K], con
             const Sel sx = selectors(x[j][e]);
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                const uint32_t* t = tab[r][j];
-                const uint32_t p0 = perm(t[1], tb.lo0[r][j], sx.s0);
-                const uint32_t p1 = perm(t[3], tb.lo2[r][j], sx.s1);
-                const uint32_t p2 = perm(t[4], t[4], sx.s2);
+                uint32_t h1, h3, h4;
+                if constexpr (K * R >= HBEC_ALLVGPR_MIN) {
+                    h1 = tb.hi[r][j][0];
+                    h3 = tb.hi[r][j][1];
+                    h4 = tb.hi[r][j][2];
+                } else {
+                    h1 = tab[r][j][1];
+                    h3 = tab[r][j][3];
+                    h4 = tab[r][j][4];
+                }
+                const uint32_t p0 = perm(h1, tb.lo0[r][j], sx.s0);
+                const uint32_t p1 = perm(h3, tb.lo2[r][j], sx.s1);
+                const uint32_t p2 = perm(h4, h4, sx.s2);
                 if (!has) {
                     acc[r][e] = xor3(acc[r][e], p0, p1);
                     pend[r] = p2;

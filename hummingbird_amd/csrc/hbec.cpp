@@ -146,7 +146,8 @@ int apply_views(int rows, int cols, const uint8_t* coeffs, const hbec_view* in, 
                     b.n_obj = no;
                     b.tiles_per_obj = (uint32_t)tpo;
                     b.n_tiles = (uint32_t)(no * tpo);
-                    const uint64_t want_blocks = (b.n_tiles + (kBlockThreads / 64) - 1) / (kBlockThreads / 64);
+                    const uint64_t wpb = (uint64_t)vec_block_threads(K, R, shard_len, c0 > 0, force_stream) / 64;
+                    const uint64_t want_blocks = (b.n_tiles + wpb - 1) / wpb;
                     const uint64_t cap = (uint64_t)cus * (uint64_t)(g_blocks_per_cu_override > 0
                                                                          ? g_blocks_per_cu_override
                                                                          : per_cu);

@@ -8,6 +8,15 @@ namespace hbec {
 constexpr int kMaxK = 16;         // inputs per kernel pass
 constexpr int kMaxR = 4;          // outputs per kernel pass
 constexpr int kBlockThreads = 256;
+#ifndef HBEC_PIPE_BLOCK
+#define HBEC_PIPE_BLOCK 256
+#endif
+#ifndef HBEC_PIPE_BLOCKS_PER_CU
+#define HBEC_PIPE_BLOCKS_PER_CU 1  // one 4-wave block per CU (0: occupancy limit)
+#endif
+constexpr int kPipeBlockThreads = HBEC_PIPE_BLOCK;  // pipelined kernel block size
+constexpr int kPipeBlocksPerCu = HBEC_PIPE_BLOCKS_PER_CU;
+
 #ifndef HBEC_WAVES_PER_SIMD
 #define HBEC_WAVES_PER_SIMD 4
 #endif
@@ -33,8 +42,21 @@ struct PassArgs {
 int vec_tile_bytes(int k, int r, uint64_t shard_len, int accumulate, int force_stream);
 int is_streaming_shape(int k, int r, int force_stream);
 int is_pipe_shape(int k, int r, uint64_t shard_len, int force_stream);
+// threads per block of the kernel a pass launches (pipelined vs the others)
+int vec_block_threads(int k, int r, uint64_t shard_len, int accumulate, int force_stream);
 // Pipelined kernels: U = 16/K KiB of each input per wave tile (K*U = 16 loads).
-__host__ __device__ constexpr int pipe_u(int k) { return k >= 16 ? 1 : (16 / k > 4 ? 4 : 16 / k); }
+// Tile depth of the pipelined kernels, U KiB of each input per wave tile,
+// from A/B sweeps on MI355X (profiles/r01_tune_*.jsonl): HBM streams best with
+// few outstanding requests per CU — 4+2 peaks at 1 KiB tiles (4 loads per
+// wave, 32 KiB in flight per CU), while 8+3 (more inputs per output byte)
+// peaks at 3 KiB tiles.  HBEC_PIPE_LOADS overrides with K*U ~= that value.
+#ifndef HBEC_PIPE_LOADS
+#define HBEC_PIPE_LOADS 0
+#endif
+__host__ __device__ constexpr int pipe_u(int k) {
+    if (HBEC_PIPE_LOADS > 0) return k >= HBEC_PIPE_LOADS ? 1 : (HBEC_PIPE_LOADS / k > 4 ? 4 : HBEC_PIPE_LOADS / k);
+    return k <= 4 ? (4 / k) : (k <= 8 ? 3 : 1);
+}
 
 hipError_t launch_vec(int k, int r, const PassArgs& a, int grid, hipStream_t stream, int force_stream);
 hipError_t launch_bytes(int k, int r, const PassArgs& a, int grid, hipStream_t stream);

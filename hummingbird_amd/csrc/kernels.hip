@@ -32,18 +32,25 @@ __device__ __forceinline__ void process_tile(const PassArgs& a, const Tables<K, 
                                              uint64_t off0, bool full, bool accumulate) {
     // Issue every load of the tile first (K x U x 16 B per lane in flight),
     // then retire one 1 KiB sub-tile at a time so only its accumulators and
-    // selectors are live.
+    // selectors are live.  Loads are branch-free: lanes past the shard end
+    // read its last 16 B (never stored), so no exec branch splits the loads.
     u32x4 x[U][K];
+    const uint64_t last = a.shard_len - 16u;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-        const uint64_t off = off0 + (uint64_t)u * 1024u;
+        uint64_t off = off0 + (uint64_t)u * 1024u;
+        if (!full) off = off < last ? off : last;
 #pragma unroll
-        for (int j = 0; j < K; ++j) {
-            if (full || off < a.shard_len) {
-                x[u][j] = ld16(a.in[j] + obj * a.in_stride[j] + off);
-            } else {
-                x[u][j] = u32x4{0, 0, 0, 0};
-            }
+        for (int j = 0; j < K; ++j) x[u][j] = ld16(a.in[j] + obj * a.in_stride[j] + off);
+    }
+    u32x4 old[U][R];
+    if (accumulate) {  // wave-uniform: read-modify-write passes (inputs beyond kMaxK)
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            uint64_t off = off0 + (uint64_t)u * 1024u;
+            if (!full) off = off < last ? off : last;
+#pragma unroll
+            for (int r = 0; r < R; ++r) old[u][r] = *reinterpret_cast<const u32x4*>(a.out[r] + obj * a.out_stride[r] + off);
         }
     }
 #pragma unroll
@@ -52,10 +59,7 @@ __device__ __forceinline__ void process_tile(const PassArgs& a, const Tables<K, 
         const bool live = full || off < a.shard_len;
         u32x4 acc[R];
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-            acc[r] = u32x4{0, 0, 0, 0};
-            if (accumulate && live) acc[r] = *reinterpret_cast<const u32x4*>(a.out[r] + obj * a.out_stride[r] + off);
-        }
+        for (int r = 0; r < R; ++r) acc[r] = accumulate ? old[u][r] : u32x4{0, 0, 0, 0};
 #if HBEC_XOR3
         {
             u32x4 xs[K];
@@ -167,14 +171,14 @@ __device__ __forceinline__ void compute_store_tile(const u32x4 (&x)[U][K], const
 #endif
 
 template <int K, int R>
-__global__ __launch_bounds__(kBlockThreads, HBEC_PIPE_WAVES_PER_SIMD) void gf_apply_vec_pipe(PassArgs a) {
+__global__ __launch_bounds__(kPipeBlockThreads, HBEC_PIPE_WAVES_PER_SIMD) void gf_apply_vec_pipe(PassArgs a) {
     // never launched with a.accumulate (launch_vec routes those to gf_apply_vec)
     constexpr int U = pipe_u(K);
     constexpr uint64_t TILE = (uint64_t)U * 1024u;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave =
-        __builtin_amdgcn_readfirstlane(blockIdx.x * (kBlockThreads / 64) + (threadIdx.x >> 6));
-    const uint32_t nwaves = gridDim.x * (kBlockThreads / 64);
+        __builtin_amdgcn_readfirstlane(blockIdx.x * (kPipeBlockThreads / 64) + (threadIdx.x >> 6));
+    const uint32_t nwaves = gridDim.x * (kPipeBlockThreads / 64);
     const uint32_t tpo = a.tiles_per_obj;
     const Tables<K, R> tb = load_tables<K, R>(a.tab);
     uint32_t t = wave;
@@ -402,6 +406,11 @@ int vec_tile_bytes(int k, int r, uint64_t shard_len, int accumulate, int force_s
     return 4 * 1024;
 }
 
+int vec_block_threads(int k, int r, uint64_t shard_len, int accumulate, int force_stream) {
+    return (!is_streaming_shape(k, r, force_stream) && use_pipe(k, shard_len, accumulate != 0)) ? kPipeBlockThreads
+                                                                                               : kBlockThreads;
+}
+
 hipError_t launch_vec(int k, int r, const PassArgs& a, int grid, hipStream_t stream, int force_stream) {
     // accumulate passes (inputs beyond kMaxK) need the output read-back, which
     // the pipelined kernel does not do: they take the plain unrolled kernel.
@@ -409,7 +418,7 @@ hipError_t launch_vec(int k, int r, const PassArgs& a, int grid, hipStream_t str
     const void* fn = force_stream ? nullptr : unrolled_kernel(k, r, pipe);
     if (fn) {
         void* args[] = {const_cast<PassArgs*>(&a)};
-        return hipLaunchKernel(fn, dim3(grid), dim3(kBlockThreads), args, 0, stream);
+        return hipLaunchKernel(fn, dim3(grid), dim3(pipe ? kPipeBlockThreads : kBlockThreads), args, 0, stream);
     }
     fn = stream_kernel(r);
     if (!fn || k < 1 || k > kMaxK) return hipErrorInvalidValue;
@@ -431,9 +440,14 @@ hipError_t launch_fill(uint8_t* dst, uint64_t n_obj, uint64_t obj_len, uint64_t 
 
 hipError_t vec_occupancy(int k, int r, int pipe, int force_stream, int* blocks_per_cu) {
     const void* fn = force_stream ? nullptr : unrolled_kernel(k, r, pipe != 0);
+    const bool is_pipe = fn && pipe;
     if (!fn) fn = stream_kernel(r);
     if (!fn) return hipErrorInvalidValue;
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, kBlockThreads, 0);
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn,
+                                                                is_pipe ? kPipeBlockThreads : kBlockThreads, 0);
+    if (e == hipSuccess && is_pipe && kPipeBlocksPerCu > 0 && *blocks_per_cu > kPipeBlocksPerCu)
+        *blocks_per_cu = kPipeBlocksPerCu;
+    return e;
 }
 
 }  // namespace hbec

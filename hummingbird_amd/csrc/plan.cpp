@@ -56,7 +56,9 @@ int stripes_grid(int k, int r, uint64_t n_tiles, int* grid) {
         int b = 0;
         e = hbec::stripes_occupancy(k, r, &b);
         if (e != hipSuccess) return hip_fail(e, "stripes occupancy");
-        occ[dev][k][r] = std::max(1, b);
+        b = std::max(1, b);
+        if (hbec::kPipeBlocksPerCu > 0) b = std::min(b, hbec::kPipeBlocksPerCu);  // same HBM sweet spot
+        occ[dev][k][r] = b;
     }
     const uint64_t want = (n_tiles + 3) / 4;  // 4 waves per block
     const uint64_t cap = (uint64_t)cus[dev] * (uint64_t)occ[dev][k][r];

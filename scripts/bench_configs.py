@@ -1,0 +1,130 @@
+#!/usr/bin/env python3
+"""BASELINE.json configs beyond the headline, device-resident, one MI355X.
+
+  config 2: 4+2 encode, 4096 x 1 MiB
+  config 3: 4+2 reconstruct, 4096 x 1 MiB, erasures {0,1} {0,4} {4,5} {2,3}
+  config 4: 8+3 encode + reconstruct{0,1,2}, 4096 objects of 4 KiB or 1 MiB
+            (p = 0.5 each, drawn by splitmix64(seed) per index; one launch per
+            op through a stripe plan)
+  extra   : 8+3 @ 1 MiB uniform (strided views)
+
+Algorithmic bytes per object: encode (k+m)*S, reconstruct (k+e)*S.
+Prints one JSON line per measurement (GiB/s, GB/s and fraction of 8 TB/s).
+"""
+from __future__ import annotations
+
+import json
+import statistics
+import sys
+from pathlib import Path
+
+import numpy as np
+import torch
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+from hummingbird_amd import batch as B  # noqa: E402
+from hummingbird_amd import reedsolomon as RS  # noqa: E402
+from oracle import coracle as CO  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+
+MiB = 1 << 20
+GiB = float(1 << 30)
+PEAK = 8000.0
+
+
+def timeit(fn, reps=10, warm=2):
+    for _ in range(warm):
+        fn()
+    ts = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    return statistics.median(ts)
+
+
+def line(name, nbytes, ms, **kw):
+    d = {"config": name, "ms": round(ms, 4), "algorithmic_bytes": nbytes,
+         "GiB_s": round(nbytes / (ms * 1e-3) / GiB, 1), "GB_s": round(nbytes / (ms * 1e-3) / 1e9, 1),
+         "frac_of_8TBs": round(nbytes / (ms * 1e-3) / 1e9 / PEAK, 4)}
+    d.update(kw)
+    print(json.dumps(d), flush=True)
+
+
+def uniform(k, m, n, size, patterns):
+    s = size // k
+    enc = RS.New(k, m)
+    objs = torch.empty((n, size), dtype=torch.uint8, device="cuda")
+    B.fill_splitmix(objs, size)
+    par = torch.empty((n, m * s), dtype=torch.uint8, device="cuda")
+    views = B.shard_views(objs, k, s) + B.shard_views(par, m, s)
+    ms = timeit(lambda: B.encode_views(enc, views, n, s))
+    line(f"{k}+{m} encode {n}x{size}", n * (k + m) * s, ms, kernel=B.kernel_info(k, m, s)["kind"])
+    idx = [0, n // 2, n - 1]
+    want, _ = CO.encode_batch(k, m, objs[idx].cpu().numpy(), threads=CO.cpu_threads())
+    assert np.array_equal(par[idx].cpu().numpy(), want)
+    for miss in patterns:
+        out = torch.empty((n, len(miss) * s), dtype=torch.uint8, device="cuda")
+        rv = list(views)
+        for slot, i in enumerate(miss):
+            rv[i] = (out.data_ptr() + slot * s, out.stride(0))
+        present = [0 if i in miss else 1 for i in range(k + m)]
+        ms = timeit(lambda: B.reconstruct_views(enc, rv, present, n, s))
+        torch.cuda.synchronize()
+        for slot, i in enumerate(miss):
+            src = objs[:, i * s:(i + 1) * s] if i < k else par[:, (i - k) * s:(i - k + 1) * s]
+            assert torch.equal(out[:, slot * s:(slot + 1) * s], src), miss
+        line(f"{k}+{m} reconstruct{set(miss)} {n}x{size}", n * (k + len(miss)) * s, ms)
+
+
+def mixed_8_3(n=4096):
+    k, m = 8, 3
+    flags = O.splitmix_bytes(O.HBEC_SEED, n)
+    sizes = [MiB if b & 1 else 4096 for b in flags]
+    layout, off = [], 0
+    for size in sizes:
+        s = size // k
+        layout.append((off, s))
+        off += (k + m) * s
+    pool = torch.empty(off, dtype=torch.uint8, device="cuda")
+    B.fill_splitmix(pool.view(1, -1), off)
+    enc = RS.New(k, m)
+    plan = B.StripePlan(enc, [(pool.data_ptr() + o, s) for o, s in layout])
+    enc_bytes = sum((k + m) * s for _, s in layout)
+    ms = timeit(plan.encode)
+    n_big = sum(1 for x in sizes if x == MiB)
+    line(f"8+3 encode mixed 4KiB/1MiB x{n} (plan)", enc_bytes, ms, n_1MiB=n_big, n_4KiB=n - n_big,
+         plan=plan.info())
+    host = pool.cpu().numpy()
+    mat = CO.build_matrix(k, m)[k:]
+    for i in [0, 1, 2, n - 1] + [j for j in range(n) if sizes[j] == 4096][:3]:
+        o, s = layout[i]
+        want = CO.apply(mat, [host[o + j * s:o + (j + 1) * s] for j in range(k)])
+        for r in range(m):
+            assert np.array_equal(host[o + (k + r) * s:o + (k + r + 1) * s], want[r])
+    ref = pool.clone()
+    miss = (0, 1, 2)
+    present = [0 if i in miss else 1 for i in range(k + m)]
+    ms = timeit(lambda: plan.reconstruct(present))
+    assert torch.equal(pool, ref)  # rebuilt in place == original
+    rec_bytes = sum((k + len(miss)) * s for _, s in layout)
+    line(f"8+3 reconstruct{{0,1,2}} mixed 4KiB/1MiB x{n} (plan)", rec_bytes, ms)
+    t_enc = timeit(plan.encode, reps=5)
+    t_rec = timeit(lambda: plan.reconstruct(present), reps=5)
+    line(f"8+3 encode+reconstruct mixed x{n} (config 4)", enc_bytes + rec_bytes, t_enc + t_rec)
+
+
+def main():
+    torch.cuda.set_device(0)
+    uniform(4, 2, 4096, MiB, [(0, 1), (0, 4), (4, 5), (2, 3)])
+    uniform(8, 3, 4096, MiB, [(0, 1, 2)])
+    mixed_8_3()
+
+
+if __name__ == "__main__":
+    main()

@@ -40,6 +40,7 @@ for s in "$@"; do
       (cd /tmp && step pmcwrite 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o run -- python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline) || exit $?
       ;;
     dist2) step dist2 600 env HBEC_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 10 --warmup 2 --objects 2048 ;;
+    configs) step configs 600 python scripts/bench_configs.py ;;
     host) step host 600 python scripts/bench_host.py ;;
     seq) step seq 600 python scripts/tune.py seq ;;
     xorsweep) step xorsweep 600 python scripts/tune.py xorsweep ;;

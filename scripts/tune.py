@@ -29,6 +29,29 @@ T2 = BASE + ["HBEC_TILE_MID=2"]
 T4 = BASE + ["HBEC_TILE_MID=4"]
 P = T1 + ["HBEC_USE_PIPE=1"]
 VARIANTS = {
+    "cur": ([], {}),
+    "cur_b1": ([], {"HBEC_BLOCKS_PER_CU": "1"}),
+    "pl8_b1": (["HBEC_PIPE_LOADS=8"], {"HBEC_BLOCKS_PER_CU": "1"}),
+    "pl4_b1": (["HBEC_PIPE_LOADS=4"], {"HBEC_BLOCKS_PER_CU": "1"}),
+    "pl16_b1": (["HBEC_PIPE_LOADS=16"], {"HBEC_BLOCKS_PER_CU": "1"}),
+    "pl24_b1": (["HBEC_PIPE_LOADS=24"], {"HBEC_BLOCKS_PER_CU": "1"}),
+    "pl32_b1": (["HBEC_PIPE_LOADS=32"], {"HBEC_BLOCKS_PER_CU": "1"}),
+    "pl24_b2": (["HBEC_PIPE_LOADS=24"], {"HBEC_BLOCKS_PER_CU": "2"}),
+    "pl4_t128_b1": (["HBEC_PIPE_LOADS=4", "HBEC_PIPE_BLOCK=128"], {"HBEC_BLOCKS_PER_CU": "1"}),
+    "pl4_t128_b2": (["HBEC_PIPE_LOADS=4", "HBEC_PIPE_BLOCK=128"], {"HBEC_BLOCKS_PER_CU": "2"}),
+    "pl4_t64_b2": (["HBEC_PIPE_LOADS=4", "HBEC_PIPE_BLOCK=64"], {"HBEC_BLOCKS_PER_CU": "2"}),
+    "pl4_t64_b3": (["HBEC_PIPE_LOADS=4", "HBEC_PIPE_BLOCK=64"], {"HBEC_BLOCKS_PER_CU": "3"}),
+    "pl4_t64_b4": (["HBEC_PIPE_LOADS=4", "HBEC_PIPE_BLOCK=64"], {"HBEC_BLOCKS_PER_CU": "4"}),
+    "pl4_t512_b1": (["HBEC_PIPE_LOADS=4", "HBEC_PIPE_BLOCK=512"], {"HBEC_BLOCKS_PER_CU": "1"}),
+    "pl12_b1": (["HBEC_PIPE_LOADS=12"], {"HBEC_BLOCKS_PER_CU": "1"}),
+    "pl8_b1_ldplain": (["HBEC_PIPE_LOADS=8", "HBEC_NT_LOADS=0"], {"HBEC_BLOCKS_PER_CU": "1"}),
+    "pl8_b2": (["HBEC_PIPE_LOADS=8"], {"HBEC_BLOCKS_PER_CU": "2"}),
+    "pl4_b2": (["HBEC_PIPE_LOADS=4"], {"HBEC_BLOCKS_PER_CU": "2"}),
+    "pl4_b4": (["HBEC_PIPE_LOADS=4"], {"HBEC_BLOCKS_PER_CU": "4"}),
+    "av16": (["HBEC_ALLVGPR_MIN=16"], {}),
+    "av16_pl8": (["HBEC_ALLVGPR_MIN=16", "HBEC_PIPE_LOADS=8"], {}),
+    "pl8": (["HBEC_PIPE_LOADS=8"], {}),
+    "av16_pl12": (["HBEC_ALLVGPR_MIN=16", "HBEC_PIPE_LOADS=12"], {}),
     "pipe": (P, {}),
     "pipe_b1": (P, {"HBEC_BLOCKS_PER_CU": "1"}),
     "pipe_b2": (P, {"HBEC_BLOCKS_PER_CU": "2"}),
@@ -75,24 +98,25 @@ def build(names):
         print("built", n, flush=True)
 
 
-def run(names, rounds, n_obj, launches):
+def run(names, rounds, n_obj, launches, k=4, m=2):
     import torch
 
     from hummingbird_amd import _native as N
 
     torch.cuda.set_device(0)
-    k, m, s = 4, 2, (1 << 20) // 4
+    s = (1 << 20) // k
+    e = min(m, 3)  # erased data shards 0..e-1
     libs = {}
     for n in names:
         _, env = VARIANTS[n]
-        old = {e: os.environ.get(e) for e in env}
+        old = {var: os.environ.get(var) for var in env}
         os.environ.update(env)
         h = C.CDLL(str(OUTDIR / n / "libhbec.so"))
-        for e, v in old.items():
+        for var, v in old.items():
             if v is None:
-                os.environ.pop(e, None)
+                os.environ.pop(var, None)
             else:
-                os.environ[e] = v
+                os.environ[var] = v
         for name, res, args in N._SIG:
             f = getattr(h, name)
             f.restype, f.argtypes = res, args
@@ -100,28 +124,28 @@ def run(names, rounds, n_obj, launches):
         assert h.hbec_new(k, m, C.byref(codec)) == 0
         libs[n] = (h, codec)
 
-    objs = torch.empty((n_obj, 4 * s), dtype=torch.uint8, device="cuda")
+    objs = torch.empty((n_obj, k * s), dtype=torch.uint8, device="cuda")
     h0 = libs[names[0]][0]
     stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
-    assert h0.hbec_fill_splitmix(C.c_void_p(objs.data_ptr()), n_obj, 4 * s, 4 * s, 0x48424543, 0, stream) == 0
-    shared_p = torch.zeros((n_obj, 2 * s), dtype=torch.uint8, device="cuda")
-    shared_r = torch.zeros((n_obj, 2 * s), dtype=torch.uint8, device="cuda")
+    assert h0.hbec_fill_splitmix(C.c_void_p(objs.data_ptr()), n_obj, k * s, k * s, 0x48424543, 0, stream) == 0
+    shared_p = torch.zeros((n_obj, m * s), dtype=torch.uint8, device="cuda")
+    shared_r = torch.zeros((n_obj, e * s), dtype=torch.uint8, device="cuda")
     parity = {n: shared_p for n in names}
     rebuilt = {n: shared_r for n in names}
     ok = {n: [True, True] for n in names}
     ref_p = None
 
     def views(n):
-        enc = [(objs.data_ptr() + j * s, 4 * s) for j in range(4)] + \
-              [(parity[n].data_ptr() + r * s, 2 * s) for r in range(2)]
+        enc = [(objs.data_ptr() + j * s, k * s) for j in range(k)] + \
+              [(parity[n].data_ptr() + r * s, m * s) for r in range(m)]
         rec = list(enc)
-        rec[0] = (rebuilt[n].data_ptr(), 2 * s)
-        rec[1] = (rebuilt[n].data_ptr() + s, 2 * s)
-        mk = lambda vs: (N.View * 6)(*[N.View(b, st) for b, st in vs])  # noqa: E731
+        for i in range(e):
+            rec[i] = (rebuilt[n].data_ptr() + i * s, e * s)
+        mk = lambda vs: (N.View * (k + m))(*[N.View(b, st) for b, st in vs])  # noqa: E731
         return mk(enc), mk(rec)
 
     vv = {n: views(n) for n in names}
-    present = (C.c_uint8 * 6)(0, 0, 1, 1, 1, 1)
+    present = (C.c_uint8 * (k + m))(*([0] * e + [1] * (k + m - e)))
     times = {n: {"enc": [], "rec": []} for n in names}
     for rnd in range(rounds):
         for n in names:
@@ -139,26 +163,27 @@ def run(names, rounds, n_obj, launches):
             if ref_p is None:
                 ref_p = shared_p.clone()
             if rnd == rounds - 1:
-                ok[n] = [bool(torch.equal(shared_p, ref_p)), bool(torch.equal(shared_r, objs[:, :2 * s]))]
+                ok[n] = [bool(torch.equal(shared_p, ref_p)), bool(torch.equal(shared_r, objs[:, :e * s]))]
                 shared_p.zero_()
                 shared_r.zero_()
             if rnd > 0:  # round 0 = warmup
                 for i in range(launches):
                     times[n]["enc"].append(evs[2 * i].elapsed_time(evs[2 * i + 1]))
                     times[n]["rec"].append(evs[2 * i + 1].elapsed_time(evs[2 * i + 2]))
-    bytes_per_launch = n_obj * 6 * s
+    bytes_per_launch = n_obj * (k + m) * s
+    rec_bytes = n_obj * (k + e) * s
     res = []
     for n in names:
         okp, okr = ok[n]
         h = libs[n][0]
         tb, st, bpc = C.c_int(), C.c_int(), C.c_int()
-        h.hbec_kernel_info(4, 2, s, C.byref(tb), C.byref(st), C.byref(bpc))
-        e = statistics.median(times[n]["enc"])
+        h.hbec_kernel_info(k, m, s, C.byref(tb), C.byref(st), C.byref(bpc))
+        e_ms = statistics.median(times[n]["enc"])
         r = statistics.median(times[n]["rec"])
-        row = {"variant": n, "enc_ms_med": round(e, 4), "rec_ms_med": round(r, 4),
+        row = {"variant": n, "k": k, "m": m, "enc_ms_med": round(e_ms, 4), "rec_ms_med": round(r, 4),
                "enc_ms_min": round(min(times[n]["enc"]), 4), "rec_ms_min": round(min(times[n]["rec"]), 4),
-               "enc_GBs": round(bytes_per_launch / e / 1e6, 1), "rec_GBs": round(bytes_per_launch / r / 1e6, 1),
-               "frac": round(2 * bytes_per_launch / (e + r) / 1e6 / 8000, 4), "parity_ok": okp, "rebuilt_ok": okr,
+               "enc_GBs": round(bytes_per_launch / e_ms / 1e6, 1), "rec_GBs": round(rec_bytes / r / 1e6, 1),
+               "frac": round((bytes_per_launch + rec_bytes) / (e_ms + r) / 1e6 / 8000, 4), "parity_ok": okp, "rebuilt_ok": okr,
                "tile": tb.value, "blocks_per_cu": bpc.value}
         res.append(row)
         print(json.dumps(row), flush=True)
@@ -411,6 +436,8 @@ if __name__ == "__main__":
     ap.add_argument("--rounds", type=int, default=12)
     ap.add_argument("--objects", type=int, default=4096)
     ap.add_argument("--launches", type=int, default=5)
+    ap.add_argument("--k", type=int, default=4)
+    ap.add_argument("--m", type=int, default=2)
     a = ap.parse_args()
     names = a.variants.split(",")
     if a.cmd == "build":
@@ -428,4 +455,4 @@ if __name__ == "__main__":
     elif a.cmd == "layout":
         run_layout()
     else:
-        run(names, a.rounds, a.objects, a.launches)
+        run(names, a.rounds, a.objects, a.launches, a.k, a.m)
