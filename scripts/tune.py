@@ -30,6 +30,7 @@ T4 = BASE + ["HBEC_TILE_MID=4"]
 P = T1 + ["HBEC_USE_PIPE=1"]
 VARIANTS = {
     "cur": ([], {}),
+    "prev": (["HBEC_PIPE_LOADS=16", "HBEC_PIPE_BLOCKS_PER_CU=0"], {}),
     "cur_b1": ([], {"HBEC_BLOCKS_PER_CU": "1"}),
     "pl8_b1": (["HBEC_PIPE_LOADS=8"], {"HBEC_BLOCKS_PER_CU": "1"}),
     "pl4_b1": (["HBEC_PIPE_LOADS=4"], {"HBEC_BLOCKS_PER_CU": "1"}),
