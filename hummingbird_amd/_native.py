@@ -67,6 +67,8 @@ _SIG = [
      [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_int), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     ("hbec_encode_plan", C.c_int, [_P, _P, _P]),
     ("hbec_reconstruct_plan", C.c_int, [_P, _P, _U8P, C.c_int, _P]),
+    ("hbec_encode_host", C.c_int, [_P, C.POINTER(Stripe), C.c_uint64]),
+    ("hbec_reconstruct_host", C.c_int, [_P, C.POINTER(Stripe), C.c_uint64, _U8P, C.c_int]),
     ("hbec_set_force_stream", C.c_int, [C.c_int]),
     ("hbec_kernel_info", C.c_int,
      [C.c_int, C.c_int, C.c_uint64, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),

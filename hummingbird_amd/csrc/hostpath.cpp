@@ -1,0 +1,418 @@
+// hostpath.cpp — streaming host path: code a batch of
+// HOST-resident stripes (ecSplit databuf layout, objectserver/ecutils.go:31-35,
+// 55-58) through a pinned staging ring.  Per chunk of stripes:
+//
+//   CPU gather (thread pool) caller memory -> pinned IN slot
+//   H2D IN slot -> device IN region            (copy stream)
+//   gf_apply_stripes over the chunk's tiles    (compute stream)
+//   D2H device OUT region -> pinned OUT slot   (copy-back stream)
+//   CPU scatter pinned OUT slot -> caller memory
+//
+// with three slots in flight, so the CPU copies of one chunk overlap the DMA
+// and kernel work of the others.  Stripes wider than a slot are cut into
+// column pieces.  Everything is synchronous for the caller: when the call
+// returns, parity (encode) or the rebuilt shards (reconstruct) are in the
+// caller's buffers.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <condition_variable>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "../../include/hbec.h"
+#include "gf256.h"
+#include "internal.h"
+#include "kernels.h"
+
+using hbec::fail;
+using hbec::hip_fail;
+
+namespace {
+
+// ---------------------------------------------------------------- thread pool
+class Pool {
+   public:
+    explicit Pool(int n) {
+        for (int i = 0; i < n; ++i) threads_.emplace_back([this] { loop(); });
+    }
+    ~Pool() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : threads_) t.join();
+    }
+    int size() const { return (int)threads_.size(); }
+    // run f(i) for i in [0, n) on the pool + calling thread; returns when done
+    void parallel_for(size_t n, const std::function<void(size_t)>& f) {
+        if (n == 0) return;
+        std::unique_lock<std::mutex> lk(mu_);
+        fn_ = &f;
+        next_ = 0;
+        total_ = n;
+        done_ = 0;
+        ++gen_;
+        lk.unlock();
+        cv_.notify_all();
+        work();
+        lk.lock();
+        done_cv_.wait(lk, [&] { return done_ == total_; });
+        fn_ = nullptr;
+    }
+
+   private:
+    void work() {
+        for (;;) {
+            size_t i;
+            const std::function<void(size_t)>* f;
+            {
+                std::lock_guard<std::mutex> g(mu_);
+                if (!fn_ || next_ >= total_) return;
+                i = next_++;
+                f = fn_;
+            }
+            (*f)(i);
+            {
+                std::lock_guard<std::mutex> g(mu_);
+                if (++done_ == total_) done_cv_.notify_all();
+            }
+        }
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_ || (gen_ != seen && fn_ && next_ < total_); });
+                if (stop_) return;
+                seen = gen_;
+            }
+            work();
+        }
+    }
+    std::vector<std::thread> threads_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_cv_;
+    const std::function<void(size_t)>* fn_ = nullptr;
+    size_t next_ = 0, total_ = 0, done_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
+// One column piece of one stripe: columns [col, col+len) of its K inputs / R outputs.
+struct Piece {
+    uint64_t stripe;
+    uint64_t col;
+    uint64_t len;   // bytes (<= shard_len - col)
+    uint64_t lpad;  // len rounded up to 16
+    uint64_t in_off, out_off;  // offsets of this piece in the slot's IN / OUT regions
+};
+
+constexpr int kSlots = 3;
+
+struct Ring {
+    int dev = -1;
+    size_t in_cap = 0, out_cap = 0, tile_cap = 0;
+    hipStream_t s_h2d = nullptr, s_cmp = nullptr, s_d2h = nullptr;
+    uint8_t* pin_in[kSlots] = {};
+    uint8_t* pin_out[kSlots] = {};
+    uint8_t* dev_in[kSlots] = {};
+    uint8_t* dev_out[kSlots] = {};
+    hbec::TileRec* pin_tiles[kSlots] = {};
+    hbec::TileRec* dev_tiles[kSlots] = {};
+    hipEvent_t ev_h2d[kSlots] = {}, ev_cmp[kSlots] = {}, ev_done[kSlots] = {};
+    std::unique_ptr<Pool> pool;
+
+    ~Ring() {
+        for (int i = 0; i < kSlots; ++i) {
+            if (pin_in[i]) (void)hipHostFree(pin_in[i]);
+            if (pin_out[i]) (void)hipHostFree(pin_out[i]);
+            if (pin_tiles[i]) (void)hipHostFree(pin_tiles[i]);
+            if (dev_in[i]) (void)hipFree(dev_in[i]);
+            if (dev_out[i]) (void)hipFree(dev_out[i]);
+            if (dev_tiles[i]) (void)hipFree(dev_tiles[i]);
+            if (ev_h2d[i]) (void)hipEventDestroy(ev_h2d[i]);
+            if (ev_cmp[i]) (void)hipEventDestroy(ev_cmp[i]);
+            if (ev_done[i]) (void)hipEventDestroy(ev_done[i]);
+        }
+        if (s_h2d) (void)hipStreamDestroy(s_h2d);
+        if (s_cmp) (void)hipStreamDestroy(s_cmp);
+        if (s_d2h) (void)hipStreamDestroy(s_d2h);
+    }
+};
+
+size_t env_size(const char* name, size_t dflt) {
+    const char* e = std::getenv(name);
+    if (!e) return dflt;
+    long long v = std::atoll(e);
+    return v > 0 ? (size_t)v : dflt;
+}
+
+int ring_init(Ring& r, int dev) {
+    r.dev = dev;
+    const size_t slot = env_size("HBEC_HOST_SLOT_MB", 64) << 20;  // IN bytes per slot
+    r.in_cap = slot;
+    r.out_cap = slot;  // outputs per piece <= inputs (R <= K) except tiny K: sized below per call
+    r.tile_cap = slot / 1024 + 1024;
+    hipError_t e;
+#define HB_CHECK(x, what)                       \
+    do {                                        \
+        e = (x);                                \
+        if (e != hipSuccess) return hip_fail(e, what); \
+    } while (0)
+    HB_CHECK(hipStreamCreateWithFlags(&r.s_h2d, hipStreamNonBlocking), "stream");
+    HB_CHECK(hipStreamCreateWithFlags(&r.s_cmp, hipStreamNonBlocking), "stream");
+    HB_CHECK(hipStreamCreateWithFlags(&r.s_d2h, hipStreamNonBlocking), "stream");
+    for (int i = 0; i < kSlots; ++i) {
+        HB_CHECK(hipHostMalloc(reinterpret_cast<void**>(&r.pin_in[i]), r.in_cap, hipHostMallocDefault), "pinned in");
+        HB_CHECK(hipHostMalloc(reinterpret_cast<void**>(&r.pin_out[i]), r.out_cap, hipHostMallocDefault),
+                 "pinned out");
+        HB_CHECK(hipHostMalloc(reinterpret_cast<void**>(&r.pin_tiles[i]), r.tile_cap * sizeof(hbec::TileRec),
+                               hipHostMallocDefault),
+                 "pinned tiles");
+        HB_CHECK(hipMalloc(&r.dev_in[i], r.in_cap), "device in");
+        HB_CHECK(hipMalloc(&r.dev_out[i], r.out_cap), "device out");
+        HB_CHECK(hipMalloc(&r.dev_tiles[i], r.tile_cap * sizeof(hbec::TileRec)), "device tiles");
+        HB_CHECK(hipEventCreateWithFlags(&r.ev_h2d[i], hipEventDisableTiming), "event");
+        HB_CHECK(hipEventCreateWithFlags(&r.ev_cmp[i], hipEventDisableTiming), "event");
+        HB_CHECK(hipEventCreateWithFlags(&r.ev_done[i], hipEventDisableTiming), "event");
+    }
+#undef HB_CHECK
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const size_t want = env_size("HBEC_HOST_THREADS", std::min<size_t>(8, hw));
+    r.pool.reset(new Pool((int)std::max<size_t>(0, want - 1)));  // + the calling thread
+    return HBEC_OK;
+}
+
+std::mutex g_rings_mu;
+std::vector<Ring*> g_free_rings;
+
+int ring_acquire(Ring** out) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+    {
+        std::lock_guard<std::mutex> g(g_rings_mu);
+        for (size_t i = 0; i < g_free_rings.size(); ++i)
+            if (g_free_rings[i]->dev == dev) {
+                *out = g_free_rings[i];
+                g_free_rings.erase(g_free_rings.begin() + i);
+                return HBEC_OK;
+            }
+    }
+    std::unique_ptr<Ring> r(new Ring());
+    int rc = ring_init(*r, dev);
+    if (rc) return rc;
+    *out = r.release();
+    return HBEC_OK;
+}
+
+void ring_release(Ring* r) {
+    std::lock_guard<std::mutex> g(g_rings_mu);
+    g_free_rings.push_back(r);
+}
+
+// Code every stripe: inputs = shards in_idx, outputs = shards out_idx with `rows`.
+int host_run(const hbec_stripe* stripes, uint64_t n, const std::vector<int>& in_idx,
+             const std::vector<int>& out_idx, const std::vector<uint8_t>& rows) {
+    const int K = (int)in_idx.size(), R = (int)out_idx.size();
+    if (R == 0 || n == 0) return HBEC_OK;
+    if (K > 8 || !hbec::stripes_supported(K, std::min(R, 3)))
+        return fail(HBEC_ERR_INVALID_ARG, "host path supports k <= 8");
+    Ring* ring = nullptr;
+    int rc = ring_acquire(&ring);
+    if (rc) return rc;
+    struct Releaser {
+        Ring* r;
+        ~Releaser() { ring_release(r); }
+    } rel{ring};
+    const uint64_t tile = (uint64_t)hbec::stripes_tile_bytes(K);
+    // max columns per piece so that K*lpad fits the IN slot and R*lpad the OUT slot
+    const uint64_t max_cols = (std::min(ring->in_cap / K, ring->out_cap / R) / 16) * 16;
+    if (max_cols < 16) return fail(HBEC_ERR_INVALID_ARG, "staging slot too small");
+
+    // Cut the batch into chunks of pieces that fit a slot.
+    std::vector<std::vector<Piece>> chunks(1);
+    uint64_t in_used = 0, out_used = 0, tiles_used = 0;
+    for (uint64_t s = 0; s < n; ++s) {
+        const uint64_t S = stripes[s].shard_len;
+        if (S == 0) continue;
+        if (!stripes[s].base) return fail(HBEC_ERR_INVALID_ARG, "stripe with null base");
+        for (uint64_t col = 0; col < S; col += max_cols) {
+            Piece p;
+            p.stripe = s;
+            p.col = col;
+            p.len = std::min(max_cols, S - col);
+            p.lpad = (p.len + 15) / 16 * 16;
+            const uint64_t nt = (p.lpad + tile - 1) / tile;
+            if (in_used + K * p.lpad > ring->in_cap || out_used + R * p.lpad > ring->out_cap ||
+                tiles_used + nt > ring->tile_cap) {
+                chunks.emplace_back();
+                in_used = out_used = tiles_used = 0;
+            }
+            p.in_off = in_used;
+            p.out_off = out_used;
+            in_used += K * p.lpad;
+            out_used += R * p.lpad;
+            tiles_used += nt;
+            chunks.back().push_back(p);
+        }
+    }
+    if (chunks.back().empty()) chunks.pop_back();
+
+    // kernel arguments per row group (<= 3 outputs per launch)
+    std::vector<hbec::StripeArgs> args;
+    for (int r0 = 0; r0 < R; r0 += 3) {
+        const int Rg = std::min(3, R - r0);
+        hbec::StripeArgs a;
+        std::memset(&a, 0, sizeof(a));
+        for (int j = 0; j < K; ++j) a.in_idx[j] = (uint32_t)j;  // inputs packed 0..K-1 in the slot
+        for (int r = 0; r < Rg; ++r) {
+            a.out_idx[r] = (uint32_t)(r0 + r);
+            for (int j = 0; j < K; ++j) hbec::perm_table(rows[(size_t)(r0 + r) * K + j], a.tab[r][j]);
+        }
+        a.pad_ = (uint32_t)Rg;  // carries the group's row count to the launch below
+        args.push_back(a);
+    }
+    int cus = 0;
+    {
+        hipDeviceProp_t prop;
+        hipError_t e = hipGetDeviceProperties(&prop, ring->dev);
+        if (e != hipSuccess) return hip_fail(e, "hipGetDeviceProperties");
+        cus = prop.multiProcessorCount;
+    }
+
+    std::vector<int64_t> slot_chunk(kSlots, -1);
+    auto scatter = [&](int slot) -> int {
+        const int64_t c = slot_chunk[slot];
+        if (c < 0) return HBEC_OK;
+        hipError_t e = hipEventSynchronize(ring->ev_done[slot]);
+        if (e != hipSuccess) return hip_fail(e, "hipEventSynchronize");
+        const auto& pieces = chunks[c];
+        ring->pool->parallel_for(pieces.size() * R, [&](size_t i) {
+            const Piece& p = pieces[i / R];
+            const int r = (int)(i % R);
+            const hbec_stripe& st = stripes[p.stripe];
+            std::memcpy(static_cast<uint8_t*>(st.base) + (uint64_t)out_idx[r] * st.shard_len + p.col,
+                        ring->pin_out[slot] + p.out_off + (uint64_t)r * p.lpad, p.len);
+        });
+        slot_chunk[slot] = -1;
+        return HBEC_OK;
+    };
+
+    for (size_t c = 0; c < chunks.size(); ++c) {
+        const int slot = (int)(c % kSlots);
+        rc = scatter(slot);  // the slot's previous chunk is complete; hand its output back
+        if (rc) return rc;
+        const auto& pieces = chunks[c];
+        // gather inputs into the pinned IN slot and build the tile records
+        ring->pool->parallel_for(pieces.size() * K, [&](size_t i) {
+            const Piece& p = pieces[i / K];
+            const int j = (int)(i % K);
+            const hbec_stripe& st = stripes[p.stripe];
+            uint8_t* dst = ring->pin_in[slot] + p.in_off + (uint64_t)j * p.lpad;
+            std::memcpy(dst, static_cast<const uint8_t*>(st.base) + (uint64_t)in_idx[j] * st.shard_len + p.col,
+                        p.len);
+            if (p.lpad > p.len) std::memset(dst + p.len, 0, p.lpad - p.len);
+        });
+        uint64_t nt = 0, in_bytes = 0, out_bytes = 0;
+        const uint64_t din = reinterpret_cast<uint64_t>(ring->dev_in[slot]);
+        const uint64_t dout = reinterpret_cast<uint64_t>(ring->dev_out[slot]);
+        for (const Piece& p : pieces) {
+            for (uint64_t off = 0; off < p.lpad; off += tile) {
+                hbec::TileRec& t = ring->pin_tiles[slot][nt++];
+                t.in_addr = din + p.in_off + off;
+                t.out_addr = dout + p.out_off + off;
+                t.in_stride = (uint32_t)p.lpad;
+                t.out_stride = (uint32_t)p.lpad;
+                t.valid = (uint32_t)std::min<uint64_t>(tile, p.lpad - off);
+                t.pad_ = 0;
+            }
+            in_bytes = std::max(in_bytes, p.in_off + K * p.lpad);
+            out_bytes = std::max(out_bytes, p.out_off + R * p.lpad);
+        }
+        hipError_t e;
+        e = hipMemcpyAsync(ring->dev_tiles[slot], ring->pin_tiles[slot], nt * sizeof(hbec::TileRec),
+                           hipMemcpyHostToDevice, ring->s_h2d);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(ring->dev_in[slot], ring->pin_in[slot], in_bytes, hipMemcpyHostToDevice, ring->s_h2d);
+        if (e == hipSuccess) e = hipEventRecord(ring->ev_h2d[slot], ring->s_h2d);
+        if (e == hipSuccess) e = hipStreamWaitEvent(ring->s_cmp, ring->ev_h2d[slot], 0);
+        if (e != hipSuccess) return hip_fail(e, "host path H2D");
+        for (auto a : args) {
+            const int Rg = (int)a.pad_;
+            a.pad_ = 0;
+            a.tiles = ring->dev_tiles[slot];
+            a.n_tiles = (uint32_t)nt;
+            int bpc = 1;
+            e = hbec::stripes_occupancy(K, Rg, &bpc);
+            if (e != hipSuccess) return hip_fail(e, "stripes occupancy");
+            if (hbec::kPipeBlocksPerCu > 0) bpc = std::min(bpc, hbec::kPipeBlocksPerCu);
+            const uint64_t want = (nt + 3) / 4;
+            const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cus * std::max(1, bpc)));
+            e = hbec::launch_stripes(K, Rg, a, grid, ring->s_cmp);
+            if (e != hipSuccess) return hip_fail(e, "launch gf_apply_stripes (host path)");
+        }
+        e = hipEventRecord(ring->ev_cmp[slot], ring->s_cmp);
+        if (e == hipSuccess) e = hipStreamWaitEvent(ring->s_d2h, ring->ev_cmp[slot], 0);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(ring->pin_out[slot], ring->dev_out[slot], out_bytes, hipMemcpyDeviceToHost,
+                               ring->s_d2h);
+        if (e == hipSuccess) e = hipEventRecord(ring->ev_done[slot], ring->s_d2h);
+        if (e != hipSuccess) return hip_fail(e, "host path D2H");
+        slot_chunk[slot] = (int64_t)c;
+    }
+    for (size_t i = 0; i < chunks.size() + kSlots; ++i) {  // drain in chunk order
+        const int slot = (int)(i % kSlots);
+        rc = scatter(slot);
+        if (rc) return rc;
+    }
+    return HBEC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hbec_encode_host(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n_stripes) {
+    if (!codec || (n_stripes && !stripes)) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+    const int k = hbec_data_shards(codec), m = hbec_parity_shards(codec);
+    if (m == 0) return HBEC_OK;
+    std::vector<uint8_t> mat((size_t)(k + m) * k);
+    hbec_matrix(codec, mat.data());
+    std::vector<uint8_t> rows(mat.begin() + (size_t)k * k, mat.end());
+    std::vector<int> in_idx(k), out_idx(m);
+    for (int j = 0; j < k; ++j) in_idx[j] = j;
+    for (int r = 0; r < m; ++r) out_idx[r] = k + r;
+    return host_run(stripes, n_stripes, in_idx, out_idx, rows);
+}
+
+int hbec_reconstruct_host(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n_stripes,
+                          const uint8_t* present, int data_only) {
+    if (!codec || !present || (n_stripes && !stripes)) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+    const int k = hbec_data_shards(codec), m = hbec_parity_shards(codec), n = k + m;
+    int n_present = 0, data_present = 0;
+    for (int i = 0; i < n; ++i) {
+        n_present += present[i] ? 1 : 0;
+        if (i < k) data_present += present[i] ? 1 : 0;
+    }
+    if (n_present == n || (data_only && data_present == k)) return HBEC_OK;
+    if (n_present < k) return fail(HBEC_ERR_TOO_FEW_SHARDS, "too few shards given");
+    std::vector<int> surv(k), outs(n);
+    std::vector<uint8_t> rows((size_t)n * k);
+    int n_out = 0;
+    int rc = hbec_decode_rows(codec, present, data_only, surv.data(), outs.data(), &n_out, rows.data());
+    if (rc) return rc;
+    outs.resize(n_out);
+    rows.resize((size_t)n_out * k);
+    return host_run(stripes, n_stripes, surv, outs, rows);
+}
+
+}  // extern "C"

@@ -65,12 +65,18 @@ hipError_t launch_fill(uint8_t* dst, uint64_t n_obj, uint64_t obj_len, uint64_t 
 hipError_t vec_occupancy(int k, int r, int pipe, int force_stream, int* blocks_per_cu);
 
 // ---- stripes (stripes.hip): mixed shard lengths in one launch ----
-// One record per tile: shard i of the tile starts at addr + i*shard_len;
-// lanes at offsets >= valid are masked on store.
+// One record per tile: input j of the tile starts at in_addr +
+// in_idx[j]*in_stride, output r at out_addr + out_idx[r]*out_stride; lanes at
+// offsets >= valid are masked on store.  In-place stripe plans use
+// in_addr == out_addr and stride == shard_len; the host-path ring keeps
+// inputs and outputs in separate device regions.
 struct TileRec {
-    uint64_t addr;
-    uint32_t shard_len;
+    uint64_t in_addr;
+    uint64_t out_addr;
+    uint32_t in_stride;
+    uint32_t out_stride;
     uint32_t valid;
+    uint32_t pad_;
 };
 
 struct StripeArgs {

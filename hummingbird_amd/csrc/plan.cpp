@@ -144,9 +144,10 @@ int hbec_plan_stripes(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n,
         p->tiled.push_back(s);
         for (uint64_t off = 0; off < s.shard_len; off += (uint64_t)p->tile_bytes) {
             hbec::TileRec r;
-            r.addr = reinterpret_cast<uint64_t>(s.base) + off;
-            r.shard_len = (uint32_t)s.shard_len;
+            r.in_addr = r.out_addr = reinterpret_cast<uint64_t>(s.base) + off;
+            r.in_stride = r.out_stride = (uint32_t)s.shard_len;
             r.valid = (uint32_t)std::min<uint64_t>((uint64_t)p->tile_bytes, s.shard_len - off);
+            r.pad_ = 0;
             recs.push_back(r);
         }
     }

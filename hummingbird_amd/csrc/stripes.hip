@@ -5,8 +5,9 @@
 // A stripe is ecSplit's databuf layout (ecutils.go:31-35,55-58): k+m shards of
 // shard_len bytes back to back at `base`, data first.  The host plan cuts
 // every stripe into tiles of TILE = pipe_u(k) KiB of shard column and writes
-// one 16-B record per tile: {address of the tile in shard 0, shard_len, valid
-// bytes}.  Shard i of the tile then starts at addr + i*shard_len.  Waves walk
+// one 32-B record per tile (kernels.h TileRec: input/output base, strides,
+// valid bytes).  For a stripe, shard i of the tile starts at addr +
+// i*shard_len.  Waves walk
 // the tile list grid-stride with the same pipeline as gf_apply_vec_pipe: the
 // NEXT tile's data loads and the tile record after that are in flight while
 // the current tile computes and stores.
@@ -27,7 +28,7 @@ __device__ __forceinline__ void load_stripe_tile(u32x4 (&x)[U][K], const StripeA
         uint64_t off = (uint64_t)lane * 16u + (uint64_t)u * 1024u;
         off = off < last ? off : last;
 #pragma unroll
-        for (int j = 0; j < K; ++j) x[u][j] = ld16_addr(t.addr + (uint64_t)a.in_idx[j] * t.shard_len + off);
+        for (int j = 0; j < K; ++j) x[u][j] = ld16_addr(t.in_addr + (uint64_t)a.in_idx[j] * t.in_stride + off);
     }
 }
 
@@ -44,7 +45,7 @@ __device__ __forceinline__ void store_stripe_tile_(const u32x4 (&x)[U][K], const
         if (FULL || off < t.valid) {
 #pragma unroll
             for (int r = 0; r < R; ++r)
-                st16_addr(t.addr + (uint64_t)a.out_idx[r] * t.shard_len + off, acc[r]);
+                st16_addr(t.out_addr + (uint64_t)a.out_idx[r] * t.out_stride + off, acc[r]);
         }
     }
 }

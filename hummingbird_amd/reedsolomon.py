@@ -153,6 +153,25 @@ class Encoder:
     def ReconstructData(self, shards) -> None:
         self._reconstruct(shards, 1)
 
+    # ---- streaming host path: many host stripes (ecSplit databuf layout) ----
+    def _stripes(self, stripes):
+        """stripes: list of 1-D uint8 arrays, each (k+m)*S bytes (data then parity)."""
+        arr = (N.Stripe * max(1, len(stripes)))()
+        for i, st in enumerate(stripes):
+            a = _as_array(st)
+            if a.size % self.Shards:
+                raise ValueError("stripe length must be a multiple of k+m")
+            arr[i].base = a.ctypes.data if a.size else None
+            arr[i].shard_len = a.size // self.Shards
+        return arr
+
+    def EncodeStripes(self, stripes) -> None:
+        check(N.lib().hbec_encode_host(self._h, self._stripes(stripes), len(stripes)))
+
+    def ReconstructStripes(self, stripes, present, data_only: bool = False) -> None:
+        p = (C.c_uint8 * self.Shards)(*[1 if x else 0 for x in present])
+        check(N.lib().hbec_reconstruct_host(self._h, self._stripes(stripes), len(stripes), p, int(data_only)))
+
     def DecodeRows(self, present, data_only: bool = False):
         """(survivors, outputs, rows) the reconstruct kernels apply."""
         n = self.Shards

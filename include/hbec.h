@@ -140,6 +140,15 @@ int hbec_encode_plan(hbec_codec* codec, const hbec_plan* plan, void* hip_stream)
 int hbec_reconstruct_plan(hbec_codec* codec, const hbec_plan* plan, const uint8_t* present, int data_only,
                           void* hip_stream);
 
+/* Host-memory batches (streaming host path): stripes in HOST memory (same
+ * ecSplit layout), coded through a pinned staging ring — CPU gather, H2D,
+ * kernel and D2H of successive chunks overlap on three streams.  Synchronous:
+ * on return the parity (encode) or the rebuilt shards (reconstruct) are in the
+ * caller's stripes.  k <= 8.  Env: HBEC_HOST_SLOT_MB (64), HBEC_HOST_THREADS. */
+int hbec_encode_host(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n_stripes);
+int hbec_reconstruct_host(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n_stripes, const uint8_t* present,
+                          int data_only);
+
 /* Tuning / introspection: force the runtime-K streaming kernel (0/1), and
  * report what a pass of k inputs -> r outputs over shard_len bytes launches:
  * tile bytes per wave, kind (0 = unrolled, 1 = pipelined, 2 = streaming) and

@@ -465,3 +465,56 @@ def test_plan_rejects_other_codec_shape():
     with pytest.raises(RS.ErrInvalidArg):
         N_plan_encode = __import__("hummingbird_amd._native", fromlist=["lib"]).lib().hbec_encode_plan
         RS.check(N_plan_encode(RS.New(8, 3).handle, plan._h, None))
+
+
+# ------------------------------------------------------------ streaming host path
+def _host_stripes(k, m, sizes, seed=0):
+    stripes = []
+    for i, size in enumerate(sizes):
+        s = O.ec_shard_length(size, k)
+        st = np.zeros((k + m) * s, dtype=np.uint8)
+        st[:size] = CO.fill_objects(seed + i, 1, size)[0]
+        stripes.append(st)
+    return stripes
+
+
+def _encoded_copy(k, m, stripes):
+    mat = CO.build_matrix(k, m)[k:]
+    out = []
+    for st in stripes:
+        s = st.size // (k + m)
+        w = st.copy()
+        for r, p in enumerate(CO.apply(mat, [w[j * s:(j + 1) * s] for j in range(k)])):
+            w[(k + r) * s:(k + r + 1) * s] = p
+        out.append(w)
+    return out
+
+
+@pytest.mark.parametrize("k,m,sizes", [
+    (4, 2, [MiB] * 70 + [7, 4096, 1001]),          # > one 64 MiB slot of 1 MiB objects
+    (8, 3, [4096, MiB, 4096, 3 * MiB + 8, 1]),
+    (4, 2, [68 * MiB]),                             # one stripe wider than a slot (column pieces)
+    (3, 5, [3000, 30000]),                          # more outputs than inputs, 2 row groups
+])
+def test_host_path_encode_reconstruct(k, m, sizes):
+    enc = RS.New(k, m)
+    stripes = _host_stripes(k, m, sizes, seed=len(sizes))
+    want = _encoded_copy(k, m, stripes)
+    enc.EncodeStripes(stripes)
+    for got, w in zip(stripes, want):
+        assert np.array_equal(got, w)
+    for missing in [tuple(range(min(m, 3))), (0, k)]:
+        damaged = [w.copy() for w in want]
+        for st in damaged:
+            s = st.size // (k + m)
+            for i in missing:
+                st[i * s:(i + 1) * s] = 0x33
+        enc.ReconstructStripes(damaged, [0 if i in missing else 1 for i in range(k + m)])
+        for got, w in zip(damaged, want):
+            assert np.array_equal(got, w), missing
+
+
+def test_host_path_rejects_wide_k():
+    enc = RS.New(10, 2)
+    with pytest.raises(RS.ErrInvalidArg):
+        enc.EncodeStripes(_host_stripes(10, 2, [1000]))
