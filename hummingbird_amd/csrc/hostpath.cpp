@@ -185,8 +185,11 @@ int ring_init(Ring& r, int dev) {
         HB_CHECK(hipEventCreateWithFlags(&r.ev_done[i], hipEventDisableTiming), "event");
     }
 #undef HB_CHECK
+    // gather/scatter threads: HBEC_HOST_THREADS, else the process's CPU share
+    // (OMP_NUM_THREADS, 16 per GPU on the MI355X boxes), capped by the hardware
     const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    const size_t want = env_size("HBEC_HOST_THREADS", std::min<size_t>(8, hw));
+    const size_t share = env_size("OMP_NUM_THREADS", 16);
+    const size_t want = std::min<size_t>(env_size("HBEC_HOST_THREADS", share), hw);
     r.pool.reset(new Pool((int)std::max<size_t>(0, want - 1)));  // + the calling thread
     return HBEC_OK;
 }
