@@ -60,6 +60,13 @@ def reconstruct_views(enc: Encoder, views, present, n_objects: int, shard_len: i
                                          _stream_ptr(stream)))
 
 
+def verify_views(enc: Encoder, views, n_objects: int, shard_len: int, flags, stream=None) -> None:
+    """Set flags[o] = 1 (uint32 CUDA tensor, caller-zeroed) for objects whose parity is wrong."""
+    v = _views(views)
+    check(N.lib().hbec_verify_batch(enc.handle, v, int(n_objects), int(shard_len), C.c_void_p(flags.data_ptr()),
+                                    _stream_ptr(stream)))
+
+
 def encode_objects(enc: Encoder, objs, parity, shard_len: int, stream=None) -> None:
     """Encode every row of ``objs`` [n, k*S] into ``parity`` [n, m*S]."""
     n = objs.shape[0]

@@ -496,6 +496,137 @@ int hbec_fill_splitmix(void* dst, uint64_t n_objects, uint64_t obj_len, uint64_t
     return HBEC_OK;
 }
 
+// ---- Encoder.Verify ------------------------------------------------------
+static int verify_views(hbec_codec* c, const hbec_view* views, uint64_t n_obj, uint64_t shard_len, uint32_t* flags,
+                        hipStream_t stream) {
+    const int k = c->k, m = c->m;
+    if (m == 0 || n_obj == 0 || shard_len == 0) return HBEC_OK;
+    bool vec = (shard_len % 16) == 0;
+    for (int i = 0; i < k + m && vec; ++i) vec = aligned16(views[i].base) && (views[i].obj_stride % 16) == 0;
+    const uint8_t* prow = c->matrix.data() + (size_t)k * k;
+    if (vec && verify_supported(k, m)) {
+        PassArgs a;
+        std::memset(&a, 0, sizeof(a));
+        for (int j = 0; j < k; ++j) {
+            a.in[j] = static_cast<const uint8_t*>(views[j].base);
+            a.in_stride[j] = views[j].obj_stride;
+        }
+        for (int r = 0; r < m; ++r) {
+            a.out[r] = static_cast<uint8_t*>(views[k + r].base);
+            a.out_stride[r] = views[k + r].obj_stride;
+            for (int j = 0; j < k; ++j) perm_table(prow[(size_t)r * k + j], a.tab[r][j]);
+        }
+        a.shard_len = shard_len;
+        const uint64_t tile = (uint64_t)verify_tile_bytes(k);
+        const uint64_t tpo = (shard_len + tile - 1) / tile;
+        int dev = 0, cus = 0, bpc = 1;
+        int rc = current_device(&dev);
+        if (rc) return rc;
+        {
+            hipDeviceProp_t p;
+            hipError_t e = hipGetDeviceProperties(&p, dev);
+            if (e != hipSuccess) return hip_fail(e, "hipGetDeviceProperties");
+            cus = p.multiProcessorCount;
+            e = verify_occupancy(k, m, &bpc);
+            if (e != hipSuccess) return hip_fail(e, "verify occupancy");
+            bpc = std::max(1, kPipeBlocksPerCu > 0 ? std::min(bpc, kPipeBlocksPerCu) : bpc);
+        }
+        const uint64_t max_obj = std::max<uint64_t>(1, (1ull << 31) / tpo);
+        for (uint64_t o0 = 0; o0 < n_obj; o0 += max_obj) {
+            const uint64_t no = std::min(max_obj, n_obj - o0);
+            PassArgs b = a;
+            for (int j = 0; j < k; ++j) b.in[j] = a.in[j] + o0 * a.in_stride[j];
+            for (int r = 0; r < m; ++r) b.out[r] = a.out[r] + o0 * a.out_stride[r];
+            b.n_obj = no;
+            b.tiles_per_obj = (uint32_t)tpo;
+            b.n_tiles = (uint32_t)(no * tpo);
+            const uint64_t want = (b.n_tiles + 3) / 4;
+            const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cus * bpc));
+            hipError_t e = launch_verify(k, m, b, flags + o0, grid, stream);
+            if (e != hipSuccess) return hip_fail(e, "launch gf_verify_pipe");
+        }
+        return HBEC_OK;
+    }
+    // generic: recompute parity into scratch, then compare bytewise
+    uint8_t* scratch = nullptr;
+    const size_t bytes = (size_t)n_obj * m * shard_len;
+    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&scratch), bytes, stream);
+    if (e != hipSuccess) return hip_fail(e, "hipMallocAsync verify scratch");
+    std::vector<hbec_view> out(m);
+    for (int r = 0; r < m; ++r) out[r] = {scratch + (size_t)r * shard_len, (uint64_t)m * shard_len};
+    int rc = apply_views(m, k, prow, views, out.data(), n_obj, shard_len, stream);
+    for (int r0 = 0; r0 < m && rc == HBEC_OK; r0 += kMaxR) {
+        const int R = std::min(kMaxR, m - r0);
+        PassArgs a;
+        std::memset(&a, 0, sizeof(a));
+        for (int r = 0; r < R; ++r) {
+            a.in[r] = static_cast<const uint8_t*>(out[r0 + r].base);
+            a.in_stride[r] = out[r0 + r].obj_stride;
+            a.out[r] = static_cast<uint8_t*>(views[k + r0 + r].base);
+            a.out_stride[r] = views[k + r0 + r].obj_stride;
+        }
+        a.shard_len = shard_len;
+        a.n_obj = n_obj;
+        const uint64_t want = (shard_len * n_obj + kBlockThreads - 1) / kBlockThreads;
+        const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, 16384));
+        e = launch_compare(R, a, flags, grid, stream);
+        if (e != hipSuccess) rc = hip_fail(e, "launch compare_views");
+    }
+    hipError_t e2 = hipFreeAsync(scratch, stream);
+    if (rc) return rc;
+    if (e2 != hipSuccess) return hip_fail(e2, "hipFreeAsync verify scratch");
+    return HBEC_OK;
+}
+
+int hbec_verify_batch(hbec_codec* c, const hbec_view* views, uint64_t n_objects, uint64_t shard_len,
+                      uint32_t* d_flags, void* hip_stream) {
+    if (!c || !views || (!d_flags && n_objects)) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+    return verify_views(c, views, n_objects, shard_len, d_flags, static_cast<hipStream_t>(hip_stream));
+}
+
+int hbec_verify(hbec_codec* c, uint8_t* const* shards, const size_t* lens, int n_shards, int* ok) {
+    if (!c || !shards || !lens || !ok) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+    *ok = 0;
+    if (n_shards != c->k + c->m) return fail(HBEC_ERR_TOO_FEW_SHARDS, "too few shards given");
+    size_t s = 0;
+    int rc = check_shards(lens, n_shards, false, &s);
+    if (rc) return rc;
+    if (c->m == 0) {
+        *ok = 1;
+        return HBEC_OK;
+    }
+    const uint64_t pad = round16(s);
+    const int n = c->k + c->m;
+    Staging* st = nullptr;
+    rc = staging_acquire((size_t)pad * n + 16, &st);
+    if (rc) return rc;
+    std::vector<hbec_view> v(n);
+    hipError_t e = hipSuccess;
+    for (int i = 0; i < n && e == hipSuccess; ++i) {
+        v[i] = {st->dbuf + (size_t)i * pad, 0};
+        e = hipMemcpyAsync(v[i].base, shards[i], s, hipMemcpyHostToDevice, st->stream);
+        // padding bytes must compare equal: zero both sides' tails
+        if (e == hipSuccess && pad > s)
+            e = hipMemsetAsync(static_cast<uint8_t*>(v[i].base) + s, 0, pad - s, st->stream);
+    }
+    uint32_t* d_flag = reinterpret_cast<uint32_t*>(st->dbuf + (size_t)pad * n);
+    if (e == hipSuccess) e = hipMemsetAsync(d_flag, 0, sizeof(uint32_t), st->stream);
+    if (e != hipSuccess) {
+        staging_release(st);
+        return hip_fail(e, "verify staging");
+    }
+    rc = verify_views(c, v.data(), 1, pad, d_flag, st->stream);
+    uint32_t h_flag = 1;
+    if (rc == HBEC_OK) e = hipMemcpyAsync(&h_flag, d_flag, sizeof(h_flag), hipMemcpyDeviceToHost, st->stream);
+    hipError_t e2 = hipStreamSynchronize(st->stream);
+    staging_release(st);
+    if (rc) return rc;
+    if (e != hipSuccess) return hip_fail(e, "verify D2H");
+    if (e2 != hipSuccess) return hip_fail(e2, "hipStreamSynchronize");
+    *ok = h_flag == 0 ? 1 : 0;
+    return HBEC_OK;
+}
+
 int hbec_set_force_stream(int on) {
     g_force_stream.store(on ? 1 : 0);
     return HBEC_OK;

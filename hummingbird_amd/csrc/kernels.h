@@ -93,4 +93,11 @@ bool stripes_supported(int k, int r);
 hipError_t launch_stripes(int k, int r, const StripeArgs& a, int grid, hipStream_t stream);
 hipError_t stripes_occupancy(int k, int r, int* blocks_per_cu);
 
+// ---- verify (verify.hip): recompute parity, compare, flag mismatching objects ----
+int verify_tile_bytes(int k);
+bool verify_supported(int k, int r);
+hipError_t launch_verify(int k, int r, const PassArgs& a, uint32_t* flags, int grid, hipStream_t stream);
+hipError_t verify_occupancy(int k, int r, int* blocks_per_cu);
+hipError_t launch_compare(int r, const PassArgs& a, uint32_t* flags, int grid, hipStream_t stream);
+
 }  // namespace hbec

@@ -130,6 +130,14 @@ class Encoder:
         ptrs, lens = self._ptrs(arrs)
         check(N.lib().hbec_encode(self._h, ptrs, lens, len(arrs)))
 
+    def Verify(self, shards) -> bool:
+        """Encoder.Verify: True when the parity shards match the data."""
+        arrs = [_as_array(s) for s in shards]
+        ptrs, lens = self._ptrs(arrs)
+        ok = C.c_int()
+        check(N.lib().hbec_verify(self._h, ptrs, lens, len(arrs), C.byref(ok)))
+        return bool(ok.value)
+
     def _reconstruct(self, shards, data_only: int) -> None:
         arrs = [_as_array(s) for s in shards]
         size = next((a.size for a in arrs if a.size), 0)

@@ -80,6 +80,11 @@ int hbec_encode(hbec_codec* codec, uint8_t* const* shards, const size_t* lens, i
  * share one length S.  On success lens[i] = S for every shard filled in. */
 int hbec_reconstruct(hbec_codec* codec, uint8_t* const* shards, size_t* lens, int n_shards, int data_only);
 
+/* Encoder.Verify (klauspost reedsolomon.go Verify): *ok = 1 when every parity
+ * shard equals the parity recomputed from the data shards.  Same argument
+ * checks as hbec_encode.  Host memory, synchronous. */
+int hbec_verify(hbec_codec* codec, uint8_t* const* shards, const size_t* lens, int n_shards, int* ok);
+
 /* ---------------------------------------------------------------------------
  * Device-resident batches (the GPU hot path).  A view places shard i of
  * object o at base + o * obj_stride in device memory.  Work is queued on
@@ -100,6 +105,12 @@ int hbec_encode_batch(hbec_codec* codec, const hbec_view* views, uint64_t n_obje
  * order are the survivors.  data_only = 1 leaves missing parity untouched. */
 int hbec_reconstruct_batch(hbec_codec* codec, const hbec_view* views, const uint8_t* present, uint64_t n_objects,
                            uint64_t shard_len, int data_only, void* hip_stream);
+
+/* Verify a batch (read-only stream over k+m shards per object): sets
+ * d_flags[o] (device memory, n_objects uint32, caller-zeroed) to 1 for every
+ * object whose stored parity differs from the recomputed parity. */
+int hbec_verify_batch(hbec_codec* codec, const hbec_view* views, uint64_t n_objects, uint64_t shard_len,
+                      uint32_t* d_flags, void* hip_stream);
 
 /* The decode rows a reconstruct applies: survivors[0..k) (shard indices read),
  * outputs[0..*n_outputs) (shard indices written), rows[*n_outputs][k]. */

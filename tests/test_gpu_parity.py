@@ -518,3 +518,49 @@ def test_host_path_rejects_wide_k():
     enc = RS.New(10, 2)
     with pytest.raises(RS.ErrInvalidArg):
         enc.EncodeStripes(_host_stripes(10, 2, [1000]))
+
+
+# ------------------------------------------------------------------ Verify
+@pytest.mark.parametrize("k,m,n", [(4, 2, 4096), (8, 3, 1000), (5, 5, 17), (10, 4, 3000), (2, 1, 1)])
+def test_verify_host(k, m, n):
+    enc = RS.New(k, m)
+    rng = np.random.default_rng(k + m + n)
+    shards = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)] + [np.zeros(n, np.uint8) for _ in range(m)]
+    assert enc.Verify(shards) is (m == 0)
+    enc.Encode(shards)
+    assert enc.Verify(shards)
+    for victim in (0, k - 1, k, k + m - 1):
+        bad = [s.copy() for s in shards]
+        bad[victim][n // 2] ^= 0x40
+        assert not enc.Verify(bad), victim
+    with pytest.raises(RS.ErrShardSize):
+        enc.Verify(shards[:-1] + [np.zeros(n + 1, np.uint8)])
+    with pytest.raises(RS.ErrTooFewShards):
+        enc.Verify(shards[:-1])
+
+
+@pytest.mark.parametrize("k,m,size,unaligned", [(4, 2, MiB, False), (8, 3, 4096, False), (8, 3, MiB, False),
+                                                (4, 2, 1000 * 4, True), (12, 4, 12 * 4096, False)])
+def test_verify_batch_flags(k, m, size, unaligned):
+    n = 64
+    s = size // k
+    extra = 3 if unaligned else 0
+    objs = torch.empty((n, k * s + extra), dtype=torch.uint8, device="cuda")
+    B.fill_splitmix(objs, k * s + extra)
+    parity = torch.empty((n, m * s + extra), dtype=torch.uint8, device="cuda")
+    enc = RS.New(k, m)
+    views = [(objs.data_ptr() + extra + j * s, objs.stride(0)) for j in range(k)]
+    views += [(parity.data_ptr() + extra + r * s, parity.stride(0)) for r in range(m)]
+    B.encode_views(enc, views, n, s)
+    flags = torch.zeros(n, dtype=torch.int32, device="cuda")
+    B.verify_views(enc, views, n, s, flags)
+    torch.cuda.synchronize()
+    assert int(flags.sum()) == 0
+    corrupt = {3: ("data", 0, 5), 17: ("parity", m - 1, s - 1), 40: ("data", k - 1, s // 2), 63: ("parity", 0, 0)}
+    for o, (kind, i, off) in corrupt.items():
+        t = objs if kind == "data" else parity
+        t[o, extra + i * s + off] ^= 0x01
+    flags.zero_()
+    B.verify_views(enc, views, n, s, flags)
+    torch.cuda.synchronize()
+    assert sorted(torch.nonzero(flags).flatten().tolist()) == sorted(corrupt)
