@@ -71,6 +71,11 @@ _SIG = [
     ("hbec_reconstruct_plan", C.c_int, [_P, _P, _U8P, C.c_int, _P]),
     ("hbec_encode_host", C.c_int, [_P, C.POINTER(Stripe), C.c_uint64]),
     ("hbec_reconstruct_host", C.c_int, [_P, C.POINTER(Stripe), C.c_uint64, _U8P, C.c_int]),
+    ("hbec_batcher_new", C.c_int, [_P, C.c_uint64, C.c_uint32, C.POINTER(_P)]),
+    ("hbec_batcher_free", None, [_P]),
+    ("hbec_batcher_encode", C.c_int, [_P, C.POINTER(Stripe)]),
+    ("hbec_batcher_reconstruct", C.c_int, [_P, C.POINTER(Stripe), _U8P, C.c_int]),
+    ("hbec_batcher_stats", C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     ("hbec_set_force_stream", C.c_int, [C.c_int]),
     ("hbec_kernel_info", C.c_int,
      [C.c_int, C.c_int, C.c_uint64, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),

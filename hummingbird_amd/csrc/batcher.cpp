@@ -1,0 +1,176 @@
+// batcher.cpp — batched stabilization driver.
+//
+// In the reference every nursery object is stabilized by its own call chain
+// (objectserver/nurserystabilizer.go:72-99: one object at a time per device,
+// `object-nursery.concurrency` workers, a 1 ms sleep between objects), and
+// ecSplit encodes each stripe with its own Encoder call (ecutils.go:59).  On
+// the GPU a single 1 MiB encode is dominated by launch + PCIe latency, so this
+// driver lets concurrent callers share launches: each caller submits one host
+// stripe (ecSplit databuf layout) and blocks; a worker thread takes everything
+// queued — up to max_batch_bytes, or whatever has arrived when max_wait_us
+// passes after the oldest request — codes it with one streaming host-path
+// call (hostpath.cpp), and wakes the callers.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/hbec.h"
+#include "internal.h"
+
+using hbec::fail;
+
+namespace {
+
+struct Request {
+    hbec_stripe stripe;
+    int op;  // 0 encode, 1 reconstruct
+    std::vector<uint8_t> present;
+    int data_only = 0;
+    int rc = HBEC_OK;
+    std::string err;
+    bool done = false;
+};
+
+}  // namespace
+
+struct hbec_batcher {
+    hbec_codec* codec = nullptr;
+    int device = 0;
+    uint64_t max_batch_bytes = 0;
+    std::chrono::microseconds max_wait{0};
+    std::mutex mu;
+    std::condition_variable cv_work, cv_done;
+    std::deque<Request*> queue;
+    bool stop = false;
+    std::thread worker;
+    // statistics
+    uint64_t batches = 0, stripes = 0;
+
+    void run() {
+        (void)hipSetDevice(device);
+        std::unique_lock<std::mutex> lk(mu);
+        for (;;) {
+            cv_work.wait(lk, [&] { return stop || !queue.empty(); });
+            if (queue.empty() && stop) return;
+            // let the batch fill: until max bytes queued or max_wait after the oldest arrived
+            const auto deadline = std::chrono::steady_clock::now() + max_wait;
+            const int n_shards = hbec_data_shards(codec) + hbec_parity_shards(codec);
+            while (!stop) {
+                uint64_t queued = 0;
+                for (auto* r : queue) queued += r->stripe.shard_len * (uint64_t)n_shards;
+                if (queued >= max_batch_bytes) break;
+                if (cv_work.wait_until(lk, deadline) == std::cv_status::timeout) break;
+            }
+            // take one homogeneous group (same op and erasure pattern) from the front
+            std::vector<Request*> batch;
+            uint64_t bytes = 0;
+            while (!queue.empty()) {
+                Request* r = queue.front();
+                if (!batch.empty() && (r->op != batch[0]->op || r->present != batch[0]->present ||
+                                       r->data_only != batch[0]->data_only))
+                    break;
+                const uint64_t b = r->stripe.shard_len * (uint64_t)n_shards;
+                if (!batch.empty() && bytes + b > max_batch_bytes) break;
+                batch.push_back(r);
+                bytes += b;
+                queue.pop_front();
+            }
+            lk.unlock();
+            std::vector<hbec_stripe> st(batch.size());
+            for (size_t i = 0; i < batch.size(); ++i) st[i] = batch[i]->stripe;
+            int rc;
+            if (batch[0]->op == 0)
+                rc = hbec_encode_host(codec, st.data(), st.size());
+            else
+                rc = hbec_reconstruct_host(codec, st.data(), st.size(), batch[0]->present.data(), batch[0]->data_only);
+            const std::string err = rc ? hbec_last_error() : "";
+            lk.lock();
+            ++batches;
+            stripes += batch.size();
+            for (auto* r : batch) {
+                r->rc = rc;
+                r->err = err;
+                r->done = true;
+            }
+            cv_done.notify_all();
+        }
+    }
+
+    int submit(Request& r) {
+        std::unique_lock<std::mutex> lk(mu);
+        if (stop) return fail(HBEC_ERR_INVALID_ARG, "batcher stopped");
+        queue.push_back(&r);
+        cv_work.notify_one();
+        cv_done.wait(lk, [&] { return r.done; });
+        return r.rc ? fail(r.rc, r.err) : HBEC_OK;
+    }
+};
+
+extern "C" {
+
+int hbec_batcher_new(hbec_codec* codec, uint64_t max_batch_bytes, uint32_t max_wait_us, hbec_batcher** out) {
+    if (!codec || !out) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+    *out = nullptr;
+    if (hbec_data_shards(codec) > 8) return fail(HBEC_ERR_INVALID_ARG, "batcher supports k <= 8");
+    std::unique_ptr<hbec_batcher> b(new (std::nothrow) hbec_batcher());
+    if (!b) return fail(HBEC_ERR_NOMEM, "batcher allocation");
+    hipError_t e = hipGetDevice(&b->device);
+    if (e != hipSuccess) return hbec::hip_fail(e, "hipGetDevice");
+    b->codec = codec;
+    b->max_batch_bytes = max_batch_bytes ? max_batch_bytes : (256ull << 20);
+    b->max_wait = std::chrono::microseconds(max_wait_us);
+    hbec_batcher* raw = b.get();
+    b->worker = std::thread([raw] { raw->run(); });
+    *out = b.release();
+    return HBEC_OK;
+}
+
+void hbec_batcher_free(hbec_batcher* b) {
+    if (!b) return;
+    {
+        std::lock_guard<std::mutex> g(b->mu);
+        b->stop = true;
+    }
+    b->cv_work.notify_all();
+    b->worker.join();
+    delete b;
+}
+
+int hbec_batcher_encode(hbec_batcher* b, const hbec_stripe* stripe) {
+    if (!b || !stripe) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+    if (stripe->shard_len == 0) return HBEC_OK;
+    Request r;
+    r.stripe = *stripe;
+    r.op = 0;
+    return b->submit(r);
+}
+
+int hbec_batcher_reconstruct(hbec_batcher* b, const hbec_stripe* stripe, const uint8_t* present, int data_only) {
+    if (!b || !stripe || !present) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+    if (stripe->shard_len == 0) return HBEC_OK;
+    const int n = hbec_data_shards(b->codec) + hbec_parity_shards(b->codec);
+    Request r;
+    r.stripe = *stripe;
+    r.op = 1;
+    r.present.assign(present, present + n);
+    for (auto& v : r.present) v = v ? 1 : 0;
+    r.data_only = data_only ? 1 : 0;
+    return b->submit(r);
+}
+
+int hbec_batcher_stats(hbec_batcher* b, uint64_t* batches, uint64_t* stripes) {
+    if (!b) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+    std::lock_guard<std::mutex> g(b->mu);
+    if (batches) *batches = b->batches;
+    if (stripes) *stripes = b->stripes;
+    return HBEC_OK;
+}
+
+}  // extern "C"

@@ -193,6 +193,46 @@ class Encoder:
         return list(surv), list(outs)[: nout.value], r.reshape(nout.value, self.DataShards)
 
 
+class Batcher:
+    """hbec_batcher: concurrent callers each submit one host stripe (ecSplit
+    databuf layout, (k+m)*S bytes) and block; the library codes whatever has
+    queued in one streaming host-path call.  ctypes releases the GIL during
+    the call, so Python threads really run concurrently."""
+
+    def __init__(self, enc: Encoder, max_batch_bytes: int = 256 << 20, max_wait_us: int = 200):
+        self.enc = enc
+        self._h = C.c_void_p()
+        check(N.lib().hbec_batcher_new(enc.handle, int(max_batch_bytes), int(max_wait_us), C.byref(self._h)))
+
+    def close(self):
+        if self._h:
+            N.lib().hbec_batcher_free(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def _stripe(self, st):
+        a = _as_array(st)
+        s = N.Stripe()
+        s.base = a.ctypes.data
+        s.shard_len = a.size // self.enc.Shards
+        return s
+
+    def Encode(self, stripe) -> None:
+        s = self._stripe(stripe)
+        check(N.lib().hbec_batcher_encode(self._h, C.byref(s)))
+
+    def Reconstruct(self, stripe, present, data_only: bool = False) -> None:
+        s = self._stripe(stripe)
+        p = (C.c_uint8 * self.enc.Shards)(*[1 if x else 0 for x in present])
+        check(N.lib().hbec_batcher_reconstruct(self._h, C.byref(s), p, int(data_only)))
+
+    def stats(self):
+        b, s = C.c_uint64(), C.c_uint64()
+        check(N.lib().hbec_batcher_stats(self._h, C.byref(b), C.byref(s)))
+        return {"batches": b.value, "stripes": s.value}
+
+
 def New(data_shards: int, parity_shards: int) -> Encoder:
     """reedsolomon.New (ecutils.go:27,77,135)."""
     return Encoder(data_shards, parity_shards)

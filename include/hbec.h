@@ -160,6 +160,19 @@ int hbec_encode_host(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n_s
 int hbec_reconstruct_host(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n_stripes, const uint8_t* present,
                           int data_only);
 
+/* Batching driver for concurrent callers (e.g. one cgo call per Stabilize):
+ * each call submits ONE host stripe and blocks until it is coded; a worker
+ * thread codes everything queued — up to max_batch_bytes (0 = 256 MiB), or
+ * what has arrived max_wait_us after the oldest request — with one host-path
+ * call.  Requests with different ops / erasure patterns form separate
+ * batches.  k <= 8.  The codec must outlive the batcher. */
+typedef struct hbec_batcher hbec_batcher;
+int hbec_batcher_new(hbec_codec* codec, uint64_t max_batch_bytes, uint32_t max_wait_us, hbec_batcher** out);
+void hbec_batcher_free(hbec_batcher* batcher);
+int hbec_batcher_encode(hbec_batcher* batcher, const hbec_stripe* stripe);
+int hbec_batcher_reconstruct(hbec_batcher* batcher, const hbec_stripe* stripe, const uint8_t* present, int data_only);
+int hbec_batcher_stats(hbec_batcher* batcher, uint64_t* batches, uint64_t* stripes);
+
 /* Tuning / introspection: force the runtime-K streaming kernel (0/1), and
  * report what a pass of k inputs -> r outputs over shard_len bytes launches:
  * tile bytes per wave, kind (0 = unrolled, 1 = pipelined, 2 = streaming) and

@@ -132,6 +132,40 @@ def library_host_path(op: str, n_obj=4096, reps=3):
             "algorithmic_GiB_s": round(n_obj * (k + 2) * S / t / GiB, 2), "objects_per_s": round(n_obj / t, 1)}
 
 
+def batched_callers(n_threads=64, per_thread=32):
+    """Many concurrent callers, one 1 MiB object each per call, through the
+    batching driver (what concurrent Stabilize goroutines would do)."""
+    import threading
+
+    k, m, S = 4, 2, MiB // 4
+    enc = RS.New(k, m)
+    bat = RS.Batcher(enc, max_batch_bytes=96 << 20, max_wait_us=300)
+    from oracle import coracle as CO
+    n = n_threads * per_thread
+    pool = np.empty((n, (k + m) * S), dtype=np.uint8)
+    pool[:, :k * S] = CO.fill_objects(0, n, k * S)
+
+    def worker(t):
+        for i in range(t * per_thread, (t + 1) * per_thread):
+            bat.Encode(pool[i])
+
+    bat.Encode(pool[0])  # warm the ring
+    t0 = time.perf_counter()
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(n_threads)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    t = time.perf_counter() - t0
+    st = bat.stats()
+    bat.close()
+    want = CO.encode_batch(k, m, pool[n - 1:, :k * S])[0][0]
+    assert np.array_equal(pool[n - 1, k * S:], want)
+    return {"measure": "batcher_concurrent_Encode_1MiB", "threads": n_threads, "objects": n,
+            "seconds": round(t, 4), "object_data_GiB_s": round(n * k * S / t / GiB, 2),
+            "us_per_object": round(t / n * 1e6, 1), "batches": st["batches"]}
+
+
 def per_call(n_calls=200):
     k, m, S = 4, 2, MiB // 4
     enc = RS.New(k, m)
@@ -150,7 +184,7 @@ def per_call(n_calls=200):
 def main():
     torch.cuda.set_device(0)
     for r in (pipelined("encode"), pipelined("reconstruct"), library_host_path("encode"),
-              library_host_path("reconstruct"), per_call()):
+              library_host_path("reconstruct"), batched_callers(), per_call()):
         print(json.dumps(r), flush=True)
 
 

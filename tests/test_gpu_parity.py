@@ -564,3 +564,45 @@ def test_verify_batch_flags(k, m, size, unaligned):
     B.verify_views(enc, views, n, s, flags)
     torch.cuda.synchronize()
     assert sorted(torch.nonzero(flags).flatten().tolist()) == sorted(corrupt)
+
+
+# ------------------------------------------------------------ batching driver
+def test_batcher_concurrent_callers_share_launches():
+    import threading
+
+    k, m = 4, 2
+    enc = RS.New(k, m)
+    bat = RS.Batcher(enc, max_batch_bytes=64 << 20, max_wait_us=2000)
+    sizes = [MiB if i % 3 else 4096 + 16 * i for i in range(48)]
+    stripes = _host_stripes(k, m, sizes, seed=77)
+    want = _encoded_copy(k, m, stripes)
+    errors = []
+
+    def worker(idx):
+        try:
+            bat.Encode(stripes[idx])
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(e)
+
+    threads = [threading.Thread(target=worker, args=(i,)) for i in range(len(stripes))]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    assert not errors
+    assert all(np.array_equal(a, b) for a, b in zip(stripes, want))
+    st = bat.stats()
+    assert st["stripes"] == len(stripes) and st["batches"] < len(stripes)
+    # reconstruct through the batcher too
+    damaged = [w.copy() for w in want]
+    for d in damaged:
+        s = d.size // (k + m)
+        d[:s] = 0
+    threads = [threading.Thread(target=lambda i=i: bat.Reconstruct(damaged[i], [0, 1, 1, 1, 1, 1]))
+               for i in range(len(damaged))]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    assert all(np.array_equal(a, b) for a, b in zip(damaged, want))
+    bat.close()
