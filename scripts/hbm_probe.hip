@@ -115,6 +115,26 @@ __global__ __launch_bounds__(256) void probe_xor42u(const uint8_t* objs, uint8_t
     }
 }
 
+// same 4->2 XOR but shard-INTERLEAVED layout: per object, per 1 KiB column
+// block, the 4 input blocks are adjacent (in [n][S/1K][4][1K]) and so are the
+// 2 outputs (out [n][S/1K][2][1K]): 2 streams instead of 6.
+__global__ __launch_bounds__(256) void probe_xor42_il(const uint8_t* objs, uint8_t* out, uint32_t n_obj, uint32_t S) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    const uint32_t nw = gridDim.x * 4;
+    const uint64_t nt = (uint64_t)n_obj * (S / 1024);
+    for (uint64_t t = wave; t < nt; t += nw) {
+        const u32x4* src = reinterpret_cast<const u32x4*>(objs + t * 4096) + lane;
+        u32x4 x0 = __builtin_nontemporal_load(src), x1 = __builtin_nontemporal_load(src + 64),
+              x2 = __builtin_nontemporal_load(src + 128), x3 = __builtin_nontemporal_load(src + 192);
+        u32x4* dst = reinterpret_cast<u32x4*>(out + t * 2048) + lane;
+        u32x4 a = x0 ^ x1 ^ x2 ^ x3;
+        __builtin_nontemporal_store(a, dst);
+        a.x ^= 1u;
+        __builtin_nontemporal_store(a, dst + 64);
+    }
+}
+
 // store-flavour probes: aux bits of the buffer store (1 = sc0, 2 = nt, 16 = sc1)
 template <int AUX, int UNR>
 __global__ __launch_bounds__(256) void probe_write_buf(uint8_t* dst, uint64_t n16) {
@@ -174,7 +194,8 @@ int probe_xor_variant(int u, const void* src, void* dst, uint32_t n_obj, uint32_
     hipStream_t st = (hipStream_t)stream;
     const uint8_t* a = (const uint8_t*)src;
     uint8_t* b = (uint8_t*)dst;
-    if (u == 1) hipLaunchKernelGGL((probe_xor42u<1>), dim3(grid), dim3(256), 0, st, a, b, n_obj, S);
+    if (u == 0) hipLaunchKernelGGL(probe_xor42_il, dim3(grid), dim3(256), 0, st, a, b, n_obj, S);
+    else if (u == 1) hipLaunchKernelGGL((probe_xor42u<1>), dim3(grid), dim3(256), 0, st, a, b, n_obj, S);
     else if (u == 2) hipLaunchKernelGGL((probe_xor42u<2>), dim3(grid), dim3(256), 0, st, a, b, n_obj, S);
     else if (u == 4) hipLaunchKernelGGL((probe_xor42u<4>), dim3(grid), dim3(256), 0, st, a, b, n_obj, S);
     else return -1;

@@ -293,8 +293,8 @@ def run_xor_sweep(reps=8):
     out = torch.empty((n_obj, 2 * S), dtype=torch.uint8, device="cuda")
     st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     rows = []
-    for u in (1, 2, 4):
-        for grid in (256, 512, 768, 1024, 1792, 2048, 4096):
+    for u in (0, 1, 4):  # 0 = shard-interleaved layout
+        for grid in (256, 512, 1024, 2048, 4096):
             ts = []
             for r in range(reps + 1):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -175,3 +175,16 @@ def test_plan_build_needs_no_kernel_launch_for_empty():
     assert N.lib().hbec_plan_info(h, C.byref(nt), C.byref(tb), C.byref(fb), C.byref(sb)) == 0
     assert (nt.value, fb.value, sb.value) == (0, 0, 0) and tb.value in (1024, 2048, 3072, 4096)
     N.lib().hbec_plan_free(h)
+
+
+def test_pure_c_client(tmp_path):
+    """The header compiles as C11 with gcc and the library links and answers
+    from a plain C program (what cgo does)."""
+    exe = tmp_path / "abi_smoke"
+    lib_dir = N.LIB_PATH.parent
+    subprocess.run(["gcc", "-std=c11", "-Wall", "-Werror", "-I", str(ROOT / "include"),
+                    str(ROOT / "tests" / "native" / "abi_smoke.c"), "-L", str(lib_dir), "-lhbec",
+                    f"-Wl,-rpath,{lib_dir}", "-o", str(exe)], check=True, capture_output=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert out.returncode == 0, (out.returncode, out.stderr)
+    assert "abi ok v1" in out.stdout
