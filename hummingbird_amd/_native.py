@@ -58,6 +58,12 @@ _SIG = [
     ("hbec_encode_batch", C.c_int, [_P, C.POINTER(View), C.c_uint64, C.c_uint64, _P]),
     ("hbec_reconstruct_batch", C.c_int,
      [_P, C.POINTER(View), _U8P, C.c_uint64, C.c_uint64, C.c_int, _P]),
+    ("hbec_md5_batch", C.c_int, [C.POINTER(View), C.c_int, C.c_uint64, C.c_uint64, _P, _P]),
+    ("hbec_md5_new", C.c_int, [C.c_int, C.c_uint64, C.POINTER(_P)]),
+    ("hbec_md5_free", None, [_P]),
+    ("hbec_md5_update", C.c_int, [_P, C.POINTER(View), C.c_uint64, _P]),
+    ("hbec_md5_final", C.c_int, [_P, _P, _P]),
+    ("hbec_encode_md5_batch", C.c_int, [_P, C.POINTER(View), C.c_uint64, C.c_uint64, _P, _P]),
     ("hbec_decode_rows", C.c_int,
      [_P, _U8P, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int), _U8P]),
     ("hbec_apply_batch", C.c_int,
@@ -81,6 +87,8 @@ _SIG = [
      [C.c_int, C.c_int, C.c_uint64, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     ("hbec_ec_shard_length", C.c_int64, [C.c_int64, C.c_int]),
     ("hbec_ec_split", C.c_int, [C.c_int, C.c_int, READ_FN, _P, C.c_int, C.c_int64, WRITE_FN, C.POINTER(_P)]),
+    ("hbec_ec_split_md5", C.c_int,
+     [C.c_int, C.c_int, READ_FN, _P, C.c_int, C.c_int64, WRITE_FN, C.POINTER(_P), _U8P]),
     ("hbec_ec_reconstruct", C.c_int,
      [C.c_int, C.c_int, READ_FN, C.POINTER(_P), C.c_int, C.c_int64, WRITE_FN, C.POINTER(_P),
       C.POINTER(C.c_int), C.c_int]),

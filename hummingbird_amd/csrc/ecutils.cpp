@@ -3,6 +3,7 @@
 //
 //   hbec_ec_shard_length  <- ecShardLength   ecutils.go:14-24
 //   hbec_ec_split         <- ecSplit         ecutils.go:26-72
+//   hbec_ec_split_md5     <- ecSplit + the receivers' ShardHash (indexdb.go:746-753)
 //   hbec_ec_reconstruct   <- ecReconstruct   ecutils.go:74-132
 //   hbec_ec_glue          <- ecGlue          ecutils.go:134-186
 //   hbec_parse_ec_scheme  <- parseECScheme   ecobj.go:82-98
@@ -13,6 +14,8 @@
 // truncation of the last stripe on glue).  Reference quirk kept: ecReconstruct
 // never marks a body failed, so a body whose read fails is retried on the
 // next stripe (ecutils.go:103-107).
+#include <hip/hip_runtime.h>
+
 #include <cerrno>
 #include <climits>
 #include <cstdlib>
@@ -52,6 +55,19 @@ struct CodecHolder {
     ~CodecHolder() { hbec_free(c); }
 };
 
+// Device side of ecSplit with hashing: one stripe buffer (k+m shards) plus the
+// digests, a private stream, and the per-shard MD5 chains.
+struct DeviceStripe {
+    hipStream_t stream = nullptr;
+    uint8_t* buf = nullptr;
+    hbec_md5* md5 = nullptr;
+    ~DeviceStripe() {
+        hbec_md5_free(md5);
+        if (buf) hipFree(buf);
+        if (stream) hipStreamDestroy(stream);
+    }
+};
+
 // ecReconstruct / ecGlue per-stripe shard size (ecutils.go:86-92, :144-150)
 int64_t stripe_shard_size(int k, int chunk, int64_t remaining) {
     int64_t s = chunk;
@@ -75,8 +91,8 @@ int64_t hbec_ec_shard_length(int64_t length, int data_shards) {
     return s;
 }
 
-int hbec_ec_split(int k, int m, hbec_read_fn read, void* fp, int chunk_size, int64_t content_length,
-                  hbec_write_fn write, void* const* writers) {
+static int ec_split(int k, int m, hbec_read_fn read, void* fp, int chunk_size, int64_t content_length,
+                    hbec_write_fn write, void* const* writers, uint8_t* shard_md5) {
     CodecHolder enc;
     int rc = hbec_new(k, m, &enc.c);
     if (rc) return rc;
@@ -87,6 +103,15 @@ int hbec_ec_split(int k, int m, hbec_read_fn read, void* fp, int chunk_size, int
     std::vector<uint8_t*> shards(n);
     std::vector<size_t> lens(n);
     std::vector<char> failed(n, 0);
+    std::vector<hbec_view> views(n);
+    DeviceStripe dev;
+    if (shard_md5) {
+        hipError_t e = hipStreamCreateWithFlags(&dev.stream, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipMalloc(&dev.buf, 16u * (size_t)n + databuf.size());  // digests, then stripe
+        if (e != hipSuccess) return hbec::hip_fail(e, "ecSplit device buffers");
+        rc = hbec_md5_new(n, 1, &dev.md5);
+        if (rc) return rc;
+    }
     int64_t total = 0;
     while (total < content_length) {
         int64_t expected = (int64_t)k * chunk_size;
@@ -103,15 +128,47 @@ int hbec_ec_split(int k, int m, hbec_read_fn read, void* fp, int chunk_size, int
             shards[i] = databuf.data() + (size_t)i * s;
             lens[i] = s;
         }
-        rc = hbec_encode(enc.c, shards.data(), lens.data(), n);
-        if (rc) return rc;
+        if (!shard_md5) {
+            rc = hbec_encode(enc.c, shards.data(), lens.data(), n);
+            if (rc) return rc;
+        } else {  // stripe to the GPU, encode and hash there, parity back
+            uint8_t* d_stripe = dev.buf + 16u * (size_t)n;
+            for (int i = 0; i < n; ++i) views[i] = hbec_view{d_stripe + (size_t)i * s, 0};
+            hipError_t e = hipMemcpyAsync(d_stripe, databuf.data(), (size_t)k * s, hipMemcpyHostToDevice, dev.stream);
+            if (e != hipSuccess) return hbec::hip_fail(e, "ecSplit H2D");
+            rc = hbec_encode_batch(enc.c, views.data(), 1, s, dev.stream);
+            if (!rc) rc = hbec_md5_update(dev.md5, views.data(), s, dev.stream);
+            if (rc) return rc;
+            e = hipMemcpyAsync(shards[k], d_stripe + (size_t)k * s, (size_t)m * s, hipMemcpyDeviceToHost, dev.stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(dev.stream);
+            if (e != hipSuccess) return hbec::hip_fail(e, "ecSplit D2H");
+        }
         for (int i = 0; i < n; ++i) {
             if (writers && writers[i] && !failed[i]) {
                 if (!write || write(writers[i], shards[i], s) != 0) failed[i] = 1;
             }
         }
     }
+    if (shard_md5) {
+        uint8_t* d_dig = dev.buf;
+        rc = hbec_md5_final(dev.md5, d_dig, dev.stream);
+        if (rc) return rc;
+        hipError_t e = hipMemcpyAsync(shard_md5, d_dig, 16u * (size_t)n, hipMemcpyDeviceToHost, dev.stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(dev.stream);
+        if (e != hipSuccess) return hbec::hip_fail(e, "ecSplit digests");
+    }
     return HBEC_OK;
+}
+
+int hbec_ec_split(int k, int m, hbec_read_fn read, void* fp, int chunk_size, int64_t content_length,
+                  hbec_write_fn write, void* const* writers) {
+    return ec_split(k, m, read, fp, chunk_size, content_length, write, writers, nullptr);
+}
+
+int hbec_ec_split_md5(int k, int m, hbec_read_fn read, void* fp, int chunk_size, int64_t content_length,
+                      hbec_write_fn write, void* const* writers, uint8_t* shard_md5) {
+    if (!shard_md5) return fail(HBEC_ERR_INVALID_ARG, "ecSplit: null digest buffer");
+    return ec_split(k, m, read, fp, chunk_size, content_length, write, writers, shard_md5);
 }
 
 int hbec_ec_reconstruct(int k, int m, hbec_read_fn read, void* const* bodies, int chunk_size,

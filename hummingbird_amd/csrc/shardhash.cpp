@@ -1,0 +1,241 @@
+// shardhash.cpp — ShardHash (MD5 of a shard body, objectserver/indexdb.go:746-753)
+// on the GPU: one-shot batches, streaming chains fed stripe by stripe, and
+// encode + hash of every shard with the two overlapped.
+//
+// Why the hash is not computed inside the encode kernel's output pass: the
+// encode streams each object's shards in 1-4 KiB column tiles spread over
+// many waves at once, while an MD5 chain must see its shard's 64-byte blocks
+// strictly in order on one lane.  Instead hbec_encode_md5_batch cuts the shard
+// range into column segments: the encode of segment s+1 (HBM-bound, one block
+// per CU) runs on the caller's stream while the MD5 chains consume segment s
+// (VALU-latency-bound, one lane per chain) on a side stream, so the hash
+// mostly hides under the encode.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "../../include/hbec.h"
+#include "internal.h"
+
+namespace hbec {
+
+hipError_t launch_md5(const void* const* bases, const uint64_t* strides, int n_views, uint32_t chain_stride,
+                      uint32_t view0, uint64_t n_obj, uint64_t len, uint64_t total, uint32_t flags, void* state,
+                      uint8_t* digest, bool aligned, hipStream_t stream);
+uint64_t md5_state_bytes();
+
+namespace {
+
+constexpr int kViewsPerLaunch = 32;
+constexpr uint32_t kInit = 1u, kFinal = 2u;
+
+// All views of one update/final step, launched 32 views at a time.
+int md5_step(const hbec_view* views, int n_views, uint64_t n_obj, uint64_t len, uint64_t total, uint32_t flags,
+             void* state, uint8_t* digest, hipStream_t stream) {
+    const uint64_t carry = total & 63u;
+    const uint64_t first = carry ? 64u - carry : 0u;  // data offset of the first whole block
+    bool aligned = true;
+    for (int v = 0; v < n_views; ++v) {
+        const uintptr_t b = reinterpret_cast<uintptr_t>(views[v].base) + first;
+        if ((b & 15u) || (views[v].obj_stride & 15u)) aligned = false;
+    }
+    for (int v0 = 0; v0 < n_views; v0 += kViewsPerLaunch) {
+        const int nv = std::min(kViewsPerLaunch, n_views - v0);
+        const void* bases[kViewsPerLaunch];
+        uint64_t strides[kViewsPerLaunch];
+        for (int v = 0; v < nv; ++v) {
+            bases[v] = views[v0 + v].base;
+            strides[v] = views[v0 + v].obj_stride;
+        }
+        hipError_t e = launch_md5(bases, strides, nv, (uint32_t)n_views, (uint32_t)v0, n_obj, len, total, flags,
+                                  state, digest, aligned, stream);
+        if (e != hipSuccess) return hip_fail(e, "md5 launch");
+    }
+    return HBEC_OK;
+}
+
+int check_digests(const uint8_t* d) {
+    if (!d) return fail(HBEC_ERR_INVALID_ARG, "md5: null digest buffer");
+    if (reinterpret_cast<uintptr_t>(d) & 3u) return fail(HBEC_ERR_INVALID_ARG, "md5: digest buffer not 4-byte aligned");
+    return HBEC_OK;
+}
+
+int check_views(const hbec_view* views, int n_views, uint64_t n_obj, uint64_t len) {
+    if (!views || n_views <= 0) return fail(HBEC_ERR_INVALID_ARG, "md5: need at least one view");
+    if (n_obj > (1ull << 31) / 64 * 64) return fail(HBEC_ERR_INVALID_ARG, "md5: too many objects for one call");
+    if (len > 0)
+        for (int v = 0; v < n_views; ++v)
+            if (!views[v].base) return fail(HBEC_ERR_INVALID_ARG, "md5: null view");
+    return HBEC_OK;
+}
+
+// Side streams for the segment pipeline: taken per call, returned right after
+// the call has queued its work (later users only queue behind it).  Created
+// on first use per device and kept for the life of the process.
+std::mutex g_side_mu;
+std::vector<std::pair<int, hipStream_t>> g_side_free;
+
+int side_stream_get(int dev, hipStream_t* s) {
+    {
+        std::lock_guard<std::mutex> g(g_side_mu);
+        for (size_t i = 0; i < g_side_free.size(); ++i)
+            if (g_side_free[i].first == dev) {
+                *s = g_side_free[i].second;
+                g_side_free.erase(g_side_free.begin() + (long)i);
+                return HBEC_OK;
+            }
+    }
+    hipError_t e = hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+    if (e != hipSuccess) return hip_fail(e, "hipStreamCreate");
+    return HBEC_OK;
+}
+
+void side_stream_put(int dev, hipStream_t s) {
+    std::lock_guard<std::mutex> g(g_side_mu);
+    g_side_free.emplace_back(dev, s);
+}
+
+// Event-ordered "b waits for everything queued on a so far".
+int order_after(hipStream_t b, hipStream_t a) {
+    hipEvent_t ev;
+    hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (e != hipSuccess) return hip_fail(e, "hipEventCreate");
+    e = hipEventRecord(ev, a);
+    if (e == hipSuccess) e = hipStreamWaitEvent(b, ev, 0);
+    hipEventDestroy(ev);  // released once the recorded work completes
+    if (e != hipSuccess) return hip_fail(e, "stream ordering");
+    return HBEC_OK;
+}
+
+}  // namespace
+
+// Segment length for the encode/hash pipeline: ~8 segments, 4 KiB multiples
+// (whole MD5 blocks, whole encode tiles), none below 32 KiB.
+static uint64_t md5_segment(uint64_t shard_len) {
+    uint64_t seg = (shard_len / 8 + 4095) & ~uint64_t(4095);
+    return std::max<uint64_t>(seg, 32768);
+}
+
+}  // namespace hbec
+
+using namespace hbec;
+
+struct hbec_md5 {
+    int n_views = 0;
+    uint64_t n_obj = 0;
+    uint64_t total = 0;
+    bool started = false;
+    void* d_state = nullptr;
+};
+
+extern "C" {
+
+int hbec_md5_batch(const hbec_view* views, int n_views, uint64_t n_objects, uint64_t len, uint8_t* d_digests,
+                   void* hip_stream) {
+    int rc = check_views(views, n_views, n_objects, len);
+    if (rc) return rc;
+    rc = check_digests(d_digests);
+    if (rc) return rc;
+    if (n_objects == 0) return HBEC_OK;
+    return md5_step(views, n_views, n_objects, len, 0, kInit | kFinal, nullptr, d_digests,
+                    static_cast<hipStream_t>(hip_stream));
+}
+
+int hbec_md5_new(int n_views, uint64_t n_objects, hbec_md5** out) {
+    if (!out || n_views <= 0 || n_objects == 0) return fail(HBEC_ERR_INVALID_ARG, "md5_new: bad arguments");
+    *out = nullptr;
+    hbec_md5* c = new (std::nothrow) hbec_md5();
+    if (!c) return fail(HBEC_ERR_NOMEM, "md5_new");
+    c->n_views = n_views;
+    c->n_obj = n_objects;
+    hipError_t e = hipMalloc(&c->d_state, (size_t)n_views * n_objects * md5_state_bytes());
+    if (e != hipSuccess) {
+        delete c;
+        return e == hipErrorOutOfMemory ? fail(HBEC_ERR_NOMEM, "md5 state") : hip_fail(e, "hipMalloc");
+    }
+    *out = c;
+    return HBEC_OK;
+}
+
+void hbec_md5_free(hbec_md5* c) {
+    if (!c) return;
+    if (c->d_state) hipFree(c->d_state);
+    delete c;
+}
+
+int hbec_md5_update(hbec_md5* c, const hbec_view* views, uint64_t len, void* hip_stream) {
+    if (!c) return fail(HBEC_ERR_INVALID_ARG, "md5_update: null context");
+    int rc = check_views(views, c->n_views, c->n_obj, len);
+    if (rc) return rc;
+    if (len == 0 && c->started) return HBEC_OK;
+    rc = md5_step(views, c->n_views, c->n_obj, len, c->total, c->started ? 0u : kInit, c->d_state, nullptr,
+                  static_cast<hipStream_t>(hip_stream));
+    if (rc) return rc;
+    c->started = true;
+    c->total += len;
+    return HBEC_OK;
+}
+
+int hbec_md5_final(hbec_md5* c, uint8_t* d_digests, void* hip_stream) {
+    if (!c) return fail(HBEC_ERR_INVALID_ARG, "md5_final: null context");
+    int rc0 = check_digests(d_digests);
+    if (rc0) return rc0;
+    std::vector<hbec_view> none((size_t)c->n_views, hbec_view{nullptr, 0});
+    int rc = md5_step(none.data(), c->n_views, c->n_obj, 0, c->total, kFinal | (c->started ? 0u : kInit),
+                      c->d_state, d_digests, static_cast<hipStream_t>(hip_stream));
+    if (rc) return rc;
+    c->started = false;
+    c->total = 0;
+    return HBEC_OK;
+}
+
+int hbec_encode_md5_batch(hbec_codec* codec, const hbec_view* views, uint64_t n_objects, uint64_t shard_len,
+                          uint8_t* d_digests, void* hip_stream) {
+    if (!codec || !views) return fail(HBEC_ERR_INVALID_ARG, "encode_md5: null argument");
+    const int n = hbec_data_shards(codec) + hbec_parity_shards(codec);
+    int rc = check_digests(d_digests);
+    if (rc) return rc;
+    if (n_objects == 0) return HBEC_OK;
+    if (shard_len == 0) return fail(HBEC_ERR_SHARD_NO_DATA, "encode_md5: zero shard length");
+    rc = check_views(views, n, n_objects, shard_len);
+    if (rc) return rc;
+    hipStream_t main = static_cast<hipStream_t>(hip_stream);
+    const uint64_t seg = md5_segment(shard_len);
+    if (seg >= shard_len) {  // one segment: encode, then hash every shard
+        rc = hbec_encode_batch(codec, views, n_objects, shard_len, hip_stream);
+        if (rc) return rc;
+        return md5_step(views, n, n_objects, shard_len, 0, kInit | kFinal, nullptr, d_digests, main);
+    }
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+    void* state = nullptr;
+    e = hipMallocAsync(&state, (size_t)n * n_objects * md5_state_bytes(), main);
+    if (e != hipSuccess) return hip_fail(e, "hipMallocAsync");
+    hipStream_t side;
+    rc = side_stream_get(dev, &side);
+    if (rc) {
+        hipFreeAsync(state, main);
+        return rc;
+    }
+    std::vector<hbec_view> sv((size_t)n);
+    for (uint64_t off = 0; off < shard_len && rc == HBEC_OK; off += seg) {
+        const uint64_t len = std::min(seg, shard_len - off);
+        for (int i = 0; i < n; ++i) sv[i] = hbec_view{static_cast<uint8_t*>(views[i].base) + off, views[i].obj_stride};
+        rc = hbec_encode_batch(codec, sv.data(), n_objects, len, hip_stream);
+        if (rc) break;
+        rc = order_after(side, main);  // segment encoded (and, first time, state allocated)
+        if (rc) break;
+        const uint32_t flags = (off == 0 ? kInit : 0u) | (off + len == shard_len ? kFinal : 0u);
+        rc = md5_step(sv.data(), n, n_objects, len, off, flags, state, d_digests, side);
+    }
+    const int rc2 = order_after(main, side);  // caller's stream: digests ready
+    hipFreeAsync(state, main);
+    side_stream_put(dev, side);
+    return rc ? rc : rc2;
+}
+
+}  // extern "C"

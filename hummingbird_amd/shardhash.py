@@ -1,0 +1,102 @@
+"""ShardHash on the GPU: MD5 of shard bodies (objectserver/indexdb.go:746-753,
+``hex.EncodeToString(md5(body))``; re-checked by the auditor,
+objectserver/auditor.go:100-156), computed by libhbec's md5 kernel — one GPU
+lane per (object, shard) chain.
+
+Digest layout everywhere: uint8 [n_objects, n_views, 16] (raw MD5), device
+memory.  ``hexdigests`` turns it into the strings the index DB stores.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+from . import _native as N
+from .batch import _stream_ptr, _views, shard_views
+from .reedsolomon import Encoder, check
+
+
+def _digest_tensor(n_objects: int, n_views: int, device):
+    import torch
+
+    return torch.empty((n_objects, n_views, 16), dtype=torch.uint8, device=device)
+
+
+def md5_views(views, n_objects: int, length: int, digests=None, device="cuda", stream=None):
+    """MD5 of `length` bytes at every (base + o*stride) of every view."""
+    n = len(views)
+    if digests is None:
+        digests = _digest_tensor(n_objects, n, device)
+    check(N.lib().hbec_md5_batch(_views(views), n, int(n_objects), int(length), C.c_void_p(digests.data_ptr()),
+                                 _stream_ptr(stream)))
+    return digests
+
+
+def md5_rows(t, n_shards: int, shard_len: int, stream=None):
+    """MD5 of each of the n_shards consecutive shards in every row of a 2-D tensor."""
+    return md5_views(shard_views(t, n_shards, shard_len), t.shape[0], shard_len, device=t.device, stream=stream)
+
+
+def encode_md5_views(enc: Encoder, views, n_objects: int, shard_len: int, digests=None, device="cuda",
+                     stream=None):
+    """hbec_encode_md5_batch: parity of every object plus the MD5 of all k+m shards."""
+    n = enc.DataShards + enc.ParityShards
+    if len(views) != n:
+        raise ValueError("need k+m views")
+    if digests is None:
+        digests = _digest_tensor(n_objects, n, device)
+    check(N.lib().hbec_encode_md5_batch(enc.handle, _views(views), int(n_objects), int(shard_len),
+                                        C.c_void_p(digests.data_ptr()), _stream_ptr(stream)))
+    return digests
+
+
+def encode_objects_md5(enc: Encoder, objs, parity, shard_len: int, stream=None):
+    """encode_objects (batch.py) + ShardHash of every data and parity shard."""
+    views = shard_views(objs, enc.DataShards, shard_len) + shard_views(parity, enc.ParityShards, shard_len)
+    return encode_md5_views(enc, views, objs.shape[0], shard_len, device=objs.device, stream=stream)
+
+
+class MD5Chains:
+    """Streaming MD5 chains (hbec_md5_*): n_views x n_objects chains fed one
+    stripe's sub-chunks per update — a multi-stripe shard file's hash."""
+
+    def __init__(self, n_views: int, n_objects: int):
+        h = C.c_void_p()
+        check(N.lib().hbec_md5_new(int(n_views), int(n_objects), C.byref(h)))
+        self._h = h
+        self.n_views = n_views
+        self.n_objects = n_objects
+
+    def close(self):
+        if getattr(self, "_h", None):
+            N.lib().hbec_md5_free(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def update(self, views, length: int, stream=None):
+        if len(views) != self.n_views:
+            raise ValueError("need n_views views")
+        check(N.lib().hbec_md5_update(self._h, _views(views), int(length), _stream_ptr(stream)))
+
+    def final(self, digests=None, device="cuda", stream=None):
+        if digests is None:
+            digests = _digest_tensor(self.n_objects, self.n_views, device)
+        check(N.lib().hbec_md5_final(self._h, C.c_void_p(digests.data_ptr()), _stream_ptr(stream)))
+        return digests
+
+
+def hexdigests(digests):
+    """uint8 [..., 16] digests -> nested lists of hex strings (ShardHash form)."""
+    import numpy as np
+
+    a = np.ascontiguousarray(digests.cpu().numpy() if hasattr(digests, "cpu") else digests)
+    flat = a.reshape(-1, 16)
+    out = [bytes(r).hex() for r in flat]
+    shape = a.shape[:-1]
+    if len(shape) == 1:
+        return out
+    res, i = [], 0
+    for _ in range(shape[0]):
+        res.append(out[i:i + shape[1]])
+        i += shape[1]
+    return res

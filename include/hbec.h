@@ -112,6 +112,35 @@ int hbec_reconstruct_batch(hbec_codec* codec, const hbec_view* views, const uint
 int hbec_verify_batch(hbec_codec* codec, const hbec_view* views, uint64_t n_objects, uint64_t shard_len,
                       uint32_t* d_flags, void* hip_stream);
 
+/* ---------------------------------------------------------------------------
+ * ShardHash on the GPU.  The object server keys each stored shard by
+ * hex(MD5(shard body)) (objectserver/indexdb.go:746-753) and the auditor
+ * re-hashes shard files against it (objectserver/auditor.go:100-156).
+ * Digests are raw 16-byte MD5s in DEVICE memory: chain (object o, view v)
+ * at d_digests + (o * n_views + v) * 16 (4-byte aligned buffer).  One GPU
+ * lane per chain.
+ * ------------------------------------------------------------------------- */
+/* MD5 of len bytes of every view of every object (len may be 0). */
+int hbec_md5_batch(const hbec_view* views, int n_views, uint64_t n_objects, uint64_t len, uint8_t* d_digests,
+                   void* hip_stream);
+
+/* Streaming chains for multi-stripe shards (a shard file is the concatenation
+ * of its per-stripe sub-chunks, ecutils.go:55-69): n_views x n_objects chains
+ * fed any number of updates (every chain gets the same len per update), then
+ * final, which also resets the context for reuse.  One thread at a time. */
+typedef struct hbec_md5 hbec_md5;
+int hbec_md5_new(int n_views, uint64_t n_objects, hbec_md5** out);
+void hbec_md5_free(hbec_md5* ctx);
+int hbec_md5_update(hbec_md5* ctx, const hbec_view* views, uint64_t len, void* hip_stream);
+int hbec_md5_final(hbec_md5* ctx, uint8_t* d_digests, void* hip_stream);
+
+/* hbec_encode_batch + the MD5 of all k+m shards of every object (digest of
+ * shard i of object o at (o * (k+m) + i) * 16).  The hash of column segment s
+ * runs on a side stream while segment s+1 is encoded; the caller's stream
+ * waits for both. */
+int hbec_encode_md5_batch(hbec_codec* codec, const hbec_view* views, uint64_t n_objects, uint64_t shard_len,
+                          uint8_t* d_digests, void* hip_stream);
+
 /* The decode rows a reconstruct applies: survivors[0..k) (shard indices read),
  * outputs[0..*n_outputs) (shard indices written), rows[*n_outputs][k]. */
 int hbec_decode_rows(hbec_codec* codec, const uint8_t* present, int data_only, int* survivors, int* outputs,
@@ -196,6 +225,12 @@ int64_t hbec_ec_shard_length(int64_t length, int data_shards);
  * failing writer is dropped for the rest of the object, as in Go. */
 int hbec_ec_split(int data_shards, int parity_shards, hbec_read_fn read, void* fp, int chunk_size,
                   int64_t content_length, hbec_write_fn write, void* const* writers);
+
+/* ecSplit that also returns the ShardHash of everything written to each
+ * writer: shard_md5 (host) receives (k+m) raw 16-byte digests, shard i at
+ * i * 16 — what each receiving StablePut (indexdb.go:746-753) would compute. */
+int hbec_ec_split_md5(int data_shards, int parity_shards, hbec_read_fn read, void* fp, int chunk_size,
+                      int64_t content_length, hbec_write_fn write, void* const* writers, uint8_t* shard_md5);
 
 /* ecReconstruct (ecutils.go:74-132).  bodies: k+m reader contexts, NULL = nil. */
 int hbec_ec_reconstruct(int data_shards, int parity_shards, hbec_read_fn read, void* const* bodies, int chunk_size,

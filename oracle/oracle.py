@@ -27,6 +27,7 @@ plus the byte-level striping of the reference's own code:
 * ``ec_glue``          <- objectserver/ecutils.go:134-186
 * ``parse_ec_scheme``  <- objectserver/ecobj.go:82-98
 * ``range_chunk_align``<- objectserver/ecobj.go:814-824
+* ``shard_hash``       <- objectserver/indexdb.go:746-753 (hex MD5 of a shard body)
 
 Parity pinning
 --------------
@@ -279,6 +280,22 @@ class Encoder:
 # --------------------------------------------------------------------------
 # ecutils.go / ecobj.go byte semantics
 # --------------------------------------------------------------------------
+def shard_hash(body) -> str:
+    """StablePut's ShardHash (objectserver/indexdb.go:746-753): md5.New() fed
+    the whole shard body by common.Copy, hex.EncodeToString of the sum.  The
+    MD5 itself is Python's hashlib (RFC 1321), pinned by the RFC 1321 test
+    suite in tests/golden/kats.json."""
+    import hashlib
+
+    return hashlib.md5(bytes(body)).hexdigest()
+
+
+def ec_split_hashes(k: int, m: int, data: bytes, chunk_size: int) -> list[str]:
+    """ShardHash of every shard file ec_split produces (what the k+m receiving
+    StablePut calls compute, ecobj.go:756-774 -> indexdb.go:746-753)."""
+    return [shard_hash(f) for f in ec_split(k, m, data, chunk_size)]
+
+
 def ec_shard_length(length: int, data_shards: int) -> int:
     """objectserver/ecutils.go:14-24."""
     if length < 0:

@@ -42,6 +42,12 @@ for s in "$@"; do
     dist2) step dist2 600 env HBEC_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 10 --warmup 2 --objects 2048 ;;
     configs) step configs 600 python scripts/bench_configs.py ;;
     host) step host 600 python scripts/bench_host.py ;;
+    md5tests) step md5tests 600 python -m pytest tests/test_gpu_md5.py -q -x -p no:cacheprovider ;;
+    md5) step md5 600 python scripts/bench_md5.py ;;
+    md5prof)
+      mkdir -p "$OUT/md5prof"
+      (cd /tmp && step md5prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/md5prof" -o run -- python3 "$ROOT/scripts/bench_md5.py") || exit $?
+      ;;
     seq) step seq 600 python scripts/tune.py seq ;;
     xorsweep) step xorsweep 600 python scripts/tune.py xorsweep ;;
     copysweep) step copysweep 600 python scripts/tune.py copysweep ;;

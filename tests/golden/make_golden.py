@@ -55,6 +55,21 @@ def kats():
                             "err": ["1/2/16", "reedsolomon/1/2/X"]},
         # reference objectserver/ecobj_test.go:144-206: 7 bytes, 3+2 -> 3-byte shards
         "stabilize_lengths": {"body": "TESTING", "k": 3, "m": 2, "chunk": 100, "shard_len": 3},
+        # RFC 1321 appendix A.5 test suite (MD5, the ShardHash function)
+        "md5_rfc1321": [
+            ["", "d41d8cd98f00b204e9800998ecf8427e"],
+            ["a", "0cc175b9c0f1b6a831c399e269772661"],
+            ["abc", "900150983cd24fb0d6963f7d28e17f72"],
+            ["message digest", "f96b697d7cb7938d525a2f31aaf161d0"],
+            ["abcdefghijklmnopqrstuvwxyz", "c3fcd3d76192e4007dfb496cca67e13b"],
+            ["ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789", "d174ab98d277d9f5a5611c2c9f419d9f"],
+            ["1234567890" * 8, "57edf4a22be3c955ac49da2e2107b67a"],
+        ],
+        # reference objectserver/auditor_test.go:585-612: the ShardHash the
+        # auditor accepts for a shard file holding "testcontents", and rejects
+        # for "asdftestcontents"
+        "shard_hash": {"hash": "d3ac5112fe464b81184352ccba743001", "match": "testcontents",
+                       "mismatch": "asdftestcontents"},
     }
 
 
@@ -63,6 +78,10 @@ def vectors():
     # (2) TESTING 3+2
     files = O.ec_split(3, 2, b"TESTING", 100)
     v["testing_3_2"] = {"files": [list(f) for f in files]}
+    # (7) ShardHash of every shard file of a multi-stripe split (4+2, chunk 1 KiB)
+    body = bytes(O.object_bytes(3, 10000))
+    v["shard_hashes_4_2_chunk1k"] = {"object": 3, "len": 10000, "chunk": 1024,
+                                     "hashes": O.ec_split_hashes(4, 2, body, 1024)}
     # parity rows of the configs
     v["parity_rows"] = {f"{k}+{m}": O.Encoder(k, m).parity for k, m in [(2, 1), (3, 2), (4, 2), (8, 3), (10, 4)]}
     # (3) seeded objects: digests of every shard

@@ -188,3 +188,28 @@ def test_pure_c_client(tmp_path):
     out = subprocess.run([str(exe)], capture_output=True, text=True)
     assert out.returncode == 0, (out.returncode, out.stderr)
     assert "abi ok v1" in out.stdout
+
+
+def test_shardhash_validation_before_device():
+    """hbec_md5_* / ec_split_md5 argument checks answer without a GPU; the
+    hashing itself has no CPU fallback."""
+    L = N.lib()
+    v = (N.View * 1)()
+    v[0].base = 4096
+    dig = (C.c_uint8 * 64)()
+    assert L.hbec_md5_batch(None, 1, 1, 16, C.cast(dig, C.c_void_p), None) == N.ERR_INVALID_ARG
+    assert L.hbec_md5_batch(v, 0, 1, 16, C.cast(dig, C.c_void_p), None) == N.ERR_INVALID_ARG
+    assert L.hbec_md5_batch(v, 1, 1, 16, None, None) == N.ERR_INVALID_ARG
+    odd = C.c_void_p(C.addressof(dig) + 1)
+    assert L.hbec_md5_batch(v, 1, 1, 16, odd, None) == N.ERR_INVALID_ARG
+    assert "aligned" in N.last_error()
+    v[0].base = None
+    assert L.hbec_md5_batch(v, 1, 1, 16, C.cast(dig, C.c_void_p), None) == N.ERR_INVALID_ARG
+    h = C.c_void_p()
+    assert L.hbec_md5_new(0, 1, C.byref(h)) == N.ERR_INVALID_ARG
+    assert L.hbec_md5_update(None, v, 16, None) == N.ERR_INVALID_ARG
+    assert L.hbec_md5_final(None, C.cast(dig, C.c_void_p), None) == N.ERR_INVALID_ARG
+    enc = RS.New(4, 2)
+    assert L.hbec_encode_md5_batch(enc.handle, None, 1, 16, C.cast(dig, C.c_void_p), None) == N.ERR_INVALID_ARG
+    with pytest.raises(RS.ErrInvalidArg):
+        RS.check(L.hbec_ec_split_md5(4, 2, E._read_cb, None, 16, 0, E._write_cb, None, None))

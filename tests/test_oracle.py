@@ -163,3 +163,19 @@ def test_ec_reconstruct_oracle_roundtrip():
     assert out == [files[1], files[5]]
     assert O.ec_glue(4, 2, damaged, 1024, len(obj)) == obj
     assert io.BytesIO(obj).read() == obj
+
+
+def test_shard_hash_kats(kats):
+    """ShardHash oracle (indexdb.go:746-753) against RFC 1321's suite and the
+    reference auditor fixture (auditor_test.go:585-612)."""
+    for msg, want in kats["md5_rfc1321"]:
+        assert O.shard_hash(msg.encode()) == want
+    sh = kats["shard_hash"]
+    assert O.shard_hash(sh["match"].encode()) == sh["hash"]
+    assert O.shard_hash(sh["mismatch"].encode()) != sh["hash"]
+
+
+def test_shard_hash_vectors(vectors):
+    v = vectors["shard_hashes_4_2_chunk1k"]
+    body = bytes(O.object_bytes(v["object"], v["len"]))
+    assert O.ec_split_hashes(4, 2, body, v["chunk"]) == v["hashes"]
