@@ -13,7 +13,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdint>
+#include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <vector>
 
@@ -98,6 +101,32 @@ void side_stream_put(int dev, hipStream_t s) {
     g_side_free.emplace_back(dev, s);
 }
 
+// Library-owned stream-ordered memory pool per device for the per-call chain
+// state (the default pool returns memory to the driver at every sync, which
+// turned each call's hipMallocAsync into a real allocation).
+std::mutex g_pool_mu;
+std::map<int, hipMemPool_t> g_pools;
+
+int state_pool(int dev, hipMemPool_t* out) {
+    std::lock_guard<std::mutex> g(g_pool_mu);
+    auto it = g_pools.find(dev);
+    if (it == g_pools.end()) {
+        hipMemPoolProps props{};
+        props.allocType = hipMemAllocationTypePinned;
+        props.location.type = hipMemLocationTypeDevice;
+        props.location.id = dev;
+        hipMemPool_t pool;
+        hipError_t e = hipMemPoolCreate(&pool, &props);
+        if (e != hipSuccess) return hip_fail(e, "hipMemPoolCreate");
+        uint64_t keep = UINT64_MAX;
+        e = hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+        if (e != hipSuccess) return hip_fail(e, "hipMemPoolSetAttribute");
+        it = g_pools.emplace(dev, pool).first;
+    }
+    *out = it->second;
+    return HBEC_OK;
+}
+
 // Event-ordered "b waits for everything queued on a so far".
 int order_after(hipStream_t b, hipStream_t a) {
     hipEvent_t ev;
@@ -112,11 +141,23 @@ int order_after(hipStream_t b, hipStream_t a) {
 
 }  // namespace
 
-// Segment length for the encode/hash pipeline: ~8 segments, 4 KiB multiples
-// (whole MD5 blocks, whole encode tiles), none below 32 KiB.
-static uint64_t md5_segment(uint64_t shard_len) {
-    uint64_t seg = (shard_len / 8 + 4095) & ~uint64_t(4095);
-    return std::max<uint64_t>(seg, 32768);
+// Segment length for the encode/hash pipeline: ~n segments, 4 KiB multiples
+// (whole MD5 blocks, whole encode tiles), none below 16 KiB.  n = 8 for
+// k <= 4 and 1 (encode, then hash, one stream) above: the pipelined encode
+// kernels for k >= 5 hold most of a SIMD's register file (8+3: 506 of 512),
+// so co-resident MD5 waves block their launch and the overlap turns into
+// serialisation (profiles/r01_md5_sweep.jsonl: 8+3 pipelined 3.4 ms vs 2.45
+// sequential; 4+2 3.13 vs 3.87).  HBEC_MD5_SEGMENTS overrides n.
+static const int g_md5_segments = [] {
+    const char* e = std::getenv("HBEC_MD5_SEGMENTS");
+    return e ? std::max(1, std::atoi(e)) : 0;
+}();
+
+static uint64_t md5_segment(uint64_t shard_len, int k) {
+    const int n = g_md5_segments ? g_md5_segments : (k <= 4 ? 8 : 1);
+    if (n == 1) return shard_len;
+    uint64_t seg = (shard_len / (uint64_t)n + 4095) & ~uint64_t(4095);
+    return std::max<uint64_t>(seg, 16384);
 }
 
 }  // namespace hbec
@@ -203,7 +244,7 @@ int hbec_encode_md5_batch(hbec_codec* codec, const hbec_view* views, uint64_t n_
     rc = check_views(views, n, n_objects, shard_len);
     if (rc) return rc;
     hipStream_t main = static_cast<hipStream_t>(hip_stream);
-    const uint64_t seg = md5_segment(shard_len);
+    const uint64_t seg = md5_segment(shard_len, hbec_data_shards(codec));
     if (seg >= shard_len) {  // one segment: encode, then hash every shard
         rc = hbec_encode_batch(codec, views, n_objects, shard_len, hip_stream);
         if (rc) return rc;
@@ -212,9 +253,12 @@ int hbec_encode_md5_batch(hbec_codec* codec, const hbec_view* views, uint64_t n_
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+    hipMemPool_t pool;
+    rc = state_pool(dev, &pool);
+    if (rc) return rc;
     void* state = nullptr;
-    e = hipMallocAsync(&state, (size_t)n * n_objects * md5_state_bytes(), main);
-    if (e != hipSuccess) return hip_fail(e, "hipMallocAsync");
+    e = hipMallocFromPoolAsync(&state, (size_t)n * n_objects * md5_state_bytes(), pool, main);
+    if (e != hipSuccess) return hip_fail(e, "hipMallocFromPoolAsync");
     hipStream_t side;
     rc = side_stream_get(dev, &side);
     if (rc) {

@@ -135,9 +135,9 @@ int hbec_md5_update(hbec_md5* ctx, const hbec_view* views, uint64_t len, void* h
 int hbec_md5_final(hbec_md5* ctx, uint8_t* d_digests, void* hip_stream);
 
 /* hbec_encode_batch + the MD5 of all k+m shards of every object (digest of
- * shard i of object o at (o * (k+m) + i) * 16).  The hash of column segment s
- * runs on a side stream while segment s+1 is encoded; the caller's stream
- * waits for both. */
+ * shard i of object o at (o * (k+m) + i) * 16).  For k <= 4 the hash of
+ * column segment s runs on a side stream while segment s+1 is encoded; the
+ * caller's stream waits for both. */
 int hbec_encode_md5_batch(hbec_codec* codec, const hbec_view* views, uint64_t n_objects, uint64_t shard_len,
                           uint8_t* d_digests, void* hip_stream);
 

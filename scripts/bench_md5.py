@@ -32,7 +32,7 @@ from hummingbird_amd import reedsolomon as RS  # noqa: E402
 from hummingbird_amd import shardhash as H  # noqa: E402
 
 MiB = 1 << 20
-VALU_PER_BLOCK = 356  # md5_chains<true,4> main loop: ~340 VALU + 16 register moves per 64-B block
+VALU_PER_BLOCK = 340  # md5_chains<true,4> main loop: 339 VALU per 64-B block (ISA count)
 
 
 def timed(fn, reps=7):
@@ -95,8 +95,18 @@ def cpu_md5(seconds=3.0):
 
 
 def main():
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--label", default="")
+    args = ap.parse_args()
     torch.cuda.set_device(0)
-    for r in (config(4, 2), config(8, 3), cpu_md5()):
+    rows = [config(4, 2), config(8, 3)] + ([] if args.no_cpu else [cpu_md5()])
+    for r in rows:
+        if args.label:
+            r["label"] = args.label
+            r["segments"] = os.environ.get("HBEC_MD5_SEGMENTS", "8")
         print(json.dumps(r), flush=True)
 
 
