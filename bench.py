@@ -144,10 +144,19 @@ def cpu_baseline(k, m, obj_len, erased, budget_s=12.0, sample_objs=512):
             break
     assert np.array_equal(rebuilt, np.concatenate([objs[:, i * s:(i + 1) * s] for i in erased], axis=1))
     nbytes = passes * sample_objs * ((k + m) * s + (k + len(erased)) * s)
-    # config 1: one object through an ecSplit-shaped call, single thread
+    # single thread, same two ops, bounded (~2 s)
+    t1, p1 = 0.0, 0
+    while t1 < 2.0 and p1 < 2000:
+        t1 += CO.apply_batch(mat[k:], enc_in, enc_out, 32, s, 1)
+        t1 += CO.apply_batch(rows, rec_in, rec_out, 32, s, 1)
+        p1 += 1
+    single = p1 * 32 * ((k + m) * s + (k + len(erased)) * s) / t1 / GiB
+    # config 1: one object through an ecSplit-shaped call, single thread, with
+    # the per-call New + (k+m)*chunk alloc ecSplit does (ecutils.go:27,31-35)
+    # and kernel-only
     one = objs[0].copy()
-    reps = [CO.ecsplit_once(k, m, one, MiB, CO.AVX2, True) for _ in range(100)]
-    reps.sort()
+    reps = sorted(CO.ecsplit_once(k, m, one, MiB, CO.AVX2, True) for _ in range(100))
+    reps_k = sorted(CO.ecsplit_once(k, m, one, MiB, CO.AVX2, False) for _ in range(100))
     return {
         "value": round(nbytes / t_total / GiB, 3),
         "unit": "GiB/s",
@@ -156,7 +165,9 @@ def cpu_baseline(k, m, obj_len, erased, budget_s=12.0, sample_objs=512):
         "sample": f"{passes} passes x {sample_objs} x 1 MiB objects, encode + reconstruct{{{','.join(map(str, erased))}}}, "
                   f"{t_total:.1f} s wall, AVX2 nibble-table port of klauspost galMulAVX2Xor "
                   f"(oracle/gf_oracle.c), {threads} threads, {cpu_model()}",
+        "single_thread_GiB_s": round(single, 3),
         "config1_ecsplit_1mib_single_thread_ms": round(reps[len(reps) // 2] * 1e3, 4),
+        "config1_kernel_only_single_thread_ms": round(reps_k[len(reps_k) // 2] * 1e3, 4),
     }
 
 

@@ -6,7 +6,7 @@
   config 4: 8+3 encode + reconstruct{0,1,2}, 4096 objects of 4 KiB or 1 MiB
             (p = 0.5 each, drawn by splitmix64(seed) per index; one launch per
             op through a stripe plan)
-  extra   : 8+3 @ 1 MiB uniform (strided views)
+  extra   : 8+3 @ 1 MiB uniform (strided views); Verify of both uniform configs
 
 Algorithmic bytes per object: encode (k+m)*S, reconstruct (k+e)*S.
 Prints one JSON line per measurement (GiB/s, GB/s and fraction of 8 TB/s).
@@ -68,6 +68,17 @@ def uniform(k, m, n, size, patterns):
     idx = [0, n // 2, n - 1]
     want, _ = CO.encode_batch(k, m, objs[idx].cpu().numpy(), threads=CO.cpu_threads())
     assert np.array_equal(par[idx].cpu().numpy(), want)
+    # Verify (read-only: k+m shards read per object, one flag word written)
+    flags = torch.zeros(n, dtype=torch.int32, device="cuda")
+    ms = timeit(lambda: B.verify_views(enc, views, n, s, flags))
+    assert int(flags.sum()) == 0
+    par[n // 3, 5] ^= 1
+    flags.zero_()
+    B.verify_views(enc, views, n, s, flags)
+    torch.cuda.synchronize()
+    assert flags.nonzero().flatten().tolist() == [n // 3]
+    par[n // 3, 5] ^= 1
+    line(f"{k}+{m} verify {n}x{size}", n * (k + m) * s, ms, bound="HBM read")
     for miss in patterns:
         out = torch.empty((n, len(miss) * s), dtype=torch.uint8, device="cuda")
         rv = list(views)
