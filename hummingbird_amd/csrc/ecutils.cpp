@@ -1,5 +1,6 @@
 // ecutils.cpp — the stripe loops of objectserver/ecutils.go over C io callbacks,
-// with every GF step on the GPU codec (hbec_encode / hbec_reconstruct).
+// with every GF step on the GPU, pipelined: stripe i+1 is read while stripe i
+// is on the GPU (pinned two-slot ring, see Ring below).
 //
 //   hbec_ec_shard_length  <- ecShardLength   ecutils.go:14-24
 //   hbec_ec_split         <- ecSplit         ecutils.go:26-72
@@ -20,7 +21,9 @@
 #include <climits>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -55,19 +58,6 @@ struct CodecHolder {
     ~CodecHolder() { hbec_free(c); }
 };
 
-// Device side of ecSplit with hashing: one stripe buffer (k+m shards) plus the
-// digests, a private stream, and the per-shard MD5 chains.
-struct DeviceStripe {
-    hipStream_t stream = nullptr;
-    uint8_t* buf = nullptr;
-    hbec_md5* md5 = nullptr;
-    ~DeviceStripe() {
-        hbec_md5_free(md5);
-        if (buf) hipFree(buf);
-        if (stream) hipStreamDestroy(stream);
-    }
-};
-
 // ecReconstruct / ecGlue per-stripe shard size (ecutils.go:86-92, :144-150)
 int64_t stripe_shard_size(int k, int chunk, int64_t remaining) {
     int64_t s = chunk;
@@ -76,6 +66,185 @@ int64_t stripe_shard_size(int k, int chunk, int64_t remaining) {
         if (remaining % k != 0) ++s;
     }
     return s;
+}
+
+
+// ---------------------------------------------------------------------------
+// Two-slot stripe ring: pinned host stripe buffers (the Go loops' databuf),
+// device stripe buffers, one stream, one event per slot.  Pooled per device
+// (the stripe loops run once per object; pinned allocation is expensive).
+// The loops below read stripe i+1 from the callbacks while stripe i's H2D,
+// kernel and D2H run, then write stripe i: GPU time hides under the I/O.
+// Callers see the Go loop's write sequence; the one visible difference is
+// that stripe i+1 is read before stripe i is written.
+// ---------------------------------------------------------------------------
+struct Ring {
+    int dev = 0;
+    size_t host_bytes = 0, dev_bytes = 0;
+    hipStream_t stream = nullptr;
+    uint8_t* host[2] = {nullptr, nullptr};
+    uint8_t* dbuf[2] = {nullptr, nullptr};
+    uint8_t* digests = nullptr;  // 16 B x 256 chains
+    hipEvent_t ev[2] = {nullptr, nullptr};
+};
+
+std::mutex g_ring_mu;
+std::vector<Ring*> g_rings;
+constexpr size_t kMaxPooledRings = 8;
+
+void ring_destroy(Ring* r) {
+    for (int i = 0; i < 2; ++i) {
+        if (r->host[i]) (void)hipHostFree(r->host[i]);
+        if (r->dbuf[i]) (void)hipFree(r->dbuf[i]);
+        if (r->ev[i]) (void)hipEventDestroy(r->ev[i]);
+    }
+    if (r->digests) (void)hipFree(r->digests);
+    if (r->stream) (void)hipStreamDestroy(r->stream);
+    delete r;
+}
+
+int ring_acquire(size_t host_bytes, size_t dev_bytes, Ring** out) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return hbec::hip_fail(e, "hipGetDevice");
+    {
+        std::lock_guard<std::mutex> g(g_ring_mu);
+        for (size_t i = 0; i < g_rings.size(); ++i) {
+            Ring* r = g_rings[i];
+            if (r->dev == dev && r->host_bytes >= host_bytes && r->dev_bytes >= dev_bytes) {
+                g_rings.erase(g_rings.begin() + (long)i);
+                *out = r;
+                return HBEC_OK;
+            }
+        }
+    }
+    std::unique_ptr<Ring> r(new (std::nothrow) Ring());
+    if (!r) return fail(HBEC_ERR_NOMEM, "stripe ring");
+    r->dev = dev;
+    r->host_bytes = std::max<size_t>(host_bytes, 1);
+    r->dev_bytes = std::max<size_t>(dev_bytes, 16);
+    e = hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking);
+    for (int i = 0; i < 2 && e == hipSuccess; ++i) {
+        e = hipHostMalloc(reinterpret_cast<void**>(&r->host[i]), r->host_bytes, hipHostMallocDefault);
+        if (e == hipSuccess) e = hipMalloc(&r->dbuf[i], r->dev_bytes);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&r->ev[i], hipEventDisableTiming);
+    }
+    if (e == hipSuccess) e = hipMalloc(&r->digests, 16 * 256);
+    if (e != hipSuccess) {
+        ring_destroy(r.release());
+        return e == hipErrorOutOfMemory ? fail(HBEC_ERR_NOMEM, "stripe ring") : hbec::hip_fail(e, "stripe ring");
+    }
+    *out = r.release();
+    return HBEC_OK;
+}
+
+void ring_release(Ring* r) {
+    std::lock_guard<std::mutex> g(g_ring_mu);
+    if (g_rings.size() >= kMaxPooledRings) {
+        ring_destroy(g_rings.front());
+        g_rings.erase(g_rings.begin());
+    }
+    g_rings.push_back(r);
+}
+
+struct RingHolder {
+    Ring* r = nullptr;
+    ~RingHolder() {
+        if (r) {
+            (void)hipStreamSynchronize(r->stream);  // nothing of ours still in flight
+            ring_release(r);
+        }
+    }
+};
+
+uint64_t round16(uint64_t v) { return (v + 15) & ~uint64_t(15); }
+
+// Device slot layout for a stripe of n shards of s bytes: shard i at i * pad,
+// pad = s when 16-aligned (one contiguous copy each way), else round16(s)
+// (per-shard copies; the vector kernels then run over pad bytes, whose tail
+// is never copied back).
+struct SlotLayout {
+    uint64_t s = 0, pad = 0;
+    bool contiguous() const { return pad == s; }
+};
+
+SlotLayout layout_for(uint64_t s) { return SlotLayout{s, (s % 16) == 0 ? s : round16(s)}; }
+
+// H2D of shards [lo, hi) of a host stripe (shard i at host + i*s) into device
+// slot b's layout.
+hipError_t upload(const Ring& r, int b, const uint8_t* host, const SlotLayout& L, int lo, int hi) {
+    if (hi <= lo) return hipSuccess;
+    if (L.contiguous())
+        return hipMemcpyAsync(r.dbuf[b] + (size_t)lo * L.s, host + (size_t)lo * L.s, (size_t)(hi - lo) * L.s,
+                              hipMemcpyHostToDevice, r.stream);
+    for (int i = lo; i < hi; ++i) {
+        hipError_t e = hipMemcpyAsync(r.dbuf[b] + (size_t)i * L.pad, host + (size_t)i * L.s, L.s,
+                                      hipMemcpyHostToDevice, r.stream);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+hipError_t download(const Ring& r, int b, uint8_t* host, const SlotLayout& L, int i) {
+    return hipMemcpyAsync(host + (size_t)i * L.s, r.dbuf[b] + (size_t)i * L.pad, L.s, hipMemcpyDeviceToHost,
+                          r.stream);
+}
+
+// Host stripe buffers for the loops: pageable (Go's databuf) until the first
+// stripe that needs the GPU acquires the ring, pinned ring buffers after that.
+// So a healthy ecGlue never touches the GPU, and read errors come first, as
+// in Go, even on a host without one.
+struct HostBufs {
+    size_t bytes = 0;
+    std::vector<uint8_t> pageable[2];
+    uint8_t* get(const Ring* r, int b) {
+        if (r) return r->host[b];
+        if (pageable[b].size() < bytes) pageable[b].resize(bytes);
+        return pageable[b].data();
+    }
+};
+
+void device_views(const Ring& r, int b, const SlotLayout& L, int n, std::vector<hbec_view>& v) {
+    v.resize((size_t)n);
+    for (int i = 0; i < n; ++i) v[i] = hbec_view{r.dbuf[b] + (size_t)i * L.pad, 0};
+}
+
+// Queue a reconstruct of one stripe in slot b: survivors up, rebuilt shards
+// down.  present[i] = 1 for shards read.  Returns the shard indices written.
+int queue_reconstruct(hbec_codec* c, const Ring& r, int b, uint8_t* host, const SlotLayout& L,
+                      const std::vector<uint8_t>& present, int data_only, std::vector<int>& outputs) {
+    const int k = hbec_data_shards(c), n = k + hbec_parity_shards(c);
+    std::vector<int> surv((size_t)k), outs((size_t)n);
+    std::vector<uint8_t> rows((size_t)n * k);
+    int n_out = 0;
+    int rc = hbec_decode_rows(c, present.data(), data_only, surv.data(), outs.data(), &n_out, rows.data());
+    if (rc) return rc;
+    outputs.assign(outs.begin(), outs.begin() + n_out);
+    if (n_out == 0) return HBEC_OK;
+    hipError_t e = hipSuccess;
+    if (L.contiguous()) {
+        e = upload(r, b, host, L, surv.front(), surv.back() + 1);  // one copy over the survivors' span
+    } else {
+        for (int j = 0; j < k && e == hipSuccess; ++j) e = upload(r, b, host, L, surv[j], surv[j] + 1);
+    }
+    if (e != hipSuccess) return hbec::hip_fail(e, "stripe upload");
+    std::vector<hbec_view> v;
+    device_views(r, b, L, n, v);
+    rc = hbec_reconstruct_batch(c, v.data(), present.data(), 1, L.pad, data_only, r.stream);
+    if (rc) return rc;
+    for (int o : outputs) {
+        e = download(r, b, host, L, o);
+        if (e != hipSuccess) return hbec::hip_fail(e, "stripe download");
+    }
+    e = hipEventRecord(r.ev[b], r.stream);
+    if (e != hipSuccess) return hbec::hip_fail(e, "hipEventRecord");
+    return HBEC_OK;
+}
+
+int wait_slot(const Ring& r, int b) {
+    hipError_t e = hipEventSynchronize(r.ev[b]);
+    if (e != hipSuccess) return hbec::hip_fail(e, "stripe wait");
+    return HBEC_OK;
 }
 
 }  // namespace
@@ -91,6 +260,8 @@ int64_t hbec_ec_shard_length(int64_t length, int data_shards) {
     return s;
 }
 
+// ecSplit (ecutils.go:26-72), optionally hashing every shard (ShardHash,
+// indexdb.go:746-753) on the GPU while the stripe is resident.
 static int ec_split(int k, int m, hbec_read_fn read, void* fp, int chunk_size, int64_t content_length,
                     hbec_write_fn write, void* const* writers, uint8_t* shard_md5) {
     CodecHolder enc;
@@ -98,63 +269,91 @@ static int ec_split(int k, int m, hbec_read_fn read, void* fp, int chunk_size, i
     if (rc) return rc;
     if (!read || chunk_size < 0) return fail(HBEC_ERR_INVALID_ARG, "ecSplit: bad arguments");
     const int n = k + m;
-    // databuf := make([]byte, (k+m)*chunkSize)   (ecutils.go:32)
-    std::vector<uint8_t> databuf((size_t)n * (size_t)chunk_size);
-    std::vector<uint8_t*> shards(n);
-    std::vector<size_t> lens(n);
+    if (shard_md5 && n > 256) return fail(HBEC_ERR_INVALID_ARG, "ecSplit: too many shards to hash");
     std::vector<char> failed(n, 0);
-    std::vector<hbec_view> views(n);
-    DeviceStripe dev;
-    if (shard_md5) {
-        hipError_t e = hipStreamCreateWithFlags(&dev.stream, hipStreamNonBlocking);
-        if (e == hipSuccess) e = hipMalloc(&dev.buf, 16u * (size_t)n + databuf.size());  // digests, then stripe
-        if (e != hipSuccess) return hbec::hip_fail(e, "ecSplit device buffers");
-        rc = hbec_md5_new(n, 1, &dev.md5);
-        if (rc) return rc;
-    }
+    struct Pending {
+        bool live = false;
+        uint8_t* host = nullptr;
+        uint64_t s = 0;
+    } pend[2];
+    RingHolder ring;
+    HostBufs bufs;
+    bufs.bytes = (size_t)n * (size_t)chunk_size;  // databuf := make([]byte, (k+m)*chunkSize)  (ecutils.go:32)
+    hbec_md5* md5 = nullptr;
+    struct Md5Holder {
+        hbec_md5*& p;
+        ~Md5Holder() { hbec_md5_free(p); }
+    } md5_holder{md5};
+    auto ensure_ring = [&]() -> int {
+        if (ring.r) return HBEC_OK;
+        int r2 = ring_acquire(bufs.bytes, (size_t)n * round16((uint64_t)chunk_size), &ring.r);
+        if (r2 == HBEC_OK && shard_md5) r2 = hbec_md5_new(n, 1, &md5);
+        return r2;
+    };
+    // write one finished stripe (ecutils.go:62-69): a failing writer is dropped
+    auto flush = [&](int b) -> int {
+        if (!pend[b].live) return HBEC_OK;
+        pend[b].live = false;
+        int r2 = wait_slot(*ring.r, b);
+        if (r2) return r2;
+        const uint64_t s = pend[b].s;
+        for (int i = 0; i < n; ++i)
+            if (writers && writers[i] && !failed[i])
+                if (!write || write(writers[i], pend[b].host + (size_t)i * s, s) != 0) failed[i] = 1;
+        return HBEC_OK;
+    };
     int64_t total = 0;
+    int b = 0;
+    std::vector<hbec_view> v;
     while (total < content_length) {
+        uint8_t* databuf = bufs.get(ring.r, b);
         int64_t expected = (int64_t)k * chunk_size;
         if (content_length - total < expected) expected = content_length - total;
         size_t got = 0;
-        ReadStatus st = read_full(read, fp, databuf.data(), (size_t)expected, &got);
-        if (st == READ_ERR) return fail(HBEC_ERR_IO, "ecSplit: read failed");
-        if (st == READ_UNEXPECTED_EOF) return fail(HBEC_ERR_UNEXPECTED_EOF, "ecSplit: unexpected EOF");
-        if (got == 0) return fail(HBEC_ERR_UNEXPECTED_EOF, "ecSplit: unexpected EOF");
+        ReadStatus st = read_full(read, fp, databuf, (size_t)expected, &got);
+        if (st == READ_ERR || st == READ_UNEXPECTED_EOF || got == 0) {
+            const int r2 = flush(b ^ 1);  // the Go loop wrote the previous stripe before this read
+            if (r2) return r2;
+            if (st == READ_ERR) return fail(HBEC_ERR_IO, "ecSplit: read failed");
+            return fail(HBEC_ERR_UNEXPECTED_EOF, "ecSplit: unexpected EOF");
+        }
         total += (int64_t)got;
         while (got % (size_t)k != 0) databuf[got++] = 0;  // zero pad (ecutils.go:51-54)
-        const size_t s = got / (size_t)k;
-        for (int i = 0; i < n; ++i) {
-            shards[i] = databuf.data() + (size_t)i * s;
-            lens[i] = s;
-        }
-        if (!shard_md5) {
-            rc = hbec_encode(enc.c, shards.data(), lens.data(), n);
-            if (rc) return rc;
-        } else {  // stripe to the GPU, encode and hash there, parity back
-            uint8_t* d_stripe = dev.buf + 16u * (size_t)n;
-            for (int i = 0; i < n; ++i) views[i] = hbec_view{d_stripe + (size_t)i * s, 0};
-            hipError_t e = hipMemcpyAsync(d_stripe, databuf.data(), (size_t)k * s, hipMemcpyHostToDevice, dev.stream);
-            if (e != hipSuccess) return hbec::hip_fail(e, "ecSplit H2D");
-            rc = hbec_encode_batch(enc.c, views.data(), 1, s, dev.stream);
-            if (!rc) rc = hbec_md5_update(dev.md5, views.data(), s, dev.stream);
-            if (rc) return rc;
-            e = hipMemcpyAsync(shards[k], d_stripe + (size_t)k * s, (size_t)m * s, hipMemcpyDeviceToHost, dev.stream);
-            if (e == hipSuccess) e = hipStreamSynchronize(dev.stream);
-            if (e != hipSuccess) return hbec::hip_fail(e, "ecSplit D2H");
-        }
-        for (int i = 0; i < n; ++i) {
-            if (writers && writers[i] && !failed[i]) {
-                if (!write || write(writers[i], shards[i], s) != 0) failed[i] = 1;
-            }
-        }
-    }
-    if (shard_md5) {
-        uint8_t* d_dig = dev.buf;
-        rc = hbec_md5_final(dev.md5, d_dig, dev.stream);
+        rc = ensure_ring();
         if (rc) return rc;
-        hipError_t e = hipMemcpyAsync(shard_md5, d_dig, 16u * (size_t)n, hipMemcpyDeviceToHost, dev.stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(dev.stream);
+        const SlotLayout L = layout_for(got / (size_t)k);
+        hipError_t e = upload(*ring.r, b, databuf, L, 0, k);
+        if (e != hipSuccess) return hbec::hip_fail(e, "ecSplit upload");
+        device_views(*ring.r, b, L, n, v);
+        rc = hbec_encode_batch(enc.c, v.data(), 1, L.pad, ring.r->stream);
+        if (rc) return rc;
+        if (md5) {
+            rc = hbec_md5_update(md5, v.data(), L.s, ring.r->stream);
+            if (rc) return rc;
+        }
+        if (L.contiguous()) {
+            e = hipMemcpyAsync(databuf + (size_t)k * L.s, ring.r->dbuf[b] + (size_t)k * L.s, (size_t)m * L.s,
+                               hipMemcpyDeviceToHost, ring.r->stream);
+        } else {
+            for (int r = 0; r < m && e == hipSuccess; ++r) e = download(*ring.r, b, databuf, L, k + r);
+        }
+        if (e == hipSuccess) e = hipEventRecord(ring.r->ev[b], ring.r->stream);
+        if (e != hipSuccess) return hbec::hip_fail(e, "ecSplit download");
+        pend[b] = Pending{true, databuf, L.s};
+        rc = flush(b ^ 1);  // previous stripe: write it while this one is on the GPU
+        if (rc) return rc;
+        b ^= 1;
+    }
+    rc = flush(b ^ 1);
+    if (rc) return rc;
+    if (shard_md5) {
+        rc = ensure_ring();  // zero-length object: hash of every (empty) shard
+        if (rc) return rc;
+        rc = hbec_md5_final(md5, ring.r->digests, ring.r->stream);
+        if (rc) return rc;
+        hipError_t e = hipMemcpyAsync(shard_md5, ring.r->digests, 16u * (size_t)n, hipMemcpyDeviceToHost,
+                                      ring.r->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(ring.r->stream);
         if (e != hipSuccess) return hbec::hip_fail(e, "ecSplit digests");
     }
     return HBEC_OK;
@@ -171,6 +370,7 @@ int hbec_ec_split_md5(int k, int m, hbec_read_fn read, void* fp, int chunk_size,
     return ec_split(k, m, read, fp, chunk_size, content_length, write, writers, shard_md5);
 }
 
+// ecReconstruct (ecutils.go:74-132).
 int hbec_ec_reconstruct(int k, int m, hbec_read_fn read, void* const* bodies, int chunk_size,
                         int64_t content_length, hbec_write_fn write, void* const* dsts, const int* dst_chunk_num,
                         int n_dsts) {
@@ -183,38 +383,70 @@ int hbec_ec_reconstruct(int k, int m, hbec_read_fn read, void* const* bodies, in
     for (int i = 0; i < n_dsts; ++i)
         if (dst_chunk_num[i] < 0 || dst_chunk_num[i] >= n)
             return fail(HBEC_ERR_INVALID_ARG, "ecReconstruct: chunk number out of range");
-    std::vector<uint8_t> databuf((size_t)n * (size_t)chunk_size);
-    std::vector<uint8_t*> data(n);
-    std::vector<size_t> lens(n);
+    struct Pending {
+        bool live = false, gpu = false;
+        uint8_t* host = nullptr;
+        uint64_t s = 0;
+    } pend[2];
+    RingHolder ring;
+    HostBufs bufs;
+    bufs.bytes = (size_t)n * (size_t)chunk_size;
+    auto flush = [&](int b) -> int {
+        if (!pend[b].live) return HBEC_OK;
+        pend[b].live = false;
+        if (pend[b].gpu) {
+            int r2 = wait_slot(*ring.r, b);
+            if (r2) return r2;
+        }
+        const uint64_t s = pend[b].s;
+        for (int i = 0; i < n_dsts; ++i)  // ecutils.go:115-120
+            if (write(dsts[i], pend[b].host + (size_t)dst_chunk_num[i] * s, s) != 0)
+                return fail(HBEC_ERR_IO, "ecReconstruct: write failed");
+        return HBEC_OK;
+    };
+    std::vector<uint8_t> present((size_t)n);
+    std::vector<int> outputs;
     int64_t total = 0;
+    int b = 0;
     while (total < content_length) {
         const int64_t exp = stripe_shard_size(k, chunk_size, content_length - total);
         if (exp <= 0) return fail(HBEC_ERR_INVALID_ARG, "ecReconstruct: chunk size is zero");
-        for (int i = 0; i < n; ++i) {
-            data[i] = databuf.data() + (size_t)i * (size_t)exp;
-            lens[i] = bodies[i] ? (size_t)exp : 0;
-        }
-        for (int i = 0; i < n; ++i) {
+        uint8_t* databuf = bufs.get(ring.r, b);
+        int n_present = 0;
+        for (int i = 0; i < n; ++i) {  // a failed read is missing for this stripe only (ecutils.go:103-109)
+            present[i] = 0;
             if (bodies[i]) {
                 size_t got = 0;
-                if (!read || read_full(read, bodies[i], data[i], (size_t)exp, &got) != READ_OK) lens[i] = 0;
+                if (read && read_full(read, bodies[i], databuf + (size_t)i * exp, (size_t)exp, &got) == READ_OK)
+                    present[i] = 1;
             }
+            n_present += present[i];
         }
-        rc = hbec_reconstruct(enc.c, data.data(), lens.data(), n, 0);
-        if (rc) return rc;
-        for (int i = 0; i < n_dsts; ++i) {
-            const int c = dst_chunk_num[i];
-            if (write(dsts[i], data[c], lens[c]) != 0) return fail(HBEC_ERR_IO, "ecReconstruct: write failed");
+        const SlotLayout L = layout_for((uint64_t)exp);
+        bool gpu = false;
+        if (n_present < n) {  // Reconstruct (ecutils.go:111) is a no-op when nothing is missing
+            if (!ring.r) rc = ring_acquire(bufs.bytes, (size_t)n * round16((uint64_t)chunk_size), &ring.r);
+            if (!rc) rc = queue_reconstruct(enc.c, *ring.r, b, databuf, L, present, 0, outputs);
+            if (rc) {
+                const int r2 = flush(b ^ 1);
+                return r2 ? r2 : rc;
+            }
+            gpu = !outputs.empty();
         }
-        for (int i = 0; i < k; ++i) {
-            int64_t dl = (int64_t)lens[i];
+        pend[b] = Pending{true, gpu, databuf, L.s};
+        for (int i = 0; i < k; ++i) {  // every data shard now has exp bytes
+            int64_t dl = exp;
             if (content_length - total < dl) dl = content_length - total;
             total += dl;
         }
+        rc = flush(b ^ 1);
+        if (rc) return rc;
+        b ^= 1;
     }
-    return HBEC_OK;
+    return flush(b ^ 1);
 }
 
+// ecGlue (ecutils.go:134-186): healthy stripes never touch the GPU.
 int hbec_ec_glue(int k, int m, hbec_read_fn read, void* const* bodies, int chunk_size, int64_t content_length,
                  hbec_write_fn write, void* const* dsts, int n_dsts) {
     CodecHolder enc;
@@ -224,41 +456,80 @@ int hbec_ec_glue(int k, int m, hbec_read_fn read, void* const* bodies, int chunk
     if (!bodies || chunk_size < 0 || n_dsts < 0 || (n_dsts > 0 && !dsts))
         return fail(HBEC_ERR_INVALID_ARG, "ecGlue: bad arguments");
     std::vector<void*> live(dsts, dsts + n_dsts);
-    std::vector<uint8_t> databuf((size_t)n * (size_t)chunk_size);
-    std::vector<uint8_t*> data(n);
-    std::vector<size_t> lens(n);
     std::vector<char> failed(n, 0);
+    struct Pending {
+        bool live = false, gpu = false;
+        uint8_t* host = nullptr;
+        uint64_t s = 0;
+        int64_t remaining = 0;  // object bytes left when this stripe was read
+    } pend[2];
+    RingHolder ring;
+    HostBufs bufs;
+    bufs.bytes = (size_t)n * (size_t)chunk_size;
+    auto flush = [&](int b) -> int {
+        if (!pend[b].live) return HBEC_OK;
+        pend[b].live = false;
+        if (pend[b].gpu) {
+            int r2 = wait_slot(*ring.r, b);
+            if (r2) return r2;
+        }
+        const uint64_t s = pend[b].s;
+        int64_t remaining = pend[b].remaining;
+        for (int i = 0; i < k; ++i) {  // data shards, the last truncated (ecutils.go:171-183)
+            size_t len = (size_t)s;
+            if (remaining < (int64_t)len) len = (size_t)remaining;
+            for (int j = 0; j < n_dsts; ++j)
+                if (live[j] && (!write || write(live[j], pend[b].host + (size_t)i * s, len) != 0)) live[j] = nullptr;
+            remaining -= (int64_t)len;
+        }
+        return HBEC_OK;
+    };
+    std::vector<uint8_t> present((size_t)n);
+    std::vector<int> outputs;
     int64_t written = 0;
+    int b = 0;
     while (written < content_length) {
         const int64_t exp = stripe_shard_size(k, chunk_size, content_length - written);
         if (exp <= 0) return fail(HBEC_ERR_INVALID_ARG, "ecGlue: chunk size is zero");
-        for (int i = 0; i < n; ++i) {
-            data[i] = databuf.data() + (size_t)i * (size_t)exp;
-            lens[i] = (bodies[i] && !failed[i]) ? (size_t)exp : 0;
-        }
-        for (int i = 0; i < n; ++i) {
+        uint8_t* databuf = bufs.get(ring.r, b);
+        bool data_missing = false;
+        for (int i = 0; i < n; ++i) {  // a failed body stays failed (ecutils.go:152-163)
+            present[i] = 0;
             if (bodies[i] && !failed[i]) {
                 size_t got = 0;
-                if (!read || read_full(read, bodies[i], data[i], (size_t)exp, &got) != READ_OK) {
-                    lens[i] = 0;
+                if (read && read_full(read, bodies[i], databuf + (size_t)i * exp, (size_t)exp, &got) == READ_OK)
+                    present[i] = 1;
+                else
                     failed[i] = 1;
-                }
             }
+            if (i < k && !present[i]) data_missing = true;
         }
-        rc = hbec_reconstruct(enc.c, data.data(), lens.data(), n, 1);
-        if (rc) return rc;
+        const SlotLayout L = layout_for((uint64_t)exp);
+        bool gpu = false;
+        if (data_missing) {  // ReconstructData (ecutils.go:168)
+            if (!ring.r) rc = ring_acquire(bufs.bytes, (size_t)n * round16((uint64_t)chunk_size), &ring.r);
+            if (!rc) rc = queue_reconstruct(enc.c, *ring.r, b, databuf, L, present, 1, outputs);
+            if (rc) {
+                const int r2 = flush(b ^ 1);
+                return r2 ? r2 : rc;
+            }
+            gpu = !outputs.empty();
+        }
+        pend[b].live = true;
+        pend[b].gpu = gpu;
+        pend[b].host = databuf;
+        pend[b].s = L.s;
+        pend[b].remaining = content_length - written;
         for (int i = 0; i < k; ++i) {
-            size_t len = lens[i];
-            if (content_length - written < (int64_t)len) len = (size_t)(content_length - written);
-            for (int j = 0; j < n_dsts; ++j) {
-                if (live[j]) {
-                    if (!write || write(live[j], data[i], len) != 0) live[j] = nullptr;
-                }
-            }
-            written += (int64_t)len;
+            int64_t len = exp;
+            if (content_length - written < len) len = content_length - written;
+            written += len;
         }
+        rc = flush(b ^ 1);
+        if (rc) return rc;
+        b ^= 1;
     }
-    return HBEC_OK;
+    return flush(b ^ 1);
 }
 
 int hbec_parse_ec_scheme(const char* scheme, char* algo, size_t algo_cap, int* data_shards, int* parity_shards,

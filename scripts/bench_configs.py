@@ -93,6 +93,19 @@ def uniform(k, m, n, size, patterns):
         line(f"{k}+{m} reconstruct{set(miss)} {n}x{size}", n * (k + len(miss)) * s, ms)
 
 
+def uniform_plan(k, m, n, size):
+    """Uniform stripes through a stripe plan (gf_apply_stripes) instead of
+    strided views (gf_apply_vec_pipe): isolates the plan kernel's own cost
+    from config 4's size mix."""
+    s = size // k
+    pool = torch.empty((n, (k + m) * s), dtype=torch.uint8, device="cuda")
+    B.fill_splitmix(pool, (k + m) * s)
+    enc = RS.New(k, m)
+    plan = B.StripePlan(enc, [(pool.data_ptr() + i * pool.stride(0), s) for i in range(n)])
+    ms = timeit(plan.encode)
+    line(f"{k}+{m} encode {n}x{size} (plan, uniform)", n * (k + m) * s, ms, plan=plan.info())
+
+
 def mixed_8_3(n=4096):
     k, m = 8, 3
     flags = O.splitmix_bytes(O.HBEC_SEED, n)
@@ -134,6 +147,8 @@ def main():
     torch.cuda.set_device(0)
     uniform(4, 2, 4096, MiB, [(0, 1), (0, 4), (4, 5), (2, 3)])
     uniform(8, 3, 4096, MiB, [(0, 1, 2)])
+    uniform_plan(4, 2, 4096, MiB)
+    uniform_plan(8, 3, 4096, MiB)
     mixed_8_3()
 
 

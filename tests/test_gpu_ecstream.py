@@ -1,0 +1,180 @@
+"""The pipelined stripe loops (csrc/ecutils.cpp): stripe i+1 is read while
+stripe i is on the GPU, so these check what a caller of ecutils.go can
+observe across many stripes — output bytes, the sequence of writes, and the
+error paths — against the oracle's restatement of ecutils.go:26-186.
+"""
+import io
+
+import numpy as np
+import pytest
+import torch
+
+from hummingbird_amd import ecutils as E
+from hummingbird_amd import reedsolomon as RS
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    yield
+
+
+class Rec:
+    """Writer recording each write call separately."""
+
+    def __init__(self):
+        self.calls = []
+
+    def write(self, b):
+        self.calls.append(bytes(b))
+
+    def value(self):
+        return b"".join(self.calls)
+
+
+class FailingReader:
+    """Reads from a bytes body; raises once `fail_at` bytes have been served."""
+
+    def __init__(self, data, fail_at=None):
+        self.f = io.BytesIO(data)
+        self.fail_at = fail_at
+        self.served = 0
+
+    def read(self, n):
+        if self.fail_at is not None and self.served >= self.fail_at:
+            raise IOError("body broke")
+        if self.fail_at is not None:
+            n = min(n, self.fail_at - self.served)
+        b = self.f.read(n)
+        self.served += len(b)
+        return b
+
+
+@pytest.mark.parametrize("k,m,chunk,length", [(4, 2, 1024, 40_000), (8, 3, 4096, 300_001), (3, 2, 1000, 7),
+                                              (4, 2, 65536, 4 * 65536 * 5), (10, 4, 1003, 51_234)])
+def test_split_many_stripes_write_sequence(k, m, chunk, length):
+    body = bytes(O.object_bytes(k * 31 + m, length))
+    ws = [Rec() for _ in range(k + m)]
+    E.ec_split(k, m, io.BytesIO(body), chunk, length, ws)
+    files = O.ec_split(k, m, body, chunk)
+    stripes = -(-length // (k * chunk))
+    for i in range(k + m):
+        assert ws[i].value() == files[i]
+        assert len(ws[i].calls) == stripes  # one write per stripe, in stripe order
+
+
+@pytest.mark.parametrize("cut_stripe", [0, 1, 4])
+def test_split_short_read_writes_complete_stripes_first(cut_stripe):
+    k, m, chunk = 4, 2, 1024
+    stripe = k * chunk
+    length = 8 * stripe
+    body = bytes(O.object_bytes(5, length))
+    avail = cut_stripe * stripe + 100  # the read of stripe `cut_stripe` comes up short
+    ws = [Rec() for _ in range(k + m)]
+    with pytest.raises(RS.ErrUnexpectedEOF):
+        E.ec_split(k, m, io.BytesIO(body[:avail]), chunk, length, ws)
+    want = O.ec_split(k, m, body[:cut_stripe * stripe], chunk) if cut_stripe else [b""] * (k + m)
+    for i in range(k + m):
+        assert ws[i].value() == want[i]
+
+
+def test_split_reader_error_mid_object():
+    k, m, chunk = 4, 2, 2048
+    length = 6 * k * chunk
+    body = bytes(O.object_bytes(9, length))
+    ws = [Rec() for _ in range(k + m)]
+    with pytest.raises(RS.ErrIO):
+        E.ec_split(k, m, FailingReader(body, fail_at=3 * k * chunk), chunk, length, ws)
+    want = O.ec_split(k, m, body[:3 * k * chunk], chunk)
+    assert [w.value() for w in ws] == want
+
+
+def test_split_failing_writer_dropped_midway():
+    k, m, chunk = 4, 2, 1024
+    length = 10 * k * chunk
+    body = bytes(O.object_bytes(11, length))
+
+    class Breaks(Rec):
+        def write(self, b):
+            if len(self.calls) == 3:
+                raise IOError("peer went away")
+            super().write(b)
+
+    ws = [Rec() for _ in range(k + m)]
+    ws[1] = Breaks()
+    ws[5] = Breaks()
+    E.ec_split(k, m, io.BytesIO(body), chunk, length, ws)
+    files = O.ec_split(k, m, body, chunk)
+    for i in range(k + m):
+        if i in (1, 5):
+            assert ws[i].value() == files[i][:3 * chunk]
+        else:
+            assert ws[i].value() == files[i]
+
+
+@pytest.mark.parametrize("k,m,chunk,length,erased", [(4, 2, 1024, 50_000, (0, 5)), (8, 3, 4096, 400_000, (1, 2, 9)),
+                                                     (4, 2, 1000, 9_999, (3,)), (3, 2, 100, 7, (0, 1))])
+def test_reconstruct_many_stripes(k, m, chunk, length, erased):
+    body = bytes(O.object_bytes(k + 100 * m, length))
+    files = O.ec_split(k, m, body, chunk)
+    bodies = [None if i in erased else io.BytesIO(files[i]) for i in range(k + m)]
+    dsts = [Rec() for _ in erased]
+    E.ec_reconstruct(k, m, bodies, chunk, length, dsts, list(erased))
+    for d, i in zip(dsts, erased):
+        assert d.value() == files[i]
+
+
+def test_reconstruct_body_failure_is_per_stripe():
+    """ecutils.go:103-109: a body whose read fails is missing for that stripe
+    only (never marked failed) and is read again on the next stripe."""
+    k, m, chunk = 4, 2, 1024
+    length = 6 * k * chunk
+    body = bytes(O.object_bytes(21, length))
+    files = O.ec_split(k, m, body, chunk)
+
+    class FlakyOnce:
+        def __init__(self, data, bad_stripe):
+            self.f = io.BytesIO(data)
+            self.bad = bad_stripe
+            self.calls = 0
+
+        def read(self, n):
+            stripe = self.f.tell() // chunk
+            if stripe == self.bad and self.calls == 0:
+                self.calls += 1
+                self.f.seek(chunk, 1)  # the stripe's bytes are consumed by the failed read
+                raise IOError("flaky")
+            return self.f.read(n)
+
+    bodies = [io.BytesIO(f) for f in files]
+    bodies[2] = FlakyOnce(files[2], bad_stripe=3)
+    bodies[0] = None  # erased: rebuilt every stripe
+    dsts = [Rec()]
+    E.ec_reconstruct(k, m, bodies, chunk, length, dsts, [0])
+    assert dsts[0].value() == files[0]
+
+
+@pytest.mark.parametrize("k,m,chunk,length,lost", [(4, 2, 1024, 70_000, ()), (4, 2, 1024, 70_000, (1, 4)),
+                                                   (8, 3, 4096, 333_333, (0, 7, 8)), (3, 2, 10, 7, (2,))])
+def test_glue_many_stripes(k, m, chunk, length, lost):
+    body = bytes(O.object_bytes(k * 7 + len(lost), length))
+    files = O.ec_split(k, m, body, chunk)
+    bodies = [None if i in lost else io.BytesIO(files[i]) for i in range(k + m)]
+    out = Rec()
+    E.ec_glue(k, m, bodies, chunk, length, out)
+    assert out.value() == body
+
+
+def test_glue_body_failing_midway_stays_failed():
+    k, m, chunk = 4, 2, 1024
+    length = 8 * k * chunk
+    body = bytes(O.object_bytes(33, length))
+    files = O.ec_split(k, m, body, chunk)
+    bodies = [io.BytesIO(f) for f in files]
+    bodies[1] = FailingReader(files[1], fail_at=3 * chunk)
+    out = Rec()
+    E.ec_glue(k, m, bodies, chunk, length, out)
+    assert out.value() == body
