@@ -62,6 +62,13 @@ struct DeviceInfo {
 static std::mutex g_dev_mu;
 static std::map<int, DeviceInfo> g_devs;
 
+// Occupancy ceiling of the verify kernel (for the tuning override).
+static int bpc_occ_cap(int k, int r) {
+    int b = 1;
+    if (verify_occupancy(k, r, &b) != hipSuccess) return 1;
+    return b;
+}
+
 static int current_device(int* dev) {
     hipError_t e = hipGetDevice(dev);
     if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
@@ -530,6 +537,7 @@ static int verify_views(hbec_codec* c, const hbec_view* views, uint64_t n_obj, u
             e = verify_occupancy(k, m, &bpc);
             if (e != hipSuccess) return hip_fail(e, "verify occupancy");
             bpc = std::max(1, kPipeBlocksPerCu > 0 ? std::min(bpc, kPipeBlocksPerCu) : bpc);
+            if (g_blocks_per_cu_override > 0) bpc = std::min(std::max(1, bpc_occ_cap(k, m)), g_blocks_per_cu_override);
         }
         const uint64_t max_obj = std::max<uint64_t>(1, (1ull << 31) / tpo);
         for (uint64_t o0 = 0; o0 < n_obj; o0 += max_obj) {

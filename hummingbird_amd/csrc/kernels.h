@@ -58,6 +58,29 @@ __host__ __device__ constexpr int pipe_u(int k) {
     return k <= 4 ? (4 / k) : (k <= 8 ? 3 : 1);
 }
 
+// Tile depth of the stripe-plan and verify kernels, from A/B runs on MI355X
+// (profiles/r01_tune_plan_verify.jsonl; HBEC_STRIPE_LOADS / HBEC_VERIFY_LOADS
+// override with K*U ~= that value):
+//  * stripes: pipe_u for K <= 4, 1 KiB for K >= 5 — config 4's 4 KiB objects
+//    (512-B shards) waste less of a shallow tile: 67.2 % vs 63.7 % at 3 KiB;
+//  * verify (read-only): 4 KiB for K <= 4 (85.1 % vs 81.9 % at 1 KiB),
+//    1 KiB for K >= 5 (82.0 % vs 79.8 % at 3 KiB).
+#ifndef HBEC_STRIPE_LOADS
+#define HBEC_STRIPE_LOADS 0
+#endif
+#ifndef HBEC_VERIFY_LOADS
+#define HBEC_VERIFY_LOADS 0
+#endif
+__host__ __device__ constexpr int loads_u(int k, int loads) {
+    return k >= loads ? 1 : (loads / k > 4 ? 4 : loads / k);
+}
+__host__ __device__ constexpr int stripes_u(int k) {
+    return HBEC_STRIPE_LOADS > 0 ? loads_u(k, HBEC_STRIPE_LOADS) : (k <= 4 ? pipe_u(k) : 1);
+}
+__host__ __device__ constexpr int verify_u(int k) {
+    return HBEC_VERIFY_LOADS > 0 ? loads_u(k, HBEC_VERIFY_LOADS) : (k <= 4 ? 4 : 1);
+}
+
 hipError_t launch_vec(int k, int r, const PassArgs& a, int grid, hipStream_t stream, int force_stream);
 hipError_t launch_bytes(int k, int r, const PassArgs& a, int grid, hipStream_t stream);
 hipError_t launch_fill(uint8_t* dst, uint64_t n_obj, uint64_t obj_len, uint64_t obj_stride, uint64_t base_seed,

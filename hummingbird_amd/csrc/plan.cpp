@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -58,6 +59,7 @@ int stripes_grid(int k, int r, uint64_t n_tiles, int* grid) {
         if (e != hipSuccess) return hip_fail(e, "stripes occupancy");
         b = std::max(1, b);
         if (hbec::kPipeBlocksPerCu > 0) b = std::min(b, hbec::kPipeBlocksPerCu);  // same HBM sweet spot
+        if (const char* env = std::getenv("HBEC_STRIPE_BLOCKS_PER_CU")) b = std::max(1, std::min(b, std::atoi(env)));
         occ[dev][k][r] = b;
     }
     const uint64_t want = (n_tiles + 3) / 4;  // 4 waves per block

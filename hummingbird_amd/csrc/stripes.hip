@@ -4,7 +4,7 @@
 //
 // A stripe is ecSplit's databuf layout (ecutils.go:31-35,55-58): k+m shards of
 // shard_len bytes back to back at `base`, data first.  The host plan cuts
-// every stripe into tiles of TILE = pipe_u(k) KiB of shard column and writes
+// every stripe into tiles of TILE = stripes_u(k) KiB of shard column and writes
 // one 32-B record per tile (kernels.h TileRec: input/output base, strides,
 // valid bytes).  For a stripe, shard i of the tile starts at addr +
 // i*shard_len.  Waves walk
@@ -68,7 +68,7 @@ __device__ __forceinline__ TileRec load_rec(const TileRec* __restrict__ recs, ui
 template <int K, int R>
 __global__ __launch_bounds__(kBlockThreads, 1) void gf_apply_stripes(StripeArgs a,
                                                                      const TileRec* __restrict__ tiles) {
-    constexpr int U = pipe_u(K);
+    constexpr int U = stripes_u(K);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave =
         __builtin_amdgcn_readfirstlane(blockIdx.x * (kBlockThreads / 64) + (threadIdx.x >> 6));
@@ -123,7 +123,7 @@ static const void* stripes_kernel(int k, int r) {
     return nullptr;
 }
 
-int stripes_tile_bytes(int k) { return pipe_u(k) * 1024; }
+int stripes_tile_bytes(int k) { return stripes_u(k) * 1024; }
 
 bool stripes_supported(int k, int r) { return stripes_kernel(k, r) != nullptr; }
 

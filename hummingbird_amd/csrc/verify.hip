@@ -59,7 +59,7 @@ __device__ __forceinline__ void check_tile(const u32x4 (&x)[U][K + R], const Pas
 
 template <int K, int R>
 __global__ __launch_bounds__(kPipeBlockThreads, 1) void gf_verify_pipe(PassArgs a, uint32_t* flags) {
-    constexpr int U = pipe_u(K);
+    constexpr int U = verify_u(K);
     constexpr uint64_t TILE = (uint64_t)U * 1024u;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave =
@@ -142,7 +142,7 @@ hipError_t verify_occupancy(int k, int r, int* blocks_per_cu) {
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, kPipeBlockThreads, 0);
 }
 
-int verify_tile_bytes(int k) { return pipe_u(k) * 1024; }
+int verify_tile_bytes(int k) { return verify_u(k) * 1024; }
 
 hipError_t launch_verify(int k, int r, const PassArgs& a, uint32_t* flags, int grid, hipStream_t stream) {
     const void* fn = verify_kernel(k, r);

@@ -45,6 +45,7 @@ for s in "$@"; do
     md5tests) step md5tests 600 python -m pytest tests/test_gpu_md5.py -q -x -p no:cacheprovider ;;
     md5) step md5 600 python scripts/bench_md5.py ;;
     md5sweep) step md5sweep 900 bash scripts/md5_sweep.sh ;;
+    tuneplan) step tuneplan 1000 bash scripts/tune_plan.sh ;;
     md5prof)
       mkdir -p "$OUT/md5prof"
       (cd /tmp && step md5prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/md5prof" -o run -- python3 "$ROOT/scripts/bench_md5.py") || exit $?

@@ -3,7 +3,7 @@
 # side by `python scripts/md5_sweep_build.py`) and pipeline segment counts.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-for v in d1 d2 d4 d2rot d4rot d2 d1; do
+for v in ${MD5_VARIANTS:-}; do
   HBEC_LIB=tune_build/md5_$v/libhbec.so timeout -k 10 120 python scripts/bench_md5.py --no-cpu --label md5_$v || exit $?
 done
 for n in ${MD5_SEGMENTS:-}; do
