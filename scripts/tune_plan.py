@@ -20,6 +20,7 @@ sys.path.insert(0, str(ROOT))
 
 VARIANTS = {
     "base": [],
+    "st24": ["HBEC_STRIPE_LOADS=24"],
     "st8": ["HBEC_STRIPE_LOADS=8"],
     "st16": ["HBEC_STRIPE_LOADS=16"],
     "st32": ["HBEC_STRIPE_LOADS=32"],
@@ -91,6 +92,9 @@ def run(label):
     enc = RS.New(k, m)
     plan = B.StripePlan(enc, [(pool.data_ptr() + o, s) for o, s in layout])
     emit("8+3 mixed encode (config 4)", sum((k + m) * s for _, s in layout), timeit(plan.encode))
+    present = [0, 0, 0] + [1] * 8
+    emit("8+3 mixed reconstruct{0,1,2} (config 4)", sum((k + 3) * s for _, s in layout),
+         timeit(lambda: plan.reconstruct(present)))
 
 
 if __name__ == "__main__":

@@ -3,8 +3,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 for round in 1 2 3; do
-  for v in base st8 st16 st32 vf8 vf16 vf32; do
+  for v in ${PLAN_VARIANTS:-base st8 st16 st32 vf8 vf16 vf32}; do
     HBEC_LIB=tune_build/plan_$v/libhbec.so TUNE_LABEL=$v timeout -k 10 120 python scripts/tune_plan.py || exit $?
   done
-  HBEC_LIB=tune_build/plan_base/libhbec.so HBEC_BLOCKS_PER_CU=2 HBEC_STRIPE_BLOCKS_PER_CU=2 TUNE_LABEL=base_b2 timeout -k 10 120 python scripts/tune_plan.py || exit $?
 done
