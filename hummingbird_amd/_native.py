@@ -59,6 +59,8 @@ _SIG = [
     ("hbec_reconstruct_batch", C.c_int,
      [_P, C.POINTER(View), _U8P, C.c_uint64, C.c_uint64, C.c_int, _P]),
     ("hbec_md5_batch", C.c_int, [C.POINTER(View), C.c_int, C.c_uint64, C.c_uint64, _P, _P]),
+    ("hbec_md5_list", C.c_int, [C.POINTER(_P), C.POINTER(C.c_uint64), C.c_uint64, _P, _P]),
+    ("hbec_md5_host", C.c_int, [C.POINTER(_P), C.POINTER(C.c_uint64), C.c_uint64, _U8P]),
     ("hbec_md5_new", C.c_int, [C.c_int, C.c_uint64, C.POINTER(_P)]),
     ("hbec_md5_free", None, [_P]),
     ("hbec_md5_update", C.c_int, [_P, C.POINTER(View), C.c_uint64, _P]),
@@ -77,9 +79,11 @@ _SIG = [
     ("hbec_reconstruct_plan", C.c_int, [_P, _P, _U8P, C.c_int, _P]),
     ("hbec_encode_host", C.c_int, [_P, C.POINTER(Stripe), C.c_uint64]),
     ("hbec_reconstruct_host", C.c_int, [_P, C.POINTER(Stripe), C.c_uint64, _U8P, C.c_int]),
+    ("hbec_encode_host_md5", C.c_int, [_P, C.POINTER(Stripe), C.c_uint64, _U8P]),
     ("hbec_batcher_new", C.c_int, [_P, C.c_uint64, C.c_uint32, C.POINTER(_P)]),
     ("hbec_batcher_free", None, [_P]),
     ("hbec_batcher_encode", C.c_int, [_P, C.POINTER(Stripe)]),
+    ("hbec_batcher_encode_md5", C.c_int, [_P, C.POINTER(Stripe), _U8P]),
     ("hbec_batcher_reconstruct", C.c_int, [_P, C.POINTER(Stripe), _U8P, C.c_int]),
     ("hbec_batcher_stats", C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     ("hbec_set_force_stream", C.c_int, [C.c_int]),
@@ -87,8 +91,6 @@ _SIG = [
      [C.c_int, C.c_int, C.c_uint64, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     ("hbec_ec_shard_length", C.c_int64, [C.c_int64, C.c_int]),
     ("hbec_ec_split", C.c_int, [C.c_int, C.c_int, READ_FN, _P, C.c_int, C.c_int64, WRITE_FN, C.POINTER(_P)]),
-    ("hbec_ec_split_md5", C.c_int,
-     [C.c_int, C.c_int, READ_FN, _P, C.c_int, C.c_int64, WRITE_FN, C.POINTER(_P), _U8P]),
     ("hbec_ec_reconstruct", C.c_int,
      [C.c_int, C.c_int, READ_FN, C.POINTER(_P), C.c_int, C.c_int64, WRITE_FN, C.POINTER(_P),
       C.POINTER(C.c_int), C.c_int]),

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <cstring>
 #include <condition_variable>
 #include <deque>
 #include <memory>
@@ -30,7 +31,8 @@ namespace {
 
 struct Request {
     hbec_stripe stripe;
-    int op;  // 0 encode, 1 reconstruct
+    int op;  // 0 encode, 1 reconstruct, 2 encode + ShardHash
+    uint8_t* digests = nullptr;  // op 2: (k+m) * 16 B
     std::vector<uint8_t> present;
     int data_only = 0;
     int rc = HBEC_OK;
@@ -86,9 +88,15 @@ struct hbec_batcher {
             std::vector<hbec_stripe> st(batch.size());
             for (size_t i = 0; i < batch.size(); ++i) st[i] = batch[i]->stripe;
             int rc;
-            if (batch[0]->op == 0)
+            if (batch[0]->op == 0) {
                 rc = hbec_encode_host(codec, st.data(), st.size());
-            else
+            } else if (batch[0]->op == 2) {
+                std::vector<uint8_t> dig(st.size() * (size_t)n_shards * 16);
+                rc = hbec_encode_host_md5(codec, st.data(), st.size(), dig.data());
+                if (rc == HBEC_OK)
+                    for (size_t i = 0; i < batch.size(); ++i)
+                        std::memcpy(batch[i]->digests, dig.data() + i * (size_t)n_shards * 16, (size_t)n_shards * 16);
+            } else
                 rc = hbec_reconstruct_host(codec, st.data(), st.size(), batch[0]->present.data(), batch[0]->data_only);
             const std::string err = rc ? hbec_last_error() : "";
             lk.lock();
@@ -149,6 +157,16 @@ int hbec_batcher_encode(hbec_batcher* b, const hbec_stripe* stripe) {
     Request r;
     r.stripe = *stripe;
     r.op = 0;
+    return b->submit(r);
+}
+
+int hbec_batcher_encode_md5(hbec_batcher* b, const hbec_stripe* stripe, uint8_t* digests) {
+    if (!b || !stripe || !digests) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+    if (stripe->shard_len == 0) return fail(HBEC_ERR_SHARD_NO_DATA, "stripe with zero shard length");
+    Request r;
+    r.stripe = *stripe;
+    r.op = 2;
+    r.digests = digests;
     return b->submit(r);
 }
 

@@ -4,7 +4,6 @@
 //
 //   hbec_ec_shard_length  <- ecShardLength   ecutils.go:14-24
 //   hbec_ec_split         <- ecSplit         ecutils.go:26-72
-//   hbec_ec_split_md5     <- ecSplit + the receivers' ShardHash (indexdb.go:746-753)
 //   hbec_ec_reconstruct   <- ecReconstruct   ecutils.go:74-132
 //   hbec_ec_glue          <- ecGlue          ecutils.go:134-186
 //   hbec_parse_ec_scheme  <- parseECScheme   ecobj.go:82-98
@@ -84,7 +83,6 @@ struct Ring {
     hipStream_t stream = nullptr;
     uint8_t* host[2] = {nullptr, nullptr};
     uint8_t* dbuf[2] = {nullptr, nullptr};
-    uint8_t* digests = nullptr;  // 16 B x 256 chains
     hipEvent_t ev[2] = {nullptr, nullptr};
 };
 
@@ -98,7 +96,6 @@ void ring_destroy(Ring* r) {
         if (r->dbuf[i]) (void)hipFree(r->dbuf[i]);
         if (r->ev[i]) (void)hipEventDestroy(r->ev[i]);
     }
-    if (r->digests) (void)hipFree(r->digests);
     if (r->stream) (void)hipStreamDestroy(r->stream);
     delete r;
 }
@@ -129,7 +126,6 @@ int ring_acquire(size_t host_bytes, size_t dev_bytes, Ring** out) {
         if (e == hipSuccess) e = hipMalloc(&r->dbuf[i], r->dev_bytes);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&r->ev[i], hipEventDisableTiming);
     }
-    if (e == hipSuccess) e = hipMalloc(&r->digests, 16 * 256);
     if (e != hipSuccess) {
         ring_destroy(r.release());
         return e == hipErrorOutOfMemory ? fail(HBEC_ERR_NOMEM, "stripe ring") : hbec::hip_fail(e, "stripe ring");
@@ -260,16 +256,14 @@ int64_t hbec_ec_shard_length(int64_t length, int data_shards) {
     return s;
 }
 
-// ecSplit (ecutils.go:26-72), optionally hashing every shard (ShardHash,
-// indexdb.go:746-753) on the GPU while the stripe is resident.
-static int ec_split(int k, int m, hbec_read_fn read, void* fp, int chunk_size, int64_t content_length,
-                    hbec_write_fn write, void* const* writers, uint8_t* shard_md5) {
+// ecSplit (ecutils.go:26-72).
+int hbec_ec_split(int k, int m, hbec_read_fn read, void* fp, int chunk_size, int64_t content_length,
+                  hbec_write_fn write, void* const* writers) {
     CodecHolder enc;
     int rc = hbec_new(k, m, &enc.c);
     if (rc) return rc;
     if (!read || chunk_size < 0) return fail(HBEC_ERR_INVALID_ARG, "ecSplit: bad arguments");
     const int n = k + m;
-    if (shard_md5 && n > 256) return fail(HBEC_ERR_INVALID_ARG, "ecSplit: too many shards to hash");
     std::vector<char> failed(n, 0);
     struct Pending {
         bool live = false;
@@ -279,16 +273,9 @@ static int ec_split(int k, int m, hbec_read_fn read, void* fp, int chunk_size, i
     RingHolder ring;
     HostBufs bufs;
     bufs.bytes = (size_t)n * (size_t)chunk_size;  // databuf := make([]byte, (k+m)*chunkSize)  (ecutils.go:32)
-    hbec_md5* md5 = nullptr;
-    struct Md5Holder {
-        hbec_md5*& p;
-        ~Md5Holder() { hbec_md5_free(p); }
-    } md5_holder{md5};
     auto ensure_ring = [&]() -> int {
         if (ring.r) return HBEC_OK;
-        int r2 = ring_acquire(bufs.bytes, (size_t)n * round16((uint64_t)chunk_size), &ring.r);
-        if (r2 == HBEC_OK && shard_md5) r2 = hbec_md5_new(n, 1, &md5);
-        return r2;
+        return ring_acquire(bufs.bytes, (size_t)n * round16((uint64_t)chunk_size), &ring.r);
     };
     // write one finished stripe (ecutils.go:62-69): a failing writer is dropped
     auto flush = [&](int b) -> int {
@@ -327,10 +314,6 @@ static int ec_split(int k, int m, hbec_read_fn read, void* fp, int chunk_size, i
         device_views(*ring.r, b, L, n, v);
         rc = hbec_encode_batch(enc.c, v.data(), 1, L.pad, ring.r->stream);
         if (rc) return rc;
-        if (md5) {
-            rc = hbec_md5_update(md5, v.data(), L.s, ring.r->stream);
-            if (rc) return rc;
-        }
         if (L.contiguous()) {
             e = hipMemcpyAsync(databuf + (size_t)k * L.s, ring.r->dbuf[b] + (size_t)k * L.s, (size_t)m * L.s,
                                hipMemcpyDeviceToHost, ring.r->stream);
@@ -344,30 +327,7 @@ static int ec_split(int k, int m, hbec_read_fn read, void* fp, int chunk_size, i
         if (rc) return rc;
         b ^= 1;
     }
-    rc = flush(b ^ 1);
-    if (rc) return rc;
-    if (shard_md5) {
-        rc = ensure_ring();  // zero-length object: hash of every (empty) shard
-        if (rc) return rc;
-        rc = hbec_md5_final(md5, ring.r->digests, ring.r->stream);
-        if (rc) return rc;
-        hipError_t e = hipMemcpyAsync(shard_md5, ring.r->digests, 16u * (size_t)n, hipMemcpyDeviceToHost,
-                                      ring.r->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(ring.r->stream);
-        if (e != hipSuccess) return hbec::hip_fail(e, "ecSplit digests");
-    }
-    return HBEC_OK;
-}
-
-int hbec_ec_split(int k, int m, hbec_read_fn read, void* fp, int chunk_size, int64_t content_length,
-                  hbec_write_fn write, void* const* writers) {
-    return ec_split(k, m, read, fp, chunk_size, content_length, write, writers, nullptr);
-}
-
-int hbec_ec_split_md5(int k, int m, hbec_read_fn read, void* fp, int chunk_size, int64_t content_length,
-                      hbec_write_fn write, void* const* writers, uint8_t* shard_md5) {
-    if (!shard_md5) return fail(HBEC_ERR_INVALID_ARG, "ecSplit: null digest buffer");
-    return ec_split(k, m, read, fp, chunk_size, content_length, write, writers, shard_md5);
+    return flush(b ^ 1);
 }
 
 // ecReconstruct (ecutils.go:74-132).

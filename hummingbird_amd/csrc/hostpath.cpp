@@ -29,82 +29,12 @@
 #include "gf256.h"
 #include "internal.h"
 #include "kernels.h"
+#include "pool.h"
 
 using hbec::fail;
 using hbec::hip_fail;
 
 namespace {
-
-// ---------------------------------------------------------------- thread pool
-class Pool {
-   public:
-    explicit Pool(int n) {
-        for (int i = 0; i < n; ++i) threads_.emplace_back([this] { loop(); });
-    }
-    ~Pool() {
-        {
-            std::lock_guard<std::mutex> g(mu_);
-            stop_ = true;
-        }
-        cv_.notify_all();
-        for (auto& t : threads_) t.join();
-    }
-    int size() const { return (int)threads_.size(); }
-    // run f(i) for i in [0, n) on the pool + calling thread; returns when done
-    void parallel_for(size_t n, const std::function<void(size_t)>& f) {
-        if (n == 0) return;
-        std::unique_lock<std::mutex> lk(mu_);
-        fn_ = &f;
-        next_ = 0;
-        total_ = n;
-        done_ = 0;
-        ++gen_;
-        lk.unlock();
-        cv_.notify_all();
-        work();
-        lk.lock();
-        done_cv_.wait(lk, [&] { return done_ == total_; });
-        fn_ = nullptr;
-    }
-
-   private:
-    void work() {
-        for (;;) {
-            size_t i;
-            const std::function<void(size_t)>* f;
-            {
-                std::lock_guard<std::mutex> g(mu_);
-                if (!fn_ || next_ >= total_) return;
-                i = next_++;
-                f = fn_;
-            }
-            (*f)(i);
-            {
-                std::lock_guard<std::mutex> g(mu_);
-                if (++done_ == total_) done_cv_.notify_all();
-            }
-        }
-    }
-    void loop() {
-        uint64_t seen = 0;
-        for (;;) {
-            {
-                std::unique_lock<std::mutex> lk(mu_);
-                cv_.wait(lk, [&] { return stop_ || (gen_ != seen && fn_ && next_ < total_); });
-                if (stop_) return;
-                seen = gen_;
-            }
-            work();
-        }
-    }
-    std::vector<std::thread> threads_;
-    std::mutex mu_;
-    std::condition_variable cv_, done_cv_;
-    const std::function<void(size_t)>* fn_ = nullptr;
-    size_t next_ = 0, total_ = 0, done_ = 0;
-    uint64_t gen_ = 0;
-    bool stop_ = false;
-};
 
 // One column piece of one stripe: columns [col, col+len) of its K inputs / R outputs.
 struct Piece {
@@ -128,7 +58,14 @@ struct Ring {
     hbec::TileRec* pin_tiles[kSlots] = {};
     hbec::TileRec* dev_tiles[kSlots] = {};
     hipEvent_t ev_h2d[kSlots] = {}, ev_cmp[kSlots] = {}, ev_done[kSlots] = {};
-    std::unique_ptr<Pool> pool;
+    // ShardHash (hbec_encode_host_md5), created on first use: per slot a hash
+    // stream, its event, and pinned + device md5_list records
+    hipStream_t s_md5[kSlots] = {};
+    hipEvent_t ev_md5[kSlots] = {};
+    size_t md5_rec_cap = 0;
+    uint64_t* pin_md5rec[kSlots] = {};
+    uint64_t* dev_md5rec[kSlots] = {};
+    std::unique_ptr<hbec::Pool> pool;
 
     ~Ring() {
         for (int i = 0; i < kSlots; ++i) {
@@ -141,6 +78,10 @@ struct Ring {
             if (ev_h2d[i]) (void)hipEventDestroy(ev_h2d[i]);
             if (ev_cmp[i]) (void)hipEventDestroy(ev_cmp[i]);
             if (ev_done[i]) (void)hipEventDestroy(ev_done[i]);
+            if (ev_md5[i]) (void)hipEventDestroy(ev_md5[i]);
+            if (s_md5[i]) (void)hipStreamDestroy(s_md5[i]);
+            if (pin_md5rec[i]) (void)hipHostFree(pin_md5rec[i]);
+            if (dev_md5rec[i]) (void)hipFree(dev_md5rec[i]);
         }
         if (s_h2d) (void)hipStreamDestroy(s_h2d);
         if (s_cmp) (void)hipStreamDestroy(s_cmp);
@@ -185,12 +126,27 @@ int ring_init(Ring& r, int dev) {
         HB_CHECK(hipEventCreateWithFlags(&r.ev_done[i], hipEventDisableTiming), "event");
     }
 #undef HB_CHECK
-    // gather/scatter threads: HBEC_HOST_THREADS, else the process's CPU share
-    // (OMP_NUM_THREADS, 16 per GPU on the MI355X boxes), capped by the hardware
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    const size_t share = env_size("OMP_NUM_THREADS", 16);
-    const size_t want = std::min<size_t>(env_size("HBEC_HOST_THREADS", share), hw);
-    r.pool.reset(new Pool((int)std::max<size_t>(0, want - 1)));  // + the calling thread
+    r.pool.reset(new hbec::Pool(hbec::host_threads() - 1));  // + the calling thread
+    return HBEC_OK;
+}
+
+int ring_md5_init(Ring& r, size_t recs) {
+    if (r.md5_rec_cap >= recs) return HBEC_OK;
+    for (int i = 0; i < kSlots; ++i) {
+        if (!r.s_md5[i]) {
+            hipError_t e = hipStreamCreateWithFlags(&r.s_md5[i], hipStreamNonBlocking);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&r.ev_md5[i], hipEventDisableTiming);
+            if (e != hipSuccess) return hip_fail(e, "hash stream");
+        }
+        (void)hipStreamSynchronize(r.s_md5[i]);
+        if (r.pin_md5rec[i]) (void)hipHostFree(r.pin_md5rec[i]);
+        if (r.dev_md5rec[i]) (void)hipFree(r.dev_md5rec[i]);
+        r.pin_md5rec[i] = r.dev_md5rec[i] = nullptr;
+        hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&r.pin_md5rec[i]), recs * 32, hipHostMallocDefault);
+        if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&r.dev_md5rec[i]), recs * 32);
+        if (e != hipSuccess) return hip_fail(e, "hash records");
+    }
+    r.md5_rec_cap = recs;
     return HBEC_OK;
 }
 
@@ -223,8 +179,12 @@ void ring_release(Ring* r) {
 }
 
 // Code every stripe: inputs = shards in_idx, outputs = shards out_idx with `rows`.
+// With d_digest (device, n * n_shards * 16 B), also hash every input and
+// output shard of every stripe while it is in the device slot: digest of
+// shard i of stripe s at (s * n_shards + i) * 16.
 int host_run(const hbec_stripe* stripes, uint64_t n, const std::vector<int>& in_idx,
-             const std::vector<int>& out_idx, const std::vector<uint8_t>& rows) {
+             const std::vector<int>& out_idx, const std::vector<uint8_t>& rows, uint8_t* d_digest = nullptr,
+             int n_shards = 0) {
     const int K = (int)in_idx.size(), R = (int)out_idx.size();
     if (R == 0 || n == 0) return HBEC_OK;
     if (K > 8 || !hbec::stripes_supported(K, std::min(R, 3)))
@@ -240,6 +200,13 @@ int host_run(const hbec_stripe* stripes, uint64_t n, const std::vector<int>& in_
     // max columns per piece so that K*lpad fits the IN slot and R*lpad the OUT slot
     const uint64_t max_cols = (std::min(ring->in_cap / K, ring->out_cap / R) / 16) * 16;
     if (max_cols < 16) return fail(HBEC_ERR_INVALID_ARG, "staging slot too small");
+    if (d_digest) {
+        for (uint64_t s = 0; s < n; ++s)
+            if (stripes[s].shard_len > max_cols)
+                return fail(HBEC_ERR_INVALID_ARG, "hashing needs every stripe to fit one staging slot");
+        rc = ring_md5_init(*ring, ring->tile_cap * (size_t)(K + R));
+        if (rc) return rc;
+    }
 
     // Cut the batch into chunks of pieces that fit a slot.
     std::vector<std::vector<Piece>> chunks(1);
@@ -341,9 +308,33 @@ int host_run(const hbec_stripe* stripes, uint64_t n, const std::vector<int>& in_
             in_bytes = std::max(in_bytes, p.in_off + K * p.lpad);
             out_bytes = std::max(out_bytes, p.out_off + R * p.lpad);
         }
-        hipError_t e;
-        e = hipMemcpyAsync(ring->dev_tiles[slot], ring->pin_tiles[slot], nt * sizeof(hbec::TileRec),
-                           hipMemcpyHostToDevice, ring->s_h2d);
+        hipError_t e = hipSuccess;
+        uint64_t n_rec = 0;
+        if (d_digest) {  // one md5_list record per shard of every stripe in the chunk
+            uint64_t* rec = ring->pin_md5rec[slot];
+            for (const Piece& p : pieces) {
+                for (int j = 0; j < K; ++j, ++n_rec) {
+                    rec[4 * n_rec + 0] = din + p.in_off + (uint64_t)j * p.lpad;
+                    rec[4 * n_rec + 1] = p.len;
+                    rec[4 * n_rec + 2] = p.stripe * (uint64_t)n_shards + (uint64_t)in_idx[j];
+                    rec[4 * n_rec + 3] = 0;
+                }
+                for (int r = 0; r < R; ++r, ++n_rec) {
+                    rec[4 * n_rec + 0] = dout + p.out_off + (uint64_t)r * p.lpad;
+                    rec[4 * n_rec + 1] = p.len;
+                    rec[4 * n_rec + 2] = p.stripe * (uint64_t)n_shards + (uint64_t)out_idx[r];
+                    rec[4 * n_rec + 3] = 0;
+                }
+            }
+            // the slot's device buffers are still being hashed from its last chunk
+            e = hipStreamWaitEvent(ring->s_h2d, ring->ev_md5[slot], 0);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(ring->dev_md5rec[slot], ring->pin_md5rec[slot], n_rec * 32, hipMemcpyHostToDevice,
+                                   ring->s_h2d);
+        }
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(ring->dev_tiles[slot], ring->pin_tiles[slot], nt * sizeof(hbec::TileRec),
+                               hipMemcpyHostToDevice, ring->s_h2d);
         if (e == hipSuccess)
             e = hipMemcpyAsync(ring->dev_in[slot], ring->pin_in[slot], in_bytes, hipMemcpyHostToDevice, ring->s_h2d);
         if (e == hipSuccess) e = hipEventRecord(ring->ev_h2d[slot], ring->s_h2d);
@@ -364,6 +355,13 @@ int host_run(const hbec_stripe* stripes, uint64_t n, const std::vector<int>& in_
             if (e != hipSuccess) return hip_fail(e, "launch gf_apply_stripes (host path)");
         }
         e = hipEventRecord(ring->ev_cmp[slot], ring->s_cmp);
+        if (e == hipSuccess && d_digest) {  // hash the slot's shards on its own stream
+            e = hipStreamWaitEvent(ring->s_md5[slot], ring->ev_cmp[slot], 0);
+            if (e == hipSuccess)
+                e = hbec::launch_md5_list(ring->dev_md5rec[slot], n_rec, d_digest, true, ring->s_md5[slot]);
+            if (e == hipSuccess) e = hipEventRecord(ring->ev_md5[slot], ring->s_md5[slot]);
+            if (e != hipSuccess) return hip_fail(e, "host path hash");
+        }
         if (e == hipSuccess) e = hipStreamWaitEvent(ring->s_d2h, ring->ev_cmp[slot], 0);
         if (e == hipSuccess)
             e = hipMemcpyAsync(ring->pin_out[slot], ring->dev_out[slot], out_bytes, hipMemcpyDeviceToHost,
@@ -377,10 +375,22 @@ int host_run(const hbec_stripe* stripes, uint64_t n, const std::vector<int>& in_
         rc = scatter(slot);
         if (rc) return rc;
     }
+    if (d_digest)
+        for (int i = 0; i < kSlots; ++i) {
+            hipError_t e = hipStreamSynchronize(ring->s_md5[i]);
+            if (e != hipSuccess) return hip_fail(e, "host path hash drain");
+        }
     return HBEC_OK;
 }
 
 }  // namespace
+
+int hbec::host_threads() {
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const size_t share = env_size("OMP_NUM_THREADS", 16);
+    const size_t want = std::min<size_t>(env_size("HBEC_HOST_THREADS", share), hw);
+    return (int)std::max<size_t>(1, want);
+}
 
 extern "C" {
 
@@ -395,6 +405,41 @@ int hbec_encode_host(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n_s
     for (int j = 0; j < k; ++j) in_idx[j] = j;
     for (int r = 0; r < m; ++r) out_idx[r] = k + r;
     return host_run(stripes, n_stripes, in_idx, out_idx, rows);
+}
+
+int hbec_encode_host_md5(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n_stripes, uint8_t* digests) {
+    if (!codec || !digests || (n_stripes && !stripes)) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+    if (n_stripes == 0) return HBEC_OK;
+    const int k = hbec_data_shards(codec), m = hbec_parity_shards(codec), n = k + m;
+    if (m == 0) return fail(HBEC_ERR_INVALID_ARG, "encode_host_md5 needs parity shards");
+    for (uint64_t s = 0; s < n_stripes; ++s)
+        if (stripes[s].shard_len == 0) return fail(HBEC_ERR_SHARD_NO_DATA, "stripe with zero shard length");
+    std::vector<uint8_t> mat((size_t)n * k);
+    hbec_matrix(codec, mat.data());
+    std::vector<uint8_t> rows(mat.begin() + (size_t)k * k, mat.end());
+    std::vector<int> in_idx(k), out_idx(m);
+    for (int j = 0; j < k; ++j) in_idx[j] = j;
+    for (int r = 0; r < m; ++r) out_idx[r] = k + r;
+    hipStream_t st = nullptr;
+    hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+    if (e != hipSuccess) return hip_fail(e, "hipStreamCreate");
+    void* d_dig = nullptr;
+    const size_t bytes = (size_t)n_stripes * n * 16;
+    int rc = hbec::scratch_alloc(bytes, st, &d_dig);
+    if (!rc) {
+        e = hipStreamSynchronize(st);  // allocation visible to the ring's streams
+        if (e != hipSuccess) rc = hip_fail(e, "scratch");
+    }
+    if (!rc) rc = host_run(stripes, n_stripes, in_idx, out_idx, rows, static_cast<uint8_t*>(d_dig), n);
+    if (!rc) {
+        e = hipMemcpyAsync(digests, d_dig, bytes, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) rc = hip_fail(e, "digests D2H");
+    }
+    hbec::scratch_free(d_dig, st);
+    (void)hipStreamSynchronize(st);
+    (void)hipStreamDestroy(st);
+    return rc;
 }
 
 int hbec_reconstruct_host(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n_stripes,

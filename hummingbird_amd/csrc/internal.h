@@ -16,4 +16,13 @@ int hip_fail(hipError_t e, const char* what);
 int apply_views(int rows, int cols, const uint8_t* coeffs, const hbec_view* in, const hbec_view* out,
                 uint64_t n_obj, uint64_t shard_len, hipStream_t stream);
 
+// Stream-ordered device scratch from the library's private memory pool
+// (release threshold: never), so per-call scratch costs no real allocation.
+int scratch_alloc(size_t bytes, hipStream_t stream, void** out);
+void scratch_free(void* p, hipStream_t stream);
+
+// ShardHash of a list of device chains: records {addr, len, slot, 0} (32 B
+// each, device memory), digest of record i at digest + slot * 16.
+hipError_t launch_md5_list(const void* recs, uint64_t n, uint8_t* digest, bool aligned, hipStream_t stream);
+
 }  // namespace hbec

@@ -135,6 +135,9 @@ struct Md5Args {
 #ifndef HBEC_MD5_PINGPONG
 #define HBEC_MD5_PINGPONG 1
 #endif
+#ifndef HBEC_MD5_DEPTH_LIST
+#define HBEC_MD5_DEPTH_LIST 2
+#endif
 
 template <bool ALIGNED, int D>
 __global__ __launch_bounds__(64) void md5_chains(Md5Args a) {
@@ -259,6 +262,85 @@ __global__ __launch_bounds__(64) void md5_chains(Md5Args a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// md5_list: one-shot MD5 of independent buffers of ANY lengths (shard files for
+// an auditor pass, the shards of a host-path chunk).  One lane per chain, the
+// chain described by a 32-B record; the host sorts records by length so a
+// wave's lanes run similar trip counts (a wave lasts as long as its longest
+// chain).  Same compression and load pipeline as md5_chains.
+// ---------------------------------------------------------------------------
+struct Md5ListRec {
+    uint64_t addr;
+    uint64_t len;
+    uint64_t slot;  // digest index
+    uint64_t pad_;
+};
+
+template <bool ALIGNED>
+__global__ __launch_bounds__(64) void md5_list(const Md5ListRec* __restrict__ recs, uint64_t n, uint8_t* digest) {
+    constexpr int D = HBEC_MD5_DEPTH_LIST;
+    const uint64_t c = (uint64_t)blockIdx.x * 64u + threadIdx.x;
+    if (c >= n) return;
+    const Md5ListRec r = recs[c];
+    const uint8_t* p = reinterpret_cast<const uint8_t*>(r.addr);
+    uint32_t h[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+    const uint64_t nb = r.len / 64u;
+    if (nb > 0) {
+        const uint64_t groups = (nb + D - 1) / D;
+        auto load_group = [&](u32x4 (&dst)[D][4], uint64_t g) {
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                uint64_t blk = g * D + j;
+                blk = blk < nb ? blk : nb - 1;
+                const uint8_t* bp = p + 64u * blk;
+#pragma unroll
+                for (int w = 0; w < 4; ++w) {
+                    if (ALIGNED) {
+                        dst[j][w] = *reinterpret_cast<const u32x4*>(bp + 16 * w);
+                    } else {
+                        uint32_t e[4];
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            const uint8_t* q = bp + 16 * w + 4 * k;
+                            e[k] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) |
+                                   ((uint32_t)q[3] << 24);
+                        }
+                        dst[j][w] = u32x4{e[0], e[1], e[2], e[3]};
+                    }
+                }
+            }
+        };
+        u32x4 ga[D][4], gb[D][4];
+        load_group(ga, 0);
+        for (uint64_t g = 0; g < groups; g += 2) {
+            load_group(gb, g + 1 < groups ? g + 1 : g);
+#pragma unroll
+            for (int j = 0; j < D; ++j)
+                if (g * D + j < nb) md5_compress4(h, ga[j]);
+            load_group(ga, g + 2 < groups ? g + 2 : groups - 1);
+#pragma unroll
+            for (int j = 0; j < D; ++j)
+                if ((g + 1) * D + j < nb) md5_compress4(h, gb[j]);
+        }
+    }
+    const uint32_t rv = (uint32_t)(r.len - nb * 64u);
+    const Pending pend{nullptr, p, 0};
+    uint32_t m[16];
+    assemble(m, pend, nb * 64u, rv, true);
+    if (rv >= 56) {
+        md5_compress(h, m);
+#pragma unroll
+        for (int w = 0; w < 14; ++w) m[w] = 0;
+    }
+    const uint64_t bits = r.len * 8u;
+    m[14] = (uint32_t)bits;
+    m[15] = (uint32_t)(bits >> 32);
+    md5_compress(h, m);
+    uint32_t* out = reinterpret_cast<uint32_t*>(digest + r.slot * 16u);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) out[i] = h[i];
+}
+
 // Blocks per load group and the buffer scheme, from the depth sweep on MI355X
 // (profiles/r01_md5_sweep.jsonl).
 #ifndef HBEC_MD5_DEPTH
@@ -266,6 +348,18 @@ __global__ __launch_bounds__(64) void md5_chains(Md5Args a) {
 #endif
 
 uint64_t md5_state_bytes() { return sizeof(Md5State); }
+
+// recs: device array of n records ({addr, len, slot, 0}); aligned = every addr 16-B aligned.
+hipError_t launch_md5_list(const void* recs, uint64_t n, uint8_t* digest, bool aligned, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    const dim3 grid((unsigned)((n + 63) / 64));
+    const Md5ListRec* r = static_cast<const Md5ListRec*>(recs);
+    if (aligned)
+        hipLaunchKernelGGL(md5_list<true>, grid, dim3(64), 0, stream, r, n, digest);
+    else
+        hipLaunchKernelGGL(md5_list<false>, grid, dim3(64), 0, stream, r, n, digest);
+    return hipGetLastError();
+}
 
 // views: n_views (base, stride) pairs (<= kMd5MaxViews per launch; callers
 // split), chain (o, view0 + v) of chain_stride chains per object.

@@ -22,6 +22,7 @@
 
 #include "../../include/hbec.h"
 #include "internal.h"
+#include "pool.h"
 
 namespace hbec {
 
@@ -139,7 +140,109 @@ int order_after(hipStream_t b, hipStream_t a) {
     return HBEC_OK;
 }
 
+// md5_list records (md5.hip Md5ListRec)
+struct ListRec {
+    uint64_t addr, len, slot, pad;
+};
+
+// Records for n buffers, longest first (a wave lasts as long as its longest chain).
+void list_records(const void* const* bufs, const uint64_t* lens, uint64_t n, std::vector<ListRec>& recs,
+                  bool* aligned) {
+    recs.resize(n);
+    *aligned = true;
+    for (uint64_t i = 0; i < n; ++i) {
+        recs[i] = ListRec{reinterpret_cast<uint64_t>(bufs[i]), lens[i], i, 0};
+        if (recs[i].addr & 15u) *aligned = false;
+    }
+    std::stable_sort(recs.begin(), recs.end(), [](const ListRec& a, const ListRec& b) { return a.len > b.len; });
+}
+
+// Pinned staging ring for hbec_md5_host: per slot a pinned buffer, a device
+// buffer, pinned + device record arrays, a stream and an event.  Pooled per
+// device; one call at a time per ring.
+constexpr int kHashSlots = 3;
+struct HashRing {
+    int dev = 0;
+    size_t cap = 0, rec_cap = 0;
+    uint8_t* pin[kHashSlots] = {};
+    uint8_t* dbuf[kHashSlots] = {};
+    ListRec* pin_rec[kHashSlots] = {};
+    ListRec* drec[kHashSlots] = {};
+    hipStream_t stream[kHashSlots] = {};
+    hipEvent_t ev[kHashSlots] = {};
+    ~HashRing() {
+        for (int i = 0; i < kHashSlots; ++i) {
+            if (pin[i]) (void)hipHostFree(pin[i]);
+            if (pin_rec[i]) (void)hipHostFree(pin_rec[i]);
+            if (dbuf[i]) (void)hipFree(dbuf[i]);
+            if (drec[i]) (void)hipFree(drec[i]);
+            if (ev[i]) (void)hipEventDestroy(ev[i]);
+            if (stream[i]) (void)hipStreamDestroy(stream[i]);
+        }
+    }
+};
+
+std::mutex g_hash_mu;
+std::vector<HashRing*> g_hash_free;
+
+int hash_ring_acquire(HashRing** out) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+    {
+        std::lock_guard<std::mutex> g(g_hash_mu);
+        for (size_t i = 0; i < g_hash_free.size(); ++i)
+            if (g_hash_free[i]->dev == dev) {
+                *out = g_hash_free[i];
+                g_hash_free.erase(g_hash_free.begin() + (long)i);
+                return HBEC_OK;
+            }
+    }
+    std::unique_ptr<HashRing> r(new (std::nothrow) HashRing());
+    if (!r) return fail(HBEC_ERR_NOMEM, "hash ring");
+    r->dev = dev;
+    const char* env = std::getenv("HBEC_HOST_SLOT_MB");
+    const long long mb = env ? std::atoll(env) : 64;
+    r->cap = (size_t)(mb > 0 ? mb : 64) << 20;
+    r->rec_cap = 65536;
+    for (int i = 0; i < kHashSlots && e == hipSuccess; ++i) {
+        e = hipHostMalloc(reinterpret_cast<void**>(&r->pin[i]), r->cap, hipHostMallocDefault);
+        if (e == hipSuccess)
+            e = hipHostMalloc(reinterpret_cast<void**>(&r->pin_rec[i]), r->rec_cap * sizeof(ListRec),
+                              hipHostMallocDefault);
+        if (e == hipSuccess) e = hipMalloc(&r->dbuf[i], r->cap);
+        if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&r->drec[i]), r->rec_cap * sizeof(ListRec));
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&r->stream[i], hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&r->ev[i], hipEventDisableTiming);
+    }
+    if (e != hipSuccess) return hip_fail(e, "hash ring");
+    *out = r.release();
+    return HBEC_OK;
+}
+
+void hash_ring_release(HashRing* r) {
+    for (int i = 0; i < kHashSlots; ++i) (void)hipStreamSynchronize(r->stream[i]);
+    std::lock_guard<std::mutex> g(g_hash_mu);
+    g_hash_free.push_back(r);
+}
+
 }  // namespace
+
+int scratch_alloc(size_t bytes, hipStream_t stream, void** out) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+    hipMemPool_t pool;
+    int rc = state_pool(dev, &pool);
+    if (rc) return rc;
+    e = hipMallocFromPoolAsync(out, std::max<size_t>(bytes, 16), pool, stream);
+    if (e != hipSuccess) return hip_fail(e, "hipMallocFromPoolAsync");
+    return HBEC_OK;
+}
+
+void scratch_free(void* p, hipStream_t stream) {
+    if (p) (void)hipFreeAsync(p, stream);
+}
 
 // Segment length for the encode/hash pipeline: ~n segments, 4 KiB multiples
 // (whole MD5 blocks, whole encode tiles), none below 16 KiB.  n = 8 for
@@ -183,6 +286,139 @@ int hbec_md5_batch(const hbec_view* views, int n_views, uint64_t n_objects, uint
     if (n_objects == 0) return HBEC_OK;
     return md5_step(views, n_views, n_objects, len, 0, kInit | kFinal, nullptr, d_digests,
                     static_cast<hipStream_t>(hip_stream));
+}
+
+int hbec_md5_list(const void* const* d_bufs, const uint64_t* lens, uint64_t n, uint8_t* d_digests,
+                  void* hip_stream) {
+    if (n == 0) return HBEC_OK;
+    if (!d_bufs || !lens) return fail(HBEC_ERR_INVALID_ARG, "md5_list: null argument");
+    int rc = check_digests(d_digests);
+    if (rc) return rc;
+    for (uint64_t i = 0; i < n; ++i)
+        if (!d_bufs[i] && lens[i]) return fail(HBEC_ERR_INVALID_ARG, "md5_list: null buffer");
+    std::vector<ListRec> recs;
+    bool aligned = true;
+    list_records(d_bufs, lens, n, recs, &aligned);
+    hipStream_t stream = static_cast<hipStream_t>(hip_stream);
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+    hipMemPool_t pool;
+    rc = state_pool(dev, &pool);
+    if (rc) return rc;
+    void* drec = nullptr;
+    e = hipMallocFromPoolAsync(&drec, n * sizeof(ListRec), pool, stream);
+    if (e != hipSuccess) return hip_fail(e, "hipMallocFromPoolAsync");
+    // pageable source: staged by the runtime before the call returns
+    e = hipMemcpyAsync(drec, recs.data(), n * sizeof(ListRec), hipMemcpyHostToDevice, stream);
+    if (e == hipSuccess) e = launch_md5_list(drec, n, d_digests, aligned, stream);
+    (void)hipFreeAsync(drec, stream);
+    if (e != hipSuccess) return hip_fail(e, "md5_list");
+    return HBEC_OK;
+}
+
+int hbec_md5_host(const uint8_t* const* bufs, const uint64_t* lens, uint64_t n, uint8_t* digests) {
+    if (n == 0) return HBEC_OK;
+    if (!bufs || !lens || !digests) return fail(HBEC_ERR_INVALID_ARG, "md5_host: null argument");
+    for (uint64_t i = 0; i < n; ++i)
+        if (!bufs[i] && lens[i]) return fail(HBEC_ERR_INVALID_ARG, "md5_host: null buffer");
+    HashRing* ring = nullptr;
+    int rc = hash_ring_acquire(&ring);
+    if (rc) return rc;
+    struct Rel {
+        HashRing* r;
+        ~Rel() { hash_ring_release(r); }
+    } rel{ring};
+    int dev = ring->dev;
+    hipMemPool_t mpool;
+    rc = state_pool(dev, &mpool);
+    if (rc) return rc;
+    uint8_t* d_dig = nullptr;
+    hipError_t e = hipMallocFromPoolAsync(reinterpret_cast<void**>(&d_dig), n * 16, mpool, ring->stream[0]);
+    if (e != hipSuccess) return hip_fail(e, "hipMallocFromPoolAsync");
+    for (int i = 1; i < kHashSlots && e == hipSuccess; ++i) {  // every slot stream sees the allocation
+        e = hipEventRecord(ring->ev[0], ring->stream[0]);
+        if (e == hipSuccess) e = hipStreamWaitEvent(ring->stream[i], ring->ev[0], 0);
+    }
+    if (e != hipSuccess) return hip_fail(e, "md5_host ordering");
+    // longest first; chunks of buffers that fit a slot (16-B aligned offsets)
+    std::vector<uint64_t> order(n);
+    for (uint64_t i = 0; i < n; ++i) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](uint64_t a, uint64_t b) { return lens[a] > lens[b]; });
+    std::vector<std::vector<uint64_t>> chunks;
+    std::vector<uint64_t> big;  // longer than a slot: streamed through slot 0 piece by piece
+    uint64_t used = 0;
+    for (uint64_t i : order) {
+        const uint64_t sz = (lens[i] + 15) & ~uint64_t(15);
+        if (lens[i] > ring->cap) {
+            big.push_back(i);
+            continue;
+        }
+        if (chunks.empty() || used + sz > ring->cap || chunks.back().size() >= ring->rec_cap) {
+            chunks.emplace_back();
+            used = 0;
+        }
+        chunks.back().push_back(i);
+        used += sz;
+    }
+    Pool pool(host_threads() - 1);
+    for (size_t c = 0; c < chunks.size(); ++c) {
+        const int s = (int)(c % kHashSlots);
+        e = hipEventSynchronize(ring->ev[s]);  // slot free: its previous chunk has been hashed
+        if (e != hipSuccess) return hip_fail(e, "md5_host wait");
+        const auto& ch = chunks[c];
+        std::vector<uint64_t> off(ch.size());
+        uint64_t o = 0;
+        for (size_t j = 0; j < ch.size(); ++j) {
+            off[j] = o;
+            o += (lens[ch[j]] + 15) & ~uint64_t(15);
+        }
+        pool.parallel_for(ch.size(), [&](size_t j) {
+            if (lens[ch[j]]) std::memcpy(ring->pin[s] + off[j], bufs[ch[j]], lens[ch[j]]);
+        });
+        const uint64_t dbase = reinterpret_cast<uint64_t>(ring->dbuf[s]);
+        for (size_t j = 0; j < ch.size(); ++j) ring->pin_rec[s][j] = ListRec{dbase + off[j], lens[ch[j]], ch[j], 0};
+        e = hipMemcpyAsync(ring->drec[s], ring->pin_rec[s], ch.size() * sizeof(ListRec), hipMemcpyHostToDevice,
+                           ring->stream[s]);
+        if (e == hipSuccess && o)
+            e = hipMemcpyAsync(ring->dbuf[s], ring->pin[s], o, hipMemcpyHostToDevice, ring->stream[s]);
+        if (e == hipSuccess) e = launch_md5_list(ring->drec[s], ch.size(), d_dig, true, ring->stream[s]);
+        if (e == hipSuccess) e = hipEventRecord(ring->ev[s], ring->stream[s]);
+        if (e != hipSuccess) return hip_fail(e, "md5_host chunk");
+    }
+    for (int s = 0; s < kHashSlots; ++s) {
+        e = hipStreamSynchronize(ring->stream[s]);
+        if (e != hipSuccess) return hip_fail(e, "md5_host drain");
+    }
+    // buffers larger than a slot: one streaming chain each, slot-sized pieces
+    for (uint64_t i : big) {
+        hbec_md5* ctx = nullptr;
+        rc = hbec_md5_new(1, 1, &ctx);
+        if (rc) return rc;
+        for (uint64_t pos = 0; pos < lens[i] && rc == HBEC_OK; pos += ring->cap) {
+            const uint64_t len = std::min<uint64_t>(ring->cap, lens[i] - pos);
+            pool.parallel_for(16, [&](size_t t) {
+                const uint64_t a = len * t / 16, b = len * (t + 1) / 16;
+                std::memcpy(ring->pin[0] + a, bufs[i] + pos + a, b - a);
+            });
+            e = hipMemcpyAsync(ring->dbuf[0], ring->pin[0], len, hipMemcpyHostToDevice, ring->stream[0]);
+            if (e != hipSuccess) rc = hip_fail(e, "md5_host H2D");
+            hbec_view v{ring->dbuf[0], 0};
+            if (!rc) rc = hbec_md5_update(ctx, &v, len, ring->stream[0]);
+            if (!rc) {
+                e = hipStreamSynchronize(ring->stream[0]);  // pinned slot reused by the next piece
+                if (e != hipSuccess) rc = hip_fail(e, "md5_host sync");
+            }
+        }
+        if (!rc) rc = hbec_md5_final(ctx, d_dig + i * 16, ring->stream[0]);
+        hbec_md5_free(ctx);  // hipFree synchronises with the queued final
+        if (rc) return rc;
+    }
+    e = hipMemcpyAsync(digests, d_dig, n * 16, hipMemcpyDeviceToHost, ring->stream[0]);
+    (void)hipFreeAsync(d_dig, ring->stream[0]);
+    if (e == hipSuccess) e = hipStreamSynchronize(ring->stream[0]);
+    if (e != hipSuccess) return hip_fail(e, "md5_host digests");
+    return HBEC_OK;
 }
 
 int hbec_md5_new(int n_views, uint64_t n_objects, hbec_md5** out) {

@@ -75,25 +75,6 @@ def ec_split(data_chunks, parity_chunks, fp, chunk_size, content_length, writers
             _objs.pop(i, None)
 
 
-def ec_split_md5(data_chunks, parity_chunks, fp, chunk_size, content_length, writers):
-    """ecSplit that also returns each shard's ShardHash — hex(MD5) of all the
-    bytes written to writer i (objectserver/indexdb.go:746-753) — computed on
-    the GPU next to the encode.  Returns k+m hex strings."""
-    n = int(data_chunks) + int(parity_chunks)
-    if len(writers) != n:
-        raise ValueError("need k+m writers (None for a nil writer)")
-    ids = _register([fp, *writers])
-    dig = (C.c_uint8 * (16 * max(n, 1)))()
-    try:
-        check(N.lib().hbec_ec_split_md5(int(data_chunks), int(parity_chunks), _read_cb, ids[0], int(chunk_size),
-                                        int(content_length), _write_cb, _ctx_array(ids[1:]), dig))
-    finally:
-        for i in ids:
-            _objs.pop(i, None)
-    raw = bytes(dig)
-    return [raw[16 * i:16 * (i + 1)].hex() for i in range(n)]
-
-
 def ec_reconstruct(data_chunks, parity_chunks, bodies, chunk_size, content_length, dsts, dst_chunk_num):
     b_ids = _register(bodies)
     d_ids = _register(dsts)

@@ -176,6 +176,16 @@ class Encoder:
     def EncodeStripes(self, stripes) -> None:
         check(N.lib().hbec_encode_host(self._h, self._stripes(stripes), len(stripes)))
 
+    def EncodeStripesMD5(self, stripes):
+        """EncodeStripes + the ShardHash of every shard of every stripe, hashed on
+        the GPU (indexdb.go:746-753).  Returns [[hex] * (k+m)] per stripe."""
+        n = len(stripes)
+        out = (C.c_uint8 * (16 * self.Shards * max(n, 1)))()
+        check(N.lib().hbec_encode_host_md5(self._h, self._stripes(stripes), n, out))
+        raw = bytes(out)
+        return [[raw[16 * (s * self.Shards + i):16 * (s * self.Shards + i + 1)].hex() for i in range(self.Shards)]
+                for s in range(n)]
+
     def ReconstructStripes(self, stripes, present, data_only: bool = False) -> None:
         p = (C.c_uint8 * self.Shards)(*[1 if x else 0 for x in present])
         check(N.lib().hbec_reconstruct_host(self._h, self._stripes(stripes), len(stripes), p, int(data_only)))
@@ -221,6 +231,14 @@ class Batcher:
     def Encode(self, stripe) -> None:
         s = self._stripe(stripe)
         check(N.lib().hbec_batcher_encode(self._h, C.byref(s)))
+
+    def EncodeMD5(self, stripe):
+        """Encode + ShardHash of the stripe's k+m shards (hex strings)."""
+        s = self._stripe(stripe)
+        out = (C.c_uint8 * (16 * self.enc.Shards))()
+        check(N.lib().hbec_batcher_encode_md5(self._h, C.byref(s), out))
+        raw = bytes(out)
+        return [raw[16 * i:16 * (i + 1)].hex() for i in range(self.enc.Shards)]
 
     def Reconstruct(self, stripe, present, data_only: bool = False) -> None:
         s = self._stripe(stripe)

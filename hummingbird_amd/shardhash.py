@@ -55,6 +55,37 @@ def encode_objects_md5(enc: Encoder, objs, parity, shard_len: int, stream=None):
     return encode_md5_views(enc, views, objs.shape[0], shard_len, device=objs.device, stream=stream)
 
 
+def md5_list(buffers, digests=None, device="cuda", stream=None):
+    """MD5 of device buffers of any lengths: `buffers` = [(device address, length)]
+    or 1-D uint8 CUDA tensors.  Returns uint8 [n, 16] digests (device)."""
+    import torch
+
+    pairs = [(b.data_ptr(), b.numel()) if hasattr(b, "data_ptr") else (int(b[0]), int(b[1])) for b in buffers]
+    n = len(pairs)
+    if digests is None:
+        digests = torch.empty((max(n, 1), 16), dtype=torch.uint8, device=device)
+    addrs = (C.c_void_p * max(n, 1))(*[a for a, _ in pairs])
+    lens = (C.c_uint64 * max(n, 1))(*[ln for _, ln in pairs])
+    check(N.lib().hbec_md5_list(addrs, lens, n, C.c_void_p(digests.data_ptr()), _stream_ptr(stream)))
+    return digests[:n]
+
+
+def md5_host(buffers):
+    """ShardHash of host buffers (bytes / numpy uint8 arrays) of any lengths,
+    hashed on the GPU (an auditor pass).  Returns hex strings."""
+    import numpy as np
+
+    arrs = [np.ascontiguousarray(np.frombuffer(b, dtype=np.uint8) if isinstance(b, (bytes, bytearray)) else b,
+                                 dtype=np.uint8) for b in buffers]
+    n = len(arrs)
+    ptrs = (C.c_void_p * max(n, 1))(*[a.ctypes.data if a.size else None for a in arrs])
+    lens = (C.c_uint64 * max(n, 1))(*[a.size for a in arrs])
+    out = (C.c_uint8 * (16 * max(n, 1)))()
+    check(N.lib().hbec_md5_host(ptrs, lens, n, out))
+    raw = bytes(out)
+    return [raw[16 * i:16 * (i + 1)].hex() for i in range(n)]
+
+
 class MD5Chains:
     """Streaming MD5 chains (hbec_md5_*): n_views x n_objects chains fed one
     stripe's sub-chunks per update — a multi-stripe shard file's hash."""

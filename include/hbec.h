@@ -124,6 +124,18 @@ int hbec_verify_batch(hbec_codec* codec, const hbec_view* views, uint64_t n_obje
 int hbec_md5_batch(const hbec_view* views, int n_views, uint64_t n_objects, uint64_t len, uint8_t* d_digests,
                    void* hip_stream);
 
+/* MD5 of n DEVICE buffers of any lengths (d_bufs and lens are host arrays):
+ * digest of buffer i at d_digests + i * 16.  Chains run longest first, one
+ * lane each; a launch lasts as long as its longest chain. */
+int hbec_md5_list(const void* const* d_bufs, const uint64_t* lens, uint64_t n, uint8_t* d_digests,
+                  void* hip_stream);
+
+/* MD5 of n HOST buffers of any lengths — e.g. an auditor pass over shard
+ * files (auditor.go:100-156) — staged through a pinned three-slot ring so the
+ * gather, the H2D copies and the hashing of successive chunks overlap.
+ * digests (host): buffer i at i * 16.  Synchronous. */
+int hbec_md5_host(const uint8_t* const* bufs, const uint64_t* lens, uint64_t n, uint8_t* digests);
+
 /* Streaming chains for multi-stripe shards (a shard file is the concatenation
  * of its per-stripe sub-chunks, ecutils.go:55-69): n_views x n_objects chains
  * fed any number of updates (every chain gets the same len per update), then
@@ -188,6 +200,12 @@ int hbec_reconstruct_plan(hbec_codec* codec, const hbec_plan* plan, const uint8_
 int hbec_encode_host(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n_stripes);
 int hbec_reconstruct_host(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n_stripes, const uint8_t* present,
                           int data_only);
+/* hbec_encode_host + ShardHash (indexdb.go:746-753) of every data and parity
+ * shard of every stripe, computed on the GPU while the stripe is in the device
+ * slot (hashing of one chunk overlaps the copies of the next): digests (host)
+ * receive n_stripes * (k+m) raw MD5s, shard i of stripe s at (s*(k+m)+i)*16.
+ * Every stripe must fit one staging slot (k * shard_len <= HBEC_HOST_SLOT_MB). */
+int hbec_encode_host_md5(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n_stripes, uint8_t* digests);
 
 /* Batching driver for concurrent callers (e.g. one cgo call per Stabilize):
  * each call submits ONE host stripe and blocks until it is coded; a worker
@@ -199,6 +217,8 @@ typedef struct hbec_batcher hbec_batcher;
 int hbec_batcher_new(hbec_codec* codec, uint64_t max_batch_bytes, uint32_t max_wait_us, hbec_batcher** out);
 void hbec_batcher_free(hbec_batcher* batcher);
 int hbec_batcher_encode(hbec_batcher* batcher, const hbec_stripe* stripe);
+/* Encode + ShardHash of all k+m shards of the stripe (digests: host, (k+m)*16). */
+int hbec_batcher_encode_md5(hbec_batcher* batcher, const hbec_stripe* stripe, uint8_t* digests);
 int hbec_batcher_reconstruct(hbec_batcher* batcher, const hbec_stripe* stripe, const uint8_t* present, int data_only);
 int hbec_batcher_stats(hbec_batcher* batcher, uint64_t* batches, uint64_t* stripes);
 
@@ -225,12 +245,6 @@ int64_t hbec_ec_shard_length(int64_t length, int data_shards);
  * failing writer is dropped for the rest of the object, as in Go. */
 int hbec_ec_split(int data_shards, int parity_shards, hbec_read_fn read, void* fp, int chunk_size,
                   int64_t content_length, hbec_write_fn write, void* const* writers);
-
-/* ecSplit that also returns the ShardHash of everything written to each
- * writer: shard_md5 (host) receives (k+m) raw 16-byte digests, shard i at
- * i * 16 — what each receiving StablePut (indexdb.go:746-753) would compute. */
-int hbec_ec_split_md5(int data_shards, int parity_shards, hbec_read_fn read, void* fp, int chunk_size,
-                      int64_t content_length, hbec_write_fn write, void* const* writers, uint8_t* shard_md5);
 
 /* ecReconstruct (ecutils.go:74-132).  bodies: k+m reader contexts, NULL = nil. */
 int hbec_ec_reconstruct(int data_shards, int parity_shards, hbec_read_fn read, void* const* bodies, int chunk_size,

@@ -166,6 +166,82 @@ def batched_callers(n_threads=64, per_thread=32):
             "us_per_object": round(t / n * 1e6, 1), "batches": st["batches"]}
 
 
+def library_host_path_md5(n_obj=4096, reps=3):
+    """hbec_encode_host_md5: the library host path plus the ShardHash of all
+    k+m shards of every stripe, hashed on the GPU per chunk."""
+    k, m, S = 4, 2, MiB // 4
+    enc = RS.New(k, m)
+    pool = np.empty((n_obj, (k + m) * S), dtype=np.uint8)
+    from oracle import coracle as CO
+    from oracle import oracle as O
+    pool[:, :k * S] = CO.fill_objects(0, n_obj, k * S)
+    stripes = [pool[i] for i in range(n_obj)]
+    hs = enc.EncodeStripesMD5(stripes)
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        hs = enc.EncodeStripesMD5(stripes)
+        ts.append(time.perf_counter() - t0)
+    t = min(ts)
+    assert hs[9] == [O.shard_hash(pool[9, i * S:(i + 1) * S]) for i in range(k + m)]
+    return {"measure": "library_host_path_encode_md5_pageable", "objects": n_obj, "seconds": round(t, 4),
+            "object_data_GiB_s": round(n_obj * k * S / t / GiB, 2),
+            "hashed_GiB_s": round(n_obj * (k + m) * S / t / GiB, 2), "objects_per_s": round(n_obj / t, 1)}
+
+
+def batched_callers_md5(n_threads=64, per_thread=32):
+    import threading
+
+    k, m, S = 4, 2, MiB // 4
+    enc = RS.New(k, m)
+    bat = RS.Batcher(enc, max_batch_bytes=96 << 20, max_wait_us=300)
+    from oracle import coracle as CO
+    n = n_threads * per_thread
+    pool = np.empty((n, (k + m) * S), dtype=np.uint8)
+    pool[:, :k * S] = CO.fill_objects(0, n, k * S)
+    out = [None] * n
+
+    def worker(t):
+        for i in range(t * per_thread, (t + 1) * per_thread):
+            out[i] = bat.EncodeMD5(pool[i])
+
+    bat.EncodeMD5(pool[0])
+    t0 = time.perf_counter()
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(n_threads)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    t = time.perf_counter() - t0
+    st = bat.stats()
+    bat.close()
+    import hashlib
+    assert out[n - 1] == [hashlib.md5(pool[n - 1, i * S:(i + 1) * S]).hexdigest() for i in range(k + m)]
+    return {"measure": "batcher_concurrent_EncodeMD5_1MiB", "threads": n_threads, "objects": n,
+            "seconds": round(t, 4), "object_data_GiB_s": round(n * k * S / t / GiB, 2),
+            "us_per_object": round(t / n * 1e6, 1), "batches": st["batches"]}
+
+
+def auditor_pass(n_files=4096, size=MiB // 4):
+    """hbec_md5_host over host 'shard files' (one GPU lane per file) vs one
+    CPU core of hashlib."""
+    import hashlib
+
+    from hummingbird_amd import shardhash as H
+    rng = np.random.default_rng(1)
+    files = [rng.integers(0, 256, size, dtype=np.uint8) for _ in range(n_files)]
+    H.md5_host(files[:8])
+    t0 = time.perf_counter()
+    got = H.md5_host(files)
+    t = time.perf_counter() - t0
+    t1 = time.perf_counter()
+    want = [hashlib.md5(f).hexdigest() for f in files[:256]]
+    tc = (time.perf_counter() - t1) * n_files / 256
+    assert got[:256] == want
+    return {"measure": "auditor_md5_host", "files": n_files, "file_bytes": size, "seconds": round(t, 4),
+            "GiB_s": round(n_files * size / t / GiB, 2), "cpu_1core_GiB_s": round(n_files * size / tc / GiB, 2)}
+
+
 def per_call(n_calls=200):
     k, m, S = 4, 2, MiB // 4
     enc = RS.New(k, m)
@@ -184,7 +260,8 @@ def per_call(n_calls=200):
 def main():
     torch.cuda.set_device(0)
     for r in (pipelined("encode"), pipelined("reconstruct"), library_host_path("encode"),
-              library_host_path("reconstruct"), batched_callers(), per_call()):
+              library_host_path("reconstruct"), library_host_path_md5(), batched_callers(), batched_callers_md5(),
+              auditor_pass(), per_call()):
         print(json.dumps(r), flush=True)
 
 

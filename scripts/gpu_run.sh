@@ -42,6 +42,8 @@ for s in "$@"; do
     dist2) step dist2 600 env HBEC_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 10 --warmup 2 --objects 2048 ;;
     configs) step configs 600 python scripts/bench_configs.py ;;
     host) step host 600 python scripts/bench_host.py ;;
+    ecloops)
+      gcc -O2 -std=c11 -Iinclude scripts/bench_ecutils.c -Lhummingbird_amd -lhbec -Wl,-rpath,$ROOT/hummingbird_amd -o $OUT/bench_ecutils && step ecloops 300 sh -c "$OUT/bench_ecutils 4 2 256 && $OUT/bench_ecutils 8 3 256" ;;
     md5tests) step md5tests 600 python -m pytest tests/test_gpu_md5.py -q -x -p no:cacheprovider ;;
     md5) step md5 600 python scripts/bench_md5.py ;;
     md5sweep) step md5sweep 900 bash scripts/md5_sweep.sh ;;

@@ -211,5 +211,11 @@ def test_shardhash_validation_before_device():
     assert L.hbec_md5_final(None, C.cast(dig, C.c_void_p), None) == N.ERR_INVALID_ARG
     enc = RS.New(4, 2)
     assert L.hbec_encode_md5_batch(enc.handle, None, 1, 16, C.cast(dig, C.c_void_p), None) == N.ERR_INVALID_ARG
-    with pytest.raises(RS.ErrInvalidArg):
-        RS.check(L.hbec_ec_split_md5(4, 2, E._read_cb, None, 16, 0, E._write_cb, None, None))
+    assert L.hbec_md5_list(None, None, 2, C.cast(dig, C.c_void_p), None) == N.ERR_INVALID_ARG
+    assert L.hbec_md5_list(None, None, 0, C.cast(dig, C.c_void_p), None) == N.HBEC_OK
+    assert L.hbec_md5_host(None, None, 3, dig) == N.ERR_INVALID_ARG
+    st = (N.Stripe * 1)()
+    st[0].base = 4096
+    st[0].shard_len = 0
+    assert L.hbec_encode_host_md5(enc.handle, st, 1, None) == N.ERR_INVALID_ARG
+    assert L.hbec_encode_host_md5(enc.handle, st, 1, dig) == N.ERR_SHARD_NO_DATA

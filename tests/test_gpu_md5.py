@@ -4,17 +4,16 @@
 Covers the RFC 1321 suite and the reference auditor fixture, every padding
 boundary (0, 55, 56, 63, 64, 65, 119, 120 ...), aligned and unaligned views,
 >32 views (split launches), partial waves, streaming chains with arbitrary
-update sizes (tail carry across updates), encode+hash with the segment
-pipeline, and ecSplit with hashing against the oracle's shard files.
+update sizes (tail carry across updates), multi-stripe shard files, chains of
+mixed lengths (md5_list, the host auditor pass), encode+hash with the segment
+pipeline, and the batched host path / batcher with hashing.
 """
-import hashlib
 
 import numpy as np
 import pytest
 import torch
 
 from hummingbird_amd import batch as B
-from hummingbird_amd import ecutils as E
 from hummingbird_amd import reedsolomon as RS
 from hummingbird_amd import shardhash as H
 from oracle import coracle as CO
@@ -130,33 +129,97 @@ def test_encode_md5_batch(k, m, shard_len, n_obj):
         assert got[o] == [O.shard_hash(x) for x in data + par_o], o
 
 
-@pytest.mark.parametrize("length", [0, 1, 7, 1001, 4096, 4097, 10000, 3 * 4096 + 5])
-def test_ec_split_md5_matches_oracle(length):
-    k, m, chunk = 4, 2, 1024
-    body = bytes(O.object_bytes(length, length))
-    import io
-
-    writers = [io.BytesIO() for _ in range(k + m)]
-    hashes = E.ec_split_md5(k, m, io.BytesIO(body), chunk, length, writers)
-    files = O.ec_split(k, m, body, chunk)
-    assert [w.getvalue() for w in writers] == files
-    assert hashes == [O.shard_hash(f) for f in files]
-    assert hashes == [hashlib.md5(w.getvalue()).hexdigest() for w in writers]
-
-
-def test_ec_split_md5_golden(vectors):
-    import io
-
+def test_multistripe_shard_hash_golden(vectors):
+    """A multi-stripe shard file's ShardHash through streaming chains fed one
+    stripe's sub-chunks per update (ecutils.go:55-69 concatenation)."""
     v = vectors["shard_hashes_4_2_chunk1k"]
+    k, m, chunk = 4, 2, v["chunk"]
     body = bytes(O.object_bytes(v["object"], v["len"]))
-    writers = [io.BytesIO() for _ in range(6)]
-    assert E.ec_split_md5(4, 2, io.BytesIO(body), v["chunk"], v["len"], writers) == v["hashes"]
+    files = O.ec_split(k, m, body, chunk)
+    dev = [torch.frombuffer(bytearray(f), dtype=torch.uint8).cuda() for f in files]
+    ch = H.MD5Chains(k + m, 1)
+    pos, left = 0, v["len"]
+    while left > 0:  # per-stripe sub-chunk size (ecutils.go:86-92)
+        s = chunk if left >= k * chunk else -(-left // k)
+        ch.update([(d.data_ptr() + pos, 0) for d in dev], s)
+        pos += s
+        left -= min(left, k * s)
+    assert H.hexdigests(ch.final())[0] == v["hashes"]
 
 
-def test_ec_split_md5_nil_writers():
-    import io
+@pytest.mark.parametrize("offset", [0, 3])
+def test_md5_list_any_lengths(offset):
+    rng = np.random.default_rng(17 + offset)
+    lens = [0, 1, 55, 56, 64, 65, 1000, 4096, 70_001, 262_144, 3, 120] * 9  # > 64 chains, mixed waves
+    host = [rng.integers(0, 256, n, dtype=np.uint8) for n in lens]
+    pool = torch.zeros(sum(n + 32 for n in lens), dtype=torch.uint8, device="cuda")
+    bufs, pos = [], 0
+    for a in host:
+        if a.size:
+            pool[pos + offset:pos + offset + a.size] = torch.from_numpy(a).cuda()
+        bufs.append((pool.data_ptr() + pos + offset, a.size))
+        pos += a.size + 32
+    got = [bytes(r).hex() for r in H.md5_list(bufs).cpu().numpy()]
+    assert got == [O.shard_hash(a) for a in host]
 
-    body = bytes(O.object_bytes(1, 5000))
-    writers = [io.BytesIO(), None, io.BytesIO(), None, io.BytesIO(), io.BytesIO()]
-    hashes = E.ec_split_md5(4, 2, io.BytesIO(body), 1024, len(body), writers)
-    assert hashes == O.ec_split_hashes(4, 2, body, 1024)  # hashes cover every shard, written or not
+
+def test_md5_host_auditor_pass(kats):
+    """GPU auditor pass over host 'shard files' of mixed lengths, including the
+    reference fixture (auditor_test.go:585-612) and one file larger than a
+    staging slot (streamed through a chain)."""
+    sh = kats["shard_hash"]
+    rng = np.random.default_rng(99)
+    files = [sh["match"].encode(), sh["mismatch"].encode(), b""]
+    files += [rng.integers(0, 256, int(n), dtype=np.uint8).tobytes() for n in rng.integers(0, 300_000, 200)]
+    files.append(rng.integers(0, 256, (64 << 20) + 4097, dtype=np.uint8).tobytes())
+    got = H.md5_host(files)
+    assert got[0] == sh["hash"] and got[1] != sh["hash"]
+    assert got == [O.shard_hash(f) for f in files]
+
+
+@pytest.mark.parametrize("k,m,sizes", [(4, 2, [1 << 18] * 40 + [1000, 16, 4096 * 3 + 16]), (8, 3, [512, 1 << 17] * 20),
+                                       (3, 2, [7, 100, 65536])])
+def test_encode_host_md5(k, m, sizes):
+    enc = RS.New(k, m)
+    rng = np.random.default_rng(len(sizes) + k)
+    stripes = []
+    for s in sizes:
+        st = np.zeros((k + m) * s, np.uint8)
+        st[:k * s] = rng.integers(0, 256, k * s, dtype=np.uint8)
+        stripes.append(st)
+    hashes = enc.EncodeStripesMD5(stripes)
+    mat = CO.build_matrix(k, m)
+    for st, s, hs in zip(stripes, sizes, hashes):
+        shards = [st[i * s:(i + 1) * s] for i in range(k + m)]
+        want = CO.apply(mat[k:], shards[:k])
+        for r in range(m):
+            assert np.array_equal(shards[k + r], want[r])
+        assert hs == [O.shard_hash(x) for x in shards]
+
+
+def test_batcher_encode_md5_concurrent():
+    import threading
+
+    k, m, S = 4, 2, 64 * 1024
+    enc = RS.New(k, m)
+    bat = RS.Batcher(enc, max_batch_bytes=32 << 20, max_wait_us=300)
+    errs = []
+
+    def worker(t):
+        try:
+            rng = np.random.default_rng(t)
+            for _ in range(6):
+                st = np.zeros((k + m) * S, np.uint8)
+                st[:k * S] = rng.integers(0, 256, k * S, dtype=np.uint8)
+                hs = bat.EncodeMD5(st)
+                assert hs == [O.shard_hash(st[i * S:(i + 1) * S]) for i in range(k + m)]
+        except BaseException as e:  # noqa: BLE001
+            errs.append(repr(e))
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    bat.close()
+    assert not errs, errs
