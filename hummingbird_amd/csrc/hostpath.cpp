@@ -58,13 +58,18 @@ struct Ring {
     hbec::TileRec* pin_tiles[kSlots] = {};
     hbec::TileRec* dev_tiles[kSlots] = {};
     hipEvent_t ev_h2d[kSlots] = {}, ev_cmp[kSlots] = {}, ev_done[kSlots] = {};
-    // ShardHash (hbec_encode_host_md5), created on first use: per slot a hash
-    // stream, its event, and pinned + device md5_list records
-    hipStream_t s_md5[kSlots] = {};
-    hipEvent_t ev_md5[kSlots] = {};
-    size_t md5_rec_cap = 0;
-    uint64_t* pin_md5rec[kSlots] = {};
-    uint64_t* dev_md5rec[kSlots] = {};
+    // ShardHash (hbec_encode_host_md5), created on first use: two device hash
+    // arenas.  After a chunk's kernel its shards are copied (D2D) into the
+    // current arena and the slot is free again; a full arena is hashed by ONE
+    // md5_list launch (thousands of chains, full-chip) on s_md5 while the other
+    // arena fills, so hashing hides behind the PCIe stream.
+    static constexpr int kArenas = 2;
+    hipStream_t s_md5 = nullptr;
+    uint8_t* arena[kArenas] = {};
+    size_t arena_cap = 0, arena_rec_cap = 0;
+    uint64_t* pin_md5rec[kArenas] = {};
+    uint64_t* dev_md5rec[kArenas] = {};
+    hipEvent_t ev_arena_copied[kArenas] = {}, ev_arena_hashed[kArenas] = {};
     std::unique_ptr<hbec::Pool> pool;
 
     ~Ring() {
@@ -78,11 +83,15 @@ struct Ring {
             if (ev_h2d[i]) (void)hipEventDestroy(ev_h2d[i]);
             if (ev_cmp[i]) (void)hipEventDestroy(ev_cmp[i]);
             if (ev_done[i]) (void)hipEventDestroy(ev_done[i]);
-            if (ev_md5[i]) (void)hipEventDestroy(ev_md5[i]);
-            if (s_md5[i]) (void)hipStreamDestroy(s_md5[i]);
-            if (pin_md5rec[i]) (void)hipHostFree(pin_md5rec[i]);
-            if (dev_md5rec[i]) (void)hipFree(dev_md5rec[i]);
         }
+        for (int a = 0; a < kArenas; ++a) {
+            if (arena[a]) (void)hipFree(arena[a]);
+            if (pin_md5rec[a]) (void)hipHostFree(pin_md5rec[a]);
+            if (dev_md5rec[a]) (void)hipFree(dev_md5rec[a]);
+            if (ev_arena_copied[a]) (void)hipEventDestroy(ev_arena_copied[a]);
+            if (ev_arena_hashed[a]) (void)hipEventDestroy(ev_arena_hashed[a]);
+        }
+        if (s_md5) (void)hipStreamDestroy(s_md5);
         if (s_h2d) (void)hipStreamDestroy(s_h2d);
         if (s_cmp) (void)hipStreamDestroy(s_cmp);
         if (s_d2h) (void)hipStreamDestroy(s_d2h);
@@ -130,23 +139,21 @@ int ring_init(Ring& r, int dev) {
     return HBEC_OK;
 }
 
-int ring_md5_init(Ring& r, size_t recs) {
-    if (r.md5_rec_cap >= recs) return HBEC_OK;
-    for (int i = 0; i < kSlots; ++i) {
-        if (!r.s_md5[i]) {
-            hipError_t e = hipStreamCreateWithFlags(&r.s_md5[i], hipStreamNonBlocking);
-            if (e == hipSuccess) e = hipEventCreateWithFlags(&r.ev_md5[i], hipEventDisableTiming);
-            if (e != hipSuccess) return hip_fail(e, "hash stream");
-        }
-        (void)hipStreamSynchronize(r.s_md5[i]);
-        if (r.pin_md5rec[i]) (void)hipHostFree(r.pin_md5rec[i]);
-        if (r.dev_md5rec[i]) (void)hipFree(r.dev_md5rec[i]);
-        r.pin_md5rec[i] = r.dev_md5rec[i] = nullptr;
-        hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&r.pin_md5rec[i]), recs * 32, hipHostMallocDefault);
-        if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&r.dev_md5rec[i]), recs * 32);
-        if (e != hipSuccess) return hip_fail(e, "hash records");
+int ring_md5_init(Ring& r) {
+    if (r.arena[0]) return HBEC_OK;
+    const size_t cap = env_size("HBEC_HASH_ARENA_MB", 1024) << 20;
+    r.arena_cap = std::max(cap, r.in_cap + r.out_cap);
+    r.arena_rec_cap = r.arena_cap / 16 + 1024;  // >= one record per 16-B shard
+    hipError_t e = hipStreamCreateWithFlags(&r.s_md5, hipStreamNonBlocking);
+    for (int a = 0; a < Ring::kArenas && e == hipSuccess; ++a) {
+        e = hipMalloc(&r.arena[a], r.arena_cap);
+        if (e == hipSuccess)
+            e = hipHostMalloc(reinterpret_cast<void**>(&r.pin_md5rec[a]), r.arena_rec_cap * 32, hipHostMallocDefault);
+        if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&r.dev_md5rec[a]), r.arena_rec_cap * 32);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&r.ev_arena_copied[a], hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&r.ev_arena_hashed[a], hipEventDisableTiming);
     }
-    r.md5_rec_cap = recs;
+    if (e != hipSuccess) return hip_fail(e, "hash arena");
     return HBEC_OK;
 }
 
@@ -204,9 +211,30 @@ int host_run(const hbec_stripe* stripes, uint64_t n, const std::vector<int>& in_
         for (uint64_t s = 0; s < n; ++s)
             if (stripes[s].shard_len > max_cols)
                 return fail(HBEC_ERR_INVALID_ARG, "hashing needs every stripe to fit one staging slot");
-        rc = ring_md5_init(*ring, ring->tile_cap * (size_t)(K + R));
+        rc = ring_md5_init(*ring);
         if (rc) return rc;
     }
+    // hash arena state: current arena, bytes and records queued in it
+    int cur_arena = 0;
+    uint64_t arena_used = 0, arena_recs = 0;
+    auto hash_arena = [&]() -> int {  // hash everything queued in the current arena, switch arenas
+        if (arena_recs == 0) return HBEC_OK;
+        const int a = cur_arena;
+        hipError_t e = hipEventRecord(ring->ev_arena_copied[a], ring->s_cmp);  // its copies are queued on s_cmp
+        if (e == hipSuccess) e = hipStreamWaitEvent(ring->s_md5, ring->ev_arena_copied[a], 0);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(ring->dev_md5rec[a], ring->pin_md5rec[a], arena_recs * 32, hipMemcpyHostToDevice,
+                               ring->s_md5);
+        if (e == hipSuccess) e = hbec::launch_md5_list(ring->dev_md5rec[a], arena_recs, d_digest, true, ring->s_md5);
+        if (e == hipSuccess) e = hipEventRecord(ring->ev_arena_hashed[a], ring->s_md5);
+        if (e != hipSuccess) return hip_fail(e, "hash arena launch");
+        cur_arena ^= 1;
+        arena_used = arena_recs = 0;
+        // the next arena (and its pinned records) may still be hashing its last fill
+        e = hipEventSynchronize(ring->ev_arena_hashed[cur_arena]);
+        if (e != hipSuccess) return hip_fail(e, "hash arena wait");
+        return HBEC_OK;
+    };
 
     // Cut the batch into chunks of pieces that fit a slot.
     std::vector<std::vector<Piece>> chunks(1);
@@ -309,29 +337,6 @@ int host_run(const hbec_stripe* stripes, uint64_t n, const std::vector<int>& in_
             out_bytes = std::max(out_bytes, p.out_off + R * p.lpad);
         }
         hipError_t e = hipSuccess;
-        uint64_t n_rec = 0;
-        if (d_digest) {  // one md5_list record per shard of every stripe in the chunk
-            uint64_t* rec = ring->pin_md5rec[slot];
-            for (const Piece& p : pieces) {
-                for (int j = 0; j < K; ++j, ++n_rec) {
-                    rec[4 * n_rec + 0] = din + p.in_off + (uint64_t)j * p.lpad;
-                    rec[4 * n_rec + 1] = p.len;
-                    rec[4 * n_rec + 2] = p.stripe * (uint64_t)n_shards + (uint64_t)in_idx[j];
-                    rec[4 * n_rec + 3] = 0;
-                }
-                for (int r = 0; r < R; ++r, ++n_rec) {
-                    rec[4 * n_rec + 0] = dout + p.out_off + (uint64_t)r * p.lpad;
-                    rec[4 * n_rec + 1] = p.len;
-                    rec[4 * n_rec + 2] = p.stripe * (uint64_t)n_shards + (uint64_t)out_idx[r];
-                    rec[4 * n_rec + 3] = 0;
-                }
-            }
-            // the slot's device buffers are still being hashed from its last chunk
-            e = hipStreamWaitEvent(ring->s_h2d, ring->ev_md5[slot], 0);
-            if (e == hipSuccess)
-                e = hipMemcpyAsync(ring->dev_md5rec[slot], ring->pin_md5rec[slot], n_rec * 32, hipMemcpyHostToDevice,
-                                   ring->s_h2d);
-        }
         if (e == hipSuccess)
             e = hipMemcpyAsync(ring->dev_tiles[slot], ring->pin_tiles[slot], nt * sizeof(hbec::TileRec),
                                hipMemcpyHostToDevice, ring->s_h2d);
@@ -354,14 +359,39 @@ int host_run(const hbec_stripe* stripes, uint64_t n, const std::vector<int>& in_
             e = hbec::launch_stripes(K, Rg, a, grid, ring->s_cmp);
             if (e != hipSuccess) return hip_fail(e, "launch gf_apply_stripes (host path)");
         }
-        e = hipEventRecord(ring->ev_cmp[slot], ring->s_cmp);
-        if (e == hipSuccess && d_digest) {  // hash the slot's shards on its own stream
-            e = hipStreamWaitEvent(ring->s_md5[slot], ring->ev_cmp[slot], 0);
+        if (d_digest) {  // the chunk's shards -> hash arena (D2D, same stream, before the slot is released)
+            if (arena_used + in_bytes + out_bytes > ring->arena_cap ||
+                arena_recs + pieces.size() * (size_t)(K + R) > ring->arena_rec_cap) {
+                rc = hash_arena();
+                if (rc) return rc;
+            }
+            const int a = cur_arena;
+            const uint64_t ain = reinterpret_cast<uint64_t>(ring->arena[a]) + arena_used;
+            const uint64_t aout = ain + in_bytes;
+            e = hipMemcpyAsync(reinterpret_cast<void*>(ain), ring->dev_in[slot], in_bytes, hipMemcpyDeviceToDevice,
+                               ring->s_cmp);
             if (e == hipSuccess)
-                e = hbec::launch_md5_list(ring->dev_md5rec[slot], n_rec, d_digest, true, ring->s_md5[slot]);
-            if (e == hipSuccess) e = hipEventRecord(ring->ev_md5[slot], ring->s_md5[slot]);
-            if (e != hipSuccess) return hip_fail(e, "host path hash");
+                e = hipMemcpyAsync(reinterpret_cast<void*>(aout), ring->dev_out[slot], out_bytes,
+                                   hipMemcpyDeviceToDevice, ring->s_cmp);
+            if (e != hipSuccess) return hip_fail(e, "hash arena copy");
+            uint64_t* rec = ring->pin_md5rec[a];
+            for (const Piece& p : pieces) {
+                for (int j = 0; j < K; ++j, ++arena_recs) {
+                    rec[4 * arena_recs + 0] = ain + p.in_off + (uint64_t)j * p.lpad;
+                    rec[4 * arena_recs + 1] = p.len;
+                    rec[4 * arena_recs + 2] = p.stripe * (uint64_t)n_shards + (uint64_t)in_idx[j];
+                    rec[4 * arena_recs + 3] = 0;
+                }
+                for (int r = 0; r < R; ++r, ++arena_recs) {
+                    rec[4 * arena_recs + 0] = aout + p.out_off + (uint64_t)r * p.lpad;
+                    rec[4 * arena_recs + 1] = p.len;
+                    rec[4 * arena_recs + 2] = p.stripe * (uint64_t)n_shards + (uint64_t)out_idx[r];
+                    rec[4 * arena_recs + 3] = 0;
+                }
+            }
+            arena_used += (in_bytes + out_bytes + 255) & ~uint64_t(255);
         }
+        e = hipEventRecord(ring->ev_cmp[slot], ring->s_cmp);
         if (e == hipSuccess) e = hipStreamWaitEvent(ring->s_d2h, ring->ev_cmp[slot], 0);
         if (e == hipSuccess)
             e = hipMemcpyAsync(ring->pin_out[slot], ring->dev_out[slot], out_bytes, hipMemcpyDeviceToHost,
@@ -375,11 +405,12 @@ int host_run(const hbec_stripe* stripes, uint64_t n, const std::vector<int>& in_
         rc = scatter(slot);
         if (rc) return rc;
     }
-    if (d_digest)
-        for (int i = 0; i < kSlots; ++i) {
-            hipError_t e = hipStreamSynchronize(ring->s_md5[i]);
-            if (e != hipSuccess) return hip_fail(e, "host path hash drain");
-        }
+    if (d_digest) {
+        rc = hash_arena();  // the last partial arena
+        if (rc) return rc;
+        hipError_t e = hipStreamSynchronize(ring->s_md5);
+        if (e != hipSuccess) return hip_fail(e, "host path hash drain");
+    }
     return HBEC_OK;
 }
 

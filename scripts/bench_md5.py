@@ -83,6 +83,25 @@ def config(k, m, n_obj=4096, obj=MiB):
             "pipelined_vs_sequential": round(t_seq / t_fused, 3)}
 
 
+def chain_scaling(S=MiB // 4):
+    """md5_list launch time vs number of 256 KiB chains: one wave per 64
+    chains, so few chains expose one lane's latency per 64-B block."""
+    rows = []
+    total = 24576
+    for spacing in (S, S + 4160):  # power-of-two vs skewed chain starts
+        buf = torch.empty((total, spacing), dtype=torch.uint8, device="cuda")
+        B.fill_splitmix(buf, spacing)
+        for n in (1, 64, 1024, 4096, 24576):
+            bufs = [(buf.data_ptr() + i * spacing, S) for i in range(n)]
+            dig = torch.empty((n, 16), dtype=torch.uint8, device="cuda")
+            t = timed(lambda: H.md5_list(bufs, digests=dig), reps=5)
+            rows.append({"measure": "md5_list_chain_scaling", "chains": n, "chain_bytes": S, "spacing": spacing,
+                         "ms": round(t, 3), "us_per_block": round(t * 1e3 / (S // 64), 4),
+                         "GB_s_hashed": round(n * S / t / 1e6, 2)})
+        del buf
+    return rows
+
+
 def cpu_md5(seconds=3.0):
     buf = np.random.default_rng(0).integers(0, 256, 64 * MiB, dtype=np.uint8).tobytes()
     n, t0 = 0, time.perf_counter()
@@ -102,7 +121,7 @@ def main():
     ap.add_argument("--label", default="")
     args = ap.parse_args()
     torch.cuda.set_device(0)
-    rows = [config(4, 2), config(8, 3)] + ([] if args.no_cpu else [cpu_md5()])
+    rows = [config(4, 2), config(8, 3)] + chain_scaling() + ([] if args.no_cpu else [cpu_md5()])
     for r in rows:
         if args.label:
             r["label"] = args.label
