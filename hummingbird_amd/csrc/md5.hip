@@ -276,32 +276,52 @@ struct Md5ListRec {
     uint64_t pad_;
 };
 
+__device__ uint8_t kMd5ZeroBlock[64 * HBEC_MD5_DEPTH_LIST];  // load target of empty chains
+
+// The loop runs the WAVE's longest chain (uniform trip count, so loads stay
+// pipelined: divergent per-lane loops made the compiler wait for every load
+// before each block); lanes past their own end compress clamped blocks and
+// keep their state with a select.
 template <bool ALIGNED>
 __global__ __launch_bounds__(64) void md5_list(const Md5ListRec* __restrict__ recs, uint64_t n, uint8_t* digest) {
     constexpr int D = HBEC_MD5_DEPTH_LIST;
     const uint64_t c = (uint64_t)blockIdx.x * 64u + threadIdx.x;
-    if (c >= n) return;
-    const Md5ListRec r = recs[c];
+    const bool live = c < n;
+    Md5ListRec r{0, 0, 0, 0};
+    if (live) r = recs[c];
     const uint8_t* p = reinterpret_cast<const uint8_t*>(r.addr);
     uint32_t h[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
     const uint64_t nb = r.len / 64u;
-    if (nb > 0) {
-        const uint64_t groups = (nb + D - 1) / D;
+    uint64_t nb_max = nb;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t o = (uint64_t)__shfl_xor((long long)nb_max, off, 64);
+        nb_max = o > nb_max ? o : nb_max;
+    }
+    nb_max = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(nb_max >> 32)) << 32) |
+             __builtin_amdgcn_readfirstlane((uint32_t)nb_max);
+    // integer addresses + address_space(1) loads: a generic pointer here makes
+    // the compiler emit flat loads, whose lgkmcnt share forces full waits
+    const uint64_t base = nb > 0 ? r.addr : reinterpret_cast<uint64_t>(kMd5ZeroBlock);
+    const uint64_t last = nb > 0 ? nb - 1 : 0;
+    if (nb_max > 0) {
+        const uint64_t groups = (nb_max + D - 1) / D;
         auto load_group = [&](u32x4 (&dst)[D][4], uint64_t g) {
 #pragma unroll
             for (int j = 0; j < D; ++j) {
                 uint64_t blk = g * D + j;
-                blk = blk < nb ? blk : nb - 1;
-                const uint8_t* bp = p + 64u * blk;
+                blk = blk < last ? blk : last;  // clamp to this lane's chain
+                const uint64_t bp = base + 64u * blk;
 #pragma unroll
                 for (int w = 0; w < 4; ++w) {
                     if (ALIGNED) {
-                        dst[j][w] = *reinterpret_cast<const u32x4*>(bp + 16 * w);
+                        dst[j][w] = *reinterpret_cast<gu32x4_c*>(bp + 16 * w);
                     } else {
+                        typedef __attribute__((address_space(1))) const uint8_t gu8_c;
                         uint32_t e[4];
 #pragma unroll
                         for (int k = 0; k < 4; ++k) {
-                            const uint8_t* q = bp + 16 * w + 4 * k;
+                            gu8_c* q = reinterpret_cast<gu8_c*>(bp + 16 * w + 4 * k);
                             e[k] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) |
                                    ((uint32_t)q[3] << 24);
                         }
@@ -310,19 +330,27 @@ __global__ __launch_bounds__(64) void md5_list(const Md5ListRec* __restrict__ re
                 }
             }
         };
+        auto step = [&](const u32x4 (&q)[4], uint64_t blk) {
+            uint32_t t[4] = {h[0], h[1], h[2], h[3]};
+            md5_compress4(t, q);
+            const bool keep = blk < nb;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) h[i] = keep ? t[i] : h[i];
+        };
         u32x4 ga[D][4], gb[D][4];
         load_group(ga, 0);
-        for (uint64_t g = 0; g < groups; g += 2) {
+        for (uint64_t g = 0; g < groups; g += 2) {  // uniform: groups from the wave maximum
             load_group(gb, g + 1 < groups ? g + 1 : g);
 #pragma unroll
             for (int j = 0; j < D; ++j)
-                if (g * D + j < nb) md5_compress4(h, ga[j]);
+                if (g * D + j < nb_max) step(ga[j], g * D + j);
             load_group(ga, g + 2 < groups ? g + 2 : groups - 1);
 #pragma unroll
             for (int j = 0; j < D; ++j)
-                if ((g + 1) * D + j < nb) md5_compress4(h, gb[j]);
+                if ((g + 1) * D + j < nb_max) step(gb[j], (g + 1) * D + j);
         }
     }
+    if (!live) return;
     const uint32_t rv = (uint32_t)(r.len - nb * 64u);
     const Pending pend{nullptr, p, 0};
     uint32_t m[16];
