@@ -41,6 +41,7 @@ sys.path.insert(0, str(ROOT))
 
 from hummingbird_amd import batch as B  # noqa: E402
 from hummingbird_amd import reedsolomon as RS  # noqa: E402
+from hummingbird_amd import split as SP  # noqa: E402
 
 METRIC = "GiB/s device-resident EC encode+reconstruct, 4+2 @ 1 MiB; % HBM roofline"
 GiB = float(1 << 30)
@@ -171,6 +172,69 @@ def cpu_baseline(k, m, obj_len, erased, budget_s=12.0, sample_objs=512):
     }
 
 
+def batch_split(pg, k, m, obj_len, n_global, world, rank, ctl_device):
+    """BASELINE configs[4]: a 4+2 batch of n_global objects lands on rank 0's
+    GPU; it is scattered over xGMI (RCCL P2P, hummingbird_amd/split.py), every
+    rank encodes its partition, and the parity is gathered back to rank 0,
+    which checks it against its own encode of the whole batch.  Runs after the
+    headline measurement; its times are reported next to it, never in `value`."""
+    s = obj_len // k
+    first, n = SP.object_range(n_global, world, rank)
+    enc = RS.New(k, m)
+    device = "cuda"
+    batch = dest = want = part = parity = None
+    err = ""
+    try:  # allocate everything first; all ranks agree before any P2P starts
+        if rank == 0:
+            batch = torch.empty((n_global, obj_len), dtype=torch.uint8, device=device)
+            B.fill_splitmix(batch, obj_len)
+            dest = torch.empty((n_global, m * s), dtype=torch.uint8, device=device)
+            want = torch.empty_like(dest)
+        part = torch.empty((n, obj_len), dtype=torch.uint8, device=device)
+        parity = torch.empty((n, m * s), dtype=torch.uint8, device=device)
+        torch.cuda.synchronize()
+    except Exception as e:  # noqa: BLE001 - reported, and every rank skips together
+        err = f"rank {rank}: {type(e).__name__}: {e}"[:200]
+    (failed,) = max_over_ranks(pg, [1.0 if err else 0.0], ctl_device)
+    if failed:
+        return {"skipped": err or "allocation failed on another rank", "objects": n_global}
+
+    def timed(fn):
+        pg.barrier()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        pg.barrier()
+        return time.perf_counter() - t
+
+    t_sc = timed(lambda: SP.scatter_objects(pg, batch, part, n_global))
+    t_enc = timed(lambda: B.encode_objects(enc, part, parity, s))
+    t_ga = timed(lambda: SP.gather_rows(pg, parity, dest, n_global))
+    ok = 1.0
+    if rank == 0:  # the gathered parity must equal rank 0's own encode of the whole batch
+        B.encode_objects(enc, batch, want, s)
+        for a in range(0, n_global, 1024):  # chunked: torch.equal materialises a bool temp
+            if not torch.equal(want[a:a + 1024], dest[a:a + 1024]):
+                ok = 0.0
+                break
+    t_sc, t_enc, t_ga, bad = max_over_ranks(pg, [t_sc, t_enc, t_ga, 1.0 - ok], ctl_device)
+    peer_objs = n_global - SP.object_range(n_global, world, 0)[1]
+    sc_bytes = peer_objs * obj_len
+    ga_bytes = peer_objs * m * s
+    return {
+        "backend": "rccl (torch.distributed nccl, P2P over xGMI)",
+        "objects": n_global, "objects_per_rank_max": SP.object_range(n_global, world, 0)[1],
+        "scatter_ms": round(t_sc * 1e3, 3), "scatter_GBs": round(sc_bytes / t_sc / 1e9, 2),
+        "scatter_GBs_per_peer": round(sc_bytes / max(1, world - 1) / t_sc / 1e9, 2),
+        "encode_ms": round(t_enc * 1e3, 3),
+        "encode_GiB_s_all_ranks": round(n_global * (k + m) * s / t_enc / GiB, 2),
+        "gather_ms": round(t_ga * 1e3, 3), "gather_GBs": round(ga_bytes / t_ga / 1e9, 2),
+        "end_to_end_ms": round((t_sc + t_enc + t_ga) * 1e3, 3),
+        "parity_ok": bad == 0.0,
+    }
+
+
 def cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -189,6 +253,8 @@ def main():
     ap.add_argument("--objects", type=int, default=4096, help="objects per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--split-objects", type=int, default=65536,
+                    help="N>1 on RCCL: objects in the batch split from rank 0 (BASELINE configs[4]); 0 = skip")
     args = ap.parse_args()
 
     world, rank, local = dist_env()
@@ -297,6 +363,14 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(k, m, obj_len, erased, budget_s=args.cpu_budget)
+    if world > 1 and backend == "nccl" and args.split_objects > 0:
+        del w  # free this rank's headline batch before the split's buffers
+        torch.cuda.empty_cache()
+        split = batch_split(pg, k, m, obj_len, args.split_objects, world, rank, ctl_device)
+        if rank == 0:
+            line["batch_split"] = split
+            ok = ok and split["parity_ok"]
+    if rank == 0:
         print(json.dumps(line), flush=True)
     if pg:
         pg.destroy_process_group()

@@ -108,7 +108,7 @@ __global__ __launch_bounds__(kBlockThreads, kVecWavesPerSimd) void gf_apply_vec(
     constexpr int U = tile_kib(K);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave =
-        __builtin_amdgcn_readfirstlane(blockIdx.x * (kBlockThreads / 64) + (threadIdx.x >> 6));
+        __builtin_amdgcn_readfirstlane(xcd_block() * (kBlockThreads / 64) + (threadIdx.x >> 6));
     const uint32_t nwaves = gridDim.x * (kBlockThreads / 64);
     const uint32_t tpo = a.tiles_per_obj;
     const bool accumulate = a.accumulate != 0;
@@ -176,9 +176,8 @@ __global__ __launch_bounds__(kPipeBlockThreads, HBEC_PIPE_WAVES_PER_SIMD) void g
     constexpr int U = pipe_u(K);
     constexpr uint64_t TILE = (uint64_t)U * 1024u;
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave =
-        __builtin_amdgcn_readfirstlane(blockIdx.x * (kPipeBlockThreads / 64) + (threadIdx.x >> 6));
     const uint32_t nwaves = gridDim.x * (kPipeBlockThreads / 64);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(xcd_block() * (kPipeBlockThreads / 64) + (threadIdx.x >> 6));
     const uint32_t tpo = a.tiles_per_obj;
     const Tables<K, R> tb = load_tables<K, R>(a.tab);
     uint32_t t = wave;
@@ -219,7 +218,7 @@ __global__ __launch_bounds__(kBlockThreads, kVecWavesPerSimd) void gf_apply_vec_
     constexpr int U = 4;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave =
-        __builtin_amdgcn_readfirstlane(blockIdx.x * (kBlockThreads / 64) + (threadIdx.x >> 6));
+        __builtin_amdgcn_readfirstlane(xcd_block() * (kBlockThreads / 64) + (threadIdx.x >> 6));
     const uint32_t nwaves = gridDim.x * (kBlockThreads / 64);
     const uint32_t tpo = a.tiles_per_obj;
     for (uint32_t t = wave; t < a.n_tiles; t += nwaves) {

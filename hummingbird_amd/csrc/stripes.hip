@@ -71,7 +71,7 @@ __global__ __launch_bounds__(kBlockThreads, 1) void gf_apply_stripes(StripeArgs 
     constexpr int U = stripes_u(K);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave =
-        __builtin_amdgcn_readfirstlane(blockIdx.x * (kBlockThreads / 64) + (threadIdx.x >> 6));
+        __builtin_amdgcn_readfirstlane(xcd_block() * (kBlockThreads / 64) + (threadIdx.x >> 6));
     const uint32_t nw = gridDim.x * (kBlockThreads / 64);
     const uint32_t n = a.n_tiles;
     if (wave >= n) return;

@@ -62,6 +62,8 @@ __global__ __launch_bounds__(kPipeBlockThreads, 1) void gf_verify_pipe(PassArgs 
     constexpr int U = verify_u(K);
     constexpr uint64_t TILE = (uint64_t)U * 1024u;
     const uint32_t lane = threadIdx.x & 63u;
+    // raw block id, not xcd_block(): for this read-only stream the XCD-grouped
+    // order measured 4 % slower at 8+3 and equal at 4+2 (profiles/r01_tune_xcd.jsonl)
     const uint32_t wave =
         __builtin_amdgcn_readfirstlane(blockIdx.x * (kPipeBlockThreads / 64) + (threadIdx.x >> 6));
     const uint32_t nwaves = gridDim.x * (kPipeBlockThreads / 64);

@@ -30,6 +30,8 @@ T4 = BASE + ["HBEC_TILE_MID=4"]
 P = T1 + ["HBEC_USE_PIPE=1"]
 VARIANTS = {
     "cur": ([], {}),
+    "xcd1": ([], {}),
+    "xcd0": (["HBEC_XCD_MAP=0"], {}),
     "prev": (["HBEC_PIPE_LOADS=16", "HBEC_PIPE_BLOCKS_PER_CU=0"], {}),
     "cur_b1": ([], {"HBEC_BLOCKS_PER_CU": "1"}),
     "pl8_b1": (["HBEC_PIPE_LOADS=8"], {"HBEC_BLOCKS_PER_CU": "1"}),

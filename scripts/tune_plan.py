@@ -2,7 +2,7 @@
 """A/B of the stripe-plan and verify kernels' tile depth / grid (one variant
 per process: HBEC_LIB selects the variant library, env the grid override).
 
-    python scripts/tune_plan.py build        # CPU side: tune_build/plan_*/libhbec.so
+    python scripts/tune_plan.py build [v1,v2]  # CPU side: tune_build/plan_*/libhbec.so
     bash   scripts/tune_plan.sh              # GPU side: every variant, 3 rounds
 
 Prints one JSON line per (variant, workload): median ms and % of 8 TB/s.
@@ -27,13 +27,16 @@ VARIANTS = {
     "vf8": ["HBEC_VERIFY_LOADS=8"],
     "vf16": ["HBEC_VERIFY_LOADS=16"],
     "vf32": ["HBEC_VERIFY_LOADS=32"],
+    "xcd0": ["HBEC_XCD_MAP=0"],
 }
 
 
-def build():
+def build(names=None):
     from hummingbird_amd import build as Bd
 
     for name, defs in VARIANTS.items():
+        if names and name not in names:
+            continue
         out = ROOT / "tune_build" / f"plan_{name}"
         Bd.build(defs=defs, lib=out / "libhbec.so", objdir=out / "obj", verbose=False)
         print("built", out, flush=True)
@@ -99,6 +102,6 @@ def run(label):
 
 if __name__ == "__main__":
     if sys.argv[1:2] == ["build"]:
-        build()
+        build(sys.argv[2].split(",") if len(sys.argv) > 2 else None)
     else:
         run(os.environ.get("TUNE_LABEL", "base"))

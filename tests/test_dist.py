@@ -58,3 +58,67 @@ def test_single_process_helpers():
     assert bench.partition(4096, 0) == (0, 4096)
     assert bench.partition(4096, 7) == (7 * 4096, 4096)
     assert bench.max_over_ranks(None, [1.0, 2.0], "cpu") == [1.0, 2.0]
+
+
+def _split_worker(rank, world, port, n_global, row, chunk, q):
+    """scatter_objects / gather_rows (hummingbird_amd/split.py) over gloo with
+    CPU tensors: the same P2P rounds bench.py runs over RCCL for configs[4]."""
+    from hummingbird_amd import split as SP
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        first, n = SP.object_range(n_global, world, rank)
+        batch = None
+        if rank == 0:
+            batch = torch.arange(n_global * row, dtype=torch.int64).remainder(251).to(torch.uint8).view(n_global, row)
+        part = torch.zeros((n, row), dtype=torch.uint8)
+        SP.scatter_objects(dist, batch, part, n_global, chunk_bytes=chunk)
+        want = torch.arange(first * row, (first + n) * row, dtype=torch.int64).remainder(251).to(torch.uint8)
+        got_ok = bool(torch.equal(part.view(-1), want))
+        # "parity": a per-object function of the received rows, gathered back
+        res = (part[:, :3].to(torch.int32) * 7 + rank).to(torch.uint8).contiguous()
+        dest = torch.zeros((n_global, 3), dtype=torch.uint8) if rank == 0 else None
+        SP.gather_rows(dist, res, dest, n_global, chunk_bytes=chunk)
+        gather_ok = True
+        if rank == 0:
+            for r in range(world):
+                f, c = SP.object_range(n_global, world, r)
+                src_rows = batch[f:f + c, :3].to(torch.int32)
+                gather_ok &= bool(torch.equal(dest[f:f + c], (src_rows * 7 + r).to(torch.uint8)))
+        q.put((rank, first, n, got_ok, gather_ok))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_global,chunk", [(2, 8, 64), (3, 10, 48), (3, 2, 1 << 20)])
+def test_batch_split_scatter_gather_gloo(world, n_global, chunk):
+    row = 16  # chunk // row objects per P2P message: several rounds per peer
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_split_worker, args=(r, world, port, n_global, row, chunk, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    res = sorted(q.get(timeout=10) for _ in range(world))
+    assert sum(n for _, _, n, _, _ in res) == n_global
+    assert all(ok and gok for *_, ok, gok in res)
+
+
+def test_object_range_partition():
+    from hummingbird_amd import split as SP
+
+    for n_global in (0, 1, 7, 65536, 65537):
+        for world in (1, 2, 3, 8):
+            parts = [SP.object_range(n_global, world, r) for r in range(world)]
+            assert parts[0][0] == 0
+            for (f0, n0), (f1, _) in zip(parts, parts[1:]):
+                assert f0 + n0 == f1
+            assert sum(n for _, n in parts) == n_global
+            assert max(n for _, n in parts) - min(n for _, n in parts) <= 1
+    assert SP.object_range(65536, 8, 7) == (7 * 8192, 8192)
+    with pytest.raises(ValueError):
+        SP.object_range(4, 0, 0)
