@@ -78,6 +78,9 @@ _SIG = [
     ("hbec_encode_plan", C.c_int, [_P, _P, _P]),
     ("hbec_reconstruct_plan", C.c_int, [_P, _P, _U8P, C.c_int, _P]),
     ("hbec_encode_host", C.c_int, [_P, C.POINTER(Stripe), C.c_uint64]),
+    ("hbec_host_alloc", C.c_int, [C.c_size_t, C.POINTER(_P)]),
+    ("hbec_host_free", None, [_P]),
+    ("hbec_host_device_addr", C.c_int, [_P, C.c_uint64, C.POINTER(C.c_uint64)]),
     ("hbec_reconstruct_host", C.c_int, [_P, C.POINTER(Stripe), C.c_uint64, _U8P, C.c_int]),
     ("hbec_encode_host_md5", C.c_int, [_P, C.POINTER(Stripe), C.c_uint64, _U8P]),
     ("hbec_batcher_new", C.c_int, [_P, C.c_uint64, C.c_uint32, C.POINTER(_P)]),

@@ -13,6 +13,12 @@
 // column pieces.  Everything is synchronous for the caller: when the call
 // returns, parity (encode) or the rebuilt shards (reconstruct) are in the
 // caller's buffers.
+//
+// Zero-copy: stripes that live in pinned, device-mapped host memory
+// (hbec_host_alloc, or any hipHostMalloc / hipHostRegister buffer) skip the
+// ring entirely.  The stripe kernel reads their data shards and writes their
+// parity in place over PCIe, so there is no CPU copy and no DMA call per
+// chunk; only 32-B tile records travel.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -20,6 +26,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <thread>
@@ -185,6 +192,125 @@ void ring_release(Ring* r) {
     g_free_rings.push_back(r);
 }
 
+// ---- pinned host memory (zero-copy host path) ----
+struct PinnedRange {
+    uint64_t len;
+    uint64_t dev;  // device address of the range's first byte
+};
+std::mutex g_pin_mu;
+std::map<uint64_t, PinnedRange> g_pinned;  // host base -> range (hbec_host_alloc)
+
+bool zero_copy_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("HBEC_ZEROCOPY");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+// Device address of host range [p, p + len) when all of it lies in one
+// pinned, device-mapped allocation; 0 otherwise.  hbec_host_alloc ranges are
+// looked up in the registry; other pinned memory is asked of the runtime at
+// both ends of the range.
+uint64_t pinned_device_addr(const void* p, uint64_t len) {
+    const uint64_t h = reinterpret_cast<uint64_t>(p);
+    if (!p || len == 0) return 0;
+    {
+        std::lock_guard<std::mutex> g(g_pin_mu);
+        auto it = g_pinned.upper_bound(h);
+        if (it != g_pinned.begin()) {
+            --it;
+            if (h >= it->first && h + len <= it->first + it->second.len) return it->second.dev + (h - it->first);
+        }
+    }
+    hipPointerAttribute_t a0, a1;
+    if (hipPointerGetAttributes(&a0, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    if (a0.type != hipMemoryTypeHost || !a0.devicePointer) return 0;
+    if (hipPointerGetAttributes(&a1, reinterpret_cast<const uint8_t*>(p) + (len - 1)) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    const uint64_t d0 = reinterpret_cast<uint64_t>(a0.devicePointer);
+    const uint64_t d1 = reinterpret_cast<uint64_t>(a1.devicePointer);
+    if (a1.type != hipMemoryTypeHost || d1 != d0 + (len - 1)) return 0;
+    return d0;
+}
+
+struct ZcStripe {
+    uint64_t dev;  // device address of the stripe base
+    uint64_t shard_len;
+};
+
+// Code pinned stripes in place: tile records (rings of kSlots pinned/device
+// buffers) are the only host->device traffic; the kernel streams the shards
+// over PCIe.  One stream, so records, kernels and their reuse are ordered.
+int zero_copy_run(Ring* ring, const std::vector<ZcStripe>& zs, const std::vector<int>& in_idx,
+                  const std::vector<int>& out_idx, const std::vector<uint8_t>& rows, int cus) {
+    const int K = (int)in_idx.size(), R = (int)out_idx.size();
+    const uint64_t tile = (uint64_t)hbec::stripes_tile_bytes(K);
+    std::vector<hbec::StripeArgs> args;
+    for (int r0 = 0; r0 < R; r0 += 3) {
+        const int Rg = std::min(3, R - r0);
+        hbec::StripeArgs a;
+        std::memset(&a, 0, sizeof(a));
+        for (int j = 0; j < K; ++j) a.in_idx[j] = (uint32_t)in_idx[j];
+        for (int r = 0; r < Rg; ++r) {
+            a.out_idx[r] = (uint32_t)out_idx[r0 + r];
+            for (int j = 0; j < K; ++j) hbec::perm_table(rows[(size_t)(r0 + r) * K + j], a.tab[r][j]);
+        }
+        a.pad_ = (uint32_t)Rg;
+        args.push_back(a);
+    }
+    size_t si = 0;
+    uint64_t off = 0;
+    hipError_t e = hipSuccess;
+    for (int c = 0; si < zs.size(); ++c) {
+        const int slot = c % kSlots;
+        e = hipEventSynchronize(ring->ev_cmp[slot]);  // the slot's previous records are consumed
+        if (e != hipSuccess) return hip_fail(e, "zero-copy slot wait");
+        hbec::TileRec* rec = ring->pin_tiles[slot];
+        uint64_t nt = 0;
+        while (si < zs.size() && nt < ring->tile_cap) {
+            const ZcStripe& z = zs[si];
+            hbec::TileRec& t = rec[nt++];
+            t.in_addr = t.out_addr = z.dev + off;
+            t.in_stride = t.out_stride = (uint32_t)z.shard_len;
+            t.valid = (uint32_t)std::min<uint64_t>(tile, z.shard_len - off);
+            t.pad_ = 0;
+            off += tile;
+            if (off >= z.shard_len) {
+                off = 0;
+                ++si;
+            }
+        }
+        e = hipMemcpyAsync(ring->dev_tiles[slot], rec, nt * sizeof(hbec::TileRec), hipMemcpyHostToDevice,
+                           ring->s_cmp);
+        if (e != hipSuccess) return hip_fail(e, "zero-copy records H2D");
+        for (auto a : args) {
+            const int Rg = (int)a.pad_;
+            a.pad_ = 0;
+            a.tiles = ring->dev_tiles[slot];
+            a.n_tiles = (uint32_t)nt;
+            int bpc = 1;
+            e = hbec::stripes_occupancy(K, Rg, &bpc);
+            if (e != hipSuccess) return hip_fail(e, "stripes occupancy");
+            if (hbec::kPipeBlocksPerCu > 0) bpc = std::min(bpc, hbec::kPipeBlocksPerCu);
+            const uint64_t want = (nt + 3) / 4;
+            const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cus * std::max(1, bpc)));
+            e = hbec::launch_stripes(K, Rg, a, grid, ring->s_cmp);
+            if (e != hipSuccess) return hip_fail(e, "launch gf_apply_stripes (zero-copy)");
+        }
+        e = hipEventRecord(ring->ev_cmp[slot], ring->s_cmp);
+        if (e != hipSuccess) return hip_fail(e, "zero-copy event");
+    }
+    e = hipStreamSynchronize(ring->s_cmp);
+    if (e != hipSuccess) return hip_fail(e, "zero-copy drain");
+    return HBEC_OK;
+}
+
 // Code every stripe: inputs = shards in_idx, outputs = shards out_idx with `rows`.
 // With d_digest (device, n * n_shards * 16 B), also hash every input and
 // output shard of every stripe while it is in the device slot: digest of
@@ -203,6 +329,34 @@ int host_run(const hbec_stripe* stripes, uint64_t n, const std::vector<int>& in_
         Ring* r;
         ~Releaser() { ring_release(r); }
     } rel{ring};
+    // Pinned stripes are coded in place (zero-copy); the rest take the ring.
+    // (Hashing needs every shard on the device, so it always takes the ring.)
+    std::vector<hbec_stripe> staged;
+    if (!d_digest && zero_copy_enabled()) {
+        int top = 0;
+        for (int i : in_idx) top = std::max(top, i);
+        for (int i : out_idx) top = std::max(top, i);
+        std::vector<ZcStripe> zs;
+        for (uint64_t s = 0; s < n; ++s) {
+            const uint64_t S = stripes[s].shard_len;
+            if (S == 0) continue;
+            const bool aligned = (reinterpret_cast<uintptr_t>(stripes[s].base) & 15u) == 0 && S % 16 == 0 &&
+                                 S < (1ull << 32);
+            const uint64_t d = aligned ? pinned_device_addr(stripes[s].base, (uint64_t)(top + 1) * S) : 0;
+            if (d && (d & 15u) == 0) zs.push_back({d, S});
+            else staged.push_back(stripes[s]);
+        }
+        if (!zs.empty()) {
+            hipDeviceProp_t prop;
+            hipError_t e = hipGetDeviceProperties(&prop, ring->dev);
+            if (e != hipSuccess) return hip_fail(e, "hipGetDeviceProperties");
+            rc = zero_copy_run(ring, zs, in_idx, out_idx, rows, prop.multiProcessorCount);
+            if (rc) return rc;
+        }
+        if (staged.empty()) return HBEC_OK;
+        stripes = staged.data();
+        n = staged.size();
+    }
     const uint64_t tile = (uint64_t)hbec::stripes_tile_bytes(K);
     // max columns per piece so that K*lpad fits the IN slot and R*lpad the OUT slot
     const uint64_t max_cols = (std::min(ring->in_cap / K, ring->out_cap / R) / 16) * 16;
@@ -424,6 +578,41 @@ int hbec::host_threads() {
 }
 
 extern "C" {
+
+int hbec_host_alloc(size_t bytes, void** out) {
+    if (!out || bytes == 0) return fail(HBEC_ERR_INVALID_ARG, "null out or zero size");
+    *out = nullptr;
+    void* h = nullptr;
+    hipError_t e = hipHostMalloc(&h, bytes, hipHostMallocDefault);
+    if (e != hipSuccess) return hip_fail(e, "hipHostMalloc");
+    void* d = nullptr;
+    e = hipHostGetDevicePointer(&d, h, 0);
+    if (e != hipSuccess || !d) {
+        (void)hipHostFree(h);
+        return hip_fail(e != hipSuccess ? e : hipErrorInvalidValue, "hipHostGetDevicePointer");
+    }
+    {
+        std::lock_guard<std::mutex> g(g_pin_mu);
+        g_pinned[reinterpret_cast<uint64_t>(h)] = PinnedRange{(uint64_t)bytes, reinterpret_cast<uint64_t>(d)};
+    }
+    *out = h;
+    return HBEC_OK;
+}
+
+void hbec_host_free(void* p) {
+    if (!p) return;
+    {
+        std::lock_guard<std::mutex> g(g_pin_mu);
+        g_pinned.erase(reinterpret_cast<uint64_t>(p));
+    }
+    (void)hipHostFree(p);
+}
+
+int hbec_host_device_addr(const void* p, uint64_t len, uint64_t* dev) {
+    if (!dev) return fail(HBEC_ERR_INVALID_ARG, "null out");
+    *dev = pinned_device_addr(p, len);
+    return HBEC_OK;
+}
 
 int hbec_encode_host(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n_stripes) {
     if (!codec || (n_stripes && !stripes)) return fail(HBEC_ERR_INVALID_ARG, "null argument");

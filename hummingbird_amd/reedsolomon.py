@@ -254,3 +254,40 @@ class Batcher:
 def New(data_shards: int, parity_shards: int) -> Encoder:
     """reedsolomon.New (ecutils.go:27,77,135)."""
     return Encoder(data_shards, parity_shards)
+
+
+class HostBuffer:
+    """Pinned, device-mapped host memory from ``hbec_host_alloc`` — what the
+    cgo shim would hand ecSplit as its databuf (ecutils.go:31-35) so that
+    ``EncodeStripes`` / ``ReconstructStripes`` code the stripes in place over
+    PCIe (zero-copy) instead of staging them through the pinned ring.
+
+    ``.array`` is a numpy uint8 view; keep the HostBuffer alive while it is used."""
+
+    def __init__(self, nbytes: int):
+        self._p = C.c_void_p()
+        check(N.lib().hbec_host_alloc(int(nbytes), C.byref(self._p)))
+        self.nbytes = int(nbytes)
+        self.array = np.ctypeslib.as_array(C.cast(self._p, C.POINTER(C.c_uint8)), shape=(self.nbytes,))
+
+    @property
+    def ptr(self) -> int:
+        return self._p.value
+
+    def free(self) -> None:
+        if self._p and self._p.value and N._lib is not None:
+            self.array = None
+            N._lib.hbec_host_free(self._p)
+            self._p = C.c_void_p()
+
+    def __del__(self):
+        self.free()
+
+
+def host_device_addr(buf) -> int:
+    """Device address of a host buffer when all of it is pinned and device
+    mapped (the zero-copy condition), else 0."""
+    a = _as_array(buf)
+    out = C.c_uint64()
+    check(N.lib().hbec_host_device_addr(C.c_void_p(a.ctypes.data), a.size, C.byref(out)))
+    return out.value

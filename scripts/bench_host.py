@@ -104,12 +104,19 @@ def pipelined(op: str, n_obj=4096, chunk=256, reps=3):
             "objects_per_s": round(n_obj / t, 1)}
 
 
-def library_host_path(op: str, n_obj=4096, reps=3):
-    """hbec_encode_host / hbec_reconstruct_host on pageable numpy stripes (the
-    library's own pinned ring: CPU gather -> H2D -> kernel -> D2H -> scatter)."""
+def library_host_path(op: str, n_obj=4096, reps=3, mem="pageable"):
+    """hbec_encode_host / hbec_reconstruct_host.  mem="pageable": numpy stripes
+    through the library's pinned ring (CPU gather -> H2D -> kernel -> D2H ->
+    scatter).  mem="pinned": stripes in hbec_host_alloc memory, coded in place
+    by the GPU over PCIe (zero-copy, no CPU copies)."""
     k, m, S = 4, 2, MiB // 4
     enc = RS.New(k, m)
-    pool = np.empty((n_obj, (k + m) * S), dtype=np.uint8)
+    hb = None
+    if mem == "pinned":
+        hb = RS.HostBuffer(n_obj * (k + m) * S)
+        pool = hb.array.reshape(n_obj, (k + m) * S)
+    else:
+        pool = np.empty((n_obj, (k + m) * S), dtype=np.uint8)
     from oracle import coracle as CO
     pool[:, :k * S] = CO.fill_objects(0, n_obj, k * S)
     stripes = [pool[i] for i in range(n_obj)]
@@ -127,14 +134,20 @@ def library_host_path(op: str, n_obj=4096, reps=3):
     check = pool[7].copy()
     want = CO.encode_batch(k, m, check[None, :k * S])[0][0]
     assert np.array_equal(check[k * S:], want)
-    return {"measure": f"library_host_path_{op}_pageable", "objects": n_obj, "seconds": round(t, 4),
-            "object_data_GiB_s": round(n_obj * k * S / t / GiB, 2),
-            "algorithmic_GiB_s": round(n_obj * (k + 2) * S / t / GiB, 2), "objects_per_s": round(n_obj / t, 1)}
+    res = {"measure": f"library_host_path_{op}_{mem}", "objects": n_obj, "seconds": round(t, 4),
+           "object_data_GiB_s": round(n_obj * k * S / t / GiB, 2),
+           "algorithmic_GiB_s": round(n_obj * (k + 2) * S / t / GiB, 2),
+           "pcie_GB_s": round(n_obj * (k + 2) * S / t / 1e9, 2), "objects_per_s": round(n_obj / t, 1)}
+    del stripes, pool
+    if hb is not None:
+        hb.free()
+    return res
 
 
-def batched_callers(n_threads=64, per_thread=32):
+def batched_callers(n_threads=64, per_thread=32, mem="pageable"):
     """Many concurrent callers, one 1 MiB object each per call, through the
-    batching driver (what concurrent Stabilize goroutines would do)."""
+    batching driver (what concurrent Stabilize goroutines would do).
+    mem="pinned": the callers' stripes are hbec_host_alloc buffers (zero-copy)."""
     import threading
 
     k, m, S = 4, 2, MiB // 4
@@ -142,7 +155,12 @@ def batched_callers(n_threads=64, per_thread=32):
     bat = RS.Batcher(enc, max_batch_bytes=96 << 20, max_wait_us=300)
     from oracle import coracle as CO
     n = n_threads * per_thread
-    pool = np.empty((n, (k + m) * S), dtype=np.uint8)
+    hb = None
+    if mem == "pinned":
+        hb = RS.HostBuffer(n * (k + m) * S)
+        pool = hb.array.reshape(n, (k + m) * S)
+    else:
+        pool = np.empty((n, (k + m) * S), dtype=np.uint8)
     pool[:, :k * S] = CO.fill_objects(0, n, k * S)
 
     def worker(t):
@@ -161,7 +179,10 @@ def batched_callers(n_threads=64, per_thread=32):
     bat.close()
     want = CO.encode_batch(k, m, pool[n - 1:, :k * S])[0][0]
     assert np.array_equal(pool[n - 1, k * S:], want)
-    return {"measure": "batcher_concurrent_Encode_1MiB", "threads": n_threads, "objects": n,
+    del pool
+    if hb is not None:
+        hb.free()
+    return {"measure": f"batcher_concurrent_Encode_1MiB_{mem}", "threads": n_threads, "objects": n,
             "seconds": round(t, 4), "object_data_GiB_s": round(n * k * S / t / GiB, 2),
             "us_per_object": round(t / n * 1e6, 1), "batches": st["batches"]}
 
@@ -259,10 +280,16 @@ def per_call(n_calls=200):
 
 def main():
     torch.cuda.set_device(0)
-    for r in (pipelined("encode"), pipelined("reconstruct"), library_host_path("encode"),
-              library_host_path("reconstruct"), library_host_path_md5(), batched_callers(), batched_callers_md5(),
-              auditor_pass(), per_call()):
-        print(json.dumps(r), flush=True)
+    steps = [lambda: pipelined("encode"), lambda: pipelined("reconstruct"),
+             lambda: library_host_path("encode"), lambda: library_host_path("reconstruct"),
+             lambda: library_host_path("encode", mem="pinned"), lambda: library_host_path("reconstruct", mem="pinned"),
+             library_host_path_md5, batched_callers, lambda: batched_callers(mem="pinned"), batched_callers_md5,
+             auditor_pass, per_call]
+    only = sys.argv[1:]
+    for i, f in enumerate(steps):
+        if only and str(i) not in only:
+            continue
+        print(json.dumps(f()), flush=True)
 
 
 if __name__ == "__main__":

@@ -514,6 +514,80 @@ def test_host_path_encode_reconstruct(k, m, sizes):
             assert np.array_equal(got, w), missing
 
 
+def _pinned_stripes(buf, k, m, sizes, seed, gap=0):
+    """Stripes laid out back to back (16-B aligned starts, `gap` bytes apart)
+    inside one pinned host buffer's numpy view."""
+    out, off = [], 0
+    for i, size in enumerate(sizes):
+        s = O.ec_shard_length(size, k)
+        st = buf[off:off + (k + m) * s]
+        st[:] = 0
+        st[:size] = CO.fill_objects(seed + i, 1, size)[0]
+        out.append(st)
+        off = (off + (k + m) * s + gap + 15) // 16 * 16
+    return out
+
+
+@pytest.mark.parametrize("k,m,sizes", [
+    (4, 2, [MiB] * 40 + [4096, 1001, 16 * 7]),      # 1001 -> S=251: unaligned, takes the ring
+    (8, 3, [4096, MiB, 4096, 3 * MiB + 8, 1]),
+    (3, 5, [3000 * 16, 30000 * 16]),                # more outputs than inputs, 2 row groups
+])
+def test_host_path_zero_copy_pinned(k, m, sizes):
+    """Stripes in hbec_host_alloc memory are coded in place by the GPU (no
+    staging); the batch also mixes in pageable stripes, which take the ring."""
+    enc = RS.New(k, m)
+    total = sum((k + m) * O.ec_shard_length(x, k) + 16 for x in sizes) + 16
+    hb = RS.HostBuffer(total)
+    pinned = _pinned_stripes(hb.array, k, m, sizes, seed=3)
+    pageable = _host_stripes(k, m, [MiB, 5000], seed=99)
+    assert all(RS.host_device_addr(st) != 0 for st in pinned)
+    assert all(RS.host_device_addr(st) == 0 for st in pageable)
+    stripes = pinned[:len(pinned) // 2] + pageable + pinned[len(pinned) // 2:]
+    want = _encoded_copy(k, m, stripes)
+    enc.EncodeStripes(stripes)
+    for got, w in zip(stripes, want):
+        assert np.array_equal(got, w)
+    for missing in [tuple(range(min(m, 3))), (0, k)]:
+        for st in stripes:
+            s = st.size // (k + m)
+            for i in missing:
+                st[i * s:(i + 1) * s] = 0x5A
+        enc.ReconstructStripes(stripes, [0 if i in missing else 1 for i in range(k + m)])
+        for got, w in zip(stripes, want):
+            assert np.array_equal(got, w), missing
+    del stripes, pinned
+    hb.free()
+
+
+def test_host_path_zero_copy_foreign_pinned_memory():
+    """Pinned memory the library did not allocate (torch pin_memory ->
+    hipHostMalloc) is recognised through the runtime's pointer attributes."""
+    k, m, S, n = 4, 2, MiB // 4, 64
+    host = torch.zeros((n, (k + m) * S), dtype=torch.uint8).pin_memory()
+    arr = host.numpy()
+    objs = CO.fill_objects(7, n, k * S)
+    arr[:, :k * S] = objs
+    rows = [arr[i] for i in range(n)]
+    assert RS.host_device_addr(rows[0]) != 0
+    enc = RS.New(k, m)
+    enc.EncodeStripes(rows)
+    want, _ = CO.encode_batch(k, m, objs, threads=CO.cpu_threads())
+    assert np.array_equal(arr[:, k * S:], want)
+    arr[:, :2 * S] = 0
+    enc.ReconstructStripes(rows, [0, 0, 1, 1, 1, 1])
+    assert np.array_equal(arr[:, :k * S], objs)
+
+
+def test_host_alloc_errors_and_ranges():
+    with pytest.raises(RS.ErrInvalidArg):
+        RS.HostBuffer(0)
+    hb = RS.HostBuffer(4096)
+    assert RS.host_device_addr(hb.array[16:4096]) == RS.host_device_addr(hb.array) + 16
+    hb.free()
+    hb.free()  # idempotent
+
+
 def test_host_path_rejects_wide_k():
     enc = RS.New(10, 2)
     with pytest.raises(RS.ErrInvalidArg):
