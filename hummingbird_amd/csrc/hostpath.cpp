@@ -252,6 +252,7 @@ int zero_copy_run(Ring* ring, const std::vector<ZcStripe>& zs, const std::vector
     const int K = (int)in_idx.size(), R = (int)out_idx.size();
     const uint64_t tile = (uint64_t)hbec::stripes_tile_bytes(K);
     std::vector<hbec::StripeArgs> args;
+    std::vector<int> rg;  // output rows of each group (<= 3 per launch)
     for (int r0 = 0; r0 < R; r0 += 3) {
         const int Rg = std::min(3, R - r0);
         hbec::StripeArgs a;
@@ -261,7 +262,7 @@ int zero_copy_run(Ring* ring, const std::vector<ZcStripe>& zs, const std::vector
             a.out_idx[r] = (uint32_t)out_idx[r0 + r];
             for (int j = 0; j < K; ++j) hbec::perm_table(rows[(size_t)(r0 + r) * K + j], a.tab[r][j]);
         }
-        a.pad_ = (uint32_t)Rg;
+        rg.push_back(Rg);
         args.push_back(a);
     }
     size_t si = 0;
@@ -289,9 +290,9 @@ int zero_copy_run(Ring* ring, const std::vector<ZcStripe>& zs, const std::vector
         e = hipMemcpyAsync(ring->dev_tiles[slot], rec, nt * sizeof(hbec::TileRec), hipMemcpyHostToDevice,
                            ring->s_cmp);
         if (e != hipSuccess) return hip_fail(e, "zero-copy records H2D");
-        for (auto a : args) {
-            const int Rg = (int)a.pad_;
-            a.pad_ = 0;
+        for (size_t gi = 0; gi < args.size(); ++gi) {
+            auto a = args[gi];
+            const int Rg = rg[gi];
             a.tiles = ring->dev_tiles[slot];
             a.n_tiles = (uint32_t)nt;
             int bpc = 1;
@@ -421,6 +422,7 @@ int host_run(const hbec_stripe* stripes, uint64_t n, const std::vector<int>& in_
 
     // kernel arguments per row group (<= 3 outputs per launch)
     std::vector<hbec::StripeArgs> args;
+    std::vector<int> rg;  // output rows of each group (<= 3 per launch)
     for (int r0 = 0; r0 < R; r0 += 3) {
         const int Rg = std::min(3, R - r0);
         hbec::StripeArgs a;
@@ -430,7 +432,7 @@ int host_run(const hbec_stripe* stripes, uint64_t n, const std::vector<int>& in_
             a.out_idx[r] = (uint32_t)(r0 + r);
             for (int j = 0; j < K; ++j) hbec::perm_table(rows[(size_t)(r0 + r) * K + j], a.tab[r][j]);
         }
-        a.pad_ = (uint32_t)Rg;  // carries the group's row count to the launch below
+        rg.push_back(Rg);
         args.push_back(a);
     }
     int cus = 0;
@@ -499,9 +501,9 @@ int host_run(const hbec_stripe* stripes, uint64_t n, const std::vector<int>& in_
         if (e == hipSuccess) e = hipEventRecord(ring->ev_h2d[slot], ring->s_h2d);
         if (e == hipSuccess) e = hipStreamWaitEvent(ring->s_cmp, ring->ev_h2d[slot], 0);
         if (e != hipSuccess) return hip_fail(e, "host path H2D");
-        for (auto a : args) {
-            const int Rg = (int)a.pad_;
-            a.pad_ = 0;
+        for (size_t gi = 0; gi < args.size(); ++gi) {
+            auto a = args[gi];
+            const int Rg = rg[gi];
             a.tiles = ring->dev_tiles[slot];
             a.n_tiles = (uint32_t)nt;
             int bpc = 1;
