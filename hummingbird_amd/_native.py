@@ -83,6 +83,11 @@ _SIG = [
     ("hbec_host_device_addr", C.c_int, [_P, C.c_uint64, C.POINTER(C.c_uint64)]),
     ("hbec_reconstruct_host", C.c_int, [_P, C.POINTER(Stripe), C.c_uint64, _U8P, C.c_int]),
     ("hbec_encode_host_md5", C.c_int, [_P, C.POINTER(Stripe), C.c_uint64, _U8P]),
+    ("hbec_device_count", C.c_int, [C.POINTER(C.c_int)]),
+    ("hbec_set_device", C.c_int, [C.c_int]),
+    ("hbec_encode_host_devices", C.c_int, [_P, C.POINTER(Stripe), C.c_uint64, C.POINTER(C.c_int), C.c_int]),
+    ("hbec_reconstruct_host_devices", C.c_int,
+     [_P, C.POINTER(Stripe), C.c_uint64, _U8P, C.c_int, C.POINTER(C.c_int), C.c_int]),
     ("hbec_batcher_new", C.c_int, [_P, C.c_uint64, C.c_uint32, C.POINTER(_P)]),
     ("hbec_batcher_free", None, [_P]),
     ("hbec_batcher_encode", C.c_int, [_P, C.POINTER(Stripe)]),

@@ -29,6 +29,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -570,6 +571,61 @@ int host_run(const hbec_stripe* stripes, uint64_t n, const std::vector<int>& in_
     return HBEC_OK;
 }
 
+// One process, several GPUs (how a single object server would use a node):
+// stripes are cut into contiguous runs of about equal bytes, one per device,
+// and each run is coded by its own host thread on its device's ring (rings
+// are per device), all at once.  Stripes are independent (ecutils.go:38-70),
+// so there is no exchange between devices.
+template <typename Fn>
+int run_on_devices(const hbec_stripe* stripes, uint64_t n, const int* devices, int n_devices, Fn fn) {
+    if (n && !stripes) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+    std::vector<int> devs;
+    if (devices) {
+        if (n_devices <= 0) return fail(HBEC_ERR_INVALID_ARG, "n_devices must be > 0");
+        devs.assign(devices, devices + n_devices);
+    } else {
+        int count = 0;
+        hipError_t e = hipGetDeviceCount(&count);
+        if (e != hipSuccess) return hip_fail(e, "hipGetDeviceCount");
+        for (int d = 0; d < count; ++d) devs.push_back(d);
+        if (n_devices > 0 && n_devices < count) devs.resize(n_devices);
+    }
+    if (devs.empty()) return fail(HBEC_ERR_DEVICE, "no device");
+    if (n == 0) return HBEC_OK;
+    uint64_t total = 0;
+    for (uint64_t i = 0; i < n; ++i) total += stripes[i].shard_len;
+    // contiguous runs of ~total / D shard bytes
+    std::vector<uint64_t> cut(devs.size() + 1, n);
+    cut[0] = 0;
+    {
+        uint64_t acc = 0;
+        size_t d = 1;
+        for (uint64_t i = 0; i < n && d < devs.size(); ++i) {
+            acc += stripes[i].shard_len;
+            while (d < devs.size() && acc * devs.size() >= total * d) cut[d++] = i + 1;
+        }
+    }
+    std::vector<int> rcs(devs.size(), HBEC_OK);
+    std::vector<std::string> errs(devs.size());
+    std::vector<std::thread> th;
+    for (size_t d = 0; d < devs.size(); ++d) {
+        if (cut[d + 1] <= cut[d]) continue;
+        th.emplace_back([&, d] {
+            hipError_t e = hipSetDevice(devs[d]);
+            if (e != hipSuccess) {
+                rcs[d] = hip_fail(e, "hipSetDevice");
+            } else {
+                rcs[d] = fn(stripes + cut[d], cut[d + 1] - cut[d]);
+            }
+            if (rcs[d]) errs[d] = hbec_last_error();
+        });
+    }
+    for (auto& t : th) t.join();
+    for (size_t d = 0; d < devs.size(); ++d)
+        if (rcs[d]) return fail(rcs[d], "device " + std::to_string(devs[d]) + ": " + errs[d]);
+    return HBEC_OK;
+}
+
 }  // namespace
 
 int hbec::host_threads() {
@@ -662,6 +718,35 @@ int hbec_encode_host_md5(hbec_codec* codec, const hbec_stripe* stripes, uint64_t
     (void)hipStreamSynchronize(st);
     (void)hipStreamDestroy(st);
     return rc;
+}
+
+int hbec_device_count(int* n) {
+    if (!n) return fail(HBEC_ERR_INVALID_ARG, "null out");
+    *n = 0;
+    hipError_t e = hipGetDeviceCount(n);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDeviceCount");
+    return HBEC_OK;
+}
+
+int hbec_set_device(int device) {
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+    return HBEC_OK;
+}
+
+int hbec_encode_host_devices(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n_stripes, const int* devices,
+                             int n_devices) {
+    return run_on_devices(stripes, n_stripes, devices, n_devices, [codec](const hbec_stripe* s, uint64_t n) {
+        return hbec_encode_host(codec, s, n);
+    });
+}
+
+int hbec_reconstruct_host_devices(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n_stripes,
+                                  const uint8_t* present, int data_only, const int* devices, int n_devices) {
+    if (!present) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+    return run_on_devices(stripes, n_stripes, devices, n_devices, [=](const hbec_stripe* s, uint64_t n) {
+        return hbec_reconstruct_host(codec, s, n, present, data_only);
+    });
 }
 
 int hbec_reconstruct_host(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n_stripes,

@@ -186,6 +186,18 @@ class Encoder:
         return [[raw[16 * (s * self.Shards + i):16 * (s * self.Shards + i + 1)].hex() for i in range(self.Shards)]
                 for s in range(n)]
 
+    def EncodeStripesDevices(self, stripes, devices=None) -> None:
+        """EncodeStripes spread over several GPUs (one host thread each);
+        devices=None: every visible device."""
+        d, nd = _devices(devices)
+        check(N.lib().hbec_encode_host_devices(self._h, self._stripes(stripes), len(stripes), d, nd))
+
+    def ReconstructStripesDevices(self, stripes, present, data_only: bool = False, devices=None) -> None:
+        p = (C.c_uint8 * self.Shards)(*[1 if x else 0 for x in present])
+        d, nd = _devices(devices)
+        check(N.lib().hbec_reconstruct_host_devices(self._h, self._stripes(stripes), len(stripes), p, int(data_only),
+                                                    d, nd))
+
     def ReconstructStripes(self, stripes, present, data_only: bool = False) -> None:
         p = (C.c_uint8 * self.Shards)(*[1 if x else 0 for x in present])
         check(N.lib().hbec_reconstruct_host(self._h, self._stripes(stripes), len(stripes), p, int(data_only)))
@@ -291,3 +303,16 @@ def host_device_addr(buf) -> int:
     out = C.c_uint64()
     check(N.lib().hbec_host_device_addr(C.c_void_p(a.ctypes.data), a.size, C.byref(out)))
     return out.value
+
+
+def _devices(devices):
+    if devices is None:
+        return None, 0
+    arr = (C.c_int * len(devices))(*[int(x) for x in devices])
+    return arr, len(devices)
+
+
+def device_count() -> int:
+    n = C.c_int()
+    check(N.lib().hbec_device_count(C.byref(n)))
+    return n.value

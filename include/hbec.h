@@ -211,6 +211,18 @@ void hbec_host_free(void* p);
 int hbec_host_device_addr(const void* p, uint64_t len, uint64_t* dev);
 int hbec_reconstruct_host(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n_stripes, const uint8_t* present,
                           int data_only);
+/* Several GPUs from one process (a node's object server): the stripes are
+ * cut into contiguous runs of about equal bytes, one per device, coded
+ * concurrently by one host thread per device (each on its own ring /
+ * zero-copy path).  devices = NULL: the first n_devices visible devices
+ * (n_devices <= 0: all).  Synchronous.  hbec_set_device selects the calling
+ * thread's device for the device-batch and single-device host calls. */
+int hbec_device_count(int* n);
+int hbec_set_device(int device);
+int hbec_encode_host_devices(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n_stripes, const int* devices,
+                             int n_devices);
+int hbec_reconstruct_host_devices(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n_stripes,
+                                  const uint8_t* present, int data_only, const int* devices, int n_devices);
 /* hbec_encode_host + ShardHash (indexdb.go:746-753) of every data and parity
  * shard of every stripe, computed on the GPU while the stripe is in the device
  * slot (hashing of one chunk overlaps the copies of the next): digests (host)

@@ -588,6 +588,41 @@ def test_host_alloc_errors_and_ranges():
     hb.free()  # idempotent
 
 
+@pytest.mark.parametrize("devices", [None, [0], [0, 0], [0, 0, 0]])
+def test_host_path_devices_partition(devices):
+    """hbec_*_host_devices: stripes cut into per-device runs coded by one host
+    thread each (here several threads share device 0, each with its own ring),
+    pageable and pinned stripes mixed."""
+    k, m = 4, 2
+    sizes = [MiB] * 9 + [4096, 1001, 3 * MiB + 8, 7]
+    enc = RS.New(k, m)
+    hb = RS.HostBuffer(sum((k + m) * O.ec_shard_length(x, k) + 16 for x in sizes[:6]) + 16)
+    stripes = _pinned_stripes(hb.array, k, m, sizes[:6], seed=11) + _host_stripes(k, m, sizes[6:], seed=17)
+    want = _encoded_copy(k, m, stripes)
+    enc.EncodeStripesDevices(stripes, devices)
+    for got, w in zip(stripes, want):
+        assert np.array_equal(got, w)
+    missing = (1, k)
+    for st in stripes:
+        sl = st.size // (k + m)
+        for i in missing:
+            st[i * sl:(i + 1) * sl] = 0x77
+    enc.ReconstructStripesDevices(stripes, [0 if i in missing else 1 for i in range(k + m)], devices=devices)
+    for got, w in zip(stripes, want):
+        assert np.array_equal(got, w)
+    del stripes
+    hb.free()
+
+
+def test_host_path_devices_errors():
+    enc = RS.New(4, 2)
+    st = _host_stripes(4, 2, [4096])
+    with pytest.raises(RS.ReedSolomonError):
+        enc.EncodeStripesDevices(st, devices=[RS.device_count() + 3])
+    assert RS.device_count() >= 1
+    enc.EncodeStripesDevices([], devices=[0])
+
+
 def test_host_path_rejects_wide_k():
     enc = RS.New(10, 2)
     with pytest.raises(RS.ErrInvalidArg):
