@@ -235,6 +235,42 @@ def batch_split(pg, k, m, obj_len, n_global, world, rank, ctl_device):
     }
 
 
+def host_path(k, m, obj_len, n_obj=2048, passes=5, all_devices=False):
+    """The path as the object server runs it: stripes (ecSplit databuf layout,
+    ecutils.go:31-35) in pinned host memory from hbec_host_alloc, coded in
+    place over PCIe by Encoder.EncodeStripes (zero-copy host path).  With
+    all_devices, one process drives every visible GPU (hbec_encode_host_devices).
+    PCIe-inclusive; reported beside `value`, never as it."""
+    s = obj_len // k
+    enc = RS.New(k, m)
+    hb = RS.HostBuffer(n_obj * (k + m) * s)
+    try:
+        rows = hb.array.reshape(n_obj, (k + m) * s)
+        dev = torch.empty((n_obj, obj_len), dtype=torch.uint8, device="cuda")
+        B.fill_splitmix(dev, obj_len)
+        par = torch.empty((n_obj, m * s), dtype=torch.uint8, device="cuda")
+        B.encode_objects(enc, dev, par, s)
+        rows[:, :k * s] = dev.cpu().numpy()
+        want = par.cpu().numpy()
+        del dev, par
+        stripes = [rows[i] for i in range(n_obj)]
+        run = (lambda: enc.EncodeStripesDevices(stripes)) if all_devices else (lambda: enc.EncodeStripes(stripes))
+        run()
+        ok = bool((rows[:, k * s:] == want).all())
+        ts = []
+        for _ in range(passes):
+            t0 = time.perf_counter()
+            run()
+            ts.append(time.perf_counter() - t0)
+        t = sorted(ts)[len(ts) // 2]
+        return {"op": "encode", "objects": n_obj, "memory": "pinned (hbec_host_alloc), zero-copy",
+                "devices": RS.device_count() if all_devices else 1,
+                "ms": round(t * 1e3, 3), "object_data_GiB_s": round(n_obj * obj_len / t / GiB, 2),
+                "pcie_GB_s": round(n_obj * (k + m) * s / t / 1e9, 2), "parity_ok": ok}
+    finally:
+        hb.free()
+
+
 def cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -253,6 +289,8 @@ def main():
     ap.add_argument("--objects", type=int, default=4096, help="objects per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--no-host-path", action="store_true",
+                    help="skip the PCIe-inclusive host-path line (pinned stripes, zero-copy)")
     ap.add_argument("--split-objects", type=int, default=65536,
                     help="N>1 on RCCL: objects in the batch split from rank 0 (BASELINE configs[4]); 0 = skip")
     args = ap.parse_args()
@@ -370,6 +408,16 @@ def main():
         if rank == 0:
             line["batch_split"] = split
             ok = ok and split["parity_ok"]
+    if not args.no_host_path:
+        # rank 0 drives every GPU of the node from one process; the others wait
+        if rank == 0:
+            try:
+                line["host_path"] = host_path(k, m, obj_len, all_devices=world > 1)
+                ok = ok and line["host_path"]["parity_ok"]
+            except Exception as e:  # noqa: BLE001 - reported; never blocks the other ranks
+                line["host_path"] = {"error": f"{type(e).__name__}: {e}"[:200]}
+        if pg:
+            pg.barrier()
     if rank == 0:
         print(json.dumps(line), flush=True)
     if pg:
