@@ -36,6 +36,10 @@ class Stripe(C.Structure):
     _fields_ = [("base", C.c_void_p), ("shard_len", C.c_uint64)]
 
 
+class Object(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("parity", C.c_void_p), ("shard_len", C.c_uint64)]
+
+
 READ_FN = C.CFUNCTYPE(C.c_int64, C.c_void_p, C.POINTER(C.c_uint8), C.c_size_t)
 WRITE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint8), C.c_size_t)
 
@@ -72,6 +76,7 @@ _SIG = [
      [C.c_int, C.c_int, _U8P, C.POINTER(View), C.POINTER(View), C.c_uint64, C.c_uint64, _P]),
     ("hbec_fill_splitmix", C.c_int, [_P, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, _P]),
     ("hbec_plan_stripes", C.c_int, [_P, C.POINTER(Stripe), C.c_uint64, C.POINTER(_P)]),
+    ("hbec_plan_objects", C.c_int, [_P, C.POINTER(Object), C.c_uint64, C.POINTER(_P)]),
     ("hbec_plan_free", None, [_P]),
     ("hbec_plan_info", C.c_int,
      [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_int), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),

@@ -100,13 +100,22 @@ class StripePlan:
     back to back (ecSplit's databuf layout).  Buffers must outlive the plan's
     queued work."""
 
-    def __init__(self, enc: Encoder, stripes):
+    def __init__(self, enc: Encoder, stripes=None, objects=None):
+        """stripes = [(base, shard_len)] (ecSplit databuf layout), or
+        objects = [(data, parity, shard_len)] (data and parity in separate
+        regions, hbec_plan_objects)."""
         self.enc = enc
+        self._h = C.c_void_p()
+        if objects is not None:
+            arr = (N.Object * max(1, len(objects)))()
+            for i, (d, p, s) in enumerate(objects):
+                arr[i].data, arr[i].parity, arr[i].shard_len = d, p, s
+            check(N.lib().hbec_plan_objects(enc.handle, arr, len(objects), C.byref(self._h)))
+            return
         arr = (N.Stripe * max(1, len(stripes)))()
         for i, (b, s) in enumerate(stripes):
             arr[i].base = b
             arr[i].shard_len = s
-        self._h = C.c_void_p()
         check(N.lib().hbec_plan_stripes(enc.handle, arr, len(stripes), C.byref(self._h)))
 
     def __del__(self):

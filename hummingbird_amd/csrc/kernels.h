@@ -102,12 +102,18 @@ struct TileRec {
     uint32_t pad_;
 };
 
+// Stripe plans and the host ring: input j of a tile at in_addr +
+// in_idx[j]*in_stride, output r at out_addr + out_idx[r]*out_stride.
+// Object plans (split launches): every tile has two bases, A = (in_addr,
+// in_stride) for data shards and B = (out_addr, out_stride) for parity
+// shards; bit j of in_sel / out_sel picks B for input j / output r.
 struct StripeArgs {
     const TileRec* tiles;
     uint32_t n_tiles;
-    uint32_t pad_;
-    uint32_t in_idx[kMaxK];   // shard index read as input j
-    uint32_t out_idx[kMaxR];  // shard index written as output r
+    uint32_t split;           // 1: object plan (in_sel / out_sel apply)
+    uint32_t in_idx[kMaxK];   // shard index (within its base) read as input j
+    uint32_t out_idx[kMaxR];  // shard index (within its base) written as output r
+    uint32_t in_sel, out_sel;
     uint32_t tab[kMaxR][kMaxK][5];
 };
 

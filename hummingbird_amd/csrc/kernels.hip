@@ -169,6 +169,9 @@ __device__ __forceinline__ void compute_store_tile(const u32x4 (&x)[U][K], const
 #ifndef HBEC_PIPE_WAVES_PER_SIMD
 #define HBEC_PIPE_WAVES_PER_SIMD 1
 #endif
+#ifndef HBEC_PIPE_SLEEP
+#define HBEC_PIPE_SLEEP 6  // x 64 cycles
+#endif
 
 template <int K, int R>
 __global__ __launch_bounds__(kPipeBlockThreads, HBEC_PIPE_WAVES_PER_SIMD) void gf_apply_vec_pipe(PassArgs a) {
@@ -192,6 +195,11 @@ __global__ __launch_bounds__(kPipeBlockThreads, HBEC_PIPE_WAVES_PER_SIMD) void g
         const uint32_t obj_n = tn / tpo;
         const uint64_t base_n = (uint64_t)(tn - obj_n * tpo) * TILE;
         load_tile<K, R, U>(nxt, a, obj_n, base_n + lane * 16u);
+        // Pace the wave: ~380 cycles of s_sleep after issuing the next tile's
+        // loads lowers the requests in flight at the HBM; 4+2: +1.0-1.5 %
+        // (flat from 6 to 8, a cliff from 12), 8+3 (longer tiles): no effect
+        // (profiles/r01_tune_sleep.jsonl)
+        if (HBEC_PIPE_SLEEP > 0 && K <= 4) __builtin_amdgcn_s_sleep(HBEC_PIPE_SLEEP);
         if (base + TILE <= a.shard_len)
             compute_store_tile<K, R, U>(cur, a, tb, obj, base + lane * 16u, true);
         else

@@ -27,6 +27,10 @@ struct hbec_plan {
     uint64_t n_tiles = 0;
     std::vector<hbec_stripe> tiled;     // stripes covered by d_tiles
     std::vector<hbec_stripe> fallback;  // stripes coded one by one
+    // object plans (hbec_plan_objects): data shards and parity shards in
+    // separate regions; tiles carry base A = data, base B = parity
+    bool objects = false;
+    std::vector<hbec_object> obj_tiled, obj_fallback;
     uint64_t shard_bytes = 0;           // sum of shard_len over all stripes
 };
 
@@ -35,6 +39,17 @@ namespace {
 bool aligned_stripe(const hbec_stripe& s) {
     return (reinterpret_cast<uintptr_t>(s.base) & 15u) == 0 && (s.shard_len % 16) == 0 &&
            s.shard_len < (1ull << 32);
+}
+
+bool aligned_object(const hbec_object& o) {
+    return ((reinterpret_cast<uintptr_t>(o.data) | reinterpret_cast<uintptr_t>(o.parity)) & 15u) == 0 &&
+           (o.shard_len % 16) == 0 && o.shard_len < (1ull << 32);
+}
+
+// Shard i of an object: data shard i (i < k) or parity shard i - k.
+uint8_t* object_shard(const hbec_object& o, int k, int i) {
+    return i < k ? static_cast<uint8_t*>(o.data) + (uint64_t)i * o.shard_len
+                 : static_cast<uint8_t*>(o.parity) + (uint64_t)(i - k) * o.shard_len;
 }
 
 std::mutex g_occ_mu;
@@ -80,6 +95,16 @@ int apply_one(const hbec_stripe& s, int n_shards, const std::vector<int>& in_idx
                              stream);
 }
 
+// Codes one object of an object plan through the generic strided path.
+int apply_one_object(const hbec_object& o, int k, const std::vector<int>& in_idx, const std::vector<int>& out_idx,
+                     const uint8_t* rows, hipStream_t stream) {
+    std::vector<hbec_view> vin(in_idx.size()), vout(out_idx.size());
+    for (size_t j = 0; j < in_idx.size(); ++j) vin[j] = {object_shard(o, k, in_idx[j]), 0};
+    for (size_t r = 0; r < out_idx.size(); ++r) vout[r] = {object_shard(o, k, out_idx[r]), 0};
+    return hbec::apply_views((int)out_idx.size(), (int)in_idx.size(), rows, vin.data(), vout.data(), 1, o.shard_len,
+                             stream);
+}
+
 // out rows (given as shard indices + coefficient rows over in_idx) for every stripe
 int run_plan(const hbec_plan* p, const std::vector<int>& in_idx, const std::vector<int>& out_idx,
              const std::vector<uint8_t>& rows, hipStream_t stream) {
@@ -94,9 +119,20 @@ int run_plan(const hbec_plan* p, const std::vector<int>& in_idx, const std::vect
             std::memset(&a, 0, sizeof(a));
             a.tiles = p->d_tiles;
             a.n_tiles = (uint32_t)p->n_tiles;
-            for (int j = 0; j < K; ++j) a.in_idx[j] = (uint32_t)in_idx[j];
+            a.split = p->objects ? 1u : 0u;
+            for (int j = 0; j < K; ++j) {
+                a.in_idx[j] = (uint32_t)in_idx[j];
+                if (p->objects && in_idx[j] >= p->k) {  // parity shard: base B
+                    a.in_sel |= 1u << j;
+                    a.in_idx[j] -= (uint32_t)p->k;
+                }
+            }
             for (int r = 0; r < R; ++r) {
                 a.out_idx[r] = (uint32_t)out_idx[r0 + r];
+                if (p->objects) {
+                    if (out_idx[r0 + r] < p->k) a.out_sel |= 1u << r;  // data shard: base A
+                    else a.out_idx[r] -= (uint32_t)p->k;
+                }
                 for (int j = 0; j < K; ++j) hbec::perm_table(rows[(size_t)(r0 + r) * K + j], a.tab[r][j]);
             }
             int grid = 0;
@@ -105,6 +141,19 @@ int run_plan(const hbec_plan* p, const std::vector<int>& in_idx, const std::vect
             hipError_t e = hbec::launch_stripes(K, R, a, grid, stream);
             if (e != hipSuccess) return hip_fail(e, "launch gf_apply_stripes");
         }
+    }
+    if (p->objects) {
+        if (!tiled_ok) {
+            for (const auto& o : p->obj_tiled) {
+                int rc = apply_one_object(o, p->k, in_idx, out_idx, rows.data(), stream);
+                if (rc) return rc;
+            }
+        }
+        for (const auto& o : p->obj_fallback) {
+            int rc = apply_one_object(o, p->k, in_idx, out_idx, rows.data(), stream);
+            if (rc) return rc;
+        }
+        return HBEC_OK;
     }
     const auto& singles = tiled_ok ? p->fallback : p->tiled;
     for (const auto& s : singles) {
@@ -169,6 +218,53 @@ int hbec_plan_stripes(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n,
     return HBEC_OK;
 }
 
+int hbec_plan_objects(hbec_codec* codec, const hbec_object* objects, uint64_t n, hbec_plan** out) {
+    if (!codec || !out || (n && !objects)) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+    *out = nullptr;
+    const int k = hbec_data_shards(codec), m = hbec_parity_shards(codec);
+    std::unique_ptr<hbec_plan> p(new (std::nothrow) hbec_plan());
+    if (!p) return fail(HBEC_ERR_NOMEM, "plan allocation");
+    p->k = k;
+    p->m = m;
+    p->objects = true;
+    p->tile_bytes = hbec::stripes_tile_bytes(std::min(k, 8));
+    std::vector<hbec::TileRec> recs;
+    for (uint64_t i = 0; i < n; ++i) {
+        const hbec_object& o = objects[i];
+        if (o.shard_len == 0) continue;
+        if (!o.data || (m > 0 && !o.parity)) return fail(HBEC_ERR_INVALID_ARG, "object with null data or parity");
+        p->shard_bytes += o.shard_len;
+        if (!aligned_object(o)) {
+            p->obj_fallback.push_back(o);
+            continue;
+        }
+        p->obj_tiled.push_back(o);
+        for (uint64_t off = 0; off < o.shard_len; off += (uint64_t)p->tile_bytes) {
+            hbec::TileRec r;
+            r.in_addr = reinterpret_cast<uint64_t>(o.data) + off;
+            r.out_addr = reinterpret_cast<uint64_t>(o.parity) + off;
+            r.in_stride = r.out_stride = (uint32_t)o.shard_len;
+            r.valid = (uint32_t)std::min<uint64_t>((uint64_t)p->tile_bytes, o.shard_len - off);
+            r.pad_ = 0;
+            recs.push_back(r);
+        }
+    }
+    if (recs.size() >= (1ull << 31)) return fail(HBEC_ERR_INVALID_ARG, "plan too large (>= 2^31 tiles)");
+    p->n_tiles = recs.size();
+    if (!recs.empty()) {
+        hipError_t e = hipMalloc(&p->d_tiles, recs.size() * sizeof(hbec::TileRec));
+        if (e != hipSuccess) return hip_fail(e, "hipMalloc plan tiles");
+        e = hipMemcpy(p->d_tiles, recs.data(), recs.size() * sizeof(hbec::TileRec), hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            (void)hipFree(p->d_tiles);
+            p->d_tiles = nullptr;
+            return hip_fail(e, "hipMemcpy plan tiles");
+        }
+    }
+    *out = p.release();
+    return HBEC_OK;
+}
+
 void hbec_plan_free(hbec_plan* plan) {
     if (!plan) return;
     if (plan->d_tiles) (void)hipFree(plan->d_tiles);
@@ -180,7 +276,7 @@ int hbec_plan_info(const hbec_plan* plan, uint64_t* n_tiles, int* tile_bytes, ui
     if (!plan) return fail(HBEC_ERR_INVALID_ARG, "null plan");
     if (n_tiles) *n_tiles = plan->n_tiles;
     if (tile_bytes) *tile_bytes = plan->tile_bytes;
-    if (n_fallback) *n_fallback = plan->fallback.size();
+    if (n_fallback) *n_fallback = plan->objects ? plan->obj_fallback.size() : plan->fallback.size();
     if (shard_bytes) *shard_bytes = plan->shard_bytes;
     return HBEC_OK;
 }

@@ -19,22 +19,39 @@
 
 namespace hbec {
 
+// Per-tile shard bases, wave-uniform (scalar): inputs src[j], outputs dst[r].
+template <int K, int R, bool SPLIT>
+__device__ __forceinline__ void tile_bases(uint64_t (&src)[K], uint64_t (&dst)[R], const StripeArgs& a,
+                                           const TileRec& t) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        const bool b = SPLIT && ((a.in_sel >> j) & 1u);
+        src[j] = b ? t.out_addr + (uint64_t)a.in_idx[j] * t.out_stride : t.in_addr + (uint64_t)a.in_idx[j] * t.in_stride;
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const bool b = SPLIT && ((a.out_sel >> r) & 1u);
+        dst[r] = b ? t.in_addr + (uint64_t)a.out_idx[r] * t.in_stride : t.out_addr + (uint64_t)a.out_idx[r] * t.out_stride;
+    }
+}
+
 template <int K, int U>
-__device__ __forceinline__ void load_stripe_tile(u32x4 (&x)[U][K], const StripeArgs& a, const TileRec& t,
+__device__ __forceinline__ void load_stripe_tile(u32x4 (&x)[U][K], const uint64_t (&src)[K], uint32_t valid,
                                                  uint32_t lane) {
-    const uint64_t last = (uint64_t)t.valid - 16u;  // valid >= 16, multiple of 16
+    const uint64_t last = (uint64_t)valid - 16u;  // valid >= 16, multiple of 16
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         uint64_t off = (uint64_t)lane * 16u + (uint64_t)u * 1024u;
         off = off < last ? off : last;
 #pragma unroll
-        for (int j = 0; j < K; ++j) x[u][j] = ld16_addr(t.in_addr + (uint64_t)a.in_idx[j] * t.in_stride + off);
+        for (int j = 0; j < K; ++j) x[u][j] = ld16_addr(src[j] + off);
     }
 }
 
 template <int K, int R, int U, bool FULL>
 __device__ __forceinline__ void store_stripe_tile_(const u32x4 (&x)[U][K], const StripeArgs& a,
-                                                   const Tables<K, R>& tb, const TileRec& t, uint32_t lane) {
+                                                   const Tables<K, R>& tb, const uint64_t (&dst)[R], uint32_t valid,
+                                                   uint32_t lane) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const uint64_t off = (uint64_t)lane * 16u + (uint64_t)u * 1024u;
@@ -42,21 +59,20 @@ __device__ __forceinline__ void store_stripe_tile_(const u32x4 (&x)[U][K], const
 #pragma unroll
         for (int r = 0; r < R; ++r) acc[r] = u32x4{0, 0, 0, 0};
         gf_dot<K, R>(acc, x[u], a.tab, tb);
-        if (FULL || off < t.valid) {
+        if (FULL || off < valid) {
 #pragma unroll
-            for (int r = 0; r < R; ++r)
-                st16_addr(t.out_addr + (uint64_t)a.out_idx[r] * t.out_stride + off, acc[r]);
+            for (int r = 0; r < R; ++r) st16_addr(dst[r] + off, acc[r]);
         }
     }
 }
 
 template <int K, int R, int U>
 __device__ __forceinline__ void store_stripe_tile(const u32x4 (&x)[U][K], const StripeArgs& a, const Tables<K, R>& tb,
-                                                  const TileRec& t, uint32_t lane) {
-    if (t.valid >= (uint32_t)U * 1024u)  // wave-uniform: whole tile live
-        store_stripe_tile_<K, R, U, true>(x, a, tb, t, lane);
+                                                  const uint64_t (&dst)[R], uint32_t valid, uint32_t lane) {
+    if (valid >= (uint32_t)U * 1024u)  // wave-uniform: whole tile live
+        store_stripe_tile_<K, R, U, true>(x, a, tb, dst, valid, lane);
     else
-        store_stripe_tile_<K, R, U, false>(x, a, tb, t, lane);
+        store_stripe_tile_<K, R, U, false>(x, a, tb, dst, valid, lane);
 }
 
 // Tile records are read-only for the whole launch and passed as a separate
@@ -65,7 +81,7 @@ __device__ __forceinline__ TileRec load_rec(const TileRec* __restrict__ recs, ui
     return recs[i];
 }
 
-template <int K, int R>
+template <int K, int R, bool SPLIT>
 __global__ __launch_bounds__(kBlockThreads, 1) void gf_apply_stripes(StripeArgs a,
                                                                      const TileRec* __restrict__ tiles) {
     constexpr int U = stripes_u(K);
@@ -77,50 +93,61 @@ __global__ __launch_bounds__(kBlockThreads, 1) void gf_apply_stripes(StripeArgs 
     if (wave >= n) return;
     const Tables<K, R> tb = load_tables<K, R>(a.tab);
     TileRec cur = load_rec(tiles, wave);
+    uint64_t src[K], dst[R];
+    tile_bases<K, R, SPLIT>(src, dst, a, cur);
     u32x4 x[U][K];
-    load_stripe_tile<K, U>(x, a, cur, lane);
+    load_stripe_tile<K, U>(x, src, cur.valid, lane);
     uint32_t tn = wave + nw;
     TileRec nxt = load_rec(tiles, tn < n ? tn : wave);
     for (; tn < n; tn += nw) {
         u32x4 y[U][K];
-        load_stripe_tile<K, U>(y, a, nxt, lane);  // data one tile ahead
+        uint64_t nsrc[K], ndst[R];
+        tile_bases<K, R, SPLIT>(nsrc, ndst, a, nxt);
+        load_stripe_tile<K, U>(y, nsrc, nxt.valid, lane);  // data one tile ahead
         // record two tiles ahead, issued after the data loads: scalar loads
         // return out of order, so waiting for `nxt` is an lgkmcnt(0)
         const uint32_t t2 = tn + nw;
         const TileRec after = load_rec(tiles, t2 < n ? t2 : tn);
-        store_stripe_tile<K, R, U>(x, a, tb, cur, lane);
+        store_stripe_tile<K, R, U>(x, a, tb, dst, cur.valid, lane);
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
             for (int j = 0; j < K; ++j) x[u][j] = y[u][j];
+#pragma unroll
+        for (int r = 0; r < R; ++r) dst[r] = ndst[r];
         cur = nxt;
         nxt = after;
     }
-    store_stripe_tile<K, R, U>(x, a, tb, cur, lane);
+    store_stripe_tile<K, R, U>(x, a, tb, dst, cur.valid, lane);
 }
 
-template <int K>
+template <int K, bool SPLIT>
 static const void* stripes_for_r(int r) {
     switch (r) {
-        case 1: return reinterpret_cast<const void*>(&gf_apply_stripes<K, 1>);
-        case 2: return reinterpret_cast<const void*>(&gf_apply_stripes<K, 2>);
-        case 3: return reinterpret_cast<const void*>(&gf_apply_stripes<K, 3>);
+        case 1: return reinterpret_cast<const void*>(&gf_apply_stripes<K, 1, SPLIT>);
+        case 2: return reinterpret_cast<const void*>(&gf_apply_stripes<K, 2, SPLIT>);
+        case 3: return reinterpret_cast<const void*>(&gf_apply_stripes<K, 3, SPLIT>);
     }
     return nullptr;
 }
 
-static const void* stripes_kernel(int k, int r) {
+template <bool SPLIT>
+static const void* stripes_kernel_(int k, int r) {
     switch (k) {
-        case 1: return stripes_for_r<1>(r);
-        case 2: return stripes_for_r<2>(r);
-        case 3: return stripes_for_r<3>(r);
-        case 4: return stripes_for_r<4>(r);
-        case 5: return stripes_for_r<5>(r);
-        case 6: return stripes_for_r<6>(r);
-        case 7: return stripes_for_r<7>(r);
-        case 8: return stripes_for_r<8>(r);
+        case 1: return stripes_for_r<1, SPLIT>(r);
+        case 2: return stripes_for_r<2, SPLIT>(r);
+        case 3: return stripes_for_r<3, SPLIT>(r);
+        case 4: return stripes_for_r<4, SPLIT>(r);
+        case 5: return stripes_for_r<5, SPLIT>(r);
+        case 6: return stripes_for_r<6, SPLIT>(r);
+        case 7: return stripes_for_r<7, SPLIT>(r);
+        case 8: return stripes_for_r<8, SPLIT>(r);
     }
     return nullptr;
+}
+
+static const void* stripes_kernel(int k, int r, bool split = false) {
+    return split ? stripes_kernel_<true>(k, r) : stripes_kernel_<false>(k, r);
 }
 
 int stripes_tile_bytes(int k) { return stripes_u(k) * 1024; }
@@ -128,7 +155,7 @@ int stripes_tile_bytes(int k) { return stripes_u(k) * 1024; }
 bool stripes_supported(int k, int r) { return stripes_kernel(k, r) != nullptr; }
 
 hipError_t launch_stripes(int k, int r, const StripeArgs& a, int grid, hipStream_t stream) {
-    const void* fn = stripes_kernel(k, r);
+    const void* fn = stripes_kernel(k, r, a.split != 0);
     if (!fn) return hipErrorInvalidValue;
     const TileRec* tiles = a.tiles;
     void* args[] = {const_cast<StripeArgs*>(&a), &tiles};

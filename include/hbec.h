@@ -183,6 +183,17 @@ typedef struct {
 typedef struct hbec_plan hbec_plan;
 
 int hbec_plan_stripes(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n_stripes, hbec_plan** out);
+/* Object plans: each object's k data shards back to back at `data` and its m
+ * parity shards back to back at `parity` (two regions, e.g. a data arena and
+ * a parity arena), shard_len bytes each.  Same encode / reconstruct / info /
+ * free calls as stripe plans.  Keeping parity out of the data rows streams
+ * faster on MI355X than ecSplit's in-row layout. */
+typedef struct {
+    void* data;
+    void* parity;
+    uint64_t shard_len;
+} hbec_object;
+int hbec_plan_objects(hbec_codec* codec, const hbec_object* objects, uint64_t n_objects, hbec_plan** out);
 void hbec_plan_free(hbec_plan* plan);
 int hbec_plan_info(const hbec_plan* plan, uint64_t* n_tiles, int* tile_bytes, uint64_t* n_fallback,
                    uint64_t* shard_bytes);

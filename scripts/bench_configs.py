@@ -143,6 +143,47 @@ def mixed_8_3(n=4096):
     line(f"8+3 encode+reconstruct mixed x{n} (config 4)", enc_bytes + rec_bytes, t_enc + t_rec)
 
 
+def mixed_8_3_objects(n=4096):
+    """Config 4 over an object plan: objects back to back in a data arena,
+    parity back to back in a parity arena (hbec_plan_objects)."""
+    k, m = 8, 3
+    flags = O.splitmix_bytes(O.HBEC_SEED, n)
+    sizes = [MiB if b & 1 else 4096 for b in flags]
+    dl, pl, doff, poff = [], [], 0, 0
+    for size in sizes:
+        s = size // k
+        dl.append((doff, s))
+        pl.append(poff)
+        doff += k * s
+        poff += m * s
+    data = torch.empty(doff, dtype=torch.uint8, device="cuda")
+    parity = torch.empty(poff, dtype=torch.uint8, device="cuda")
+    B.fill_splitmix(data.view(1, -1), doff)
+    enc = RS.New(k, m)
+    plan = B.StripePlan(enc, objects=[(data.data_ptr() + o, parity.data_ptr() + po, s)
+                                      for (o, s), po in zip(dl, pl)])
+    enc_bytes = sum((k + m) * s for _, s in dl)
+    ms = timeit(plan.encode)
+    line(f"8+3 encode mixed 4KiB/1MiB x{n} (object plan)", enc_bytes, ms, plan=plan.info())
+    hd, hp = data.cpu().numpy(), parity.cpu().numpy()
+    mat = CO.build_matrix(k, m)[k:]
+    for i in [0, 1, 2, n - 1] + [j for j in range(n) if sizes[j] == 4096][:3]:
+        (o, s), po = dl[i], pl[i]
+        want = CO.apply(mat, [hd[o + j * s:o + (j + 1) * s] for j in range(k)])
+        for r in range(m):
+            assert np.array_equal(hp[po + r * s:po + (r + 1) * s], want[r])
+    ref = data.clone()
+    miss = (0, 1, 2)
+    present = [0 if i in miss else 1 for i in range(k + m)]
+    ms = timeit(lambda: plan.reconstruct(present))
+    assert torch.equal(data, ref)  # rebuilt in place == original
+    rec_bytes = sum((k + len(miss)) * s for _, s in dl)
+    line(f"8+3 reconstruct{{0,1,2}} mixed 4KiB/1MiB x{n} (object plan)", rec_bytes, ms)
+    t_enc = timeit(plan.encode, reps=5)
+    t_rec = timeit(lambda: plan.reconstruct(present), reps=5)
+    line(f"8+3 encode+reconstruct mixed x{n} (config 4, object plan)", enc_bytes + rec_bytes, t_enc + t_rec)
+
+
 def main():
     torch.cuda.set_device(0)
     uniform(4, 2, 4096, MiB, [(0, 1), (0, 4), (4, 5), (2, 3)])
@@ -150,6 +191,7 @@ def main():
     uniform_plan(4, 2, 4096, MiB)
     uniform_plan(8, 3, 4096, MiB)
     mixed_8_3()
+    mixed_8_3_objects()
 
 
 if __name__ == "__main__":

@@ -30,6 +30,20 @@ T4 = BASE + ["HBEC_TILE_MID=4"]
 P = T1 + ["HBEC_USE_PIPE=1"]
 VARIANTS = {
     "cur": ([], {}),
+    "sl0": ([], {}),
+    "sl1": (["HBEC_PIPE_SLEEP=1"], {}),
+    "sl2": (["HBEC_PIPE_SLEEP=2"], {}),
+    "sl4": (["HBEC_PIPE_SLEEP=4"], {}),
+    "sl8": (["HBEC_PIPE_SLEEP=8"], {}),
+    "sl5": (["HBEC_PIPE_SLEEP=5"], {}),
+    "sl6": (["HBEC_PIPE_SLEEP=6"], {}),
+    "sl7": (["HBEC_PIPE_SLEEP=7"], {}),
+    "sl9": (["HBEC_PIPE_SLEEP=9"], {}),
+    "sl10": (["HBEC_PIPE_SLEEP=10"], {}),
+    "sl12": (["HBEC_PIPE_SLEEP=12"], {}),
+    "sl16": (["HBEC_PIPE_SLEEP=16"], {}),
+    "sl24": (["HBEC_PIPE_SLEEP=24"], {}),
+    "sl32": (["HBEC_PIPE_SLEEP=32"], {}),
     "xcd1": ([], {}),
     "xcd0": (["HBEC_XCD_MAP=0"], {}),
     "prev": (["HBEC_PIPE_LOADS=16", "HBEC_PIPE_BLOCKS_PER_CU=0"], {}),

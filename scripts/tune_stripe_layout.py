@@ -208,9 +208,9 @@ def split_ab(n=4096, k=4, m=2, rounds=12, reps=4,
                           "frac": round((nbytes + n * (k + e) * S) / (em + rm) / 1e6 / 8000, 4)}), flush=True)
 
 
-def kernels_ab(n=4096, k=4, m=2, rounds=10, reps=3):
-    """Encode only, interleaved: strided kernel on the split and stripe
-    layouts, and the stripe-plan kernel on the stripe layout."""
+def kernels_ab(n=4096, k=4, m=2, rounds=16, reps=3):
+    """Interleaved: strided kernel vs stripe-plan kernel vs object-plan kernel,
+    on the split and stripe layouts; encode, and reconstruct{0,1} in place."""
     torch.cuda.set_device(0)
     S = (1 << 20) // k
     enc = RS.New(k, m)
@@ -222,10 +222,22 @@ def kernels_ab(n=4096, k=4, m=2, rounds=10, reps=3):
     sv = B.shard_views(objs, k, S) + B.shard_views(par, m, S)
     rv = B.shard_views(rows, k + m, S)
     splan = B.StripePlan(enc, [(rows.data_ptr() + i * rows.stride(0), S) for i in range(n)])
+    oplan = B.StripePlan(enc, objects=[(objs.data_ptr() + i * objs.stride(0), par.data_ptr() + i * par.stride(0), S)
+                                       for i in range(n)])
+    present = [0, 0] + [1] * (k + m - 2)
+    reb = torch.empty((n, 2 * S), dtype=torch.uint8, device="cuda")
+    sv_reb = [(reb.data_ptr(), reb.stride(0)), (reb.data_ptr() + S, reb.stride(0))] + sv[2:]
+    rplan = B.StripePlan(enc, objects=[(objs.data_ptr() + i * objs.stride(0), par.data_ptr() + i * par.stride(0), S)
+                                       for i in range(n)])
     cases = {
         "strided_split": lambda: B.encode_views(enc, sv, n, S),
         "strided_stripe": lambda: B.encode_views(enc, rv, n, S),
         "plan_stripe": splan.encode,
+        "plan_split": oplan.encode,
+        "rec01_strided_split": lambda: B.reconstruct_views(enc, sv, present, n, S),
+        "rec01_plan_split": lambda: oplan.reconstruct(present),
+        "rec01_plan_stripe": lambda: splan.reconstruct(present),
+        "rec01_strided_rebuilt": lambda: B.reconstruct_views(enc, sv_reb, present, n, S),
     }
     t = {c: [] for c in cases}
     names = list(cases)
@@ -239,11 +251,12 @@ def kernels_ab(n=4096, k=4, m=2, rounds=10, reps=3):
                 torch.cuda.synchronize()
                 if rnd:
                     t[c].append(e0.elapsed_time(e1))
-    ok = bool(torch.equal(par, rows[:, k * S:]))
+    ok = bool(torch.equal(par, rows[:, k * S:])) and bool(torch.equal(rows[:, :k * S], objs))
     for c in names:
         ms = statistics.median(t[c])
+        nb = n * ((k + 2) if c.startswith("rec01") else (k + m)) * S
         print(json.dumps({"sweep": "kernels", "k": k, "m": m, "case": c, "ms": round(ms, 4),
-                          "frac": round(n * (k + m) * S / ms / 1e6 / 8000, 4), "ok": ok}), flush=True)
+                          "frac": round(nb / ms / 1e6 / 8000, 4), "ok": ok}), flush=True)
 
 
 if __name__ == "__main__":

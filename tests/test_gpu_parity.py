@@ -452,6 +452,67 @@ def test_plan_config4_shape_counts():
     assert np.array_equal(dev.cpu().numpy(), _expected_pool(k, m, pool, layout))
 
 
+def _object_arenas(k, m, sizes, misalign=()):
+    """Object-plan layout: objects back to back in a data arena (k*S bytes
+    each, zero padded), their parity back to back in a parity arena."""
+    dl, pl, doff, poff = [], [], 0, 0
+    for i, size in enumerate(sizes):
+        s = O.ec_shard_length(size, k)
+        doff = (doff + 15) // 16 * 16 + (5 if i in misalign else 0)
+        poff = (poff + 15) // 16 * 16
+        dl.append((doff, s, size))
+        pl.append(poff)
+        doff += k * s
+        poff += m * s
+    data = np.zeros(doff + 64, dtype=np.uint8)
+    for i, (o, s, size) in enumerate(dl):
+        data[o:o + size] = CO.fill_objects(2000 + i, 1, size)[0]
+    parity = np.zeros(poff + 64, dtype=np.uint8)
+    mat = CO.build_matrix(k, m)[k:]
+    for (o, s, _), po in zip(dl, pl):
+        for r, par in enumerate(CO.apply(mat, [data[o + j * s:o + (j + 1) * s] for j in range(k)])):
+            parity[po + r * s:po + (r + 1) * s] = par
+    return data, parity, dl, pl
+
+
+@pytest.mark.parametrize("k,m,sizes,misalign", [
+    (8, 3, [4096, MiB, 4096, 4096, MiB, 4096, MiB, 4096] * 3, ()),
+    (4, 2, [MiB, 7, 4096, 1001, MiB + 16, 64, 4097], (1, 3)),
+    (10, 4, [4096, 40960, 160], ()),
+    (5, 5, [5 * 4096, 5 * 100000, 80], ()),
+])
+def test_object_plan_encode_reconstruct(k, m, sizes, misalign):
+    """hbec_plan_objects: data and parity in separate arenas; every erasure
+    pattern family rebuilds into the right arena."""
+    data, parity, dl, pl = _object_arenas(k, m, sizes, misalign)
+    enc = RS.New(k, m)
+    d = torch.from_numpy(data).cuda()
+    p = torch.zeros(parity.size, dtype=torch.uint8, device="cuda")
+
+    def objs(dt, pt):
+        return [(dt.data_ptr() + o, pt.data_ptr() + po, s) for (o, s, _), po in zip(dl, pl)]
+
+    plan = B.StripePlan(enc, objects=objs(d, p))
+    assert plan.info()["n_fallback"] == sum(1 for o, s, _ in dl if o % 16 or s % 16)
+    plan.encode()
+    torch.cuda.synchronize()
+    assert np.array_equal(p.cpu().numpy(), parity)
+    assert np.array_equal(d.cpu().numpy(), data)
+    for missing in [tuple(range(min(m, 3))), (0, k), (k - 1,), tuple(range(k, k + m)), (k - 1, k + m - 1)]:
+        dd = torch.from_numpy(data.copy()).cuda()
+        pp = torch.from_numpy(parity.copy()).cuda()
+        for (o, s, _), po in zip(dl, pl):
+            for i in missing:
+                if i < k:
+                    dd[o + i * s:o + (i + 1) * s] = 0xEE
+                else:
+                    pp[po + (i - k) * s:po + (i - k + 1) * s] = 0xEE
+        B.StripePlan(enc, objects=objs(dd, pp)).reconstruct([0 if i in missing else 1 for i in range(k + m)])
+        torch.cuda.synchronize()
+        assert np.array_equal(dd.cpu().numpy(), data), missing
+        assert np.array_equal(pp.cpu().numpy(), parity), missing
+
+
 def test_plan_empty_and_zero_length():
     enc = RS.New(4, 2)
     B.StripePlan(enc, []).encode()
