@@ -184,6 +184,59 @@ def mixed_8_3_objects(n=4096):
     line(f"8+3 encode+reconstruct mixed x{n} (config 4, object plan)", enc_bytes + rec_bytes, t_enc + t_rec)
 
 
+def mixed_8_3_size_classes(n=4096):
+    """Config 4 with size-classed arenas: the batch's objects are placed by
+    size class, each class as a strided batch (objs [n_c][L_c] + parity
+    [n_c][m*S_c], the layout of the headline): 1 MiB objects run on the
+    pipelined kernel, 4 KiB objects on the short-shard kernel.  Two launches
+    per op, timed together."""
+    k, m = 8, 3
+    flags = O.splitmix_bytes(O.HBEC_SEED, n)
+    sizes = [MiB if b & 1 else 4096 for b in flags]
+    enc = RS.New(k, m)
+    classes = []
+    for size in (MiB, 4096):
+        idx = [i for i, x in enumerate(sizes) if x == size]
+        s = size // k
+        objs = torch.empty((len(idx), size), dtype=torch.uint8, device="cuda")
+        B.fill_splitmix(objs, size)
+        par = torch.empty((len(idx), m * s), dtype=torch.uint8, device="cuda")
+        views = B.shard_views(objs, k, s) + B.shard_views(par, m, s)
+        classes.append((len(idx), s, objs, par, views))
+    miss = (0, 1, 2)
+    present = [0 if i in miss else 1 for i in range(k + m)]
+
+    def encode():
+        for cnt, s, _, _, v in classes:
+            B.encode_views(enc, v, cnt, s)
+
+    def reconstruct():
+        for cnt, s, _, _, v in classes:
+            B.reconstruct_views(enc, v, present, cnt, s)
+
+    encode()
+    torch.cuda.synchronize()
+    mat = CO.build_matrix(k, m)[k:]
+    for cnt, s, objs, par, _ in classes:
+        ho, hp = objs[:3].cpu().numpy(), par[:3].cpu().numpy()
+        for i in range(3):
+            want = CO.apply(mat, [ho[i, j * s:(j + 1) * s] for j in range(k)])
+            assert np.array_equal(hp[i], np.concatenate(want))
+    refs = [objs.clone() for _, _, objs, _, _ in classes]
+    enc_bytes = sum(cnt * (k + m) * s for cnt, s, _, _, _ in classes)
+    rec_bytes = sum(cnt * (k + len(miss)) * s for cnt, s, _, _, _ in classes)
+    ms = timeit(encode)
+    line(f"8+3 encode mixed 4KiB/1MiB x{n} (size-classed arenas)", enc_bytes, ms,
+         n_1MiB=classes[0][0], n_4KiB=classes[1][0])
+    ms = timeit(reconstruct)
+    for ref, (_, _, objs, _, _) in zip(refs, classes):
+        assert torch.equal(objs, ref)  # rebuilt in place == original
+    line(f"8+3 reconstruct{{0,1,2}} mixed 4KiB/1MiB x{n} (size-classed arenas)", rec_bytes, ms)
+    t_enc = timeit(encode, reps=5)
+    t_rec = timeit(reconstruct, reps=5)
+    line(f"8+3 encode+reconstruct mixed x{n} (config 4, size-classed arenas)", enc_bytes + rec_bytes, t_enc + t_rec)
+
+
 def main():
     torch.cuda.set_device(0)
     uniform(4, 2, 4096, MiB, [(0, 1), (0, 4), (4, 5), (2, 3)])
@@ -192,6 +245,7 @@ def main():
     uniform_plan(8, 3, 4096, MiB)
     mixed_8_3()
     mixed_8_3_objects()
+    mixed_8_3_size_classes()
 
 
 if __name__ == "__main__":
