@@ -30,7 +30,13 @@ T4 = BASE + ["HBEC_TILE_MID=4"]
 P = T1 + ["HBEC_USE_PIPE=1"]
 VARIANTS = {
     "cur": ([], {}),
-    "sl0": ([], {}),
+    "d": ([], {}),
+    "u2s6": (["HBEC_PIPE_LOADS=8"], {}),
+    "u2s10": (["HBEC_PIPE_LOADS=8", "HBEC_PIPE_SLEEP=10"], {}),
+    "u2s14": (["HBEC_PIPE_LOADS=8", "HBEC_PIPE_SLEEP=14"], {}),
+    "b2s6": ([], {"HBEC_BLOCKS_PER_CU": "2"}),
+    "b2s12": (["HBEC_PIPE_SLEEP=12"], {"HBEC_BLOCKS_PER_CU": "2"}),
+    "sl0": (["HBEC_PIPE_SLEEP=0"], {}),
     "sl1": (["HBEC_PIPE_SLEEP=1"], {}),
     "sl2": (["HBEC_PIPE_SLEEP=2"], {}),
     "sl4": (["HBEC_PIPE_SLEEP=4"], {}),
