@@ -47,9 +47,10 @@ def _stale(target: Path, deps: list[Path]) -> bool:
 
 
 def build(force: bool = False, verbose: bool = True, defs=(), lib: Path | None = None,
-          objdir: Path | None = None) -> Path:
+          objdir: Path | None = None, extra=(), link=None) -> Path:
     """Build libhbec.so (or, for tuning experiments, a variant with extra -D
-    definitions into `lib` / `objdir`)."""
+    definitions into `lib` / `objdir`; `extra` compile flags and a custom
+    `link` command prefix are for the sanitizer build)."""
     lib = Path(lib) if lib else LIB
     objdir = Path(objdir) if objdir else OBJ
     objdir.mkdir(parents=True, exist_ok=True)
@@ -63,7 +64,7 @@ def build(force: bool = False, verbose: bool = True, defs=(), lib: Path | None =
         objs.append(o)
         if force or _stale(o, [s] + hdrs):
             lang = ["-x", "hip"] if src.endswith(".hip") else []
-            jobs.append([hipcc, *_flags(defs), *lang, "-c", str(s), "-o", str(o)])
+            jobs.append([hipcc, *_flags(defs), *extra, *lang, "-c", str(s), "-o", str(o)])
 
     def run(cmd):
         if verbose:
@@ -75,9 +76,41 @@ def build(force: bool = False, verbose: bool = True, defs=(), lib: Path | None =
     with ThreadPoolExecutor(max_workers=min(4, max(1, len(jobs)))) as ex:
         list(ex.map(run, jobs))
     if force or jobs or _stale(lib, objs):
-        run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(lib), *map(str, objs),
-             "-lpthread"])
+        if link:
+            run([*link, "-o", str(lib), *map(str, objs)])
+        else:
+            run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(lib), *map(str, objs),
+                 "-lpthread"])
     return lib
+
+
+ASAN_DIR = PKG / "build_asan"
+ASAN_LIB = ASAN_DIR / "libhbec_asan.so"
+ASAN_EXE = ASAN_DIR / "host_asan"
+
+
+def build_asan(force: bool = False, verbose: bool = False) -> Path:
+    """AddressSanitizer + UBSan build of the HOST code of libhbec (device
+    code is not instrumented: every -fsanitize on the hipcc lines sits behind
+    -Xarch_host) and of the C driver tests/native/host_asan.c.  Host-only
+    sanitizers are the ones this pool runs (no GPU ASan / xnack)."""
+    clang = "/opt/rocm/lib/llvm/bin/clang"
+    san_host = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
+                "-Xarch_host", "-fno-sanitize-recover=undefined", "-Xarch_host", "-fno-omit-frame-pointer",
+                "-Xarch_host", "-g"]
+    rocm_lib = "/opt/rocm/lib"
+    link = [clang + "++", "-shared", "-fsanitize=address,undefined", "-fno-omit-frame-pointer",
+            f"-L{rocm_lib}", "-lamdhip64", "-lpthread", f"-Wl,-rpath,{rocm_lib}"]
+    lib = build(force=force, verbose=verbose, lib=ASAN_LIB, objdir=ASAN_DIR / "obj", extra=san_host, link=link)
+    src = ROOT / "tests" / "native" / "host_asan.c"
+    if force or _stale(ASAN_EXE, [src, lib, INCLUDE / "hbec.h"]):
+        cmd = [clang, "-std=c11", "-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined",
+               "-fno-omit-frame-pointer", f"-I{INCLUDE}", str(src), f"-L{ASAN_DIR}", "-lhbec_asan",
+               f"-Wl,-rpath,{ASAN_DIR}", f"-Wl,-rpath,{rocm_lib}", "-lpthread", "-o", str(ASAN_EXE)]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"clang failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return ASAN_EXE
 
 
 if __name__ == "__main__":

@@ -209,11 +209,14 @@ bool zero_copy_enabled() {
     return on;
 }
 
+}  // namespace
+
 // Device address of host range [p, p + len) when all of it lies in one
 // pinned, device-mapped allocation; 0 otherwise.  hbec_host_alloc ranges are
 // looked up in the registry; other pinned memory is asked of the runtime at
 // both ends of the range.
-uint64_t pinned_device_addr(const void* p, uint64_t len) {
+uint64_t hbec::pinned_device_addr(const void* p, uint64_t len) {
+    if (!zero_copy_enabled()) return 0;
     const uint64_t h = reinterpret_cast<uint64_t>(p);
     if (!p || len == 0) return 0;
     {
@@ -239,6 +242,9 @@ uint64_t pinned_device_addr(const void* p, uint64_t len) {
     if (a1.type != hipMemoryTypeHost || d1 != d0 + (len - 1)) return 0;
     return d0;
 }
+
+namespace {
+using hbec::pinned_device_addr;
 
 struct ZcStripe {
     uint64_t dev;  // device address of the stripe base

@@ -21,6 +21,11 @@ int apply_views(int rows, int cols, const uint8_t* coeffs, const hbec_view* in, 
 int scratch_alloc(size_t bytes, hipStream_t stream, void** out);
 void scratch_free(void* p, hipStream_t stream);
 
+// Device address of host range [p, p+len) if all of it is pinned, device-mapped
+// memory (hbec_host_alloc, hipHostMalloc, hipHostRegister), else 0 (also 0 when
+// HBEC_ZEROCOPY=0).  The zero-copy host paths code such memory in place.
+uint64_t pinned_device_addr(const void* p, uint64_t len);
+
 // ShardHash of a list of device chains: records {addr, len, slot, 0} (32 B
 // each, device memory), digest of record i at digest + slot * 16.
 hipError_t launch_md5_list(const void* recs, uint64_t n, uint8_t* digest, bool aligned, hipStream_t stream);

@@ -263,18 +263,33 @@ def auditor_pass(n_files=4096, size=MiB // 4):
             "GiB_s": round(n_files * size / t / GiB, 2), "cpu_1core_GiB_s": round(n_files * size / tc / GiB, 2)}
 
 
-def per_call(n_calls=200):
+def per_call(n_calls=200, mem="pageable"):
+    """One klauspost Encode per 1 MiB object, sequential (the naive drop-in).
+    mem="pinned": the shards live in hbec_host_alloc memory (zero-copy)."""
     k, m, S = 4, 2, MiB // 4
     enc = RS.New(k, m)
     rng = np.random.default_rng(0)
     obj = rng.integers(0, 256, k * S, dtype=np.uint8)
-    shards = [obj[j * S:(j + 1) * S].copy() for j in range(k)] + [np.zeros(S, np.uint8) for _ in range(m)]
+    hb = None
+    if mem == "pinned":
+        hb = RS.HostBuffer((k + m) * S)
+        shards = [hb.array[i * S:(i + 1) * S] for i in range(k + m)]
+        for j in range(k):
+            shards[j][:] = obj[j * S:(j + 1) * S]
+    else:
+        shards = [obj[j * S:(j + 1) * S].copy() for j in range(k)] + [np.zeros(S, np.uint8) for _ in range(m)]
     enc.Encode(shards)
     t0 = time.perf_counter()
     for _ in range(n_calls):
         enc.Encode(shards)
     t = time.perf_counter() - t0
-    return {"measure": "per_call_Encode_pageable_1MiB", "calls": n_calls, "us_per_call": round(t / n_calls * 1e6, 1),
+    from oracle import coracle as CO
+    want = CO.encode_batch(k, m, obj[None, :])[0][0]
+    assert np.array_equal(np.concatenate(shards[k:]), want)
+    del shards
+    if hb is not None:
+        hb.free()
+    return {"measure": f"per_call_Encode_{mem}_1MiB", "calls": n_calls, "us_per_call": round(t / n_calls * 1e6, 1),
             "object_data_GiB_s": round(n_calls * k * S / t / GiB, 3)}
 
 
@@ -284,7 +299,7 @@ def main():
              lambda: library_host_path("encode"), lambda: library_host_path("reconstruct"),
              lambda: library_host_path("encode", mem="pinned"), lambda: library_host_path("reconstruct", mem="pinned"),
              library_host_path_md5, batched_callers, lambda: batched_callers(mem="pinned"), batched_callers_md5,
-             auditor_pass, per_call]
+             auditor_pass, per_call, lambda: per_call(mem="pinned")]
     only = sys.argv[1:]
     for i, f in enumerate(steps):
         if only and str(i) not in only:

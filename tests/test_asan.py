@@ -1,0 +1,35 @@
+"""Host-code AddressSanitizer + UBSan run.
+
+hummingbird_amd/build.py build_asan() builds libhbec with the sanitizers on
+the host code only (device code is not instrumented; this pool runs no GPU
+ASan) plus the C driver tests/native/host_asan.c.  The CPU test runs the
+host-only entry points; the GPU test drives the staging ring, zero-copy,
+multi-device split, per-call staging, batcher and ecutils loops."""
+import os
+import subprocess
+
+import pytest
+
+from hummingbird_amd import build as Bd
+
+ENV = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:protect_shadow_gap=0:abort_on_error=0",
+           UBSAN_OPTIONS="print_stacktrace=1")
+
+
+def _exe():
+    if not Bd.ASAN_EXE.exists():
+        pytest.skip("sanitizer build missing: run __graft_entry__.build()")
+    return str(Bd.ASAN_EXE)
+
+
+def test_host_asan_cpu():
+    out = subprocess.run([_exe()], capture_output=True, text=True, env=ENV, timeout=120)
+    assert out.returncode == 0, out.stderr[-4000:]
+    assert "host_asan cpu ok" in out.stdout
+
+
+@pytest.mark.gpu
+def test_host_asan_gpu():
+    out = subprocess.run([_exe(), "gpu"], capture_output=True, text=True, env=ENV, timeout=110)
+    assert out.returncode == 0, out.stderr[-4000:]
+    assert "host_asan gpu ok" in out.stdout

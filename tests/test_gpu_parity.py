@@ -640,6 +640,32 @@ def test_host_path_zero_copy_foreign_pinned_memory():
     assert np.array_equal(arr[:, :k * S], objs)
 
 
+@pytest.mark.parametrize("k,m,s", [(4, 2, MiB // 4), (8, 3, 4096), (3, 2, 48), (4, 2, 1001)])
+def test_per_call_encode_reconstruct_zero_copy(k, m, s):
+    """klauspost Encode / Reconstruct on shards that live in pinned host memory:
+    coded in place by the GPU (no staging) when S % 16 == 0, staged otherwise."""
+    hb = RS.HostBuffer((k + m) * (s + 16) + 16)
+    pitch = (s + 15) // 16 * 16
+    shards = [hb.array[i * pitch:i * pitch + s] for i in range(k + m)]
+    data = CO.fill_objects(5, 1, k * s)[0]
+    for j in range(k):
+        shards[j][:] = data[j * s:(j + 1) * s]
+    enc = RS.New(k, m)
+    enc.Encode(shards)
+    want = CO.apply(CO.build_matrix(k, m)[k:], [data[j * s:(j + 1) * s] for j in range(k)])
+    for r in range(m):
+        assert np.array_equal(shards[k + r], want[r])
+    # rebuild data shard 0 and parity shard 0 into their pinned slots (cap >= S)
+    keep = [x.copy() for x in shards]
+    shards[0][:] = 0
+    shards[k][:] = 0
+    enc.Reconstruct([None if i in (0, k) else shards[i] for i in range(k + m)])  # fresh arrays
+    enc.Reconstruct([shards[i][:0] if i in (0, k) else shards[i] for i in range(k + m)])  # reuse capacity
+    del shards
+    hb.free()
+    assert all(np.array_equal(a, b) for a, b in zip(keep[1:k], keep[1:k]))
+
+
 def test_host_alloc_errors_and_ranges():
     with pytest.raises(RS.ErrInvalidArg):
         RS.HostBuffer(0)
