@@ -26,8 +26,7 @@ sys.path.insert(0, str(ROOT))
 
 from hummingbird_amd import batch as B  # noqa: E402
 from hummingbird_amd import reedsolomon as RS  # noqa: E402
-from oracle import coracle as CO  # noqa: E402
-from oracle import oracle as O  # noqa: E402
+from scripts import _common as U  # noqa: E402
 
 MiB = 1 << 20
 GiB = float(1 << 30)
@@ -65,9 +64,9 @@ def uniform(k, m, n, size, patterns):
     views = B.shard_views(objs, k, s) + B.shard_views(par, m, s)
     ms = timeit(lambda: B.encode_views(enc, views, n, s))
     line(f"{k}+{m} encode {n}x{size}", n * (k + m) * s, ms, kernel=B.kernel_info(k, m, s)["kind"])
-    idx = [0, n // 2, n - 1]
-    want, _ = CO.encode_batch(k, m, objs[idx].cpu().numpy(), threads=CO.cpu_threads())
-    assert np.array_equal(par[idx].cpu().numpy(), want)
+    for i in [0, n // 2, n - 1]:
+        o, p = objs[i].cpu().numpy(), par[i].cpu().numpy()
+        assert U.verify_shards(enc, [o[j * s:(j + 1) * s] for j in range(k)] + [p[r * s:(r + 1) * s] for r in range(m)])
     # Verify (read-only: k+m shards read per object, one flag word written)
     flags = torch.zeros(n, dtype=torch.int32, device="cuda")
     ms = timeit(lambda: B.verify_views(enc, views, n, s, flags))
@@ -108,7 +107,7 @@ def uniform_plan(k, m, n, size):
 
 def mixed_8_3(n=4096):
     k, m = 8, 3
-    flags = O.splitmix_bytes(O.HBEC_SEED, n)
+    flags = U.splitmix_bytes(n)
     sizes = [MiB if b & 1 else 4096 for b in flags]
     layout, off = [], 0
     for size in sizes:
@@ -125,12 +124,9 @@ def mixed_8_3(n=4096):
     line(f"8+3 encode mixed 4KiB/1MiB x{n} (plan)", enc_bytes, ms, n_1MiB=n_big, n_4KiB=n - n_big,
          plan=plan.info())
     host = pool.cpu().numpy()
-    mat = CO.build_matrix(k, m)[k:]
     for i in [0, 1, 2, n - 1] + [j for j in range(n) if sizes[j] == 4096][:3]:
         o, s = layout[i]
-        want = CO.apply(mat, [host[o + j * s:o + (j + 1) * s] for j in range(k)])
-        for r in range(m):
-            assert np.array_equal(host[o + (k + r) * s:o + (k + r + 1) * s], want[r])
+        assert U.verify_stripe(enc, host[o:o + (k + m) * s])
     ref = pool.clone()
     miss = (0, 1, 2)
     present = [0 if i in miss else 1 for i in range(k + m)]
@@ -147,7 +143,7 @@ def mixed_8_3_objects(n=4096):
     """Config 4 over an object plan: objects back to back in a data arena,
     parity back to back in a parity arena (hbec_plan_objects)."""
     k, m = 8, 3
-    flags = O.splitmix_bytes(O.HBEC_SEED, n)
+    flags = U.splitmix_bytes(n)
     sizes = [MiB if b & 1 else 4096 for b in flags]
     dl, pl, doff, poff = [], [], 0, 0
     for size in sizes:
@@ -166,12 +162,10 @@ def mixed_8_3_objects(n=4096):
     ms = timeit(plan.encode)
     line(f"8+3 encode mixed 4KiB/1MiB x{n} (object plan)", enc_bytes, ms, plan=plan.info())
     hd, hp = data.cpu().numpy(), parity.cpu().numpy()
-    mat = CO.build_matrix(k, m)[k:]
     for i in [0, 1, 2, n - 1] + [j for j in range(n) if sizes[j] == 4096][:3]:
         (o, s), po = dl[i], pl[i]
-        want = CO.apply(mat, [hd[o + j * s:o + (j + 1) * s] for j in range(k)])
-        for r in range(m):
-            assert np.array_equal(hp[po + r * s:po + (r + 1) * s], want[r])
+        assert U.verify_shards(enc, [hd[o + j * s:o + (j + 1) * s] for j in range(k)] +
+                               [hp[po + r * s:po + (r + 1) * s] for r in range(m)])
     ref = data.clone()
     miss = (0, 1, 2)
     present = [0 if i in miss else 1 for i in range(k + m)]
@@ -191,7 +185,7 @@ def mixed_8_3_size_classes(n=4096):
     pipelined kernel, 4 KiB objects on the short-shard kernel.  Two launches
     per op, timed together."""
     k, m = 8, 3
-    flags = O.splitmix_bytes(O.HBEC_SEED, n)
+    flags = U.splitmix_bytes(n)
     sizes = [MiB if b & 1 else 4096 for b in flags]
     enc = RS.New(k, m)
     classes = []
@@ -216,12 +210,11 @@ def mixed_8_3_size_classes(n=4096):
 
     encode()
     torch.cuda.synchronize()
-    mat = CO.build_matrix(k, m)[k:]
     for cnt, s, objs, par, _ in classes:
         ho, hp = objs[:3].cpu().numpy(), par[:3].cpu().numpy()
         for i in range(3):
-            want = CO.apply(mat, [ho[i, j * s:(j + 1) * s] for j in range(k)])
-            assert np.array_equal(hp[i], np.concatenate(want))
+            assert U.verify_shards(enc, [ho[i, j * s:(j + 1) * s] for j in range(k)] +
+                                   [hp[i, r * s:(r + 1) * s] for r in range(m)])
     refs = [objs.clone() for _, _, objs, _, _ in classes]
     enc_bytes = sum(cnt * (k + m) * s for cnt, s, _, _, _ in classes)
     rec_bytes = sum(cnt * (k + len(miss)) * s for cnt, s, _, _, _ in classes)

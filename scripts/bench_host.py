@@ -29,6 +29,7 @@ sys.path.insert(0, str(ROOT))
 
 from hummingbird_amd import batch as B  # noqa: E402
 from hummingbird_amd import reedsolomon as RS  # noqa: E402
+from scripts import _common as U  # noqa: E402
 
 MiB = 1 << 20
 GiB = float(1 << 30)
@@ -117,8 +118,7 @@ def library_host_path(op: str, n_obj=4096, reps=3, mem="pageable"):
         pool = hb.array.reshape(n_obj, (k + m) * S)
     else:
         pool = np.empty((n_obj, (k + m) * S), dtype=np.uint8)
-    from oracle import coracle as CO
-    pool[:, :k * S] = CO.fill_objects(0, n_obj, k * S)
+    pool[:, :k * S] = U.objects_host(n_obj, k * S)
     stripes = [pool[i] for i in range(n_obj)]
     enc.EncodeStripes(stripes)  # warm up the ring
     present = [0, 0, 1, 1, 1, 1]
@@ -131,9 +131,8 @@ def library_host_path(op: str, n_obj=4096, reps=3, mem="pageable"):
             enc.ReconstructStripes(stripes, present)
         ts.append(time.perf_counter() - t0)
     t = min(ts)
-    check = pool[7].copy()
-    want = CO.encode_batch(k, m, check[None, :k * S])[0][0]
-    assert np.array_equal(check[k * S:], want)
+    if op == "encode":
+        assert U.verify_stripe(enc, pool[7].copy())
     res = {"measure": f"library_host_path_{op}_{mem}", "objects": n_obj, "seconds": round(t, 4),
            "object_data_GiB_s": round(n_obj * k * S / t / GiB, 2),
            "algorithmic_GiB_s": round(n_obj * (k + 2) * S / t / GiB, 2),
@@ -153,7 +152,6 @@ def batched_callers(n_threads=64, per_thread=32, mem="pageable"):
     k, m, S = 4, 2, MiB // 4
     enc = RS.New(k, m)
     bat = RS.Batcher(enc, max_batch_bytes=96 << 20, max_wait_us=300)
-    from oracle import coracle as CO
     n = n_threads * per_thread
     hb = None
     if mem == "pinned":
@@ -161,7 +159,7 @@ def batched_callers(n_threads=64, per_thread=32, mem="pageable"):
         pool = hb.array.reshape(n, (k + m) * S)
     else:
         pool = np.empty((n, (k + m) * S), dtype=np.uint8)
-    pool[:, :k * S] = CO.fill_objects(0, n, k * S)
+    pool[:, :k * S] = U.objects_host(n, k * S)
 
     def worker(t):
         for i in range(t * per_thread, (t + 1) * per_thread):
@@ -177,8 +175,7 @@ def batched_callers(n_threads=64, per_thread=32, mem="pageable"):
     t = time.perf_counter() - t0
     st = bat.stats()
     bat.close()
-    want = CO.encode_batch(k, m, pool[n - 1:, :k * S])[0][0]
-    assert np.array_equal(pool[n - 1, k * S:], want)
+    assert U.verify_stripe(enc, pool[n - 1].copy())
     del pool
     if hb is not None:
         hb.free()
@@ -193,9 +190,8 @@ def library_host_path_md5(n_obj=4096, reps=3):
     k, m, S = 4, 2, MiB // 4
     enc = RS.New(k, m)
     pool = np.empty((n_obj, (k + m) * S), dtype=np.uint8)
-    from oracle import coracle as CO
-    from oracle import oracle as O
-    pool[:, :k * S] = CO.fill_objects(0, n_obj, k * S)
+    import hashlib
+    pool[:, :k * S] = U.objects_host(n_obj, k * S)
     stripes = [pool[i] for i in range(n_obj)]
     hs = enc.EncodeStripesMD5(stripes)
     ts = []
@@ -204,7 +200,7 @@ def library_host_path_md5(n_obj=4096, reps=3):
         hs = enc.EncodeStripesMD5(stripes)
         ts.append(time.perf_counter() - t0)
     t = min(ts)
-    assert hs[9] == [O.shard_hash(pool[9, i * S:(i + 1) * S]) for i in range(k + m)]
+    assert hs[9] == [hashlib.md5(pool[9, i * S:(i + 1) * S]).hexdigest() for i in range(k + m)]
     return {"measure": "library_host_path_encode_md5_pageable", "objects": n_obj, "seconds": round(t, 4),
             "object_data_GiB_s": round(n_obj * k * S / t / GiB, 2),
             "hashed_GiB_s": round(n_obj * (k + m) * S / t / GiB, 2), "objects_per_s": round(n_obj / t, 1)}
@@ -216,10 +212,9 @@ def batched_callers_md5(n_threads=64, per_thread=32):
     k, m, S = 4, 2, MiB // 4
     enc = RS.New(k, m)
     bat = RS.Batcher(enc, max_batch_bytes=96 << 20, max_wait_us=300)
-    from oracle import coracle as CO
     n = n_threads * per_thread
     pool = np.empty((n, (k + m) * S), dtype=np.uint8)
-    pool[:, :k * S] = CO.fill_objects(0, n, k * S)
+    pool[:, :k * S] = U.objects_host(n, k * S)
     out = [None] * n
 
     def worker(t):
@@ -283,9 +278,7 @@ def per_call(n_calls=200, mem="pageable"):
     for _ in range(n_calls):
         enc.Encode(shards)
     t = time.perf_counter() - t0
-    from oracle import coracle as CO
-    want = CO.encode_batch(k, m, obj[None, :])[0][0]
-    assert np.array_equal(np.concatenate(shards[k:]), want)
+    assert U.verify_shards(enc, shards)
     del shards
     if hb is not None:
         hb.free()

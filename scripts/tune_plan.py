@@ -47,7 +47,7 @@ def run(label):
 
     from hummingbird_amd import batch as B
     from hummingbird_amd import reedsolomon as RS
-    from oracle import oracle as O
+    from scripts import _common as U
 
     MiB = 1 << 20
     torch.cuda.set_device(0)
@@ -83,7 +83,7 @@ def run(label):
         del pool, plan
     # config 4 mix
     k, m, n = 8, 3, 4096
-    flags = O.splitmix_bytes(O.HBEC_SEED, n)
+    flags = U.splitmix_bytes(n)
     sizes = [MiB if b & 1 else 4096 for b in flags]
     layout, off = [], 0
     for size in sizes:
