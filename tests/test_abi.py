@@ -219,3 +219,33 @@ def test_shardhash_validation_before_device():
     st[0].shard_len = 0
     assert L.hbec_encode_host_md5(enc.handle, st, 1, None) == N.ERR_INVALID_ARG
     assert L.hbec_encode_host_md5(enc.handle, st, 1, dig) == N.ERR_SHARD_NO_DATA
+
+
+def test_object_plan_validation_needs_no_device():
+    """hbec_plan_objects: argument checks and an empty plan answer without a GPU."""
+    import ctypes as C
+    enc = RS.New(4, 2)
+    h = C.c_void_p()
+    arr = (N.Object * 1)()
+    assert N.lib().hbec_plan_objects(None, arr, 1, C.byref(h)) == N.ERR_INVALID_ARG
+    assert N.lib().hbec_plan_objects(enc.handle, None, 1, C.byref(h)) == N.ERR_INVALID_ARG
+    arr[0].data, arr[0].parity, arr[0].shard_len = 4096, None, 16
+    assert N.lib().hbec_plan_objects(enc.handle, arr, 1, C.byref(h)) == N.ERR_INVALID_ARG  # m > 0, no parity
+    assert N.lib().hbec_plan_objects(enc.handle, arr, 0, C.byref(h)) == 0
+    nt, fb, sb, tb = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_int()
+    assert N.lib().hbec_plan_info(h, C.byref(nt), C.byref(tb), C.byref(fb), C.byref(sb)) == 0
+    assert (nt.value, fb.value, sb.value) == (0, 0, 0)
+    N.lib().hbec_plan_free(h)
+
+
+def test_host_devices_validation_needs_no_device():
+    import ctypes as C
+    enc = RS.New(4, 2)
+    devs = (C.c_int * 1)(0)
+    assert N.lib().hbec_encode_host_devices(enc.handle, None, 1, devs, 1) == N.ERR_INVALID_ARG
+    assert N.lib().hbec_encode_host_devices(enc.handle, None, 0, devs, 0) == N.ERR_INVALID_ARG  # n_devices <= 0
+    assert N.lib().hbec_reconstruct_host_devices(enc.handle, None, 0, None, 0, devs, 1) == N.ERR_INVALID_ARG
+    assert N.lib().hbec_host_alloc(0, C.byref(C.c_void_p())) == N.ERR_INVALID_ARG
+    out = C.c_uint64(7)
+    buf = (C.c_uint8 * 64)()
+    assert N.lib().hbec_host_device_addr(buf, 64, C.byref(out)) == 0 and out.value == 0  # pageable
