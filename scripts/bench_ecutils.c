@@ -97,19 +97,6 @@ int main(int argc, char** argv) {
     if (rc) { fprintf(stderr, "ec_split: %s\n", hbec_last_error()); return 1; }
     report("ec_split", k, m, (double)len, best);
 
-    uint8_t dig[16 * 64];
-    best = 1e30;
-    for (int r = 0; r < reps; ++r) {
-        Reader in = {obj, len, 0};
-        for (int i = 0; i < n; ++i) ws[i].pos = 0;
-        double t0 = now();
-        rc |= hbec_ec_split_md5(k, m, rd, &in, chunk, (int64_t)len, wr, wctx, dig);
-        double t = now() - t0;
-        if (t < best) best = t;
-    }
-    if (rc) { fprintf(stderr, "ec_split_md5: %s\n", hbec_last_error()); return 1; }
-    report("ec_split_md5", k, m, (double)len, best);
-
     /* ecGlue healthy (no GPU work) and with data shards 0..m-1 lost */
     uint8_t* out = malloc(len);
     Writer ow = {out, len, 0};

@@ -191,7 +191,7 @@ def test_pure_c_client(tmp_path):
 
 
 def test_shardhash_validation_before_device():
-    """hbec_md5_* / ec_split_md5 argument checks answer without a GPU; the
+    """hbec_md5_* argument checks answer without a GPU; the
     hashing itself has no CPU fallback."""
     L = N.lib()
     v = (N.View * 1)()
