@@ -233,6 +233,13 @@ uint64_t hbec::pinned_device_addr(const void* p, uint64_t len) {
         return 0;
     }
     if (a0.type != hipMemoryTypeHost || !a0.devicePointer) return 0;
+    // memory pinned elsewhere is only trusted on the device it was pinned for
+    // (hbec_host_alloc memory is portable: every device)
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess || a0.device != cur) {
+        (void)hipGetLastError();
+        return 0;
+    }
     if (hipPointerGetAttributes(&a1, reinterpret_cast<const uint8_t*>(p) + (len - 1)) != hipSuccess) {
         (void)hipGetLastError();
         return 0;
@@ -647,7 +654,9 @@ int hbec_host_alloc(size_t bytes, void** out) {
     if (!out || bytes == 0) return fail(HBEC_ERR_INVALID_ARG, "null out or zero size");
     *out = nullptr;
     void* h = nullptr;
-    hipError_t e = hipHostMalloc(&h, bytes, hipHostMallocDefault);
+    // portable + mapped: every device of the process may code it in place
+    // (coherent or non-coherent flags measured the same: 46.2-46.4 GiB/s)
+    hipError_t e = hipHostMalloc(&h, bytes, hipHostMallocPortable | hipHostMallocMapped);
     if (e != hipSuccess) return hip_fail(e, "hipHostMalloc");
     void* d = nullptr;
     e = hipHostGetDevicePointer(&d, h, 0);

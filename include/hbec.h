@@ -208,15 +208,18 @@ int hbec_reconstruct_plan(hbec_codec* codec, const hbec_plan* plan, const uint8_
  * kernel and D2H of successive chunks overlap on three streams.  Synchronous:
  * on return the parity (encode) or the rebuilt shards (reconstruct) are in the
  * caller's stripes.  k <= 8.  Env: HBEC_HOST_SLOT_MB (64), HBEC_HOST_THREADS.
- * Zero-copy: 16-B-aligned stripes in pinned, device-mapped host memory
- * (hbec_host_alloc, hipHostMalloc, hipHostRegister) are coded IN PLACE by the
- * GPU over PCIe — no staging copies, no CPU gather/scatter (HBEC_ZEROCOPY=0
- * sends them through the ring too).  Not for hbec_encode_host_md5. */
+ * Zero-copy: 16-B-aligned stripes in pinned, device-mapped host memory are
+ * coded IN PLACE by the GPU over PCIe — no staging copies, no CPU
+ * gather/scatter (HBEC_ZEROCOPY=0 sends them through the ring too).
+ * hbec_host_alloc memory qualifies on every device; memory pinned elsewhere
+ * (hipHostMalloc, hipHostRegister) on the device it was pinned for.  Not for
+ * hbec_encode_host_md5. */
 int hbec_encode_host(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n_stripes);
-/* Pinned, device-mapped host memory for stripe buffers (e.g. the cgo shim's
- * databuf pool, ecutils.go:31-35), so the host path above runs zero-copy.
- * hbec_host_device_addr: the device address of [p, p+len) if all of it is such
- * memory (any pinned allocation), else *dev = 0. */
+/* Pinned, device-mapped, portable host memory for stripe buffers (e.g. the
+ * cgo shim's databuf pool, ecutils.go:31-35), so the host path above runs
+ * zero-copy on any device.  hbec_host_device_addr: the device address of
+ * [p, p+len) for the calling thread's device if all of it is such memory,
+ * else *dev = 0. */
 int hbec_host_alloc(size_t bytes, void** out);
 void hbec_host_free(void* p);
 int hbec_host_device_addr(const void* p, uint64_t len, uint64_t* dev);
