@@ -124,20 +124,22 @@ struct hbec_batcher {
 extern "C" {
 
 int hbec_batcher_new(hbec_codec* codec, uint64_t max_batch_bytes, uint32_t max_wait_us, hbec_batcher** out) {
-    if (!codec || !out) return fail(HBEC_ERR_INVALID_ARG, "null argument");
-    *out = nullptr;
-    if (hbec_data_shards(codec) > 8) return fail(HBEC_ERR_INVALID_ARG, "batcher supports k <= 8");
-    std::unique_ptr<hbec_batcher> b(new (std::nothrow) hbec_batcher());
-    if (!b) return fail(HBEC_ERR_NOMEM, "batcher allocation");
-    hipError_t e = hipGetDevice(&b->device);
-    if (e != hipSuccess) return hbec::hip_fail(e, "hipGetDevice");
-    b->codec = codec;
-    b->max_batch_bytes = max_batch_bytes ? max_batch_bytes : (256ull << 20);
-    b->max_wait = std::chrono::microseconds(max_wait_us);
-    hbec_batcher* raw = b.get();
-    b->worker = std::thread([raw] { raw->run(); });
-    *out = b.release();
-    return HBEC_OK;
+    return hbec::guarded("hbec_batcher_new", [&]() -> int {
+        if (!codec || !out) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+        *out = nullptr;
+        if (hbec_data_shards(codec) > 8) return fail(HBEC_ERR_INVALID_ARG, "batcher supports k <= 8");
+        std::unique_ptr<hbec_batcher> b(new (std::nothrow) hbec_batcher());
+        if (!b) return fail(HBEC_ERR_NOMEM, "batcher allocation");
+        hipError_t e = hipGetDevice(&b->device);
+        if (e != hipSuccess) return hbec::hip_fail(e, "hipGetDevice");
+        b->codec = codec;
+        b->max_batch_bytes = max_batch_bytes ? max_batch_bytes : (256ull << 20);
+        b->max_wait = std::chrono::microseconds(max_wait_us);
+        hbec_batcher* raw = b.get();
+        b->worker = std::thread([raw] { raw->run(); });
+        *out = b.release();
+        return HBEC_OK;
+    });
 }
 
 void hbec_batcher_free(hbec_batcher* b) {
@@ -152,43 +154,51 @@ void hbec_batcher_free(hbec_batcher* b) {
 }
 
 int hbec_batcher_encode(hbec_batcher* b, const hbec_stripe* stripe) {
-    if (!b || !stripe) return fail(HBEC_ERR_INVALID_ARG, "null argument");
-    if (stripe->shard_len == 0) return HBEC_OK;
-    Request r;
-    r.stripe = *stripe;
-    r.op = 0;
-    return b->submit(r);
+    return hbec::guarded("hbec_batcher_encode", [&]() -> int {
+        if (!b || !stripe) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+        if (stripe->shard_len == 0) return HBEC_OK;
+        Request r;
+        r.stripe = *stripe;
+        r.op = 0;
+        return b->submit(r);
+    });
 }
 
 int hbec_batcher_encode_md5(hbec_batcher* b, const hbec_stripe* stripe, uint8_t* digests) {
-    if (!b || !stripe || !digests) return fail(HBEC_ERR_INVALID_ARG, "null argument");
-    if (stripe->shard_len == 0) return fail(HBEC_ERR_SHARD_NO_DATA, "stripe with zero shard length");
-    Request r;
-    r.stripe = *stripe;
-    r.op = 2;
-    r.digests = digests;
-    return b->submit(r);
+    return hbec::guarded("hbec_batcher_encode_md5", [&]() -> int {
+        if (!b || !stripe || !digests) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+        if (stripe->shard_len == 0) return fail(HBEC_ERR_SHARD_NO_DATA, "stripe with zero shard length");
+        Request r;
+        r.stripe = *stripe;
+        r.op = 2;
+        r.digests = digests;
+        return b->submit(r);
+    });
 }
 
 int hbec_batcher_reconstruct(hbec_batcher* b, const hbec_stripe* stripe, const uint8_t* present, int data_only) {
-    if (!b || !stripe || !present) return fail(HBEC_ERR_INVALID_ARG, "null argument");
-    if (stripe->shard_len == 0) return HBEC_OK;
-    const int n = hbec_data_shards(b->codec) + hbec_parity_shards(b->codec);
-    Request r;
-    r.stripe = *stripe;
-    r.op = 1;
-    r.present.assign(present, present + n);
-    for (auto& v : r.present) v = v ? 1 : 0;
-    r.data_only = data_only ? 1 : 0;
-    return b->submit(r);
+    return hbec::guarded("hbec_batcher_reconstruct", [&]() -> int {
+        if (!b || !stripe || !present) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+        if (stripe->shard_len == 0) return HBEC_OK;
+        const int n = hbec_data_shards(b->codec) + hbec_parity_shards(b->codec);
+        Request r;
+        r.stripe = *stripe;
+        r.op = 1;
+        r.present.assign(present, present + n);
+        for (auto& v : r.present) v = v ? 1 : 0;
+        r.data_only = data_only ? 1 : 0;
+        return b->submit(r);
+    });
 }
 
 int hbec_batcher_stats(hbec_batcher* b, uint64_t* batches, uint64_t* stripes) {
-    if (!b) return fail(HBEC_ERR_INVALID_ARG, "null argument");
-    std::lock_guard<std::mutex> g(b->mu);
-    if (batches) *batches = b->batches;
-    if (stripes) *stripes = b->stripes;
-    return HBEC_OK;
+    return hbec::guarded("hbec_batcher_stats", [&]() -> int {
+        if (!b) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+        std::lock_guard<std::mutex> g(b->mu);
+        if (batches) *batches = b->batches;
+        if (stripes) *stripes = b->stripes;
+        return HBEC_OK;
+    });
 }
 
 }  // extern "C"

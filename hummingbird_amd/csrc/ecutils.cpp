@@ -259,279 +259,287 @@ int64_t hbec_ec_shard_length(int64_t length, int data_shards) {
 // ecSplit (ecutils.go:26-72).
 int hbec_ec_split(int k, int m, hbec_read_fn read, void* fp, int chunk_size, int64_t content_length,
                   hbec_write_fn write, void* const* writers) {
-    CodecHolder enc;
-    int rc = hbec_new(k, m, &enc.c);
-    if (rc) return rc;
-    if (!read || chunk_size < 0) return fail(HBEC_ERR_INVALID_ARG, "ecSplit: bad arguments");
-    const int n = k + m;
-    std::vector<char> failed(n, 0);
-    struct Pending {
-        bool live = false;
-        uint8_t* host = nullptr;
-        uint64_t s = 0;
-    } pend[2];
-    RingHolder ring;
-    HostBufs bufs;
-    bufs.bytes = (size_t)n * (size_t)chunk_size;  // databuf := make([]byte, (k+m)*chunkSize)  (ecutils.go:32)
-    auto ensure_ring = [&]() -> int {
-        if (ring.r) return HBEC_OK;
-        return ring_acquire(bufs.bytes, (size_t)n * round16((uint64_t)chunk_size), &ring.r);
-    };
-    // write one finished stripe (ecutils.go:62-69): a failing writer is dropped
-    auto flush = [&](int b) -> int {
-        if (!pend[b].live) return HBEC_OK;
-        pend[b].live = false;
-        int r2 = wait_slot(*ring.r, b);
-        if (r2) return r2;
-        const uint64_t s = pend[b].s;
-        for (int i = 0; i < n; ++i)
-            if (writers && writers[i] && !failed[i])
-                if (!write || write(writers[i], pend[b].host + (size_t)i * s, s) != 0) failed[i] = 1;
-        return HBEC_OK;
-    };
-    int64_t total = 0;
-    int b = 0;
-    std::vector<hbec_view> v;
-    while (total < content_length) {
-        uint8_t* databuf = bufs.get(ring.r, b);
-        int64_t expected = (int64_t)k * chunk_size;
-        if (content_length - total < expected) expected = content_length - total;
-        size_t got = 0;
-        ReadStatus st = read_full(read, fp, databuf, (size_t)expected, &got);
-        if (st == READ_ERR || st == READ_UNEXPECTED_EOF || got == 0) {
-            const int r2 = flush(b ^ 1);  // the Go loop wrote the previous stripe before this read
+    return hbec::guarded("hbec_ec_split", [&]() -> int {
+        CodecHolder enc;
+        int rc = hbec_new(k, m, &enc.c);
+        if (rc) return rc;
+        if (!read || chunk_size < 0) return fail(HBEC_ERR_INVALID_ARG, "ecSplit: bad arguments");
+        const int n = k + m;
+        std::vector<char> failed(n, 0);
+        struct Pending {
+            bool live = false;
+            uint8_t* host = nullptr;
+            uint64_t s = 0;
+        } pend[2];
+        RingHolder ring;
+        HostBufs bufs;
+        bufs.bytes = (size_t)n * (size_t)chunk_size;  // databuf := make([]byte, (k+m)*chunkSize)  (ecutils.go:32)
+        auto ensure_ring = [&]() -> int {
+            if (ring.r) return HBEC_OK;
+            return ring_acquire(bufs.bytes, (size_t)n * round16((uint64_t)chunk_size), &ring.r);
+        };
+        // write one finished stripe (ecutils.go:62-69): a failing writer is dropped
+        auto flush = [&](int b) -> int {
+            if (!pend[b].live) return HBEC_OK;
+            pend[b].live = false;
+            int r2 = wait_slot(*ring.r, b);
             if (r2) return r2;
-            if (st == READ_ERR) return fail(HBEC_ERR_IO, "ecSplit: read failed");
-            return fail(HBEC_ERR_UNEXPECTED_EOF, "ecSplit: unexpected EOF");
+            const uint64_t s = pend[b].s;
+            for (int i = 0; i < n; ++i)
+                if (writers && writers[i] && !failed[i])
+                    if (!write || write(writers[i], pend[b].host + (size_t)i * s, s) != 0) failed[i] = 1;
+            return HBEC_OK;
+        };
+        int64_t total = 0;
+        int b = 0;
+        std::vector<hbec_view> v;
+        while (total < content_length) {
+            uint8_t* databuf = bufs.get(ring.r, b);
+            int64_t expected = (int64_t)k * chunk_size;
+            if (content_length - total < expected) expected = content_length - total;
+            size_t got = 0;
+            ReadStatus st = read_full(read, fp, databuf, (size_t)expected, &got);
+            if (st == READ_ERR || st == READ_UNEXPECTED_EOF || got == 0) {
+                const int r2 = flush(b ^ 1);  // the Go loop wrote the previous stripe before this read
+                if (r2) return r2;
+                if (st == READ_ERR) return fail(HBEC_ERR_IO, "ecSplit: read failed");
+                return fail(HBEC_ERR_UNEXPECTED_EOF, "ecSplit: unexpected EOF");
+            }
+            total += (int64_t)got;
+            while (got % (size_t)k != 0) databuf[got++] = 0;  // zero pad (ecutils.go:51-54)
+            rc = ensure_ring();
+            if (rc) return rc;
+            const SlotLayout L = layout_for(got / (size_t)k);
+            hipError_t e = upload(*ring.r, b, databuf, L, 0, k);
+            if (e != hipSuccess) return hbec::hip_fail(e, "ecSplit upload");
+            device_views(*ring.r, b, L, n, v);
+            rc = hbec_encode_batch(enc.c, v.data(), 1, L.pad, ring.r->stream);
+            if (rc) return rc;
+            if (L.contiguous()) {
+                e = hipMemcpyAsync(databuf + (size_t)k * L.s, ring.r->dbuf[b] + (size_t)k * L.s, (size_t)m * L.s,
+                                   hipMemcpyDeviceToHost, ring.r->stream);
+            } else {
+                for (int r = 0; r < m && e == hipSuccess; ++r) e = download(*ring.r, b, databuf, L, k + r);
+            }
+            if (e == hipSuccess) e = hipEventRecord(ring.r->ev[b], ring.r->stream);
+            if (e != hipSuccess) return hbec::hip_fail(e, "ecSplit download");
+            pend[b] = Pending{true, databuf, L.s};
+            rc = flush(b ^ 1);  // previous stripe: write it while this one is on the GPU
+            if (rc) return rc;
+            b ^= 1;
         }
-        total += (int64_t)got;
-        while (got % (size_t)k != 0) databuf[got++] = 0;  // zero pad (ecutils.go:51-54)
-        rc = ensure_ring();
-        if (rc) return rc;
-        const SlotLayout L = layout_for(got / (size_t)k);
-        hipError_t e = upload(*ring.r, b, databuf, L, 0, k);
-        if (e != hipSuccess) return hbec::hip_fail(e, "ecSplit upload");
-        device_views(*ring.r, b, L, n, v);
-        rc = hbec_encode_batch(enc.c, v.data(), 1, L.pad, ring.r->stream);
-        if (rc) return rc;
-        if (L.contiguous()) {
-            e = hipMemcpyAsync(databuf + (size_t)k * L.s, ring.r->dbuf[b] + (size_t)k * L.s, (size_t)m * L.s,
-                               hipMemcpyDeviceToHost, ring.r->stream);
-        } else {
-            for (int r = 0; r < m && e == hipSuccess; ++r) e = download(*ring.r, b, databuf, L, k + r);
-        }
-        if (e == hipSuccess) e = hipEventRecord(ring.r->ev[b], ring.r->stream);
-        if (e != hipSuccess) return hbec::hip_fail(e, "ecSplit download");
-        pend[b] = Pending{true, databuf, L.s};
-        rc = flush(b ^ 1);  // previous stripe: write it while this one is on the GPU
-        if (rc) return rc;
-        b ^= 1;
-    }
-    return flush(b ^ 1);
+        return flush(b ^ 1);
+    });
 }
 
 // ecReconstruct (ecutils.go:74-132).
 int hbec_ec_reconstruct(int k, int m, hbec_read_fn read, void* const* bodies, int chunk_size,
                         int64_t content_length, hbec_write_fn write, void* const* dsts, const int* dst_chunk_num,
                         int n_dsts) {
-    CodecHolder enc;
-    int rc = hbec_new(k, m, &enc.c);
-    if (rc) return rc;
-    const int n = k + m;
-    if (!bodies || chunk_size < 0 || n_dsts < 0 || (n_dsts > 0 && (!dsts || !dst_chunk_num || !write)))
-        return fail(HBEC_ERR_INVALID_ARG, "ecReconstruct: bad arguments");
-    for (int i = 0; i < n_dsts; ++i)
-        if (dst_chunk_num[i] < 0 || dst_chunk_num[i] >= n)
-            return fail(HBEC_ERR_INVALID_ARG, "ecReconstruct: chunk number out of range");
-    struct Pending {
-        bool live = false, gpu = false;
-        uint8_t* host = nullptr;
-        uint64_t s = 0;
-    } pend[2];
-    RingHolder ring;
-    HostBufs bufs;
-    bufs.bytes = (size_t)n * (size_t)chunk_size;
-    auto flush = [&](int b) -> int {
-        if (!pend[b].live) return HBEC_OK;
-        pend[b].live = false;
-        if (pend[b].gpu) {
-            int r2 = wait_slot(*ring.r, b);
-            if (r2) return r2;
-        }
-        const uint64_t s = pend[b].s;
-        for (int i = 0; i < n_dsts; ++i)  // ecutils.go:115-120
-            if (write(dsts[i], pend[b].host + (size_t)dst_chunk_num[i] * s, s) != 0)
-                return fail(HBEC_ERR_IO, "ecReconstruct: write failed");
-        return HBEC_OK;
-    };
-    std::vector<uint8_t> present((size_t)n);
-    std::vector<int> outputs;
-    int64_t total = 0;
-    int b = 0;
-    while (total < content_length) {
-        const int64_t exp = stripe_shard_size(k, chunk_size, content_length - total);
-        if (exp <= 0) return fail(HBEC_ERR_INVALID_ARG, "ecReconstruct: chunk size is zero");
-        uint8_t* databuf = bufs.get(ring.r, b);
-        int n_present = 0;
-        for (int i = 0; i < n; ++i) {  // a failed read is missing for this stripe only (ecutils.go:103-109)
-            present[i] = 0;
-            if (bodies[i]) {
-                size_t got = 0;
-                if (read && read_full(read, bodies[i], databuf + (size_t)i * exp, (size_t)exp, &got) == READ_OK)
-                    present[i] = 1;
-            }
-            n_present += present[i];
-        }
-        const SlotLayout L = layout_for((uint64_t)exp);
-        bool gpu = false;
-        if (n_present < n) {  // Reconstruct (ecutils.go:111) is a no-op when nothing is missing
-            if (!ring.r) rc = ring_acquire(bufs.bytes, (size_t)n * round16((uint64_t)chunk_size), &ring.r);
-            if (!rc) rc = queue_reconstruct(enc.c, *ring.r, b, databuf, L, present, 0, outputs);
-            if (rc) {
-                const int r2 = flush(b ^ 1);
-                return r2 ? r2 : rc;
-            }
-            gpu = !outputs.empty();
-        }
-        pend[b] = Pending{true, gpu, databuf, L.s};
-        for (int i = 0; i < k; ++i) {  // every data shard now has exp bytes
-            int64_t dl = exp;
-            if (content_length - total < dl) dl = content_length - total;
-            total += dl;
-        }
-        rc = flush(b ^ 1);
+    return hbec::guarded("hbec_ec_reconstruct", [&]() -> int {
+        CodecHolder enc;
+        int rc = hbec_new(k, m, &enc.c);
         if (rc) return rc;
-        b ^= 1;
-    }
-    return flush(b ^ 1);
+        const int n = k + m;
+        if (!bodies || chunk_size < 0 || n_dsts < 0 || (n_dsts > 0 && (!dsts || !dst_chunk_num || !write)))
+            return fail(HBEC_ERR_INVALID_ARG, "ecReconstruct: bad arguments");
+        for (int i = 0; i < n_dsts; ++i)
+            if (dst_chunk_num[i] < 0 || dst_chunk_num[i] >= n)
+                return fail(HBEC_ERR_INVALID_ARG, "ecReconstruct: chunk number out of range");
+        struct Pending {
+            bool live = false, gpu = false;
+            uint8_t* host = nullptr;
+            uint64_t s = 0;
+        } pend[2];
+        RingHolder ring;
+        HostBufs bufs;
+        bufs.bytes = (size_t)n * (size_t)chunk_size;
+        auto flush = [&](int b) -> int {
+            if (!pend[b].live) return HBEC_OK;
+            pend[b].live = false;
+            if (pend[b].gpu) {
+                int r2 = wait_slot(*ring.r, b);
+                if (r2) return r2;
+            }
+            const uint64_t s = pend[b].s;
+            for (int i = 0; i < n_dsts; ++i)  // ecutils.go:115-120
+                if (write(dsts[i], pend[b].host + (size_t)dst_chunk_num[i] * s, s) != 0)
+                    return fail(HBEC_ERR_IO, "ecReconstruct: write failed");
+            return HBEC_OK;
+        };
+        std::vector<uint8_t> present((size_t)n);
+        std::vector<int> outputs;
+        int64_t total = 0;
+        int b = 0;
+        while (total < content_length) {
+            const int64_t exp = stripe_shard_size(k, chunk_size, content_length - total);
+            if (exp <= 0) return fail(HBEC_ERR_INVALID_ARG, "ecReconstruct: chunk size is zero");
+            uint8_t* databuf = bufs.get(ring.r, b);
+            int n_present = 0;
+            for (int i = 0; i < n; ++i) {  // a failed read is missing for this stripe only (ecutils.go:103-109)
+                present[i] = 0;
+                if (bodies[i]) {
+                    size_t got = 0;
+                    if (read && read_full(read, bodies[i], databuf + (size_t)i * exp, (size_t)exp, &got) == READ_OK)
+                        present[i] = 1;
+                }
+                n_present += present[i];
+            }
+            const SlotLayout L = layout_for((uint64_t)exp);
+            bool gpu = false;
+            if (n_present < n) {  // Reconstruct (ecutils.go:111) is a no-op when nothing is missing
+                if (!ring.r) rc = ring_acquire(bufs.bytes, (size_t)n * round16((uint64_t)chunk_size), &ring.r);
+                if (!rc) rc = queue_reconstruct(enc.c, *ring.r, b, databuf, L, present, 0, outputs);
+                if (rc) {
+                    const int r2 = flush(b ^ 1);
+                    return r2 ? r2 : rc;
+                }
+                gpu = !outputs.empty();
+            }
+            pend[b] = Pending{true, gpu, databuf, L.s};
+            for (int i = 0; i < k; ++i) {  // every data shard now has exp bytes
+                int64_t dl = exp;
+                if (content_length - total < dl) dl = content_length - total;
+                total += dl;
+            }
+            rc = flush(b ^ 1);
+            if (rc) return rc;
+            b ^= 1;
+        }
+        return flush(b ^ 1);
+    });
 }
 
 // ecGlue (ecutils.go:134-186): healthy stripes never touch the GPU.
 int hbec_ec_glue(int k, int m, hbec_read_fn read, void* const* bodies, int chunk_size, int64_t content_length,
                  hbec_write_fn write, void* const* dsts, int n_dsts) {
-    CodecHolder enc;
-    int rc = hbec_new(k, m, &enc.c);
-    if (rc) return rc;
-    const int n = k + m;
-    if (!bodies || chunk_size < 0 || n_dsts < 0 || (n_dsts > 0 && !dsts))
-        return fail(HBEC_ERR_INVALID_ARG, "ecGlue: bad arguments");
-    std::vector<void*> live(dsts, dsts + n_dsts);
-    std::vector<char> failed(n, 0);
-    struct Pending {
-        bool live = false, gpu = false;
-        uint8_t* host = nullptr;
-        uint64_t s = 0;
-        int64_t remaining = 0;  // object bytes left when this stripe was read
-    } pend[2];
-    RingHolder ring;
-    HostBufs bufs;
-    bufs.bytes = (size_t)n * (size_t)chunk_size;
-    auto flush = [&](int b) -> int {
-        if (!pend[b].live) return HBEC_OK;
-        pend[b].live = false;
-        if (pend[b].gpu) {
-            int r2 = wait_slot(*ring.r, b);
-            if (r2) return r2;
-        }
-        const uint64_t s = pend[b].s;
-        int64_t remaining = pend[b].remaining;
-        for (int i = 0; i < k; ++i) {  // data shards, the last truncated (ecutils.go:171-183)
-            size_t len = (size_t)s;
-            if (remaining < (int64_t)len) len = (size_t)remaining;
-            for (int j = 0; j < n_dsts; ++j)
-                if (live[j] && (!write || write(live[j], pend[b].host + (size_t)i * s, len) != 0)) live[j] = nullptr;
-            remaining -= (int64_t)len;
-        }
-        return HBEC_OK;
-    };
-    std::vector<uint8_t> present((size_t)n);
-    std::vector<int> outputs;
-    int64_t written = 0;
-    int b = 0;
-    while (written < content_length) {
-        const int64_t exp = stripe_shard_size(k, chunk_size, content_length - written);
-        if (exp <= 0) return fail(HBEC_ERR_INVALID_ARG, "ecGlue: chunk size is zero");
-        uint8_t* databuf = bufs.get(ring.r, b);
-        bool data_missing = false;
-        for (int i = 0; i < n; ++i) {  // a failed body stays failed (ecutils.go:152-163)
-            present[i] = 0;
-            if (bodies[i] && !failed[i]) {
-                size_t got = 0;
-                if (read && read_full(read, bodies[i], databuf + (size_t)i * exp, (size_t)exp, &got) == READ_OK)
-                    present[i] = 1;
-                else
-                    failed[i] = 1;
-            }
-            if (i < k && !present[i]) data_missing = true;
-        }
-        const SlotLayout L = layout_for((uint64_t)exp);
-        bool gpu = false;
-        if (data_missing) {  // ReconstructData (ecutils.go:168)
-            if (!ring.r) rc = ring_acquire(bufs.bytes, (size_t)n * round16((uint64_t)chunk_size), &ring.r);
-            if (!rc) rc = queue_reconstruct(enc.c, *ring.r, b, databuf, L, present, 1, outputs);
-            if (rc) {
-                const int r2 = flush(b ^ 1);
-                return r2 ? r2 : rc;
-            }
-            gpu = !outputs.empty();
-        }
-        pend[b].live = true;
-        pend[b].gpu = gpu;
-        pend[b].host = databuf;
-        pend[b].s = L.s;
-        pend[b].remaining = content_length - written;
-        for (int i = 0; i < k; ++i) {
-            int64_t len = exp;
-            if (content_length - written < len) len = content_length - written;
-            written += len;
-        }
-        rc = flush(b ^ 1);
+    return hbec::guarded("hbec_ec_glue", [&]() -> int {
+        CodecHolder enc;
+        int rc = hbec_new(k, m, &enc.c);
         if (rc) return rc;
-        b ^= 1;
-    }
-    return flush(b ^ 1);
+        const int n = k + m;
+        if (!bodies || chunk_size < 0 || n_dsts < 0 || (n_dsts > 0 && !dsts))
+            return fail(HBEC_ERR_INVALID_ARG, "ecGlue: bad arguments");
+        std::vector<void*> live(dsts, dsts + n_dsts);
+        std::vector<char> failed(n, 0);
+        struct Pending {
+            bool live = false, gpu = false;
+            uint8_t* host = nullptr;
+            uint64_t s = 0;
+            int64_t remaining = 0;  // object bytes left when this stripe was read
+        } pend[2];
+        RingHolder ring;
+        HostBufs bufs;
+        bufs.bytes = (size_t)n * (size_t)chunk_size;
+        auto flush = [&](int b) -> int {
+            if (!pend[b].live) return HBEC_OK;
+            pend[b].live = false;
+            if (pend[b].gpu) {
+                int r2 = wait_slot(*ring.r, b);
+                if (r2) return r2;
+            }
+            const uint64_t s = pend[b].s;
+            int64_t remaining = pend[b].remaining;
+            for (int i = 0; i < k; ++i) {  // data shards, the last truncated (ecutils.go:171-183)
+                size_t len = (size_t)s;
+                if (remaining < (int64_t)len) len = (size_t)remaining;
+                for (int j = 0; j < n_dsts; ++j)
+                    if (live[j] && (!write || write(live[j], pend[b].host + (size_t)i * s, len) != 0)) live[j] = nullptr;
+                remaining -= (int64_t)len;
+            }
+            return HBEC_OK;
+        };
+        std::vector<uint8_t> present((size_t)n);
+        std::vector<int> outputs;
+        int64_t written = 0;
+        int b = 0;
+        while (written < content_length) {
+            const int64_t exp = stripe_shard_size(k, chunk_size, content_length - written);
+            if (exp <= 0) return fail(HBEC_ERR_INVALID_ARG, "ecGlue: chunk size is zero");
+            uint8_t* databuf = bufs.get(ring.r, b);
+            bool data_missing = false;
+            for (int i = 0; i < n; ++i) {  // a failed body stays failed (ecutils.go:152-163)
+                present[i] = 0;
+                if (bodies[i] && !failed[i]) {
+                    size_t got = 0;
+                    if (read && read_full(read, bodies[i], databuf + (size_t)i * exp, (size_t)exp, &got) == READ_OK)
+                        present[i] = 1;
+                    else
+                        failed[i] = 1;
+                }
+                if (i < k && !present[i]) data_missing = true;
+            }
+            const SlotLayout L = layout_for((uint64_t)exp);
+            bool gpu = false;
+            if (data_missing) {  // ReconstructData (ecutils.go:168)
+                if (!ring.r) rc = ring_acquire(bufs.bytes, (size_t)n * round16((uint64_t)chunk_size), &ring.r);
+                if (!rc) rc = queue_reconstruct(enc.c, *ring.r, b, databuf, L, present, 1, outputs);
+                if (rc) {
+                    const int r2 = flush(b ^ 1);
+                    return r2 ? r2 : rc;
+                }
+                gpu = !outputs.empty();
+            }
+            pend[b].live = true;
+            pend[b].gpu = gpu;
+            pend[b].host = databuf;
+            pend[b].s = L.s;
+            pend[b].remaining = content_length - written;
+            for (int i = 0; i < k; ++i) {
+                int64_t len = exp;
+                if (content_length - written < len) len = content_length - written;
+                written += len;
+            }
+            rc = flush(b ^ 1);
+            if (rc) return rc;
+            b ^= 1;
+        }
+        return flush(b ^ 1);
+    });
 }
 
 int hbec_parse_ec_scheme(const char* scheme, char* algo, size_t algo_cap, int* data_shards, int* parity_shards,
                          int* chunk_size) {
-    if (!scheme) return fail(HBEC_ERR_INVALID_ARG, "scheme is NULL");
-    std::vector<std::string> sec;
-    std::string cur;
-    for (const char* p = scheme; *p; ++p) {
-        if (*p == '/') {
-            sec.push_back(cur);
-            cur.clear();
-        } else {
-            cur.push_back(*p);
+    return hbec::guarded("hbec_parse_ec_scheme", [&]() -> int {
+        if (!scheme) return fail(HBEC_ERR_INVALID_ARG, "scheme is NULL");
+        std::vector<std::string> sec;
+        std::string cur;
+        for (const char* p = scheme; *p; ++p) {
+            if (*p == '/') {
+                sec.push_back(cur);
+                cur.clear();
+            } else {
+                cur.push_back(*p);
+            }
         }
-    }
-    sec.push_back(cur);
-    if (sec.size() != 4) return fail(HBEC_ERR_SCHEME, std::to_string(sec.size()) + " scheme sections");
-    // strconv.Atoi: optional sign then one or more ASCII digits
-    auto atoi_go = [](const std::string& s, int* out) {
-        size_t i = 0;
-        if (!s.empty() && (s[0] == '+' || s[0] == '-')) i = 1;
-        if (i >= s.size()) return false;
-        for (size_t j = i; j < s.size(); ++j)
-            if (s[j] < '0' || s[j] > '9') return false;
-        errno = 0;
-        long long v = std::strtoll(s.c_str(), nullptr, 10);
-        if (errno == ERANGE || v < INT_MIN || v > INT_MAX) return false;
-        *out = (int)v;
-        return true;
-    };
-    int k = 0, m = 0, c = 0;
-    if (!atoi_go(sec[1], &k)) return fail(HBEC_ERR_SCHEME, "Invalid data shard count");
-    if (!atoi_go(sec[2], &m)) return fail(HBEC_ERR_SCHEME, "Invalid parity shard count");
-    if (!atoi_go(sec[3], &c)) return fail(HBEC_ERR_SCHEME, "Invalid chunk size");
-    if (algo) {
-        if (algo_cap < sec[0].size() + 1) return fail(HBEC_ERR_INVALID_ARG, "algo buffer too small");
-        std::memcpy(algo, sec[0].c_str(), sec[0].size() + 1);
-    }
-    if (data_shards) *data_shards = k;
-    if (parity_shards) *parity_shards = m;
-    if (chunk_size) *chunk_size = c;
-    return HBEC_OK;
+        sec.push_back(cur);
+        if (sec.size() != 4) return fail(HBEC_ERR_SCHEME, std::to_string(sec.size()) + " scheme sections");
+        // strconv.Atoi: optional sign then one or more ASCII digits
+        auto atoi_go = [](const std::string& s, int* out) {
+            size_t i = 0;
+            if (!s.empty() && (s[0] == '+' || s[0] == '-')) i = 1;
+            if (i >= s.size()) return false;
+            for (size_t j = i; j < s.size(); ++j)
+                if (s[j] < '0' || s[j] > '9') return false;
+            errno = 0;
+            long long v = std::strtoll(s.c_str(), nullptr, 10);
+            if (errno == ERANGE || v < INT_MIN || v > INT_MAX) return false;
+            *out = (int)v;
+            return true;
+        };
+        int k = 0, m = 0, c = 0;
+        if (!atoi_go(sec[1], &k)) return fail(HBEC_ERR_SCHEME, "Invalid data shard count");
+        if (!atoi_go(sec[2], &m)) return fail(HBEC_ERR_SCHEME, "Invalid parity shard count");
+        if (!atoi_go(sec[3], &c)) return fail(HBEC_ERR_SCHEME, "Invalid chunk size");
+        if (algo) {
+            if (algo_cap < sec[0].size() + 1) return fail(HBEC_ERR_INVALID_ARG, "algo buffer too small");
+            std::memcpy(algo, sec[0].c_str(), sec[0].size() + 1);
+        }
+        if (data_shards) *data_shards = k;
+        if (parity_shards) *parity_shards = m;
+        if (chunk_size) *chunk_size = c;
+        return HBEC_OK;
+    });
 }
 
 void hbec_range_chunk_align(int64_t start, int64_t end, int64_t chunk_size, int data_shards, int64_t* out_start,

@@ -391,19 +391,21 @@ const char* hbec_last_error(void) { return t_last_error.c_str(); }
 int hbec_version(void) { return HBEC_VERSION; }
 
 int hbec_new(int data_shards, int parity_shards, hbec_codec** out) {
-    if (!out) return fail(HBEC_ERR_INVALID_ARG, "out is NULL");
-    *out = nullptr;
-    if (data_shards <= 0 || parity_shards < 0)
-        return fail(HBEC_ERR_INV_SHARD_NUM, "cannot create Encoder with zero or less data/parity shards");
-    if (data_shards + parity_shards > 256)
-        return fail(HBEC_ERR_MAX_SHARD_NUM, "cannot create Encoder with more than 256 data+parity shards");
-    std::unique_ptr<hbec_codec> c(new (std::nothrow) hbec_codec());
-    if (!c) return fail(HBEC_ERR_NOMEM, "codec allocation");
-    c->k = data_shards;
-    c->m = parity_shards;
-    if (!build_matrix(c->k, c->m, c->matrix)) return fail(HBEC_ERR_SINGULAR, "matrix is singular");
-    *out = c.release();
-    return HBEC_OK;
+    return hbec::guarded("hbec_new", [&]() -> int {
+        if (!out) return fail(HBEC_ERR_INVALID_ARG, "out is NULL");
+        *out = nullptr;
+        if (data_shards <= 0 || parity_shards < 0)
+            return fail(HBEC_ERR_INV_SHARD_NUM, "cannot create Encoder with zero or less data/parity shards");
+        if (data_shards + parity_shards > 256)
+            return fail(HBEC_ERR_MAX_SHARD_NUM, "cannot create Encoder with more than 256 data+parity shards");
+        std::unique_ptr<hbec_codec> c(new (std::nothrow) hbec_codec());
+        if (!c) return fail(HBEC_ERR_NOMEM, "codec allocation");
+        c->k = data_shards;
+        c->m = parity_shards;
+        if (!build_matrix(c->k, c->m, c->matrix)) return fail(HBEC_ERR_SINGULAR, "matrix is singular");
+        *out = c.release();
+        return HBEC_OK;
+    });
 }
 
 void hbec_free(hbec_codec* codec) { delete codec; }
@@ -412,117 +414,133 @@ int hbec_data_shards(const hbec_codec* c) { return c ? c->k : HBEC_ERR_INVALID_A
 int hbec_parity_shards(const hbec_codec* c) { return c ? c->m : HBEC_ERR_INVALID_ARG; }
 
 int hbec_matrix(const hbec_codec* c, uint8_t* out) {
-    if (!c || !out) return fail(HBEC_ERR_INVALID_ARG, "null argument");
-    std::memcpy(out, c->matrix.data(), c->matrix.size());
-    return HBEC_OK;
+    return hbec::guarded("hbec_matrix", [&]() -> int {
+        if (!c || !out) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+        std::memcpy(out, c->matrix.data(), c->matrix.size());
+        return HBEC_OK;
+    });
 }
 
 int hbec_encode(hbec_codec* c, uint8_t* const* shards, const size_t* lens, int n_shards) {
-    if (!c || !shards || !lens) return fail(HBEC_ERR_INVALID_ARG, "null argument");
-    if (n_shards != c->k + c->m) return fail(HBEC_ERR_TOO_FEW_SHARDS, "too few shards given");
-    size_t s = 0;
-    int rc = check_shards(lens, n_shards, false, &s);
-    if (rc) return rc;
-    for (int i = 0; i < n_shards; ++i)
-        if (!shards[i]) return fail(HBEC_ERR_INVALID_ARG, "null shard pointer");
-    return host_apply(c->m, c->k, c->matrix.data() + (size_t)c->k * c->k, shards, shards + c->k, s);
+    return hbec::guarded("hbec_encode", [&]() -> int {
+        if (!c || !shards || !lens) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+        if (n_shards != c->k + c->m) return fail(HBEC_ERR_TOO_FEW_SHARDS, "too few shards given");
+        size_t s = 0;
+        int rc = check_shards(lens, n_shards, false, &s);
+        if (rc) return rc;
+        for (int i = 0; i < n_shards; ++i)
+            if (!shards[i]) return fail(HBEC_ERR_INVALID_ARG, "null shard pointer");
+        return host_apply(c->m, c->k, c->matrix.data() + (size_t)c->k * c->k, shards, shards + c->k, s);
+    });
 }
 
 int hbec_reconstruct(hbec_codec* c, uint8_t* const* shards, size_t* lens, int n_shards, int data_only) {
-    if (!c || !shards || !lens) return fail(HBEC_ERR_INVALID_ARG, "null argument");
-    if (n_shards != c->k + c->m) return fail(HBEC_ERR_TOO_FEW_SHARDS, "too few shards given");
-    size_t s = 0;
-    int rc = check_shards(lens, n_shards, true, &s);
-    if (rc) return rc;
-    std::vector<uint8_t> present(n_shards);
-    int n_present = 0, data_present = 0;
-    for (int i = 0; i < n_shards; ++i) {
-        present[i] = lens[i] != 0;
-        n_present += present[i];
-        if (i < c->k) data_present += present[i];
-    }
-    if (n_present == n_shards || (data_only && data_present == c->k)) return HBEC_OK;
-    if (n_present < c->k) return fail(HBEC_ERR_TOO_FEW_SHARDS, "too few shards given");
-    std::vector<int> surv, outs;
-    std::vector<uint8_t> rows;
-    rc = decode_rows(c, present, data_only != 0, surv, outs, rows);
-    if (rc) return rc;
-    std::vector<const uint8_t*> in(surv.size());
-    std::vector<uint8_t*> out(outs.size());
-    for (size_t j = 0; j < surv.size(); ++j) in[j] = shards[surv[j]];
-    for (size_t o = 0; o < outs.size(); ++o) {
-        if (!shards[outs[o]]) return fail(HBEC_ERR_INVALID_ARG, "missing shard has no buffer");
-        out[o] = shards[outs[o]];
-    }
-    rc = host_apply((int)outs.size(), c->k, rows.data(), in.data(), out.data(), s);
-    if (rc) return rc;
-    for (int i : outs) lens[i] = s;
-    return HBEC_OK;
+    return hbec::guarded("hbec_reconstruct", [&]() -> int {
+        if (!c || !shards || !lens) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+        if (n_shards != c->k + c->m) return fail(HBEC_ERR_TOO_FEW_SHARDS, "too few shards given");
+        size_t s = 0;
+        int rc = check_shards(lens, n_shards, true, &s);
+        if (rc) return rc;
+        std::vector<uint8_t> present(n_shards);
+        int n_present = 0, data_present = 0;
+        for (int i = 0; i < n_shards; ++i) {
+            present[i] = lens[i] != 0;
+            n_present += present[i];
+            if (i < c->k) data_present += present[i];
+        }
+        if (n_present == n_shards || (data_only && data_present == c->k)) return HBEC_OK;
+        if (n_present < c->k) return fail(HBEC_ERR_TOO_FEW_SHARDS, "too few shards given");
+        std::vector<int> surv, outs;
+        std::vector<uint8_t> rows;
+        rc = decode_rows(c, present, data_only != 0, surv, outs, rows);
+        if (rc) return rc;
+        std::vector<const uint8_t*> in(surv.size());
+        std::vector<uint8_t*> out(outs.size());
+        for (size_t j = 0; j < surv.size(); ++j) in[j] = shards[surv[j]];
+        for (size_t o = 0; o < outs.size(); ++o) {
+            if (!shards[outs[o]]) return fail(HBEC_ERR_INVALID_ARG, "missing shard has no buffer");
+            out[o] = shards[outs[o]];
+        }
+        rc = host_apply((int)outs.size(), c->k, rows.data(), in.data(), out.data(), s);
+        if (rc) return rc;
+        for (int i : outs) lens[i] = s;
+        return HBEC_OK;
+    });
 }
 
 int hbec_encode_batch(hbec_codec* c, const hbec_view* views, uint64_t n_objects, uint64_t shard_len,
                       void* hip_stream) {
-    if (!c || !views) return fail(HBEC_ERR_INVALID_ARG, "null argument");
-    return apply_views(c->m, c->k, c->matrix.data() + (size_t)c->k * c->k, views, views + c->k, n_objects,
-                       shard_len, static_cast<hipStream_t>(hip_stream));
+    return hbec::guarded("hbec_encode_batch", [&]() -> int {
+        if (!c || !views) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+        return apply_views(c->m, c->k, c->matrix.data() + (size_t)c->k * c->k, views, views + c->k, n_objects,
+                           shard_len, static_cast<hipStream_t>(hip_stream));
+    });
 }
 
 int hbec_decode_rows(hbec_codec* c, const uint8_t* present, int data_only, int* survivors, int* outputs,
                      int* n_outputs, uint8_t* rows) {
-    if (!c || !present || !survivors || !outputs || !n_outputs || !rows)
-        return fail(HBEC_ERR_INVALID_ARG, "null argument");
-    std::vector<uint8_t> p(present, present + c->k + c->m);
-    for (auto& v : p) v = v ? 1 : 0;
-    std::vector<int> surv, outs;
-    std::vector<uint8_t> r;
-    int rc = decode_rows(c, p, data_only != 0, surv, outs, r);
-    if (rc) return rc;
-    std::copy(surv.begin(), surv.end(), survivors);
-    std::copy(outs.begin(), outs.end(), outputs);
-    *n_outputs = (int)outs.size();
-    std::copy(r.begin(), r.end(), rows);
-    return HBEC_OK;
+    return hbec::guarded("hbec_decode_rows", [&]() -> int {
+        if (!c || !present || !survivors || !outputs || !n_outputs || !rows)
+            return fail(HBEC_ERR_INVALID_ARG, "null argument");
+        std::vector<uint8_t> p(present, present + c->k + c->m);
+        for (auto& v : p) v = v ? 1 : 0;
+        std::vector<int> surv, outs;
+        std::vector<uint8_t> r;
+        int rc = decode_rows(c, p, data_only != 0, surv, outs, r);
+        if (rc) return rc;
+        std::copy(surv.begin(), surv.end(), survivors);
+        std::copy(outs.begin(), outs.end(), outputs);
+        *n_outputs = (int)outs.size();
+        std::copy(r.begin(), r.end(), rows);
+        return HBEC_OK;
+    });
 }
 
 int hbec_reconstruct_batch(hbec_codec* c, const hbec_view* views, const uint8_t* present, uint64_t n_objects,
                            uint64_t shard_len, int data_only, void* hip_stream) {
-    if (!c || !views || !present) return fail(HBEC_ERR_INVALID_ARG, "null argument");
-    const int n = c->k + c->m;
-    std::vector<uint8_t> p(present, present + n);
-    int n_present = 0, data_present = 0;
-    for (int i = 0; i < n; ++i) {
-        p[i] = p[i] ? 1 : 0;
-        n_present += p[i];
-        if (i < c->k) data_present += p[i];
-    }
-    if (n_present == n || (data_only && data_present == c->k)) return HBEC_OK;
-    if (n_present < c->k) return fail(HBEC_ERR_TOO_FEW_SHARDS, "too few shards given");
-    std::vector<int> surv, outs;
-    std::vector<uint8_t> rows;
-    int rc = decode_rows(c, p, data_only != 0, surv, outs, rows);
-    if (rc) return rc;
-    std::vector<hbec_view> vin(surv.size()), vout(outs.size());
-    for (size_t j = 0; j < surv.size(); ++j) vin[j] = views[surv[j]];
-    for (size_t o = 0; o < outs.size(); ++o) vout[o] = views[outs[o]];
-    return apply_views((int)outs.size(), c->k, rows.data(), vin.data(), vout.data(), n_objects, shard_len,
-                       static_cast<hipStream_t>(hip_stream));
+    return hbec::guarded("hbec_reconstruct_batch", [&]() -> int {
+        if (!c || !views || !present) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+        const int n = c->k + c->m;
+        std::vector<uint8_t> p(present, present + n);
+        int n_present = 0, data_present = 0;
+        for (int i = 0; i < n; ++i) {
+            p[i] = p[i] ? 1 : 0;
+            n_present += p[i];
+            if (i < c->k) data_present += p[i];
+        }
+        if (n_present == n || (data_only && data_present == c->k)) return HBEC_OK;
+        if (n_present < c->k) return fail(HBEC_ERR_TOO_FEW_SHARDS, "too few shards given");
+        std::vector<int> surv, outs;
+        std::vector<uint8_t> rows;
+        int rc = decode_rows(c, p, data_only != 0, surv, outs, rows);
+        if (rc) return rc;
+        std::vector<hbec_view> vin(surv.size()), vout(outs.size());
+        for (size_t j = 0; j < surv.size(); ++j) vin[j] = views[surv[j]];
+        for (size_t o = 0; o < outs.size(); ++o) vout[o] = views[outs[o]];
+        return apply_views((int)outs.size(), c->k, rows.data(), vin.data(), vout.data(), n_objects, shard_len,
+                           static_cast<hipStream_t>(hip_stream));
+    });
 }
 
 int hbec_apply_batch(int rows, int cols, const uint8_t* coeffs, const hbec_view* in, const hbec_view* out,
                      uint64_t n_objects, uint64_t shard_len, void* hip_stream) {
-    return apply_views(rows, cols, coeffs, in, out, n_objects, shard_len, static_cast<hipStream_t>(hip_stream));
+    return hbec::guarded("hbec_apply_batch", [&]() -> int {
+        return apply_views(rows, cols, coeffs, in, out, n_objects, shard_len, static_cast<hipStream_t>(hip_stream));
+    });
 }
 
 int hbec_fill_splitmix(void* dst, uint64_t n_objects, uint64_t obj_len, uint64_t obj_stride, uint64_t base_seed,
                        uint64_t first, void* hip_stream) {
-    if (!dst) return fail(HBEC_ERR_INVALID_ARG, "null dst");
-    if (n_objects == 0 || obj_len == 0) return HBEC_OK;
-    const uint64_t words = ((obj_len + 7) / 8) * n_objects;
-    const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((words + kBlockThreads - 1) / kBlockThreads, 16384));
-    hipError_t e = launch_fill(static_cast<uint8_t*>(dst), n_objects, obj_len, obj_stride, base_seed, first, grid,
-                               static_cast<hipStream_t>(hip_stream));
-    if (e != hipSuccess) return hip_fail(e, "launch fill_splitmix");
-    return HBEC_OK;
+    return hbec::guarded("hbec_fill_splitmix", [&]() -> int {
+        if (!dst) return fail(HBEC_ERR_INVALID_ARG, "null dst");
+        if (n_objects == 0 || obj_len == 0) return HBEC_OK;
+        const uint64_t words = ((obj_len + 7) / 8) * n_objects;
+        const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((words + kBlockThreads - 1) / kBlockThreads, 16384));
+        hipError_t e = launch_fill(static_cast<uint8_t*>(dst), n_objects, obj_len, obj_stride, base_seed, first, grid,
+                                   static_cast<hipStream_t>(hip_stream));
+        if (e != hipSuccess) return hip_fail(e, "launch fill_splitmix");
+        return HBEC_OK;
+    });
 }
 
 // ---- Encoder.Verify ------------------------------------------------------
@@ -610,73 +628,81 @@ static int verify_views(hbec_codec* c, const hbec_view* views, uint64_t n_obj, u
 
 int hbec_verify_batch(hbec_codec* c, const hbec_view* views, uint64_t n_objects, uint64_t shard_len,
                       uint32_t* d_flags, void* hip_stream) {
-    if (!c || !views || (!d_flags && n_objects)) return fail(HBEC_ERR_INVALID_ARG, "null argument");
-    return verify_views(c, views, n_objects, shard_len, d_flags, static_cast<hipStream_t>(hip_stream));
+    return hbec::guarded("hbec_verify_batch", [&]() -> int {
+        if (!c || !views || (!d_flags && n_objects)) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+        return verify_views(c, views, n_objects, shard_len, d_flags, static_cast<hipStream_t>(hip_stream));
+    });
 }
 
 int hbec_verify(hbec_codec* c, uint8_t* const* shards, const size_t* lens, int n_shards, int* ok) {
-    if (!c || !shards || !lens || !ok) return fail(HBEC_ERR_INVALID_ARG, "null argument");
-    *ok = 0;
-    if (n_shards != c->k + c->m) return fail(HBEC_ERR_TOO_FEW_SHARDS, "too few shards given");
-    size_t s = 0;
-    int rc = check_shards(lens, n_shards, false, &s);
-    if (rc) return rc;
-    if (c->m == 0) {
-        *ok = 1;
-        return HBEC_OK;
-    }
-    const uint64_t pad = round16(s);
-    const int n = c->k + c->m;
-    Staging* st = nullptr;
-    rc = staging_acquire((size_t)pad * n + 16, &st);
-    if (rc) return rc;
-    std::vector<hbec_view> v(n);
-    hipError_t e = hipSuccess;
-    for (int i = 0; i < n && e == hipSuccess; ++i) {
-        v[i] = {st->dbuf + (size_t)i * pad, 0};
-        e = hipMemcpyAsync(v[i].base, shards[i], s, hipMemcpyHostToDevice, st->stream);
-        // padding bytes must compare equal: zero both sides' tails
-        if (e == hipSuccess && pad > s)
-            e = hipMemsetAsync(static_cast<uint8_t*>(v[i].base) + s, 0, pad - s, st->stream);
-    }
-    uint32_t* d_flag = reinterpret_cast<uint32_t*>(st->dbuf + (size_t)pad * n);
-    if (e == hipSuccess) e = hipMemsetAsync(d_flag, 0, sizeof(uint32_t), st->stream);
-    if (e != hipSuccess) {
+    return hbec::guarded("hbec_verify", [&]() -> int {
+        if (!c || !shards || !lens || !ok) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+        *ok = 0;
+        if (n_shards != c->k + c->m) return fail(HBEC_ERR_TOO_FEW_SHARDS, "too few shards given");
+        size_t s = 0;
+        int rc = check_shards(lens, n_shards, false, &s);
+        if (rc) return rc;
+        if (c->m == 0) {
+            *ok = 1;
+            return HBEC_OK;
+        }
+        const uint64_t pad = round16(s);
+        const int n = c->k + c->m;
+        Staging* st = nullptr;
+        rc = staging_acquire((size_t)pad * n + 16, &st);
+        if (rc) return rc;
+        std::vector<hbec_view> v(n);
+        hipError_t e = hipSuccess;
+        for (int i = 0; i < n && e == hipSuccess; ++i) {
+            v[i] = {st->dbuf + (size_t)i * pad, 0};
+            e = hipMemcpyAsync(v[i].base, shards[i], s, hipMemcpyHostToDevice, st->stream);
+            // padding bytes must compare equal: zero both sides' tails
+            if (e == hipSuccess && pad > s)
+                e = hipMemsetAsync(static_cast<uint8_t*>(v[i].base) + s, 0, pad - s, st->stream);
+        }
+        uint32_t* d_flag = reinterpret_cast<uint32_t*>(st->dbuf + (size_t)pad * n);
+        if (e == hipSuccess) e = hipMemsetAsync(d_flag, 0, sizeof(uint32_t), st->stream);
+        if (e != hipSuccess) {
+            staging_release(st);
+            return hip_fail(e, "verify staging");
+        }
+        rc = verify_views(c, v.data(), 1, pad, d_flag, st->stream);
+        uint32_t h_flag = 1;
+        if (rc == HBEC_OK) e = hipMemcpyAsync(&h_flag, d_flag, sizeof(h_flag), hipMemcpyDeviceToHost, st->stream);
+        hipError_t e2 = hipStreamSynchronize(st->stream);
         staging_release(st);
-        return hip_fail(e, "verify staging");
-    }
-    rc = verify_views(c, v.data(), 1, pad, d_flag, st->stream);
-    uint32_t h_flag = 1;
-    if (rc == HBEC_OK) e = hipMemcpyAsync(&h_flag, d_flag, sizeof(h_flag), hipMemcpyDeviceToHost, st->stream);
-    hipError_t e2 = hipStreamSynchronize(st->stream);
-    staging_release(st);
-    if (rc) return rc;
-    if (e != hipSuccess) return hip_fail(e, "verify D2H");
-    if (e2 != hipSuccess) return hip_fail(e2, "hipStreamSynchronize");
-    *ok = h_flag == 0 ? 1 : 0;
-    return HBEC_OK;
+        if (rc) return rc;
+        if (e != hipSuccess) return hip_fail(e, "verify D2H");
+        if (e2 != hipSuccess) return hip_fail(e2, "hipStreamSynchronize");
+        *ok = h_flag == 0 ? 1 : 0;
+        return HBEC_OK;
+    });
 }
 
 int hbec_set_force_stream(int on) {
-    g_force_stream.store(on ? 1 : 0);
-    return HBEC_OK;
+    return hbec::guarded("hbec_set_force_stream", [&]() -> int {
+        g_force_stream.store(on ? 1 : 0);
+        return HBEC_OK;
+    });
 }
 
 int hbec_kernel_info(int k, int r, uint64_t shard_len, int* tile_bytes, int* kind, int* blocks_per_cu) {
-    if (k < 1 || k > kMaxK || r < 1 || r > kMaxR) return fail(HBEC_ERR_INVALID_ARG, "shape out of range");
-    const int fs = g_force_stream.load();
-    const int pipe = is_pipe_shape(k, r, shard_len, fs);
-    if (tile_bytes) *tile_bytes = vec_tile_bytes(k, r, shard_len, 0, fs);
-    if (kind) *kind = is_streaming_shape(k, r, fs) ? 2 : (pipe ? 1 : 0);
-    if (blocks_per_cu) {
-        int dev = 0, cus = 0;
-        int rc = current_device(&dev);
-        if (rc) return rc;
-        rc = device_blocks(dev, k, r, pipe, fs, &cus, blocks_per_cu);
-        if (rc) return rc;
-        if (g_blocks_per_cu_override > 0) *blocks_per_cu = g_blocks_per_cu_override;
-    }
-    return HBEC_OK;
+    return hbec::guarded("hbec_kernel_info", [&]() -> int {
+        if (k < 1 || k > kMaxK || r < 1 || r > kMaxR) return fail(HBEC_ERR_INVALID_ARG, "shape out of range");
+        const int fs = g_force_stream.load();
+        const int pipe = is_pipe_shape(k, r, shard_len, fs);
+        if (tile_bytes) *tile_bytes = vec_tile_bytes(k, r, shard_len, 0, fs);
+        if (kind) *kind = is_streaming_shape(k, r, fs) ? 2 : (pipe ? 1 : 0);
+        if (blocks_per_cu) {
+            int dev = 0, cus = 0;
+            int rc = current_device(&dev);
+            if (rc) return rc;
+            rc = device_blocks(dev, k, r, pipe, fs, &cus, blocks_per_cu);
+            if (rc) return rc;
+            if (g_blocks_per_cu_override > 0) *blocks_per_cu = g_blocks_per_cu_override;
+        }
+        return HBEC_OK;
+    });
 }
 
 }  // extern "C"

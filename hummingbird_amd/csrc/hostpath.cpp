@@ -651,25 +651,27 @@ int hbec::host_threads() {
 extern "C" {
 
 int hbec_host_alloc(size_t bytes, void** out) {
-    if (!out || bytes == 0) return fail(HBEC_ERR_INVALID_ARG, "null out or zero size");
-    *out = nullptr;
-    void* h = nullptr;
-    // portable + mapped: every device of the process may code it in place
-    // (coherent or non-coherent flags measured the same: 46.2-46.4 GiB/s)
-    hipError_t e = hipHostMalloc(&h, bytes, hipHostMallocPortable | hipHostMallocMapped);
-    if (e != hipSuccess) return hip_fail(e, "hipHostMalloc");
-    void* d = nullptr;
-    e = hipHostGetDevicePointer(&d, h, 0);
-    if (e != hipSuccess || !d) {
-        (void)hipHostFree(h);
-        return hip_fail(e != hipSuccess ? e : hipErrorInvalidValue, "hipHostGetDevicePointer");
-    }
-    {
-        std::lock_guard<std::mutex> g(g_pin_mu);
-        g_pinned[reinterpret_cast<uint64_t>(h)] = PinnedRange{(uint64_t)bytes, reinterpret_cast<uint64_t>(d)};
-    }
-    *out = h;
-    return HBEC_OK;
+    return hbec::guarded("hbec_host_alloc", [&]() -> int {
+        if (!out || bytes == 0) return fail(HBEC_ERR_INVALID_ARG, "null out or zero size");
+        *out = nullptr;
+        void* h = nullptr;
+        // portable + mapped: every device of the process may code it in place
+        // (coherent or non-coherent flags measured the same: 46.2-46.4 GiB/s)
+        hipError_t e = hipHostMalloc(&h, bytes, hipHostMallocPortable | hipHostMallocMapped);
+        if (e != hipSuccess) return hip_fail(e, "hipHostMalloc");
+        void* d = nullptr;
+        e = hipHostGetDevicePointer(&d, h, 0);
+        if (e != hipSuccess || !d) {
+            (void)hipHostFree(h);
+            return hip_fail(e != hipSuccess ? e : hipErrorInvalidValue, "hipHostGetDevicePointer");
+        }
+        {
+            std::lock_guard<std::mutex> g(g_pin_mu);
+            g_pinned[reinterpret_cast<uint64_t>(h)] = PinnedRange{(uint64_t)bytes, reinterpret_cast<uint64_t>(d)};
+        }
+        *out = h;
+        return HBEC_OK;
+    });
 }
 
 void hbec_host_free(void* p) {
@@ -682,107 +684,123 @@ void hbec_host_free(void* p) {
 }
 
 int hbec_host_device_addr(const void* p, uint64_t len, uint64_t* dev) {
-    if (!dev) return fail(HBEC_ERR_INVALID_ARG, "null out");
-    *dev = pinned_device_addr(p, len);
-    return HBEC_OK;
+    return hbec::guarded("hbec_host_device_addr", [&]() -> int {
+        if (!dev) return fail(HBEC_ERR_INVALID_ARG, "null out");
+        *dev = pinned_device_addr(p, len);
+        return HBEC_OK;
+    });
 }
 
 int hbec_encode_host(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n_stripes) {
-    if (!codec || (n_stripes && !stripes)) return fail(HBEC_ERR_INVALID_ARG, "null argument");
-    const int k = hbec_data_shards(codec), m = hbec_parity_shards(codec);
-    if (m == 0) return HBEC_OK;
-    std::vector<uint8_t> mat((size_t)(k + m) * k);
-    hbec_matrix(codec, mat.data());
-    std::vector<uint8_t> rows(mat.begin() + (size_t)k * k, mat.end());
-    std::vector<int> in_idx(k), out_idx(m);
-    for (int j = 0; j < k; ++j) in_idx[j] = j;
-    for (int r = 0; r < m; ++r) out_idx[r] = k + r;
-    return host_run(stripes, n_stripes, in_idx, out_idx, rows);
+    return hbec::guarded("hbec_encode_host", [&]() -> int {
+        if (!codec || (n_stripes && !stripes)) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+        const int k = hbec_data_shards(codec), m = hbec_parity_shards(codec);
+        if (m == 0) return HBEC_OK;
+        std::vector<uint8_t> mat((size_t)(k + m) * k);
+        hbec_matrix(codec, mat.data());
+        std::vector<uint8_t> rows(mat.begin() + (size_t)k * k, mat.end());
+        std::vector<int> in_idx(k), out_idx(m);
+        for (int j = 0; j < k; ++j) in_idx[j] = j;
+        for (int r = 0; r < m; ++r) out_idx[r] = k + r;
+        return host_run(stripes, n_stripes, in_idx, out_idx, rows);
+    });
 }
 
 int hbec_encode_host_md5(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n_stripes, uint8_t* digests) {
-    if (!codec || !digests || (n_stripes && !stripes)) return fail(HBEC_ERR_INVALID_ARG, "null argument");
-    if (n_stripes == 0) return HBEC_OK;
-    const int k = hbec_data_shards(codec), m = hbec_parity_shards(codec), n = k + m;
-    if (m == 0) return fail(HBEC_ERR_INVALID_ARG, "encode_host_md5 needs parity shards");
-    for (uint64_t s = 0; s < n_stripes; ++s)
-        if (stripes[s].shard_len == 0) return fail(HBEC_ERR_SHARD_NO_DATA, "stripe with zero shard length");
-    std::vector<uint8_t> mat((size_t)n * k);
-    hbec_matrix(codec, mat.data());
-    std::vector<uint8_t> rows(mat.begin() + (size_t)k * k, mat.end());
-    std::vector<int> in_idx(k), out_idx(m);
-    for (int j = 0; j < k; ++j) in_idx[j] = j;
-    for (int r = 0; r < m; ++r) out_idx[r] = k + r;
-    hipStream_t st = nullptr;
-    hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
-    if (e != hipSuccess) return hip_fail(e, "hipStreamCreate");
-    void* d_dig = nullptr;
-    const size_t bytes = (size_t)n_stripes * n * 16;
-    int rc = hbec::scratch_alloc(bytes, st, &d_dig);
-    if (!rc) {
-        e = hipStreamSynchronize(st);  // allocation visible to the ring's streams
-        if (e != hipSuccess) rc = hip_fail(e, "scratch");
-    }
-    if (!rc) rc = host_run(stripes, n_stripes, in_idx, out_idx, rows, static_cast<uint8_t*>(d_dig), n);
-    if (!rc) {
-        e = hipMemcpyAsync(digests, d_dig, bytes, hipMemcpyDeviceToHost, st);
-        if (e == hipSuccess) e = hipStreamSynchronize(st);
-        if (e != hipSuccess) rc = hip_fail(e, "digests D2H");
-    }
-    hbec::scratch_free(d_dig, st);
-    (void)hipStreamSynchronize(st);
-    (void)hipStreamDestroy(st);
-    return rc;
+    return hbec::guarded("hbec_encode_host_md5", [&]() -> int {
+        if (!codec || !digests || (n_stripes && !stripes)) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+        if (n_stripes == 0) return HBEC_OK;
+        const int k = hbec_data_shards(codec), m = hbec_parity_shards(codec), n = k + m;
+        if (m == 0) return fail(HBEC_ERR_INVALID_ARG, "encode_host_md5 needs parity shards");
+        for (uint64_t s = 0; s < n_stripes; ++s)
+            if (stripes[s].shard_len == 0) return fail(HBEC_ERR_SHARD_NO_DATA, "stripe with zero shard length");
+        std::vector<uint8_t> mat((size_t)n * k);
+        hbec_matrix(codec, mat.data());
+        std::vector<uint8_t> rows(mat.begin() + (size_t)k * k, mat.end());
+        std::vector<int> in_idx(k), out_idx(m);
+        for (int j = 0; j < k; ++j) in_idx[j] = j;
+        for (int r = 0; r < m; ++r) out_idx[r] = k + r;
+        hipStream_t st = nullptr;
+        hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+        if (e != hipSuccess) return hip_fail(e, "hipStreamCreate");
+        void* d_dig = nullptr;
+        const size_t bytes = (size_t)n_stripes * n * 16;
+        int rc = hbec::scratch_alloc(bytes, st, &d_dig);
+        if (!rc) {
+            e = hipStreamSynchronize(st);  // allocation visible to the ring's streams
+            if (e != hipSuccess) rc = hip_fail(e, "scratch");
+        }
+        if (!rc) rc = host_run(stripes, n_stripes, in_idx, out_idx, rows, static_cast<uint8_t*>(d_dig), n);
+        if (!rc) {
+            e = hipMemcpyAsync(digests, d_dig, bytes, hipMemcpyDeviceToHost, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+            if (e != hipSuccess) rc = hip_fail(e, "digests D2H");
+        }
+        hbec::scratch_free(d_dig, st);
+        (void)hipStreamSynchronize(st);
+        (void)hipStreamDestroy(st);
+        return rc;
+    });
 }
 
 int hbec_device_count(int* n) {
-    if (!n) return fail(HBEC_ERR_INVALID_ARG, "null out");
-    *n = 0;
-    hipError_t e = hipGetDeviceCount(n);
-    if (e != hipSuccess) return hip_fail(e, "hipGetDeviceCount");
-    return HBEC_OK;
+    return hbec::guarded("hbec_device_count", [&]() -> int {
+        if (!n) return fail(HBEC_ERR_INVALID_ARG, "null out");
+        *n = 0;
+        hipError_t e = hipGetDeviceCount(n);
+        if (e != hipSuccess) return hip_fail(e, "hipGetDeviceCount");
+        return HBEC_OK;
+    });
 }
 
 int hbec_set_device(int device) {
-    hipError_t e = hipSetDevice(device);
-    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
-    return HBEC_OK;
+    return hbec::guarded("hbec_set_device", [&]() -> int {
+        hipError_t e = hipSetDevice(device);
+        if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+        return HBEC_OK;
+    });
 }
 
 int hbec_encode_host_devices(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n_stripes, const int* devices,
                              int n_devices) {
-    return run_on_devices(stripes, n_stripes, devices, n_devices, [codec](const hbec_stripe* s, uint64_t n) {
-        return hbec_encode_host(codec, s, n);
+    return hbec::guarded("hbec_encode_host_devices", [&]() -> int {
+        return run_on_devices(stripes, n_stripes, devices, n_devices, [codec](const hbec_stripe* s, uint64_t n) {
+            return hbec_encode_host(codec, s, n);
+        });
     });
 }
 
 int hbec_reconstruct_host_devices(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n_stripes,
                                   const uint8_t* present, int data_only, const int* devices, int n_devices) {
-    if (!present) return fail(HBEC_ERR_INVALID_ARG, "null argument");
-    return run_on_devices(stripes, n_stripes, devices, n_devices, [=](const hbec_stripe* s, uint64_t n) {
-        return hbec_reconstruct_host(codec, s, n, present, data_only);
+    return hbec::guarded("hbec_reconstruct_host_devices", [&]() -> int {
+        if (!present) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+        return run_on_devices(stripes, n_stripes, devices, n_devices, [=](const hbec_stripe* s, uint64_t n) {
+            return hbec_reconstruct_host(codec, s, n, present, data_only);
+        });
     });
 }
 
 int hbec_reconstruct_host(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n_stripes,
                           const uint8_t* present, int data_only) {
-    if (!codec || !present || (n_stripes && !stripes)) return fail(HBEC_ERR_INVALID_ARG, "null argument");
-    const int k = hbec_data_shards(codec), m = hbec_parity_shards(codec), n = k + m;
-    int n_present = 0, data_present = 0;
-    for (int i = 0; i < n; ++i) {
-        n_present += present[i] ? 1 : 0;
-        if (i < k) data_present += present[i] ? 1 : 0;
-    }
-    if (n_present == n || (data_only && data_present == k)) return HBEC_OK;
-    if (n_present < k) return fail(HBEC_ERR_TOO_FEW_SHARDS, "too few shards given");
-    std::vector<int> surv(k), outs(n);
-    std::vector<uint8_t> rows((size_t)n * k);
-    int n_out = 0;
-    int rc = hbec_decode_rows(codec, present, data_only, surv.data(), outs.data(), &n_out, rows.data());
-    if (rc) return rc;
-    outs.resize(n_out);
-    rows.resize((size_t)n_out * k);
-    return host_run(stripes, n_stripes, surv, outs, rows);
+    return hbec::guarded("hbec_reconstruct_host", [&]() -> int {
+        if (!codec || !present || (n_stripes && !stripes)) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+        const int k = hbec_data_shards(codec), m = hbec_parity_shards(codec), n = k + m;
+        int n_present = 0, data_present = 0;
+        for (int i = 0; i < n; ++i) {
+            n_present += present[i] ? 1 : 0;
+            if (i < k) data_present += present[i] ? 1 : 0;
+        }
+        if (n_present == n || (data_only && data_present == k)) return HBEC_OK;
+        if (n_present < k) return fail(HBEC_ERR_TOO_FEW_SHARDS, "too few shards given");
+        std::vector<int> surv(k), outs(n);
+        std::vector<uint8_t> rows((size_t)n * k);
+        int n_out = 0;
+        int rc = hbec_decode_rows(codec, present, data_only, surv.data(), outs.data(), &n_out, rows.data());
+        if (rc) return rc;
+        outs.resize(n_out);
+        rows.resize((size_t)n_out * k);
+        return host_run(stripes, n_stripes, surv, outs, rows);
+    });
 }
 
 }  // extern "C"

@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <exception>
+#include <new>
 #include <string>
 
 #include "../../include/hbec.h"
@@ -11,6 +13,22 @@ namespace hbec {
 // Record a thread-local error message and return code.
 int fail(int code, const std::string& msg);
 int hip_fail(hipError_t e, const char* what);
+
+// Every extern "C" entry point runs its body through this: no C++ exception
+// (std::bad_alloc from a host vector, std::system_error from std::thread)
+// may cross the C ABI into a Go / C caller.
+template <typename F>
+int guarded(const char* entry, F&& body) noexcept {
+    try {
+        return body();
+    } catch (const std::bad_alloc&) {
+        return fail(HBEC_ERR_NOMEM, std::string(entry) + ": host allocation failed");
+    } catch (const std::exception& e) {
+        return fail(HBEC_ERR_DEVICE, std::string(entry) + ": " + e.what());
+    } catch (...) {
+        return fail(HBEC_ERR_DEVICE, std::string(entry) + ": unknown exception");
+    }
+}
 
 // Queue out[r] (^)= XOR_c coeffs[r][c] * in[c] over n_obj strided objects.
 int apply_views(int rows, int cols, const uint8_t* coeffs, const hbec_view* in, const hbec_view* out,

@@ -174,95 +174,99 @@ int run_plan(const hbec_plan* p, const std::vector<int>& in_idx, const std::vect
 extern "C" {
 
 int hbec_plan_stripes(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n, hbec_plan** out) {
-    if (!codec || !out || (n && !stripes)) return fail(HBEC_ERR_INVALID_ARG, "null argument");
-    *out = nullptr;
-    const int k = hbec_data_shards(codec), m = hbec_parity_shards(codec);
-    std::unique_ptr<hbec_plan> p(new (std::nothrow) hbec_plan());
-    if (!p) return fail(HBEC_ERR_NOMEM, "plan allocation");
-    p->k = k;
-    p->m = m;
-    p->tile_bytes = hbec::stripes_tile_bytes(std::min(k, 8));
-    std::vector<hbec::TileRec> recs;
-    for (uint64_t i = 0; i < n; ++i) {
-        const hbec_stripe& s = stripes[i];
-        if (s.shard_len == 0) continue;
-        if (!s.base) return fail(HBEC_ERR_INVALID_ARG, "stripe with null base");
-        p->shard_bytes += s.shard_len;
-        if (!aligned_stripe(s)) {
-            p->fallback.push_back(s);
-            continue;
+    return hbec::guarded("hbec_plan_stripes", [&]() -> int {
+        if (!codec || !out || (n && !stripes)) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+        *out = nullptr;
+        const int k = hbec_data_shards(codec), m = hbec_parity_shards(codec);
+        std::unique_ptr<hbec_plan> p(new (std::nothrow) hbec_plan());
+        if (!p) return fail(HBEC_ERR_NOMEM, "plan allocation");
+        p->k = k;
+        p->m = m;
+        p->tile_bytes = hbec::stripes_tile_bytes(std::min(k, 8));
+        std::vector<hbec::TileRec> recs;
+        for (uint64_t i = 0; i < n; ++i) {
+            const hbec_stripe& s = stripes[i];
+            if (s.shard_len == 0) continue;
+            if (!s.base) return fail(HBEC_ERR_INVALID_ARG, "stripe with null base");
+            p->shard_bytes += s.shard_len;
+            if (!aligned_stripe(s)) {
+                p->fallback.push_back(s);
+                continue;
+            }
+            p->tiled.push_back(s);
+            for (uint64_t off = 0; off < s.shard_len; off += (uint64_t)p->tile_bytes) {
+                hbec::TileRec r;
+                r.in_addr = r.out_addr = reinterpret_cast<uint64_t>(s.base) + off;
+                r.in_stride = r.out_stride = (uint32_t)s.shard_len;
+                r.valid = (uint32_t)std::min<uint64_t>((uint64_t)p->tile_bytes, s.shard_len - off);
+                r.pad_ = 0;
+                recs.push_back(r);
+            }
         }
-        p->tiled.push_back(s);
-        for (uint64_t off = 0; off < s.shard_len; off += (uint64_t)p->tile_bytes) {
-            hbec::TileRec r;
-            r.in_addr = r.out_addr = reinterpret_cast<uint64_t>(s.base) + off;
-            r.in_stride = r.out_stride = (uint32_t)s.shard_len;
-            r.valid = (uint32_t)std::min<uint64_t>((uint64_t)p->tile_bytes, s.shard_len - off);
-            r.pad_ = 0;
-            recs.push_back(r);
+        if (recs.size() >= (1ull << 31)) return fail(HBEC_ERR_INVALID_ARG, "plan too large (>= 2^31 tiles)");
+        p->n_tiles = recs.size();
+        if (!recs.empty()) {
+            hipError_t e = hipMalloc(&p->d_tiles, recs.size() * sizeof(hbec::TileRec));
+            if (e != hipSuccess) return hip_fail(e, "hipMalloc plan tiles");
+            e = hipMemcpy(p->d_tiles, recs.data(), recs.size() * sizeof(hbec::TileRec), hipMemcpyHostToDevice);
+            if (e != hipSuccess) {
+                (void)hipFree(p->d_tiles);
+                p->d_tiles = nullptr;
+                return hip_fail(e, "hipMemcpy plan tiles");
+            }
         }
-    }
-    if (recs.size() >= (1ull << 31)) return fail(HBEC_ERR_INVALID_ARG, "plan too large (>= 2^31 tiles)");
-    p->n_tiles = recs.size();
-    if (!recs.empty()) {
-        hipError_t e = hipMalloc(&p->d_tiles, recs.size() * sizeof(hbec::TileRec));
-        if (e != hipSuccess) return hip_fail(e, "hipMalloc plan tiles");
-        e = hipMemcpy(p->d_tiles, recs.data(), recs.size() * sizeof(hbec::TileRec), hipMemcpyHostToDevice);
-        if (e != hipSuccess) {
-            (void)hipFree(p->d_tiles);
-            p->d_tiles = nullptr;
-            return hip_fail(e, "hipMemcpy plan tiles");
-        }
-    }
-    *out = p.release();
-    return HBEC_OK;
+        *out = p.release();
+        return HBEC_OK;
+    });
 }
 
 int hbec_plan_objects(hbec_codec* codec, const hbec_object* objects, uint64_t n, hbec_plan** out) {
-    if (!codec || !out || (n && !objects)) return fail(HBEC_ERR_INVALID_ARG, "null argument");
-    *out = nullptr;
-    const int k = hbec_data_shards(codec), m = hbec_parity_shards(codec);
-    std::unique_ptr<hbec_plan> p(new (std::nothrow) hbec_plan());
-    if (!p) return fail(HBEC_ERR_NOMEM, "plan allocation");
-    p->k = k;
-    p->m = m;
-    p->objects = true;
-    p->tile_bytes = hbec::stripes_tile_bytes(std::min(k, 8));
-    std::vector<hbec::TileRec> recs;
-    for (uint64_t i = 0; i < n; ++i) {
-        const hbec_object& o = objects[i];
-        if (o.shard_len == 0) continue;
-        if (!o.data || (m > 0 && !o.parity)) return fail(HBEC_ERR_INVALID_ARG, "object with null data or parity");
-        p->shard_bytes += o.shard_len;
-        if (!aligned_object(o)) {
-            p->obj_fallback.push_back(o);
-            continue;
+    return hbec::guarded("hbec_plan_objects", [&]() -> int {
+        if (!codec || !out || (n && !objects)) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+        *out = nullptr;
+        const int k = hbec_data_shards(codec), m = hbec_parity_shards(codec);
+        std::unique_ptr<hbec_plan> p(new (std::nothrow) hbec_plan());
+        if (!p) return fail(HBEC_ERR_NOMEM, "plan allocation");
+        p->k = k;
+        p->m = m;
+        p->objects = true;
+        p->tile_bytes = hbec::stripes_tile_bytes(std::min(k, 8));
+        std::vector<hbec::TileRec> recs;
+        for (uint64_t i = 0; i < n; ++i) {
+            const hbec_object& o = objects[i];
+            if (o.shard_len == 0) continue;
+            if (!o.data || (m > 0 && !o.parity)) return fail(HBEC_ERR_INVALID_ARG, "object with null data or parity");
+            p->shard_bytes += o.shard_len;
+            if (!aligned_object(o)) {
+                p->obj_fallback.push_back(o);
+                continue;
+            }
+            p->obj_tiled.push_back(o);
+            for (uint64_t off = 0; off < o.shard_len; off += (uint64_t)p->tile_bytes) {
+                hbec::TileRec r;
+                r.in_addr = reinterpret_cast<uint64_t>(o.data) + off;
+                r.out_addr = reinterpret_cast<uint64_t>(o.parity) + off;
+                r.in_stride = r.out_stride = (uint32_t)o.shard_len;
+                r.valid = (uint32_t)std::min<uint64_t>((uint64_t)p->tile_bytes, o.shard_len - off);
+                r.pad_ = 0;
+                recs.push_back(r);
+            }
         }
-        p->obj_tiled.push_back(o);
-        for (uint64_t off = 0; off < o.shard_len; off += (uint64_t)p->tile_bytes) {
-            hbec::TileRec r;
-            r.in_addr = reinterpret_cast<uint64_t>(o.data) + off;
-            r.out_addr = reinterpret_cast<uint64_t>(o.parity) + off;
-            r.in_stride = r.out_stride = (uint32_t)o.shard_len;
-            r.valid = (uint32_t)std::min<uint64_t>((uint64_t)p->tile_bytes, o.shard_len - off);
-            r.pad_ = 0;
-            recs.push_back(r);
+        if (recs.size() >= (1ull << 31)) return fail(HBEC_ERR_INVALID_ARG, "plan too large (>= 2^31 tiles)");
+        p->n_tiles = recs.size();
+        if (!recs.empty()) {
+            hipError_t e = hipMalloc(&p->d_tiles, recs.size() * sizeof(hbec::TileRec));
+            if (e != hipSuccess) return hip_fail(e, "hipMalloc plan tiles");
+            e = hipMemcpy(p->d_tiles, recs.data(), recs.size() * sizeof(hbec::TileRec), hipMemcpyHostToDevice);
+            if (e != hipSuccess) {
+                (void)hipFree(p->d_tiles);
+                p->d_tiles = nullptr;
+                return hip_fail(e, "hipMemcpy plan tiles");
+            }
         }
-    }
-    if (recs.size() >= (1ull << 31)) return fail(HBEC_ERR_INVALID_ARG, "plan too large (>= 2^31 tiles)");
-    p->n_tiles = recs.size();
-    if (!recs.empty()) {
-        hipError_t e = hipMalloc(&p->d_tiles, recs.size() * sizeof(hbec::TileRec));
-        if (e != hipSuccess) return hip_fail(e, "hipMalloc plan tiles");
-        e = hipMemcpy(p->d_tiles, recs.data(), recs.size() * sizeof(hbec::TileRec), hipMemcpyHostToDevice);
-        if (e != hipSuccess) {
-            (void)hipFree(p->d_tiles);
-            p->d_tiles = nullptr;
-            return hip_fail(e, "hipMemcpy plan tiles");
-        }
-    }
-    *out = p.release();
-    return HBEC_OK;
+        *out = p.release();
+        return HBEC_OK;
+    });
 }
 
 void hbec_plan_free(hbec_plan* plan) {
@@ -273,48 +277,54 @@ void hbec_plan_free(hbec_plan* plan) {
 
 int hbec_plan_info(const hbec_plan* plan, uint64_t* n_tiles, int* tile_bytes, uint64_t* n_fallback,
                    uint64_t* shard_bytes) {
-    if (!plan) return fail(HBEC_ERR_INVALID_ARG, "null plan");
-    if (n_tiles) *n_tiles = plan->n_tiles;
-    if (tile_bytes) *tile_bytes = plan->tile_bytes;
-    if (n_fallback) *n_fallback = plan->objects ? plan->obj_fallback.size() : plan->fallback.size();
-    if (shard_bytes) *shard_bytes = plan->shard_bytes;
-    return HBEC_OK;
+    return hbec::guarded("hbec_plan_info", [&]() -> int {
+        if (!plan) return fail(HBEC_ERR_INVALID_ARG, "null plan");
+        if (n_tiles) *n_tiles = plan->n_tiles;
+        if (tile_bytes) *tile_bytes = plan->tile_bytes;
+        if (n_fallback) *n_fallback = plan->objects ? plan->obj_fallback.size() : plan->fallback.size();
+        if (shard_bytes) *shard_bytes = plan->shard_bytes;
+        return HBEC_OK;
+    });
 }
 
 int hbec_encode_plan(hbec_codec* codec, const hbec_plan* plan, void* hip_stream) {
-    if (!codec || !plan) return fail(HBEC_ERR_INVALID_ARG, "null argument");
-    const int k = hbec_data_shards(codec), m = hbec_parity_shards(codec);
-    if (k != plan->k || m != plan->m) return fail(HBEC_ERR_INVALID_ARG, "plan built for another (k, m)");
-    if (m == 0) return HBEC_OK;
-    std::vector<uint8_t> mat((size_t)(k + m) * k);
-    hbec_matrix(codec, mat.data());
-    std::vector<uint8_t> rows(mat.begin() + (size_t)k * k, mat.end());
-    std::vector<int> in_idx(k), out_idx(m);
-    for (int j = 0; j < k; ++j) in_idx[j] = j;
-    for (int r = 0; r < m; ++r) out_idx[r] = k + r;
-    return run_plan(plan, in_idx, out_idx, rows, static_cast<hipStream_t>(hip_stream));
+    return hbec::guarded("hbec_encode_plan", [&]() -> int {
+        if (!codec || !plan) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+        const int k = hbec_data_shards(codec), m = hbec_parity_shards(codec);
+        if (k != plan->k || m != plan->m) return fail(HBEC_ERR_INVALID_ARG, "plan built for another (k, m)");
+        if (m == 0) return HBEC_OK;
+        std::vector<uint8_t> mat((size_t)(k + m) * k);
+        hbec_matrix(codec, mat.data());
+        std::vector<uint8_t> rows(mat.begin() + (size_t)k * k, mat.end());
+        std::vector<int> in_idx(k), out_idx(m);
+        for (int j = 0; j < k; ++j) in_idx[j] = j;
+        for (int r = 0; r < m; ++r) out_idx[r] = k + r;
+        return run_plan(plan, in_idx, out_idx, rows, static_cast<hipStream_t>(hip_stream));
+    });
 }
 
 int hbec_reconstruct_plan(hbec_codec* codec, const hbec_plan* plan, const uint8_t* present, int data_only,
                           void* hip_stream) {
-    if (!codec || !plan || !present) return fail(HBEC_ERR_INVALID_ARG, "null argument");
-    const int k = hbec_data_shards(codec), m = hbec_parity_shards(codec), n = k + m;
-    if (k != plan->k || m != plan->m) return fail(HBEC_ERR_INVALID_ARG, "plan built for another (k, m)");
-    int n_present = 0, data_present = 0;
-    for (int i = 0; i < n; ++i) {
-        n_present += present[i] ? 1 : 0;
-        if (i < k) data_present += present[i] ? 1 : 0;
-    }
-    if (n_present == n || (data_only && data_present == k)) return HBEC_OK;
-    if (n_present < k) return fail(HBEC_ERR_TOO_FEW_SHARDS, "too few shards given");
-    std::vector<int> surv(k), outs(n);
-    std::vector<uint8_t> rows((size_t)n * k);
-    int n_out = 0;
-    int rc = hbec_decode_rows(codec, present, data_only, surv.data(), outs.data(), &n_out, rows.data());
-    if (rc) return rc;
-    outs.resize(n_out);
-    rows.resize((size_t)n_out * k);
-    return run_plan(plan, surv, outs, rows, static_cast<hipStream_t>(hip_stream));
+    return hbec::guarded("hbec_reconstruct_plan", [&]() -> int {
+        if (!codec || !plan || !present) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+        const int k = hbec_data_shards(codec), m = hbec_parity_shards(codec), n = k + m;
+        if (k != plan->k || m != plan->m) return fail(HBEC_ERR_INVALID_ARG, "plan built for another (k, m)");
+        int n_present = 0, data_present = 0;
+        for (int i = 0; i < n; ++i) {
+            n_present += present[i] ? 1 : 0;
+            if (i < k) data_present += present[i] ? 1 : 0;
+        }
+        if (n_present == n || (data_only && data_present == k)) return HBEC_OK;
+        if (n_present < k) return fail(HBEC_ERR_TOO_FEW_SHARDS, "too few shards given");
+        std::vector<int> surv(k), outs(n);
+        std::vector<uint8_t> rows((size_t)n * k);
+        int n_out = 0;
+        int rc = hbec_decode_rows(codec, present, data_only, surv.data(), outs.data(), &n_out, rows.data());
+        if (rc) return rc;
+        outs.resize(n_out);
+        rows.resize((size_t)n_out * k);
+        return run_plan(plan, surv, outs, rows, static_cast<hipStream_t>(hip_stream));
+    });
 }
 
 }  // extern "C"

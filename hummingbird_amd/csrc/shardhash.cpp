@@ -279,162 +279,170 @@ extern "C" {
 
 int hbec_md5_batch(const hbec_view* views, int n_views, uint64_t n_objects, uint64_t len, uint8_t* d_digests,
                    void* hip_stream) {
-    int rc = check_views(views, n_views, n_objects, len);
-    if (rc) return rc;
-    rc = check_digests(d_digests);
-    if (rc) return rc;
-    if (n_objects == 0) return HBEC_OK;
-    return md5_step(views, n_views, n_objects, len, 0, kInit | kFinal, nullptr, d_digests,
-                    static_cast<hipStream_t>(hip_stream));
+    return hbec::guarded("hbec_md5_batch", [&]() -> int {
+        int rc = check_views(views, n_views, n_objects, len);
+        if (rc) return rc;
+        rc = check_digests(d_digests);
+        if (rc) return rc;
+        if (n_objects == 0) return HBEC_OK;
+        return md5_step(views, n_views, n_objects, len, 0, kInit | kFinal, nullptr, d_digests,
+                        static_cast<hipStream_t>(hip_stream));
+    });
 }
 
 int hbec_md5_list(const void* const* d_bufs, const uint64_t* lens, uint64_t n, uint8_t* d_digests,
                   void* hip_stream) {
-    if (n == 0) return HBEC_OK;
-    if (!d_bufs || !lens) return fail(HBEC_ERR_INVALID_ARG, "md5_list: null argument");
-    int rc = check_digests(d_digests);
-    if (rc) return rc;
-    for (uint64_t i = 0; i < n; ++i)
-        if (!d_bufs[i] && lens[i]) return fail(HBEC_ERR_INVALID_ARG, "md5_list: null buffer");
-    std::vector<ListRec> recs;
-    bool aligned = true;
-    list_records(d_bufs, lens, n, recs, &aligned);
-    hipStream_t stream = static_cast<hipStream_t>(hip_stream);
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
-    hipMemPool_t pool;
-    rc = state_pool(dev, &pool);
-    if (rc) return rc;
-    void* drec = nullptr;
-    e = hipMallocFromPoolAsync(&drec, n * sizeof(ListRec), pool, stream);
-    if (e != hipSuccess) return hip_fail(e, "hipMallocFromPoolAsync");
-    // pageable source: staged by the runtime before the call returns
-    e = hipMemcpyAsync(drec, recs.data(), n * sizeof(ListRec), hipMemcpyHostToDevice, stream);
-    if (e == hipSuccess) e = launch_md5_list(drec, n, d_digests, aligned, stream);
-    (void)hipFreeAsync(drec, stream);
-    if (e != hipSuccess) return hip_fail(e, "md5_list");
-    return HBEC_OK;
+    return hbec::guarded("hbec_md5_list", [&]() -> int {
+        if (n == 0) return HBEC_OK;
+        if (!d_bufs || !lens) return fail(HBEC_ERR_INVALID_ARG, "md5_list: null argument");
+        int rc = check_digests(d_digests);
+        if (rc) return rc;
+        for (uint64_t i = 0; i < n; ++i)
+            if (!d_bufs[i] && lens[i]) return fail(HBEC_ERR_INVALID_ARG, "md5_list: null buffer");
+        std::vector<ListRec> recs;
+        bool aligned = true;
+        list_records(d_bufs, lens, n, recs, &aligned);
+        hipStream_t stream = static_cast<hipStream_t>(hip_stream);
+        int dev = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+        hipMemPool_t pool;
+        rc = state_pool(dev, &pool);
+        if (rc) return rc;
+        void* drec = nullptr;
+        e = hipMallocFromPoolAsync(&drec, n * sizeof(ListRec), pool, stream);
+        if (e != hipSuccess) return hip_fail(e, "hipMallocFromPoolAsync");
+        // pageable source: staged by the runtime before the call returns
+        e = hipMemcpyAsync(drec, recs.data(), n * sizeof(ListRec), hipMemcpyHostToDevice, stream);
+        if (e == hipSuccess) e = launch_md5_list(drec, n, d_digests, aligned, stream);
+        (void)hipFreeAsync(drec, stream);
+        if (e != hipSuccess) return hip_fail(e, "md5_list");
+        return HBEC_OK;
+    });
 }
 
 int hbec_md5_host(const uint8_t* const* bufs, const uint64_t* lens, uint64_t n, uint8_t* digests) {
-    if (n == 0) return HBEC_OK;
-    if (!bufs || !lens || !digests) return fail(HBEC_ERR_INVALID_ARG, "md5_host: null argument");
-    for (uint64_t i = 0; i < n; ++i)
-        if (!bufs[i] && lens[i]) return fail(HBEC_ERR_INVALID_ARG, "md5_host: null buffer");
-    HashRing* ring = nullptr;
-    int rc = hash_ring_acquire(&ring);
-    if (rc) return rc;
-    struct Rel {
-        HashRing* r;
-        ~Rel() { hash_ring_release(r); }
-    } rel{ring};
-    int dev = ring->dev;
-    hipMemPool_t mpool;
-    rc = state_pool(dev, &mpool);
-    if (rc) return rc;
-    uint8_t* d_dig = nullptr;
-    hipError_t e = hipMallocFromPoolAsync(reinterpret_cast<void**>(&d_dig), n * 16, mpool, ring->stream[0]);
-    if (e != hipSuccess) return hip_fail(e, "hipMallocFromPoolAsync");
-    for (int i = 1; i < kHashSlots && e == hipSuccess; ++i) {  // every slot stream sees the allocation
-        e = hipEventRecord(ring->ev[0], ring->stream[0]);
-        if (e == hipSuccess) e = hipStreamWaitEvent(ring->stream[i], ring->ev[0], 0);
-    }
-    if (e != hipSuccess) return hip_fail(e, "md5_host ordering");
-    // longest first; chunks of buffers that fit a slot (16-B aligned offsets)
-    std::vector<uint64_t> order(n);
-    for (uint64_t i = 0; i < n; ++i) order[i] = i;
-    std::stable_sort(order.begin(), order.end(), [&](uint64_t a, uint64_t b) { return lens[a] > lens[b]; });
-    std::vector<std::vector<uint64_t>> chunks;
-    std::vector<uint64_t> big;  // longer than a slot: streamed through slot 0 piece by piece
-    uint64_t used = 0;
-    for (uint64_t i : order) {
-        const uint64_t sz = (lens[i] + 15) & ~uint64_t(15);
-        if (lens[i] > ring->cap) {
-            big.push_back(i);
-            continue;
-        }
-        if (chunks.empty() || used + sz > ring->cap || chunks.back().size() >= ring->rec_cap) {
-            chunks.emplace_back();
-            used = 0;
-        }
-        chunks.back().push_back(i);
-        used += sz;
-    }
-    Pool pool(host_threads() - 1);
-    for (size_t c = 0; c < chunks.size(); ++c) {
-        const int s = (int)(c % kHashSlots);
-        e = hipEventSynchronize(ring->ev[s]);  // slot free: its previous chunk has been hashed
-        if (e != hipSuccess) return hip_fail(e, "md5_host wait");
-        const auto& ch = chunks[c];
-        std::vector<uint64_t> off(ch.size());
-        uint64_t o = 0;
-        for (size_t j = 0; j < ch.size(); ++j) {
-            off[j] = o;
-            o += (lens[ch[j]] + 15) & ~uint64_t(15);
-        }
-        pool.parallel_for(ch.size(), [&](size_t j) {
-            if (lens[ch[j]]) std::memcpy(ring->pin[s] + off[j], bufs[ch[j]], lens[ch[j]]);
-        });
-        const uint64_t dbase = reinterpret_cast<uint64_t>(ring->dbuf[s]);
-        for (size_t j = 0; j < ch.size(); ++j) ring->pin_rec[s][j] = ListRec{dbase + off[j], lens[ch[j]], ch[j], 0};
-        e = hipMemcpyAsync(ring->drec[s], ring->pin_rec[s], ch.size() * sizeof(ListRec), hipMemcpyHostToDevice,
-                           ring->stream[s]);
-        if (e == hipSuccess && o)
-            e = hipMemcpyAsync(ring->dbuf[s], ring->pin[s], o, hipMemcpyHostToDevice, ring->stream[s]);
-        if (e == hipSuccess) e = launch_md5_list(ring->drec[s], ch.size(), d_dig, true, ring->stream[s]);
-        if (e == hipSuccess) e = hipEventRecord(ring->ev[s], ring->stream[s]);
-        if (e != hipSuccess) return hip_fail(e, "md5_host chunk");
-    }
-    for (int s = 0; s < kHashSlots; ++s) {
-        e = hipStreamSynchronize(ring->stream[s]);
-        if (e != hipSuccess) return hip_fail(e, "md5_host drain");
-    }
-    // buffers larger than a slot: one streaming chain each, slot-sized pieces
-    for (uint64_t i : big) {
-        hbec_md5* ctx = nullptr;
-        rc = hbec_md5_new(1, 1, &ctx);
+    return hbec::guarded("hbec_md5_host", [&]() -> int {
+        if (n == 0) return HBEC_OK;
+        if (!bufs || !lens || !digests) return fail(HBEC_ERR_INVALID_ARG, "md5_host: null argument");
+        for (uint64_t i = 0; i < n; ++i)
+            if (!bufs[i] && lens[i]) return fail(HBEC_ERR_INVALID_ARG, "md5_host: null buffer");
+        HashRing* ring = nullptr;
+        int rc = hash_ring_acquire(&ring);
         if (rc) return rc;
-        for (uint64_t pos = 0; pos < lens[i] && rc == HBEC_OK; pos += ring->cap) {
-            const uint64_t len = std::min<uint64_t>(ring->cap, lens[i] - pos);
-            pool.parallel_for(16, [&](size_t t) {
-                const uint64_t a = len * t / 16, b = len * (t + 1) / 16;
-                std::memcpy(ring->pin[0] + a, bufs[i] + pos + a, b - a);
-            });
-            e = hipMemcpyAsync(ring->dbuf[0], ring->pin[0], len, hipMemcpyHostToDevice, ring->stream[0]);
-            if (e != hipSuccess) rc = hip_fail(e, "md5_host H2D");
-            hbec_view v{ring->dbuf[0], 0};
-            if (!rc) rc = hbec_md5_update(ctx, &v, len, ring->stream[0]);
-            if (!rc) {
-                e = hipStreamSynchronize(ring->stream[0]);  // pinned slot reused by the next piece
-                if (e != hipSuccess) rc = hip_fail(e, "md5_host sync");
+        struct Rel {
+            HashRing* r;
+            ~Rel() { hash_ring_release(r); }
+        } rel{ring};
+        int dev = ring->dev;
+        hipMemPool_t mpool;
+        rc = state_pool(dev, &mpool);
+        if (rc) return rc;
+        uint8_t* d_dig = nullptr;
+        hipError_t e = hipMallocFromPoolAsync(reinterpret_cast<void**>(&d_dig), n * 16, mpool, ring->stream[0]);
+        if (e != hipSuccess) return hip_fail(e, "hipMallocFromPoolAsync");
+        for (int i = 1; i < kHashSlots && e == hipSuccess; ++i) {  // every slot stream sees the allocation
+            e = hipEventRecord(ring->ev[0], ring->stream[0]);
+            if (e == hipSuccess) e = hipStreamWaitEvent(ring->stream[i], ring->ev[0], 0);
+        }
+        if (e != hipSuccess) return hip_fail(e, "md5_host ordering");
+        // longest first; chunks of buffers that fit a slot (16-B aligned offsets)
+        std::vector<uint64_t> order(n);
+        for (uint64_t i = 0; i < n; ++i) order[i] = i;
+        std::stable_sort(order.begin(), order.end(), [&](uint64_t a, uint64_t b) { return lens[a] > lens[b]; });
+        std::vector<std::vector<uint64_t>> chunks;
+        std::vector<uint64_t> big;  // longer than a slot: streamed through slot 0 piece by piece
+        uint64_t used = 0;
+        for (uint64_t i : order) {
+            const uint64_t sz = (lens[i] + 15) & ~uint64_t(15);
+            if (lens[i] > ring->cap) {
+                big.push_back(i);
+                continue;
             }
+            if (chunks.empty() || used + sz > ring->cap || chunks.back().size() >= ring->rec_cap) {
+                chunks.emplace_back();
+                used = 0;
+            }
+            chunks.back().push_back(i);
+            used += sz;
         }
-        if (!rc) rc = hbec_md5_final(ctx, d_dig + i * 16, ring->stream[0]);
-        hbec_md5_free(ctx);  // hipFree synchronises with the queued final
-        if (rc) return rc;
-    }
-    e = hipMemcpyAsync(digests, d_dig, n * 16, hipMemcpyDeviceToHost, ring->stream[0]);
-    (void)hipFreeAsync(d_dig, ring->stream[0]);
-    if (e == hipSuccess) e = hipStreamSynchronize(ring->stream[0]);
-    if (e != hipSuccess) return hip_fail(e, "md5_host digests");
-    return HBEC_OK;
+        Pool pool(host_threads() - 1);
+        for (size_t c = 0; c < chunks.size(); ++c) {
+            const int s = (int)(c % kHashSlots);
+            e = hipEventSynchronize(ring->ev[s]);  // slot free: its previous chunk has been hashed
+            if (e != hipSuccess) return hip_fail(e, "md5_host wait");
+            const auto& ch = chunks[c];
+            std::vector<uint64_t> off(ch.size());
+            uint64_t o = 0;
+            for (size_t j = 0; j < ch.size(); ++j) {
+                off[j] = o;
+                o += (lens[ch[j]] + 15) & ~uint64_t(15);
+            }
+            pool.parallel_for(ch.size(), [&](size_t j) {
+                if (lens[ch[j]]) std::memcpy(ring->pin[s] + off[j], bufs[ch[j]], lens[ch[j]]);
+            });
+            const uint64_t dbase = reinterpret_cast<uint64_t>(ring->dbuf[s]);
+            for (size_t j = 0; j < ch.size(); ++j) ring->pin_rec[s][j] = ListRec{dbase + off[j], lens[ch[j]], ch[j], 0};
+            e = hipMemcpyAsync(ring->drec[s], ring->pin_rec[s], ch.size() * sizeof(ListRec), hipMemcpyHostToDevice,
+                               ring->stream[s]);
+            if (e == hipSuccess && o)
+                e = hipMemcpyAsync(ring->dbuf[s], ring->pin[s], o, hipMemcpyHostToDevice, ring->stream[s]);
+            if (e == hipSuccess) e = launch_md5_list(ring->drec[s], ch.size(), d_dig, true, ring->stream[s]);
+            if (e == hipSuccess) e = hipEventRecord(ring->ev[s], ring->stream[s]);
+            if (e != hipSuccess) return hip_fail(e, "md5_host chunk");
+        }
+        for (int s = 0; s < kHashSlots; ++s) {
+            e = hipStreamSynchronize(ring->stream[s]);
+            if (e != hipSuccess) return hip_fail(e, "md5_host drain");
+        }
+        // buffers larger than a slot: one streaming chain each, slot-sized pieces
+        for (uint64_t i : big) {
+            hbec_md5* ctx = nullptr;
+            rc = hbec_md5_new(1, 1, &ctx);
+            if (rc) return rc;
+            for (uint64_t pos = 0; pos < lens[i] && rc == HBEC_OK; pos += ring->cap) {
+                const uint64_t len = std::min<uint64_t>(ring->cap, lens[i] - pos);
+                pool.parallel_for(16, [&](size_t t) {
+                    const uint64_t a = len * t / 16, b = len * (t + 1) / 16;
+                    std::memcpy(ring->pin[0] + a, bufs[i] + pos + a, b - a);
+                });
+                e = hipMemcpyAsync(ring->dbuf[0], ring->pin[0], len, hipMemcpyHostToDevice, ring->stream[0]);
+                if (e != hipSuccess) rc = hip_fail(e, "md5_host H2D");
+                hbec_view v{ring->dbuf[0], 0};
+                if (!rc) rc = hbec_md5_update(ctx, &v, len, ring->stream[0]);
+                if (!rc) {
+                    e = hipStreamSynchronize(ring->stream[0]);  // pinned slot reused by the next piece
+                    if (e != hipSuccess) rc = hip_fail(e, "md5_host sync");
+                }
+            }
+            if (!rc) rc = hbec_md5_final(ctx, d_dig + i * 16, ring->stream[0]);
+            hbec_md5_free(ctx);  // hipFree synchronises with the queued final
+            if (rc) return rc;
+        }
+        e = hipMemcpyAsync(digests, d_dig, n * 16, hipMemcpyDeviceToHost, ring->stream[0]);
+        (void)hipFreeAsync(d_dig, ring->stream[0]);
+        if (e == hipSuccess) e = hipStreamSynchronize(ring->stream[0]);
+        if (e != hipSuccess) return hip_fail(e, "md5_host digests");
+        return HBEC_OK;
+    });
 }
 
 int hbec_md5_new(int n_views, uint64_t n_objects, hbec_md5** out) {
-    if (!out || n_views <= 0 || n_objects == 0) return fail(HBEC_ERR_INVALID_ARG, "md5_new: bad arguments");
-    *out = nullptr;
-    hbec_md5* c = new (std::nothrow) hbec_md5();
-    if (!c) return fail(HBEC_ERR_NOMEM, "md5_new");
-    c->n_views = n_views;
-    c->n_obj = n_objects;
-    hipError_t e = hipMalloc(&c->d_state, (size_t)n_views * n_objects * md5_state_bytes());
-    if (e != hipSuccess) {
-        delete c;
-        return e == hipErrorOutOfMemory ? fail(HBEC_ERR_NOMEM, "md5 state") : hip_fail(e, "hipMalloc");
-    }
-    *out = c;
-    return HBEC_OK;
+    return hbec::guarded("hbec_md5_new", [&]() -> int {
+        if (!out || n_views <= 0 || n_objects == 0) return fail(HBEC_ERR_INVALID_ARG, "md5_new: bad arguments");
+        *out = nullptr;
+        hbec_md5* c = new (std::nothrow) hbec_md5();
+        if (!c) return fail(HBEC_ERR_NOMEM, "md5_new");
+        c->n_views = n_views;
+        c->n_obj = n_objects;
+        hipError_t e = hipMalloc(&c->d_state, (size_t)n_views * n_objects * md5_state_bytes());
+        if (e != hipSuccess) {
+            delete c;
+            return e == hipErrorOutOfMemory ? fail(HBEC_ERR_NOMEM, "md5 state") : hip_fail(e, "hipMalloc");
+        }
+        *out = c;
+        return HBEC_OK;
+    });
 }
 
 void hbec_md5_free(hbec_md5* c) {
@@ -444,78 +452,84 @@ void hbec_md5_free(hbec_md5* c) {
 }
 
 int hbec_md5_update(hbec_md5* c, const hbec_view* views, uint64_t len, void* hip_stream) {
-    if (!c) return fail(HBEC_ERR_INVALID_ARG, "md5_update: null context");
-    int rc = check_views(views, c->n_views, c->n_obj, len);
-    if (rc) return rc;
-    if (len == 0 && c->started) return HBEC_OK;
-    rc = md5_step(views, c->n_views, c->n_obj, len, c->total, c->started ? 0u : kInit, c->d_state, nullptr,
-                  static_cast<hipStream_t>(hip_stream));
-    if (rc) return rc;
-    c->started = true;
-    c->total += len;
-    return HBEC_OK;
+    return hbec::guarded("hbec_md5_update", [&]() -> int {
+        if (!c) return fail(HBEC_ERR_INVALID_ARG, "md5_update: null context");
+        int rc = check_views(views, c->n_views, c->n_obj, len);
+        if (rc) return rc;
+        if (len == 0 && c->started) return HBEC_OK;
+        rc = md5_step(views, c->n_views, c->n_obj, len, c->total, c->started ? 0u : kInit, c->d_state, nullptr,
+                      static_cast<hipStream_t>(hip_stream));
+        if (rc) return rc;
+        c->started = true;
+        c->total += len;
+        return HBEC_OK;
+    });
 }
 
 int hbec_md5_final(hbec_md5* c, uint8_t* d_digests, void* hip_stream) {
-    if (!c) return fail(HBEC_ERR_INVALID_ARG, "md5_final: null context");
-    int rc0 = check_digests(d_digests);
-    if (rc0) return rc0;
-    std::vector<hbec_view> none((size_t)c->n_views, hbec_view{nullptr, 0});
-    int rc = md5_step(none.data(), c->n_views, c->n_obj, 0, c->total, kFinal | (c->started ? 0u : kInit),
-                      c->d_state, d_digests, static_cast<hipStream_t>(hip_stream));
-    if (rc) return rc;
-    c->started = false;
-    c->total = 0;
-    return HBEC_OK;
+    return hbec::guarded("hbec_md5_final", [&]() -> int {
+        if (!c) return fail(HBEC_ERR_INVALID_ARG, "md5_final: null context");
+        int rc0 = check_digests(d_digests);
+        if (rc0) return rc0;
+        std::vector<hbec_view> none((size_t)c->n_views, hbec_view{nullptr, 0});
+        int rc = md5_step(none.data(), c->n_views, c->n_obj, 0, c->total, kFinal | (c->started ? 0u : kInit),
+                          c->d_state, d_digests, static_cast<hipStream_t>(hip_stream));
+        if (rc) return rc;
+        c->started = false;
+        c->total = 0;
+        return HBEC_OK;
+    });
 }
 
 int hbec_encode_md5_batch(hbec_codec* codec, const hbec_view* views, uint64_t n_objects, uint64_t shard_len,
                           uint8_t* d_digests, void* hip_stream) {
-    if (!codec || !views) return fail(HBEC_ERR_INVALID_ARG, "encode_md5: null argument");
-    const int n = hbec_data_shards(codec) + hbec_parity_shards(codec);
-    int rc = check_digests(d_digests);
-    if (rc) return rc;
-    if (n_objects == 0) return HBEC_OK;
-    if (shard_len == 0) return fail(HBEC_ERR_SHARD_NO_DATA, "encode_md5: zero shard length");
-    rc = check_views(views, n, n_objects, shard_len);
-    if (rc) return rc;
-    hipStream_t main = static_cast<hipStream_t>(hip_stream);
-    const uint64_t seg = md5_segment(shard_len, hbec_data_shards(codec));
-    if (seg >= shard_len) {  // one segment: encode, then hash every shard
-        rc = hbec_encode_batch(codec, views, n_objects, shard_len, hip_stream);
+    return hbec::guarded("hbec_encode_md5_batch", [&]() -> int {
+        if (!codec || !views) return fail(HBEC_ERR_INVALID_ARG, "encode_md5: null argument");
+        const int n = hbec_data_shards(codec) + hbec_parity_shards(codec);
+        int rc = check_digests(d_digests);
         if (rc) return rc;
-        return md5_step(views, n, n_objects, shard_len, 0, kInit | kFinal, nullptr, d_digests, main);
-    }
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
-    hipMemPool_t pool;
-    rc = state_pool(dev, &pool);
-    if (rc) return rc;
-    void* state = nullptr;
-    e = hipMallocFromPoolAsync(&state, (size_t)n * n_objects * md5_state_bytes(), pool, main);
-    if (e != hipSuccess) return hip_fail(e, "hipMallocFromPoolAsync");
-    hipStream_t side;
-    rc = side_stream_get(dev, &side);
-    if (rc) {
+        if (n_objects == 0) return HBEC_OK;
+        if (shard_len == 0) return fail(HBEC_ERR_SHARD_NO_DATA, "encode_md5: zero shard length");
+        rc = check_views(views, n, n_objects, shard_len);
+        if (rc) return rc;
+        hipStream_t main = static_cast<hipStream_t>(hip_stream);
+        const uint64_t seg = md5_segment(shard_len, hbec_data_shards(codec));
+        if (seg >= shard_len) {  // one segment: encode, then hash every shard
+            rc = hbec_encode_batch(codec, views, n_objects, shard_len, hip_stream);
+            if (rc) return rc;
+            return md5_step(views, n, n_objects, shard_len, 0, kInit | kFinal, nullptr, d_digests, main);
+        }
+        int dev = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+        hipMemPool_t pool;
+        rc = state_pool(dev, &pool);
+        if (rc) return rc;
+        void* state = nullptr;
+        e = hipMallocFromPoolAsync(&state, (size_t)n * n_objects * md5_state_bytes(), pool, main);
+        if (e != hipSuccess) return hip_fail(e, "hipMallocFromPoolAsync");
+        hipStream_t side;
+        rc = side_stream_get(dev, &side);
+        if (rc) {
+            hipFreeAsync(state, main);
+            return rc;
+        }
+        std::vector<hbec_view> sv((size_t)n);
+        for (uint64_t off = 0; off < shard_len && rc == HBEC_OK; off += seg) {
+            const uint64_t len = std::min(seg, shard_len - off);
+            for (int i = 0; i < n; ++i) sv[i] = hbec_view{static_cast<uint8_t*>(views[i].base) + off, views[i].obj_stride};
+            rc = hbec_encode_batch(codec, sv.data(), n_objects, len, hip_stream);
+            if (rc) break;
+            rc = order_after(side, main);  // segment encoded (and, first time, state allocated)
+            if (rc) break;
+            const uint32_t flags = (off == 0 ? kInit : 0u) | (off + len == shard_len ? kFinal : 0u);
+            rc = md5_step(sv.data(), n, n_objects, len, off, flags, state, d_digests, side);
+        }
+        const int rc2 = order_after(main, side);  // caller's stream: digests ready
         hipFreeAsync(state, main);
-        return rc;
-    }
-    std::vector<hbec_view> sv((size_t)n);
-    for (uint64_t off = 0; off < shard_len && rc == HBEC_OK; off += seg) {
-        const uint64_t len = std::min(seg, shard_len - off);
-        for (int i = 0; i < n; ++i) sv[i] = hbec_view{static_cast<uint8_t*>(views[i].base) + off, views[i].obj_stride};
-        rc = hbec_encode_batch(codec, sv.data(), n_objects, len, hip_stream);
-        if (rc) break;
-        rc = order_after(side, main);  // segment encoded (and, first time, state allocated)
-        if (rc) break;
-        const uint32_t flags = (off == 0 ? kInit : 0u) | (off + len == shard_len ? kFinal : 0u);
-        rc = md5_step(sv.data(), n, n_objects, len, off, flags, state, d_digests, side);
-    }
-    const int rc2 = order_after(main, side);  // caller's stream: digests ready
-    hipFreeAsync(state, main);
-    side_stream_put(dev, side);
-    return rc ? rc : rc2;
+        side_stream_put(dev, side);
+        return rc ? rc : rc2;
+    });
 }
 
 }  // extern "C"
