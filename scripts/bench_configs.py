@@ -4,8 +4,8 @@
   config 2: 4+2 encode, 4096 x 1 MiB
   config 3: 4+2 reconstruct, 4096 x 1 MiB, erasures {0,1} {0,4} {4,5} {2,3}
   config 4: 8+3 encode + reconstruct{0,1,2}, 4096 objects of 4 KiB or 1 MiB
-            (p = 0.5 each, drawn by splitmix64(seed) per index; one launch per
-            op through a stripe plan)
+            (p = 0.5 each, drawn by splitmix64(seed) per index) in three
+            placements, timed interleaved (config4())
   extra   : 8+3 @ 1 MiB uniform (strided views); Verify of both uniform configs
 
 Algorithmic bytes per object: encode (k+m)*S, reconstruct (k+e)*S.
@@ -56,20 +56,32 @@ def line(name, nbytes, ms, **kw):
 
 
 def uniform(k, m, n, size, patterns):
+    """Encode, Verify and Reconstruct (each erasure pattern) of n uniform
+    objects, timed interleaved; each op's output is checked afterwards."""
     s = size // k
     enc = RS.New(k, m)
     objs = torch.empty((n, size), dtype=torch.uint8, device="cuda")
     B.fill_splitmix(objs, size)
     par = torch.empty((n, m * s), dtype=torch.uint8, device="cuda")
     views = B.shard_views(objs, k, s) + B.shard_views(par, m, s)
-    ms = timeit(lambda: B.encode_views(enc, views, n, s))
-    line(f"{k}+{m} encode {n}x{size}", n * (k + m) * s, ms, kernel=B.kernel_info(k, m, s)["kind"])
-    for i in [0, n // 2, n - 1]:
-        o, p = objs[i].cpu().numpy(), par[i].cpu().numpy()
-        assert U.verify_shards(enc, [o[j * s:(j + 1) * s] for j in range(k)] + [p[r * s:(r + 1) * s] for r in range(m)])
     # Verify (read-only: k+m shards read per object, one flag word written)
     flags = torch.zeros(n, dtype=torch.int32, device="cuda")
-    ms = timeit(lambda: B.verify_views(enc, views, n, s, flags))
+    cases = {"encode": lambda: B.encode_views(enc, views, n, s),
+             "verify": lambda: B.verify_views(enc, views, n, s, flags)}
+    outs = {}
+    for miss in patterns:
+        out = torch.empty((n, len(miss) * s), dtype=torch.uint8, device="cuda")
+        rv = list(views)
+        for slot, i in enumerate(miss):
+            rv[i] = (out.data_ptr() + slot * s, out.stride(0))
+        present = [0 if i in miss else 1 for i in range(k + m)]
+        outs[miss] = out
+        cases[miss] = (lambda rv=rv, present=present: B.reconstruct_views(enc, rv, present, n, s))
+    B.encode_views(enc, views, n, s)  # parity first: verify and reconstruct read it
+    t = interleaved(cases)
+    for i in [0, n // 2, n - 1]:
+        o, q = objs[i].cpu().numpy(), par[i].cpu().numpy()
+        assert U.verify_shards(enc, [o[j * s:(j + 1) * s] for j in range(k)] + [q[r * s:(r + 1) * s] for r in range(m)])
     assert int(flags.sum()) == 0
     par[n // 3, 5] ^= 1
     flags.zero_()
@@ -77,19 +89,14 @@ def uniform(k, m, n, size, patterns):
     torch.cuda.synchronize()
     assert flags.nonzero().flatten().tolist() == [n // 3]
     par[n // 3, 5] ^= 1
-    line(f"{k}+{m} verify {n}x{size}", n * (k + m) * s, ms, bound="HBM read")
-    for miss in patterns:
-        out = torch.empty((n, len(miss) * s), dtype=torch.uint8, device="cuda")
-        rv = list(views)
-        for slot, i in enumerate(miss):
-            rv[i] = (out.data_ptr() + slot * s, out.stride(0))
-        present = [0 if i in miss else 1 for i in range(k + m)]
-        ms = timeit(lambda: B.reconstruct_views(enc, rv, present, n, s))
-        torch.cuda.synchronize()
+    for miss, out in outs.items():
         for slot, i in enumerate(miss):
             src = objs[:, i * s:(i + 1) * s] if i < k else par[:, (i - k) * s:(i - k + 1) * s]
             assert torch.equal(out[:, slot * s:(slot + 1) * s], src), miss
-        line(f"{k}+{m} reconstruct{set(miss)} {n}x{size}", n * (k + len(miss)) * s, ms)
+    line(f"{k}+{m} encode {n}x{size}", n * (k + m) * s, t["encode"], kernel=B.kernel_info(k, m, s)["kind"])
+    line(f"{k}+{m} verify {n}x{size}", n * (k + m) * s, t["verify"], bound="HBM read")
+    for miss in patterns:
+        line(f"{k}+{m} reconstruct{set(miss)} {n}x{size}", n * (k + len(miss)) * s, t[miss])
 
 
 def uniform_plan(k, m, n, size):
@@ -105,46 +112,48 @@ def uniform_plan(k, m, n, size):
     line(f"{k}+{m} encode {n}x{size} (plan, uniform)", n * (k + m) * s, ms, plan=plan.info())
 
 
-def mixed_8_3(n=4096):
+def interleaved(cases, rounds=8, reps=3):
+    """Median ms per case, cases run in alternating order each round, so clock
+    and power drift over a long script hit every case alike."""
+    names = list(cases)
+    for f in cases.values():  # warm
+        f()
+    t = {c: [] for c in names}
+    for rnd in range(rounds):
+        for c in (names if rnd % 2 == 0 else names[::-1]):
+            for _ in range(reps):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                cases[c]()
+                e1.record()
+                torch.cuda.synchronize()
+                t[c].append(e0.elapsed_time(e1))
+    return {c: statistics.median(v) for c, v in t.items()}
+
+
+def config4(n=4096):
+    """Config 4: 8+3 encode + reconstruct{0,1,2} of n objects of 4 KiB or 1 MiB
+    (p = 0.5 each, drawn by splitmix64(seed) per index), in three placements,
+    timed interleaved:
+      stripes  - ecSplit databufs back to back (stripe plan, one launch per op)
+      objects  - a data arena + a parity arena (object plan, one launch per op)
+      classes  - size-classed strided batches (two launches per op)"""
     k, m = 8, 3
+    miss = (0, 1, 2)
+    present = [0 if i in miss else 1 for i in range(k + m)]
     flags = U.splitmix_bytes(n)
     sizes = [MiB if b & 1 else 4096 for b in flags]
-    layout, off = [], 0
+    enc = RS.New(k, m)
+    # stripes
+    lay, off = [], 0
     for size in sizes:
         s = size // k
-        layout.append((off, s))
+        lay.append((off, s))
         off += (k + m) * s
     pool = torch.empty(off, dtype=torch.uint8, device="cuda")
     B.fill_splitmix(pool.view(1, -1), off)
-    enc = RS.New(k, m)
-    plan = B.StripePlan(enc, [(pool.data_ptr() + o, s) for o, s in layout])
-    enc_bytes = sum((k + m) * s for _, s in layout)
-    ms = timeit(plan.encode)
-    n_big = sum(1 for x in sizes if x == MiB)
-    line(f"8+3 encode mixed 4KiB/1MiB x{n} (plan)", enc_bytes, ms, n_1MiB=n_big, n_4KiB=n - n_big,
-         plan=plan.info())
-    host = pool.cpu().numpy()
-    for i in [0, 1, 2, n - 1] + [j for j in range(n) if sizes[j] == 4096][:3]:
-        o, s = layout[i]
-        assert U.verify_stripe(enc, host[o:o + (k + m) * s])
-    ref = pool.clone()
-    miss = (0, 1, 2)
-    present = [0 if i in miss else 1 for i in range(k + m)]
-    ms = timeit(lambda: plan.reconstruct(present))
-    assert torch.equal(pool, ref)  # rebuilt in place == original
-    rec_bytes = sum((k + len(miss)) * s for _, s in layout)
-    line(f"8+3 reconstruct{{0,1,2}} mixed 4KiB/1MiB x{n} (plan)", rec_bytes, ms)
-    t_enc = timeit(plan.encode, reps=5)
-    t_rec = timeit(lambda: plan.reconstruct(present), reps=5)
-    line(f"8+3 encode+reconstruct mixed x{n} (config 4)", enc_bytes + rec_bytes, t_enc + t_rec)
-
-
-def mixed_8_3_objects(n=4096):
-    """Config 4 over an object plan: objects back to back in a data arena,
-    parity back to back in a parity arena (hbec_plan_objects)."""
-    k, m = 8, 3
-    flags = U.splitmix_bytes(n)
-    sizes = [MiB if b & 1 else 4096 for b in flags]
+    splan = B.StripePlan(enc, [(pool.data_ptr() + o, s) for o, s in lay])
+    # objects
     dl, pl, doff, poff = [], [], 0, 0
     for size in sizes:
         s = size // k
@@ -155,79 +164,53 @@ def mixed_8_3_objects(n=4096):
     data = torch.empty(doff, dtype=torch.uint8, device="cuda")
     parity = torch.empty(poff, dtype=torch.uint8, device="cuda")
     B.fill_splitmix(data.view(1, -1), doff)
-    enc = RS.New(k, m)
-    plan = B.StripePlan(enc, objects=[(data.data_ptr() + o, parity.data_ptr() + po, s)
-                                      for (o, s), po in zip(dl, pl)])
-    enc_bytes = sum((k + m) * s for _, s in dl)
-    ms = timeit(plan.encode)
-    line(f"8+3 encode mixed 4KiB/1MiB x{n} (object plan)", enc_bytes, ms, plan=plan.info())
-    hd, hp = data.cpu().numpy(), parity.cpu().numpy()
-    for i in [0, 1, 2, n - 1] + [j for j in range(n) if sizes[j] == 4096][:3]:
-        (o, s), po = dl[i], pl[i]
-        assert U.verify_shards(enc, [hd[o + j * s:o + (j + 1) * s] for j in range(k)] +
-                               [hp[po + r * s:po + (r + 1) * s] for r in range(m)])
-    ref = data.clone()
-    miss = (0, 1, 2)
-    present = [0 if i in miss else 1 for i in range(k + m)]
-    ms = timeit(lambda: plan.reconstruct(present))
-    assert torch.equal(data, ref)  # rebuilt in place == original
-    rec_bytes = sum((k + len(miss)) * s for _, s in dl)
-    line(f"8+3 reconstruct{{0,1,2}} mixed 4KiB/1MiB x{n} (object plan)", rec_bytes, ms)
-    t_enc = timeit(plan.encode, reps=5)
-    t_rec = timeit(lambda: plan.reconstruct(present), reps=5)
-    line(f"8+3 encode+reconstruct mixed x{n} (config 4, object plan)", enc_bytes + rec_bytes, t_enc + t_rec)
-
-
-def mixed_8_3_size_classes(n=4096):
-    """Config 4 with size-classed arenas: the batch's objects are placed by
-    size class, each class as a strided batch (objs [n_c][L_c] + parity
-    [n_c][m*S_c], the layout of the headline): 1 MiB objects run on the
-    pipelined kernel, 4 KiB objects on the short-shard kernel.  Two launches
-    per op, timed together."""
-    k, m = 8, 3
-    flags = U.splitmix_bytes(n)
-    sizes = [MiB if b & 1 else 4096 for b in flags]
-    enc = RS.New(k, m)
+    oplan = B.StripePlan(enc, objects=[(data.data_ptr() + o, parity.data_ptr() + po, s)
+                                       for (o, s), po in zip(dl, pl)])
+    # size classes
     classes = []
     for size in (MiB, 4096):
-        idx = [i for i, x in enumerate(sizes) if x == size]
+        cnt = sum(1 for x in sizes if x == size)
         s = size // k
-        objs = torch.empty((len(idx), size), dtype=torch.uint8, device="cuda")
+        objs = torch.empty((cnt, size), dtype=torch.uint8, device="cuda")
         B.fill_splitmix(objs, size)
-        par = torch.empty((len(idx), m * s), dtype=torch.uint8, device="cuda")
-        views = B.shard_views(objs, k, s) + B.shard_views(par, m, s)
-        classes.append((len(idx), s, objs, par, views))
-    miss = (0, 1, 2)
-    present = [0 if i in miss else 1 for i in range(k + m)]
+        par = torch.empty((cnt, m * s), dtype=torch.uint8, device="cuda")
+        classes.append((cnt, s, objs, par, B.shard_views(objs, k, s) + B.shard_views(par, m, s)))
 
-    def encode():
+    def cls_encode():
         for cnt, s, _, _, v in classes:
             B.encode_views(enc, v, cnt, s)
 
-    def reconstruct():
+    def cls_reconstruct():
         for cnt, s, _, _, v in classes:
             B.reconstruct_views(enc, v, present, cnt, s)
 
-    encode()
-    torch.cuda.synchronize()
+    t = interleaved({
+        "stripes_enc": splan.encode, "stripes_rec": lambda: splan.reconstruct(present),
+        "objects_enc": oplan.encode, "objects_rec": lambda: oplan.reconstruct(present),
+        "classes_enc": cls_encode, "classes_rec": cls_reconstruct,
+    })
+    # self-checks: parity verifies, and the in-place rebuilds reproduced the data
+    hp, hd, hpar = pool.cpu().numpy(), data.cpu().numpy(), parity.cpu().numpy()
+    for i in [0, 1, 2, n - 1] + [j for j in range(n) if sizes[j] == 4096][:3]:
+        o, s = lay[i]
+        assert U.verify_stripe(enc, hp[o:o + (k + m) * s])
+        (o, s), po = dl[i], pl[i]
+        assert U.verify_shards(enc, [hd[o + j * s:o + (j + 1) * s] for j in range(k)] +
+                               [hpar[po + r * s:po + (r + 1) * s] for r in range(m)])
     for cnt, s, objs, par, _ in classes:
-        ho, hp = objs[:3].cpu().numpy(), par[:3].cpu().numpy()
-        for i in range(3):
+        ho, hq = objs[:2].cpu().numpy(), par[:2].cpu().numpy()
+        for i in range(2):
             assert U.verify_shards(enc, [ho[i, j * s:(j + 1) * s] for j in range(k)] +
-                                   [hp[i, r * s:(r + 1) * s] for r in range(m)])
-    refs = [objs.clone() for _, _, objs, _, _ in classes]
-    enc_bytes = sum(cnt * (k + m) * s for cnt, s, _, _, _ in classes)
-    rec_bytes = sum(cnt * (k + len(miss)) * s for cnt, s, _, _, _ in classes)
-    ms = timeit(encode)
-    line(f"8+3 encode mixed 4KiB/1MiB x{n} (size-classed arenas)", enc_bytes, ms,
-         n_1MiB=classes[0][0], n_4KiB=classes[1][0])
-    ms = timeit(reconstruct)
-    for ref, (_, _, objs, _, _) in zip(refs, classes):
-        assert torch.equal(objs, ref)  # rebuilt in place == original
-    line(f"8+3 reconstruct{{0,1,2}} mixed 4KiB/1MiB x{n} (size-classed arenas)", rec_bytes, ms)
-    t_enc = timeit(encode, reps=5)
-    t_rec = timeit(reconstruct, reps=5)
-    line(f"8+3 encode+reconstruct mixed x{n} (config 4, size-classed arenas)", enc_bytes + rec_bytes, t_enc + t_rec)
+                                   [hq[i, r * s:(r + 1) * s] for r in range(m)])
+    enc_bytes = sum((k + m) * s for _, s in lay)
+    rec_bytes = sum((k + len(miss)) * s for _, s in lay)
+    n_big = sum(1 for x in sizes if x == MiB)
+    for name, what in (("stripes", "stripe plan, ecSplit databufs"), ("objects", "object plan, data + parity arenas"),
+                       ("classes", "size-classed strided batches, 2 launches per op")):
+        line(f"8+3 encode mixed 4KiB/1MiB x{n} ({what})", enc_bytes, t[name + "_enc"], n_1MiB=n_big, n_4KiB=n - n_big)
+        line(f"8+3 reconstruct{{0,1,2}} mixed 4KiB/1MiB x{n} ({what})", rec_bytes, t[name + "_rec"])
+        line(f"8+3 encode+reconstruct mixed x{n} (config 4, {what})", enc_bytes + rec_bytes,
+             t[name + "_enc"] + t[name + "_rec"])
 
 
 def main():
@@ -236,9 +219,7 @@ def main():
     uniform(8, 3, 4096, MiB, [(0, 1, 2)])
     uniform_plan(4, 2, 4096, MiB)
     uniform_plan(8, 3, 4096, MiB)
-    mixed_8_3()
-    mixed_8_3_objects()
-    mixed_8_3_size_classes()
+    config4()
 
 
 if __name__ == "__main__":

@@ -259,8 +259,68 @@ def kernels_ab(n=4096, k=4, m=2, rounds=16, reps=3):
                           "frac": round(nb / ms / 1e6 / 8000, 4), "ok": ok}), flush=True)
 
 
+def mixed_ab(n=4096, k=8, m=3, rounds=12, reps=3):
+    """Config 4 (8+3, 4 KiB / 1 MiB mixed, p = 0.5) interleaved: stripe plan over
+    ecSplit stripes vs object plan over data / parity arenas, and the object
+    plan restricted to the big objects or to the small ones."""
+    from scripts import _common as U
+
+    torch.cuda.set_device(0)
+    MiB = 1 << 20
+    flags = U.splitmix_bytes(n)
+    sizes = [MiB if b & 1 else 4096 for b in flags]
+    enc = RS.New(k, m)
+    # stripe layout
+    lay, off = [], 0
+    for size in sizes:
+        s = size // k
+        lay.append((off, s))
+        off += (k + m) * s
+    pool = torch.empty(off, dtype=torch.uint8, device="cuda")
+    B.fill_splitmix(pool.view(1, -1), off)
+    splan = B.StripePlan(enc, [(pool.data_ptr() + o, s) for o, s in lay])
+    # object arenas
+    dl, pl, doff, poff = [], [], 0, 0
+    for size in sizes:
+        s = size // k
+        dl.append((doff, s))
+        pl.append(poff)
+        doff += k * s
+        poff += m * s
+    data = torch.empty(doff, dtype=torch.uint8, device="cuda")
+    par = torch.empty(poff, dtype=torch.uint8, device="cuda")
+    B.fill_splitmix(data.view(1, -1), doff)
+    objs = [(data.data_ptr() + o, par.data_ptr() + po, s) for (o, s), po in zip(dl, pl)]
+    oplan = B.StripePlan(enc, objects=objs)
+    big = B.StripePlan(enc, objects=[x for x in objs if x[2] == MiB // k])
+    small = B.StripePlan(enc, objects=[x for x in objs if x[2] != MiB // k])
+    nb_all = sum((k + m) * s for _, s in lay)
+    nb_big = sum((k + m) * x[2] for x in objs if x[2] == MiB // k)
+    nb_small = nb_all - nb_big
+    cases = {"stripe_plan": (splan.encode, nb_all), "object_plan": (oplan.encode, nb_all),
+             "object_plan_big_only": (big.encode, nb_big), "object_plan_small_only": (small.encode, nb_small)}
+    t = {c: [] for c in cases}
+    names = list(cases)
+    for rnd in range(rounds + 1):
+        for c in (names if rnd % 2 == 0 else names[::-1]):
+            for _ in range(reps):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                cases[c][0]()
+                e1.record()
+                torch.cuda.synchronize()
+                if rnd:
+                    t[c].append(e0.elapsed_time(e1))
+    for c in names:
+        ms = statistics.median(t[c])
+        print(json.dumps({"sweep": "mixed", "case": c, "ms": round(ms, 4), "bytes": cases[c][1],
+                          "frac": round(cases[c][1] / ms / 1e6 / 8000, 4)}), flush=True)
+
+
 if __name__ == "__main__":
-    if sys.argv[1:2] == ["kernels"]:
+    if sys.argv[1:2] == ["mixed"]:
+        mixed_ab()
+    elif sys.argv[1:2] == ["kernels"]:
         a = [int(x) for x in sys.argv[2:]]
         kernels_ab(k=a[0], m=a[1]) if a else kernels_ab()
     elif sys.argv[1:2] == ["split_ab"]:
