@@ -18,7 +18,7 @@ data-path collective; torch.distributed carries only the barrier and the
 max-time reduction.
 
 Extra objects on the JSON line: `roofline` (dominant kernel = the
-gf_apply_vec<4,2> kernel that both ops launch; achieved = algorithmic bytes per
+gf_apply_vec_pipe2<4,2> kernel that both ops launch; achieved = algorithmic bytes per
 launch / its HIP-event-timed average launch duration on the launch stream;
 traffic = PMC HBM bytes per launch from the committed rocprofv3 summary,
 profiles/*_pmc.json) and `cpu_baseline` (oracle/gf_oracle.c's AVX2 port of
@@ -47,7 +47,7 @@ METRIC = "GiB/s device-resident EC encode+reconstruct, 4+2 @ 1 MiB; % HBM roofli
 GiB = float(1 << 30)
 MiB = 1 << 20
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
-KERNEL_NAME = "gf_apply_vec_pipe<4, 2>"
+KERNEL_NAME = "gf_apply_vec_pipe2<4, 2>"
 
 
 def dist_env():

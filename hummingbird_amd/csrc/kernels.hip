@@ -217,6 +217,104 @@ __global__ __launch_bounds__(kPipeBlockThreads, HBEC_PIPE_WAVES_PER_SIMD) void g
         compute_store_tile<K, R, U>(cur, a, tb, obj, base + lane * 16u, false);
 }
 
+#ifndef HBEC_PIPE_V2
+#define HBEC_PIPE_V2 1
+#endif
+// gf_apply_vec_pipe2: the pipelined kernel in the stripe-plan kernel's loop
+// shape -- every tile's shard bases are scalar values computed one tile ahead
+// (the plan kernel loads them as records) and full / partial tiles are a
+// uniform branch.  The hot path for K <= 4: +1.6 % over gf_apply_vec_pipe at
+// 4+2 in an interleaved A/B (75.3 % vs 74.1 % of 8 TB/s on that box), but
+// -7 % at 8+3, which keeps gf_apply_vec_pipe (profiles/r01_tune_pipe2.jsonl).
+template <int K, int R>
+struct PipeTile {
+    uint64_t in[K];
+    uint64_t out[R];
+    uint32_t valid;
+};
+
+template <int K, int R, int U>
+__device__ __forceinline__ void pipe_tile_coords(PipeTile<K, R>& b, const PassArgs& a, uint32_t t, uint32_t tpo) {
+    constexpr uint64_t TILE = (uint64_t)U * 1024u;
+    const uint32_t obj = t / tpo;
+    const uint64_t off = (uint64_t)(t - obj * tpo) * TILE;
+#pragma unroll
+    for (int j = 0; j < K; ++j) b.in[j] = reinterpret_cast<uint64_t>(a.in[j]) + obj * a.in_stride[j] + off;
+#pragma unroll
+    for (int r = 0; r < R; ++r) b.out[r] = reinterpret_cast<uint64_t>(a.out[r]) + obj * a.out_stride[r] + off;
+    const uint64_t left = a.shard_len - off;
+    b.valid = (uint32_t)(left < TILE ? left : TILE);
+}
+
+template <int K, int R, int U>
+__device__ __forceinline__ void pipe2_load(u32x4 (&x)[U][K], const PipeTile<K, R>& b, uint32_t lane) {
+    const uint64_t last = (uint64_t)b.valid - 16u;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        uint64_t off = (uint64_t)lane * 16u + (uint64_t)u * 1024u;
+        off = off < last ? off : last;
+#pragma unroll
+        for (int j = 0; j < K; ++j) x[u][j] = ld16_addr(b.in[j] + off);
+    }
+}
+
+template <int K, int R, int U, bool FULL>
+__device__ __forceinline__ void pipe2_store_(const u32x4 (&x)[U][K], const PassArgs& a, const Tables<K, R>& tb,
+                                             const PipeTile<K, R>& b, uint32_t lane) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint64_t off = (uint64_t)lane * 16u + (uint64_t)u * 1024u;
+        u32x4 acc[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r] = u32x4{0, 0, 0, 0};
+        gf_dot<K, R>(acc, x[u], a.tab, tb);
+        if (FULL || off < b.valid) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) st16_addr(b.out[r] + off, acc[r]);
+        }
+    }
+}
+
+template <int K, int R>
+__global__ __launch_bounds__(kPipeBlockThreads, HBEC_PIPE_WAVES_PER_SIMD) void gf_apply_vec_pipe2(PassArgs a) {
+    constexpr int U = pipe_u(K);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t nw = gridDim.x * (kPipeBlockThreads / 64);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(xcd_block() * (kPipeBlockThreads / 64) + (threadIdx.x >> 6));
+    const uint32_t tpo = a.tiles_per_obj;
+    const uint32_t n = a.n_tiles;
+    if (wave >= n) return;
+    const Tables<K, R> tb = load_tables<K, R>(a.tab);
+    PipeTile<K, R> cur, nxt;
+    pipe_tile_coords<K, R, U>(cur, a, wave, tpo);
+    u32x4 x[U][K];
+    pipe2_load<K, R, U>(x, cur, lane);
+    uint32_t tn = wave + nw;
+    pipe_tile_coords<K, R, U>(nxt, a, tn < n ? tn : wave, tpo);
+    for (; tn < n; tn += nw) {
+        u32x4 y[U][K];
+        pipe2_load<K, R, U>(y, nxt, lane);
+        if (HBEC_PIPE_SLEEP > 0 && K <= 4) __builtin_amdgcn_s_sleep(HBEC_PIPE_SLEEP);
+        const uint32_t t2 = tn + nw;
+        PipeTile<K, R> after;
+        pipe_tile_coords<K, R, U>(after, a, t2 < n ? t2 : tn, tpo);
+        if (cur.valid >= (uint32_t)U * 1024u)
+            pipe2_store_<K, R, U, true>(x, a, tb, cur, lane);
+        else
+            pipe2_store_<K, R, U, false>(x, a, tb, cur, lane);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int j = 0; j < K; ++j) x[u][j] = y[u][j];
+        cur = nxt;
+        nxt = after;
+    }
+    if (cur.valid >= (uint32_t)U * 1024u)
+        pipe2_store_<K, R, U, true>(x, a, tb, cur, lane);
+    else
+        pipe2_store_<K, R, U, false>(x, a, tb, cur, lane);
+}
+
 // Streaming vec path (runtime K): one input shard at a time with the next
 // input's loads in flight, coefficient tables fetched per input by scalar
 // loads, so registers stay at R x 4 KiB accumulators + 2 x 4 KiB buffers for
@@ -353,7 +451,8 @@ __global__ __launch_bounds__(kBlockThreads) void fill_splitmix(uint8_t* dst, uin
 // ---------------------------------------------------------------------------
 template <int K, int R>
 static const void* vec_kernel_ptr(bool pipe) {
-    if (pipe) return reinterpret_cast<const void*>(&gf_apply_vec_pipe<K, R>);
+    if (pipe) return (HBEC_PIPE_V2 && K <= 4) ? reinterpret_cast<const void*>(&gf_apply_vec_pipe2<K, R>)
+                                              : reinterpret_cast<const void*>(&gf_apply_vec_pipe<K, R>);
     return reinterpret_cast<const void*>(&gf_apply_vec<K, R>);
 }
 

@@ -31,6 +31,8 @@ P = T1 + ["HBEC_USE_PIPE=1"]
 VARIANTS = {
     "cur": ([], {}),
     "d": ([], {}),
+    "v2": (["HBEC_PIPE_V2=1"], {}),
+    "v2s0": (["HBEC_PIPE_V2=1", "HBEC_PIPE_SLEEP=0"], {}),
     "u2s6": (["HBEC_PIPE_LOADS=8"], {}),
     "u2s10": (["HBEC_PIPE_LOADS=8", "HBEC_PIPE_SLEEP=10"], {}),
     "u2s14": (["HBEC_PIPE_LOADS=8", "HBEC_PIPE_SLEEP=14"], {}),
