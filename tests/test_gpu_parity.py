@@ -361,7 +361,8 @@ def test_baseline_size_4096x1mib_roundtrip():
 
 
 @pytest.mark.parametrize("k,m,s,n", [(4, 2, 5 * 4096 + 48, 7), (8, 3, 3 * 2048 + 16, 5), (2, 2, 4096 * 2 + 1024, 3),
-                                     (4, 2, 4096, 1), (6, 3, 16 * 1024, 300), (4, 1, 256 * 1024, 9)])
+                                     (4, 2, 4096, 1), (6, 3, 16 * 1024, 300), (4, 1, 256 * 1024, 9),
+                                     (3, 3, 3 * 1024 + 32, 5), (1, 2, 4 * 4096 + 16, 4), (4, 3, 9 * 1024 + 16, 6)])
 def test_batch_pipelined_partial_tiles(k, m, s, n):
     """Shard lengths that are not a multiple of the pipelined kernel's tile,
     and grids with fewer tiles than waves."""
