@@ -220,6 +220,9 @@ __global__ __launch_bounds__(kPipeBlockThreads, HBEC_PIPE_WAVES_PER_SIMD) void g
 #ifndef HBEC_PIPE_V2
 #define HBEC_PIPE_V2 1
 #endif
+#ifndef HBEC_PIPE_V2_MAXK
+#define HBEC_PIPE_V2_MAXK 4
+#endif
 // gf_apply_vec_pipe2: the pipelined kernel in the stripe-plan kernel's loop
 // shape -- every tile's shard bases are scalar values computed one tile ahead
 // (the plan kernel loads them as records) and full / partial tiles are a
@@ -451,7 +454,7 @@ __global__ __launch_bounds__(kBlockThreads) void fill_splitmix(uint8_t* dst, uin
 // ---------------------------------------------------------------------------
 template <int K, int R>
 static const void* vec_kernel_ptr(bool pipe) {
-    if (pipe) return (HBEC_PIPE_V2 && K <= 4) ? reinterpret_cast<const void*>(&gf_apply_vec_pipe2<K, R>)
+    if (pipe) return (HBEC_PIPE_V2 && K <= HBEC_PIPE_V2_MAXK) ? reinterpret_cast<const void*>(&gf_apply_vec_pipe2<K, R>)
                                               : reinterpret_cast<const void*>(&gf_apply_vec_pipe<K, R>);
     return reinterpret_cast<const void*>(&gf_apply_vec<K, R>);
 }

@@ -32,6 +32,10 @@ VARIANTS = {
     "cur": ([], {}),
     "d": ([], {}),
     "v2": (["HBEC_PIPE_V2=1"], {}),
+    "v2all": (["HBEC_PIPE_V2_MAXK=16"], {}),
+    "v2all_l16": (["HBEC_PIPE_V2_MAXK=16", "HBEC_PIPE_LOADS=16"], {}),
+    "v2all_l24": (["HBEC_PIPE_V2_MAXK=16", "HBEC_PIPE_LOADS=24"], {}),
+    "v1_l16": (["HBEC_PIPE_LOADS=16"], {}),
     "v2s0": (["HBEC_PIPE_V2=1", "HBEC_PIPE_SLEEP=0"], {}),
     "u2s6": (["HBEC_PIPE_LOADS=8"], {}),
     "u2s10": (["HBEC_PIPE_LOADS=8", "HBEC_PIPE_SLEEP=10"], {}),
