@@ -236,11 +236,30 @@ struct PipeTile {
     uint32_t valid;
 };
 
+// Tuning knob (tile order): with HBEC_SWZ_G > 0, runs of HBEC_SWZ_C tiles
+// of HBEC_SWZ_G objects are interleaved, so the tiles in flight at one time
+// span G objects instead of ~4 (only when both divide the batch evenly).
+#ifndef HBEC_SWZ_G
+#define HBEC_SWZ_G 0  // off: never faster (profiles/r01_tune_swizzle.jsonl)
+#endif
+#ifndef HBEC_SWZ_C
+#define HBEC_SWZ_C 16
+#endif
+
 template <int K, int R, int U>
 __device__ __forceinline__ void pipe_tile_coords(PipeTile<K, R>& b, const PassArgs& a, uint32_t t, uint32_t tpo) {
     constexpr uint64_t TILE = (uint64_t)U * 1024u;
-    const uint32_t obj = t / tpo;
-    const uint64_t off = (uint64_t)(t - obj * tpo) * TILE;
+    uint32_t obj = t / tpo;
+    uint64_t off = (uint64_t)(t - obj * tpo) * TILE;
+    if (HBEC_SWZ_G > 0 && tpo % HBEC_SWZ_C == 0 && (a.n_tiles / tpo) % HBEC_SWZ_G == 0) {
+        const uint32_t ci = t % HBEC_SWZ_C;
+        const uint32_t oi = (t / HBEC_SWZ_C) % HBEC_SWZ_G;
+        const uint32_t rest = t / (HBEC_SWZ_C * HBEC_SWZ_G);
+        const uint32_t ncg = tpo / HBEC_SWZ_C;
+        const uint32_t og = rest / ncg;
+        obj = og * HBEC_SWZ_G + oi;
+        off = (uint64_t)((rest - og * ncg) * HBEC_SWZ_C + ci) * TILE;
+    }
 #pragma unroll
     for (int j = 0; j < K; ++j) b.in[j] = reinterpret_cast<uint64_t>(a.in[j]) + obj * a.in_stride[j] + off;
 #pragma unroll

@@ -57,6 +57,12 @@ VARIANTS = {
     "sl24": (["HBEC_PIPE_SLEEP=24"], {}),
     "sl32": (["HBEC_PIPE_SLEEP=32"], {}),
     "xcd1": ([], {}),
+    "g4c64": (["HBEC_SWZ_G=4", "HBEC_SWZ_C=64"], {}),
+    "g16c16": (["HBEC_SWZ_G=16", "HBEC_SWZ_C=16"], {}),
+    "g16c4": (["HBEC_SWZ_G=16", "HBEC_SWZ_C=4"], {}),
+    "g64c4": (["HBEC_SWZ_G=64", "HBEC_SWZ_C=4"], {}),
+    "g64c1": (["HBEC_SWZ_G=64", "HBEC_SWZ_C=1"], {}),
+    "g8c32": (["HBEC_SWZ_G=8", "HBEC_SWZ_C=32"], {}),
     "xcd0": (["HBEC_XCD_MAP=0"], {}),
     "prev": (["HBEC_PIPE_LOADS=16", "HBEC_PIPE_BLOCKS_PER_CU=0"], {}),
     "cur_b1": ([], {"HBEC_BLOCKS_PER_CU": "1"}),
@@ -127,6 +133,9 @@ def build(names):
         print("built", n, flush=True)
 
 
+_HOLD = []  # buffers of earlier runs (--allocs): kept so the next run's land elsewhere
+
+
 def run(names, rounds, n_obj, launches, k=4, m=2):
     import torch
 
@@ -154,11 +163,13 @@ def run(names, rounds, n_obj, launches, k=4, m=2):
         libs[n] = (h, codec)
 
     objs = torch.empty((n_obj, k * s), dtype=torch.uint8, device="cuda")
+    _HOLD.append(objs)
     h0 = libs[names[0]][0]
     stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     assert h0.hbec_fill_splitmix(C.c_void_p(objs.data_ptr()), n_obj, k * s, k * s, 0x48424543, 0, stream) == 0
     shared_p = torch.zeros((n_obj, m * s), dtype=torch.uint8, device="cuda")
     shared_r = torch.zeros((n_obj, e * s), dtype=torch.uint8, device="cuda")
+    _HOLD.extend([shared_p, shared_r])
     parity = {n: shared_p for n in names}
     rebuilt = {n: shared_r for n in names}
     ok = {n: [True, True] for n in names}
@@ -467,6 +478,9 @@ if __name__ == "__main__":
     ap.add_argument("--launches", type=int, default=5)
     ap.add_argument("--k", type=int, default=4)
     ap.add_argument("--m", type=int, default=2)
+    ap.add_argument("--allocs", type=int, default=1,
+                    help="repeat the run on this many fresh buffer sets (earlier ones stay allocated, "
+                         "so each set lands on different physical memory)")
     a = ap.parse_args()
     names = a.variants.split(",")
     if a.cmd == "build":
@@ -484,4 +498,7 @@ if __name__ == "__main__":
     elif a.cmd == "layout":
         run_layout()
     else:
-        run(names, a.rounds, a.objects, a.launches, a.k, a.m)
+        for i in range(a.allocs):
+            if a.allocs > 1:
+                print(json.dumps({"alloc_set": i}), flush=True)
+            run(names, a.rounds, a.objects, a.launches, a.k, a.m)
