@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU-box runner: each step under its own time limit; stop at the first step
 # that ends in anything but success / ordinary test failure (rc 0 or 1).
-# usage: scripts/gpu_run.sh STEP [STEP ...]   (steps: tests smoke bench prof pmc)
+# usage: scripts/gpu_run.sh STEP [STEP ...]   (steps: tests smoke bench prof pmcfetch pmcwrite cfgprof cfgpmcfetch cfgpmcwrite ...)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
@@ -38,6 +38,18 @@ for s in "$@"; do
     pmcwrite)
       mkdir -p "$OUT/pmc_write"
       (cd /tmp && step pmcwrite 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o run -- python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --no-host-path) || exit $?
+      ;;
+    cfgprof)
+      mkdir -p "$OUT/cfgprof"
+      (cd /tmp && step cfgprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/cfgprof" -o run -- python3 "$ROOT/scripts/bench_configs.py") || exit $?
+      ;;
+    cfgpmcfetch)
+      mkdir -p "$OUT/cfg_pmc_fetch"
+      (cd /tmp && step cfgpmcfetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/cfg_pmc_fetch" -o run -- python3 "$ROOT/scripts/bench_configs.py") || exit $?
+      ;;
+    cfgpmcwrite)
+      mkdir -p "$OUT/cfg_pmc_write"
+      (cd /tmp && step cfgpmcwrite 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/cfg_pmc_write" -o run -- python3 "$ROOT/scripts/bench_configs.py") || exit $?
       ;;
     dist2) step dist2 600 env HBEC_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 10 --warmup 2 --objects 2048 ;;
     configs) step configs 600 python scripts/bench_configs.py ;;

@@ -43,7 +43,7 @@ def main():
     write = per_kernel(write_dir, "WRITE_SIZE")
     kernels = {}
     for k in sorted(set(fetch) | set(write)):
-        if not k.startswith("gf_apply") and not k.startswith("fill"):
+        if not k.startswith("gf_") and not k.startswith("fill"):
             continue
         f = [v for v, _ in fetch.get(k, [])]
         w = [v for v, _ in write.get(k, [])]
