@@ -45,6 +45,7 @@ VARIANTS = {
     "sl0": (["HBEC_PIPE_SLEEP=0"], {}),
     "sl1": (["HBEC_PIPE_SLEEP=1"], {}),
     "sl2": (["HBEC_PIPE_SLEEP=2"], {}),
+    "sl3": (["HBEC_PIPE_SLEEP=3"], {}),
     "sl4": (["HBEC_PIPE_SLEEP=4"], {}),
     "sl8": (["HBEC_PIPE_SLEEP=8"], {}),
     "sl5": (["HBEC_PIPE_SLEEP=5"], {}),
