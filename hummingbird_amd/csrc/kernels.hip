@@ -282,14 +282,17 @@ __device__ __forceinline__ void pipe2_load(u32x4 (&x)[U][K], const PipeTile<K, R
 
 template <int K, int R, int U, bool FULL>
 __device__ __forceinline__ void pipe2_store_(const u32x4 (&x)[U][K], const PassArgs& a, const Tables<K, R>& tb,
-                                             const PipeTile<K, R>& b, uint32_t lane) {
+                                             const PipeTile<K, R>& b, uint32_t lane, const LdsGf<K, R>& lg) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const uint64_t off = (uint64_t)lane * 16u + (uint64_t)u * 1024u;
         u32x4 acc[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) acc[r] = u32x4{0, 0, 0, 0};
-        gf_dot<K, R>(acc, x[u], a.tab, tb);
+        if constexpr (HBEC_GF_LDS != 0)
+            gf_dot_lds<K, R>(acc, x[u], lg);
+        else
+            gf_dot<K, R>(acc, x[u], a.tab, tb);
         if (FULL || off < b.valid) {
 #pragma unroll
             for (int r = 0; r < R; ++r) st16_addr(b.out[r] + off, acc[r]);
@@ -305,6 +308,11 @@ __global__ __launch_bounds__(kPipeBlockThreads, HBEC_PIPE_WAVES_PER_SIMD) void g
     const uint32_t wave = __builtin_amdgcn_readfirstlane(xcd_block() * (kPipeBlockThreads / 64) + (threadIdx.x >> 6));
     const uint32_t tpo = a.tiles_per_obj;
     const uint32_t n = a.n_tiles;
+    LdsGf<K, R> lg{};
+    if constexpr (HBEC_GF_LDS != 0) {
+        __shared__ uint8_t lt[gf_lds_bytes(K, R)];
+        lg = gf_lds_init<K, R>(lt, a.tab);  // block-wide barrier: before any wave returns
+    }
     if (wave >= n) return;
     const Tables<K, R> tb = load_tables<K, R>(a.tab);
     PipeTile<K, R> cur, nxt;
@@ -321,9 +329,9 @@ __global__ __launch_bounds__(kPipeBlockThreads, HBEC_PIPE_WAVES_PER_SIMD) void g
         PipeTile<K, R> after;
         pipe_tile_coords<K, R, U>(after, a, t2 < n ? t2 : tn, tpo);
         if (cur.valid >= (uint32_t)U * 1024u)
-            pipe2_store_<K, R, U, true>(x, a, tb, cur, lane);
+            pipe2_store_<K, R, U, true>(x, a, tb, cur, lane, lg);
         else
-            pipe2_store_<K, R, U, false>(x, a, tb, cur, lane);
+            pipe2_store_<K, R, U, false>(x, a, tb, cur, lane, lg);
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -332,9 +340,9 @@ __global__ __launch_bounds__(kPipeBlockThreads, HBEC_PIPE_WAVES_PER_SIMD) void g
         nxt = after;
     }
     if (cur.valid >= (uint32_t)U * 1024u)
-        pipe2_store_<K, R, U, true>(x, a, tb, cur, lane);
+        pipe2_store_<K, R, U, true>(x, a, tb, cur, lane, lg);
     else
-        pipe2_store_<K, R, U, false>(x, a, tb, cur, lane);
+        pipe2_store_<K, R, U, false>(x, a, tb, cur, lane, lg);
 }
 
 // Streaming vec path (runtime K): one input shard at a time with the next

@@ -58,6 +58,8 @@ VARIANTS = {
     "sl24": (["HBEC_PIPE_SLEEP=24"], {}),
     "sl32": (["HBEC_PIPE_SLEEP=32"], {}),
     "xcd1": ([], {}),
+    "lds_prod": (["HBEC_GF_LDS=1"], {}),
+    "lds_log": (["HBEC_GF_LDS=2"], {}),
     "g4c64": (["HBEC_SWZ_G=4", "HBEC_SWZ_C=64"], {}),
     "g16c16": (["HBEC_SWZ_G=16", "HBEC_SWZ_C=16"], {}),
     "g16c4": (["HBEC_SWZ_G=16", "HBEC_SWZ_C=4"], {}),
