@@ -72,7 +72,7 @@ def max_over_ranks(pg, values, device):
     return t.tolist()
 
 
-def load_pmc(prefix_glob="profiles/*_pmc.json"):
+def load_pmc(prefix_glob="profiles/r[0-9][0-9]_pmc.json"):
     files = sorted(glob.glob(str(ROOT / prefix_glob)))
     if not files:
         return None, None
