@@ -7,12 +7,19 @@
 // the GPU a single 1 MiB encode is dominated by launch + PCIe latency, so this
 // driver lets concurrent callers share launches: each caller submits one host
 // stripe (ecSplit databuf layout) and blocks; a worker thread takes everything
-// queued — up to max_batch_bytes, or whatever has arrived when max_wait_us
-// passes after the oldest request — codes it with one streaming host-path
-// call (hostpath.cpp), and wakes the callers.
+// queued — up to its share of max_batch_bytes, or whatever has arrived when
+// max_wait_us passes after it started waiting — codes it with one streaming
+// host-path call (hostpath.cpp), and wakes the callers.
+//
+// Several workers (HBEC_BATCHER_WORKERS, default 2) split max_batch_bytes
+// between them, so one batch's callers can wake up and queue their next
+// stripes while another batch is on the GPU: the per-batch wake-up, fill and
+// launch overheads overlap the other batch's transfer.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <condition_variable>
 #include <deque>
@@ -37,6 +44,10 @@ struct Request {
     int data_only = 0;
     int rc = HBEC_OK;
     std::string err;
+    // completion: each caller sleeps on its own condition variable, so a
+    // finished batch wakes exactly its callers (not every queued one)
+    std::mutex m;
+    std::condition_variable cv;
     bool done = false;
 };
 
@@ -48,10 +59,11 @@ struct hbec_batcher {
     uint64_t max_batch_bytes = 0;
     std::chrono::microseconds max_wait{0};
     std::mutex mu;
-    std::condition_variable cv_work, cv_done;
+    std::condition_variable cv_work;
     std::deque<Request*> queue;
     bool stop = false;
-    std::thread worker;
+    uint64_t batch_cap = 0;  // bytes one worker takes per batch: max_batch_bytes / workers
+    std::vector<std::thread> workers;
     // statistics
     uint64_t batches = 0, stripes = 0;
 
@@ -67,9 +79,10 @@ struct hbec_batcher {
             while (!stop) {
                 uint64_t queued = 0;
                 for (auto* r : queue) queued += r->stripe.shard_len * (uint64_t)n_shards;
-                if (queued >= max_batch_bytes) break;
+                if (queued >= batch_cap) break;
                 if (cv_work.wait_until(lk, deadline) == std::cv_status::timeout) break;
             }
+            if (queue.empty()) continue;  // another worker took it while this one waited
             // take one homogeneous group (same op and erasure pattern) from the front
             std::vector<Request*> batch;
             uint64_t bytes = 0;
@@ -79,7 +92,7 @@ struct hbec_batcher {
                                        r->data_only != batch[0]->data_only))
                     break;
                 const uint64_t b = r->stripe.shard_len * (uint64_t)n_shards;
-                if (!batch.empty() && bytes + b > max_batch_bytes) break;
+                if (!batch.empty() && bytes + b > batch_cap) break;
                 batch.push_back(r);
                 bytes += b;
                 queue.pop_front();
@@ -99,24 +112,30 @@ struct hbec_batcher {
             } else
                 rc = hbec_reconstruct_host(codec, st.data(), st.size(), batch[0]->present.data(), batch[0]->data_only);
             const std::string err = rc ? hbec_last_error() : "";
-            lk.lock();
-            ++batches;
-            stripes += batch.size();
             for (auto* r : batch) {
+                // notify while holding r->m: the caller cannot see `done`, return and
+                // destroy r (it lives on the caller's stack) before this scope ends
+                std::lock_guard<std::mutex> g(r->m);
                 r->rc = rc;
                 r->err = err;
                 r->done = true;
+                r->cv.notify_one();
             }
-            cv_done.notify_all();
+            lk.lock();
+            ++batches;
+            stripes += batch.size();
         }
     }
 
     int submit(Request& r) {
-        std::unique_lock<std::mutex> lk(mu);
-        if (stop) return fail(HBEC_ERR_INVALID_ARG, "batcher stopped");
-        queue.push_back(&r);
-        cv_work.notify_one();
-        cv_done.wait(lk, [&] { return r.done; });
+        {
+            std::lock_guard<std::mutex> g(mu);
+            if (stop) return fail(HBEC_ERR_INVALID_ARG, "batcher stopped");
+            queue.push_back(&r);
+        }
+        cv_work.notify_all();  // a worker filling its batch re-checks the size; an idle one starts
+        std::unique_lock<std::mutex> lk(r.m);
+        r.cv.wait(lk, [&] { return r.done; });
         return r.rc ? fail(r.rc, r.err) : HBEC_OK;
     }
 };
@@ -135,8 +154,11 @@ int hbec_batcher_new(hbec_codec* codec, uint64_t max_batch_bytes, uint32_t max_w
         b->codec = codec;
         b->max_batch_bytes = max_batch_bytes ? max_batch_bytes : (256ull << 20);
         b->max_wait = std::chrono::microseconds(max_wait_us);
+        const char* env = std::getenv("HBEC_BATCHER_WORKERS");
+        const int n_workers = std::min(8, std::max(1, env ? std::atoi(env) : 2));
+        b->batch_cap = std::max<uint64_t>(1, b->max_batch_bytes / (uint64_t)n_workers);
         hbec_batcher* raw = b.get();
-        b->worker = std::thread([raw] { raw->run(); });
+        for (int w = 0; w < n_workers; ++w) b->workers.emplace_back([raw] { raw->run(); });
         *out = b.release();
         return HBEC_OK;
     });
@@ -149,7 +171,7 @@ void hbec_batcher_free(hbec_batcher* b) {
         b->stop = true;
     }
     b->cv_work.notify_all();
-    b->worker.join();
+    for (auto& w : b->workers) w.join();
     delete b;
 }
 

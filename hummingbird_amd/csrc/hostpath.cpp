@@ -57,6 +57,7 @@ constexpr int kSlots = 3;
 
 struct Ring {
     int dev = -1;
+    int cus = 0;  // compute units of dev (grid sizing), read once
     size_t in_cap = 0, out_cap = 0, tile_cap = 0;
     hipStream_t s_h2d = nullptr, s_cmp = nullptr, s_d2h = nullptr;
     uint8_t* pin_in[kSlots] = {};
@@ -115,6 +116,12 @@ size_t env_size(const char* name, size_t dflt) {
 
 int ring_init(Ring& r, int dev) {
     r.dev = dev;
+    {
+        hipDeviceProp_t prop;
+        hipError_t pe = hipGetDeviceProperties(&prop, dev);
+        if (pe != hipSuccess) return hip_fail(pe, "hipGetDeviceProperties");
+        r.cus = prop.multiProcessorCount;
+    }
     const size_t slot = env_size("HBEC_HOST_SLOT_MB", 64) << 20;  // IN bytes per slot
     r.in_cap = slot;
     r.out_cap = slot;  // outputs per piece <= inputs (R <= K) except tiny K: sized below per call
@@ -129,20 +136,31 @@ int ring_init(Ring& r, int dev) {
     HB_CHECK(hipStreamCreateWithFlags(&r.s_cmp, hipStreamNonBlocking), "stream");
     HB_CHECK(hipStreamCreateWithFlags(&r.s_d2h, hipStreamNonBlocking), "stream");
     for (int i = 0; i < kSlots; ++i) {
-        HB_CHECK(hipHostMalloc(reinterpret_cast<void**>(&r.pin_in[i]), r.in_cap, hipHostMallocDefault), "pinned in");
-        HB_CHECK(hipHostMalloc(reinterpret_cast<void**>(&r.pin_out[i]), r.out_cap, hipHostMallocDefault),
-                 "pinned out");
         HB_CHECK(hipHostMalloc(reinterpret_cast<void**>(&r.pin_tiles[i]), r.tile_cap * sizeof(hbec::TileRec),
                                hipHostMallocDefault),
                  "pinned tiles");
-        HB_CHECK(hipMalloc(&r.dev_in[i], r.in_cap), "device in");
-        HB_CHECK(hipMalloc(&r.dev_out[i], r.out_cap), "device out");
         HB_CHECK(hipMalloc(&r.dev_tiles[i], r.tile_cap * sizeof(hbec::TileRec)), "device tiles");
         HB_CHECK(hipEventCreateWithFlags(&r.ev_h2d[i], hipEventDisableTiming), "event");
         HB_CHECK(hipEventCreateWithFlags(&r.ev_cmp[i], hipEventDisableTiming), "event");
         HB_CHECK(hipEventCreateWithFlags(&r.ev_done[i], hipEventDisableTiming), "event");
     }
 #undef HB_CHECK
+    return HBEC_OK;
+}
+
+// The staging slots and copy threads, made on the first call that stages
+// (zero-copy calls only need the tile records).
+int ring_staging_init(Ring& r) {
+    if (r.pool) return HBEC_OK;  // set last: everything below exists
+    hipError_t e = hipSuccess;
+    for (int i = 0; i < kSlots && e == hipSuccess; ++i) {  // a failed earlier attempt keeps what it got
+        if (!r.pin_in[i]) e = hipHostMalloc(reinterpret_cast<void**>(&r.pin_in[i]), r.in_cap, hipHostMallocDefault);
+        if (e == hipSuccess && !r.pin_out[i])
+            e = hipHostMalloc(reinterpret_cast<void**>(&r.pin_out[i]), r.out_cap, hipHostMallocDefault);
+        if (e == hipSuccess && !r.dev_in[i]) e = hipMalloc(&r.dev_in[i], r.in_cap);
+        if (e == hipSuccess && !r.dev_out[i]) e = hipMalloc(&r.dev_out[i], r.out_cap);
+    }
+    if (e != hipSuccess) return hip_fail(e, "staging slots");
     r.pool.reset(new hbec::Pool(hbec::host_threads() - 1));  // + the calling thread
     return HBEC_OK;
 }
@@ -362,16 +380,15 @@ int host_run(const hbec_stripe* stripes, uint64_t n, const std::vector<int>& in_
             else staged.push_back(stripes[s]);
         }
         if (!zs.empty()) {
-            hipDeviceProp_t prop;
-            hipError_t e = hipGetDeviceProperties(&prop, ring->dev);
-            if (e != hipSuccess) return hip_fail(e, "hipGetDeviceProperties");
-            rc = zero_copy_run(ring, zs, in_idx, out_idx, rows, prop.multiProcessorCount);
+            rc = zero_copy_run(ring, zs, in_idx, out_idx, rows, ring->cus);
             if (rc) return rc;
         }
         if (staged.empty()) return HBEC_OK;
         stripes = staged.data();
         n = staged.size();
     }
+    rc = ring_staging_init(*ring);
+    if (rc) return rc;
     const uint64_t tile = (uint64_t)hbec::stripes_tile_bytes(K);
     // max columns per piece so that K*lpad fits the IN slot and R*lpad the OUT slot
     const uint64_t max_cols = (std::min(ring->in_cap / K, ring->out_cap / R) / 16) * 16;
@@ -449,13 +466,7 @@ int host_run(const hbec_stripe* stripes, uint64_t n, const std::vector<int>& in_
         rg.push_back(Rg);
         args.push_back(a);
     }
-    int cus = 0;
-    {
-        hipDeviceProp_t prop;
-        hipError_t e = hipGetDeviceProperties(&prop, ring->dev);
-        if (e != hipSuccess) return hip_fail(e, "hipGetDeviceProperties");
-        cus = prop.multiProcessorCount;
-    }
+    const int cus = ring->cus;
 
     std::vector<int64_t> slot_chunk(kSlots, -1);
     auto scatter = [&](int slot) -> int {

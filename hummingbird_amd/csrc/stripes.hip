@@ -14,6 +14,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
 #include "gf_device.h"
 #include "kernels.h"
 
@@ -163,9 +165,19 @@ hipError_t launch_stripes(int k, int r, const StripeArgs& a, int grid, hipStream
 }
 
 hipError_t stripes_occupancy(int k, int r, int* blocks_per_cu) {
+    // per (k, r), asked of the runtime once: the host paths size a grid per chunk
+    static std::atomic<int> cache[kMaxK + 1][kMaxR + 1] = {};
+    if (k < 1 || k > kMaxK || r < 1 || r > kMaxR) return hipErrorInvalidValue;
+    const int hit = cache[k][r].load(std::memory_order_relaxed);
+    if (hit > 0) {
+        *blocks_per_cu = hit;
+        return hipSuccess;
+    }
     const void* fn = stripes_kernel(k, r);
     if (!fn) return hipErrorInvalidValue;
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, kBlockThreads, 0);
+    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, kBlockThreads, 0);
+    if (e == hipSuccess && *blocks_per_cu > 0) cache[k][r].store(*blocks_per_cu, std::memory_order_relaxed);
+    return e;
 }
 
 }  // namespace hbec

@@ -245,10 +245,12 @@ int hbec_reconstruct_host_devices(hbec_codec* codec, const hbec_stripe* stripes,
 int hbec_encode_host_md5(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n_stripes, uint8_t* digests);
 
 /* Batching driver for concurrent callers (e.g. one cgo call per Stabilize):
- * each call submits ONE host stripe and blocks until it is coded; a worker
- * thread codes everything queued — up to max_batch_bytes (0 = 256 MiB), or
- * what has arrived max_wait_us after the oldest request — with one host-path
- * call.  Requests with different ops / erasure patterns form separate
+ * each call submits ONE host stripe and blocks until it is coded; worker
+ * threads (HBEC_BATCHER_WORKERS, default 2) each code what is queued — up to
+ * max_batch_bytes / workers (max_batch_bytes 0 = 256 MiB; stripe bytes =
+ * (k+m) * shard_len), or what has arrived max_wait_us after the worker
+ * started waiting — with one host-path call, so up to max_batch_bytes are in
+ * flight.  Requests with different ops / erasure patterns form separate
  * batches.  k <= 8.  The codec must outlive the batcher. */
 typedef struct hbec_batcher hbec_batcher;
 int hbec_batcher_new(hbec_codec* codec, uint64_t max_batch_bytes, uint32_t max_wait_us, hbec_batcher** out);
