@@ -803,3 +803,59 @@ def test_batcher_concurrent_callers_share_launches():
         t.join()
     assert all(np.array_equal(a, b) for a, b in zip(damaged, want))
     bat.close()
+
+
+@pytest.mark.parametrize("workers", ["1", "3"])
+def test_batcher_mixed_ops_and_patterns_concurrently(monkeypatch, workers):
+    """Encodes and reconstructs with three erasure patterns (data-only and
+    full) in flight at once: every batch must be one homogeneous group, and
+    every caller must get exactly its own result, whatever the worker count."""
+    import threading
+
+    monkeypatch.setenv("HBEC_BATCHER_WORKERS", workers)
+    k, m = 4, 2
+    enc = RS.New(k, m)
+    bat = RS.Batcher(enc, max_batch_bytes=24 << 20, max_wait_us=500)
+    sizes = [MiB if i % 4 else 4096 + 16 * i for i in range(60)]
+    stripes = _host_stripes(k, m, sizes, seed=91)
+    want = _encoded_copy(k, m, stripes)
+    patterns = [([0, 1, 1, 1, 1, 1], False), ([1, 1, 0, 1, 0, 1], False), ([0, 1, 1, 0, 1, 1], True)]
+    jobs = []
+    for i, w in enumerate(want):
+        if i % 4 == 0:
+            jobs.append(("enc", stripes[i], None, False))
+            continue
+        present, data_only = patterns[i % 3]
+        d = w.copy()
+        s = d.size // (k + m)
+        for j, p in enumerate(present):
+            if not p:
+                d[j * s:(j + 1) * s] = 0
+        jobs.append(("rec", d, present, data_only))
+    errors = []
+
+    def run(job):
+        op, buf, present, data_only = job
+        try:
+            if op == "enc":
+                bat.Encode(buf)
+            else:
+                bat.Reconstruct(buf, present, data_only=data_only)
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(e)
+
+    threads = [threading.Thread(target=run, args=(j,)) for j in jobs]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    assert not errors
+    for (op, buf, present, data_only), w in zip(jobs, want):
+        if op == "enc" or not data_only:
+            assert np.array_equal(buf, w)
+        else:  # data-only: the data shards are rebuilt, missing parity stays as it was (zeroed)
+            s = w.size // (k + m)
+            assert np.array_equal(buf[:k * s], w[:k * s])
+    st = bat.stats()
+    assert st["stripes"] == len(jobs)
+    bat.close()
