@@ -50,6 +50,11 @@ static const int g_blocks_per_cu_override = [] {
     const char* e = std::getenv("HBEC_BLOCKS_PER_CU");
     return e ? std::atoi(e) : 0;
 }();
+// Tuning knob: absolute cap on vec-kernel grids (0 = none), to run fewer CUs.
+static const int g_grid_cap = [] {
+    const char* e = std::getenv("HBEC_GRID_CAP");
+    return e ? std::atoi(e) : 0;
+}();
 
 // ---------------------------------------------------------------------------
 // Per-device facts (CU count, occupancy per kernel shape)
@@ -158,7 +163,8 @@ int apply_views(int rows, int cols, const uint8_t* coeffs, const hbec_view* in, 
                     const uint64_t cap = (uint64_t)cus * (uint64_t)(g_blocks_per_cu_override > 0
                                                                          ? g_blocks_per_cu_override
                                                                          : per_cu);
-                    const int grid = (int)std::max<uint64_t>(1, std::min(want_blocks, cap));
+                    int grid = (int)std::max<uint64_t>(1, std::min(want_blocks, cap));
+                    if (g_grid_cap > 0) grid = std::min(grid, g_grid_cap);
                     hipError_t e = launch_vec(K, R, b, grid, stream, force_stream);
                     if (e != hipSuccess) return hip_fail(e, "launch gf_apply_vec");
                 }

@@ -58,6 +58,11 @@ VARIANTS = {
     "sl24": (["HBEC_PIPE_SLEEP=24"], {}),
     "sl32": (["HBEC_PIPE_SLEEP=32"], {}),
     "xcd1": ([], {}),
+    "gc248": ([], {"HBEC_GRID_CAP": "248"}),
+    "gc240": ([], {"HBEC_GRID_CAP": "240"}),
+    "gc224": ([], {"HBEC_GRID_CAP": "224"}),
+    "gc192": ([], {"HBEC_GRID_CAP": "192"}),
+    "gc160": ([], {"HBEC_GRID_CAP": "160"}),
     "lds_prod": (["HBEC_GF_LDS=1"], {}),
     "lds_log": (["HBEC_GF_LDS=2"], {}),
     "g4c64": (["HBEC_SWZ_G=4", "HBEC_SWZ_C=64"], {}),
