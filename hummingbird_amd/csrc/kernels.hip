@@ -233,7 +233,7 @@ template <int K, int R>
 struct PipeTile {
     uint64_t in[K];
     uint64_t out[R];
-    uint32_t valid;
+    uint32_t valid;  // bytes of the tile inside the shard
 };
 
 // Tuning knob (tile order): with HBEC_SWZ_G > 0, runs of HBEC_SWZ_C tiles
@@ -300,12 +300,49 @@ __device__ __forceinline__ void pipe2_store_(const u32x4 (&x)[U][K], const PassA
     }
 }
 
+// Tile t of the launch; past the end, the launch's last tile stands in: it is
+// loaded, coded and stored again with the same bytes its owner stores (the
+// outputs never alias the inputs).  No branch around loads or stores: a
+// memory op under a branch makes the compiler drain everything in flight
+// (vmcnt(0)) at the join, which serialises the pipeline (measured 2x slower).
+template <int K, int R, int U>
+__device__ __forceinline__ void pipe_tile_at(PipeTile<K, R>& b, const PassArgs& a, uint32_t t, uint32_t n,
+                                             uint32_t tpo) {
+    pipe_tile_coords<K, R, U>(b, a, t < n ? t : n - 1u, tpo);
+}
+
+template <int K, int R, int U>
+__device__ __forceinline__ void pipe2_finish(const u32x4 (&x)[U][K], const PassArgs& a, const Tables<K, R>& tb,
+                                             const PipeTile<K, R>& cur, uint32_t lane, const LdsGf<K, R>& lg) {
+    if (cur.valid >= (uint32_t)U * 1024u)
+        pipe2_store_<K, R, U, true>(x, a, tb, cur, lane, lg);
+    else
+        pipe2_store_<K, R, U, false>(x, a, tb, cur, lane, lg);
+}
+
+// Block barrier once per tile, after the next tile's loads are issued and the
+// pacing sleep: the block's 4 waves (one per SIMD) then issue their loads and
+// stores in step.  With s_sleep 8: +1.1-1.3 % over the barrier-free loop
+// with s_sleep 6, on each of three allocations (profiles/r01_tune_barrier.jsonl).  Every wave of a block runs
+// the same number of iterations (the loop bound is the block's first wave's
+// tile; a wave past the end re-codes the last tile), so the barrier counts
+// always match.
+#ifndef HBEC_PIPE_BARRIER
+#define HBEC_PIPE_BARRIER 1
+#endif
+#ifndef HBEC_PIPE2_SLEEP
+#define HBEC_PIPE2_SLEEP 8  // x 64 cycles, K <= 4
+#endif
+
 template <int K, int R>
 __global__ __launch_bounds__(kPipeBlockThreads, HBEC_PIPE_WAVES_PER_SIMD) void gf_apply_vec_pipe2(PassArgs a) {
     constexpr int U = pipe_u(K);
+    constexpr uint32_t WPB = kPipeBlockThreads / 64;
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t nw = gridDim.x * (kPipeBlockThreads / 64);
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(xcd_block() * (kPipeBlockThreads / 64) + (threadIdx.x >> 6));
+    const uint32_t nw = gridDim.x * WPB;
+    const uint32_t wave0 = __builtin_amdgcn_readfirstlane(xcd_block() * WPB);  // the block's first wave
+    const uint32_t dw = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t wave = wave0 + dw;
     const uint32_t tpo = a.tiles_per_obj;
     const uint32_t n = a.n_tiles;
     LdsGf<K, R> lg{};
@@ -313,25 +350,21 @@ __global__ __launch_bounds__(kPipeBlockThreads, HBEC_PIPE_WAVES_PER_SIMD) void g
         __shared__ uint8_t lt[gf_lds_bytes(K, R)];
         lg = gf_lds_init<K, R>(lt, a.tab);  // block-wide barrier: before any wave returns
     }
-    if (wave >= n) return;
+    if (wave0 >= n) return;  // whole blocks only: the loop below has block barriers
     const Tables<K, R> tb = load_tables<K, R>(a.tab);
     PipeTile<K, R> cur, nxt;
-    pipe_tile_coords<K, R, U>(cur, a, wave, tpo);
+    pipe_tile_at<K, R, U>(cur, a, wave, n, tpo);
     u32x4 x[U][K];
     pipe2_load<K, R, U>(x, cur, lane);
-    uint32_t tn = wave + nw;
-    pipe_tile_coords<K, R, U>(nxt, a, tn < n ? tn : wave, tpo);
-    for (; tn < n; tn += nw) {
+    pipe_tile_at<K, R, U>(nxt, a, wave + nw, n, tpo);
+    for (uint32_t b0 = wave0 + nw; b0 < n; b0 += nw) {  // block-uniform trip count
         u32x4 y[U][K];
         pipe2_load<K, R, U>(y, nxt, lane);
-        if (HBEC_PIPE_SLEEP > 0 && K <= 4) __builtin_amdgcn_s_sleep(HBEC_PIPE_SLEEP);
-        const uint32_t t2 = tn + nw;
+        if (HBEC_PIPE2_SLEEP > 0 && K <= 4) __builtin_amdgcn_s_sleep(HBEC_PIPE2_SLEEP);
+        if (HBEC_PIPE_BARRIER) __builtin_amdgcn_s_barrier();
         PipeTile<K, R> after;
-        pipe_tile_coords<K, R, U>(after, a, t2 < n ? t2 : tn, tpo);
-        if (cur.valid >= (uint32_t)U * 1024u)
-            pipe2_store_<K, R, U, true>(x, a, tb, cur, lane, lg);
-        else
-            pipe2_store_<K, R, U, false>(x, a, tb, cur, lane, lg);
+        pipe_tile_at<K, R, U>(after, a, b0 + dw + nw, n, tpo);
+        pipe2_finish<K, R, U>(x, a, tb, cur, lane, lg);
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -339,10 +372,7 @@ __global__ __launch_bounds__(kPipeBlockThreads, HBEC_PIPE_WAVES_PER_SIMD) void g
         cur = nxt;
         nxt = after;
     }
-    if (cur.valid >= (uint32_t)U * 1024u)
-        pipe2_store_<K, R, U, true>(x, a, tb, cur, lane, lg);
-    else
-        pipe2_store_<K, R, U, false>(x, a, tb, cur, lane, lg);
+    pipe2_finish<K, R, U>(x, a, tb, cur, lane, lg);
 }
 
 // Streaming vec path (runtime K): one input shard at a time with the next

@@ -58,6 +58,17 @@ VARIANTS = {
     "sl24": (["HBEC_PIPE_SLEEP=24"], {}),
     "sl32": (["HBEC_PIPE_SLEEP=32"], {}),
     "xcd1": ([], {}),
+    "head": ([], {}),  # built by hand from the previous commit's kernels.hip
+    "p2old": (["HBEC_PIPE_BARRIER=0", "HBEC_PIPE2_SLEEP=6"], {}),
+    "p2nobar8": (["HBEC_PIPE_BARRIER=0", "HBEC_PIPE2_SLEEP=8"], {}),
+    "p2bar6": (["HBEC_PIPE2_SLEEP=6"], {}),
+    "p2bar10": (["HBEC_PIPE2_SLEEP=10"], {}),
+    "p2bar12": (["HBEC_PIPE2_SLEEP=12"], {}),
+    "bar": (["HBEC_PIPE_BARRIER=1"], {}),
+    "bar_sl0": (["HBEC_PIPE_BARRIER=1", "HBEC_PIPE_SLEEP=0"], {}),
+    "bar_sl3": (["HBEC_PIPE_BARRIER=1", "HBEC_PIPE_SLEEP=3"], {}),
+    "bar_sl8": (["HBEC_PIPE_BARRIER=1", "HBEC_PIPE_SLEEP=8"], {}),
+    "bar2": (["HBEC_PIPE_BARRIER=1"], {}),
     "gc248": ([], {"HBEC_GRID_CAP": "248"}),
     "gc240": ([], {"HBEC_GRID_CAP": "240"}),
     "gc224": ([], {"HBEC_GRID_CAP": "224"}),
