@@ -53,9 +53,12 @@ int vec_block_threads(int k, int r, uint64_t shard_len, int accumulate, int forc
 #ifndef HBEC_PIPE_LOADS
 #define HBEC_PIPE_LOADS 0
 #endif
+#ifndef HBEC_PIPE_U_BIG
+#define HBEC_PIPE_U_BIG 3  // KiB per input per wave tile for 5 <= K <= 8
+#endif
 __host__ __device__ constexpr int pipe_u(int k) {
     if (HBEC_PIPE_LOADS > 0) return k >= HBEC_PIPE_LOADS ? 1 : (HBEC_PIPE_LOADS / k > 4 ? 4 : HBEC_PIPE_LOADS / k);
-    return k <= 4 ? (4 / k) : (k <= 8 ? 3 : 1);
+    return k <= 4 ? (4 / k) : (k <= 8 ? HBEC_PIPE_U_BIG : 1);
 }
 
 // Tile depth of the stripe-plan and verify kernels, from A/B runs on MI355X

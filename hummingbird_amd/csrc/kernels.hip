@@ -333,6 +333,9 @@ __device__ __forceinline__ void pipe2_finish(const u32x4 (&x)[U][K], const PassA
 #ifndef HBEC_PIPE2_SLEEP
 #define HBEC_PIPE2_SLEEP 8  // x 64 cycles, K <= 4
 #endif
+#ifndef HBEC_PIPE2_SLEEP_BIG
+#define HBEC_PIPE2_SLEEP_BIG 0  // x 64 cycles, K > 4
+#endif
 
 template <int K, int R>
 __global__ __launch_bounds__(kPipeBlockThreads, HBEC_PIPE_WAVES_PER_SIMD) void gf_apply_vec_pipe2(PassArgs a) {
@@ -361,6 +364,7 @@ __global__ __launch_bounds__(kPipeBlockThreads, HBEC_PIPE_WAVES_PER_SIMD) void g
         u32x4 y[U][K];
         pipe2_load<K, R, U>(y, nxt, lane);
         if (HBEC_PIPE2_SLEEP > 0 && K <= 4) __builtin_amdgcn_s_sleep(HBEC_PIPE2_SLEEP);
+        if (HBEC_PIPE2_SLEEP_BIG > 0 && K > 4) __builtin_amdgcn_s_sleep(HBEC_PIPE2_SLEEP_BIG);
         if (HBEC_PIPE_BARRIER) __builtin_amdgcn_s_barrier();
         PipeTile<K, R> after;
         pipe_tile_at<K, R, U>(after, a, b0 + dw + nw, n, tpo);

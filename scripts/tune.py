@@ -34,6 +34,12 @@ VARIANTS = {
     "v2": (["HBEC_PIPE_V2=1"], {}),
     "v2all": (["HBEC_PIPE_V2_MAXK=16"], {}),
     "v2all_l16": (["HBEC_PIPE_V2_MAXK=16", "HBEC_PIPE_LOADS=16"], {}),
+    "v2all_nobar": (["HBEC_PIPE_V2_MAXK=16", "HBEC_PIPE_BARRIER=0"], {}),
+    "v2u2": (["HBEC_PIPE_V2_MAXK=16", "HBEC_PIPE_U_BIG=2"], {}),
+    "v2u1": (["HBEC_PIPE_V2_MAXK=16", "HBEC_PIPE_U_BIG=1"], {}),
+    "v2u2s4": (["HBEC_PIPE_V2_MAXK=16", "HBEC_PIPE_U_BIG=2", "HBEC_PIPE2_SLEEP_BIG=4"], {}),
+    "v2u2s8": (["HBEC_PIPE_V2_MAXK=16", "HBEC_PIPE_U_BIG=2", "HBEC_PIPE2_SLEEP_BIG=8"], {}),
+    "v2u1s8": (["HBEC_PIPE_V2_MAXK=16", "HBEC_PIPE_U_BIG=1", "HBEC_PIPE2_SLEEP_BIG=8"], {}),
     "v2all_l24": (["HBEC_PIPE_V2_MAXK=16", "HBEC_PIPE_LOADS=24"], {}),
     "v1_l16": (["HBEC_PIPE_LOADS=16"], {}),
     "v2s0": (["HBEC_PIPE_V2=1", "HBEC_PIPE_SLEEP=0"], {}),
