@@ -20,16 +20,27 @@ max-time reduction.
 Extra objects on the JSON line: `roofline` (dominant kernel = the
 gf_apply_vec_pipe2<4,2> kernel that both ops launch; achieved = algorithmic bytes per
 launch / its HIP-event-timed average launch duration on the launch stream;
-traffic = PMC HBM bytes per launch from the committed rocprofv3 summary,
-profiles/*_pmc.json) and `cpu_baseline` (oracle/gf_oracle.c's AVX2 port of
-klauspost's algorithm over the host cores on a bounded sample, rank 0 at N=1).
+traffic = PMC HBM bytes per launch from the committed rocprofv3 summary
+profiles/*_pmc.json, used only when that file was collected on the kernel
+sources being run -- same sha256 -- else null), `cpu_baseline`
+(oracle/gf_oracle.c's AVX2 port of klauspost's algorithm over the host cores
+on a bounded sample, rank 0 at N=1) and `config5` (BASELINE configs[4]: a
+65 536 x 1 MiB 4+2 batch partitioned contiguously over the N ranks, encoded
+device-resident, at every N including 1).
+
+`--gpus N` without a launcher (WORLD_SIZE unset) starts N rank processes
+itself through torch.distributed.run, before this process touches the GPU;
+a launcher whose WORLD_SIZE differs from --gpus is refused.
 """
 from __future__ import annotations
 
 import argparse
 import glob
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -72,12 +83,34 @@ def max_over_ranks(pg, values, device):
     return t.tolist()
 
 
+# Sources whose compiled code the dominant kernel is (gf_apply_vec_pipe2 and
+# its device helpers): a PMC summary is only reported as this run's traffic
+# when it was collected on exactly these sources.
+KERNEL_SOURCES = ("hummingbird_amd/csrc/kernels.hip", "hummingbird_amd/csrc/gf_device.h",
+                  "hummingbird_amd/csrc/kernels.h")
+
+
+def kernel_sources_sha256() -> str:
+    h = hashlib.sha256()
+    for rel in KERNEL_SOURCES:
+        h.update(rel.encode())
+        h.update((ROOT / rel).read_bytes())
+    return h.hexdigest()
+
+
 def load_pmc(prefix_glob="profiles/r[0-9][0-9]_pmc.json"):
+    """Latest committed PMC summary, if it was collected on the kernel
+    sources of this tree; (data, path, reason_if_rejected)."""
     files = sorted(glob.glob(str(ROOT / prefix_glob)))
     if not files:
-        return None, None
+        return None, None, "no PMC summary under profiles/"
     data = json.loads(Path(files[-1]).read_text())
-    return data, os.path.relpath(files[-1], ROOT)
+    rel = os.path.relpath(files[-1], ROOT)
+    want = kernel_sources_sha256()
+    got = data.get("kernel_sources_sha256")
+    if got != want:
+        return None, rel, f"stale: {rel} was collected on kernel sources {str(got)[:12]}, this tree is {want[:12]}"
+    return data, rel, None
 
 
 class Workload:
@@ -235,6 +268,68 @@ def batch_split(pg, k, m, obj_len, n_global, world, rank, ctl_device):
     }
 
 
+def config5(pg, k, m, obj_len, n_global, world, rank, ctl_device, reps=3):
+    """BASELINE configs[4] at this N: n_global objects partitioned
+    contiguously over the ranks (rank r owns SP.object_range(n_global, world,
+    r)), each rank's partition generated in and encoded from its own HBM (no
+    data-path collective: objects are independent, ecutils.go:38-70).  At
+    N=1 that is 64 GiB of objects + 32 GiB of parity on one GPU.  `reps`
+    encodes of the whole partition are timed between barriers; the parity is
+    then checked on the GPU by Encoder.Verify (gf_verify_pipe, a different
+    kernel from the encoder)."""
+    s = obj_len // k
+    first, n = SP.object_range(n_global, world, rank)
+    enc = RS.New(k, m)
+    objs = parity = flags = None
+    err = ""
+    try:
+        objs = torch.empty((n, obj_len), dtype=torch.uint8, device="cuda")
+        parity = torch.empty((n, m * s), dtype=torch.uint8, device="cuda")
+        flags = torch.zeros(n, dtype=torch.int32, device="cuda")
+        B.fill_splitmix(objs, obj_len, first=first)
+        torch.cuda.synchronize()
+    except Exception as e:  # noqa: BLE001 - reported; every rank skips together
+        err = f"rank {rank}: {type(e).__name__}: {e}"[:200]
+    (failed,) = max_over_ranks(pg, [1.0 if err else 0.0], ctl_device)
+    if failed:
+        return {"skipped": err or "allocation failed on another rank", "objects": n_global}
+    B.encode_objects(enc, objs, parity, s)  # warm-up
+    stream = torch.cuda.current_stream()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    if pg:
+        pg.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for e0, e1 in ev:
+        e0.record(stream)
+        B.encode_objects(enc, objs, parity, s)
+        e1.record(stream)
+    torch.cuda.synchronize()
+    if pg:
+        pg.barrier()
+    elapsed = time.perf_counter() - t0
+    launch_ms = sum(a.elapsed_time(b) for a, b in ev) / reps
+    B.verify_views(enc, B.shard_views(objs, k, s) + B.shard_views(parity, m, s), n, s, flags)
+    bad = float(int(flags.count_nonzero().item()))
+    elapsed, launch_ms, bad = max_over_ranks(pg, [elapsed, launch_ms, bad], ctl_device)
+    del objs, parity, flags
+    torch.cuda.empty_cache()
+    n_max = SP.object_range(n_global, world, 0)[1]
+    per_gpu_gbs = n_max * (k + m) * s / (launch_ms * 1e-3) / 1e9
+    return {
+        "workload": f"{k}+{m} Encode of {n_global} x {obj_len >> 20} MiB objects partitioned contiguously over "
+                    f"{world} GPU(s) (BASELINE configs[4]), device-resident",
+        "objects": n_global, "objects_per_gpu_max": n_max, "reps": reps,
+        "ms": round(elapsed / reps * 1e3, 3),
+        "value_GiB_s": round(n_global * (k + m) * s * reps / elapsed / GiB, 2),
+        "per_gpu_launch_ms_max": round(launch_ms, 3),
+        "per_gpu_roofline": {"achieved": round(per_gpu_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": round(per_gpu_gbs / HBM_PEAK_GBS, 4)},
+        "parity_ok": bad == 0.0,
+        "parity_check": "Encoder.Verify on the GPU (gf_verify_pipe), every object",
+    }
+
+
 def host_path(k, m, obj_len, n_obj=2048, passes=5, all_devices=False):
     """The path as the object server runs it: stripes (ecSplit databuf layout,
     ecutils.go:31-35) in pinned host memory from hbec_host_alloc, coded in
@@ -281,7 +376,20 @@ def cpu_model() -> str:
     return "unknown cpu"
 
 
-def main():
+def spawn_ranks(n: int, argv: list[str]) -> int:
+    """`--gpus N` with no launcher: run this script as N ranks under
+    torch.distributed.run (one process per GPU, rendezvous on 127.0.0.1) in a
+    CHILD process and return its exit status.  The caller has not touched the
+    GPU (nothing is exec'd from a process that initialised it)."""
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve()), *argv]
+    return subprocess.run(cmd).returncode
+
+
+def parse_args(argv):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -291,11 +399,50 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-host-path", action="store_true",
                     help="skip the PCIe-inclusive host-path line (pinned stripes, zero-copy)")
+    ap.add_argument("--config5-objects", type=int, default=65536,
+                    help="BASELINE configs[4]: objects partitioned over the N GPUs (0 = skip)")
     ap.add_argument("--split-objects", type=int, default=65536,
                     help="N>1 on RCCL: objects in the batch split from rank 0 (BASELINE configs[4]); 0 = skip")
-    args = ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="control path only (rank spawn, gloo rendezvous, max-over-ranks): no GPU, no value")
+    return ap.parse_args(argv)
 
+
+def dry_run(world, rank):
+    """The N>1 control path without a GPU (tests/test_dist.py): every rank
+    joins a gloo group and the max-over-ranks reduction; rank 0 reports how
+    many ranks took part."""
+    pg = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo")
+        pg = dist
+    (seen,) = max_over_ranks(pg, [float(rank + 1)], "cpu")
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": world,
+                          "ranks_seen": int(seen), "dry_run": True}), flush=True)
+    if pg:
+        pg.destroy_process_group()
+    return 0
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse_args(argv)
+    if args.gpus < 1:
+        print("bench.py: --gpus must be >= 1", file=sys.stderr)
+        return 2
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return spawn_ranks(args.gpus, argv)
     world, rank, local = dist_env()
+    if world != args.gpus:
+        print(f"bench.py: launcher WORLD_SIZE={world} but --gpus {args.gpus}; refusing to report a "
+              f"{world}-GPU number as {args.gpus}", file=sys.stderr)
+        return 2
+    if args.dry_run:
+        return dry_run(world, rank)
+
     # one rank per GPU; HBEC_DIST_BACKEND=gloo lets several ranks share one
     # GPU to rehearse the N>1 path on a 1-GPU box (control traffic only)
     backend = os.environ.get("HBEC_DIST_BACKEND", "nccl")
@@ -350,11 +497,12 @@ def main():
     value = total_bytes / elapsed / GiB
     ms_per_step = elapsed / args.steps * 1e3
 
+    line = None
     if rank == 0:
         launch_bytes = w.enc_bytes  # == rec_bytes for 2 erasures
         avg_launch_ms = (enc_ms + rec_ms) / 2
         achieved = launch_bytes / (avg_launch_ms * 1e-3) / 1e9
-        pmc, pmc_file = load_pmc()
+        pmc, pmc_file, pmc_reject = load_pmc()
         traffic = None
         if pmc and KERNEL_NAME in pmc.get("kernels", {}):
             traffic = pmc["kernels"][KERNEL_NAME].get("hbm_bytes_per_launch")
@@ -391,7 +539,9 @@ def main():
                 "bytes_per_launch": launch_bytes,
                 "encode_ms_per_launch": round(enc_ms, 4),
                 "reconstruct_ms_per_launch": round(rec_ms, 4),
-                "traffic_source": pmc_file,
+                "traffic_source": pmc_file if traffic is not None else None,
+                "traffic_note": pmc_reject,
+                "kernel_sources_sha256": kernel_sources_sha256(),
                 "tile_bytes": info["tile_bytes"], "kernel_kind": info["kind"],
                 "blocks_per_cu": info["blocks_per_cu"],
             },
@@ -401,13 +551,18 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(k, m, obj_len, erased, budget_s=args.cpu_budget)
+    del w  # free this rank's headline batch before the partition / split buffers
+    torch.cuda.empty_cache()
+    if args.config5_objects > 0:
+        c5 = config5(pg, k, m, obj_len, args.config5_objects, world, rank, ctl_device)
+        if rank == 0:
+            line["config5"] = c5
+            ok = ok and c5.get("parity_ok", True)  # a skipped leg reports why, not a failure
     if world > 1 and backend == "nccl" and args.split_objects > 0:
-        del w  # free this rank's headline batch before the split's buffers
-        torch.cuda.empty_cache()
         split = batch_split(pg, k, m, obj_len, args.split_objects, world, rank, ctl_device)
         if rank == 0:
             line["batch_split"] = split
-            ok = ok and split.get("parity_ok", True)  # a skipped split reports why, not a failure
+            ok = ok and split.get("parity_ok", True)
     if not args.no_host_path:
         # rank 0 drives every GPU of the node from one process; the others wait
         if rank == 0:
@@ -423,9 +578,8 @@ def main():
         print(json.dumps(line), flush=True)
     if pg:
         pg.destroy_process_group()
-    if not ok:
-        sys.exit(3)
+    return 0 if ok else 3
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

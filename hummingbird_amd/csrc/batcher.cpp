@@ -146,7 +146,6 @@ int hbec_batcher_new(hbec_codec* codec, uint64_t max_batch_bytes, uint32_t max_w
     return hbec::guarded("hbec_batcher_new", [&]() -> int {
         if (!codec || !out) return fail(HBEC_ERR_INVALID_ARG, "null argument");
         *out = nullptr;
-        if (hbec_data_shards(codec) > 8) return fail(HBEC_ERR_INVALID_ARG, "batcher supports k <= 8");
         std::unique_ptr<hbec_batcher> b(new (std::nothrow) hbec_batcher());
         if (!b) return fail(HBEC_ERR_NOMEM, "batcher allocation");
         hipError_t e = hipGetDevice(&b->device);

@@ -388,7 +388,10 @@ int hbec_ec_reconstruct(int k, int m, hbec_read_fn read, void* const* bodies, in
             const SlotLayout L = layout_for((uint64_t)exp);
             bool gpu = false;
             if (n_present < n) {  // Reconstruct (ecutils.go:111) is a no-op when nothing is missing
-                if (!ring.r) rc = ring_acquire(bufs.bytes, (size_t)n * round16((uint64_t)chunk_size), &ring.r);
+                // klauspost's checkShards runs before the count: a stripe with
+                // no shard at all is ErrShardNoData, not ErrTooFewShards
+                if (n_present == 0) rc = fail(HBEC_ERR_SHARD_NO_DATA, "no shard data");
+                if (!rc && !ring.r) rc = ring_acquire(bufs.bytes, (size_t)n * round16((uint64_t)chunk_size), &ring.r);
                 if (!rc) rc = queue_reconstruct(enc.c, *ring.r, b, databuf, L, present, 0, outputs);
                 if (rc) {
                     const int r2 = flush(b ^ 1);
@@ -458,6 +461,7 @@ int hbec_ec_glue(int k, int m, hbec_read_fn read, void* const* bodies, int chunk
             if (exp <= 0) return fail(HBEC_ERR_INVALID_ARG, "ecGlue: chunk size is zero");
             uint8_t* databuf = bufs.get(ring.r, b);
             bool data_missing = false;
+            int n_present = 0;
             for (int i = 0; i < n; ++i) {  // a failed body stays failed (ecutils.go:152-163)
                 present[i] = 0;
                 if (bodies[i] && !failed[i]) {
@@ -468,11 +472,13 @@ int hbec_ec_glue(int k, int m, hbec_read_fn read, void* const* bodies, int chunk
                         failed[i] = 1;
                 }
                 if (i < k && !present[i]) data_missing = true;
+                n_present += present[i];
             }
             const SlotLayout L = layout_for((uint64_t)exp);
             bool gpu = false;
             if (data_missing) {  // ReconstructData (ecutils.go:168)
-                if (!ring.r) rc = ring_acquire(bufs.bytes, (size_t)n * round16((uint64_t)chunk_size), &ring.r);
+                if (n_present == 0) rc = fail(HBEC_ERR_SHARD_NO_DATA, "no shard data");  // checkShards first
+                if (!rc && !ring.r) rc = ring_acquire(bufs.bytes, (size_t)n * round16((uint64_t)chunk_size), &ring.r);
                 if (!rc) rc = queue_reconstruct(enc.c, *ring.r, b, databuf, L, present, 1, outputs);
                 if (rc) {
                     const int r2 = flush(b ^ 1);

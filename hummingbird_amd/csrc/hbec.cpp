@@ -743,6 +743,54 @@ int hbec_verify(hbec_codec* c, uint8_t* const* shards, const size_t* lens, int n
     });
 }
 
+// ---- databuf entry points: ONE base pointer + scalars ----------------------
+// Every ecutils.go call site hands klauspost slices of one contiguous databuf:
+// shard i at databuf + i*S (ecSplit :31-35,55-58; ecReconstruct :94-101;
+// ecGlue :151-159).  Passing that base instead of a [][]byte lets a cgo shim
+// call in with no array of Go pointers (so no runtime.Pinner: Go 1.10's cgo
+// pointer rules allow a Go pointer to memory that holds no Go pointers).
+static void databuf_shards(const hbec_codec* c, uint8_t* databuf, size_t s, std::vector<uint8_t*>& p) {
+    p.resize((size_t)(c->k + c->m));
+    for (size_t i = 0; i < p.size(); ++i) p[i] = databuf + i * s;
+}
+
+int hbec_encode_databuf(hbec_codec* c, uint8_t* databuf, size_t shard_len) {
+    return hbec::guarded("hbec_encode_databuf", [&]() -> int {
+        if (!c || !databuf) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+        if (shard_len == 0) return fail(HBEC_ERR_SHARD_NO_DATA, "no shard data");  // checkShards: all empty
+        std::vector<uint8_t*> p;
+        databuf_shards(c, databuf, shard_len, p);
+        std::vector<size_t> lens(p.size(), shard_len);
+        return hbec_encode(c, p.data(), lens.data(), (int)p.size());
+    });
+}
+
+int hbec_reconstruct_databuf(hbec_codec* c, uint8_t* databuf, size_t shard_len, const uint8_t* present,
+                             int data_only) {
+    return hbec::guarded("hbec_reconstruct_databuf", [&]() -> int {
+        if (!c || !databuf || !present) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+        std::vector<uint8_t*> p;
+        databuf_shards(c, databuf, shard_len, p);
+        // a missing shard is a zero-length slice whose capacity is its slot
+        // (ecutils.go:98-100): klauspost fills it in place
+        std::vector<size_t> lens(p.size());
+        for (size_t i = 0; i < p.size(); ++i) lens[i] = present[i] ? shard_len : 0;
+        return hbec_reconstruct(c, p.data(), lens.data(), (int)p.size(), data_only);
+    });
+}
+
+int hbec_verify_databuf(hbec_codec* c, const uint8_t* databuf, size_t shard_len, int* ok) {
+    return hbec::guarded("hbec_verify_databuf", [&]() -> int {
+        if (!c || !databuf || !ok) return fail(HBEC_ERR_INVALID_ARG, "null argument");
+        *ok = 0;
+        if (shard_len == 0) return fail(HBEC_ERR_SHARD_NO_DATA, "no shard data");
+        std::vector<uint8_t*> p;
+        databuf_shards(c, const_cast<uint8_t*>(databuf), shard_len, p);
+        std::vector<size_t> lens(p.size(), shard_len);
+        return hbec_verify(c, p.data(), lens.data(), (int)p.size(), ok);
+    });
+}
+
 int hbec_set_force_stream(int on) {
     return hbec::guarded("hbec_set_force_stream", [&]() -> int {
         g_force_stream.store(on ? 1 : 0);

@@ -280,23 +280,9 @@ struct ZcStripe {
 // buffers) are the only host->device traffic; the kernel streams the shards
 // over PCIe.  One stream, so records, kernels and their reuse are ordered.
 int zero_copy_run(Ring* ring, const std::vector<ZcStripe>& zs, const std::vector<int>& in_idx,
-                  const std::vector<int>& out_idx, const std::vector<uint8_t>& rows, int cus) {
-    const int K = (int)in_idx.size(), R = (int)out_idx.size();
-    const uint64_t tile = (uint64_t)hbec::stripes_tile_bytes(K);
-    std::vector<hbec::StripeArgs> args;
-    std::vector<int> rg;  // output rows of each group (<= 3 per launch)
-    for (int r0 = 0; r0 < R; r0 += 3) {
-        const int Rg = std::min(3, R - r0);
-        hbec::StripeArgs a;
-        std::memset(&a, 0, sizeof(a));
-        for (int j = 0; j < K; ++j) a.in_idx[j] = (uint32_t)in_idx[j];
-        for (int r = 0; r < Rg; ++r) {
-            a.out_idx[r] = (uint32_t)out_idx[r0 + r];
-            for (int j = 0; j < K; ++j) hbec::perm_table(rows[(size_t)(r0 + r) * K + j], a.tab[r][j]);
-        }
-        rg.push_back(Rg);
-        args.push_back(a);
-    }
+                  const std::vector<int>& out_idx, const std::vector<uint8_t>& rows) {
+    const int K = (int)in_idx.size();
+    const uint64_t tile = (uint64_t)hbec::stripes_tile_bytes(std::min(K, hbec::kStripeMaxK));
     size_t si = 0;
     uint64_t off = 0;
     hipError_t e = hipSuccess;
@@ -322,20 +308,8 @@ int zero_copy_run(Ring* ring, const std::vector<ZcStripe>& zs, const std::vector
         e = hipMemcpyAsync(ring->dev_tiles[slot], rec, nt * sizeof(hbec::TileRec), hipMemcpyHostToDevice,
                            ring->s_cmp);
         if (e != hipSuccess) return hip_fail(e, "zero-copy records H2D");
-        for (size_t gi = 0; gi < args.size(); ++gi) {
-            auto a = args[gi];
-            const int Rg = rg[gi];
-            a.tiles = ring->dev_tiles[slot];
-            a.n_tiles = (uint32_t)nt;
-            int bpc = 1;
-            e = hbec::stripes_occupancy(K, Rg, &bpc);
-            if (e != hipSuccess) return hip_fail(e, "stripes occupancy");
-            if (hbec::kPipeBlocksPerCu > 0) bpc = std::min(bpc, hbec::kPipeBlocksPerCu);
-            const uint64_t want = (nt + 3) / 4;
-            const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cus * std::max(1, bpc)));
-            e = hbec::launch_stripes(K, Rg, a, grid, ring->s_cmp);
-            if (e != hipSuccess) return hip_fail(e, "launch gf_apply_stripes (zero-copy)");
-        }
+        int rc = hbec::launch_stripe_passes(ring->dev_tiles[slot], nt, in_idx, out_idx, rows, 0, ring->s_cmp);
+        if (rc) return rc;
         e = hipEventRecord(ring->ev_cmp[slot], ring->s_cmp);
         if (e != hipSuccess) return hip_fail(e, "zero-copy event");
     }
@@ -353,8 +327,6 @@ int host_run(const hbec_stripe* stripes, uint64_t n, const std::vector<int>& in_
              int n_shards = 0) {
     const int K = (int)in_idx.size(), R = (int)out_idx.size();
     if (R == 0 || n == 0) return HBEC_OK;
-    if (K > 8 || !hbec::stripes_supported(K, std::min(R, 3)))
-        return fail(HBEC_ERR_INVALID_ARG, "host path supports k <= 8");
     Ring* ring = nullptr;
     int rc = ring_acquire(&ring);
     if (rc) return rc;
@@ -380,7 +352,7 @@ int host_run(const hbec_stripe* stripes, uint64_t n, const std::vector<int>& in_
             else staged.push_back(stripes[s]);
         }
         if (!zs.empty()) {
-            rc = zero_copy_run(ring, zs, in_idx, out_idx, rows, ring->cus);
+            rc = zero_copy_run(ring, zs, in_idx, out_idx, rows);
             if (rc) return rc;
         }
         if (staged.empty()) return HBEC_OK;
@@ -389,7 +361,7 @@ int host_run(const hbec_stripe* stripes, uint64_t n, const std::vector<int>& in_
     }
     rc = ring_staging_init(*ring);
     if (rc) return rc;
-    const uint64_t tile = (uint64_t)hbec::stripes_tile_bytes(K);
+    const uint64_t tile = (uint64_t)hbec::stripes_tile_bytes(std::min(K, hbec::kStripeMaxK));
     // max columns per piece so that K*lpad fits the IN slot and R*lpad the OUT slot
     const uint64_t max_cols = (std::min(ring->in_cap / K, ring->out_cap / R) / 16) * 16;
     if (max_cols < 16) return fail(HBEC_ERR_INVALID_ARG, "staging slot too small");
@@ -451,22 +423,10 @@ int host_run(const hbec_stripe* stripes, uint64_t n, const std::vector<int>& in_
     }
     if (chunks.back().empty()) chunks.pop_back();
 
-    // kernel arguments per row group (<= 3 outputs per launch)
-    std::vector<hbec::StripeArgs> args;
-    std::vector<int> rg;  // output rows of each group (<= 3 per launch)
-    for (int r0 = 0; r0 < R; r0 += 3) {
-        const int Rg = std::min(3, R - r0);
-        hbec::StripeArgs a;
-        std::memset(&a, 0, sizeof(a));
-        for (int j = 0; j < K; ++j) a.in_idx[j] = (uint32_t)j;  // inputs packed 0..K-1 in the slot
-        for (int r = 0; r < Rg; ++r) {
-            a.out_idx[r] = (uint32_t)(r0 + r);
-            for (int j = 0; j < K; ++j) hbec::perm_table(rows[(size_t)(r0 + r) * K + j], a.tab[r][j]);
-        }
-        rg.push_back(Rg);
-        args.push_back(a);
-    }
-    const int cus = ring->cus;
+    // in the slots inputs are packed 0..K-1 and outputs 0..R-1
+    std::vector<int> slot_in(K), slot_out(R);
+    for (int j = 0; j < K; ++j) slot_in[j] = j;
+    for (int r = 0; r < R; ++r) slot_out[r] = r;
 
     std::vector<int64_t> slot_chunk(kSlots, -1);
     auto scatter = [&](int slot) -> int {
@@ -526,20 +486,8 @@ int host_run(const hbec_stripe* stripes, uint64_t n, const std::vector<int>& in_
         if (e == hipSuccess) e = hipEventRecord(ring->ev_h2d[slot], ring->s_h2d);
         if (e == hipSuccess) e = hipStreamWaitEvent(ring->s_cmp, ring->ev_h2d[slot], 0);
         if (e != hipSuccess) return hip_fail(e, "host path H2D");
-        for (size_t gi = 0; gi < args.size(); ++gi) {
-            auto a = args[gi];
-            const int Rg = rg[gi];
-            a.tiles = ring->dev_tiles[slot];
-            a.n_tiles = (uint32_t)nt;
-            int bpc = 1;
-            e = hbec::stripes_occupancy(K, Rg, &bpc);
-            if (e != hipSuccess) return hip_fail(e, "stripes occupancy");
-            if (hbec::kPipeBlocksPerCu > 0) bpc = std::min(bpc, hbec::kPipeBlocksPerCu);
-            const uint64_t want = (nt + 3) / 4;
-            const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cus * std::max(1, bpc)));
-            e = hbec::launch_stripes(K, Rg, a, grid, ring->s_cmp);
-            if (e != hipSuccess) return hip_fail(e, "launch gf_apply_stripes (host path)");
-        }
+        rc = hbec::launch_stripe_passes(ring->dev_tiles[slot], nt, slot_in, slot_out, rows, 0, ring->s_cmp);
+        if (rc) return rc;
         if (d_digest) {  // the chunk's shards -> hash arena (D2D, same stream, before the slot is released)
             if (arena_used + in_bytes + out_bytes > ring->arena_cap ||
                 arena_recs + pieces.size() * (size_t)(K + R) > ring->arena_rec_cap) {

@@ -5,6 +5,7 @@
 #include <exception>
 #include <new>
 #include <string>
+#include <vector>
 
 #include "../../include/hbec.h"
 
@@ -47,5 +48,15 @@ uint64_t pinned_device_addr(const void* p, uint64_t len);
 // ShardHash of a list of device chains: records {addr, len, slot, 0} (32 B
 // each, device memory), digest of record i at digest + slot * 16.
 hipError_t launch_md5_list(const void* recs, uint64_t n, uint8_t* digest, bool aligned, hipStream_t stream);
+
+struct TileRec;
+// Grid for a stripes launch of k inputs / r outputs over n_tiles records
+// (one block of 4 waves per CU at most, as the strided kernels).
+int stripes_grid(int k, int r, uint64_t n_tiles, int* grid);
+// out (^)= rows x in over tile records, in launches of <= 3 outputs and
+// <= 8 inputs (k > 8: accumulate passes).  sel_k > 0: object-plan bases.
+int launch_stripe_passes(const TileRec* tiles, uint64_t n_tiles, const std::vector<int>& in_idx,
+                         const std::vector<int>& out_idx, const std::vector<uint8_t>& rows, int sel_k,
+                         hipStream_t stream);
 
 }  // namespace hbec

@@ -110,16 +110,23 @@ struct TileRec {
 // Object plans (split launches): every tile has two bases, A = (in_addr,
 // in_stride) for data shards and B = (out_addr, out_stride) for parity
 // shards; bit j of in_sel / out_sel picks B for input j / output r.
+// At most kStripeMaxK inputs per stripes launch; more (k > 8) are split
+// into passes whose later launches set `accumulate` (outputs read back).
+constexpr int kStripeMaxK = 8;
+
 struct StripeArgs {
     const TileRec* tiles;
     uint32_t n_tiles;
     uint32_t split;           // 1: object plan (in_sel / out_sel apply)
+    uint32_t accumulate;      // 1: out ^= result (passes 2.. over > kStripeMaxK inputs; not with split)
+    uint32_t pad_;
     uint32_t in_idx[kMaxK];   // shard index (within its base) read as input j
     uint32_t out_idx[kMaxR];  // shard index (within its base) written as output r
     uint32_t in_sel, out_sel;
     uint32_t tab[kMaxR][kMaxK][5];
 };
 
+// tile bytes of a stripes pass with k inputs; accumulate passes use 1 KiB
 int stripes_tile_bytes(int k);
 bool stripes_supported(int k, int r);
 hipError_t launch_stripes(int k, int r, const StripeArgs& a, int grid, hipStream_t stream);

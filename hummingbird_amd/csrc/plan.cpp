@@ -1,8 +1,9 @@
 // plan.cpp — stripe plans: a batch of stripes of mixed shard lengths coded in
 // one launch (stripes.hip).  A stripe is ecSplit's databuf layout
 // (objectserver/ecutils.go:31-35,55-58): k+m shards of shard_len bytes back
-// to back, data first.  Stripes the tiled kernel cannot take (unaligned, or
-// shapes beyond K <= 8 inputs) go through the generic strided path one by one.
+// to back, data first.  Stripes the tiled kernel cannot take (unaligned; or
+// object plans beyond 8 inputs) go through the generic strided path one by
+// one; stripe plans with k > 8 run the tiled kernel in accumulate passes.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -54,7 +55,9 @@ uint8_t* object_shard(const hbec_object& o, int k, int i) {
 
 std::mutex g_occ_mu;
 
-int stripes_grid(int k, int r, uint64_t n_tiles, int* grid) {
+}  // namespace
+
+int hbec::stripes_grid(int k, int r, uint64_t n_tiles, int* grid) {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
@@ -82,6 +85,53 @@ int stripes_grid(int k, int r, uint64_t n_tiles, int* grid) {
     *grid = (int)std::max<uint64_t>(1, std::min(want, cap));
     return HBEC_OK;
 }
+
+// out[r] (^)= XOR_j rows[r][j] * in[j] over every tile record: launches of
+// <= 3 outputs x <= kStripeMaxK inputs; a shape with more inputs (k > 8)
+// runs in passes, the later ones accumulating into the outputs.  sel_k > 0
+// marks an object plan (split bases: shard indices >= sel_k are parity).
+int hbec::launch_stripe_passes(const TileRec* tiles, uint64_t n_tiles, const std::vector<int>& in_idx,
+                               const std::vector<int>& out_idx, const std::vector<uint8_t>& rows, int sel_k,
+                               hipStream_t stream) {
+    const int K_all = (int)in_idx.size(), R_all = (int)out_idx.size();
+    if (n_tiles == 0 || R_all == 0) return HBEC_OK;
+    if (sel_k > 0 && K_all > kStripeMaxK) return fail(HBEC_ERR_INVALID_ARG, "object plans take <= 8 inputs per pass");
+    for (int r0 = 0; r0 < R_all; r0 += 3) {
+        const int R = std::min(3, R_all - r0);
+        for (int c0 = 0; c0 < K_all; c0 += kStripeMaxK) {
+            const int K = std::min(kStripeMaxK, K_all - c0);
+            StripeArgs a;
+            std::memset(&a, 0, sizeof(a));
+            a.tiles = tiles;
+            a.n_tiles = (uint32_t)n_tiles;
+            a.split = sel_k > 0 ? 1u : 0u;
+            a.accumulate = c0 > 0 ? 1u : 0u;
+            for (int j = 0; j < K; ++j) {
+                a.in_idx[j] = (uint32_t)in_idx[c0 + j];
+                if (sel_k > 0 && in_idx[c0 + j] >= sel_k) {  // parity shard: base B
+                    a.in_sel |= 1u << j;
+                    a.in_idx[j] -= (uint32_t)sel_k;
+                }
+            }
+            for (int r = 0; r < R; ++r) {
+                a.out_idx[r] = (uint32_t)out_idx[r0 + r];
+                if (sel_k > 0) {
+                    if (out_idx[r0 + r] < sel_k) a.out_sel |= 1u << r;  // data shard: base A
+                    else a.out_idx[r] -= (uint32_t)sel_k;
+                }
+                for (int j = 0; j < K; ++j) perm_table(rows[(size_t)(r0 + r) * K_all + c0 + j], a.tab[r][j]);
+            }
+            int grid = 0;
+            int rc = stripes_grid(K, R, n_tiles, &grid);
+            if (rc) return rc;
+            hipError_t e = launch_stripes(K, R, a, grid, stream);
+            if (e != hipSuccess) return hip_fail(e, "launch gf_apply_stripes");
+        }
+    }
+    return HBEC_OK;
+}
+
+namespace {
 
 // Codes one stripe through the generic strided path (any alignment / shape).
 int apply_one(const hbec_stripe& s, int n_shards, const std::vector<int>& in_idx, const std::vector<int>& out_idx,
@@ -111,36 +161,13 @@ int run_plan(const hbec_plan* p, const std::vector<int>& in_idx, const std::vect
     const int K = (int)in_idx.size();
     const int R_all = (int)out_idx.size();
     if (R_all == 0 || p->shard_bytes == 0) return HBEC_OK;
-    const bool tiled_ok = K <= 8 && hbec::stripes_supported(K, 1);
+    // stripe plans take any k (inputs beyond 8 accumulate in later passes);
+    // object plans keep the tiled kernel to k <= 8
+    const bool tiled_ok = p->objects ? K <= hbec::kStripeMaxK : true;
     if (tiled_ok && p->n_tiles > 0) {
-        for (int r0 = 0; r0 < R_all; r0 += 3) {
-            const int R = std::min(3, R_all - r0);
-            hbec::StripeArgs a;
-            std::memset(&a, 0, sizeof(a));
-            a.tiles = p->d_tiles;
-            a.n_tiles = (uint32_t)p->n_tiles;
-            a.split = p->objects ? 1u : 0u;
-            for (int j = 0; j < K; ++j) {
-                a.in_idx[j] = (uint32_t)in_idx[j];
-                if (p->objects && in_idx[j] >= p->k) {  // parity shard: base B
-                    a.in_sel |= 1u << j;
-                    a.in_idx[j] -= (uint32_t)p->k;
-                }
-            }
-            for (int r = 0; r < R; ++r) {
-                a.out_idx[r] = (uint32_t)out_idx[r0 + r];
-                if (p->objects) {
-                    if (out_idx[r0 + r] < p->k) a.out_sel |= 1u << r;  // data shard: base A
-                    else a.out_idx[r] -= (uint32_t)p->k;
-                }
-                for (int j = 0; j < K; ++j) hbec::perm_table(rows[(size_t)(r0 + r) * K + j], a.tab[r][j]);
-            }
-            int grid = 0;
-            int rc = stripes_grid(K, R, p->n_tiles, &grid);
-            if (rc) return rc;
-            hipError_t e = hbec::launch_stripes(K, R, a, grid, stream);
-            if (e != hipSuccess) return hip_fail(e, "launch gf_apply_stripes");
-        }
+        int rc = hbec::launch_stripe_passes(p->d_tiles, p->n_tiles, in_idx, out_idx, rows, p->objects ? p->k : 0,
+                                            stream);
+        if (rc) return rc;
     }
     if (p->objects) {
         if (!tiled_ok) {
@@ -182,7 +209,7 @@ int hbec_plan_stripes(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n,
         if (!p) return fail(HBEC_ERR_NOMEM, "plan allocation");
         p->k = k;
         p->m = m;
-        p->tile_bytes = hbec::stripes_tile_bytes(std::min(k, 8));
+        p->tile_bytes = hbec::stripes_tile_bytes(std::min(k, hbec::kStripeMaxK));
         std::vector<hbec::TileRec> recs;
         for (uint64_t i = 0; i < n; ++i) {
             const hbec_stripe& s = stripes[i];
@@ -230,7 +257,7 @@ int hbec_plan_objects(hbec_codec* codec, const hbec_object* objects, uint64_t n,
         p->k = k;
         p->m = m;
         p->objects = true;
-        p->tile_bytes = hbec::stripes_tile_bytes(std::min(k, 8));
+        p->tile_bytes = hbec::stripes_tile_bytes(std::min(k, hbec::kStripeMaxK));
         std::vector<hbec::TileRec> recs;
         for (uint64_t i = 0; i < n; ++i) {
             const hbec_object& o = objects[i];

@@ -50,7 +50,10 @@ __device__ __forceinline__ void load_stripe_tile(u32x4 (&x)[U][K], const uint64_
     }
 }
 
-template <int K, int R, int U, bool FULL>
+// ACC: a later pass over inputs beyond the first 8 (k > 8): the outputs
+// already hold the earlier passes' partial sums and are read back and
+// XOR-accumulated (clamped like the input loads; stores stay masked).
+template <int K, int R, int U, bool FULL, bool ACC>
 __device__ __forceinline__ void store_stripe_tile_(const u32x4 (&x)[U][K], const StripeArgs& a,
                                                    const Tables<K, R>& tb, const uint64_t (&dst)[R], uint32_t valid,
                                                    uint32_t lane) {
@@ -58,8 +61,15 @@ __device__ __forceinline__ void store_stripe_tile_(const u32x4 (&x)[U][K], const
     for (int u = 0; u < U; ++u) {
         const uint64_t off = (uint64_t)lane * 16u + (uint64_t)u * 1024u;
         u32x4 acc[R];
+        if constexpr (ACC) {
+            const uint64_t last = (uint64_t)valid - 16u;
+            const uint64_t ro = off < last ? off : last;
 #pragma unroll
-        for (int r = 0; r < R; ++r) acc[r] = u32x4{0, 0, 0, 0};
+            for (int r = 0; r < R; ++r) acc[r] = ld16_addr(dst[r] + ro);
+        } else {
+#pragma unroll
+            for (int r = 0; r < R; ++r) acc[r] = u32x4{0, 0, 0, 0};
+        }
         gf_dot<K, R>(acc, x[u], a.tab, tb);
         if (FULL || off < valid) {
 #pragma unroll
@@ -68,13 +78,13 @@ __device__ __forceinline__ void store_stripe_tile_(const u32x4 (&x)[U][K], const
     }
 }
 
-template <int K, int R, int U>
+template <int K, int R, int U, bool ACC>
 __device__ __forceinline__ void store_stripe_tile(const u32x4 (&x)[U][K], const StripeArgs& a, const Tables<K, R>& tb,
                                                   const uint64_t (&dst)[R], uint32_t valid, uint32_t lane) {
     if (valid >= (uint32_t)U * 1024u)  // wave-uniform: whole tile live
-        store_stripe_tile_<K, R, U, true>(x, a, tb, dst, valid, lane);
+        store_stripe_tile_<K, R, U, true, ACC>(x, a, tb, dst, valid, lane);
     else
-        store_stripe_tile_<K, R, U, false>(x, a, tb, dst, valid, lane);
+        store_stripe_tile_<K, R, U, false, ACC>(x, a, tb, dst, valid, lane);
 }
 
 // Tile records are read-only for the whole launch and passed as a separate
@@ -83,10 +93,11 @@ __device__ __forceinline__ TileRec load_rec(const TileRec* __restrict__ recs, ui
     return recs[i];
 }
 
-template <int K, int R, bool SPLIT>
+template <int K, int R, bool SPLIT, bool ACC = false>
 __global__ __launch_bounds__(kBlockThreads, 1) void gf_apply_stripes(StripeArgs a,
                                                                      const TileRec* __restrict__ tiles) {
-    constexpr int U = stripes_u(K);
+    // accumulate passes follow a first pass of exactly kStripeMaxK inputs: same tiles
+    constexpr int U = ACC ? stripes_u(kStripeMaxK) : stripes_u(K);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave =
         __builtin_amdgcn_readfirstlane(xcd_block() * (kBlockThreads / 64) + (threadIdx.x >> 6));
@@ -110,7 +121,7 @@ __global__ __launch_bounds__(kBlockThreads, 1) void gf_apply_stripes(StripeArgs 
         // return out of order, so waiting for `nxt` is an lgkmcnt(0)
         const uint32_t t2 = tn + nw;
         const TileRec after = load_rec(tiles, t2 < n ? t2 : tn);
-        store_stripe_tile<K, R, U>(x, a, tb, dst, cur.valid, lane);
+        store_stripe_tile<K, R, U, ACC>(x, a, tb, dst, cur.valid, lane);
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -120,36 +131,39 @@ __global__ __launch_bounds__(kBlockThreads, 1) void gf_apply_stripes(StripeArgs 
         cur = nxt;
         nxt = after;
     }
-    store_stripe_tile<K, R, U>(x, a, tb, dst, cur.valid, lane);
+    store_stripe_tile<K, R, U, ACC>(x, a, tb, dst, cur.valid, lane);
 }
 
-template <int K, bool SPLIT>
+template <int K, bool SPLIT, bool ACC>
 static const void* stripes_for_r(int r) {
     switch (r) {
-        case 1: return reinterpret_cast<const void*>(&gf_apply_stripes<K, 1, SPLIT>);
-        case 2: return reinterpret_cast<const void*>(&gf_apply_stripes<K, 2, SPLIT>);
-        case 3: return reinterpret_cast<const void*>(&gf_apply_stripes<K, 3, SPLIT>);
+        case 1: return reinterpret_cast<const void*>(&gf_apply_stripes<K, 1, SPLIT, ACC>);
+        case 2: return reinterpret_cast<const void*>(&gf_apply_stripes<K, 2, SPLIT, ACC>);
+        case 3: return reinterpret_cast<const void*>(&gf_apply_stripes<K, 3, SPLIT, ACC>);
     }
     return nullptr;
 }
 
-template <bool SPLIT>
+template <bool SPLIT, bool ACC>
 static const void* stripes_kernel_(int k, int r) {
     switch (k) {
-        case 1: return stripes_for_r<1, SPLIT>(r);
-        case 2: return stripes_for_r<2, SPLIT>(r);
-        case 3: return stripes_for_r<3, SPLIT>(r);
-        case 4: return stripes_for_r<4, SPLIT>(r);
-        case 5: return stripes_for_r<5, SPLIT>(r);
-        case 6: return stripes_for_r<6, SPLIT>(r);
-        case 7: return stripes_for_r<7, SPLIT>(r);
-        case 8: return stripes_for_r<8, SPLIT>(r);
+        case 1: return stripes_for_r<1, SPLIT, ACC>(r);
+        case 2: return stripes_for_r<2, SPLIT, ACC>(r);
+        case 3: return stripes_for_r<3, SPLIT, ACC>(r);
+        case 4: return stripes_for_r<4, SPLIT, ACC>(r);
+        case 5: return stripes_for_r<5, SPLIT, ACC>(r);
+        case 6: return stripes_for_r<6, SPLIT, ACC>(r);
+        case 7: return stripes_for_r<7, SPLIT, ACC>(r);
+        case 8: return stripes_for_r<8, SPLIT, ACC>(r);
     }
     return nullptr;
 }
 
-static const void* stripes_kernel(int k, int r, bool split = false) {
-    return split ? stripes_kernel_<true>(k, r) : stripes_kernel_<false>(k, r);
+// accumulate passes (k > 8) exist for stripe plans and the host ring, not for
+// object plans (split), which never exceed 8 inputs per pass
+static const void* stripes_kernel(int k, int r, bool split = false, bool acc = false) {
+    if (acc) return split ? nullptr : stripes_kernel_<false, true>(k, r);
+    return split ? stripes_kernel_<true, false>(k, r) : stripes_kernel_<false, false>(k, r);
 }
 
 int stripes_tile_bytes(int k) { return stripes_u(k) * 1024; }
@@ -157,7 +171,7 @@ int stripes_tile_bytes(int k) { return stripes_u(k) * 1024; }
 bool stripes_supported(int k, int r) { return stripes_kernel(k, r) != nullptr; }
 
 hipError_t launch_stripes(int k, int r, const StripeArgs& a, int grid, hipStream_t stream) {
-    const void* fn = stripes_kernel(k, r, a.split != 0);
+    const void* fn = stripes_kernel(k, r, a.split != 0, a.accumulate != 0);
     if (!fn) return hipErrorInvalidValue;
     const TileRec* tiles = a.tiles;
     void* args[] = {const_cast<StripeArgs*>(&a), &tiles};

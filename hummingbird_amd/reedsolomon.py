@@ -161,6 +161,31 @@ class Encoder:
     def ReconstructData(self, shards) -> None:
         self._reconstruct(shards, 1)
 
+    # ---- single-pointer databuf forms (hbec_*_databuf): the k+m shards of one
+    # contiguous buffer, shard i at i*S, as every ecutils.go call site builds
+    # them (ecutils.go:31-35,55-58,94-101,151-159) ----
+    def _databuf(self, databuf, shard_len):
+        a = _as_array(databuf)
+        if shard_len < 0 or a.size < self.Shards * shard_len:
+            raise ValueError("databuf shorter than (k+m) * shard_len")
+        return C.c_void_p(a.ctypes.data if a.size else None)
+
+    def EncodeDatabuf(self, databuf, shard_len: int) -> None:
+        """Encode(data) where data[i] = databuf[i*S:(i+1)*S] (ecSplit, ecutils.go:55-59)."""
+        check(N.lib().hbec_encode_databuf(self._h, self._databuf(databuf, shard_len), int(shard_len)))
+
+    def ReconstructDatabuf(self, databuf, shard_len: int, present, data_only: bool = False) -> None:
+        """Reconstruct(data) / ReconstructData(data) with missing shards rebuilt in
+        their databuf slots (ecReconstruct ecutils.go:94-111, ecGlue :151-168)."""
+        p = (C.c_uint8 * self.Shards)(*[1 if x else 0 for x in present])
+        check(N.lib().hbec_reconstruct_databuf(self._h, self._databuf(databuf, shard_len), int(shard_len), p,
+                                               int(data_only)))
+
+    def VerifyDatabuf(self, databuf, shard_len: int) -> bool:
+        ok = C.c_int()
+        check(N.lib().hbec_verify_databuf(self._h, self._databuf(databuf, shard_len), int(shard_len), C.byref(ok)))
+        return bool(ok.value)
+
     # ---- streaming host path: many host stripes (ecSplit databuf layout) ----
     def _stripes(self, stripes):
         """stripes: list of 1-D uint8 arrays, each (k+m)*S bytes (data then parity)."""

@@ -85,6 +85,22 @@ int hbec_reconstruct(hbec_codec* codec, uint8_t* const* shards, size_t* lens, in
  * checks as hbec_encode.  Host memory, synchronous. */
 int hbec_verify(hbec_codec* codec, uint8_t* const* shards, const size_t* lens, int n_shards, int* ok);
 
+/* Single-pointer forms of Encode / Reconstruct / ReconstructData / Verify
+ * over ecutils.go's contiguous databuf: shard i (k+m of them) at
+ * databuf + i * shard_len, exactly the slices every call site builds
+ * (ecSplit ecutils.go:31-35,55-58; ecReconstruct :94-101; ecGlue :151-159).
+ * A cgo caller passes &databuf[0] and scalars — no array of Go pointers, so
+ * no runtime.Pinner (Go 1.10.2, the reference's toolchain, .travis.yml:7-8).
+ * present: k+m bytes, non-zero = shard read (len > 0 in Go); missing shards
+ * are rebuilt in their databuf slots (klauspost reuses the slice capacity,
+ * which ecReconstruct/ecGlue place at the slot, ecutils.go:98-100).
+ * shard_len == 0 (every shard empty) -> HBEC_ERR_SHARD_NO_DATA, as
+ * klauspost's checkShards.  Host memory, synchronous. */
+int hbec_encode_databuf(hbec_codec* codec, uint8_t* databuf, size_t shard_len);
+int hbec_reconstruct_databuf(hbec_codec* codec, uint8_t* databuf, size_t shard_len, const uint8_t* present,
+                             int data_only);
+int hbec_verify_databuf(hbec_codec* codec, const uint8_t* databuf, size_t shard_len, int* ok);
+
 /* ---------------------------------------------------------------------------
  * Device-resident batches (the GPU hot path).  A view places shard i of
  * object o at base + o * obj_stride in device memory.  Work is queued on
@@ -207,7 +223,8 @@ int hbec_reconstruct_plan(hbec_codec* codec, const hbec_plan* plan, const uint8_
  * ecSplit layout), coded through a pinned staging ring — CPU gather, H2D,
  * kernel and D2H of successive chunks overlap on three streams.  Synchronous:
  * on return the parity (encode) or the rebuilt shards (reconstruct) are in the
- * caller's stripes.  k <= 8.  Env: HBEC_HOST_SLOT_MB (64), HBEC_HOST_THREADS.
+ * caller's stripes.  Any k (k > 8 runs in accumulate passes).  Env:
+ * HBEC_HOST_SLOT_MB (64), HBEC_HOST_THREADS.
  * Zero-copy: 16-B-aligned stripes in pinned, device-mapped host memory are
  * coded IN PLACE by the GPU over PCIe — no staging copies, no CPU
  * gather/scatter (HBEC_ZEROCOPY=0 sends them through the ring too).
@@ -251,7 +268,7 @@ int hbec_encode_host_md5(hbec_codec* codec, const hbec_stripe* stripes, uint64_t
  * (k+m) * shard_len), or what has arrived max_wait_us after the worker
  * started waiting — with one host-path call, so up to max_batch_bytes are in
  * flight.  Requests with different ops / erasure patterns form separate
- * batches.  k <= 8.  The codec must outlive the batcher. */
+ * batches.  Any k.  The codec must outlive the batcher. */
 typedef struct hbec_batcher hbec_batcher;
 int hbec_batcher_new(hbec_codec* codec, uint64_t max_batch_bytes, uint32_t max_wait_us, hbec_batcher** out);
 void hbec_batcher_free(hbec_batcher* batcher);

@@ -249,3 +249,32 @@ def test_host_devices_validation_needs_no_device():
     out = C.c_uint64(7)
     buf = (C.c_uint8 * 64)()
     assert N.lib().hbec_host_device_addr(buf, 64, C.byref(out)) == 0 and out.value == 0  # pageable
+
+
+def test_all_missing_stripe_is_shard_no_data_without_device():
+    """klauspost's checkShards precedes the shard count, so a stripe with no
+    shard at all is ErrShardNoData in ecReconstruct / ecGlue
+    (ecutils.go:111,168) and in the databuf entry points; it is decided
+    before any device work."""
+    with pytest.raises(RS.ErrShardNoData):
+        E.ec_reconstruct(4, 2, [None] * 6, 1024, 10_000, [], [])
+    with pytest.raises(RS.ErrShardNoData):
+        E.ec_glue(4, 2, [None] * 6, 1024, 10_000)
+    with pytest.raises(O.ErrShardNoData):
+        O.ec_reconstruct(4, 2, [None] * 6, 1024, 10_000, [0])
+    with pytest.raises(O.ErrShardNoData):
+        O.ec_glue(4, 2, [None] * 6, 1024, 10_000)
+    enc = RS.New(4, 2)
+    buf = np.zeros(6 * 16, np.uint8)
+    with pytest.raises(RS.ErrShardNoData):
+        enc.EncodeDatabuf(buf, 0)
+    with pytest.raises(RS.ErrShardNoData):
+        enc.ReconstructDatabuf(buf, 16, [0] * 6)
+    with pytest.raises(RS.ErrTooFewShards):
+        enc.ReconstructDatabuf(buf, 16, [1, 1, 1, 0, 0, 0])
+    enc.ReconstructDatabuf(buf, 16, [1] * 6)          # nothing missing: no device work
+    enc.ReconstructDatabuf(buf, 16, [1] * 4 + [0, 0], data_only=True)
+    with pytest.raises(ValueError):
+        enc.EncodeDatabuf(buf, 17)                    # buffer shorter than (k+m)*S
+    ok = C.c_int(9)
+    assert N.lib().hbec_verify_databuf(enc.handle, None, 16, C.byref(ok)) == N.ERR_INVALID_ARG

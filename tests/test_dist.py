@@ -122,3 +122,55 @@ def test_object_range_partition():
     assert SP.object_range(65536, 8, 7) == (7 * 8192, 8192)
     with pytest.raises(ValueError):
         SP.object_range(4, 0, 0)
+
+
+def _clean_env():
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "LOCAL_WORLD_SIZE")}
+    env["OMP_NUM_THREADS"] = "1"
+    return env
+
+
+def _bench_cmd(*args):
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(bench.__file__).resolve().parent
+    return subprocess.run([sys.executable, str(root / "bench.py"), *args], env=_clean_env(), cwd=str(root),
+                          capture_output=True, text=True, timeout=300)
+
+
+def test_bench_gpus_without_launcher_spawns_ranks():
+    """`python bench.py --gpus 2` with no launcher env starts 2 ranks itself
+    (torch.distributed.run in a child process) and reports n_gpus 2."""
+    import json
+
+    r = _bench_cmd("--gpus", "2", "--dry-run")
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 alone prints
+    assert lines[0]["n_gpus"] == 2 and lines[0]["ranks_seen"] == 2
+
+
+def test_bench_single_gpu_dry_run():
+    import json
+
+    r = _bench_cmd("--dry-run")
+    assert r.returncode == 0, r.stderr[-2000:]
+    (line,) = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert line["n_gpus"] == 1 and line["ranks_seen"] == 1
+
+
+def test_bench_refuses_launcher_world_mismatch():
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(bench.__file__).resolve().parent
+    env = _clean_env()
+    env.update(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, str(root / "bench.py"), "--gpus", "2", "--dry-run"], env=env,
+                       cwd=str(root), capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2
+    assert "WORLD_SIZE=1" in r.stderr

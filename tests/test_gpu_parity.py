@@ -711,10 +711,107 @@ def test_host_path_devices_errors():
     enc.EncodeStripesDevices([], devices=[0])
 
 
-def test_host_path_rejects_wide_k():
-    enc = RS.New(10, 2)
-    with pytest.raises(RS.ErrInvalidArg):
-        enc.EncodeStripes(_host_stripes(10, 2, [1000]))
+# k > 8 (a `hec` policy may set any data_shards, ecengine.go:719-724): the
+# stripes kernel runs in passes of <= 8 inputs, later passes accumulating.
+WIDE = [(10, 4, [MiB, 4096 * 10, 1000, MiB + 160, 16 * 10]), (17, 3, [17 * 4096, 17 * 1024 * 3 + 17 * 16, 5]),
+        (12, 5, [12 * 8192, 12 * 16])]
+
+
+def _wide_patterns(k, m):
+    return [tuple(range(min(m, 3))), (0, k), (k - 1, 8, 9)[:m], tuple(range(k - m, k))]
+
+
+@pytest.mark.parametrize("k,m,sizes", WIDE)
+def test_host_path_wide_k_ring(k, m, sizes):
+    enc = RS.New(k, m)
+    stripes = _host_stripes(k, m, sizes, seed=k * 3 + m)
+    want = _encoded_copy(k, m, stripes)
+    enc.EncodeStripes(stripes)
+    for got, w in zip(stripes, want):
+        assert np.array_equal(got, w)
+    for missing in _wide_patterns(k, m):
+        damaged = [w.copy() for w in want]
+        for st in damaged:
+            s = st.size // (k + m)
+            for i in missing:
+                st[i * s:(i + 1) * s] = 0x3C
+        enc.ReconstructStripes(damaged, [0 if i in missing else 1 for i in range(k + m)])
+        for got, w in zip(damaged, want):
+            assert np.array_equal(got, w), missing
+
+
+@pytest.mark.parametrize("k,m,sizes", WIDE)
+def test_host_path_wide_k_zero_copy(k, m, sizes):
+    enc = RS.New(k, m)
+    total = sum((k + m) * O.ec_shard_length(x, k) + 16 for x in sizes) + 16
+    hb = RS.HostBuffer(total)
+    stripes = _pinned_stripes(hb.array, k, m, sizes, seed=5 * k + m)
+    want = _encoded_copy(k, m, stripes)
+    enc.EncodeStripes(stripes)
+    for got, w in zip(stripes, want):
+        assert np.array_equal(got, w)
+    missing = _wide_patterns(k, m)[1]
+    for st in stripes:
+        s = st.size // (k + m)
+        for i in missing:
+            st[i * s:(i + 1) * s] = 0xC3
+    enc.ReconstructStripes(stripes, [0 if i in missing else 1 for i in range(k + m)])
+    for got, w in zip(stripes, want):
+        assert np.array_equal(got, w)
+    del stripes
+    hb.free()
+
+
+@pytest.mark.parametrize("k,m", [(10, 4), (17, 3)])
+def test_batcher_wide_k(k, m):
+    import threading
+
+    enc = RS.New(k, m)
+    bat = RS.Batcher(enc, max_batch_bytes=64 << 20, max_wait_us=1000)
+    sizes = [k * 4096 * (1 + i % 5) for i in range(24)]
+    stripes = _host_stripes(k, m, sizes, seed=k + 100)
+    want = _encoded_copy(k, m, stripes)
+    errors = []
+
+    def run(i):
+        try:
+            bat.Encode(stripes[i])
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(e)
+
+    threads = [threading.Thread(target=run, args=(i,)) for i in range(len(stripes))]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    bat.close()
+    assert not errors
+    assert all(np.array_equal(a, b) for a, b in zip(stripes, want))
+
+
+@pytest.mark.parametrize("k,m", [(10, 4), (17, 3)])
+def test_stripe_plan_wide_k(k, m):
+    """Stripe plans with k > 8 take the tiled kernel in accumulate passes (no
+    per-stripe fallback)."""
+    sizes = [k * 1024 * 3, k * 16, MiB // 4 * k, k * 4096]
+    pool, layout = _stripe_pool(k, m, sizes)
+    want = _expected_pool(k, m, pool, layout)
+    dev = torch.from_numpy(pool).cuda()
+    enc = RS.New(k, m)
+    plan = B.StripePlan(enc, [(dev.data_ptr() + o, s) for o, s, _ in layout])
+    assert plan.info()["n_fallback"] == 0
+    plan.encode()
+    torch.cuda.synchronize()
+    assert np.array_equal(dev.cpu().numpy(), want)
+    for missing in [(0, 3, k)[:m], (k - 1, 8, 9)[:m]]:
+        damaged = torch.from_numpy(want.copy()).cuda()
+        for o, s, _ in layout:
+            for i in missing:
+                damaged[o + i * s:o + (i + 1) * s] = 0xEE
+        dplan = B.StripePlan(enc, [(damaged.data_ptr() + o, s) for o, s, _ in layout])
+        dplan.reconstruct([0 if i in missing else 1 for i in range(k + m)])
+        torch.cuda.synchronize()
+        assert np.array_equal(damaged.cpu().numpy(), want), missing
 
 
 # ------------------------------------------------------------------ Verify

@@ -33,3 +33,53 @@ def test_batch_split_single_rank_gpu():
     assert res["parity_ok"] is True
     assert res["objects"] == 64 and res["objects_per_rank_max"] == 64
     assert res["encode_ms"] > 0
+
+
+def test_config5_full_partition_one_gpu_sampled_oracle():
+    """BASELINE configs[4] at G=1: all 65 536 x 1 MiB 4+2 objects (64 GiB data
+    + 32 GiB parity) resident on one GPU and encoded by libhbec in ONE batch
+    call; every object checked by the GPU Verify kernel, and a sample of
+    objects (first, last, seeded interior picks) checked byte for byte
+    against the CPU oracle (oracle/gf_oracle.c) on the same splitmix inputs."""
+    import numpy as np
+
+    from hummingbird_amd import batch as B
+    from hummingbird_amd import reedsolomon as RS
+    from oracle import coracle as CO
+
+    torch.cuda.set_device(0)
+    torch.cuda.empty_cache()
+    k, m, size, n = 4, 2, 1 << 20, 65536
+    s = size // k
+    enc = RS.New(k, m)
+    objs = torch.empty((n, size), dtype=torch.uint8, device="cuda")
+    parity = torch.empty((n, m * s), dtype=torch.uint8, device="cuda")
+    try:
+        B.fill_splitmix(objs, size)
+        B.encode_objects(enc, objs, parity, s)
+        flags = torch.zeros(n, dtype=torch.int32, device="cuda")
+        B.verify_views(enc, B.shard_views(objs, k, s) + B.shard_views(parity, m, s), n, s, flags)
+        torch.cuda.synchronize()
+        assert int(flags.count_nonzero().item()) == 0
+        rng = np.random.default_rng(0x48424543)
+        picks = sorted({0, 1, n // 2, n - 2, n - 1, *rng.integers(0, n, 27).tolist()})
+        idx = torch.tensor(picks, device="cuda")
+        got = parity.index_select(0, idx).cpu().numpy()
+        host = objs.index_select(0, idx).cpu().numpy()
+        for i, o in enumerate(picks):  # the GPU's inputs are the oracle's splitmix objects
+            assert np.array_equal(host[i], CO.fill_objects(o, 1, size)[0]), o
+        want, _ = CO.encode_batch(k, m, host, threads=CO.cpu_threads())
+        assert np.array_equal(got, want)
+    finally:
+        del objs, parity
+        torch.cuda.empty_cache()
+
+
+def test_config5_leg_single_rank():
+    """bench.config5 (the JSON line's `config5` object) on one GPU with a
+    small partition: timing fields and the GPU-side parity check."""
+    torch.cuda.set_device(0)
+    res = bench.config5(None, 4, 2, 1 << 20, 512, 1, 0, "cuda", reps=2)
+    assert "skipped" not in res, res
+    assert res["parity_ok"] is True and res["objects"] == 512 and res["objects_per_gpu_max"] == 512
+    assert res["value_GiB_s"] > 0 and 0 < res["per_gpu_roofline"]["frac"] < 1.0
