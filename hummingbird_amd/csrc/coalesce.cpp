@@ -1,0 +1,163 @@
+// coalesce.cpp — group commit for the per-call Encode / Reconstruct /
+// ReconstructData entry points (the plain drop-in of INTEGRATION.md §2-3).
+//
+// In the reference every Stabilize / degraded GET / repair goroutine calls
+// klauspost on its own one-stripe databuf (objectserver/ecutils.go:59,111,168;
+// nursery concurrency x devices, replicator.go:487,530, plus per-request
+// goroutines).  On the GPU one 1 MiB stripe per call is bound by launch and
+// PCIe latency, so concurrent calls are coalesced here, inside the library,
+// with no deadline and no extra thread: a call that finds fewer than
+// kMaxInFlight groups running leads — it takes every queued call with the
+// same (device, codec, op, erasure pattern) and codes them all with ONE
+// host-path call (hostpath.cpp: pinned ring, or zero-copy for pinned
+// databufs) — while calls that arrive meanwhile queue and form the next
+// group.  A lone caller runs at once through the per-call path, so
+// single-threaded latency is unchanged; throughput grows with concurrency.
+// If a group's batched call fails, each member is retried alone so every
+// caller gets its own result.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <condition_variable>
+#include <cstdlib>
+#include <deque>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/hbec.h"
+#include "internal.h"
+
+namespace hbec {
+
+namespace {
+
+struct CoReq {
+    hbec_codec* codec = nullptr;
+    int dev = 0;
+    int op = 0;  // 0 encode, 1 reconstruct
+    uint8_t* base = nullptr;
+    uint64_t s = 0;
+    std::vector<uint8_t> present;
+    int data_only = 0;
+    int rc = HBEC_OK;
+    std::string err;
+    bool taken = false, done = false;
+
+    bool same_group(const CoReq& o) const {
+        return codec == o.codec && dev == o.dev && op == o.op && data_only == o.data_only && present == o.present;
+    }
+};
+
+constexpr int kMaxInFlight = 2;
+
+struct Coalescer {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<CoReq*> q;
+    int in_flight = 0;
+    uint64_t groups = 0, calls = 0;
+};
+
+Coalescer g_co;
+
+uint64_t group_cap_bytes() {
+    static const uint64_t cap = [] {
+        const char* e = std::getenv("HBEC_COALESCE_MB");
+        const long long v = e ? std::atoll(e) : 0;
+        return (uint64_t)(v > 0 ? v : 256) << 20;
+    }();
+    return cap;
+}
+
+// Code one group.  Direct per-call path for a group of one; else one batched
+// host-path call, falling back to per-member calls if that fails.
+void run_group(std::vector<CoReq*>& g, const DirectFns& fn) {
+    auto single = [&](CoReq* r) {
+        r->rc = r->op == 0 ? fn.encode(r->codec, r->base, r->s)
+                           : fn.reconstruct(r->codec, r->base, r->s, r->present.data(), r->data_only);
+        r->err = r->rc ? hbec_last_error() : "";
+    };
+    if (g.size() == 1) {
+        single(g[0]);
+        return;
+    }
+    std::vector<hbec_stripe> st(g.size());
+    for (size_t i = 0; i < g.size(); ++i) st[i] = hbec_stripe{g[i]->base, g[i]->s};
+    const CoReq& h = *g[0];
+    const int rc = h.op == 0 ? hbec_encode_host(h.codec, st.data(), st.size())
+                             : hbec_reconstruct_host(h.codec, st.data(), st.size(), h.present.data(), h.data_only);
+    if (rc == HBEC_OK) {
+        for (auto* r : g) r->rc = HBEC_OK;
+        return;
+    }
+    for (auto* r : g) single(r);
+}
+
+}  // namespace
+
+bool coalesce_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("HBEC_COALESCE");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+int coalesced_call(hbec_codec* codec, int op, uint8_t* base, uint64_t s, const uint8_t* present, int n_shards,
+                   int data_only, const DirectFns& fn) {
+    CoReq r;
+    r.codec = codec;
+    r.op = op;
+    r.base = base;
+    r.s = s;
+    r.data_only = data_only ? 1 : 0;
+    if (op == 1) {
+        r.present.assign(present, present + n_shards);
+        for (auto& v : r.present) v = v ? 1 : 0;
+    }
+    hipError_t e = hipGetDevice(&r.dev);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+    const uint64_t cap = group_cap_bytes();
+    std::unique_lock<std::mutex> lk(g_co.mu);
+    g_co.q.push_back(&r);
+    for (;;) {
+        if (r.done) break;
+        if (!r.taken && g_co.in_flight < kMaxInFlight) {
+            // lead: this call plus every queued call of the same group, up to cap bytes
+            std::vector<CoReq*> grp;
+            uint64_t bytes = 0;
+            for (CoReq* x : g_co.q) {
+                if (x->taken || !(x == &r || x->same_group(r))) continue;
+                const uint64_t b = x->s * (uint64_t)n_shards;
+                if (x != &r && bytes + b > cap) continue;
+                x->taken = true;
+                grp.push_back(x);
+                bytes += b;
+            }
+            g_co.q.erase(std::remove_if(g_co.q.begin(), g_co.q.end(), [](CoReq* x) { return x->taken; }),
+                         g_co.q.end());
+            ++g_co.in_flight;
+            ++g_co.groups;
+            g_co.calls += grp.size();
+            lk.unlock();
+            run_group(grp, fn);
+            lk.lock();
+            --g_co.in_flight;
+            for (auto* x : grp) x->done = true;
+            g_co.cv.notify_all();
+            continue;
+        }
+        g_co.cv.wait(lk);
+    }
+    lk.unlock();
+    return r.rc ? fail(r.rc, r.err) : HBEC_OK;
+}
+
+void coalesce_stats(uint64_t* groups, uint64_t* calls) {
+    std::lock_guard<std::mutex> g(g_co.mu);
+    if (groups) *groups = g_co.groups;
+    if (calls) *calls = g_co.calls;
+}
+
+}  // namespace hbec

@@ -89,11 +89,12 @@ static int device_blocks(int dev, int k, int r, int pipe, int force_stream, int*
         if (e != hipSuccess) return hip_fail(e, "hipGetDeviceProperties");
         d.cus = p.multiProcessorCount;
     }
-    const int key_k = force_stream ? -k : (pipe ? 1000 + k : k);
+    // pipe: 1 = pipelined kernel, 2 = packed kernel (short shards)
+    const int key_k = force_stream ? -k : (pipe == 2 ? 2000 + k : (pipe ? 1000 + k : k));
     auto it = d.blocks_per_cu.find({key_k, r});
     if (it == d.blocks_per_cu.end()) {
         int b = 0;
-        hipError_t e = vec_occupancy(k, r, pipe, force_stream, &b);
+        hipError_t e = pipe == 2 ? packed_occupancy(k, r, &b) : vec_occupancy(k, r, pipe, force_stream, &b);
         if (e != hipSuccess) return hip_fail(e, "occupancy query");
         if (b < 1) b = 1;
         it = d.blocks_per_cu.emplace(std::make_pair(key_k, r), b).first;
@@ -141,7 +142,34 @@ int apply_views(int rows, int cols, const uint8_t* coeffs, const hbec_view* in, 
             }
             a.shard_len = shard_len;
             a.accumulate = c0 > 0 ? 1u : 0u;
-            if (vec) {
+            if (vec && is_packed_shape(K, R, shard_len, c0 > 0, force_stream)) {
+                // short shards: wave tiles across objects (gf_apply_packed)
+                int cus = 0, per_cu = 0;
+                rc = device_blocks(dev, K, R, 2, 0, &cus, &per_cu);
+                if (rc) return rc;
+                const uint64_t spo = shard_len / 16;
+                const uint64_t te = (uint64_t)packed_tile_elems(K);
+                const uint64_t max_obj = std::max<uint64_t>(1, ((1ull << 31) - te) / spo);  // n_elems < 2^31
+                for (uint64_t o0 = 0; o0 < n_obj; o0 += max_obj) {
+                    const uint64_t no = std::min(max_obj, n_obj - o0);
+                    PassArgs b = a;
+                    for (int j = 0; j < K; ++j) b.in[j] = a.in[j] + o0 * a.in_stride[j];
+                    for (int r = 0; r < R; ++r) b.out[r] = a.out[r] + o0 * a.out_stride[r];
+                    b.n_obj = no;
+                    b.elems_per_obj = (uint32_t)spo;
+                    b.n_elems = (uint32_t)(no * spo);
+                    b.n_tiles = (uint32_t)((no * spo + te - 1) / te);
+                    const uint64_t wpb = (uint64_t)kPipeBlockThreads / 64;
+                    const uint64_t want_blocks = (b.n_tiles + wpb - 1) / wpb;
+                    const uint64_t cap = (uint64_t)cus * (uint64_t)(g_blocks_per_cu_override > 0
+                                                                         ? g_blocks_per_cu_override
+                                                                         : per_cu);
+                    int grid = (int)std::max<uint64_t>(1, std::min(want_blocks, cap));
+                    if (g_grid_cap > 0) grid = std::min(grid, g_grid_cap);
+                    hipError_t e = launch_packed(K, R, b, grid, stream);
+                    if (e != hipSuccess) return hip_fail(e, "launch gf_apply_packed");
+                }
+            } else if (vec) {
                 int cus = 0, per_cu = 0;
                 rc = device_blocks(dev, K, R, is_pipe_shape(K, R, shard_len, force_stream) && c0 == 0, force_stream,
                                    &cus, &per_cu);
@@ -425,6 +453,36 @@ static int host_apply(int rows, int cols, const uint8_t* coeffs, const uint8_t* 
     return HBEC_OK;
 }
 
+// Shards are the consecutive s-byte slots of one buffer (ecutils.go's databuf).
+static bool consecutive(uint8_t* const* shards, int n, size_t s) {
+    for (int i = 1; i < n; ++i)
+        if (shards[i] != shards[0] + (size_t)i * s) return false;
+    return true;
+}
+
+// Per-call paths over a databuf (no coalescing): a coalesced group of one.
+static int direct_encode(hbec_codec* c, uint8_t* base, uint64_t s) {
+    std::vector<uint8_t*> p((size_t)(c->k + c->m));
+    for (size_t i = 0; i < p.size(); ++i) p[i] = base + i * s;
+    return host_apply(c->m, c->k, c->matrix.data() + (size_t)c->k * c->k, p.data(), p.data() + c->k, s);
+}
+
+static int direct_reconstruct(hbec_codec* c, uint8_t* base, uint64_t s, const uint8_t* present, int data_only) {
+    const int n = c->k + c->m;
+    std::vector<uint8_t> p(present, present + n);
+    std::vector<int> surv, outs;
+    std::vector<uint8_t> rows;
+    int rc = decode_rows(c, p, data_only != 0, surv, outs, rows);
+    if (rc) return rc;
+    std::vector<const uint8_t*> in(surv.size());
+    std::vector<uint8_t*> out(outs.size());
+    for (size_t j = 0; j < surv.size(); ++j) in[j] = base + (size_t)surv[j] * s;
+    for (size_t o = 0; o < outs.size(); ++o) out[o] = base + (size_t)outs[o] * s;
+    return host_apply((int)outs.size(), c->k, rows.data(), in.data(), out.data(), s);
+}
+
+static const DirectFns kDirect = {direct_encode, direct_reconstruct};
+
 }  // namespace hbec
 
 using namespace hbec;
@@ -494,6 +552,10 @@ int hbec_encode(hbec_codec* c, uint8_t* const* shards, const size_t* lens, int n
         if (rc) return rc;
         for (int i = 0; i < n_shards; ++i)
             if (!shards[i]) return fail(HBEC_ERR_INVALID_ARG, "null shard pointer");
+        // one databuf's consecutive slots (every ecutils.go call site): join
+        // concurrent callers (coalesce.cpp)
+        if (coalesce_enabled() && consecutive(shards, n_shards, s))
+            return coalesced_call(c, 0, shards[0], s, nullptr, n_shards, 0, kDirect);
         return host_apply(c->m, c->k, c->matrix.data() + (size_t)c->k * c->k, shards, shards + c->k, s);
     });
 }
@@ -518,14 +580,17 @@ int hbec_reconstruct(hbec_codec* c, uint8_t* const* shards, size_t* lens, int n_
         std::vector<uint8_t> rows;
         rc = decode_rows(c, present, data_only != 0, surv, outs, rows);
         if (rc) return rc;
-        std::vector<const uint8_t*> in(surv.size());
-        std::vector<uint8_t*> out(outs.size());
-        for (size_t j = 0; j < surv.size(); ++j) in[j] = shards[surv[j]];
-        for (size_t o = 0; o < outs.size(); ++o) {
-            if (!shards[outs[o]]) return fail(HBEC_ERR_INVALID_ARG, "missing shard has no buffer");
-            out[o] = shards[outs[o]];
+        for (int o : outs)
+            if (!shards[o]) return fail(HBEC_ERR_INVALID_ARG, "missing shard has no buffer");
+        if (coalesce_enabled() && consecutive(shards, n_shards, s)) {
+            rc = coalesced_call(c, 1, shards[0], s, present.data(), n_shards, data_only, kDirect);
+        } else {
+            std::vector<const uint8_t*> in(surv.size());
+            std::vector<uint8_t*> out(outs.size());
+            for (size_t j = 0; j < surv.size(); ++j) in[j] = shards[surv[j]];
+            for (size_t o = 0; o < outs.size(); ++o) out[o] = shards[outs[o]];
+            rc = host_apply((int)outs.size(), c->k, rows.data(), in.data(), out.data(), s);
         }
-        rc = host_apply((int)outs.size(), c->k, rows.data(), in.data(), out.data(), s);
         if (rc) return rc;
         for (int i : outs) lens[i] = s;
         return HBEC_OK;
@@ -758,10 +823,8 @@ int hbec_encode_databuf(hbec_codec* c, uint8_t* databuf, size_t shard_len) {
     return hbec::guarded("hbec_encode_databuf", [&]() -> int {
         if (!c || !databuf) return fail(HBEC_ERR_INVALID_ARG, "null argument");
         if (shard_len == 0) return fail(HBEC_ERR_SHARD_NO_DATA, "no shard data");  // checkShards: all empty
-        std::vector<uint8_t*> p;
-        databuf_shards(c, databuf, shard_len, p);
-        std::vector<size_t> lens(p.size(), shard_len);
-        return hbec_encode(c, p.data(), lens.data(), (int)p.size());
+        if (coalesce_enabled()) return coalesced_call(c, 0, databuf, shard_len, nullptr, c->k + c->m, 0, kDirect);
+        return direct_encode(c, databuf, shard_len);
     });
 }
 
@@ -791,6 +854,13 @@ int hbec_verify_databuf(hbec_codec* c, const uint8_t* databuf, size_t shard_len,
     });
 }
 
+int hbec_coalesce_stats(uint64_t* groups, uint64_t* calls) {
+    return hbec::guarded("hbec_coalesce_stats", [&]() -> int {
+        coalesce_stats(groups, calls);
+        return HBEC_OK;
+    });
+}
+
 int hbec_set_force_stream(int on) {
     return hbec::guarded("hbec_set_force_stream", [&]() -> int {
         g_force_stream.store(on ? 1 : 0);
@@ -802,14 +872,15 @@ int hbec_kernel_info(int k, int r, uint64_t shard_len, int* tile_bytes, int* kin
     return hbec::guarded("hbec_kernel_info", [&]() -> int {
         if (k < 1 || k > kMaxK || r < 1 || r > kMaxR) return fail(HBEC_ERR_INVALID_ARG, "shape out of range");
         const int fs = g_force_stream.load();
-        const int pipe = is_pipe_shape(k, r, shard_len, fs);
-        if (tile_bytes) *tile_bytes = vec_tile_bytes(k, r, shard_len, 0, fs);
-        if (kind) *kind = is_streaming_shape(k, r, fs) ? 2 : (pipe ? 1 : 0);
+        const bool packed = r <= 3 && is_packed_shape(k, r, shard_len, 0, fs);
+        const int pipe = packed ? 2 : is_pipe_shape(k, r, shard_len, fs);
+        if (tile_bytes) *tile_bytes = packed ? packed_tile_elems(k) * 16 : vec_tile_bytes(k, r, shard_len, 0, fs);
+        if (kind) *kind = packed ? 3 : (is_streaming_shape(k, r, fs) ? 2 : (pipe ? 1 : 0));
         if (blocks_per_cu) {
             int dev = 0, cus = 0;
             int rc = current_device(&dev);
             if (rc) return rc;
-            rc = device_blocks(dev, k, r, pipe, fs, &cus, blocks_per_cu);
+            rc = device_blocks(dev, k, r, pipe, packed ? 0 : fs, &cus, blocks_per_cu);
             if (rc) return rc;
             if (g_blocks_per_cu_override > 0) *blocks_per_cu = g_blocks_per_cu_override;
         }

@@ -49,6 +49,18 @@ uint64_t pinned_device_addr(const void* p, uint64_t len);
 // each, device memory), digest of record i at digest + slot * 16.
 hipError_t launch_md5_list(const void* recs, uint64_t n, uint8_t* digest, bool aligned, hipStream_t stream);
 
+// Per-call codec paths the coalescer (coalesce.cpp) runs for a group of one.
+struct DirectFns {
+    int (*encode)(hbec_codec*, uint8_t* databuf, uint64_t s);
+    int (*reconstruct)(hbec_codec*, uint8_t* databuf, uint64_t s, const uint8_t* present, int data_only);
+};
+// Group commit of concurrent one-stripe calls (op 0 encode, 1 reconstruct)
+// on databuf-layout stripes (shard i at base + i*s, n_shards = k+m).
+bool coalesce_enabled();
+int coalesced_call(hbec_codec* codec, int op, uint8_t* base, uint64_t s, const uint8_t* present, int n_shards,
+                   int data_only, const DirectFns& fn);
+void coalesce_stats(uint64_t* groups, uint64_t* calls);
+
 struct TileRec;
 // Grid for a stripes launch of k inputs / r outputs over n_tiles records
 // (one block of 4 waves per CU at most, as the strided kernels).

@@ -35,8 +35,20 @@ struct PassArgs {
     uint32_t tiles_per_obj; // vec path: ceil(shard_len / vec_tile_bytes)
     uint32_t n_tiles;       // vec path: n_obj * tiles_per_obj (< 2^32)
     uint32_t accumulate;    // 1: out ^= result (passes 2.. over >kMaxK inputs)
+    uint32_t n_elems;       // packed path: n_obj * elems_per_obj (< 2^31)
+    uint32_t elems_per_obj; // packed path: shard_len / 16
     uint32_t pad_;
 };
+
+// Packed path (short shards, S < one pipelined tile, e.g. 8+3 of 4 KiB
+// objects: 512 B): wave tiles run along the concatenation of every object's
+// shard column, so one tile spans several objects and every lane is used.
+// Kernel kinds (hbec_kernel_info): 0 unrolled, 1 pipelined, 2 streaming, 3 packed.
+int is_packed_shape(int k, int r, uint64_t shard_len, int accumulate, int force_stream);
+// elements (16 B) per wave tile of the packed kernel for k inputs
+int packed_tile_elems(int k);
+hipError_t launch_packed(int k, int r, const PassArgs& a, int grid, hipStream_t stream);
+hipError_t packed_occupancy(int k, int r, int* blocks_per_cu);
 
 // Vec path launch: fully unrolled kernel for small shapes, streaming otherwise.
 int vec_tile_bytes(int k, int r, uint64_t shard_len, int accumulate, int force_stream);

@@ -22,6 +22,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
+
 #include "gf_device.h"
 #include "kernels.h"
 
@@ -233,7 +235,8 @@ template <int K, int R>
 struct PipeTile {
     uint64_t in[K];
     uint64_t out[R];
-    uint32_t valid;  // bytes of the tile inside the shard
+    uint32_t valid;  // bytes of the tile inside the shard (load clamp)
+    uint32_t live;   // bytes stored: valid, or 0 for a past-the-end stand-in tile
 };
 
 // Tuning knob (tile order): with HBEC_SWZ_G > 0, runs of HBEC_SWZ_C tiles
@@ -266,6 +269,7 @@ __device__ __forceinline__ void pipe_tile_coords(PipeTile<K, R>& b, const PassAr
     for (int r = 0; r < R; ++r) b.out[r] = reinterpret_cast<uint64_t>(a.out[r]) + obj * a.out_stride[r] + off;
     const uint64_t left = a.shard_len - off;
     b.valid = (uint32_t)(left < TILE ? left : TILE);
+    b.live = b.valid;
 }
 
 template <int K, int R, int U>
@@ -293,7 +297,7 @@ __device__ __forceinline__ void pipe2_store_(const u32x4 (&x)[U][K], const PassA
             gf_dot_lds<K, R>(acc, x[u], lg);
         else
             gf_dot<K, R>(acc, x[u], a.tab, tb);
-        if (FULL || off < b.valid) {
+        if (FULL || off < b.live) {
 #pragma unroll
             for (int r = 0; r < R; ++r) st16_addr(b.out[r] + off, acc[r]);
         }
@@ -301,20 +305,22 @@ __device__ __forceinline__ void pipe2_store_(const u32x4 (&x)[U][K], const PassA
 }
 
 // Tile t of the launch; past the end, the launch's last tile stands in: it is
-// loaded, coded and stored again with the same bytes its owner stores (the
-// outputs never alias the inputs).  No branch around loads or stores: a
+// loaded and coded (so the loop keeps one shape) but stores nothing (live =
+// 0, the masked partial-tile store path), so a caller whose outputs overlap
+// its inputs cannot see a stale re-store.  No branch around the loads: a
 // memory op under a branch makes the compiler drain everything in flight
 // (vmcnt(0)) at the join, which serialises the pipeline (measured 2x slower).
 template <int K, int R, int U>
 __device__ __forceinline__ void pipe_tile_at(PipeTile<K, R>& b, const PassArgs& a, uint32_t t, uint32_t n,
                                              uint32_t tpo) {
     pipe_tile_coords<K, R, U>(b, a, t < n ? t : n - 1u, tpo);
+    if (t >= n) b.live = 0;
 }
 
 template <int K, int R, int U>
 __device__ __forceinline__ void pipe2_finish(const u32x4 (&x)[U][K], const PassArgs& a, const Tables<K, R>& tb,
                                              const PipeTile<K, R>& cur, uint32_t lane, const LdsGf<K, R>& lg) {
-    if (cur.valid >= (uint32_t)U * 1024u)
+    if (cur.live >= (uint32_t)U * 1024u)
         pipe2_store_<K, R, U, true>(x, a, tb, cur, lane, lg);
     else
         pipe2_store_<K, R, U, false>(x, a, tb, cur, lane, lg);
@@ -377,6 +383,135 @@ __global__ __launch_bounds__(kPipeBlockThreads, HBEC_PIPE_WAVES_PER_SIMD) void g
         nxt = after;
     }
     pipe2_finish<K, R, U>(x, a, tb, cur, lane, lg);
+}
+
+// ---------------------------------------------------------------------------
+// gf_apply_packed: short shards (S < one pipelined tile; 8+3 of a 4 KiB
+// object has S = 512 B).  The per-object tiles above would leave lanes idle
+// (a 1 KiB tile over a 512-B shard loads the same line twice and stores
+// half), so here a wave tile is U x 64 consecutive 16-B ELEMENTS of the
+// concatenated shard columns of all objects: element e is byte (e % spo)*16
+// of object e / spo (spo = S/16).  Lane addresses are per lane (one object
+// per half-wave at S = 512 B: 512 contiguous bytes of each shard), and every
+// lane loads and stores live bytes.  Same pipeline as gf_apply_vec_pipe2:
+// the next tile's loads in flight while this tile computes and stores, one
+// block barrier per tile, block-uniform trip count (past-the-end waves load
+// the last tile and store nothing).
+template <int U>
+struct PackedCoord {
+    uint32_t obj[U];  // per lane
+    uint32_t off[U];  // per lane: byte offset inside the shard
+};
+
+template <int U>
+__device__ __forceinline__ void packed_coords(PackedCoord<U>& c, uint32_t t, uint32_t lane, uint32_t n_elems,
+                                              uint32_t spo, double inv) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        uint32_t e = (t * (uint32_t)U + (uint32_t)u) * 64u + lane;
+        e = e < n_elems ? e : n_elems - 1u;  // clamped lanes load live bytes, store nothing
+        uint32_t q = (uint32_t)((double)e * inv);  // e < 2^31: exact up to one step, fixed below
+        int32_t r = (int32_t)(e - q * spo);
+        if (r < 0) {
+            q -= 1u;
+            r += (int32_t)spo;
+        } else if (r >= (int32_t)spo) {
+            q += 1u;
+            r -= (int32_t)spo;
+        }
+        c.obj[u] = q;
+        c.off[u] = (uint32_t)r * 16u;
+    }
+}
+
+template <int K, int U>
+__device__ __forceinline__ void packed_load(u32x4 (&x)[U][K], const PassArgs& a, const PackedCoord<U>& c) {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int j = 0; j < K; ++j) x[u][j] = ld16(a.in[j] + (uint64_t)c.obj[u] * a.in_stride[j] + c.off[u]);
+}
+
+template <int K, int R, int U, bool FULL>
+__device__ __forceinline__ void packed_store_(const u32x4 (&x)[U][K], const PassArgs& a, const Tables<K, R>& tb,
+                                              const PackedCoord<U>& c, uint32_t t, uint32_t lane, uint32_t live) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        u32x4 acc[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r] = u32x4{0, 0, 0, 0};
+        gf_dot<K, R>(acc, x[u], a.tab, tb);
+        if (FULL || (t * (uint32_t)U + (uint32_t)u) * 64u + lane < live) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) st16(a.out[r] + (uint64_t)c.obj[u] * a.out_stride[r] + c.off[u], acc[r]);
+        }
+    }
+}
+
+// live = elements stored by this tile's lanes: n_elems, or 0 past the end
+template <int K, int R, int U>
+__device__ __forceinline__ void packed_finish(const u32x4 (&x)[U][K], const PassArgs& a, const Tables<K, R>& tb,
+                                              const PackedCoord<U>& c, uint32_t t, uint32_t n, uint32_t lane) {
+    const uint32_t live = t < n ? a.n_elems : 0u;
+    if (t < n && (t + 1u) * (uint32_t)U * 64u <= a.n_elems)
+        packed_store_<K, R, U, true>(x, a, tb, c, t, lane, live);
+    else
+        packed_store_<K, R, U, false>(x, a, tb, c, t, lane, live);
+}
+
+#ifndef HBEC_PACKED_SLEEP
+#define HBEC_PACKED_SLEEP 0  // x 64 cycles, K <= 4
+#endif
+#ifndef HBEC_PACKED_SLEEP_BIG
+#define HBEC_PACKED_SLEEP_BIG 0  // x 64 cycles, K > 4
+#endif
+
+#ifndef HBEC_PACKED_U_BIG
+#define HBEC_PACKED_U_BIG 1  // KiB per input per wave tile for K > 4 (0: pipe_u's 3 KiB)
+#endif
+#ifndef HBEC_PACKED_BARRIER
+#define HBEC_PACKED_BARRIER 1
+#endif
+__host__ __device__ constexpr int packed_u(int k) {
+    return (k > 4 && HBEC_PACKED_U_BIG > 0) ? HBEC_PACKED_U_BIG : pipe_u(k);
+}
+
+template <int K, int R>
+__global__ __launch_bounds__(kPipeBlockThreads, HBEC_PIPE_WAVES_PER_SIMD) void gf_apply_packed(PassArgs a) {
+    constexpr int U = packed_u(K);
+    constexpr uint32_t WPB = kPipeBlockThreads / 64;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t nw = gridDim.x * WPB;
+    const uint32_t wave0 = __builtin_amdgcn_readfirstlane(xcd_block() * WPB);
+    const uint32_t dw = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t n = a.n_tiles;
+    if (wave0 >= n) return;  // whole blocks only: the loop below has block barriers
+    const Tables<K, R> tb = load_tables<K, R>(a.tab);
+    const uint32_t spo = a.elems_per_obj;
+    const double inv = 1.0 / (double)spo;
+    uint32_t t = wave0 + dw;
+    PackedCoord<U> cur;
+    packed_coords<U>(cur, t < n ? t : n - 1u, lane, a.n_elems, spo, inv);
+    u32x4 x[U][K];
+    packed_load<K, U>(x, a, cur);
+    for (uint32_t b0 = wave0 + nw; b0 < n; b0 += nw) {  // block-uniform trip count
+        const uint32_t tn = b0 + dw;
+        PackedCoord<U> nxt;
+        packed_coords<U>(nxt, tn < n ? tn : n - 1u, lane, a.n_elems, spo, inv);
+        u32x4 y[U][K];
+        packed_load<K, U>(y, a, nxt);
+        if (HBEC_PACKED_SLEEP > 0 && K <= 4) __builtin_amdgcn_s_sleep(HBEC_PACKED_SLEEP);
+        if (HBEC_PACKED_SLEEP_BIG > 0 && K > 4) __builtin_amdgcn_s_sleep(HBEC_PACKED_SLEEP_BIG);
+        if (HBEC_PACKED_BARRIER) __builtin_amdgcn_s_barrier();
+        packed_finish<K, R, U>(x, a, tb, cur, t, n, lane);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int j = 0; j < K; ++j) x[u][j] = y[u][j];
+        cur = nxt;
+        t = tn;
+    }
+    packed_finish<K, R, U>(x, a, tb, cur, t, n, lane);
 }
 
 // Streaming vec path (runtime K): one input shard at a time with the next
@@ -558,6 +693,82 @@ static const void* stream_kernel(int r) {
 
 int is_streaming_shape(int k, int r, int force_stream) {
     return (force_stream || !unrolled_kernel(k, r, false)) ? 1 : 0;
+}
+
+#ifndef HBEC_USE_PACKED
+#define HBEC_USE_PACKED 1
+#endif
+
+template <int K>
+static const void* packed_for_r(int r) {
+    switch (r) {
+        case 1: return reinterpret_cast<const void*>(&gf_apply_packed<K, 1>);
+        case 2: return reinterpret_cast<const void*>(&gf_apply_packed<K, 2>);
+        case 3: return reinterpret_cast<const void*>(&gf_apply_packed<K, 3>);
+    }
+    return nullptr;
+}
+
+static const void* packed_kernel(int k, int r) {
+    switch (k) {
+        case 1: return packed_for_r<1>(r);
+        case 2: return packed_for_r<2>(r);
+        case 3: return packed_for_r<3>(r);
+        case 4: return packed_for_r<4>(r);
+        case 5: return packed_for_r<5>(r);
+        case 6: return packed_for_r<6>(r);
+        case 7: return packed_for_r<7>(r);
+        case 8: return packed_for_r<8>(r);
+    }
+    return nullptr;
+}
+
+int packed_tile_elems(int k) { return packed_u(k) * 64; }
+
+// Tuning knobs: HBEC_PACKED=0 sends short shards back to gf_apply_vec (A/B);
+// HBEC_PACKED_MAX_SHARD=B takes shards shorter than B bytes (instead of
+// shorter than one pipelined tile) through the packed kernel.
+static const bool g_packed_on = [] {
+    const char* e = std::getenv("HBEC_PACKED");
+    return !(e && e[0] == '0');
+}();
+static const uint64_t g_packed_max = [] {
+    const char* e = std::getenv("HBEC_PACKED_MAX_SHARD");
+    return e ? (uint64_t)std::atoll(e) : 0ull;
+}();
+
+int is_packed_shape(int k, int r, uint64_t shard_len, int accumulate, int force_stream) {
+    return (HBEC_USE_PACKED && g_packed_on && !force_stream && !accumulate && shard_len >= 16 && shard_len % 16 == 0 &&
+            shard_len < (g_packed_max ? g_packed_max : (uint64_t)pipe_u(k) * 1024u) &&
+            packed_kernel(k, r) != nullptr)
+               ? 1
+               : 0;
+}
+
+hipError_t launch_packed(int k, int r, const PassArgs& a, int grid, hipStream_t stream) {
+    const void* fn = packed_kernel(k, r);
+    if (!fn) return hipErrorInvalidValue;
+    void* args[] = {const_cast<PassArgs*>(&a)};
+    return hipLaunchKernel(fn, dim3(grid), dim3(kPipeBlockThreads), args, 0, stream);
+}
+
+// Resident 4-wave blocks per CU for the packed kernel: K <= 4 streams best
+// with 2 (short tiles: more waves keep enough bytes in flight), K > 4 with 1
+// (profiles/r02_tune_packed*.jsonl).
+#ifndef HBEC_PACKED_BLOCKS_SMALL
+#define HBEC_PACKED_BLOCKS_SMALL 2
+#endif
+#ifndef HBEC_PACKED_BLOCKS_BIG
+#define HBEC_PACKED_BLOCKS_BIG 1
+#endif
+
+hipError_t packed_occupancy(int k, int r, int* blocks_per_cu) {
+    const void* fn = packed_kernel(k, r);
+    if (!fn) return hipErrorInvalidValue;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, kPipeBlockThreads, 0);
+    const int cap = k <= 4 ? HBEC_PACKED_BLOCKS_SMALL : HBEC_PACKED_BLOCKS_BIG;
+    if (e == hipSuccess && cap > 0 && *blocks_per_cu > cap) *blocks_per_cu = cap;
+    return e;
 }
 
 // The pipelined kernel wants whole tiles; short shards (e.g. 8+3 of a 4 KiB

@@ -131,3 +131,31 @@ def hexdigests(digests):
         res.append(out[i:i + shape[1]])
         i += shape[1]
     return res
+
+
+def audit_ec_shard(body, content_length: str, ec_scheme: str, index_hash: str):
+    """ecAuditor.AuditItem for a stable EC shard (objectserver/auditor.go:100-158,
+    the md5BytesPerSec > 0 branch) over the library: the shard file must be
+    ecShardLength(Content-Length, k) bytes (hbec_parse_ec_scheme +
+    hbec_ec_shard_length), then its MD5, hashed on the GPU (hbec_md5_host),
+    must equal the index's ShardHash.  Returns (bytes, error or None), as
+    AuditItem returns (int64, error): (0, err) on a size mismatch, (n, err)
+    on a hash mismatch."""
+    import re
+
+    from . import ecutils as E
+    from .reedsolomon import ErrScheme
+
+    if not re.fullmatch(r"[+-]?[0-9]+", content_length or ""):  # strconv.ParseInt(s, 10, 64)
+        return 0, f"Error parsing content-length from metadata: {content_length!r}"
+    try:
+        _, ds, _, _ = E.parse_ec_scheme(ec_scheme)
+    except ErrScheme as e:
+        return 0, f"Error decoding ec-scheme: {e}"
+    f_bytes = E.ec_shard_length(int(content_length), ds)
+    if f_bytes != len(body):
+        return 0, f"File size ({len(body)}) doesn't match metadata ({f_bytes})"
+    (calc,) = md5_host([body])
+    if calc != index_hash:
+        return len(body), "File contents don't match object hash"
+    return len(body), None

@@ -101,6 +101,16 @@ int hbec_reconstruct_databuf(hbec_codec* codec, uint8_t* databuf, size_t shard_l
                              int data_only);
 int hbec_verify_databuf(hbec_codec* codec, const uint8_t* databuf, size_t shard_len, int* ok);
 
+/* Concurrent per-call Encode / Reconstruct / ReconstructData on databuf
+ * stripes (the *_databuf entries, and hbec_encode / hbec_reconstruct when
+ * the shard pointers are one buffer's consecutive slots) are coalesced: a
+ * call that finds fewer than two groups in flight codes itself plus every
+ * queued call of the same (device, codec, op, erasure pattern) with one
+ * host-path call (up to HBEC_COALESCE_MB, 256 MiB); a lone call runs at once.
+ * HBEC_COALESCE=0 turns this off.  Counters since load: groups run and calls
+ * they carried. */
+int hbec_coalesce_stats(uint64_t* groups, uint64_t* calls);
+
 /* ---------------------------------------------------------------------------
  * Device-resident batches (the GPU hot path).  A view places shard i of
  * object o at base + o * obj_stride in device memory.  Work is queued on

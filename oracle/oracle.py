@@ -450,3 +450,25 @@ def object_seed(base_seed: int, i: int) -> int:
 
 def object_bytes(i: int, n: int, base_seed: int = HBEC_SEED) -> np.ndarray:
     return splitmix_bytes(object_seed(base_seed, i), n)
+
+
+def audit_ec_shard(body: bytes, content_length: str, ec_scheme: str, index_hash: str):
+    """ecAuditor.AuditItem for a stable EC shard (objectserver/auditor.go:100-158,
+    md5BytesPerSec > 0): the file must be ecShardLength(Content-Length, k)
+    bytes, then its MD5 must equal the index's ShardHash.  Returns
+    (bytes, error message or None) as AuditItem returns (int64, error)."""
+    import re
+
+    if not re.fullmatch(r"[+-]?[0-9]+", content_length or ""):  # strconv.ParseInt(s, 10, 64)
+        return 0, f"Error parsing content-length from metadata: {content_length!r}"
+    cl = int(content_length)
+    try:
+        _, ds, _, _ = parse_ec_scheme(ec_scheme)
+    except ValueError as e:
+        return 0, f"Error decoding ec-scheme: {e}"
+    f_bytes = ec_shard_length(cl, ds)
+    if f_bytes != len(body):
+        return 0, f"File size ({len(body)}) doesn't match metadata ({f_bytes})"
+    if shard_hash(body) != index_hash:
+        return len(body), "File contents don't match object hash"
+    return len(body), None

@@ -6,7 +6,12 @@
  *
  *   gcc -O2 -std=c11 -pthread -Iinclude scripts/bench_batcher.c -Lhummingbird_amd -lhbec \
  *       -Wl,-rpath,$PWD/hummingbird_amd -o /tmp/bench_batcher
- *   /tmp/bench_batcher THREADS PER_THREAD PINNED MAX_BATCH_MB MAX_WAIT_US
+ *   /tmp/bench_batcher THREADS PER_THREAD PINNED MAX_BATCH_MB MAX_WAIT_US [MODE]
+ *
+ * MODE 0 (default): hbec_batcher_encode (the explicit batching driver);
+ * MODE 1: plain per-call hbec_encode_databuf (the 3-line shim swap of
+ *         INTEGRATION.md), coalesced inside the library (HBEC_COALESCE=0 in
+ *         the environment measures it uncoalesced).
  *
  * Prints one JSON line: object-data GiB/s, us per object, batches; checks
  * every stripe's parity afterwards with hbec_verify.
@@ -24,6 +29,8 @@
 enum { K = 4, M = 2, S = 1 << 18 };
 
 typedef struct {
+    hbec_codec* codec;
+    int mode;
     hbec_batcher* bat;
     uint8_t* pool;
     int first, count;
@@ -39,8 +46,13 @@ static double now(void) {
 static void* caller(void* arg) {
     Job* j = (Job*)arg;
     for (int i = j->first; i < j->first + j->count && !j->rc; ++i) {
-        hbec_stripe st = {j->pool + (size_t)i * (K + M) * S, S};
-        j->rc = hbec_batcher_encode(j->bat, &st);
+        uint8_t* base = j->pool + (size_t)i * (K + M) * S;
+        if (j->mode == 1) {
+            j->rc = hbec_encode_databuf(j->codec, base, S);
+        } else {
+            hbec_stripe st = {base, S};
+            j->rc = hbec_batcher_encode(j->bat, &st);
+        }
     }
     return NULL;
 }
@@ -51,6 +63,7 @@ int main(int argc, char** argv) {
     const int pinned = argc > 3 ? atoi(argv[3]) : 1;
     const uint64_t max_mb = argc > 4 ? (uint64_t)atoll(argv[4]) : 96;
     const uint32_t wait_us = argc > 5 ? (uint32_t)atoi(argv[5]) : 300;
+    const int mode = argc > 6 ? atoi(argv[6]) : 0;
     if (threads < 1 || threads > 1024 || per < 1) return 2;
     const size_t n = (size_t)threads * per, stripe = (size_t)(K + M) * S;
     uint8_t* pool = NULL;
@@ -80,15 +93,16 @@ int main(int argc, char** argv) {
     /* warm-up: one stripe per caller, all at once, so every worker has made
      * its ring before the clock starts (a long-running server's steady state) */
     for (int t = 0; t < threads; ++t) {
-        jobs[t] = (Job){bat, pool, t * per, 1, 0};
+        jobs[t] = (Job){codec, mode, bat, pool, t * per, 1, 0};
         pthread_create(&th[t], NULL, caller, &jobs[t]);
     }
     for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
     uint64_t b0 = 0, s0 = 0;
-    hbec_batcher_stats(bat, &b0, &s0);
+    if (mode == 1) hbec_coalesce_stats(&b0, &s0);
+    else hbec_batcher_stats(bat, &b0, &s0);
     const double t0 = now();
     for (int t = 0; t < threads; ++t) {
-        jobs[t] = (Job){bat, pool, t * per, per, 0};
+        jobs[t] = (Job){codec, mode, bat, pool, t * per, per, 0};
         pthread_create(&th[t], NULL, caller, &jobs[t]);
     }
     int rc = 0;
@@ -98,7 +112,8 @@ int main(int argc, char** argv) {
     }
     const double secs = now() - t0;
     uint64_t b1 = 0, s1 = 0;
-    hbec_batcher_stats(bat, &b1, &s1);
+    if (mode == 1) hbec_coalesce_stats(&b1, &s1);
+    else hbec_batcher_stats(bat, &b1, &s1);
     hbec_batcher_free(bat);
     if (rc) { fprintf(stderr, "batcher: %s\n", hbec_last_error()); return 1; }
     int bad = 0;
@@ -112,9 +127,11 @@ int main(int argc, char** argv) {
         int ok = 0;
         if (hbec_verify(codec, sh, lens, K + M, &ok) || !ok) bad = 1;
     }
-    printf("{\"measure\": \"batcher_native_callers_Encode_1MiB_%s\", \"threads\": %d, \"objects\": %zu, "
+    const char* co = getenv("HBEC_COALESCE");
+    printf("{\"measure\": \"%s_native_callers_Encode_1MiB_%s\", \"threads\": %d, \"objects\": %zu, "
            "\"max_batch_MiB\": %llu, \"max_wait_us\": %u, \"seconds\": %.4f, \"object_data_GiB_s\": %.2f, "
            "\"us_per_object\": %.1f, \"batches\": %llu, \"parity_ok\": %s}\n",
+           mode == 1 ? (co && co[0] == '0' ? "percall_databuf_uncoalesced" : "percall_databuf_coalesced") : "batcher",
            pinned ? "pinned" : "pageable", threads, n, (unsigned long long)max_mb, wait_us, secs,
            n * (double)K * S / secs / (double)(1 << 30), secs / n * 1e6, (unsigned long long)(b1 - b0),
            bad ? "false" : "true");

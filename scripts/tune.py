@@ -30,6 +30,35 @@ T4 = BASE + ["HBEC_TILE_MID=4"]
 P = T1 + ["HBEC_USE_PIPE=1"]
 VARIANTS = {
     "cur": ([], {}),
+    # packed kernel (short shards, e.g. 8+3 of 4 KiB objects)
+    "pk_vec": ([], {"HBEC_PACKED": "0"}),
+    "pk_s4": (["HBEC_PACKED_SLEEP_BIG=4"], {}),
+    "pk_s8": (["HBEC_PACKED_SLEEP_BIG=8"], {}),
+    "pk_u1": (["HBEC_PACKED_U_BIG=1"], {}),
+    "pk_u2": (["HBEC_PACKED_U_BIG=2"], {}),
+    "pk_u1s8": (["HBEC_PACKED_U_BIG=1", "HBEC_PACKED_SLEEP_BIG=8"], {}),
+    "pk_u2s4": (["HBEC_PACKED_U_BIG=2", "HBEC_PACKED_SLEEP_BIG=4"], {}),
+    "pk_nobar": (["HBEC_PACKED_BARRIER=0"], {}),
+    "pk_sb1": (["HBEC_PACKED_BLOCKS_SMALL=1"], {}),
+    "pk_sb3": (["HBEC_PACKED_BLOCKS_SMALL=3"], {}),
+    "pk_sb4": (["HBEC_PACKED_BLOCKS_SMALL=4"], {}),
+    "pk_sb2s4": (["HBEC_PACKED_SLEEP=4"], {}),
+    "pk_sb2nb": (["HBEC_PACKED_BARRIER=0"], {}),
+    "pk_max2k": ([], {"HBEC_PACKED_MAX_SHARD": "2048"}),
+    "pk_max2k_sb1": (["HBEC_PACKED_BLOCKS_SMALL=1"], {"HBEC_PACKED_MAX_SHARD": "2048"}),
+    "pk_max512k": ([], {"HBEC_PACKED_MAX_SHARD": "524288"}),
+    "pk_max512k_sb1": (["HBEC_PACKED_BLOCKS_SMALL=1"], {"HBEC_PACKED_MAX_SHARD": "524288"}),
+    "pk_u3": (["HBEC_PACKED_U_BIG=3"], {}),
+    "pk_u3nb": (["HBEC_PACKED_U_BIG=3", "HBEC_PACKED_BARRIER=0"], {}),
+    "pk_u1s2": (["HBEC_PACKED_SLEEP_BIG=2"], {}),
+    "pk_u1s4": (["HBEC_PACKED_SLEEP_BIG=4"], {}),
+    "pk_sl0": (["HBEC_PACKED_SLEEP=0"], {}),
+    "pk_sl4": (["HBEC_PACKED_SLEEP=4"], {}),
+    "pk_sl12": (["HBEC_PACKED_SLEEP=12"], {}),
+    "pk_nb_sl0": (["HBEC_PACKED_BARRIER=0", "HBEC_PACKED_SLEEP=0"], {}),
+    "pk_b2": ([], {"HBEC_BLOCKS_PER_CU": "2"}),
+    "pk_u1b2": (["HBEC_PACKED_U_BIG=1"], {"HBEC_BLOCKS_PER_CU": "2"}),
+    "pk_u1b4": (["HBEC_PACKED_U_BIG=1"], {"HBEC_BLOCKS_PER_CU": "4"}),
     "d": ([], {}),
     "v2": (["HBEC_PIPE_V2=1"], {}),
     "v2all": (["HBEC_PIPE_V2_MAXK=16"], {}),
@@ -161,13 +190,13 @@ def build(names):
 _HOLD = []  # buffers of earlier runs (--allocs): kept so the next run's land elsewhere
 
 
-def run(names, rounds, n_obj, launches, k=4, m=2):
+def run(names, rounds, n_obj, launches, k=4, m=2, size=1 << 20):
     import torch
 
     from hummingbird_amd import _native as N
 
     torch.cuda.set_device(0)
-    s = (1 << 20) // k
+    s = size // k
     e = min(m, 3)  # erased data shards 0..e-1
     libs = {}
     for n in names:
@@ -501,6 +530,7 @@ if __name__ == "__main__":
     ap.add_argument("--rounds", type=int, default=12)
     ap.add_argument("--objects", type=int, default=4096)
     ap.add_argument("--launches", type=int, default=5)
+    ap.add_argument("--size", type=int, default=1 << 20, help="object bytes (shard = size / k)")
     ap.add_argument("--k", type=int, default=4)
     ap.add_argument("--m", type=int, default=2)
     ap.add_argument("--allocs", type=int, default=1,
@@ -526,4 +556,4 @@ if __name__ == "__main__":
         for i in range(a.allocs):
             if a.allocs > 1:
                 print(json.dumps({"alloc_set": i}), flush=True)
-            run(names, a.rounds, a.objects, a.launches, a.k, a.m)
+            run(names, a.rounds, a.objects, a.launches, a.k, a.m, a.size)

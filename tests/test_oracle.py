@@ -179,3 +179,94 @@ def test_shard_hash_vectors(vectors):
     v = vectors["shard_hashes_4_2_chunk1k"]
     body = bytes(O.object_bytes(v["object"], v["len"]))
     assert O.ec_split_hashes(4, 2, body, v["chunk"]) == v["hashes"]
+
+
+# ---- second derivation: Lagrange closed form, no matrix inversion (oracle/lagrange.py)
+@pytest.mark.parametrize("k,m", [(1, 1), (2, 1), (3, 2), (4, 2), (5, 5), (8, 3), (10, 4), (12, 4), (17, 3), (32, 8)])
+def test_lagrange_matrix_equals_gauss_jordan(k, m):
+    """The closed-form rows (prod (r-b)/(a-b)) equal Vandermonde x inv(top)
+    built by Gauss-Jordan in both restatements (oracle.py and the C oracle)."""
+    from oracle import lagrange as L
+
+    want = L.coding_matrix(k, m)
+    assert O.build_matrix(k, k + m) == want
+    assert CO.build_matrix(k, m).tolist() == want
+
+
+def test_lagrange_parity_rows_vectors(vectors):
+    from oracle import lagrange as L
+
+    for shape, rows in vectors["parity_rows"].items():
+        k, m = map(int, shape.split("+"))
+        assert L.parity_rows(k, m) == rows, shape
+
+
+def test_lagrange_one_encode_kat(kats):
+    """klauspost TestOneEncode (5+5) through the closed-form rows alone."""
+    from oracle import lagrange as L
+
+    kat = kats["one_encode"]
+    data = kat["data"]
+    rows = L.parity_rows(5, 5)
+    got = [[0, 0] for _ in range(5)]
+    for r in range(5):
+        for b in range(2):
+            v = 0
+            for j in range(5):
+                v ^= O.gal_mul(rows[r][j], data[j][b])
+            got[r][b] = v
+    assert got == kat["parity"]
+
+
+def test_lagrange_decode_rows_erasure_vectors(vectors):
+    """Decode rows of every recorded erasure pattern (first k present shards
+    as survivors) from the closed form, against the committed vectors."""
+    from oracle import lagrange as L
+
+    for case in vectors["erasures"]:
+        k, m = case["k"], case["m"]
+        for p in case["patterns"]:
+            present = [0 if i in p["missing"] else 1 for i in range(k + m)]
+            surv, outs, rows = L.decode_rows(k, m, present, data_only=True)
+            assert surv == p["survivors"]
+            assert rows == p["data_rows"], p["missing"]
+
+
+@pytest.mark.parametrize("k,m,max_e", [(4, 2, 2), (8, 3, 3), (10, 4, 2)])
+def test_lagrange_decode_rows_equal_product_rows(k, m, max_e):
+    """The product's fused decode rows (hbec_decode_rows: inv(sub) rows for
+    data, M_p x inv(sub) for parity) against the closed form, every pattern.
+    Host logic only: no device."""
+    import itertools
+
+    from hummingbird_amd import reedsolomon as RS
+    from oracle import lagrange as L
+
+    enc = RS.New(k, m)
+    for e in range(1, max_e + 1):
+        for missing in itertools.combinations(range(k + m), e):
+            present = [0 if i in missing else 1 for i in range(k + m)]
+            for data_only in (False, True):
+                surv, outs, rows = enc.DecodeRows(present, data_only=data_only)
+                lsurv, louts, lrows = L.decode_rows(k, m, present, data_only)
+                assert (surv, outs) == (lsurv, louts)
+                assert rows.tolist() == lrows, (missing, data_only)
+
+
+# ---- reference-held auditor fixtures (auditor_test.go:583-661)
+def test_auditor_ec_fixtures_oracle(kats):
+    for c in kats["auditor_ec"]["cases"]:
+        got, err = O.audit_ec_shard(c["body"].encode(), c["content_length"], c["ec_scheme"], c["shard_hash"])
+        assert got == c["bytes"], c["test"]
+        assert (err is None) == c["ok"], (c["test"], err)
+
+
+def test_auditor_size_rule_product_host(kats):
+    """The size half of the audit (ecShardLength(Content-Length, k) from the
+    Ec-Scheme) through the library's host entries; no device."""
+    from hummingbird_amd import ecutils as E
+
+    for c in kats["auditor_ec"]["cases"]:
+        _, ds, _, _ = E.parse_ec_scheme(c["ec_scheme"])
+        size_ok = E.ec_shard_length(int(c["content_length"]), ds) == len(c["body"])
+        assert size_ok == (c["test"] != "TestAuditShardFailLength"), c["test"]
