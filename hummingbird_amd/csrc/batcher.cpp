@@ -15,6 +15,15 @@
 // between them, so one batch's callers can wake up and queue their next
 // stripes while another batch is on the GPU: the per-batch wake-up, fill and
 // launch overheads overlap the other batch's transfer.
+//
+// Encode + ShardHash requests have workers of their own
+// (HBEC_BATCHER_MD5_WORKERS, default 4).  An MD5 chain is strictly serial,
+// one GPU lane per shard (md5.hip): a 256 KiB shard takes ~2.3 ms however
+// small the batch, so a worker that waits for its batch's digests is
+// latency-bound.  With several hashing workers, batch i's hashes run on the
+// GPU while batches i+1.. are encoded and hashed: encode + hash throughput
+// grows with the number of waiting callers instead of stopping at one batch
+// per 2.3 ms, and plain Encode batches never queue behind a hash.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -63,61 +72,113 @@ struct hbec_batcher {
     std::deque<Request*> queue;
     bool stop = false;
     uint64_t batch_cap = 0;  // bytes one worker takes per batch: max_batch_bytes / workers
+    int md5_workers = 0;     // workers reserved for Encode + ShardHash groups
+    uint64_t md5_cap = 0;    // bytes one MD5 worker takes: max_batch_bytes / md5_workers
     std::vector<std::thread> workers;
     // statistics
     uint64_t batches = 0, stripes = 0;
 
-    void run() {
+    // Code one homogeneous group with one host-path call; if that call fails,
+    // retry each member alone so every caller gets its own result.
+    int code(const std::vector<Request*>& batch, int n_shards) {
+        auto one = [&](const std::vector<Request*>& g) -> int {
+            std::vector<hbec_stripe> st(g.size());
+            for (size_t i = 0; i < g.size(); ++i) st[i] = g[i]->stripe;
+            if (g[0]->op == 0) return hbec_encode_host(codec, st.data(), st.size());
+            if (g[0]->op == 2) {
+                std::vector<uint8_t> dig(st.size() * (size_t)n_shards * 16);
+                const int rc = hbec_encode_host_md5(codec, st.data(), st.size(), dig.data());
+                if (rc == HBEC_OK)
+                    for (size_t i = 0; i < g.size(); ++i)
+                        std::memcpy(g[i]->digests, dig.data() + i * (size_t)n_shards * 16, (size_t)n_shards * 16);
+                return rc;
+            }
+            return hbec_reconstruct_host(codec, st.data(), st.size(), g[0]->present.data(), g[0]->data_only);
+        };
+        int rc = one(batch);
+        std::string err = rc ? hbec_last_error() : "";
+        if (rc == HBEC_OK || batch.size() == 1) {
+            for (auto* r : batch) {
+                r->rc = rc;
+                r->err = err;
+            }
+            return rc;
+        }
+        for (auto* r : batch) {
+            r->rc = one({r});
+            r->err = r->rc ? hbec_last_error() : "";
+        }
+        return rc;
+    }
+
+    // md5_only: this worker takes only Encode + ShardHash groups; otherwise
+    // it takes any group except those (when MD5 workers exist)
+    void run(bool md5_only) {
         (void)hipSetDevice(device);
         std::unique_lock<std::mutex> lk(mu);
+        const int n_shards = hbec_data_shards(codec) + hbec_parity_shards(codec);
         for (;;) {
-            cv_work.wait(lk, [&] { return stop || !queue.empty(); });
-            if (queue.empty() && stop) return;
+            auto mine = [&](const Request* r) { return md5_workers == 0 || (r->op == 2) == md5_only; };
+            auto first_mine = [&]() -> Request* {
+                for (auto* r : queue)
+                    if (mine(r)) return r;
+                return nullptr;
+            };
+            cv_work.wait(lk, [&] { return stop || first_mine() != nullptr; });
+            if (stop && !first_mine()) return;
             // let the batch fill: until max bytes queued or max_wait after the oldest arrived
             const auto deadline = std::chrono::steady_clock::now() + max_wait;
-            const int n_shards = hbec_data_shards(codec) + hbec_parity_shards(codec);
+            // MD5 groups stay smaller (max_batch_bytes / md5 workers): a group
+            // is held ~2.3 ms by its hash however small it is, so the bytes
+            // are better spread over more workers hashing at once
+            const uint64_t cap = md5_only && md5_workers > 0 ? md5_cap : batch_cap;
             while (!stop) {
                 uint64_t queued = 0;
-                for (auto* r : queue) queued += r->stripe.shard_len * (uint64_t)n_shards;
-                if (queued >= batch_cap) break;
+                for (auto* r : queue)
+                    if (mine(r)) queued += r->stripe.shard_len * (uint64_t)n_shards;
+                if (queued >= cap) break;
                 if (cv_work.wait_until(lk, deadline) == std::cv_status::timeout) break;
             }
-            if (queue.empty()) continue;  // another worker took it while this one waited
-            // take one homogeneous group (same op and erasure pattern) from the front
+            const Request* head = first_mine();
+            if (!head) continue;  // another worker took it while this one waited
+            // one homogeneous group (same op and erasure pattern as the oldest
+            // request), gathered from the WHOLE queue: a request of another
+            // kind between them does not split the batch
             std::vector<Request*> batch;
             uint64_t bytes = 0;
-            while (!queue.empty()) {
-                Request* r = queue.front();
-                if (!batch.empty() && (r->op != batch[0]->op || r->present != batch[0]->present ||
-                                       r->data_only != batch[0]->data_only))
-                    break;
+            for (auto it = queue.begin(); it != queue.end();) {
+                Request* r = *it;
+                const bool same = r->op == head->op && r->present == head->present && r->data_only == head->data_only;
                 const uint64_t b = r->stripe.shard_len * (uint64_t)n_shards;
-                if (!batch.empty() && bytes + b > batch_cap) break;
-                batch.push_back(r);
-                bytes += b;
-                queue.pop_front();
+                if (same && (batch.empty() || bytes + b <= cap)) {
+                    batch.push_back(r);
+                    bytes += b;
+                    it = queue.erase(it);
+                } else {
+                    ++it;
+                }
             }
             lk.unlock();
-            std::vector<hbec_stripe> st(batch.size());
-            for (size_t i = 0; i < batch.size(); ++i) st[i] = batch[i]->stripe;
-            int rc;
-            if (batch[0]->op == 0) {
-                rc = hbec_encode_host(codec, st.data(), st.size());
-            } else if (batch[0]->op == 2) {
-                std::vector<uint8_t> dig(st.size() * (size_t)n_shards * 16);
-                rc = hbec_encode_host_md5(codec, st.data(), st.size(), dig.data());
-                if (rc == HBEC_OK)
-                    for (size_t i = 0; i < batch.size(); ++i)
-                        std::memcpy(batch[i]->digests, dig.data() + i * (size_t)n_shards * 16, (size_t)n_shards * 16);
-            } else
-                rc = hbec_reconstruct_host(codec, st.data(), st.size(), batch[0]->present.data(), batch[0]->data_only);
-            const std::string err = rc ? hbec_last_error() : "";
+            // no exception may escape the worker (std::terminate): a throw before
+            // the per-request results were recorded fails the whole group
+            int thrown = HBEC_OK;
+            try {
+                (void)code(batch, n_shards);
+            } catch (const std::bad_alloc&) {
+                thrown = HBEC_ERR_NOMEM;
+            } catch (...) {
+                thrown = HBEC_ERR_DEVICE;
+            }
+            if (thrown != HBEC_OK)
+                for (auto* r : batch) {
+                    r->rc = thrown;
+                    r->err = thrown == HBEC_ERR_NOMEM ? "batcher: host allocation failed"
+                                                      : "batcher: unexpected exception";
+                }
             for (auto* r : batch) {
                 // notify while holding r->m: the caller cannot see `done`, return and
                 // destroy r (it lives on the caller's stack) before this scope ends
                 std::lock_guard<std::mutex> g(r->m);
-                r->rc = rc;
-                r->err = err;
                 r->done = true;
                 r->cv.notify_one();
             }
@@ -128,6 +189,11 @@ struct hbec_batcher {
     }
 
     int submit(Request& r) {
+        // per-request checks before queueing, so one caller's bad stripe
+        // never fails the unrelated callers batched with it
+        if (!r.stripe.base) return fail(HBEC_ERR_INVALID_ARG, "stripe with null base");
+        if (r.op == 2 && r.stripe.shard_len > hbec::host_md5_max_shard(codec))
+            return fail(HBEC_ERR_INVALID_ARG, "hashing needs every stripe to fit one staging slot");
         {
             std::lock_guard<std::mutex> g(mu);
             if (stop) return fail(HBEC_ERR_INVALID_ARG, "batcher stopped");
@@ -155,9 +221,13 @@ int hbec_batcher_new(hbec_codec* codec, uint64_t max_batch_bytes, uint32_t max_w
         b->max_wait = std::chrono::microseconds(max_wait_us);
         const char* env = std::getenv("HBEC_BATCHER_WORKERS");
         const int n_workers = std::min(8, std::max(1, env ? std::atoi(env) : 2));
+        const char* env5 = std::getenv("HBEC_BATCHER_MD5_WORKERS");
+        b->md5_workers = std::min(16, std::max(0, env5 ? std::atoi(env5) : 4));
         b->batch_cap = std::max<uint64_t>(1, b->max_batch_bytes / (uint64_t)n_workers);
+        b->md5_cap = std::max<uint64_t>(1, b->max_batch_bytes / (uint64_t)std::max(1, b->md5_workers));
         hbec_batcher* raw = b.get();
-        for (int w = 0; w < n_workers; ++w) b->workers.emplace_back([raw] { raw->run(); });
+        for (int w = 0; w < n_workers; ++w) b->workers.emplace_back([raw] { raw->run(false); });
+        for (int w = 0; w < b->md5_workers; ++w) b->workers.emplace_back([raw] { raw->run(true); });
         *out = b.release();
         return HBEC_OK;
     });

@@ -49,7 +49,16 @@ struct CoReq {
     }
 };
 
-constexpr int kMaxInFlight = 2;
+// Groups coded at once (HBEC_COALESCE_INFLIGHT, default 2): below this many
+// concurrent callers every call still runs at once, as if uncoalesced.
+int max_in_flight() {
+    static const int v = [] {
+        const char* e = std::getenv("HBEC_COALESCE_INFLIGHT");
+        const int x = e ? std::atoi(e) : 0;
+        return x > 0 ? x : 2;
+    }();
+    return v;
+}
 
 struct Coalescer {
     std::mutex mu;
@@ -118,12 +127,21 @@ int coalesced_call(hbec_codec* codec, int op, uint8_t* base, uint64_t s, const u
     }
     hipError_t e = hipGetDevice(&r.dev);
     if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+    // Only stripes the GPU can code in place (pinned, device-mapped, 16-B
+    // aligned) are grouped: a group of those is ONE zero-copy launch with no
+    // CPU copy.  Pageable stripes take the per-call path, whose bounce-buffer
+    // copies then run in parallel on the callers' own threads — 64 concurrent
+    // callers reach 30 GiB/s that way vs 9 GiB/s funnelled through one
+    // leader's staging ring (profiles/r02_percall.jsonl).
+    const bool pinned = (reinterpret_cast<uintptr_t>(base) & 15u) == 0 && s % 16 == 0 &&
+                        pinned_device_addr(base, s * (uint64_t)n_shards) != 0;
+    if (!pinned) return op == 0 ? fn.encode(codec, base, s) : fn.reconstruct(codec, base, s, present, data_only);
     const uint64_t cap = group_cap_bytes();
     std::unique_lock<std::mutex> lk(g_co.mu);
     g_co.q.push_back(&r);
     for (;;) {
         if (r.done) break;
-        if (!r.taken && g_co.in_flight < kMaxInFlight) {
+        if (!r.taken && g_co.in_flight < max_in_flight()) {
             // lead: this call plus every queued call of the same group, up to cap bytes
             std::vector<CoReq*> grp;
             uint64_t bytes = 0;

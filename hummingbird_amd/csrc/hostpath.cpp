@@ -186,6 +186,36 @@ int ring_md5_init(Ring& r) {
 std::mutex g_rings_mu;
 std::vector<Ring*> g_free_rings;
 
+// Pooled non-blocking streams per device for short per-call work (creating
+// and destroying a stream per call costs more than a small batch's copies).
+std::mutex g_streams_mu;
+std::vector<std::pair<int, hipStream_t>> g_free_streams;
+
+int stream_acquire(hipStream_t* out) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+    {
+        std::lock_guard<std::mutex> g(g_streams_mu);
+        for (size_t i = 0; i < g_free_streams.size(); ++i)
+            if (g_free_streams[i].first == dev) {
+                *out = g_free_streams[i].second;
+                g_free_streams.erase(g_free_streams.begin() + (long)i);
+                return HBEC_OK;
+            }
+    }
+    e = hipStreamCreateWithFlags(out, hipStreamNonBlocking);
+    if (e != hipSuccess) return hip_fail(e, "hipStreamCreate");
+    return HBEC_OK;
+}
+
+void stream_release(hipStream_t s) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return;
+    std::lock_guard<std::mutex> g(g_streams_mu);
+    g_free_streams.emplace_back(dev, s);
+}
+
 int ring_acquire(Ring** out) {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
@@ -600,6 +630,13 @@ int run_on_devices(const hbec_stripe* stripes, uint64_t n, const int* devices, i
 
 }  // namespace
 
+uint64_t hbec::host_md5_max_shard(const hbec_codec* codec) {
+    const uint64_t slot = env_size("HBEC_HOST_SLOT_MB", 64) << 20;  // as ring_init
+    const int k = hbec_data_shards(codec), m = hbec_parity_shards(codec);
+    if (k < 1 || m < 1) return 0;
+    return (std::min(slot / (uint64_t)k, slot / (uint64_t)m) / 16) * 16;
+}
+
 int hbec::host_threads() {
     const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
     const size_t share = env_size("OMP_NUM_THREADS", 16);
@@ -680,8 +717,13 @@ int hbec_encode_host_md5(hbec_codec* codec, const hbec_stripe* stripes, uint64_t
         for (int j = 0; j < k; ++j) in_idx[j] = j;
         for (int r = 0; r < m; ++r) out_idx[r] = k + r;
         hipStream_t st = nullptr;
-        hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
-        if (e != hipSuccess) return hip_fail(e, "hipStreamCreate");
+        int rc0 = stream_acquire(&st);
+        if (rc0) return rc0;
+        struct StreamBack {
+            hipStream_t s;
+            ~StreamBack() { stream_release(s); }
+        } back{st};
+        hipError_t e = hipSuccess;
         void* d_dig = nullptr;
         const size_t bytes = (size_t)n_stripes * n * 16;
         int rc = hbec::scratch_alloc(bytes, st, &d_dig);
@@ -697,7 +739,6 @@ int hbec_encode_host_md5(hbec_codec* codec, const hbec_stripe* stripes, uint64_t
         }
         hbec::scratch_free(d_dig, st);
         (void)hipStreamSynchronize(st);
-        (void)hipStreamDestroy(st);
         return rc;
     });
 }

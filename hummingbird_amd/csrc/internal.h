@@ -61,6 +61,10 @@ int coalesced_call(hbec_codec* codec, int op, uint8_t* base, uint64_t s, const u
                    int data_only, const DirectFns& fn);
 void coalesce_stats(uint64_t* groups, uint64_t* calls);
 
+// Largest shard_len hbec_encode_host_md5 accepts (a stripe must fit one
+// staging slot of the host ring).
+uint64_t host_md5_max_shard(const hbec_codec* codec);
+
 struct TileRec;
 // Grid for a stripes launch of k inputs / r outputs over n_tiles records
 // (one block of 4 waves per CU at most, as the strided kernels).

@@ -725,6 +725,16 @@ static const void* packed_kernel(int k, int r) {
 
 int packed_tile_elems(int k) { return packed_u(k) * 64; }
 
+// Shards shorter than this take the packed kernel: below one pipelined tile
+// it is the only full-lane kernel (8+3 @ 4 KiB: 70 % vs 7 % of 8 TB/s); for
+// K <= 4 it also beats gf_apply_vec_pipe2 up to S = 1 KiB (4+2 @ 4 KiB:
+// 72.6 % vs 69.3 %), while at S = 256 KiB it loses (68-72 % vs 74 %)
+// (profiles/r02_tune_packed3_*.jsonl).
+static uint64_t packed_max_shard(int k) {
+    const uint64_t tile = (uint64_t)pipe_u(k) * 1024u;
+    return tile > 2048u ? tile : 2048u;
+}
+
 // Tuning knobs: HBEC_PACKED=0 sends short shards back to gf_apply_vec (A/B);
 // HBEC_PACKED_MAX_SHARD=B takes shards shorter than B bytes (instead of
 // shorter than one pipelined tile) through the packed kernel.
@@ -739,7 +749,7 @@ static const uint64_t g_packed_max = [] {
 
 int is_packed_shape(int k, int r, uint64_t shard_len, int accumulate, int force_stream) {
     return (HBEC_USE_PACKED && g_packed_on && !force_stream && !accumulate && shard_len >= 16 && shard_len % 16 == 0 &&
-            shard_len < (g_packed_max ? g_packed_max : (uint64_t)pipe_u(k) * 1024u) &&
+            shard_len < (g_packed_max ? g_packed_max : packed_max_shard(k)) &&
             packed_kernel(k, r) != nullptr)
                ? 1
                : 0;

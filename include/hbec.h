@@ -103,12 +103,14 @@ int hbec_verify_databuf(hbec_codec* codec, const uint8_t* databuf, size_t shard_
 
 /* Concurrent per-call Encode / Reconstruct / ReconstructData on databuf
  * stripes (the *_databuf entries, and hbec_encode / hbec_reconstruct when
- * the shard pointers are one buffer's consecutive slots) are coalesced: a
- * call that finds fewer than two groups in flight codes itself plus every
- * queued call of the same (device, codec, op, erasure pattern) with one
- * host-path call (up to HBEC_COALESCE_MB, 256 MiB); a lone call runs at once.
- * HBEC_COALESCE=0 turns this off.  Counters since load: groups run and calls
- * they carried. */
+ * the shard pointers are one buffer's consecutive slots) in pinned,
+ * device-mapped memory (hbec_host_alloc) are coalesced: a call that finds
+ * fewer than HBEC_COALESCE_INFLIGHT (2) groups in flight codes itself plus
+ * every queued call of the same (device, codec, op, erasure pattern) with
+ * one zero-copy launch (up to HBEC_COALESCE_MB, 256 MiB); a lone call runs
+ * at once.  Pageable stripes run per call (their staging copies parallel on
+ * the callers' threads).  HBEC_COALESCE=0 turns this off.  Counters since
+ * load: groups run and calls they carried. */
 int hbec_coalesce_stats(uint64_t* groups, uint64_t* calls);
 
 /* ---------------------------------------------------------------------------

@@ -9,6 +9,7 @@
  *   /tmp/bench_batcher THREADS PER_THREAD PINNED MAX_BATCH_MB MAX_WAIT_US [MODE]
  *
  * MODE 0 (default): hbec_batcher_encode (the explicit batching driver);
+ * MODE 2: hbec_batcher_encode_md5 (Encode + ShardHash of every shard);
  * MODE 1: plain per-call hbec_encode_databuf (the 3-line shim swap of
  *         INTEGRATION.md), coalesced inside the library (HBEC_COALESCE=0 in
  *         the environment measures it uncoalesced).
@@ -49,6 +50,10 @@ static void* caller(void* arg) {
         uint8_t* base = j->pool + (size_t)i * (K + M) * S;
         if (j->mode == 1) {
             j->rc = hbec_encode_databuf(j->codec, base, S);
+        } else if (j->mode == 2) {
+            hbec_stripe st = {base, S};
+            uint8_t dig[(K + M) * 16];
+            j->rc = hbec_batcher_encode_md5(j->bat, &st, dig);
         } else {
             hbec_stripe st = {base, S};
             j->rc = hbec_batcher_encode(j->bat, &st);
@@ -90,10 +95,10 @@ int main(int argc, char** argv) {
     }
     pthread_t* th = malloc(sizeof(pthread_t) * threads);
     Job* jobs = calloc(threads, sizeof(Job));
-    /* warm-up: one stripe per caller, all at once, so every worker has made
+    /* warm-up: a few stripes per caller, all at once, so every worker has made
      * its ring before the clock starts (a long-running server's steady state) */
     for (int t = 0; t < threads; ++t) {
-        jobs[t] = (Job){codec, mode, bat, pool, t * per, 1, 0};
+        jobs[t] = (Job){codec, mode, bat, pool, t * per, per < 4 ? per : 4, 0};
         pthread_create(&th[t], NULL, caller, &jobs[t]);
     }
     for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
@@ -131,7 +136,8 @@ int main(int argc, char** argv) {
     printf("{\"measure\": \"%s_native_callers_Encode_1MiB_%s\", \"threads\": %d, \"objects\": %zu, "
            "\"max_batch_MiB\": %llu, \"max_wait_us\": %u, \"seconds\": %.4f, \"object_data_GiB_s\": %.2f, "
            "\"us_per_object\": %.1f, \"batches\": %llu, \"parity_ok\": %s}\n",
-           mode == 1 ? (co && co[0] == '0' ? "percall_databuf_uncoalesced" : "percall_databuf_coalesced") : "batcher",
+           mode == 1 ? (co && co[0] == '0' ? "percall_databuf_uncoalesced" : "percall_databuf_coalesced")
+                     : (mode == 2 ? "batcher_md5" : "batcher"),
            pinned ? "pinned" : "pageable", threads, n, (unsigned long long)max_mb, wait_us, secs,
            n * (double)K * S / secs / (double)(1 << 30), secs / n * 1e6, (unsigned long long)(b1 - b0),
            bad ? "false" : "true");

@@ -105,12 +105,12 @@ def pipelined(op: str, n_obj=4096, chunk=256, reps=3):
             "objects_per_s": round(n_obj / t, 1)}
 
 
-def library_host_path(op: str, n_obj=4096, reps=3, mem="pageable"):
+def library_host_path(op: str, n_obj=4096, reps=3, mem="pageable", k=4, m=2):
     """hbec_encode_host / hbec_reconstruct_host.  mem="pageable": numpy stripes
     through the library's pinned ring (CPU gather -> H2D -> kernel -> D2H ->
     scatter).  mem="pinned": stripes in hbec_host_alloc memory, coded in place
     by the GPU over PCIe (zero-copy, no CPU copies)."""
-    k, m, S = 4, 2, MiB // 4
+    S = MiB // k
     enc = RS.New(k, m)
     hb = None
     if mem == "pinned":
@@ -133,10 +133,10 @@ def library_host_path(op: str, n_obj=4096, reps=3, mem="pageable"):
     t = min(ts)
     if op == "encode":
         assert U.verify_stripe(enc, pool[7].copy())
-    res = {"measure": f"library_host_path_{op}_{mem}", "objects": n_obj, "seconds": round(t, 4),
+    res = {"measure": f"library_host_path_{op}_{mem}", "k": k, "m": m, "objects": n_obj, "seconds": round(t, 4),
            "object_data_GiB_s": round(n_obj * k * S / t / GiB, 2),
-           "algorithmic_GiB_s": round(n_obj * (k + 2) * S / t / GiB, 2),
-           "pcie_GB_s": round(n_obj * (k + 2) * S / t / 1e9, 2), "objects_per_s": round(n_obj / t, 1)}
+           "algorithmic_GiB_s": round(n_obj * (k + m) * S / t / GiB, 2),
+           "pcie_GB_s": round(n_obj * (k + m) * S / t / 1e9, 2), "objects_per_s": round(n_obj / t, 1)}
     del stripes, pool
     if hb is not None:
         hb.free()
@@ -184,12 +184,17 @@ def batched_callers(n_threads=64, per_thread=32, mem="pageable"):
             "us_per_object": round(t / n * 1e6, 1), "batches": st["batches"]}
 
 
-def library_host_path_md5(n_obj=4096, reps=3):
+def library_host_path_md5(n_obj=4096, reps=3, mem="pageable", k=4, m=2):
     """hbec_encode_host_md5: the library host path plus the ShardHash of all
     k+m shards of every stripe, hashed on the GPU per chunk."""
-    k, m, S = 4, 2, MiB // 4
+    S = MiB // k
     enc = RS.New(k, m)
-    pool = np.empty((n_obj, (k + m) * S), dtype=np.uint8)
+    hb = None
+    if mem == "pinned":
+        hb = RS.HostBuffer(n_obj * (k + m) * S)
+        pool = hb.array.reshape(n_obj, (k + m) * S)
+    else:
+        pool = np.empty((n_obj, (k + m) * S), dtype=np.uint8)
     import hashlib
     pool[:, :k * S] = U.objects_host(n_obj, k * S)
     stripes = [pool[i] for i in range(n_obj)]
@@ -201,9 +206,27 @@ def library_host_path_md5(n_obj=4096, reps=3):
         ts.append(time.perf_counter() - t0)
     t = min(ts)
     assert hs[9] == [hashlib.md5(pool[9, i * S:(i + 1) * S]).hexdigest() for i in range(k + m)]
-    return {"measure": "library_host_path_encode_md5_pageable", "objects": n_obj, "seconds": round(t, 4),
-            "object_data_GiB_s": round(n_obj * k * S / t / GiB, 2),
-            "hashed_GiB_s": round(n_obj * (k + m) * S / t / GiB, 2), "objects_per_s": round(n_obj / t, 1)}
+    res = {"measure": f"library_host_path_encode_md5_{mem}", "k": k, "m": m, "objects": n_obj,
+           "seconds": round(t, 4), "object_data_GiB_s": round(n_obj * k * S / t / GiB, 2),
+           "hashed_GiB_s": round(n_obj * (k + m) * S / t / GiB, 2), "objects_per_s": round(n_obj / t, 1)}
+    del stripes, pool
+    if hb is not None:
+        hb.free()
+    return res
+
+
+def md5_vs_encode():
+    """Encode + ShardHash against Encode alone, same stripes, 4+2 and 8+3 @
+    1 MiB, pageable and pinned: the cost of the hash next to the encode."""
+    out = []
+    for k, m in ((4, 2), (8, 3)):
+        for mem in ("pageable", "pinned"):
+            e = library_host_path("encode", mem=mem, k=k, m=m)
+            h = library_host_path_md5(mem=mem, k=k, m=m)
+            out.append({"measure": f"host_path_encode_md5_vs_encode_{k}+{m}_{mem}", "objects": 4096,
+                        "encode_s": e["seconds"], "encode_md5_s": h["seconds"],
+                        "ratio": round(h["seconds"] / e["seconds"], 3)})
+    return out
 
 
 def batched_callers_md5(n_threads=64, per_thread=32):
@@ -292,12 +315,14 @@ def main():
              lambda: library_host_path("encode"), lambda: library_host_path("reconstruct"),
              lambda: library_host_path("encode", mem="pinned"), lambda: library_host_path("reconstruct", mem="pinned"),
              library_host_path_md5, batched_callers, lambda: batched_callers(mem="pinned"), batched_callers_md5,
-             auditor_pass, per_call, lambda: per_call(mem="pinned")]
+             auditor_pass, per_call, lambda: per_call(mem="pinned"), md5_vs_encode]
     only = sys.argv[1:]
     for i, f in enumerate(steps):
         if only and str(i) not in only:
             continue
-        print(json.dumps(f()), flush=True)
+        r = f()
+        for x in (r if isinstance(r, list) else [r]):
+            print(json.dumps(x), flush=True)
 
 
 if __name__ == "__main__":

@@ -195,8 +195,9 @@ def test_percall_64_threads_coalesced_match_oracle(pinned):
     """64 threads each calling the plain per-call entries (EncodeDatabuf,
     Encode on consecutive slots, ReconstructDatabuf / ReconstructData) the way
     concurrent Stabilize / GET goroutines reach klauspost through the shim:
-    calls are coalesced into shared launches (hbec_coalesce_stats) and every
-    caller gets exactly its own bytes, checked against the oracle."""
+    calls on pinned databufs are coalesced into shared launches
+    (hbec_coalesce_stats), pageable ones run per call, and every caller gets
+    exactly its own bytes, checked against the oracle."""
     import ctypes as C
     import threading
 
@@ -238,8 +239,11 @@ def test_percall_64_threads_coalesced_match_oracle(pinned):
         assert np.array_equal(b, w)
     g1, c1 = C.c_uint64(), C.c_uint64()
     N.lib().hbec_coalesce_stats(C.byref(g1), C.byref(c1))
-    assert c1.value - c0.value == n
-    assert g1.value - g0.value <= n  # groups carried several calls when callers overlapped
+    if pinned:  # pinned databufs are grouped (one zero-copy launch per group)
+        assert c1.value - c0.value == n
+        assert g1.value - g0.value <= n
+    else:  # pageable ones run per call: their staging copies parallel on the callers' threads
+        assert c1.value - c0.value == 0
     # degraded reads / repair: two patterns interleaved, ReconstructData on some
     pats = [([0, 1, 1, 1, 1, 1], False), ([1, 1, 0, 1, 0, 1], False), ([0, 1, 1, 0, 1, 1], True)]
     for i, b in enumerate(bufs):

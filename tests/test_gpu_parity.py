@@ -956,3 +956,63 @@ def test_batcher_mixed_ops_and_patterns_concurrently(monkeypatch, workers):
     st = bat.stats()
     assert st["stripes"] == len(jobs)
     bat.close()
+
+
+def test_batcher_bad_request_fails_alone():
+    """A caller's invalid stripe (null base; an MD5 stripe wider than a
+    staging slot) is rejected at submit and never fails the callers it
+    would have been batched with; a reconstruct queued between encodes does
+    not split the encodes' batch."""
+    import ctypes as C
+    import threading
+
+    from hummingbird_amd import _native as N
+
+    k, m = 4, 2
+    enc = RS.New(k, m)
+    bat = RS.Batcher(enc, max_batch_bytes=64 << 20, max_wait_us=3000)
+    stripes = _host_stripes(k, m, [4096 * (1 + i % 3) for i in range(24)], seed=5)
+    want = _encoded_copy(k, m, stripes)
+    damaged = want[0].copy()
+    s0 = damaged.size // (k + m)
+    damaged[:s0] = 0
+    errors, bad_rc = [], []
+
+    def good(i):
+        try:
+            bat.Encode(stripes[i])
+        except Exception as e:  # pragma: no cover
+            errors.append(e)
+
+    def bad_null():
+        st = N.Stripe()
+        st.base = None
+        st.shard_len = 4096
+        bad_rc.append(N.lib().hbec_batcher_encode(bat._h, C.byref(st)))
+
+    def bad_wide():
+        st = N.Stripe()
+        st.base = stripes[0].ctypes.data
+        st.shard_len = 1 << 40  # never dereferenced: rejected before queueing
+        dig = (C.c_uint8 * (16 * (k + m)))()
+        bad_rc.append(N.lib().hbec_batcher_encode_md5(bat._h, C.byref(st), dig))
+
+    def rec():
+        try:
+            bat.Reconstruct(damaged, [0, 1, 1, 1, 1, 1])
+        except Exception as e:  # pragma: no cover
+            errors.append(e)
+
+    th = [threading.Thread(target=good, args=(i,)) for i in range(12)] + [threading.Thread(target=bad_null),
+                                                                        threading.Thread(target=rec),
+                                                                        threading.Thread(target=bad_wide)]
+    th += [threading.Thread(target=good, args=(i,)) for i in range(12, 24)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    bat.close()
+    assert not errors
+    assert sorted(bad_rc) == [N.ERR_INVALID_ARG, N.ERR_INVALID_ARG]
+    assert all(np.array_equal(a, b) for a, b in zip(stripes, want))
+    assert np.array_equal(damaged, want[0])
