@@ -55,6 +55,17 @@ static const int g_grid_cap = [] {
     const char* e = std::getenv("HBEC_GRID_CAP");
     return e ? std::atoi(e) : 0;
 }();
+// Tiles per launch of the pipelined / packed kernels (HBEC_CHUNK_TILES):
+// a batch is split into launches of whole objects of at most this many
+// tiles.  Over one very long launch the blocks' grid-stride fronts drift
+// apart and HBM streams less well: 65 536 x 1 MiB 4+2 in one launch ran at
+// 72.6 % of 8 TB/s, in 16 launches of 4096 objects at 76.0 %
+// (profiles/r02_config5_tune.jsonl).
+static const uint64_t g_chunk_tiles = [] {
+    const char* e = std::getenv("HBEC_CHUNK_TILES");
+    const long long v = e ? std::atoll(e) : 0;
+    return (uint64_t)(v > 0 ? v : (1ll << 20));
+}();
 
 // ---------------------------------------------------------------------------
 // Per-device facts (CU count, occupancy per kernel shape)
@@ -149,7 +160,8 @@ int apply_views(int rows, int cols, const uint8_t* coeffs, const hbec_view* in, 
                 if (rc) return rc;
                 const uint64_t spo = shard_len / 16;
                 const uint64_t te = (uint64_t)packed_tile_elems(K);
-                const uint64_t max_obj = std::max<uint64_t>(1, ((1ull << 31) - te) / spo);  // n_elems < 2^31
+                uint64_t max_obj = std::max<uint64_t>(1, ((1ull << 31) - te) / spo);  // n_elems < 2^31
+                max_obj = std::min(max_obj, std::max<uint64_t>(1, g_chunk_tiles * te / spo));
                 for (uint64_t o0 = 0; o0 < n_obj; o0 += max_obj) {
                     const uint64_t no = std::min(max_obj, n_obj - o0);
                     PassArgs b = a;
@@ -176,8 +188,8 @@ int apply_views(int rows, int cols, const uint8_t* coeffs, const hbec_view* in, 
                 if (rc) return rc;
                 const uint64_t tile = (uint64_t)vec_tile_bytes(K, R, shard_len, c0 > 0, force_stream);
                 const uint64_t tpo = (shard_len + tile - 1) / tile;
-                // keep n_tiles < 2^31 per launch: split the batch by objects
-                const uint64_t max_obj = std::max<uint64_t>(1, (1ull << 31) / tpo);
+                // keep n_tiles < 2^31 (and <= g_chunk_tiles) per launch: split the batch by objects
+                const uint64_t max_obj = std::max<uint64_t>(1, std::min<uint64_t>((1ull << 31), g_chunk_tiles) / tpo);
                 for (uint64_t o0 = 0; o0 < n_obj; o0 += max_obj) {
                     const uint64_t no = std::min(max_obj, n_obj - o0);
                     PassArgs b = a;

@@ -29,15 +29,15 @@ for s in "$@"; do
     bench) step bench 600 python bench.py --steps 20 --warmup 5 ;;
     prof)
       mkdir -p "$OUT/prof"
-      (cd /tmp && step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-host-path) || exit $?
+      (cd /tmp && step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-host-path --config5-objects 0) || exit $?
       ;;
     pmcfetch)
       mkdir -p "$OUT/pmc_fetch"
-      (cd /tmp && step pmcfetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --no-host-path) || exit $?
+      (cd /tmp && step pmcfetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --no-host-path --config5-objects 0) || exit $?
       ;;
     pmcwrite)
       mkdir -p "$OUT/pmc_write"
-      (cd /tmp && step pmcwrite 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o run -- python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --no-host-path) || exit $?
+      (cd /tmp && step pmcwrite 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o run -- python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --no-host-path --config5-objects 0) || exit $?
       ;;
     cfgprof)
       mkdir -p "$OUT/cfgprof"
@@ -51,6 +51,19 @@ for s in "$@"; do
       mkdir -p "$OUT/cfg_pmc_write"
       (cd /tmp && step cfgpmcwrite 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/cfg_pmc_write" -o run -- python3 "$ROOT/scripts/bench_configs.py") || exit $?
       ;;
+    smallprof)
+      mkdir -p "$OUT/smallprof"
+      (cd /tmp && step smallprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/smallprof" -o run -- python3 "$ROOT/scripts/bench_small.py") || exit $?
+      ;;
+    smallpmcfetch)
+      mkdir -p "$OUT/small_pmc_fetch"
+      (cd /tmp && step smallpmcfetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/small_pmc_fetch" -o run -- python3 "$ROOT/scripts/bench_small.py") || exit $?
+      ;;
+    smallpmcwrite)
+      mkdir -p "$OUT/small_pmc_write"
+      (cd /tmp && step smallpmcwrite 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/small_pmc_write" -o run -- python3 "$ROOT/scripts/bench_small.py") || exit $?
+      ;;
+    small) step small 300 python scripts/bench_small.py ;;
     dist2) step dist2 600 env HBEC_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 10 --warmup 2 --objects 2048 ;;
     configs) step configs 600 python scripts/bench_configs.py ;;
     host) step host 600 python scripts/bench_host.py ;;

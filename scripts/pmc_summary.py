@@ -43,7 +43,7 @@ def main():
     write = per_kernel(write_dir, "WRITE_SIZE")
     kernels = {}
     for k in sorted(set(fetch) | set(write)):
-        if not k.startswith("gf_") and not k.startswith("fill"):
+        if not k.startswith("gf_") and not k.startswith("fill") and not k.startswith("md5"):
             continue
         f = [v for v, _ in fetch.get(k, [])]
         w = [v for v, _ in write.get(k, [])]
@@ -56,7 +56,11 @@ def main():
             "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
             "hbm_bytes_per_launch": (rd + wr) if (rd is not None and wr is not None) else None,
         }
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    import bench  # the sources the dominant kernel is built from: bench.py trusts only a matching summary
+
     res = {"source": [str(fetch_dir), str(write_dir)],
+           "kernel_sources_sha256": bench.kernel_sources_sha256(),
            "corrections": "read = 2 x FETCH_SIZE x 1024 (gfx950 half-count on wide streaming reads); "
                           "write = WRITE_SIZE x 1024",
            "kernels": kernels}

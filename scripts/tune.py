@@ -32,6 +32,13 @@ VARIANTS = {
     "cur": ([], {}),
     # packed kernel (short shards, e.g. 8+3 of 4 KiB objects)
     "pk_vec": ([], {"HBEC_PACKED": "0"}),
+    "ch128k": ([], {"HBEC_CHUNK_TILES": str(128 << 10)}),
+    "ch256k": ([], {"HBEC_CHUNK_TILES": str(256 << 10)}),
+    "ch512k": ([], {"HBEC_CHUNK_TILES": str(512 << 10)}),
+    "ch1m": ([], {"HBEC_CHUNK_TILES": str(1 << 20)}),
+    "ch2m": ([], {"HBEC_CHUNK_TILES": str(2 << 20)}),
+    "ch4m": ([], {"HBEC_CHUNK_TILES": str(4 << 20)}),
+    "chinf": ([], {"HBEC_CHUNK_TILES": str(1 << 40)}),
     "pk_s4": (["HBEC_PACKED_SLEEP_BIG=4"], {}),
     "pk_s8": (["HBEC_PACKED_SLEEP_BIG=8"], {}),
     "pk_u1": (["HBEC_PACKED_U_BIG=1"], {}),
@@ -178,12 +185,18 @@ VARIANTS = {
 
 
 def build(names):
+    import shutil
+
     from hummingbird_amd import build as hb
 
     for n in names:
         defs, _ = VARIANTS[n]
         d = OUTDIR / n
-        hb.build(defs=defs, lib=d / "libhbec.so", objdir=d / "obj", verbose=False)
+        if not defs:  # env-only variant: a copy of the product library (its own static state when loaded)
+            d.mkdir(parents=True, exist_ok=True)
+            shutil.copy2(hb.build(verbose=False), d / "libhbec.so")
+        else:
+            hb.build(defs=defs, lib=d / "libhbec.so", objdir=d / "obj", verbose=False)
         print("built", n, flush=True)
 
 
