@@ -249,6 +249,18 @@ struct PinnedRange {
 std::mutex g_pin_mu;
 std::map<uint64_t, PinnedRange> g_pinned;  // host base -> range (hbec_host_alloc)
 
+// Blocks per CU of the zero-copy stripes kernel (HBEC_ZC_BLOCKS_PER_CU):
+// it streams over PCIe, whose latency wants more requests in flight than
+// HBM's sweet spot of one 4-wave block per CU.
+int zero_copy_blocks_per_cu() {
+    static const int v = [] {
+        const char* e = std::getenv("HBEC_ZC_BLOCKS_PER_CU");
+        const int x = e ? std::atoi(e) : 0;
+        return x > 0 ? x : 2;  // 1: 45.9, 2: 46.7, 4: 46.6, 8: 46.8 GiB/s (profiles/r02_zc_bpc.jsonl)
+    }();
+    return v;
+}
+
 bool zero_copy_enabled() {
     static const bool on = [] {
         const char* e = std::getenv("HBEC_ZEROCOPY");
@@ -338,7 +350,8 @@ int zero_copy_run(Ring* ring, const std::vector<ZcStripe>& zs, const std::vector
         e = hipMemcpyAsync(ring->dev_tiles[slot], rec, nt * sizeof(hbec::TileRec), hipMemcpyHostToDevice,
                            ring->s_cmp);
         if (e != hipSuccess) return hip_fail(e, "zero-copy records H2D");
-        int rc = hbec::launch_stripe_passes(ring->dev_tiles[slot], nt, in_idx, out_idx, rows, 0, ring->s_cmp);
+        int rc = hbec::launch_stripe_passes(ring->dev_tiles[slot], nt, in_idx, out_idx, rows, 0, ring->s_cmp,
+                                            zero_copy_blocks_per_cu());
         if (rc) return rc;
         e = hipEventRecord(ring->ev_cmp[slot], ring->s_cmp);
         if (e != hipSuccess) return hip_fail(e, "zero-copy event");

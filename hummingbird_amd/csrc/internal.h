@@ -68,11 +68,12 @@ uint64_t host_md5_max_shard(const hbec_codec* codec);
 struct TileRec;
 // Grid for a stripes launch of k inputs / r outputs over n_tiles records
 // (one block of 4 waves per CU at most, as the strided kernels).
-int stripes_grid(int k, int r, uint64_t n_tiles, int* grid);
+// blocks_per_cu > 0 overrides the HBM sweet spot (1 block per CU).
+int stripes_grid(int k, int r, uint64_t n_tiles, int* grid, int blocks_per_cu = 0);
 // out (^)= rows x in over tile records, in launches of <= 3 outputs and
 // <= 8 inputs (k > 8: accumulate passes).  sel_k > 0: object-plan bases.
 int launch_stripe_passes(const TileRec* tiles, uint64_t n_tiles, const std::vector<int>& in_idx,
                          const std::vector<int>& out_idx, const std::vector<uint8_t>& rows, int sel_k,
-                         hipStream_t stream);
+                         hipStream_t stream, int blocks_per_cu = 0);
 
 }  // namespace hbec
