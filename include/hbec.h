@@ -117,6 +117,11 @@ int hbec_coalesce_stats(uint64_t* groups, uint64_t* calls);
  * Device-resident batches (the GPU hot path).  A view places shard i of
  * object o at base + o * obj_stride in device memory.  Work is queued on
  * hip_stream (a hipStream_t; NULL = default stream) and not waited for.
+ * Output views must not overlap input views (as with klauspost, whose
+ * outputs are separate slices): every output byte is written exactly once,
+ * but a byte that is also an input of another object or column may be read
+ * before or after that write.  Batches are split into launches of at most
+ * 2^20 tiles (HBEC_CHUNK_TILES) of whole objects.
  * ------------------------------------------------------------------------- */
 typedef struct {
     void* base;
