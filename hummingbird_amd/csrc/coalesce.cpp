@@ -22,6 +22,7 @@
 #include <cstdlib>
 #include <deque>
 #include <mutex>
+#include <new>
 #include <string>
 #include <vector>
 
@@ -159,7 +160,15 @@ int coalesced_call(hbec_codec* codec, int op, uint8_t* base, uint64_t s, const u
             ++g_co.groups;
             g_co.calls += grp.size();
             lk.unlock();
-            run_group(grp, fn);
+            // no exception may leave the group half-done: the other members
+            // would wait forever
+            try {
+                run_group(grp, fn);
+            } catch (const std::bad_alloc&) {
+                for (auto* x : grp) x->rc = HBEC_ERR_NOMEM, x->err = "coalesced call: host allocation failed";
+            } catch (...) {
+                for (auto* x : grp) x->rc = HBEC_ERR_DEVICE, x->err = "coalesced call: unexpected exception";
+            }
             lk.lock();
             --g_co.in_flight;
             for (auto* x : grp) x->done = true;
