@@ -1,0 +1,85 @@
+"""gf_apply_packed (short shards: wave tiles across objects) against the CPU
+oracle: shard lengths from one element (16 B) up to the kernel's limit, odd
+element counts (S/16 not a power of two, so objects straddle lanes at every
+offset), one object, partial last tiles, padded object strides, and
+reconstruct with survivors in two arrays and outputs in a third."""
+import numpy as np
+import pytest
+import torch
+
+from hummingbird_amd import batch as B
+from hummingbird_amd import reedsolomon as RS
+from oracle import coracle as CO
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    torch.cuda.set_device(0)
+    yield
+
+
+SHAPES = [(1, 1), (2, 1), (3, 2), (4, 2), (5, 3), (8, 3), (6, 2)]
+LENS = [16, 48, 96, 256, 512, 1008, 1024, 1040, 2032, 3056]
+
+
+def _packed(k, s):
+    """The dispatch rule of kernels.hip is_packed_shape (no device needed at
+    collection): S < 2 KiB for K <= 4, S < 3 KiB for 5 <= K <= 8."""
+    return s % 16 == 0 and s < (2048 if k <= 4 else 3072)
+
+
+def _cases():
+    for k, m in SHAPES:
+        for s in LENS:
+            if _packed(k, s):
+                yield k, m, s
+
+
+@pytest.mark.parametrize("k,m,s", list(_cases()))
+@pytest.mark.parametrize("n", [1, 7, 333])
+def test_packed_encode_matches_oracle(k, m, s, n):
+    pad = 48  # object rows longer than k*S: the views' strides differ from S
+    objs = torch.empty((n, k * s + pad), dtype=torch.uint8, device="cuda")
+    B.fill_splitmix(objs, k * s + pad, first=k * 1000 + s)
+    parity = torch.full((n, m * s + pad), 0xC5, dtype=torch.uint8, device="cuda")
+    enc = RS.New(k, m)
+    views = [(objs.data_ptr() + j * s, objs.stride(0)) for j in range(k)]
+    views += [(parity.data_ptr() + r * s, parity.stride(0)) for r in range(m)]
+    assert B.kernel_info(k, m, s)["kind"] == "packed"
+    B.encode_views(enc, views, n, s)
+    torch.cuda.synchronize()
+    host = objs.cpu().numpy()
+    want, _ = CO.encode_batch(k, m, np.ascontiguousarray(host[:, :k * s]))
+    got = parity.cpu().numpy()
+    assert np.array_equal(got[:, :m * s], want)
+    assert (got[:, m * s:] == 0xC5).all()  # nothing written past the last shard
+
+
+@pytest.mark.parametrize("k,m,s", [(8, 3, 512), (4, 2, 1024), (4, 2, 48), (3, 2, 2032), (8, 3, 3056)])
+def test_packed_reconstruct_three_arrays(k, m, s):
+    n = 501
+    enc = RS.New(k, m)
+    objs = torch.empty((n, k * s), dtype=torch.uint8, device="cuda")
+    B.fill_splitmix(objs, k * s, first=s)
+    parity = torch.empty((n, m * s), dtype=torch.uint8, device="cuda")
+    B.encode_objects(enc, objs, parity, s)
+    missing = [0, k - 1, k][:m]
+    rebuilt = torch.zeros((n, len(missing) * s), dtype=torch.uint8, device="cuda")
+    views = B.shard_views(objs, k, s) + B.shard_views(parity, m, s)
+    for slot, i in enumerate(missing):
+        views[i] = (rebuilt.data_ptr() + slot * s, rebuilt.stride(0))
+    B.reconstruct_views(enc, views, [0 if i in missing else 1 for i in range(k + m)], n, s)
+    torch.cuda.synchronize()
+    for slot, i in enumerate(missing):
+        src = objs[:, i * s:(i + 1) * s] if i < k else parity[:, (i - k) * s:(i - k + 1) * s]
+        assert torch.equal(rebuilt[:, slot * s:(slot + 1) * s], src), i
+
+
+def test_packed_kernel_is_selected_for_short_shards():
+    assert B.kernel_info(8, 3, 512)["kind"] == "packed"
+    assert B.kernel_info(4, 2, 1024)["kind"] == "packed"
+    assert B.kernel_info(4, 2, 2048)["kind"] == "pipelined"
+    assert B.kernel_info(8, 3, 3072)["kind"] == "pipelined"
