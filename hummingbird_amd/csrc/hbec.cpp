@@ -233,6 +233,8 @@ struct Staging {
     uint8_t* hbuf = nullptr;
     uint64_t hbuf_dev = 0;
     size_t hcap = 0;
+    // one event per column piece of a pipelined per-call apply (created on first use)
+    std::vector<hipEvent_t> ev;
 };
 
 // Per-call host path for pageable shards (HBEC_PERCALL_MODE):
@@ -246,6 +248,28 @@ static const bool g_percall_mapped = [] {
     const char* e = std::getenv("HBEC_PERCALL_MODE");
     return !(e && std::string(e) == "dma");
 }();
+
+// Column pieces of one per-call apply in mapped mode (HBEC_PERCALL_PIECES,
+// default 2; shards shorter than 64 KiB are one piece): the calling thread
+// copies piece p+1 into the bounce buffer while the kernel codes piece p over
+// PCIe, then copies each piece's outputs back as soon as its kernel is done.
+// 1 MiB 4+2 Encode from pageable memory, one caller: 77 us in one piece,
+// 66 us in 2, 86 us in 4 (per-piece launch cost; profiles/r02_percall_pieces.jsonl).
+static const int g_percall_pieces = [] {
+    const char* e = std::getenv("HBEC_PERCALL_PIECES");
+    const int v = e ? std::atoi(e) : 2;
+    return std::max(1, std::min(16, v));
+}();
+
+static int staging_events(Staging* s, size_t n) {
+    while (s->ev.size() < n) {
+        hipEvent_t e = nullptr;
+        hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+        if (r != hipSuccess) return hip_fail(r, "hipEventCreate");
+        s->ev.push_back(e);
+    }
+    return HBEC_OK;
+}
 
 static int staging_host(Staging* s, size_t bytes) {
     if (s->hcap >= bytes) return HBEC_OK;
@@ -429,15 +453,44 @@ static int host_apply(int rows, int cols, const uint8_t* coeffs, const uint8_t* 
             staging_release(s);
             return rc;
         }
-        for (int j = 0; j < cols; ++j) {
-            std::memcpy(s->hbuf + (size_t)j * pad, in[j], len);
-            vin[j] = {reinterpret_cast<uint8_t*>(s->hbuf_dev + (size_t)j * pad), 0};
+        // column pieces, 4 KiB-aligned, the last one padded to 16 B
+        const uint64_t want = len >= (64u << 10) ? (uint64_t)g_percall_pieces : 1u;
+        const uint64_t step = ((pad + want - 1) / want + 4095) & ~uint64_t(4095);
+        std::vector<uint64_t> cut;
+        for (uint64_t c0 = 0; c0 < pad; c0 += step) cut.push_back(c0);
+        cut.push_back(pad);
+        const size_t np = cut.size() - 1;
+        rc = staging_events(s, np);
+        hipError_t es = hipSuccess;
+        size_t launched = 0;
+        for (size_t p = 0; p < np && !rc; ++p, ++launched) {
+            const uint64_t c0 = cut[p], c1 = cut[p + 1];
+            const uint64_t copy = std::min<uint64_t>(c1, len) - c0;  // caller bytes in this piece
+            for (int j = 0; j < cols; ++j) {
+                uint8_t* dst = s->hbuf + (size_t)j * pad + c0;
+                std::memcpy(dst, in[j] + c0, copy);
+                if (c1 > len) std::memset(dst + copy, 0, c1 - c0 - copy);  // deterministic pad bytes
+                vin[j] = {reinterpret_cast<uint8_t*>(s->hbuf_dev + (size_t)j * pad + c0), 0};
+            }
+            for (int r = 0; r < rows; ++r)
+                vout[r] = {reinterpret_cast<uint8_t*>(s->hbuf_dev + (size_t)(cols + r) * pad + c0), 0};
+            rc = apply_views(rows, cols, coeffs, vin.data(), vout.data(), 1, c1 - c0, s->stream);
+            if (!rc) {
+                es = hipEventRecord(s->ev[p], s->stream);
+                if (es != hipSuccess) rc = hip_fail(es, "hipEventRecord");
+            }
         }
-        for (int r = 0; r < rows; ++r) vout[r] = {reinterpret_cast<uint8_t*>(s->hbuf_dev + (size_t)(cols + r) * pad), 0};
-        rc = apply_views(rows, cols, coeffs, vin.data(), vout.data(), 1, pad, s->stream);
-        const hipError_t es = hipStreamSynchronize(s->stream);
-        if (!rc && es == hipSuccess)
-            for (int r = 0; r < rows; ++r) std::memcpy(out[r], s->hbuf + (size_t)(cols + r) * pad, len);
+        for (size_t p = 0; p < launched; ++p) {  // outputs back, piece by piece as each completes
+            es = hipEventSynchronize(s->ev[p]);
+            if (es != hipSuccess) {
+                if (!rc) rc = hip_fail(es, "hipEventSynchronize");
+                break;
+            }
+            if (rc) continue;
+            const uint64_t c0 = cut[p], copy = std::min<uint64_t>(cut[p + 1], len) - c0;
+            for (int r = 0; r < rows; ++r) std::memcpy(out[r] + c0, s->hbuf + (size_t)(cols + r) * pad + c0, copy);
+        }
+        es = hipStreamSynchronize(s->stream);
         staging_release(s);
         if (rc) return rc;
         if (es != hipSuccess) return hip_fail(es, "hipStreamSynchronize");
