@@ -47,8 +47,9 @@ __device__ constexpr int md5_word(int i) {
 
 __device__ __forceinline__ uint32_t rotl(uint32_t x, int s) { return __builtin_amdgcn_alignbit(x, x, 32 - s); }
 
-// One 64-byte block.  Plain C logic: the compiler maps F/G to v_bfi_b32, H to
-// v_xor3_b32 and I to v_bitop3_b32 (gfx950), a + f + (m + K) to v_add3_u32.
+// One 64-byte block.  Plain C logic: the compiler maps F/G and I to
+// v_bitop3_b32 (gfx950) and a + f + (m + K) to v_add3_u32; H is written as an
+// explicit XOR3 (the compiler emitted two v_xor_b32 for b ^ c ^ d).
 __device__ __forceinline__ void md5_compress(uint32_t (&h)[4], const uint32_t (&m)[16]) {
     uint32_t a = h[0], b = h[1], c = h[2], d = h[3];
 #pragma unroll
@@ -59,7 +60,7 @@ __device__ __forceinline__ void md5_compress(uint32_t (&h)[4], const uint32_t (&
         else if (i < 32)
             f = c ^ (d & (b ^ c));
         else if (i < 48)
-            f = b ^ c ^ d;
+            f = xor3(b, c, d);  // one v_bitop3 (plain C became two v_xor_b32)
         else
             f = c ^ (b | ~d);
         const uint32_t t = a + f + (m[md5_word(i)] + kMd5K[i]);

@@ -119,9 +119,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--label", default="")
+    ap.add_argument("--objects", default="4096", help="comma list of batch sizes (objects per call)")
+    ap.add_argument("--no-scaling", action="store_true")
     args = ap.parse_args()
     torch.cuda.set_device(0)
-    rows = [config(4, 2), config(8, 3)] + chain_scaling() + ([] if args.no_cpu else [cpu_md5()])
+    rows = []
+    for n in map(int, args.objects.split(",")):
+        rows += [config(4, 2, n), config(8, 3, n)]
+    rows += ([] if args.no_scaling else chain_scaling()) + ([] if args.no_cpu else [cpu_md5()])
     for r in rows:
         if args.label:
             r["label"] = args.label

@@ -32,6 +32,10 @@ VARIANTS = {
     "cur": ([], {}),
     # packed kernel (short shards, e.g. 8+3 of 4 KiB objects)
     "pk_vec": ([], {"HBEC_PACKED": "0"}),
+    "md5d2": (["HBEC_MD5_DEPTH=2"], {}),
+    "md5d4": (["HBEC_MD5_DEPTH=4"], {}),
+    "md5d8": (["HBEC_MD5_DEPTH=8"], {}),
+    "md5d4np": (["HBEC_MD5_DEPTH=4", "HBEC_MD5_PINGPONG=0"], {}),
     "ch128k": ([], {"HBEC_CHUNK_TILES": str(128 << 10)}),
     "ch256k": ([], {"HBEC_CHUNK_TILES": str(256 << 10)}),
     "ch512k": ([], {"HBEC_CHUNK_TILES": str(512 << 10)}),
