@@ -67,6 +67,7 @@ struct hbec_batcher {
     int device = 0;
     uint64_t max_batch_bytes = 0;
     std::chrono::microseconds max_wait{0};
+    std::chrono::microseconds quiet{0};  // HBEC_BATCHER_QUIET_US: stop filling after this long with no arrival
     std::mutex mu;
     std::condition_variable cv_work;
     std::deque<Request*> queue;
@@ -126,18 +127,35 @@ struct hbec_batcher {
             };
             cv_work.wait(lk, [&] { return stop || first_mine() != nullptr; });
             if (stop && !first_mine()) return;
-            // let the batch fill: until max bytes queued or max_wait after the oldest arrived
-            const auto deadline = std::chrono::steady_clock::now() + max_wait;
+            // let the batch fill: until max bytes are queued, max_wait has
+            // passed since this worker started waiting, or no request has
+            // arrived for quiet (the callers that were going to come have
+            // come: small stripes never fill max bytes, and waiting out
+            // max_wait would dominate their round trip)
+            const auto t0 = std::chrono::steady_clock::now();
+            const auto deadline = t0 + max_wait;
             // MD5 groups stay smaller (max_batch_bytes / md5 workers): a group
             // is held ~2.3 ms by its hash however small it is, so the bytes
             // are better spread over more workers hashing at once
             const uint64_t cap = md5_only && md5_workers > 0 ? md5_cap : batch_cap;
+            size_t seen_n = 0;
+            auto last_arrival = t0;
             while (!stop) {
                 uint64_t queued = 0;
+                size_t n_mine = 0;
                 for (auto* r : queue)
-                    if (mine(r)) queued += r->stripe.shard_len * (uint64_t)n_shards;
+                    if (mine(r)) {
+                        queued += r->stripe.shard_len * (uint64_t)n_shards;
+                        ++n_mine;
+                    }
                 if (queued >= cap) break;
-                if (cv_work.wait_until(lk, deadline) == std::cv_status::timeout) break;
+                const auto now = std::chrono::steady_clock::now();
+                if (n_mine != seen_n) {
+                    seen_n = n_mine;
+                    last_arrival = now;
+                }
+                if (now >= deadline || now - last_arrival >= quiet) break;
+                (void)cv_work.wait_until(lk, std::min(deadline, last_arrival + quiet));
             }
             const Request* head = first_mine();
             if (!head) continue;  // another worker took it while this one waited
@@ -219,6 +237,8 @@ int hbec_batcher_new(hbec_codec* codec, uint64_t max_batch_bytes, uint32_t max_w
         b->codec = codec;
         b->max_batch_bytes = max_batch_bytes ? max_batch_bytes : (256ull << 20);
         b->max_wait = std::chrono::microseconds(max_wait_us);
+        const char* envq = std::getenv("HBEC_BATCHER_QUIET_US");
+        b->quiet = std::chrono::microseconds(envq ? std::max(1, std::atoi(envq)) : 20);
         const char* env = std::getenv("HBEC_BATCHER_WORKERS");
         const int n_workers = std::min(8, std::max(1, env ? std::atoi(env) : 2));
         const char* env5 = std::getenv("HBEC_BATCHER_MD5_WORKERS");

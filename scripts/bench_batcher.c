@@ -27,7 +27,8 @@
 
 #include "hbec.h"
 
-enum { K = 4, M = 2, S = 1 << 18 };
+enum { K = 4, M = 2 };
+static size_t S = 1 << 18;  /* shard bytes: object bytes / K (argv[7], default 1 MiB objects) */
 
 typedef struct {
     hbec_codec* codec;
@@ -52,7 +53,7 @@ static void* caller(void* arg) {
             j->rc = hbec_encode_databuf(j->codec, base, S);
         } else if (j->mode == 2) {
             hbec_stripe st = {base, S};
-            uint8_t dig[(K + M) * 16];
+            uint8_t dig[(K + M) * 16];  /* digests not checked here: tests compare them with hashlib */
             j->rc = hbec_batcher_encode_md5(j->bat, &st, dig);
         } else {
             hbec_stripe st = {base, S};
@@ -69,6 +70,8 @@ int main(int argc, char** argv) {
     const uint64_t max_mb = argc > 4 ? (uint64_t)atoll(argv[4]) : 96;
     const uint32_t wait_us = argc > 5 ? (uint32_t)atoi(argv[5]) : 300;
     const int mode = argc > 6 ? atoi(argv[6]) : 0;
+    if (argc > 7) S = (size_t)atoll(argv[7]) / K;
+    if (S == 0 || S % 16) return 2;
     if (threads < 1 || threads > 1024 || per < 1) return 2;
     const size_t n = (size_t)threads * per, stripe = (size_t)(K + M) * S;
     uint8_t* pool = NULL;
@@ -133,13 +136,13 @@ int main(int argc, char** argv) {
         if (hbec_verify(codec, sh, lens, K + M, &ok) || !ok) bad = 1;
     }
     const char* co = getenv("HBEC_COALESCE");
-    printf("{\"measure\": \"%s_native_callers_Encode_1MiB_%s\", \"threads\": %d, \"objects\": %zu, "
+    printf("{\"measure\": \"%s_native_callers_Encode_%zuB_%s\", \"threads\": %d, \"objects\": %zu, "
            "\"max_batch_MiB\": %llu, \"max_wait_us\": %u, \"seconds\": %.4f, \"object_data_GiB_s\": %.2f, "
-           "\"us_per_object\": %.1f, \"batches\": %llu, \"parity_ok\": %s}\n",
+           "\"us_per_object\": %.2f, \"objects_per_s\": %.0f, \"batches\": %llu, \"parity_ok\": %s}\n",
            mode == 1 ? (co && co[0] == '0' ? "percall_databuf_uncoalesced" : "percall_databuf_coalesced")
                      : (mode == 2 ? "batcher_md5" : "batcher"),
-           pinned ? "pinned" : "pageable", threads, n, (unsigned long long)max_mb, wait_us, secs,
-           n * (double)K * S / secs / (double)(1 << 30), secs / n * 1e6, (unsigned long long)(b1 - b0),
+           (size_t)K * S, pinned ? "pinned" : "pageable", threads, n, (unsigned long long)max_mb, wait_us, secs,
+           n * (double)K * S / secs / (double)(1 << 30), secs / n * 1e6, n / secs, (unsigned long long)(b1 - b0),
            bad ? "false" : "true");
     hbec_free(codec);
     if (pinned) hbec_host_free(pool);
