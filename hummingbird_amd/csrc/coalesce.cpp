@@ -43,7 +43,8 @@ struct CoReq {
     int data_only = 0;
     int rc = HBEC_OK;
     std::string err;
-    bool taken = false, done = false;
+    bool taken = false, done = false, lead = false;
+    std::condition_variable cv;  // this caller's own wake-up: done, or asked to lead
 
     bool same_group(const CoReq& o) const {
         return codec == o.codec && dev == o.dev && op == o.op && data_only == o.data_only && present == o.present;
@@ -51,7 +52,9 @@ struct CoReq {
 };
 
 // Groups coded at once (HBEC_COALESCE_INFLIGHT, default 2): below this many
-// concurrent callers every call still runs at once, as if uncoalesced.
+// concurrent callers every call still runs at once, as if uncoalesced.  A
+// call that is handed a slot but was already taken into another group passes
+// the slot on, so at most this many groups ever run.
 int max_in_flight() {
     static const int v = [] {
         const char* e = std::getenv("HBEC_COALESCE_INFLIGHT");
@@ -63,9 +66,8 @@ int max_in_flight() {
 
 struct Coalescer {
     std::mutex mu;
-    std::condition_variable cv;
     std::deque<CoReq*> q;
-    int in_flight = 0;
+    int leaders = 0;  // calls holding a lead slot: coding a group, or woken to form one
     uint64_t groups = 0, calls = 0;
 };
 
@@ -140,42 +142,64 @@ int coalesced_call(hbec_codec* codec, int op, uint8_t* base, uint64_t s, const u
     const uint64_t cap = group_cap_bytes();
     std::unique_lock<std::mutex> lk(g_co.mu);
     g_co.q.push_back(&r);
+    // Every wake-up is addressed: a finished group wakes its own members, and
+    // hands its lead slot to the oldest queued call.  (One shared condition
+    // variable woke all ~128 waiters per group and ran 4 KiB stripes at
+    // 42 k calls/s.)
+    auto pass_slot = [&] {
+        for (CoReq* x : g_co.q)  // every queued call is untaken
+            if (!x->lead) {
+                x->lead = true;
+                x->cv.notify_one();
+                return;
+            }
+        --g_co.leaders;
+    };
+    if (g_co.leaders < max_in_flight()) {
+        ++g_co.leaders;
+        r.lead = true;
+    }
     for (;;) {
-        if (r.done) break;
-        if (!r.taken && g_co.in_flight < max_in_flight()) {
-            // lead: this call plus every queued call of the same group, up to cap bytes
-            std::vector<CoReq*> grp;
-            uint64_t bytes = 0;
-            for (CoReq* x : g_co.q) {
-                if (x->taken || !(x == &r || x->same_group(r))) continue;
-                const uint64_t b = x->s * (uint64_t)n_shards;
-                if (x != &r && bytes + b > cap) continue;
-                x->taken = true;
-                grp.push_back(x);
-                bytes += b;
+        r.cv.wait(lk, [&] { return r.done || r.lead; });
+        if (r.lead) {
+            r.lead = false;
+            if (r.taken) {  // another leader's group took this call first
+                pass_slot();
+            } else {
+                // lead: this call plus every queued call of the same group, up to cap bytes
+                std::vector<CoReq*> grp;
+                uint64_t bytes = 0;
+                for (CoReq* x : g_co.q) {
+                    if (!(x == &r || x->same_group(r))) continue;
+                    const uint64_t b = x->s * (uint64_t)n_shards;
+                    if (x != &r && bytes + b > cap) continue;
+                    x->taken = true;
+                    grp.push_back(x);
+                    bytes += b;
+                }
+                g_co.q.erase(std::remove_if(g_co.q.begin(), g_co.q.end(), [](CoReq* x) { return x->taken; }),
+                             g_co.q.end());
+                ++g_co.groups;
+                g_co.calls += grp.size();
+                lk.unlock();
+                // no exception may leave the group half-done: the other
+                // members would wait forever
+                try {
+                    run_group(grp, fn);
+                } catch (const std::bad_alloc&) {
+                    for (auto* x : grp) x->rc = HBEC_ERR_NOMEM, x->err = "coalesced call: host allocation failed";
+                } catch (...) {
+                    for (auto* x : grp) x->rc = HBEC_ERR_DEVICE, x->err = "coalesced call: unexpected exception";
+                }
+                lk.lock();
+                for (auto* x : grp) {
+                    x->done = true;
+                    if (x != &r) x->cv.notify_one();
+                }
+                pass_slot();
             }
-            g_co.q.erase(std::remove_if(g_co.q.begin(), g_co.q.end(), [](CoReq* x) { return x->taken; }),
-                         g_co.q.end());
-            ++g_co.in_flight;
-            ++g_co.groups;
-            g_co.calls += grp.size();
-            lk.unlock();
-            // no exception may leave the group half-done: the other members
-            // would wait forever
-            try {
-                run_group(grp, fn);
-            } catch (const std::bad_alloc&) {
-                for (auto* x : grp) x->rc = HBEC_ERR_NOMEM, x->err = "coalesced call: host allocation failed";
-            } catch (...) {
-                for (auto* x : grp) x->rc = HBEC_ERR_DEVICE, x->err = "coalesced call: unexpected exception";
-            }
-            lk.lock();
-            --g_co.in_flight;
-            for (auto* x : grp) x->done = true;
-            g_co.cv.notify_all();
-            continue;
         }
-        g_co.cv.wait(lk);
+        if (r.done) break;
     }
     lk.unlock();
     return r.rc ? fail(r.rc, r.err) : HBEC_OK;
