@@ -26,10 +26,10 @@ for s in "$@"; do
     tests) step tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
     testsall) step testsall 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    bench) step bench 600 python bench.py --steps 20 --warmup 5 ;;
+    bench) step bench 600 python bench.py --steps 50 --warmup 10 ;;
     prof)
       mkdir -p "$OUT/prof"
-      (cd /tmp && step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-host-path --config5-objects 0) || exit $?
+      (cd /tmp && step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --steps 50 --warmup 10 --no-cpu-baseline --no-host-path --config5-objects 0) || exit $?
       ;;
     pmcfetch)
       mkdir -p "$OUT/pmc_fetch"
