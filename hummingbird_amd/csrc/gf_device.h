@@ -197,6 +197,38 @@ __device__ __forceinline__ void gf_dot(u32x4 (&acc)[R], const u32x4 (&x)[K], con
     }
 }
 
+// ---- Packed coordinates (gf_apply_packed, gf_verify_packed) ----
+// Element e (16 B) of the concatenated shard columns of all objects is byte
+// (e % spo)*16 of object e / spo (spo = shard_len / 16).  Lanes past n_elems
+// are clamped to the last element: they load live bytes and store / flag
+// nothing.
+template <int U>
+struct PackedCoord {
+    uint32_t obj[U];  // per lane
+    uint32_t off[U];  // per lane: byte offset inside the shard
+};
+
+template <int U>
+__device__ __forceinline__ void packed_coords(PackedCoord<U>& c, uint32_t t, uint32_t lane, uint32_t n_elems,
+                                              uint32_t spo, double inv) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        uint32_t e = (t * (uint32_t)U + (uint32_t)u) * 64u + lane;
+        e = e < n_elems ? e : n_elems - 1u;  // clamped lanes load live bytes, store nothing
+        uint32_t q = (uint32_t)((double)e * inv);  // e < 2^31: exact up to one step, fixed below
+        int32_t r = (int32_t)(e - q * spo);
+        if (r < 0) {
+            q -= 1u;
+            r += (int32_t)spo;
+        } else if (r >= (int32_t)spo) {
+            q += 1u;
+            r -= (int32_t)spo;
+        }
+        c.obj[u] = q;
+        c.off[u] = (uint32_t)r * 16u;
+    }
+}
+
 // ---- Tuning only: field multiply through LDS tables (HBEC_GF_LDS) ----
 // The default multiply above keeps every table in registers (v_perm_b32).
 // These variants exist to measure the classic alternatives on the same

@@ -810,6 +810,52 @@ static int verify_views(hbec_codec* c, const hbec_view* views, uint64_t n_obj, u
     bool vec = (shard_len % 16) == 0;
     for (int i = 0; i < k + m && vec; ++i) vec = aligned16(views[i].base) && (views[i].obj_stride % 16) == 0;
     const uint8_t* prow = c->matrix.data() + (size_t)k * k;
+    if (vec && is_verify_packed_shape(k, m, shard_len)) {
+        // short shards: wave tiles across objects (gf_verify_packed)
+        PassArgs a;
+        std::memset(&a, 0, sizeof(a));
+        for (int j = 0; j < k; ++j) {
+            a.in[j] = static_cast<const uint8_t*>(views[j].base);
+            a.in_stride[j] = views[j].obj_stride;
+        }
+        for (int r = 0; r < m; ++r) {
+            a.out[r] = static_cast<uint8_t*>(views[k + r].base);
+            a.out_stride[r] = views[k + r].obj_stride;
+            for (int j = 0; j < k; ++j) perm_table(prow[(size_t)r * k + j], a.tab[r][j]);
+        }
+        a.shard_len = shard_len;
+        int dev = 0, cus = 0, bpc = 1;
+        int rc = current_device(&dev);
+        if (rc) return rc;
+        hipDeviceProp_t p;
+        hipError_t e = hipGetDeviceProperties(&p, dev);
+        if (e != hipSuccess) return hip_fail(e, "hipGetDeviceProperties");
+        cus = p.multiProcessorCount;
+        e = verify_packed_occupancy(k, m, &bpc);
+        if (e != hipSuccess) return hip_fail(e, "verify occupancy");
+        bpc = std::max(1, bpc);
+        if (g_blocks_per_cu_override > 0) bpc = g_blocks_per_cu_override;
+        const uint64_t spo = shard_len / 16;
+        const uint64_t te = (uint64_t)verify_packed_tile_elems(k);
+        uint64_t max_obj = std::max<uint64_t>(1, ((1ull << 31) - te) / spo);  // n_elems < 2^31
+        max_obj = std::min(max_obj, std::max<uint64_t>(1, g_chunk_tiles * te / spo));
+        for (uint64_t o0 = 0; o0 < n_obj; o0 += max_obj) {
+            const uint64_t no = std::min(max_obj, n_obj - o0);
+            PassArgs b = a;
+            for (int j = 0; j < k; ++j) b.in[j] = a.in[j] + o0 * a.in_stride[j];
+            for (int r = 0; r < m; ++r) b.out[r] = a.out[r] + o0 * a.out_stride[r];
+            b.n_obj = no;
+            b.elems_per_obj = (uint32_t)spo;
+            b.n_elems = (uint32_t)(no * spo);
+            b.n_tiles = (uint32_t)((no * spo + te - 1) / te);
+            const uint64_t wpb = (uint64_t)kPipeBlockThreads / 64;
+            const uint64_t want = (b.n_tiles + wpb - 1) / wpb;
+            const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cus * bpc));
+            e = launch_verify_packed(k, m, b, flags + o0, grid, stream);
+            if (e != hipSuccess) return hip_fail(e, "launch gf_verify_packed");
+        }
+        return HBEC_OK;
+    }
     if (vec && verify_supported(k, m)) {
         PassArgs a;
         std::memset(&a, 0, sizeof(a));

@@ -150,5 +150,10 @@ bool verify_supported(int k, int r);
 hipError_t launch_verify(int k, int r, const PassArgs& a, uint32_t* flags, int grid, hipStream_t stream);
 hipError_t verify_occupancy(int k, int r, int* blocks_per_cu);
 hipError_t launch_compare(int r, const PassArgs& a, uint32_t* flags, int grid, hipStream_t stream);
+// packed verify (short shards; same element walk as the packed apply path)
+int is_verify_packed_shape(int k, int r, uint64_t shard_len);
+int verify_packed_tile_elems(int k);
+hipError_t verify_packed_occupancy(int k, int r, int* blocks_per_cu);
+hipError_t launch_verify_packed(int k, int r, const PassArgs& a, uint32_t* flags, int grid, hipStream_t stream);
 
 }  // namespace hbec

@@ -397,33 +397,6 @@ __global__ __launch_bounds__(kPipeBlockThreads, HBEC_PIPE_WAVES_PER_SIMD) void g
 // the next tile's loads in flight while this tile computes and stores, one
 // block barrier per tile, block-uniform trip count (past-the-end waves load
 // the last tile and store nothing).
-template <int U>
-struct PackedCoord {
-    uint32_t obj[U];  // per lane
-    uint32_t off[U];  // per lane: byte offset inside the shard
-};
-
-template <int U>
-__device__ __forceinline__ void packed_coords(PackedCoord<U>& c, uint32_t t, uint32_t lane, uint32_t n_elems,
-                                              uint32_t spo, double inv) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        uint32_t e = (t * (uint32_t)U + (uint32_t)u) * 64u + lane;
-        e = e < n_elems ? e : n_elems - 1u;  // clamped lanes load live bytes, store nothing
-        uint32_t q = (uint32_t)((double)e * inv);  // e < 2^31: exact up to one step, fixed below
-        int32_t r = (int32_t)(e - q * spo);
-        if (r < 0) {
-            q -= 1u;
-            r += (int32_t)spo;
-        } else if (r >= (int32_t)spo) {
-            q += 1u;
-            r -= (int32_t)spo;
-        }
-        c.obj[u] = q;
-        c.off[u] = (uint32_t)r * 16u;
-    }
-}
-
 template <int K, int U>
 __device__ __forceinline__ void packed_load(u32x4 (&x)[U][K], const PassArgs& a, const PackedCoord<U>& c) {
 #pragma unroll

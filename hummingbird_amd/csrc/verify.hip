@@ -10,6 +10,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
+
 #include "gf_device.h"
 #include "kernels.h"
 
@@ -91,6 +93,125 @@ __global__ __launch_bounds__(kPipeBlockThreads, 1) void gf_verify_pipe(PassArgs 
     check_tile<K, R, U>(cur, a, tb, obj, base + lane * 16u, flags);
 }
 
+// ---------------------------------------------------------------------------
+// gf_verify_packed: Verify for short shards (below one verify tile, e.g. the
+// 512-B shards of 8+3 over 4 KiB objects, or 1 KiB of 4+2), where
+// gf_verify_pipe's per-object tiles leave most lanes clamped.  Like
+// gf_apply_packed it walks the concatenated shard columns of all objects
+// (gf_device.h packed_coords), so every lane reads live bytes: K + R loads
+// per 16-B element, the next tile's loads in flight, and each lane flags its
+// own object on a mismatch.
+#ifndef HBEC_VERIFY_PACKED_U_SMALL
+#define HBEC_VERIFY_PACKED_U_SMALL 2  // 16-B elements per lane per tile, K <= 4
+#endif
+#ifndef HBEC_VERIFY_PACKED_U_BIG
+#define HBEC_VERIFY_PACKED_U_BIG 1  // K > 4
+#endif
+#ifndef HBEC_VERIFY_PACKED_BARRIER
+#define HBEC_VERIFY_PACKED_BARRIER 1
+#endif
+__host__ __device__ constexpr int verify_packed_u(int k) {
+    return k <= 4 ? HBEC_VERIFY_PACKED_U_SMALL : HBEC_VERIFY_PACKED_U_BIG;
+}
+
+template <int K, int R, int U>
+__device__ __forceinline__ void packed_verify_load(u32x4 (&x)[U][K + R], const PassArgs& a,
+                                                   const PackedCoord<U>& c) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+        for (int j = 0; j < K; ++j) x[u][j] = ld16(a.in[j] + (uint64_t)c.obj[u] * a.in_stride[j] + c.off[u]);
+#pragma unroll
+        for (int r = 0; r < R; ++r) x[u][K + r] = ld16(a.out[r] + (uint64_t)c.obj[u] * a.out_stride[r] + c.off[u]);
+    }
+}
+
+// live = elements this tile may flag: n_elems, or 0 for a past-the-end wave
+template <int K, int R, int U>
+__device__ __forceinline__ void packed_check(const u32x4 (&x)[U][K + R], const PassArgs& a, const Tables<K, R>& tb,
+                                             const PackedCoord<U>& c, uint32_t t, uint32_t live, uint32_t lane,
+                                             uint32_t* flags) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        u32x4 acc[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r] = u32x4{0, 0, 0, 0};
+        u32x4 in[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) in[j] = x[u][j];
+        gf_dot<K, R>(acc, in, a.tab, tb);
+        uint32_t bad = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const u32x4 d = acc[r] ^ x[u][K + r];
+            bad |= d.x | d.y | d.z | d.w;
+        }
+        if (bad != 0 && (t * (uint32_t)U + (uint32_t)u) * 64u + lane < live) atomicOr(flags + c.obj[u], 1u);
+    }
+}
+
+template <int K, int R>
+__global__ __launch_bounds__(kPipeBlockThreads, 1) void gf_verify_packed(PassArgs a, uint32_t* flags) {
+    constexpr int U = verify_packed_u(K);
+    constexpr uint32_t WPB = kPipeBlockThreads / 64;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t nw = gridDim.x * WPB;
+    // raw block order, as gf_verify_pipe (read-only stream)
+    const uint32_t wave0 = __builtin_amdgcn_readfirstlane(blockIdx.x * WPB);
+    const uint32_t dw = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t n = a.n_tiles;
+    if (wave0 >= n) return;  // whole blocks only: the loop below has block barriers
+    const Tables<K, R> tb = load_tables<K, R>(a.tab);
+    const uint32_t spo = a.elems_per_obj;
+    const double inv = 1.0 / (double)spo;
+    uint32_t t = wave0 + dw;
+    PackedCoord<U> cur;
+    packed_coords<U>(cur, t < n ? t : n - 1u, lane, a.n_elems, spo, inv);
+    u32x4 x[U][K + R];
+    packed_verify_load<K, R, U>(x, a, cur);
+    for (uint32_t b0 = wave0 + nw; b0 < n; b0 += nw) {  // block-uniform trip count
+        const uint32_t tn = b0 + dw;
+        PackedCoord<U> nxt;
+        packed_coords<U>(nxt, tn < n ? tn : n - 1u, lane, a.n_elems, spo, inv);
+        u32x4 y[U][K + R];
+        packed_verify_load<K, R, U>(y, a, nxt);
+        if (HBEC_VERIFY_PACKED_BARRIER) __builtin_amdgcn_s_barrier();
+        packed_check<K, R, U>(x, a, tb, cur, t, t < n ? a.n_elems : 0u, lane, flags);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int j = 0; j < K + R; ++j) x[u][j] = y[u][j];
+        cur = nxt;
+        t = tn;
+    }
+    packed_check<K, R, U>(x, a, tb, cur, t, t < n ? a.n_elems : 0u, lane, flags);
+}
+
+template <int K>
+static const void* verify_packed_for_r(int r) {
+    switch (r) {
+        case 1: return reinterpret_cast<const void*>(&gf_verify_packed<K, 1>);
+        case 2: return reinterpret_cast<const void*>(&gf_verify_packed<K, 2>);
+        case 3: return reinterpret_cast<const void*>(&gf_verify_packed<K, 3>);
+        case 4: return reinterpret_cast<const void*>(&gf_verify_packed<K, 4>);
+    }
+    return nullptr;
+}
+
+static const void* verify_packed_kernel(int k, int r) {
+    switch (k) {
+        case 1: return verify_packed_for_r<1>(r);
+        case 2: return verify_packed_for_r<2>(r);
+        case 3: return verify_packed_for_r<3>(r);
+        case 4: return verify_packed_for_r<4>(r);
+        case 5: return verify_packed_for_r<5>(r);
+        case 6: return verify_packed_for_r<6>(r);
+        case 7: return verify_packed_for_r<7>(r);
+        case 8: return verify_packed_for_r<8>(r);
+    }
+    return nullptr;
+}
+
 template <int K>
 static const void* verify_for_r(int r) {
     switch (r) {
@@ -145,6 +266,52 @@ hipError_t verify_occupancy(int k, int r, int* blocks_per_cu) {
 }
 
 int verify_tile_bytes(int k) { return verify_u(k) * 1024; }
+
+// Shards shorter than max(one verify tile, 2 KiB) take the packed verify
+// (HBEC_VERIFY_PACKED=0 turns it off for A/B; HBEC_VERIFY_PACKED_MAX_SHARD=B
+// moves the threshold).
+static const bool g_verify_packed_on = [] {
+    const char* e = std::getenv("HBEC_VERIFY_PACKED");
+    return !(e && e[0] == '0');
+}();
+static const uint64_t g_verify_packed_max = [] {
+    const char* e = std::getenv("HBEC_VERIFY_PACKED_MAX_SHARD");
+    return e ? (uint64_t)std::atoll(e) : 0ull;
+}();
+
+int is_verify_packed_shape(int k, int r, uint64_t shard_len) {
+    const uint64_t tile = (uint64_t)verify_tile_bytes(k);
+    const uint64_t lim = g_verify_packed_max ? g_verify_packed_max : (tile > 2048u ? tile : 2048u);
+    return (g_verify_packed_on && shard_len >= 16 && shard_len % 16 == 0 && shard_len < lim &&
+            verify_packed_kernel(k, r) != nullptr)
+               ? 1
+               : 0;
+}
+
+int verify_packed_tile_elems(int k) { return verify_packed_u(k) * 64; }
+
+#ifndef HBEC_VERIFY_PACKED_BLOCKS_SMALL
+#define HBEC_VERIFY_PACKED_BLOCKS_SMALL 2
+#endif
+#ifndef HBEC_VERIFY_PACKED_BLOCKS_BIG
+#define HBEC_VERIFY_PACKED_BLOCKS_BIG 2
+#endif
+
+hipError_t verify_packed_occupancy(int k, int r, int* blocks_per_cu) {
+    const void* fn = verify_packed_kernel(k, r);
+    if (!fn) return hipErrorInvalidValue;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, kPipeBlockThreads, 0);
+    const int cap = k <= 4 ? HBEC_VERIFY_PACKED_BLOCKS_SMALL : HBEC_VERIFY_PACKED_BLOCKS_BIG;
+    if (e == hipSuccess && cap > 0 && *blocks_per_cu > cap) *blocks_per_cu = cap;
+    return e;
+}
+
+hipError_t launch_verify_packed(int k, int r, const PassArgs& a, uint32_t* flags, int grid, hipStream_t stream) {
+    const void* fn = verify_packed_kernel(k, r);
+    if (!fn) return hipErrorInvalidValue;
+    void* args[] = {const_cast<PassArgs*>(&a), &flags};
+    return hipLaunchKernel(fn, dim3(grid), dim3(kPipeBlockThreads), args, 0, stream);
+}
 
 hipError_t launch_verify(int k, int r, const PassArgs& a, uint32_t* flags, int grid, hipStream_t stream) {
     const void* fn = verify_kernel(k, r);

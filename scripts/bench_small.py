@@ -91,9 +91,15 @@ def run(k, m, n, size, miss, scrub):
     emit(f"{k}+{m} encode {n}x{size} isolated", enc_b, isolated_ms(encode, scrub), kernel=info["kind"])
     emit(f"{k}+{m} reconstruct{set(miss)} {n}x{size} stream", rec_b, stream_ms(reconstruct), kernel=info["kind"])
     emit(f"{k}+{m} reconstruct{set(miss)} {n}x{size} isolated", rec_b, isolated_ms(reconstruct, scrub))
-    # self-check: every object's parity verifies; rebuilt shards equal the originals
+    # self-check: every object's parity verifies (Encoder.Verify, a different
+    # kernel, timed too: (k+m)*S read per object); rebuilt shards equal the originals
     flags = torch.zeros(n, dtype=torch.int32, device="cuda")
-    B.verify_views(enc, views, n, s, flags)
+
+    def verify():
+        B.verify_views(enc, views, n, s, flags)
+
+    emit(f"{k}+{m} verify {n}x{size} stream", enc_b, stream_ms(verify), bound="HBM read")
+    emit(f"{k}+{m} verify {n}x{size} isolated", enc_b, isolated_ms(verify, scrub), bound="HBM read")
     torch.cuda.synchronize()
     assert int(flags.count_nonzero()) == 0, "parity does not verify"
     for slot, i in enumerate(miss):

@@ -32,6 +32,13 @@ VARIANTS = {
     "cur": ([], {}),
     # packed kernel (short shards, e.g. 8+3 of 4 KiB objects)
     "pk_vec": ([], {"HBEC_PACKED": "0"}),
+    # packed verify (short shards): run scripts/bench_small.py with HBEC_LIB=tune_build/<name>/libhbec.so
+    "vp_u1": (["HBEC_VERIFY_PACKED_U_SMALL=1"], {}),
+    "vp_u4": (["HBEC_VERIFY_PACKED_U_SMALL=4"], {}),
+    "vp_b1": (["HBEC_VERIFY_PACKED_BLOCKS_SMALL=1", "HBEC_VERIFY_PACKED_BLOCKS_BIG=1"], {}),
+    "vp_b3": (["HBEC_VERIFY_PACKED_BLOCKS_SMALL=3", "HBEC_VERIFY_PACKED_BLOCKS_BIG=2"], {}),
+    "vp_ub2": (["HBEC_VERIFY_PACKED_U_BIG=2"], {}),
+    "vp_nobar": (["HBEC_VERIFY_PACKED_BARRIER=0"], {}),
     "md5d2": (["HBEC_MD5_DEPTH=2"], {}),
     "md5d4": (["HBEC_MD5_DEPTH=4"], {}),
     "md5d8": (["HBEC_MD5_DEPTH=8"], {}),

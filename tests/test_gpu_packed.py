@@ -83,3 +83,55 @@ def test_packed_kernel_is_selected_for_short_shards():
     assert B.kernel_info(4, 2, 1024)["kind"] == "packed"
     assert B.kernel_info(4, 2, 2048)["kind"] == "pipelined"
     assert B.kernel_info(8, 3, 3072)["kind"] == "pipelined"
+
+
+def _verify_packed(k, s):
+    """verify.hip is_verify_packed_shape: S < max(verify tile, 2 KiB), i.e.
+    S < 4 KiB for K <= 4 and S < 2 KiB for 5 <= K <= 8."""
+    return s % 16 == 0 and s < (4096 if k <= 4 else 2048)
+
+
+def _verify_cases():
+    for k, m in SHAPES + [(4, 4), (8, 4), (2, 4)]:
+        for s in LENS + [3072, 4080]:
+            if _verify_packed(k, s):
+                yield k, m, s
+
+
+@pytest.mark.parametrize("k,m,s", list(_verify_cases()))
+@pytest.mark.parametrize("n", [1, 7, 333])
+def test_packed_verify_oracle_parity_and_flips(k, m, s, n):
+    """gf_verify_packed on parity the oracle computed (not the GPU encoder):
+    every object clean, then single-byte flips in chosen objects' data or
+    parity shards flag exactly those objects — objects share a wave here, so
+    each lane must flag its own object."""
+    pad = 32
+    rng = np.random.default_rng(k * 7919 + m * 131 + s + n)
+    data = rng.integers(0, 256, size=(n, k * s + pad), dtype=np.uint8)
+    want, _ = CO.encode_batch(k, m, np.ascontiguousarray(data[:, :k * s]))
+    par = np.zeros((n, m * s + pad), dtype=np.uint8)
+    par[:, :m * s] = want
+    objs = torch.from_numpy(data).cuda()
+    parity = torch.from_numpy(par).cuda()
+    enc = RS.New(k, m)
+    views = [(objs.data_ptr() + j * s, objs.stride(0)) for j in range(k)]
+    views += [(parity.data_ptr() + r * s, parity.stride(0)) for r in range(m)]
+    flags = torch.zeros(n, dtype=torch.int32, device="cuda")
+    B.verify_views(enc, views, n, s, flags)
+    torch.cuda.synchronize()
+    assert int(flags.count_nonzero()) == 0
+    bad = sorted(set(rng.integers(0, n, size=min(n, 5)).tolist()))
+    for o in bad:
+        shard = int(rng.integers(0, k + m))
+        off = int(rng.integers(0, s))
+        if shard < k:
+            objs[o, shard * s + off] ^= 0x5A
+        else:
+            parity[o, (shard - k) * s + off] ^= 0x5A
+    # bytes outside the shards (row padding) are not part of any object
+    objs[:, k * s:] ^= 0xFF
+    parity[:, m * s:] ^= 0xFF
+    flags.zero_()
+    B.verify_views(enc, views, n, s, flags)
+    torch.cuda.synchronize()
+    assert torch.nonzero(flags).flatten().tolist() == bad
