@@ -52,11 +52,13 @@ __device__ __forceinline__ void load_stripe_tile(u32x4 (&x)[U][K], const uint64_
 
 // ACC: a later pass over inputs beyond the first 8 (k > 8): the outputs
 // already hold the earlier passes' partial sums and are read back and
-// XOR-accumulated (clamped like the input loads; stores stay masked).
+// XOR-accumulated (clamped to the tile's `valid` bytes like the input loads).
+// `live` = bytes this wave stores: the tile's valid bytes, or 0 for a
+// past-the-end stand-in tile (block-uniform trip count below).
 template <int K, int R, int U, bool FULL, bool ACC>
 __device__ __forceinline__ void store_stripe_tile_(const u32x4 (&x)[U][K], const StripeArgs& a,
                                                    const Tables<K, R>& tb, const uint64_t (&dst)[R], uint32_t valid,
-                                                   uint32_t lane) {
+                                                   uint32_t live, uint32_t lane) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const uint64_t off = (uint64_t)lane * 16u + (uint64_t)u * 1024u;
@@ -71,7 +73,7 @@ __device__ __forceinline__ void store_stripe_tile_(const u32x4 (&x)[U][K], const
             for (int r = 0; r < R; ++r) acc[r] = u32x4{0, 0, 0, 0};
         }
         gf_dot<K, R>(acc, x[u], a.tab, tb);
-        if (FULL || off < valid) {
+        if (FULL || off < live) {
 #pragma unroll
             for (int r = 0; r < R; ++r) st16_addr(dst[r] + off, acc[r]);
         }
@@ -80,11 +82,12 @@ __device__ __forceinline__ void store_stripe_tile_(const u32x4 (&x)[U][K], const
 
 template <int K, int R, int U, bool ACC>
 __device__ __forceinline__ void store_stripe_tile(const u32x4 (&x)[U][K], const StripeArgs& a, const Tables<K, R>& tb,
-                                                  const uint64_t (&dst)[R], uint32_t valid, uint32_t lane) {
-    if (valid >= (uint32_t)U * 1024u)  // wave-uniform: whole tile live
-        store_stripe_tile_<K, R, U, true, ACC>(x, a, tb, dst, valid, lane);
+                                                  const uint64_t (&dst)[R], uint32_t valid, uint32_t live,
+                                                  uint32_t lane) {
+    if (live >= (uint32_t)U * 1024u)  // wave-uniform: whole tile live
+        store_stripe_tile_<K, R, U, true, ACC>(x, a, tb, dst, valid, live, lane);
     else
-        store_stripe_tile_<K, R, U, false, ACC>(x, a, tb, dst, valid, lane);
+        store_stripe_tile_<K, R, U, false, ACC>(x, a, tb, dst, valid, live, lane);
 }
 
 // Tile records are read-only for the whole launch and passed as a separate
@@ -93,26 +96,41 @@ __device__ __forceinline__ TileRec load_rec(const TileRec* __restrict__ recs, ui
     return recs[i];
 }
 
+// Pacing as in gf_apply_vec_pipe2 (DESIGN.md §4 ladder steps 7 and 9): one
+// block barrier per tile after the next tile's loads are issued, so a
+// block's 4 waves load and store in step, and an optional s_sleep (x 64
+// cycles) before it.  The trip count is block-uniform: waves past the end
+// load a stand-in tile (the last one) and store nothing.
+#ifndef HBEC_STRIPES_BARRIER
+#define HBEC_STRIPES_BARRIER 1
+#endif
+#ifndef HBEC_STRIPES_SLEEP
+#define HBEC_STRIPES_SLEEP 0
+#endif
+
 template <int K, int R, bool SPLIT, bool ACC = false>
 __global__ __launch_bounds__(kBlockThreads, 1) void gf_apply_stripes(StripeArgs a,
                                                                      const TileRec* __restrict__ tiles) {
     // accumulate passes follow a first pass of exactly kStripeMaxK inputs: same tiles
     constexpr int U = ACC ? stripes_u(kStripeMaxK) : stripes_u(K);
+    constexpr uint32_t WPB = kBlockThreads / 64;
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave =
-        __builtin_amdgcn_readfirstlane(xcd_block() * (kBlockThreads / 64) + (threadIdx.x >> 6));
-    const uint32_t nw = gridDim.x * (kBlockThreads / 64);
+    const uint32_t wave0 = __builtin_amdgcn_readfirstlane(xcd_block() * WPB);
+    const uint32_t dw = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t nw = gridDim.x * WPB;
     const uint32_t n = a.n_tiles;
-    if (wave >= n) return;
+    if (wave0 >= n) return;  // whole blocks only: the loop below has block barriers
     const Tables<K, R> tb = load_tables<K, R>(a.tab);
-    TileRec cur = load_rec(tiles, wave);
+    uint32_t t = wave0 + dw;
+    TileRec cur = load_rec(tiles, t < n ? t : n - 1u);
     uint64_t src[K], dst[R];
     tile_bases<K, R, SPLIT>(src, dst, a, cur);
     u32x4 x[U][K];
     load_stripe_tile<K, U>(x, src, cur.valid, lane);
-    uint32_t tn = wave + nw;
-    TileRec nxt = load_rec(tiles, tn < n ? tn : wave);
-    for (; tn < n; tn += nw) {
+    uint32_t tn = t + nw;
+    TileRec nxt = load_rec(tiles, tn < n ? tn : n - 1u);
+    for (uint32_t b0 = wave0 + nw; b0 < n; b0 += nw) {  // block-uniform trip count
+        tn = b0 + dw;
         u32x4 y[U][K];
         uint64_t nsrc[K], ndst[R];
         tile_bases<K, R, SPLIT>(nsrc, ndst, a, nxt);
@@ -120,8 +138,10 @@ __global__ __launch_bounds__(kBlockThreads, 1) void gf_apply_stripes(StripeArgs 
         // record two tiles ahead, issued after the data loads: scalar loads
         // return out of order, so waiting for `nxt` is an lgkmcnt(0)
         const uint32_t t2 = tn + nw;
-        const TileRec after = load_rec(tiles, t2 < n ? t2 : tn);
-        store_stripe_tile<K, R, U, ACC>(x, a, tb, dst, cur.valid, lane);
+        const TileRec after = load_rec(tiles, t2 < n ? t2 : n - 1u);
+        if (HBEC_STRIPES_SLEEP > 0) __builtin_amdgcn_s_sleep(HBEC_STRIPES_SLEEP);
+        if (HBEC_STRIPES_BARRIER) __builtin_amdgcn_s_barrier();
+        store_stripe_tile<K, R, U, ACC>(x, a, tb, dst, cur.valid, t < n ? cur.valid : 0u, lane);
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -130,8 +150,9 @@ __global__ __launch_bounds__(kBlockThreads, 1) void gf_apply_stripes(StripeArgs 
         for (int r = 0; r < R; ++r) dst[r] = ndst[r];
         cur = nxt;
         nxt = after;
+        t = tn;
     }
-    store_stripe_tile<K, R, U, ACC>(x, a, tb, dst, cur.valid, lane);
+    store_stripe_tile<K, R, U, ACC>(x, a, tb, dst, cur.valid, t < n ? cur.valid : 0u, lane);
 }
 
 template <int K, bool SPLIT, bool ACC>

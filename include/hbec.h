@@ -109,8 +109,9 @@ int hbec_verify_databuf(hbec_codec* codec, const uint8_t* databuf, size_t shard_
  * every queued call of the same (device, codec, op, erasure pattern) with
  * one zero-copy launch (up to HBEC_COALESCE_MB, 256 MiB); a lone call runs
  * at once.  Pageable stripes run per call (their staging copies parallel on
- * the callers' threads).  HBEC_COALESCE=0 turns this off.  Counters since
- * load: groups run and calls they carried. */
+ * the callers' threads), at most HBEC_PERCALL_CONCURRENCY (16; 0 = no limit)
+ * at once, the rest waiting in arrival order.  HBEC_COALESCE=0 turns the
+ * grouping off.  Counters since load: groups run and calls they carried. */
 int hbec_coalesce_stats(uint64_t* groups, uint64_t* calls);
 
 /* ---------------------------------------------------------------------------

@@ -28,6 +28,11 @@ VARIANTS = {
     "vf16": ["HBEC_VERIFY_LOADS=16"],
     "vf32": ["HBEC_VERIFY_LOADS=32"],
     "xcd0": ["HBEC_XCD_MAP=0"],
+    # stripes kernel pacing (round 2): barrier per tile on (default) / off, s_sleep
+    "stnb": ["HBEC_STRIPES_BARRIER=0"],
+    "stb_s4": ["HBEC_STRIPES_SLEEP=4"],
+    "stb_s8": ["HBEC_STRIPES_SLEEP=8"],
+    "stnb_s8": ["HBEC_STRIPES_BARRIER=0", "HBEC_STRIPES_SLEEP=8"],
 }
 
 
