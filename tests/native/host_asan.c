@@ -125,6 +125,31 @@ static void* batcher_worker(void* arg) {
     return NULL;
 }
 
+/* per-call databuf entries from many threads: pinned stripes take the
+ * coalescer, pageable ones the per-call concurrency gate */
+struct PercallJob {
+    hbec_codec* c;
+    uint8_t* base;
+    uint64_t s;
+    int k, m, rc;
+};
+
+static void* percall_worker(void* arg) {
+    struct PercallJob* j = (struct PercallJob*)arg;
+    for (int it = 0; it < 4 && !j->rc; ++it) {
+        j->rc = hbec_encode_databuf(j->c, j->base, j->s);
+        if (j->rc) break;
+        uint8_t present[32];
+        for (int i = 0; i < j->k + j->m; ++i) present[i] = i == 0 ? 0 : 1;
+        memset(j->base, 0, j->s);
+        j->rc = hbec_reconstruct_databuf(j->c, j->base, j->s, present, 1);
+        int ok = 0;
+        if (!j->rc) j->rc = hbec_verify_databuf(j->c, j->base, j->s, &ok);
+        if (!j->rc && !ok) j->rc = -100;
+    }
+    return NULL;
+}
+
 /* in-memory io for the ecutils loops */
 struct Mem {
     uint8_t* p;
@@ -271,6 +296,26 @@ static int gpu_part(void) {
         free(jobs[i].st.base);
     }
     hbec_batcher_free(b);
+    /* 7. 24 concurrent per-call callers, half on one pinned pool, half pageable */
+    {
+        enum { NT = 24 };
+        const uint64_t s = 4096;
+        void* pool = NULL;
+        CHECK(hbec_host_alloc((size_t)(NT / 2) * (k + m) * s, &pool) == HBEC_OK, 32);
+        pthread_t pt[NT];
+        struct PercallJob pj[NT];
+        for (int i = 0; i < NT; ++i) {
+            uint8_t* mem = i % 2 == 0 ? (uint8_t*)pool + (size_t)(i / 2) * (k + m) * s : NULL;
+            pj[i] = (struct PercallJob){c, make_stripe(k, m, s, mem), s, k, m, 0};
+            pthread_create(&pt[i], NULL, percall_worker, &pj[i]);
+        }
+        for (int i = 0; i < NT; ++i) {
+            pthread_join(pt[i], NULL);
+            CHECK(pj[i].rc == HBEC_OK, 33);
+            if (i % 2) free(pj[i].base);
+        }
+        hbec_host_free(pool);
+    }
     hbec_free(c);
     rc = ecutils_part();
     if (rc) return rc;
