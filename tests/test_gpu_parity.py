@@ -63,6 +63,29 @@ def test_encode_matches_oracle(k, m, n):
         assert np.array_equal(shards[k + r], want[r]), f"parity {r}"
 
 
+@pytest.mark.parametrize("k,m", [(200, 56), (128, 128), (1, 255), (255, 1)])
+def test_max_shards_encode_and_round_trip(k, m):
+    """k + m = 256, klauspost's limit: parity against the oracle, then m
+    random erasures (every parity shard lost for 255+1, all but one shard for
+    1+255) rebuilt by Reconstruct and ReconstructData."""
+    rng = np.random.default_rng(k * 1000 + m)
+    s = 1040  # 65 16-B elements: a partial last tile everywhere
+    enc = RS.New(k, m)
+    full = [rng.integers(0, 256, s, dtype=np.uint8) for _ in range(k)] + [np.zeros(s, np.uint8)
+                                                                          for _ in range(m)]
+    enc.Encode(full)
+    want = CO.apply(CO.build_matrix(k, m)[k:], full[:k])
+    for r in range(m):
+        assert np.array_equal(full[k + r], want[r]), f"parity {r}"
+    missing = set(rng.choice(k + m, size=m, replace=False).tolist())
+    sh = [x.copy() if i not in missing else None for i, x in enumerate(full)]
+    enc.Reconstruct(sh)
+    assert all(np.array_equal(a, b) for a, b in zip(sh, full))
+    sh = [x.copy() if i not in missing else None for i, x in enumerate(full)]
+    enc.ReconstructData(sh)
+    assert all(np.array_equal(sh[i], full[i]) for i in range(k))
+
+
 @pytest.mark.parametrize("fill", [0x00, 0xFF])
 def test_encode_constant_shards(fill):
     enc = RS.New(4, 2)
