@@ -40,9 +40,15 @@ int fail(int code, const std::string& msg) {
     return code;
 }
 
+// A failed runtime call also leaves its code in the thread's last-error slot,
+// where the next successful launch's hipGetLastError() check would find it
+// and fail a call that did nothing wrong: clear it here.  Out of memory is
+// HBEC_ERR_NOMEM (the caller may retry smaller or fall back), anything else
+// HBEC_ERR_DEVICE.
 int hip_fail(hipError_t e, const char* what) {
+    (void)hipGetLastError();
     std::string m = std::string(what) + ": " + hipGetErrorString(e);
-    return fail(HBEC_ERR_DEVICE, m);
+    return fail(e == hipErrorOutOfMemory ? HBEC_ERR_NOMEM : HBEC_ERR_DEVICE, m);
 }
 
 static std::atomic<int> g_force_stream{0};

@@ -71,8 +71,15 @@ class ErrScheme(ReedSolomonError):
     code = N.ERR_SCHEME
 
 
+class ErrNoMem(ReedSolomonError):
+    """Host or device allocation failed (HBEC_ERR_NOMEM): like ErrDevice, the
+    caller may fall back to its own CPU codec."""
+    code = N.ERR_NOMEM
+
+
 _BY_CODE = {c.code: c for c in (ErrInvShardNum, ErrMaxShardNum, ErrTooFewShards, ErrShardNoData, ErrShardSize,
-                                ErrSingular, ErrDevice, ErrInvalidArg, ErrUnexpectedEOF, ErrIO, ErrScheme)}
+                                ErrSingular, ErrDevice, ErrInvalidArg, ErrUnexpectedEOF, ErrIO, ErrScheme,
+                                ErrNoMem)}
 
 
 def check(rc: int) -> None:

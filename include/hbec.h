@@ -17,7 +17,8 @@
  * thread-safe (cgo calls arrive on arbitrary OS threads).  The library never
  * keeps a caller pointer after a call returns (batch calls: after the work
  * queued on the caller's stream completes).  There is NO CPU fallback inside
- * the library: a GPU failure returns HBEC_ERR_DEVICE and the caller decides.
+ * the library: a GPU failure returns HBEC_ERR_DEVICE (HBEC_ERR_NOMEM when
+ * HBM or pinned host memory runs out) and the caller decides.
  */
 #ifndef HBEC_H
 #define HBEC_H

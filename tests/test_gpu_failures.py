@@ -1,0 +1,91 @@
+"""Failure detection at the boundary (a GPU failure or OOM must
+come back as an error code so the Go shim can fall back to klauspost's CPU
+codec): allocation failures return HBEC_ERR_NOMEM, nothing is half-written,
+and the very next call on the same thread succeeds (a failed HIP call must not
+leave its code in the runtime's last-error slot for the next launch check)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+
+from hummingbird_amd import _native as N
+from hummingbird_amd import batch as B
+from hummingbird_amd import reedsolomon as RS
+from oracle import coracle as CO
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    torch.cuda.set_device(0)
+    yield
+    torch.cuda.empty_cache()
+
+
+def _encode_ok(enc, k, m, s=4096, seed=0):
+    rng = np.random.default_rng(seed)
+    sh = [rng.integers(0, 256, s, dtype=np.uint8) for _ in range(k)] + [np.zeros(s, np.uint8) for _ in range(m)]
+    enc.Encode(sh)
+    want = CO.apply(CO.build_matrix(k, m)[k:], sh[:k])
+    assert all(np.array_equal(sh[k + r], want[r]) for r in range(m))
+
+
+def test_pinned_host_alloc_failure_is_nomem_and_recovers():
+    p = C.c_void_p()
+    # 1 PiB: beyond the 47-bit user address space, so it fails before pinning anything
+    rc = N.lib().hbec_host_alloc(1 << 50, C.byref(p))
+    assert rc in (N.ERR_NOMEM, N.ERR_DEVICE), rc
+    assert p.value is None
+    assert "hipHostMalloc" in N.last_error()
+    assert N.lib().hbec_host_alloc(1 << 20, C.byref(p)) == N.HBEC_OK
+    N.lib().hbec_host_free(p)
+    _encode_ok(RS.New(4, 2), 4, 2, seed=1)
+
+
+def test_device_oom_is_nomem_and_next_call_succeeds():
+    """Verify over unaligned views needs an n*m*S scratch buffer in HBM
+    (hbec.cpp verify_views, generic path).  With HBM nearly full that
+    allocation fails: ErrNoMem, no flag set.  With the memory back, the same
+    call and an aligned pipelined encode both succeed."""
+    k, m, n, s = 4, 2, 512, (1 << 20) + 1  # odd shard length: generic path, 1 GiB scratch
+    enc = RS.New(k, m)
+    objs = torch.empty((n, k * s + 1), dtype=torch.uint8, device="cuda")
+    B.fill_splitmix(objs, k * s + 1)
+    parity = torch.empty((n, m * s + 1), dtype=torch.uint8, device="cuda")
+    views = [(objs.data_ptr() + 1 + j * s, objs.stride(0)) for j in range(k)]
+    views += [(parity.data_ptr() + 1 + r * s, parity.stride(0)) for r in range(m)]
+    B.encode_views(enc, views, n, s)
+    flags = torch.zeros(n, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+
+    free, _ = torch.cuda.mem_get_info()
+    hog = None
+    for slack in (256 << 20, 512 << 20, 1 << 30):  # leave less than the 1 GiB scratch
+        try:
+            hog = torch.empty(free - slack, dtype=torch.uint8, device="cuda")
+            break
+        except RuntimeError:
+            continue
+    assert hog is not None, "could not fill HBM for the test"
+    try:
+        with pytest.raises(RS.ErrNoMem):
+            B.verify_views(enc, views, n, s, flags)
+        torch.cuda.synchronize()
+    finally:
+        del hog
+        torch.cuda.empty_cache()
+    assert int(flags.count_nonzero()) == 0
+
+    B.verify_views(enc, views, n, s, flags)  # the same call, memory back
+    torch.cuda.synchronize()
+    assert int(flags.count_nonzero()) == 0
+    a = torch.empty((64, 4 << 18), dtype=torch.uint8, device="cuda")
+    B.fill_splitmix(a, 4 << 18)
+    p = torch.empty((64, 2 << 18), dtype=torch.uint8, device="cuda")
+    B.encode_objects(enc, a, p, 1 << 18)  # aligned: the pipelined kernel launch check
+    torch.cuda.synchronize()
+    want, _ = CO.encode_batch(k, m, a[:2].cpu().numpy())
+    assert np.array_equal(p[:2].cpu().numpy(), want)
