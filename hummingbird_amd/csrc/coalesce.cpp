@@ -6,13 +6,14 @@
 // nursery concurrency x devices, replicator.go:487,530, plus per-request
 // goroutines).  On the GPU one 1 MiB stripe per call is bound by launch and
 // PCIe latency, so concurrent calls are coalesced here, inside the library,
-// with no deadline and no extra thread: a call that finds fewer than
-// kMaxInFlight groups running leads — it takes every queued call with the
-// same (device, codec, op, erasure pattern) and codes them all with ONE
-// host-path call (hostpath.cpp: pinned ring, or zero-copy for pinned
-// databufs) — while calls that arrive meanwhile queue and form the next
-// group.  A lone caller runs at once through the per-call path, so
-// single-threaded latency is unchanged; throughput grows with concurrency.
+// with no deadline and no extra thread.  Up to HBEC_COALESCE_DIRECT
+// concurrent callers each run at once through the per-call path (their
+// zero-copy launches overlap on the GPU), so latency at low concurrency is
+// unchanged.  Beyond that, a call that finds fewer than max_in_flight()
+// groups running leads — it takes every queued call with the same (device,
+// codec, op, erasure pattern) and codes them all with ONE host-path call
+// (hostpath.cpp: zero-copy for pinned databufs) — while calls that arrive
+// meanwhile queue and form the next group.
 // If a group's batched call fails, each member is retried alone so every
 // caller gets its own result.
 #include <hip/hip_runtime.h>
@@ -64,8 +65,22 @@ int max_in_flight() {
     return v;
 }
 
+// Below this many pinned calls inside the library at once (counting the new
+// one), a call runs alone at once (HBEC_COALESCE_DIRECT, default 16): up to
+// ~16 callers, independent zero-copy launches overlap on the GPU and beat
+// grouping (1 MiB: 35 vs 25-29 GiB/s at 16 callers); from ~64 callers,
+// grouping wins (38-42 vs 35 GiB/s) (profiles/r02_coalesce_direct.jsonl).
+int direct_limit() {
+    static const int v = [] {
+        const char* e = std::getenv("HBEC_COALESCE_DIRECT");
+        return e ? std::max(0, std::atoi(e)) : 16;
+    }();
+    return v;
+}
+
 struct Coalescer {
     std::mutex mu;
+    int inside = 0;  // pinned calls between entry and return
     std::deque<CoReq*> q;
     int leaders = 0;  // calls holding a lead slot: coding a group, or woken to form one
     uint64_t groups = 0, calls = 0;
@@ -141,6 +156,29 @@ int coalesced_call(hbec_codec* codec, int op, uint8_t* base, uint64_t s, const u
     if (!pinned) return op == 0 ? fn.encode(codec, base, s) : fn.reconstruct(codec, base, s, present, data_only);
     const uint64_t cap = group_cap_bytes();
     std::unique_lock<std::mutex> lk(g_co.mu);
+    if (++g_co.inside <= direct_limit()) {  // few callers: run alone, now (a group of one)
+        ++g_co.groups;
+        ++g_co.calls;
+        lk.unlock();
+        int rc = HBEC_OK;
+        try {
+            rc = op == 0 ? fn.encode(codec, base, s) : fn.reconstruct(codec, base, s, present, data_only);
+        } catch (...) {
+            lk.lock();
+            --g_co.inside;
+            throw;  // guarded() at the entry point maps it
+        }
+        lk.lock();
+        --g_co.inside;
+        return rc;
+    }
+    struct Leave {  // leaves the count on every way out of the queued path
+        std::unique_lock<std::mutex>& lk;
+        ~Leave() {
+            if (!lk.owns_lock()) lk.lock();
+            --g_co.inside;
+        }
+    } leave{lk};
     g_co.q.push_back(&r);
     // Every wake-up is addressed: a finished group wakes its own members, and
     // hands its lead slot to the oldest queued call.  (One shared condition
@@ -201,7 +239,6 @@ int coalesced_call(hbec_codec* codec, int op, uint8_t* base, uint64_t s, const u
         }
         if (r.done) break;
     }
-    lk.unlock();
     return r.rc ? fail(r.rc, r.err) : HBEC_OK;
 }
 

@@ -105,7 +105,9 @@ int hbec_verify_databuf(hbec_codec* codec, const uint8_t* databuf, size_t shard_
 /* Concurrent per-call Encode / Reconstruct / ReconstructData on databuf
  * stripes (the *_databuf entries, and hbec_encode / hbec_reconstruct when
  * the shard pointers are one buffer's consecutive slots) in pinned,
- * device-mapped memory (hbec_host_alloc) are coalesced: a call that finds
+ * device-mapped memory (hbec_host_alloc) are coalesced: while at most
+ * HBEC_COALESCE_DIRECT (16) such calls are inside the library each runs alone;
+ * beyond that, a call that finds
  * fewer than HBEC_COALESCE_INFLIGHT (2) groups in flight codes itself plus
  * every queued call of the same (device, codec, op, erasure pattern) with
  * one zero-copy launch (up to HBEC_COALESCE_MB, 256 MiB); a lone call runs
