@@ -71,6 +71,8 @@ for s in "$@"; do
       gcc -O2 -std=c11 -Iinclude scripts/bench_ecutils.c -Lhummingbird_amd -lhbec -Wl,-rpath,$ROOT/hummingbird_amd -o $OUT/bench_ecutils && step ecloops 300 sh -c "$OUT/bench_ecutils 4 2 256 && $OUT/bench_ecutils 8 3 256" ;;
     batcher)
       gcc -O2 -std=c11 -pthread -Iinclude scripts/bench_batcher.c -Lhummingbird_amd -lhbec -Wl,-rpath,$ROOT/hummingbird_amd -o $OUT/bench_batcher && step batcher 300 sh -c "for w in 1 2 3; do HBEC_BATCHER_WORKERS=\$w $OUT/bench_batcher 64 32 1 96 300 && HBEC_BATCHER_WORKERS=\$w $OUT/bench_batcher 64 32 0 96 300 && HBEC_BATCHER_WORKERS=\$w $OUT/bench_batcher 16 128 1 96 300 || exit 1; done" ;;
+    soak)
+      gcc -O2 -std=c11 -pthread -Iinclude scripts/soak.c -Lhummingbird_amd -lhbec -Wl,-rpath,$ROOT/hummingbird_amd -o $OUT/soak && step soak 400 sh -c "$OUT/soak 8 20 && $OUT/soak 48 60 && $OUT/soak 128 40" ;;
     md5tests) step md5tests 600 python -m pytest tests/test_gpu_md5.py -q -x -p no:cacheprovider ;;
     md5) step md5 600 python scripts/bench_md5.py ;;
     md5sweep) step md5sweep 900 bash scripts/md5_sweep.sh ;;

@@ -1,0 +1,209 @@
+/* Concurrency soak of every host-facing entry point at once (the way a busy
+ * object server reaches the library: Stabilize, degraded GETs, repairs and
+ * the auditor on arbitrary OS threads).  T threads run for SECONDS, each
+ * cycling over its own stripes and picking an operation per iteration:
+ *
+ *   0  hbec_encode_databuf (pinned: coalescer; pageable: per-call gate)
+ *   1  hbec_reconstruct_databuf of 1-2 erased shards, data-only or full
+ *   2  hbec_batcher_encode
+ *   3  hbec_batcher_encode_md5 (digest of shard 0 checked against a CPU MD5
+ *      of the same bytes is left to the tests; here: call succeeds)
+ *   4  hbec_batcher_reconstruct
+ *   5  hbec_encode_host of a small batch of the thread's stripes
+ *   6  hbec_verify_databuf
+ *
+ * After every write operation the stripe is verified (hbec_verify_databuf)
+ * and every rebuilt shard compared with a saved copy, so a wrong byte, a
+ * lost wake-up (hang: the run is under `timeout`) or a crash ends the run.
+ * Sizes mix 4 KiB and 1 MiB objects, 4+2.  Prints one JSON line.
+ *
+ *   gcc -O2 -std=c11 -pthread -Iinclude scripts/soak.c -Lhummingbird_amd -lhbec \
+ *       -Wl,-rpath,$PWD/hummingbird_amd -o gpurun_out/soak
+ *   timeout -k 10 180 gpurun_out/soak THREADS SECONDS */
+#define _POSIX_C_SOURCE 199309L
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "hbec.h"
+
+enum { K = 4, M = 2, N = K + M, PER = 6 };
+
+static hbec_codec* g_codec;
+static hbec_batcher* g_bat;
+static double g_stop;
+
+typedef struct {
+    int id, pinned;
+    uint8_t* base[PER];
+    uint8_t* keep[PER];
+    size_t s[PER];
+    uint64_t ops[7], rng;
+    int rc, where;
+} Job;
+
+static double now(void) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec + t.tv_nsec * 1e-9;
+}
+
+static uint64_t next(uint64_t* x) {
+    uint64_t z = (*x += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+static int check(Job* j, int i) {
+    int ok = 0;
+    if (hbec_verify_databuf(g_codec, j->base[i], j->s[i], &ok) || !ok) return -1001;
+    if (memcmp(j->base[i], j->keep[i], N * j->s[i])) return -1002;
+    return 0;
+}
+
+static void* run(void* arg) {
+    Job* j = (Job*)arg;
+    while (now() < g_stop && !j->rc) {
+        const int i = (int)(next(&j->rng) % PER), op = (int)(next(&j->rng) % 7);
+        uint8_t* b = j->base[i];
+        const size_t s = j->s[i];
+        int rc = 0;
+        switch (op) {
+            case 0:
+                memset(b + K * s, 0x33, M * s);
+                rc = hbec_encode_databuf(g_codec, b, s);
+                break;
+            case 1: {
+                uint8_t present[N];
+                for (int t = 0; t < N; ++t) present[t] = 1;
+                const int e0 = (int)(next(&j->rng) % N), e1 = (int)(next(&j->rng) % N);
+                present[e0] = present[e1] = 0;
+                const int data_only = (int)(next(&j->rng) & 1);
+                for (int t = 0; t < N; ++t)
+                    if (!present[t] && (t < K || !data_only)) memset(b + t * s, 0x77, s);
+                rc = hbec_reconstruct_databuf(g_codec, b, s, present, data_only);
+                if (!rc && data_only)  /* parity shards stay as they were erased: restore them */
+                    for (int t = K; t < N; ++t)
+                        if (!present[t]) memcpy(b + t * s, j->keep[i] + t * s, s);
+                break;
+            }
+            case 2: {
+                hbec_stripe st = {b, s};
+                memset(b + K * s, 0x55, M * s);
+                rc = hbec_batcher_encode(g_bat, &st);
+                break;
+            }
+            case 3: {
+                hbec_stripe st = {b, s};
+                uint8_t dig[N * 16];
+                if (s <= (1u << 20)) rc = hbec_batcher_encode_md5(g_bat, &st, dig);
+                break;
+            }
+            case 4: {
+                hbec_stripe st = {b, s};
+                uint8_t present[N] = {1, 0, 1, 1, 0, 1};
+                memset(b + 1 * s, 0x99, s);
+                memset(b + 4 * s, 0x99, s);
+                rc = hbec_batcher_reconstruct(g_bat, &st, present, 0);
+                break;
+            }
+            case 5: {
+                hbec_stripe st[PER];
+                for (int t = 0; t < PER; ++t) {
+                    st[t] = (hbec_stripe){j->base[t], j->s[t]};
+                    memset(j->base[t] + K * j->s[t], 0x11, M * j->s[t]);
+                }
+                rc = hbec_encode_host(g_codec, st, PER);
+                for (int t = 0; t < PER && !rc; ++t) rc = check(j, t);
+                break;
+            }
+            case 6: {
+                int ok = 0;
+                rc = hbec_verify_databuf(g_codec, b, s, &ok);
+                if (!rc && !ok) rc = -1003;
+                break;
+            }
+        }
+        if (!rc && op != 5 && op != 6) rc = check(j, i);
+        if (rc) {
+            j->rc = rc;
+            j->where = op;
+        }
+        ++j->ops[op];
+    }
+    return NULL;
+}
+
+int main(int argc, char** argv) {
+    const int threads = argc > 1 ? atoi(argv[1]) : 32;
+    const double secs = argc > 2 ? atof(argv[2]) : 60.0;
+    if (threads < 1 || threads > 256) return 2;
+    if (hbec_new(K, M, &g_codec) || hbec_batcher_new(g_codec, 64u << 20, 200, &g_bat)) {
+        fprintf(stderr, "%s\n", hbec_last_error());
+        return 1;
+    }
+    Job* jobs = calloc(threads, sizeof(Job));
+    pthread_t* th = malloc(sizeof(pthread_t) * threads);
+    uint64_t seed = 0x48424543ull;
+    for (int t = 0; t < threads; ++t) {
+        Job* j = &jobs[t];
+        j->id = t;
+        j->pinned = t % 2 == 0;
+        j->rng = seed + (uint64_t)t * 7919u;
+        for (int i = 0; i < PER; ++i) {
+            j->s[i] = (i % 3 == 0) ? (1u << 18) : 1024u;  /* 1 MiB or 4 KiB objects */
+            const size_t bytes = N * j->s[i];
+            if (j->pinned) {
+                if (hbec_host_alloc(bytes, (void**)&j->base[i])) {
+                    fprintf(stderr, "%s\n", hbec_last_error());
+                    return 1;
+                }
+            } else {
+                j->base[i] = malloc(bytes);
+            }
+            j->keep[i] = malloc(bytes);
+            for (size_t o = 0; o < K * j->s[i]; o += 8) {
+                const uint64_t z = next(&seed);
+                memcpy(j->base[i] + o, &z, 8);
+            }
+            if (hbec_encode_databuf(g_codec, j->base[i], j->s[i])) {
+                fprintf(stderr, "%s\n", hbec_last_error());
+                return 1;
+            }
+            memcpy(j->keep[i], j->base[i], bytes);
+        }
+    }
+    const double t0 = now();
+    g_stop = t0 + secs;
+    for (int t = 0; t < threads; ++t) pthread_create(&th[t], NULL, run, &jobs[t]);
+    int rc = 0, where = -1, who = -1;
+    uint64_t ops[7] = {0}, total = 0;
+    for (int t = 0; t < threads; ++t) {
+        pthread_join(th[t], NULL);
+        if (jobs[t].rc && !rc) {
+            rc = jobs[t].rc;
+            where = jobs[t].where;
+            who = t;
+        }
+        for (int o = 0; o < 7; ++o) ops[o] += jobs[t].ops[o];
+    }
+    for (int o = 0; o < 7; ++o) total += ops[o];
+    uint64_t groups = 0, calls = 0, batches = 0, stripes = 0;
+    hbec_coalesce_stats(&groups, &calls);
+    hbec_batcher_stats(g_bat, &batches, &stripes);
+    hbec_batcher_free(g_bat);
+    printf("{\"measure\": \"soak\", \"threads\": %d, \"seconds\": %.1f, \"ops\": %llu, \"per_op\": [%llu, %llu, %llu, "
+           "%llu, %llu, %llu, %llu], \"coalesce_groups\": %llu, \"coalesce_calls\": %llu, \"batches\": %llu, "
+           "\"batched_stripes\": %llu, \"rc\": %d, \"failed_op\": %d, \"failed_thread\": %d}\n",
+           threads, now() - t0, (unsigned long long)total, (unsigned long long)ops[0], (unsigned long long)ops[1],
+           (unsigned long long)ops[2], (unsigned long long)ops[3], (unsigned long long)ops[4],
+           (unsigned long long)ops[5], (unsigned long long)ops[6], (unsigned long long)groups,
+           (unsigned long long)calls, (unsigned long long)batches, (unsigned long long)stripes, rc, where, who);
+    if (rc) fprintf(stderr, "soak failed: thread %d op %d rc %d: %s\n", who, where, rc, hbec_last_error());
+    hbec_free(g_codec);
+    return rc ? 1 : 0;
+}
