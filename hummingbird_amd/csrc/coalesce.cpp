@@ -45,6 +45,7 @@ struct CoReq {
     int rc = HBEC_OK;
     std::string err;
     bool taken = false, done = false, lead = false;
+    CoReq* next = nullptr;       // group membership as an intrusive list: forming a group allocates nothing
     std::condition_variable cv;  // this caller's own wake-up: done, or asked to lead
 
     bool same_group(const CoReq& o) const {
@@ -97,28 +98,43 @@ uint64_t group_cap_bytes() {
     return cap;
 }
 
-// Code one group.  Direct per-call path for a group of one; else one batched
-// host-path call, falling back to per-member calls if that fails.
-void run_group(std::vector<CoReq*>& g, const DirectFns& fn) {
+// Code one group (list from `head`, n members).  Direct per-call path for a
+// group of one; else one batched host-path call, falling back to per-member
+// calls if that fails.
+void run_group(CoReq* head, size_t n, const DirectFns& fn) {
     auto single = [&](CoReq* r) {
         r->rc = r->op == 0 ? fn.encode(r->codec, r->base, r->s)
                            : fn.reconstruct(r->codec, r->base, r->s, r->present.data(), r->data_only);
         r->err = r->rc ? hbec_last_error() : "";
     };
-    if (g.size() == 1) {
-        single(g[0]);
+    if (n == 1) {
+        single(head);
         return;
     }
-    std::vector<hbec_stripe> st(g.size());
-    for (size_t i = 0; i < g.size(); ++i) st[i] = hbec_stripe{g[i]->base, g[i]->s};
-    const CoReq& h = *g[0];
+    std::vector<hbec_stripe> st;
+    st.reserve(n);
+    for (CoReq* x = head; x; x = x->next) st.push_back(hbec_stripe{x->base, x->s});
+    const CoReq& h = *head;
     const int rc = h.op == 0 ? hbec_encode_host(h.codec, st.data(), st.size())
                              : hbec_reconstruct_host(h.codec, st.data(), st.size(), h.present.data(), h.data_only);
-    if (rc == HBEC_OK) {
-        for (auto* r : g) r->rc = HBEC_OK;
-        return;
+    for (CoReq* x = head; x; x = x->next) {
+        if (rc == HBEC_OK)
+            x->rc = HBEC_OK;
+        else
+            single(x);
     }
-    for (auto* r : g) single(r);
+}
+
+// A whole group failed by exception: every member gets the code (the message
+// is best effort — assigning it may itself fail to allocate).
+void fail_group(CoReq* head, int code, const char* msg) noexcept {
+    for (CoReq* x = head; x; x = x->next) {
+        x->rc = code;
+        try {
+            x->err = msg;
+        } catch (...) {
+        }
+    }
 }
 
 }  // namespace
@@ -204,35 +220,43 @@ int coalesced_call(hbec_codec* codec, int op, uint8_t* base, uint64_t s, const u
             if (r.taken) {  // another leader's group took this call first
                 pass_slot();
             } else {
-                // lead: this call plus every queued call of the same group, up to cap bytes
-                std::vector<CoReq*> grp;
+                // lead: this call plus every queued call of the same group, up
+                // to cap bytes (nothing below allocates while members are marked)
+                CoReq* head = nullptr;
+                CoReq** tail = &head;
+                size_t members = 0;
                 uint64_t bytes = 0;
                 for (CoReq* x : g_co.q) {
                     if (!(x == &r || x->same_group(r))) continue;
                     const uint64_t b = x->s * (uint64_t)n_shards;
                     if (x != &r && bytes + b > cap) continue;
                     x->taken = true;
-                    grp.push_back(x);
+                    x->next = nullptr;
+                    *tail = x;
+                    tail = &x->next;
+                    ++members;
                     bytes += b;
                 }
                 g_co.q.erase(std::remove_if(g_co.q.begin(), g_co.q.end(), [](CoReq* x) { return x->taken; }),
                              g_co.q.end());
                 ++g_co.groups;
-                g_co.calls += grp.size();
+                g_co.calls += members;
                 lk.unlock();
                 // no exception may leave the group half-done: the other
                 // members would wait forever
                 try {
-                    run_group(grp, fn);
+                    run_group(head, members, fn);
                 } catch (const std::bad_alloc&) {
-                    for (auto* x : grp) x->rc = HBEC_ERR_NOMEM, x->err = "coalesced call: host allocation failed";
+                    fail_group(head, HBEC_ERR_NOMEM, "coalesced call: host allocation failed");
                 } catch (...) {
-                    for (auto* x : grp) x->rc = HBEC_ERR_DEVICE, x->err = "coalesced call: unexpected exception";
+                    fail_group(head, HBEC_ERR_DEVICE, "coalesced call: unexpected exception");
                 }
                 lk.lock();
-                for (auto* x : grp) {
+                for (CoReq* x = head; x;) {
+                    CoReq* nx = x->next;  // read before `done`: a woken member may return at once
                     x->done = true;
                     if (x != &r) x->cv.notify_one();
+                    x = nx;
                 }
                 pass_slot();
             }
