@@ -163,6 +163,14 @@ struct hbec_batcher {
             // request), gathered from the WHOLE queue: a request of another
             // kind between them does not split the batch
             std::vector<Request*> batch;
+            try {  // reserved up front: nothing below may throw once requests leave the queue
+                batch.reserve(queue.size());
+            } catch (...) {
+                lk.unlock();
+                std::this_thread::sleep_for(std::chrono::microseconds(100));  // requests stay queued; retry
+                lk.lock();
+                continue;
+            }
             uint64_t bytes = 0;
             for (auto it = queue.begin(); it != queue.end();) {
                 Request* r = *it;
@@ -190,8 +198,11 @@ struct hbec_batcher {
             if (thrown != HBEC_OK)
                 for (auto* r : batch) {
                     r->rc = thrown;
-                    r->err = thrown == HBEC_ERR_NOMEM ? "batcher: host allocation failed"
-                                                      : "batcher: unexpected exception";
+                    try {  // the message is best effort
+                        r->err = thrown == HBEC_ERR_NOMEM ? "batcher: host allocation failed"
+                                                          : "batcher: unexpected exception";
+                    } catch (...) {
+                    }
                 }
             for (auto* r : batch) {
                 // notify while holding r->m: the caller cannot see `done`, return and
