@@ -26,7 +26,9 @@ sources being run -- same sha256 -- else null), `cpu_baseline`
 (oracle/gf_oracle.c's AVX2 port of klauspost's algorithm over the host cores
 on a bounded sample, rank 0 at N=1) and `config5` (BASELINE configs[4]: a
 65 536 x 1 MiB 4+2 batch partitioned contiguously over the N ranks, encoded
-device-resident, at every N including 1).
+device-resident, at every N including 1) and `small_objects` (the reference
+README's 4 KB shape: 65 536 x 4 KiB objects, 8+3 and 4+2, Encode /
+Reconstruct / Verify, rank 0).
 
 `--gpus N` without a launcher (WORLD_SIZE unset) starts N rank processes
 itself through torch.distributed.run, before this process touches the GPU;
@@ -330,6 +332,58 @@ def config5(pg, k, m, obj_len, n_global, world, rank, ctl_device, reps=3):
     }
 
 
+def small_objects(n=65536, obj_len=4096, reps=20):
+    """The reference README's 4 KB shape (/root/reference/README.md:19-27)
+    device-resident: n x 4 KiB objects, 8+3 (512-B shards) and 4+2 (1 KiB),
+    Encode, Reconstruct of the first m data shards and Verify, each timed over
+    `reps` back-to-back launches with HIP events on the launch stream.
+    Algorithmic bytes per object: (k+m)*S for Encode and Verify, (k+e)*S for
+    Reconstruct.  Rebuilt shards are compared with the
+    originals and Verify must pass every object."""
+    out = {"workload": f"{n} x {obj_len} B objects, device-resident (README 4 KB shape)", "shapes": []}
+    stream = torch.cuda.current_stream()
+    for k, m in ((8, 3), (4, 2)):
+        s = obj_len // k
+        miss = list(range(m))
+        enc = RS.New(k, m)
+        objs = torch.empty((n, obj_len), dtype=torch.uint8, device="cuda")
+        B.fill_splitmix(objs, obj_len, first=1 << 20)
+        par = torch.empty((n, m * s), dtype=torch.uint8, device="cuda")
+        rebuilt = torch.empty((n, m * s), dtype=torch.uint8, device="cuda")
+        flags = torch.zeros(n, dtype=torch.int32, device="cuda")
+        views = B.shard_views(objs, k, s) + B.shard_views(par, m, s)
+        rv = list(views)
+        for slot, i in enumerate(miss):
+            rv[i] = (rebuilt.data_ptr() + slot * s, rebuilt.stride(0))
+        present = [0 if i in miss else 1 for i in range(k + m)]
+        ops = {
+            "encode": (lambda: B.encode_views(enc, views, n, s), n * (k + m) * s),
+            "reconstruct": (lambda: B.reconstruct_views(enc, rv, present, n, s), n * (k + m) * s),
+            "verify": (lambda: B.verify_views(enc, views, n, s, flags), n * (k + m) * s),
+        }
+        row = {"k": k, "m": m, "shard_bytes": s, "kernel_kind": B.kernel_info(k, m, s)["kind"]}
+        for name, (fn, nbytes) in ops.items():
+            for _ in range(3):  # warm-up: clocks up before the events
+                fn()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(reps):
+                fn()
+            e1.record(stream)
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / reps
+            gbs = nbytes / (ms * 1e-3) / 1e9
+            row[name] = {"ms": round(ms, 5), "GB_s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
+        ok = int(flags.count_nonzero()) == 0
+        for slot, i in enumerate(miss):
+            ok = ok and torch.equal(rebuilt[:, slot * s:(slot + 1) * s], objs[:, i * s:(i + 1) * s])
+        row["parity_ok"] = bool(ok)
+        out["shapes"].append(row)
+        del objs, par, rebuilt, flags
+    torch.cuda.empty_cache()
+    return out
+
+
 def host_path(k, m, obj_len, n_obj=2048, passes=5, all_devices=False):
     """The path as the object server runs it: stripes (ecSplit databuf layout,
     ecutils.go:31-35) in pinned host memory from hbec_host_alloc, coded in
@@ -397,6 +451,7 @@ def parse_args(argv):
     ap.add_argument("--objects", type=int, default=4096, help="objects per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--no-small", action="store_true", help="skip the README 4 KB shape leg (small_objects)")
     ap.add_argument("--no-host-path", action="store_true",
                     help="skip the PCIe-inclusive host-path line (pinned stripes, zero-copy)")
     ap.add_argument("--config5-objects", type=int, default=65536,
@@ -563,6 +618,11 @@ def main(argv=None):
         if rank == 0:
             line["config5"] = c5
             ok = ok and c5.get("parity_ok", True)  # a skipped leg reports why, not a failure
+    if rank == 0 and not args.no_small:
+        try:
+            line["small_objects"] = small_objects()
+        except Exception as e:  # noqa: BLE001 - reported; never blocks the other ranks
+            line["small_objects"] = {"error": f"{type(e).__name__}: {e}"[:200]}
     if world > 1 and backend == "nccl" and args.split_objects > 0:
         split = batch_split(pg, k, m, obj_len, args.split_objects, world, rank, ctl_device)
         if rank == 0:
