@@ -116,7 +116,9 @@ def test_split_failing_writer_dropped_midway():
 
 
 @pytest.mark.parametrize("k,m,chunk,length,erased", [(4, 2, 1024, 50_000, (0, 5)), (8, 3, 4096, 400_000, (1, 2, 9)),
-                                                     (4, 2, 1000, 9_999, (3,)), (3, 2, 100, 7, (0, 1))])
+                                                     (4, 2, 1000, 9_999, (3,)), (3, 2, 100, 7, (0, 1)),
+                                                     (10, 4, 1003, 51_234, (0, 9, 11, 13)),
+                                                     (17, 3, 2048, 200_000, (0, 16, 19))])
 def test_reconstruct_many_stripes(k, m, chunk, length, erased):
     body = bytes(O.object_bytes(k + 100 * m, length))
     files = O.ec_split(k, m, body, chunk)
@@ -158,7 +160,9 @@ def test_reconstruct_body_failure_is_per_stripe():
 
 
 @pytest.mark.parametrize("k,m,chunk,length,lost", [(4, 2, 1024, 70_000, ()), (4, 2, 1024, 70_000, (1, 4)),
-                                                   (8, 3, 4096, 333_333, (0, 7, 8)), (3, 2, 10, 7, (2,))])
+                                                   (8, 3, 4096, 333_333, (0, 7, 8)), (3, 2, 10, 7, (2,)),
+                                                   (10, 4, 1003, 51_234, (2, 5, 10, 12)),
+                                                   (17, 3, 2048, 200_000, (0, 8, 16))])
 def test_glue_many_stripes(k, m, chunk, length, lost):
     body = bytes(O.object_bytes(k * 7 + len(lost), length))
     files = O.ec_split(k, m, body, chunk)
