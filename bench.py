@@ -332,14 +332,18 @@ def config5(pg, k, m, obj_len, n_global, world, rank, ctl_device, reps=3):
     }
 
 
-def small_objects(n=65536, obj_len=4096, reps=20):
+def small_objects(n=65536, obj_len=4096, reps=100, settle=200):
     """The reference README's 4 KB shape (/root/reference/README.md:19-27)
     device-resident: n x 4 KiB objects, 8+3 (512-B shards) and 4+2 (1 KiB),
     Encode, Reconstruct of the first m data shards and Verify, each timed over
     `reps` back-to-back launches with HIP events on the launch stream.
     Algorithmic bytes per object: (k+m)*S for Encode and Verify, (k+e)*S for
     Reconstruct.  Rebuilt shards are compared with the
-    originals and Verify must pass every object."""
+    originals and Verify must pass every object.  `settle` launches run
+    first: over the first ~10 ms of sustained short launches the GPU's clocks
+    dip and recover (8+3 @ 4 KiB: 65 % -> 56 % -> 72 % of 8 TB/s over ~150
+    launches, profiles/r02_small_dvfs_drift.jsonl), and a shorter warm-up
+    times the dip, not the kernel."""
     out = {"workload": f"{n} x {obj_len} B objects, device-resident (README 4 KB shape)", "shapes": []}
     stream = torch.cuda.current_stream()
     for k, m in ((8, 3), (4, 2)):
@@ -362,8 +366,10 @@ def small_objects(n=65536, obj_len=4096, reps=20):
             "verify": (lambda: B.verify_views(enc, views, n, s, flags), n * (k + m) * s),
         }
         row = {"k": k, "m": m, "shard_bytes": s, "kernel_kind": B.kernel_info(k, m, s)["kind"]}
+        for _ in range(settle):
+            ops["encode"][0]()
         for name, (fn, nbytes) in ops.items():
-            for _ in range(3):  # warm-up: clocks up before the events
+            for _ in range(10):
                 fn()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)

@@ -3,7 +3,10 @@
 README.md:19-27): 65 536 x 4 KiB, device-resident, 8+3 (S = 512 B) and 4+2
 (S = 1 KiB), encode and reconstruct.  Two timings per op:
 
-  stream   - 20 launches back to back on one stream (HIP events, average)
+  stream   - 20 launches back to back on one stream (HIP events, average),
+             after 200 settling launches: the clocks dip and recover over the
+             first ~10 ms of sustained short launches (profiles/
+             r02_small_dvfs_drift.jsonl)
   isolated - one launch after a sync and a 1 GiB write that evicts L2 and the
              256 MiB Infinity Cache of the previous launch's lines (median of 9)
 
@@ -84,6 +87,8 @@ def run(k, m, n, size, miss, scrub):
     def reconstruct():
         B.reconstruct_views(enc, rv, present, n, s)
 
+    for _ in range(200):  # settle the clocks (see the module docstring)
+        encode()
     info = B.kernel_info(k, m, s)
     enc_b, rec_b = n * (k + m) * s, n * (k + len(miss)) * s
     emit(f"{k}+{m} encode {n}x{size} stream", enc_b, stream_ms(encode), kernel=info["kind"],
