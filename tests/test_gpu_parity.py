@@ -343,6 +343,39 @@ def test_batch_mixed_sizes_8_3():
         assert torch.equal(objs2, objs)
 
 
+def _apply_cases():
+    rng = np.random.default_rng(20261016)
+    for _ in range(60):
+        yield (int(rng.choice([1, 2, 3, 4, 5, 9])), int(rng.choice([1, 3, 4, 8, 9, 16, 17, 33])),
+               int(rng.choice([16, 48, 512, 1000, 1024, 4112, 65536])), int(rng.choice([1, 37])))
+
+
+@pytest.mark.parametrize("rows,cols,s,n", list(_apply_cases()))
+def test_apply_random_shapes_match_oracle(rows, cols, s, n):
+    """hbec_apply_batch (the general matrix apply under Encode / Reconstruct)
+    over random shapes: every kernel family (packed, pipelined, vec, streaming,
+    bytes for odd lengths, multi-pass accumulate above 16 inputs / 4 outputs)
+    against the oracle, with coefficients 0 and 1 over-represented."""
+    rng = np.random.default_rng(rows * 1000 + cols * 10 + s + n)
+    coeffs = rng.integers(0, 256, (rows, cols), dtype=np.uint8)
+    special = rng.random((rows, cols))
+    coeffs[special < 0.15] = 0
+    coeffs[(special >= 0.15) & (special < 0.3)] = 1
+    pad = 32 if s % 16 == 0 else 0  # strided views: row longer than the shards
+    ins = torch.from_numpy(rng.integers(0, 256, (n, cols * s + pad), dtype=np.uint8)).cuda()
+    outs = torch.full((n, rows * s + pad), 0xA5, dtype=torch.uint8, device="cuda")
+    iv = [(ins.data_ptr() + c * s, ins.stride(0)) for c in range(cols)]
+    ov = [(outs.data_ptr() + r * s, outs.stride(0)) for r in range(rows)]
+    B.apply_views(rows, cols, coeffs.tolist(), iv, ov, n, s)
+    torch.cuda.synchronize()
+    i_np, o_np = ins.cpu().numpy(), outs.cpu().numpy()
+    for o in range(n):
+        want = CO.apply(coeffs, [np.ascontiguousarray(i_np[o, c * s:(c + 1) * s]) for c in range(cols)])
+        for r in range(rows):
+            assert np.array_equal(o_np[o, r * s:(r + 1) * s], want[r]), (o, r)
+    assert (o_np[:, rows * s:] == 0xA5).all()
+
+
 def test_apply_many_inputs_outputs():
     rng = np.random.default_rng(1)
     rows, cols, n, s = 6, 19, 3, 4096
