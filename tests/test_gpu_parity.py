@@ -376,6 +376,50 @@ def test_apply_random_shapes_match_oracle(rows, cols, s, n):
     assert (o_np[:, rows * s:] == 0xA5).all()
 
 
+def _reconstruct_cases():
+    rng = np.random.default_rng(777)
+    for _ in range(40):
+        k = int(rng.choice([1, 2, 3, 4, 5, 8, 10, 12, 17, 32]))
+        m = int(rng.choice([1, 2, 3, 4, 6, 8]))
+        yield k, m, int(rng.choice([16, 512, 1008, 1024, 4096, 65536, 1000, 333])), int(rng.choice([1, 5, 64]))
+
+
+@pytest.mark.parametrize("k,m,s,n", list(_reconstruct_cases()))
+def test_batch_reconstruct_random_erasures(k, m, s, n):
+    """Device-batch Encode then Reconstruct / ReconstructData of a random
+    erasure set (1..m shards, data and parity mixed) over random shapes:
+    rebuilt shards equal the originals; with data_only the erased parity
+    slots are left untouched (klauspost ReconstructData)."""
+    rng = np.random.default_rng(k * 100 + m * 10 + s + n)
+    enc = RS.New(k, m)
+    data = torch.from_numpy(rng.integers(0, 256, (n, k * s), dtype=np.uint8)).cuda()
+    par = torch.empty((n, m * s), dtype=torch.uint8, device="cuda")
+    views = [(data.data_ptr() + j * s, data.stride(0)) for j in range(k)]
+    views += [(par.data_ptr() + r * s, par.stride(0)) for r in range(m)]
+    B.encode_views(enc, views, n, s)
+    torch.cuda.synchronize()
+    want = CO.apply(CO.build_matrix(k, m)[k:], [np.ascontiguousarray(data[0, j * s:(j + 1) * s].cpu().numpy())
+                                                for j in range(k)])
+    assert all(np.array_equal(par[0, r * s:(r + 1) * s].cpu().numpy(), want[r]) for r in range(m))
+    n_lost = int(rng.integers(1, m + 1))
+    lost = sorted(rng.choice(k + m, size=n_lost, replace=False).tolist())
+    for data_only in (False, True):
+        d2, p2 = data.clone(), par.clone()
+        for i in lost:
+            (d2[:, i * s:(i + 1) * s] if i < k else p2[:, (i - k) * s:(i - k + 1) * s]).fill_(0x3C)
+        v2 = [(d2.data_ptr() + j * s, d2.stride(0)) for j in range(k)]
+        v2 += [(p2.data_ptr() + r * s, p2.stride(0)) for r in range(m)]
+        B.reconstruct_views(enc, v2, [0 if i in lost else 1 for i in range(k + m)], n, s, data_only=data_only)
+        torch.cuda.synchronize()
+        assert torch.equal(d2, data), (lost, data_only)
+        if data_only:
+            for i in lost:
+                if i >= k:
+                    assert bool((p2[:, (i - k) * s:(i - k + 1) * s] == 0x3C).all()), i
+        else:
+            assert torch.equal(p2, par), lost
+
+
 def test_apply_many_inputs_outputs():
     rng = np.random.default_rng(1)
     rows, cols, n, s = 6, 19, 3, 4096
