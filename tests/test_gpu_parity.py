@@ -722,6 +722,44 @@ def test_host_path_zero_copy_pinned(k, m, sizes):
     hb.free()
 
 
+def _host_random_cases():
+    rng = np.random.default_rng(4242)
+    for _ in range(10):
+        k = int(rng.choice([2, 3, 4, 6, 8, 10, 12]))
+        m = int(rng.choice([1, 2, 3, 4, 5]))
+        sizes = [int(x) for x in rng.choice([1, 17, 4096, 4096 * 3 + 5, 65536, MiB, MiB + 48, 5 * MiB], size=9)]
+        yield k, m, sizes
+
+
+@pytest.mark.parametrize("k,m,sizes", list(_host_random_cases()))
+def test_host_path_random_mixed(k, m, sizes):
+    """Random shapes through the host path: pinned stripes (zero-copy when
+    aligned) interleaved with pageable ones (staging ring), encoded against
+    the oracle, then a random erasure set rebuilt."""
+    rng = np.random.default_rng(k * 31 + m + len(sizes))
+    enc = RS.New(k, m)
+    half = sizes[: len(sizes) // 2]
+    total = sum((k + m) * O.ec_shard_length(x, k) + 16 for x in half) + 16
+    hb = RS.HostBuffer(total)
+    pinned = _pinned_stripes(hb.array, k, m, half, seed=k + m)
+    pageable = _host_stripes(k, m, sizes[len(sizes) // 2:], seed=7 * k + m)
+    stripes = [x for pair in zip(pinned, pageable) for x in pair] + pageable[len(pinned):]
+    want = _encoded_copy(k, m, stripes)
+    enc.EncodeStripes(stripes)
+    for got, w in zip(stripes, want):
+        assert np.array_equal(got, w)
+    lost = sorted(rng.choice(k + m, size=int(rng.integers(1, m + 1)), replace=False).tolist())
+    for st in stripes:
+        sl = st.size // (k + m)
+        for i in lost:
+            st[i * sl:(i + 1) * sl] = 0x6B
+    enc.ReconstructStripes(stripes, [0 if i in lost else 1 for i in range(k + m)])
+    for got, w in zip(stripes, want):
+        assert np.array_equal(got, w), lost
+    del stripes, pinned
+    hb.free()
+
+
 def test_host_path_zero_copy_foreign_pinned_memory():
     """Pinned memory the library did not allocate (torch pin_memory ->
     hipHostMalloc) is recognised through the runtime's pointer attributes."""
