@@ -17,7 +17,6 @@
 #include <hip/hip_runtime.h>
 
 #include <cerrno>
-#include <climits>
 #include <cstdlib>
 #include <cstring>
 #include <algorithm>
@@ -504,8 +503,8 @@ int hbec_ec_glue(int k, int m, hbec_read_fn read, void* const* bodies, int chunk
     });
 }
 
-int hbec_parse_ec_scheme(const char* scheme, char* algo, size_t algo_cap, int* data_shards, int* parity_shards,
-                         int* chunk_size) {
+int hbec_parse_ec_scheme(const char* scheme, char* algo, size_t algo_cap, int64_t* data_shards,
+                         int64_t* parity_shards, int64_t* chunk_size) {
     return hbec::guarded("hbec_parse_ec_scheme", [&]() -> int {
         if (!scheme) return fail(HBEC_ERR_INVALID_ARG, "scheme is NULL");
         std::vector<std::string> sec;
@@ -520,8 +519,9 @@ int hbec_parse_ec_scheme(const char* scheme, char* algo, size_t algo_cap, int* d
         }
         sec.push_back(cur);
         if (sec.size() != 4) return fail(HBEC_ERR_SCHEME, std::to_string(sec.size()) + " scheme sections");
-        // strconv.Atoi: optional sign then one or more ASCII digits
-        auto atoi_go = [](const std::string& s, int* out) {
+        // strconv.Atoi: optional sign then one or more ASCII digits, into Go's
+        // int (64-bit on the reference's amd64 build), ErrRange beyond it
+        auto atoi_go = [](const std::string& s, int64_t* out) {
             size_t i = 0;
             if (!s.empty() && (s[0] == '+' || s[0] == '-')) i = 1;
             if (i >= s.size()) return false;
@@ -529,11 +529,11 @@ int hbec_parse_ec_scheme(const char* scheme, char* algo, size_t algo_cap, int* d
                 if (s[j] < '0' || s[j] > '9') return false;
             errno = 0;
             long long v = std::strtoll(s.c_str(), nullptr, 10);
-            if (errno == ERANGE || v < INT_MIN || v > INT_MAX) return false;
-            *out = (int)v;
+            if (errno == ERANGE) return false;
+            *out = (int64_t)v;
             return true;
         };
-        int k = 0, m = 0, c = 0;
+        int64_t k = 0, m = 0, c = 0;
         if (!atoi_go(sec[1], &k)) return fail(HBEC_ERR_SCHEME, "Invalid data shard count");
         if (!atoi_go(sec[2], &m)) return fail(HBEC_ERR_SCHEME, "Invalid parity shard count");
         if (!atoi_go(sec[3], &c)) return fail(HBEC_ERR_SCHEME, "Invalid chunk size");

@@ -103,7 +103,7 @@ def ec_glue(data_chunks, parity_chunks, bodies, chunk_size, content_length, *dst
 def parse_ec_scheme(scheme: str):
     """Returns (algo, data_shards, parity_shards, chunk_size); raises ErrScheme."""
     algo = C.create_string_buffer(len(scheme.encode()) + 1)
-    k, m, c = C.c_int(), C.c_int(), C.c_int()
+    k, m, c = C.c_int64(), C.c_int64(), C.c_int64()  # Go int
     check(N.lib().hbec_parse_ec_scheme(scheme.encode(), algo, len(algo), C.byref(k), C.byref(m), C.byref(c)))
     return algo.value.decode(), k.value, m.value, c.value
 

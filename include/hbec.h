@@ -333,8 +333,8 @@ int hbec_ec_glue(int data_shards, int parity_shards, hbec_read_fn read, void* co
                  int64_t content_length, hbec_write_fn write, void* const* dsts, int n_dsts);
 
 /* parseECScheme (ecobj.go:82-98): "reedsolomon/<k>/<m>/<chunk>". */
-int hbec_parse_ec_scheme(const char* scheme, char* algo, size_t algo_cap, int* data_shards, int* parity_shards,
-                         int* chunk_size);
+int hbec_parse_ec_scheme(const char* scheme, char* algo, size_t algo_cap, int64_t* data_shards,
+                         int64_t* parity_shards, int64_t* chunk_size);
 
 /* rangeChunkAlign (ecobj.go:814-824). */
 void hbec_range_chunk_align(int64_t start, int64_t end, int64_t chunk_size, int data_shards, int64_t* out_start,

@@ -404,11 +404,15 @@ def parse_ec_scheme(scheme: str):
 
 
 def _go_atoi(s: str) -> int:
-    # strconv.Atoi: optional sign, decimal digits only, no spaces/underscores
+    # strconv.Atoi: optional sign, decimal digits only, no spaces/underscores;
+    # Go's int is 64-bit on the reference's amd64 build (ErrRange beyond it)
     body = s[1:] if s[:1] in "+-" else s
     if not body or not body.isascii() or not body.isdigit():
         raise ValueError(s)
-    return int(s)
+    v = int(s)
+    if not -(1 << 63) <= v < (1 << 63):
+        raise ValueError(s)
+    return v
 
 
 def range_chunk_align(start: int, end: int, chunk_size: int, data_shards: int):

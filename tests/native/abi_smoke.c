@@ -70,7 +70,7 @@ int main(int argc, char** argv) {
     if (hbec_new(200, 57, &c) != HBEC_ERR_MAX_SHARD_NUM) return 8;
     if (hbec_ec_shard_length(1001, 4) != 251 || hbec_ec_shard_length(-5, 4) != 0) return 9;
     char algo[32];
-    int k, p, chunk;
+    int64_t k, p, chunk;
     if (hbec_parse_ec_scheme("reedsolomon/4/2/1048576", algo, sizeof algo, &k, &p, &chunk) != HBEC_OK) return 10;
     if (strcmp(algo, "reedsolomon") || k != 4 || p != 2 || chunk != 1048576) return 11;
     if (hbec_parse_ec_scheme("1/2/16", algo, sizeof algo, &k, &p, &chunk) != HBEC_ERR_SCHEME) return 12;
