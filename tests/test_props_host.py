@@ -86,3 +86,22 @@ def test_decode_rows_match_lagrange(case):
 def test_coding_matrix_matches_lagrange(k, m):
     got = RS.New(k, m).matrix()
     assert [list(map(int, r)) for r in got] == L.coding_matrix(k, m)
+
+
+@settings(max_examples=60, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(k=st.integers(1, 10), m=st.integers(1, 4), chunk=st.integers(1, 300), length=st.integers(0, 3000),
+       data=st.data())
+def test_oracle_stripe_loops_round_trip(k, m, chunk, length, data):
+    """The oracle's ecSplit / ecGlue / ecReconstruct restatements are
+    consistent with each other: any <= m lost shard files still glue to the
+    object, and rebuilt shard files equal the split's (ecutils.go:26-186)."""
+    body = bytes(O.object_bytes(k * 131 + m * 7 + chunk, length))
+    files = O.ec_split(k, m, body, chunk)
+    assert all(len(f) == O.ec_shard_length(length, k) for f in files) or length == 0
+    lost = data.draw(st.lists(st.integers(0, k + m - 1), max_size=m, unique=True))
+    kept = [None if i in lost else f for i, f in enumerate(files)]
+    if length:
+        assert O.ec_glue(k, m, kept, chunk, length) == body
+        if lost:
+            rebuilt = O.ec_reconstruct(k, m, kept, chunk, length, lost)
+            assert [bytes(x) for x in rebuilt] == [bytes(files[i]) for i in lost]
