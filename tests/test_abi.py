@@ -278,3 +278,17 @@ def test_all_missing_stripe_is_shard_no_data_without_device():
         enc.EncodeDatabuf(buf, 17)                    # buffer shorter than (k+m)*S
     ok = C.c_int(9)
     assert N.lib().hbec_verify_databuf(enc.handle, None, 16, C.byref(ok)) == N.ERR_INVALID_ARG
+
+
+def test_verify_validation_before_device():
+    """Encoder.Verify's argument checks (klauspost: shard count, then
+    checkShards without nil) answer without a GPU."""
+    enc = RS.New(4, 2)
+    with pytest.raises(RS.ErrTooFewShards):
+        enc.Verify([np.ones(8, np.uint8)] * 5)
+    with pytest.raises(RS.ErrShardSize):
+        enc.Verify([np.ones(8, np.uint8)] * 5 + [np.ones(9, np.uint8)])
+    with pytest.raises(RS.ErrShardSize):
+        enc.Verify([np.ones(8, np.uint8)] * 5 + [np.zeros(0, np.uint8)])  # a missing shard is not allowed
+    with pytest.raises(RS.ErrShardNoData):
+        enc.Verify([np.zeros(0, np.uint8)] * 6)
