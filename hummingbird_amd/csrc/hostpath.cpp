@@ -169,7 +169,11 @@ int ring_md5_init(Ring& r) {
     if (r.arena[0]) return HBEC_OK;
     const size_t cap = env_size("HBEC_HASH_ARENA_MB", 1024) << 20;
     r.arena_cap = std::max(cap, r.in_cap + r.out_cap);
-    r.arena_rec_cap = r.arena_cap / 16 + 1024;  // >= one record per 16-B shard
+    // MD5 records per arena (32 B pinned each; HBEC_HASH_ARENA_RECS, default
+    // 256 K = 8 MiB): an arena is hashed early when its records run out, so
+    // this bounds pinned memory, not batch size (one record per 16-B shard
+    // would pin 2 GiB per arena)
+    r.arena_rec_cap = std::min<size_t>(r.arena_cap / 16 + 1024, env_size("HBEC_HASH_ARENA_RECS", 1u << 18));
     hipError_t e = hipStreamCreateWithFlags(&r.s_md5, hipStreamNonBlocking);
     for (int a = 0; a < Ring::kArenas && e == hipSuccess; ++a) {
         e = hipMalloc(&r.arena[a], r.arena_cap);
@@ -183,8 +187,26 @@ int ring_md5_init(Ring& r) {
     return HBEC_OK;
 }
 
+// Rings per device are bounded (HBEC_HOST_RINGS, default 8): each staged
+// ring pins 384 MiB of host memory and runs a copy pool of host_threads()
+// threads, so one ring per concurrent caller (a busy object server has
+// hundreds) would pin tens of GiB and spawn thousands of threads; the first
+// 64-thread soak spent minutes creating them.  Callers beyond the bound wait,
+// in arrival order, for a ring to come back.  No caller holds a ring while
+// waiting for another, so the bound cannot deadlock.
 std::mutex g_rings_mu;
+std::condition_variable g_rings_cv;
 std::vector<Ring*> g_free_rings;
+std::map<int, int> g_rings_made;  // per device
+
+int ring_limit() {
+    static const int v = [] {
+        const char* e = std::getenv("HBEC_HOST_RINGS");
+        const int x = e ? std::atoi(e) : 0;
+        return x > 0 ? x : 8;
+    }();
+    return v;
+}
 
 // Pooled non-blocking streams per device for short per-call work (creating
 // and destroying a stream per call costs more than a small batch's copies).
@@ -221,24 +243,39 @@ int ring_acquire(Ring** out) {
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
     {
-        std::lock_guard<std::mutex> g(g_rings_mu);
-        for (size_t i = 0; i < g_free_rings.size(); ++i)
-            if (g_free_rings[i]->dev == dev) {
-                *out = g_free_rings[i];
-                g_free_rings.erase(g_free_rings.begin() + i);
-                return HBEC_OK;
-            }
+        std::unique_lock<std::mutex> lk(g_rings_mu);
+        for (;;) {
+            for (size_t i = 0; i < g_free_rings.size(); ++i)
+                if (g_free_rings[i]->dev == dev) {
+                    *out = g_free_rings[i];
+                    g_free_rings.erase(g_free_rings.begin() + (long)i);
+                    return HBEC_OK;
+                }
+            if (g_rings_made[dev] < ring_limit()) break;
+            g_rings_cv.wait(lk);
+        }
+        ++g_rings_made[dev];  // reserved: made below, outside the lock
     }
-    std::unique_ptr<Ring> r(new Ring());
-    int rc = ring_init(*r, dev);
-    if (rc) return rc;
+    std::unique_ptr<Ring> r(new (std::nothrow) Ring());
+    int rc = r ? ring_init(*r, dev) : fail(HBEC_ERR_NOMEM, "ring allocation");
+    if (rc) {
+        {
+            std::lock_guard<std::mutex> g(g_rings_mu);
+            --g_rings_made[dev];
+        }
+        g_rings_cv.notify_one();
+        return rc;
+    }
     *out = r.release();
     return HBEC_OK;
 }
 
 void ring_release(Ring* r) {
-    std::lock_guard<std::mutex> g(g_rings_mu);
-    g_free_rings.push_back(r);
+    {
+        std::lock_guard<std::mutex> g(g_rings_mu);
+        g_free_rings.push_back(r);
+    }
+    g_rings_cv.notify_all();  // waiters may be on different devices
 }
 
 // ---- pinned host memory (zero-copy host path) ----

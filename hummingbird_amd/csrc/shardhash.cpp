@@ -16,6 +16,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
 #include <map>
 #include <mutex>
 #include <vector>
@@ -182,22 +183,55 @@ struct HashRing {
     }
 };
 
+// Bounded per device like the host path's rings (HBEC_HOST_RINGS, default
+// 8; each pins 192 MiB): callers beyond the bound wait for one to come back.
 std::mutex g_hash_mu;
+std::condition_variable g_hash_cv;
 std::vector<HashRing*> g_hash_free;
+std::map<int, int> g_hash_made;
+
+int hash_ring_limit() {
+    static const int v = [] {
+        const char* e = std::getenv("HBEC_HOST_RINGS");
+        const int x = e ? std::atoi(e) : 0;
+        return x > 0 ? x : 8;
+    }();
+    return v;
+}
+
+int hash_ring_make(int dev, HashRing** out);
 
 int hash_ring_acquire(HashRing** out) {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
     {
-        std::lock_guard<std::mutex> g(g_hash_mu);
-        for (size_t i = 0; i < g_hash_free.size(); ++i)
-            if (g_hash_free[i]->dev == dev) {
-                *out = g_hash_free[i];
-                g_hash_free.erase(g_hash_free.begin() + (long)i);
-                return HBEC_OK;
-            }
+        std::unique_lock<std::mutex> lk(g_hash_mu);
+        for (;;) {
+            for (size_t i = 0; i < g_hash_free.size(); ++i)
+                if (g_hash_free[i]->dev == dev) {
+                    *out = g_hash_free[i];
+                    g_hash_free.erase(g_hash_free.begin() + (long)i);
+                    return HBEC_OK;
+                }
+            if (g_hash_made[dev] < hash_ring_limit()) break;
+            g_hash_cv.wait(lk);
+        }
+        ++g_hash_made[dev];  // reserved: made below, outside the lock
     }
+    const int rc = hash_ring_make(dev, out);
+    if (rc) {
+        {
+            std::lock_guard<std::mutex> g(g_hash_mu);
+            --g_hash_made[dev];
+        }
+        g_hash_cv.notify_one();
+    }
+    return rc;
+}
+
+int hash_ring_make(int dev, HashRing** out) {
+    hipError_t e = hipSuccess;
     std::unique_ptr<HashRing> r(new (std::nothrow) HashRing());
     if (!r) return fail(HBEC_ERR_NOMEM, "hash ring");
     r->dev = dev;
@@ -222,8 +256,11 @@ int hash_ring_acquire(HashRing** out) {
 
 void hash_ring_release(HashRing* r) {
     for (int i = 0; i < kHashSlots; ++i) (void)hipStreamSynchronize(r->stream[i]);
-    std::lock_guard<std::mutex> g(g_hash_mu);
-    g_hash_free.push_back(r);
+    {
+        std::lock_guard<std::mutex> g(g_hash_mu);
+        g_hash_free.push_back(r);
+    }
+    g_hash_cv.notify_all();
 }
 
 }  // namespace

@@ -43,6 +43,7 @@ typedef struct {
     size_t s[PER];
     uint64_t ops[7], rng;
     int rc, where;
+    volatile int cur;  /* operation in progress (-1: none), for the stall report */
 } Job;
 
 static double now(void) {
@@ -72,6 +73,7 @@ static void* run(void* arg) {
         uint8_t* b = j->base[i];
         const size_t s = j->s[i];
         int rc = 0;
+        j->cur = op;
         switch (op) {
             case 0:
                 memset(b + K * s, 0x33, M * s);
@@ -128,7 +130,9 @@ static void* run(void* arg) {
                 break;
             }
         }
+        j->cur = 10 + op;  /* the check after op */
         if (!rc && op != 5 && op != 6) rc = check(j, i);
+        j->cur = -1;
         if (rc) {
             j->rc = rc;
             j->where = op;
@@ -152,6 +156,7 @@ int main(int argc, char** argv) {
     for (int t = 0; t < threads; ++t) {
         Job* j = &jobs[t];
         j->id = t;
+        j->cur = -1;
         j->pinned = t % 2 == 0;
         j->rng = seed + (uint64_t)t * 7919u;
         for (int i = 0; i < PER; ++i) {
@@ -180,6 +185,33 @@ int main(int argc, char** argv) {
     const double t0 = now();
     g_stop = t0 + secs;
     for (int t = 0; t < threads; ++t) pthread_create(&th[t], NULL, run, &jobs[t]);
+    /* progress every 10 s on stderr (long runs must not look hung) */
+    while (now() < g_stop) {
+        struct timespec ts = {10, 0};
+        const double left = g_stop - now();
+        if (left < 10.0) ts = (struct timespec){(time_t)left, (long)((left - (time_t)left) * 1e9)};
+        nanosleep(&ts, NULL);
+        uint64_t sofar = 0;
+        int bad = 0;
+        for (int t = 0; t < threads; ++t) {
+            for (int o = 0; o < 7; ++o) sofar += jobs[t].ops[o];
+            bad |= jobs[t].rc != 0;
+        }
+        int hist[20] = {0};
+        for (int t = 0; t < threads; ++t) {
+            const int c = jobs[t].cur;
+            hist[c < 0 ? 19 : c]++;
+        }
+        uint64_t g = 0, c = 0, b = 0, bs = 0;
+        hbec_coalesce_stats(&g, &c);
+        hbec_batcher_stats(g_bat, &b, &bs);
+        fprintf(stderr, "soak: %.0f s, %llu ops%s; in op 0-6: %d %d %d %d %d %d %d; in check after 0-4: %d %d %d %d %d; "
+                "coalesce %llu/%llu, batches %llu/%llu\n", now() - t0, (unsigned long long)sofar, bad ? ", FAILED" : "",
+                hist[0], hist[1], hist[2], hist[3], hist[4], hist[5], hist[6], hist[10], hist[11], hist[12], hist[13],
+                hist[14], (unsigned long long)g, (unsigned long long)c, (unsigned long long)b, (unsigned long long)bs);
+        fflush(stderr);
+        if (bad) break;
+    }
     int rc = 0, where = -1, who = -1;
     uint64_t ops[7] = {0}, total = 0;
     for (int t = 0; t < threads; ++t) {
