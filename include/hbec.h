@@ -244,8 +244,9 @@ int hbec_reconstruct_plan(hbec_codec* codec, const hbec_plan* plan, const uint8_
  * ecSplit layout), coded through a pinned staging ring — CPU gather, H2D,
  * kernel and D2H of successive chunks overlap on three streams.  Synchronous:
  * on return the parity (encode) or the rebuilt shards (reconstruct) are in the
- * caller's stripes.  Any k (k > 8 runs in accumulate passes).  Env:
- * HBEC_HOST_SLOT_MB (64), HBEC_HOST_THREADS.
+ * caller's stripes.  Any k (k > 8 runs in accumulate passes).  Concurrent
+ * calls share at most HBEC_HOST_RINGS (8) rings per device and wait for one
+ * beyond that.  Env: HBEC_HOST_SLOT_MB (64), HBEC_HOST_THREADS.
  * Zero-copy: 16-B-aligned stripes in pinned, device-mapped host memory are
  * coded IN PLACE by the GPU over PCIe — no staging copies, no CPU
  * gather/scatter (HBEC_ZEROCOPY=0 sends them through the ring too).
