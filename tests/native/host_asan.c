@@ -49,7 +49,7 @@ static int cpu_part(void) {
     CHECK(hbec_encode(c, shards, lens, 5) == HBEC_ERR_TOO_FEW_SHARDS, 5);
     hbec_free(c);
     char algo[4];
-    int k, p, chunk;
+    int64_t k, p, chunk;
     const int rc = hbec_parse_ec_scheme("reedsolomon/4/2/1048576", algo, sizeof algo, &k, &p, &chunk);
     CHECK(rc != HBEC_OK || strlen(algo) < sizeof algo, 6); /* short buffer: rejected or truncated */
     CHECK(hbec_parse_ec_scheme("reedsolomon/4/2/x", algo, sizeof algo, &k, &p, &chunk) == HBEC_ERR_SCHEME, 7);
