@@ -454,6 +454,9 @@ def parse_args(argv):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--settle-ms", type=float, default=60.0,
+                    help="untimed steps before the W warm-up steps until this much GPU time has passed, "
+                         "so the clocks have left their start-up ramp (0 = none)")
     ap.add_argument("--objects", type=int, default=4096, help="objects per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
@@ -530,6 +533,18 @@ def main(argv=None):
     # drop its clocks, and the next ~15 launches then ramp from 1.37 back to
     # 1.08 ms (kernel trace, profiles/r02_ramp_kernel_trace.txt).  The result
     # is verified after the timed region instead.
+    # The clock ramp lasts ~10-14 launches (~15 ms); the driver's `--warmup 5`
+    # is 10 launches, so untimed settle steps run first until --settle-ms of
+    # GPU time has passed.  They are reported as `settle_steps`.
+    settle_steps = 0
+    if args.settle_ms > 0:
+        t_settle = time.perf_counter()
+        while (time.perf_counter() - t_settle) * 1e3 < args.settle_ms and settle_steps < 1000:
+            w.encode()
+            w.reconstruct()
+            settle_steps += 1
+            if settle_steps % 4 == 0:
+                torch.cuda.synchronize()
     for _ in range(args.warmup):
         w.encode()
         w.reconstruct()
@@ -580,6 +595,7 @@ def main(argv=None):
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "settle_steps": settle_steps,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
             "scaling": "weak",
