@@ -155,9 +155,19 @@ __device__ __forceinline__ Tables<K, R> load_tables(const TabArray& tab) {
 // acc[r] ^= XOR_j C[r][j] * x[j] for one 16-B column of K inputs.  The 3K
 // perm terms per (row, dword) are folded by v_bitop3 XOR3s; a pending odd
 // term is carried so every XOR3 retires two terms.
+#ifndef HBEC_GF_NONE
+#define HBEC_GF_NONE 0  // tuning only: plain XOR of the inputs (same loads / stores, no field multiply)
+#endif
 template <int K, int R>
 __device__ __forceinline__ void gf_dot(u32x4 (&acc)[R], const u32x4 (&x)[K], const TabArray& tab,
                                        const Tables<K, R>& tb) {
+    if constexpr (HBEC_GF_NONE != 0) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int j = 0; j < K; ++j) acc[r] ^= x[(j + r) % K];
+        return;
+    }
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
         uint32_t pend[R];

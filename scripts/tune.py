@@ -78,6 +78,9 @@ VARIANTS = {
     "pk_u1b2": (["HBEC_PACKED_U_BIG=1"], {"HBEC_BLOCKS_PER_CU": "2"}),
     "pk_u1b4": (["HBEC_PACKED_U_BIG=1"], {"HBEC_BLOCKS_PER_CU": "4"}),
     "d": ([], {}),
+    # GF-free twin of the shipped kernel: same loop, loads, stores, pacing and
+    # barrier; the field multiply replaced by a plain XOR (parity differs by design)
+    "gfnone": (["HBEC_GF_NONE=1"], {}),
     "v2": (["HBEC_PIPE_V2=1"], {}),
     "v2all": (["HBEC_PIPE_V2_MAXK=16"], {}),
     "v2all_l16": (["HBEC_PIPE_V2_MAXK=16", "HBEC_PIPE_LOADS=16"], {}),
