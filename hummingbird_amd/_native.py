@@ -62,6 +62,7 @@ _SIG = [
     ("hbec_reconstruct_databuf", C.c_int, [_P, _P, C.c_size_t, _U8P, C.c_int]),
     ("hbec_verify_databuf", C.c_int, [_P, _P, C.c_size_t, C.POINTER(C.c_int)]),
     ("hbec_coalesce_stats", C.c_int, [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    ("hbec_host_md5_stats", C.c_int, [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     ("hbec_verify_batch", C.c_int, [_P, C.POINTER(View), C.c_uint64, C.c_uint64, _P, _P]),
     ("hbec_encode_batch", C.c_int, [_P, C.POINTER(View), C.c_uint64, C.c_uint64, _P]),
     ("hbec_reconstruct_batch", C.c_int,

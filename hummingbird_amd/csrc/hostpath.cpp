@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
@@ -67,13 +68,16 @@ struct Ring {
     hbec::TileRec* pin_tiles[kSlots] = {};
     hbec::TileRec* dev_tiles[kSlots] = {};
     hipEvent_t ev_h2d[kSlots] = {}, ev_cmp[kSlots] = {}, ev_done[kSlots] = {};
-    // ShardHash (hbec_encode_host_md5), created on first use: two device hash
-    // arenas.  After a chunk's kernel its shards are copied (D2D) into the
-    // current arena and the slot is free again; a full arena is hashed by ONE
-    // md5_list launch (thousands of chains, full-chip) on s_md5 while the other
-    // arena fills, so hashing hides behind the PCIe stream.
-    static constexpr int kArenas = 2;
-    hipStream_t s_md5 = nullptr;
+    // ShardHash (hbec_encode_host_md5), created on first use: n_arenas device
+    // hash arenas (HBEC_HASH_ARENAS, default 4, of HBEC_HASH_ARENA_MB, default
+    // 512).  A chunk's shards land in the current arena (copied D2D after the
+    // ring's kernel, or written by the mirrored zero-copy kernel); a full
+    // arena is hashed by ONE md5_list launch on its own stream while the next
+    // arenas fill, so hashing hides behind the PCIe stream, and the hashes of
+    // several arenas may run at once.
+    static constexpr int kArenas = 8;
+    int n_arenas = 0;
+    hipStream_t s_md5[kArenas] = {};
     uint8_t* arena[kArenas] = {};
     size_t arena_cap = 0, arena_rec_cap = 0;
     uint64_t* pin_md5rec[kArenas] = {};
@@ -100,7 +104,8 @@ struct Ring {
             if (ev_arena_copied[a]) (void)hipEventDestroy(ev_arena_copied[a]);
             if (ev_arena_hashed[a]) (void)hipEventDestroy(ev_arena_hashed[a]);
         }
-        if (s_md5) (void)hipStreamDestroy(s_md5);
+        for (int a = 0; a < kArenas; ++a)
+            if (s_md5[a]) (void)hipStreamDestroy(s_md5[a]);
         if (s_h2d) (void)hipStreamDestroy(s_h2d);
         if (s_cmp) (void)hipStreamDestroy(s_cmp);
         if (s_d2h) (void)hipStreamDestroy(s_d2h);
@@ -166,26 +171,88 @@ int ring_staging_init(Ring& r) {
 }
 
 int ring_md5_init(Ring& r) {
-    if (r.arena[0]) return HBEC_OK;
-    const size_t cap = env_size("HBEC_HASH_ARENA_MB", 1024) << 20;
+    if (r.n_arenas > 0) return HBEC_OK;  // set last: everything below exists
+    const size_t cap = env_size("HBEC_HASH_ARENA_MB", 512) << 20;
+    const int n_arenas = (int)std::min<size_t>(Ring::kArenas, std::max<size_t>(2, env_size("HBEC_HASH_ARENAS", 4)));
     r.arena_cap = std::max(cap, r.in_cap + r.out_cap);
     // MD5 records per arena (32 B pinned each; HBEC_HASH_ARENA_RECS, default
     // 256 K = 8 MiB): an arena is hashed early when its records run out, so
     // this bounds pinned memory, not batch size (one record per 16-B shard
     // would pin 2 GiB per arena)
     r.arena_rec_cap = std::min<size_t>(r.arena_cap / 16 + 1024, env_size("HBEC_HASH_ARENA_RECS", 1u << 18));
-    hipError_t e = hipStreamCreateWithFlags(&r.s_md5, hipStreamNonBlocking);
-    for (int a = 0; a < Ring::kArenas && e == hipSuccess; ++a) {
-        e = hipMalloc(&r.arena[a], r.arena_cap);
-        if (e == hipSuccess)
+    hipError_t e = hipSuccess;
+    for (int a = 0; a < n_arenas && e == hipSuccess; ++a) {  // a failed earlier attempt keeps what it got
+        if (!r.s_md5[a]) e = hipStreamCreateWithFlags(&r.s_md5[a], hipStreamNonBlocking);
+        if (e == hipSuccess && !r.arena[a]) e = hipMalloc(&r.arena[a], r.arena_cap);
+        if (e == hipSuccess && !r.pin_md5rec[a])
             e = hipHostMalloc(reinterpret_cast<void**>(&r.pin_md5rec[a]), r.arena_rec_cap * 32, hipHostMallocDefault);
-        if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&r.dev_md5rec[a]), r.arena_rec_cap * 32);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&r.ev_arena_copied[a], hipEventDisableTiming);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&r.ev_arena_hashed[a], hipEventDisableTiming);
+        if (e == hipSuccess && !r.dev_md5rec[a])
+            e = hipMalloc(reinterpret_cast<void**>(&r.dev_md5rec[a]), r.arena_rec_cap * 32);
+        if (e == hipSuccess && !r.ev_arena_copied[a])
+            e = hipEventCreateWithFlags(&r.ev_arena_copied[a], hipEventDisableTiming);
+        if (e == hipSuccess && !r.ev_arena_hashed[a])
+            e = hipEventCreateWithFlags(&r.ev_arena_hashed[a], hipEventDisableTiming);
     }
     if (e != hipSuccess) return hip_fail(e, "hash arena");
+    r.n_arenas = n_arenas;
     return HBEC_OK;
 }
+
+// The hash arenas of one hbec_encode_host_md5 call.  Shards are appended to
+// the current arena and a record per shard to its pinned record list; a full
+// arena is hashed by one md5_list launch on the arena's stream, ordered after
+// the work `producer` queued to fill it, and the call moves on to the next
+// arena once that arena's previous hash has finished (its memory and pinned
+// records are then free).
+struct ArenaCursor {
+    Ring* ring;
+    hipStream_t producer;
+    uint8_t* d_digest;
+    bool serial = false;  // hash on the producer stream, in order with the work that fills the arenas
+    int cur = 0;
+    uint64_t used = 0, recs = 0;
+
+    uint64_t base() const { return reinterpret_cast<uint64_t>(ring->arena[cur]) + used; }
+    bool fits(uint64_t bytes, uint64_t n_recs) const {
+        return used + bytes <= ring->arena_cap && recs + n_recs <= ring->arena_rec_cap;
+    }
+    void add(uint64_t addr, uint64_t len, uint64_t slot) {
+        uint64_t* r = ring->pin_md5rec[cur] + 4 * recs++;
+        r[0] = addr;
+        r[1] = len;
+        r[2] = slot;
+        r[3] = 0;
+    }
+    int flush() {  // hash the current arena, move to the next free one
+        if (recs == 0) return HBEC_OK;
+        const int a = cur;
+        hipStream_t hs = serial ? producer : ring->s_md5[a];
+        hipError_t e = hipSuccess;
+        if (!serial) {
+            e = hipEventRecord(ring->ev_arena_copied[a], producer);
+            if (e == hipSuccess) e = hipStreamWaitEvent(hs, ring->ev_arena_copied[a], 0);
+        }
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(ring->dev_md5rec[a], ring->pin_md5rec[a], recs * 32, hipMemcpyHostToDevice, hs);
+        if (e == hipSuccess) e = hbec::launch_md5_list(ring->dev_md5rec[a], recs, d_digest, true, hs);
+        if (e == hipSuccess) e = hipEventRecord(ring->ev_arena_hashed[a], hs);
+        if (e != hipSuccess) return hip_fail(e, "hash arena launch");
+        cur = (cur + 1) % ring->n_arenas;
+        used = recs = 0;
+        e = hipEventSynchronize(ring->ev_arena_hashed[cur]);  // may still hash its last fill
+        if (e != hipSuccess) return hip_fail(e, "hash arena wait");
+        return HBEC_OK;
+    }
+    int finish() {  // hash the last partial arena and wait for every hash
+        int rc = flush();
+        if (rc) return rc;
+        for (int a = 0; a < ring->n_arenas; ++a) {
+            hipError_t e = hipStreamSynchronize(ring->s_md5[a]);
+            if (e != hipSuccess) return hip_fail(e, "hash drain");
+        }
+        return HBEC_OK;
+    }
+};
 
 // Rings per device are bounded (HBEC_HOST_RINGS, default 8): each staged
 // ring pins 384 MiB of host memory and runs a copy pool of host_threads()
@@ -398,6 +465,96 @@ int zero_copy_run(Ring* ring, const std::vector<ZcStripe>& zs, const std::vector
     return HBEC_OK;
 }
 
+// Zero-copy with ShardHash (hbec_encode_host_md5 when every stripe is pinned):
+// the stripes kernel codes each stripe in place over PCIe, exactly as
+// zero_copy_run, and also writes every shard column it holds (inputs and
+// outputs) to a device hash arena (StripeArgs::mirror), so nothing crosses
+// PCIe twice and no CPU copy runs.  A full arena is hashed by one md5_list
+// launch on its own stream while the stripes kernel fills the next ones.
+// Stripe s's shard i lands at arena + its offset + i*S; its digest at
+// (s * n_shards + i) * 16 of d_digest.
+int md5_serial_mode();
+
+int zero_copy_md5_run(Ring* ring, const std::vector<ZcStripe>& zs, const std::vector<int>& in_idx,
+                      const std::vector<int>& out_idx, const std::vector<uint8_t>& rows, uint8_t* d_digest,
+                      int n_shards) {
+    const int K = (int)in_idx.size(), R = (int)out_idx.size();
+    int rc = ring_md5_init(*ring);
+    if (rc) return rc;
+    const uint64_t tile = (uint64_t)hbec::stripes_tile_bytes(std::min(K, hbec::kStripeMaxK));
+    ArenaCursor ac{ring, ring->s_cmp, d_digest, md5_serial_mode() != 0};
+    hipError_t e = hipSuccess;
+    size_t si = 0;
+    for (int c = 0; si < zs.size(); ++c) {
+        const int slot = c % kSlots;
+        e = hipEventSynchronize(ring->ev_cmp[slot]);  // the slot's previous records are consumed
+        if (e != hipSuccess) return hip_fail(e, "zero-copy slot wait");
+        hbec::TileRec* rec = ring->pin_tiles[slot];
+        uint64_t nt = 0;
+        while (si < zs.size()) {
+            const ZcStripe& z = zs[si];
+            const uint64_t S = z.shard_len;
+            const uint64_t tiles = (S + tile - 1) / tile;
+            const uint64_t bytes = ((uint64_t)n_shards * S + 255) & ~uint64_t(255);
+            if (tiles > ring->tile_cap || bytes > ring->arena_cap)
+                return fail(HBEC_ERR_INVALID_ARG, "stripe too large for a hash arena");
+            if (nt > 0 && nt + tiles > ring->tile_cap) break;
+            if (!ac.fits(bytes, (uint64_t)(K + R))) {
+                if (nt > 0) break;  // launch this chunk first: the arena is hashed after its kernels
+                rc = ac.flush();
+                if (rc) return rc;
+            }
+            const uint64_t mbase = ac.base();
+            for (uint64_t off = 0; off < S; off += tile) {
+                hbec::TileRec& t = rec[nt++];
+                t.in_addr = z.dev + off;
+                t.out_addr = mbase + off;
+                t.in_stride = t.out_stride = (uint32_t)S;
+                t.valid = (uint32_t)std::min<uint64_t>(tile, S - off);
+                t.pad_ = 0;
+            }
+            for (int i : in_idx) ac.add(mbase + (uint64_t)i * S, S, (uint64_t)si * (uint64_t)n_shards + (uint64_t)i);
+            for (int i : out_idx) ac.add(mbase + (uint64_t)i * S, S, (uint64_t)si * (uint64_t)n_shards + (uint64_t)i);
+            ac.used += bytes;
+            ++si;
+        }
+        e = hipMemcpyAsync(ring->dev_tiles[slot], rec, nt * sizeof(hbec::TileRec), hipMemcpyHostToDevice,
+                           ring->s_cmp);
+        if (e != hipSuccess) return hip_fail(e, "zero-copy records H2D");
+        rc = hbec::launch_stripe_passes(ring->dev_tiles[slot], nt, in_idx, out_idx, rows, 0, ring->s_cmp,
+                                        zero_copy_blocks_per_cu(), true);
+        if (rc) return rc;
+        e = hipEventRecord(ring->ev_cmp[slot], ring->s_cmp);
+        if (e != hipSuccess) return hip_fail(e, "zero-copy event");
+    }
+    rc = ac.finish();
+    if (rc) return rc;
+    e = hipStreamSynchronize(ring->s_cmp);
+    if (e != hipSuccess) return hip_fail(e, "zero-copy drain");
+    return HBEC_OK;
+}
+
+std::atomic<uint64_t> g_md5_zc_calls{0}, g_md5_ring_calls{0};
+
+// HBEC_MD5_SERIAL (tuning): "0" hash arenas beside the work that fills the
+// next ones, "1" in order with it, unset: in order for zero-copy, beside for
+// the ring.
+int md5_serial_mode() {
+    static const int v = [] {
+        const char* e = std::getenv("HBEC_MD5_SERIAL");
+        return e ? (e[0] == '1' ? 1 : 0) : -1;
+    }();
+    return v;
+}
+
+bool zero_copy_md5_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("HBEC_MD5_ZEROCOPY");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 // Code every stripe: inputs = shards in_idx, outputs = shards out_idx with `rows`.
 // With d_digest (device, n * n_shards * 16 B), also hash every input and
 // output shard of every stripe while it is in the device slot: digest of
@@ -415,7 +572,34 @@ int host_run(const hbec_stripe* stripes, uint64_t n, const std::vector<int>& in_
         ~Releaser() { ring_release(r); }
     } rel{ring};
     // Pinned stripes are coded in place (zero-copy); the rest take the ring.
-    // (Hashing needs every shard on the device, so it always takes the ring.)
+    // Hashing needs every shard on the device: when every stripe is pinned,
+    // the zero-copy kernel also copies them to a device hash arena
+    // (zero_copy_md5_run); otherwise the whole batch takes the ring.
+    if (d_digest && zero_copy_enabled() && zero_copy_md5_enabled()) {
+        int top = 0;
+        for (int i : in_idx) top = std::max(top, i);
+        for (int i : out_idx) top = std::max(top, i);
+        std::vector<ZcStripe> zs;
+        zs.reserve(n);
+        for (uint64_t s = 0; s < n; ++s) {
+            const uint64_t S = stripes[s].shard_len;
+            const bool aligned = stripes[s].base && (reinterpret_cast<uintptr_t>(stripes[s].base) & 15u) == 0 &&
+                                 S % 16 == 0 && S > 0 && S < (1ull << 32);
+            const uint64_t d = aligned ? pinned_device_addr(stripes[s].base, (uint64_t)(top + 1) * S) : 0;
+            if (!d || (d & 15u) != 0) break;
+            zs.push_back({d, S});
+        }
+        if (zs.size() == n) {
+            // the same stripe bound as the ring (hbec.h: one staging slot)
+            const uint64_t max_cols = (std::min(ring->in_cap / in_idx.size(), ring->out_cap / out_idx.size()) / 16) * 16;
+            for (const ZcStripe& z : zs)
+                if (z.shard_len > max_cols)
+                    return fail(HBEC_ERR_INVALID_ARG, "hashing needs every stripe to fit one staging slot");
+            g_md5_zc_calls.fetch_add(1, std::memory_order_relaxed);
+            return zero_copy_md5_run(ring, zs, in_idx, out_idx, rows, d_digest, n_shards);
+        }
+    }
+    if (d_digest) g_md5_ring_calls.fetch_add(1, std::memory_order_relaxed);
     std::vector<hbec_stripe> staged;
     if (!d_digest && zero_copy_enabled()) {
         int top = 0;
@@ -452,27 +636,7 @@ int host_run(const hbec_stripe* stripes, uint64_t n, const std::vector<int>& in_
         rc = ring_md5_init(*ring);
         if (rc) return rc;
     }
-    // hash arena state: current arena, bytes and records queued in it
-    int cur_arena = 0;
-    uint64_t arena_used = 0, arena_recs = 0;
-    auto hash_arena = [&]() -> int {  // hash everything queued in the current arena, switch arenas
-        if (arena_recs == 0) return HBEC_OK;
-        const int a = cur_arena;
-        hipError_t e = hipEventRecord(ring->ev_arena_copied[a], ring->s_cmp);  // its copies are queued on s_cmp
-        if (e == hipSuccess) e = hipStreamWaitEvent(ring->s_md5, ring->ev_arena_copied[a], 0);
-        if (e == hipSuccess)
-            e = hipMemcpyAsync(ring->dev_md5rec[a], ring->pin_md5rec[a], arena_recs * 32, hipMemcpyHostToDevice,
-                               ring->s_md5);
-        if (e == hipSuccess) e = hbec::launch_md5_list(ring->dev_md5rec[a], arena_recs, d_digest, true, ring->s_md5);
-        if (e == hipSuccess) e = hipEventRecord(ring->ev_arena_hashed[a], ring->s_md5);
-        if (e != hipSuccess) return hip_fail(e, "hash arena launch");
-        cur_arena ^= 1;
-        arena_used = arena_recs = 0;
-        // the next arena (and its pinned records) may still be hashing its last fill
-        e = hipEventSynchronize(ring->ev_arena_hashed[cur_arena]);
-        if (e != hipSuccess) return hip_fail(e, "hash arena wait");
-        return HBEC_OK;
-    };
+    ArenaCursor ac{ring, ring->s_cmp, d_digest, md5_serial_mode() == 1};  // hash arenas (d_digest only)
 
     // Cut the batch into chunks of pieces that fit a slot.
     std::vector<std::vector<Piece>> chunks(1);
@@ -569,13 +733,11 @@ int host_run(const hbec_stripe* stripes, uint64_t n, const std::vector<int>& in_
         rc = hbec::launch_stripe_passes(ring->dev_tiles[slot], nt, slot_in, slot_out, rows, 0, ring->s_cmp);
         if (rc) return rc;
         if (d_digest) {  // the chunk's shards -> hash arena (D2D, same stream, before the slot is released)
-            if (arena_used + in_bytes + out_bytes > ring->arena_cap ||
-                arena_recs + pieces.size() * (size_t)(K + R) > ring->arena_rec_cap) {
-                rc = hash_arena();
+            if (!ac.fits(in_bytes + out_bytes, pieces.size() * (uint64_t)(K + R))) {
+                rc = ac.flush();
                 if (rc) return rc;
             }
-            const int a = cur_arena;
-            const uint64_t ain = reinterpret_cast<uint64_t>(ring->arena[a]) + arena_used;
+            const uint64_t ain = ac.base();
             const uint64_t aout = ain + in_bytes;
             e = hipMemcpyAsync(reinterpret_cast<void*>(ain), ring->dev_in[slot], in_bytes, hipMemcpyDeviceToDevice,
                                ring->s_cmp);
@@ -583,22 +745,14 @@ int host_run(const hbec_stripe* stripes, uint64_t n, const std::vector<int>& in_
                 e = hipMemcpyAsync(reinterpret_cast<void*>(aout), ring->dev_out[slot], out_bytes,
                                    hipMemcpyDeviceToDevice, ring->s_cmp);
             if (e != hipSuccess) return hip_fail(e, "hash arena copy");
-            uint64_t* rec = ring->pin_md5rec[a];
             for (const Piece& p : pieces) {
-                for (int j = 0; j < K; ++j, ++arena_recs) {
-                    rec[4 * arena_recs + 0] = ain + p.in_off + (uint64_t)j * p.lpad;
-                    rec[4 * arena_recs + 1] = p.len;
-                    rec[4 * arena_recs + 2] = p.stripe * (uint64_t)n_shards + (uint64_t)in_idx[j];
-                    rec[4 * arena_recs + 3] = 0;
-                }
-                for (int r = 0; r < R; ++r, ++arena_recs) {
-                    rec[4 * arena_recs + 0] = aout + p.out_off + (uint64_t)r * p.lpad;
-                    rec[4 * arena_recs + 1] = p.len;
-                    rec[4 * arena_recs + 2] = p.stripe * (uint64_t)n_shards + (uint64_t)out_idx[r];
-                    rec[4 * arena_recs + 3] = 0;
-                }
+                for (int j = 0; j < K; ++j)
+                    ac.add(ain + p.in_off + (uint64_t)j * p.lpad, p.len, p.stripe * (uint64_t)n_shards + (uint64_t)in_idx[j]);
+                for (int r = 0; r < R; ++r)
+                    ac.add(aout + p.out_off + (uint64_t)r * p.lpad, p.len,
+                           p.stripe * (uint64_t)n_shards + (uint64_t)out_idx[r]);
             }
-            arena_used += (in_bytes + out_bytes + 255) & ~uint64_t(255);
+            ac.used += (in_bytes + out_bytes + 255) & ~uint64_t(255);
         }
         e = hipEventRecord(ring->ev_cmp[slot], ring->s_cmp);
         if (e == hipSuccess) e = hipStreamWaitEvent(ring->s_d2h, ring->ev_cmp[slot], 0);
@@ -614,12 +768,7 @@ int host_run(const hbec_stripe* stripes, uint64_t n, const std::vector<int>& in_
         rc = scatter(slot);
         if (rc) return rc;
     }
-    if (d_digest) {
-        rc = hash_arena();  // the last partial arena
-        if (rc) return rc;
-        hipError_t e = hipStreamSynchronize(ring->s_md5);
-        if (e != hipSuccess) return hip_fail(e, "host path hash drain");
-    }
+    if (d_digest) return ac.finish();
     return HBEC_OK;
 }
 
@@ -791,6 +940,12 @@ int hbec_encode_host_md5(hbec_codec* codec, const hbec_stripe* stripes, uint64_t
         (void)hipStreamSynchronize(st);
         return rc;
     });
+}
+
+int hbec_host_md5_stats(uint64_t* zero_copy_calls, uint64_t* ring_calls) {
+    if (zero_copy_calls) *zero_copy_calls = g_md5_zc_calls.load(std::memory_order_relaxed);
+    if (ring_calls) *ring_calls = g_md5_ring_calls.load(std::memory_order_relaxed);
+    return HBEC_OK;
 }
 
 int hbec_device_count(int* n) {

@@ -72,8 +72,10 @@ struct TileRec;
 int stripes_grid(int k, int r, uint64_t n_tiles, int* grid, int blocks_per_cu = 0);
 // out (^)= rows x in over tile records, in launches of <= 3 outputs and
 // <= 8 inputs (k > 8: accumulate passes).  sel_k > 0: object-plan bases.
+// mirror: code in place at each record's in_addr and copy every input and
+// output column to the device arena at out_addr (StripeArgs::mirror).
 int launch_stripe_passes(const TileRec* tiles, uint64_t n_tiles, const std::vector<int>& in_idx,
                          const std::vector<int>& out_idx, const std::vector<uint8_t>& rows, int sel_k,
-                         hipStream_t stream, int blocks_per_cu = 0);
+                         hipStream_t stream, int blocks_per_cu = 0, bool mirror = false);
 
 }  // namespace hbec

@@ -131,7 +131,8 @@ struct StripeArgs {
     uint32_t n_tiles;
     uint32_t split;           // 1: object plan (in_sel / out_sel apply)
     uint32_t accumulate;      // 1: out ^= result (passes 2.. over > kStripeMaxK inputs; not with split)
-    uint32_t pad_;
+    uint32_t mirror;          // 1: code in place at in_addr (stride in_stride) and copy every input and
+                              //    output column to the device arena at out_addr (stride out_stride)
     uint32_t in_idx[kMaxK];   // shard index (within its base) read as input j
     uint32_t out_idx[kMaxR];  // shard index (within its base) written as output r
     uint32_t in_sel, out_sel;

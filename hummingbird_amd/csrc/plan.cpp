@@ -98,10 +98,11 @@ int hbec::stripes_grid(int k, int r, uint64_t n_tiles, int* grid, int blocks_per
 // marks an object plan (split bases: shard indices >= sel_k are parity).
 int hbec::launch_stripe_passes(const TileRec* tiles, uint64_t n_tiles, const std::vector<int>& in_idx,
                                const std::vector<int>& out_idx, const std::vector<uint8_t>& rows, int sel_k,
-                               hipStream_t stream, int blocks_per_cu) {
+                               hipStream_t stream, int blocks_per_cu, bool mirror) {
     const int K_all = (int)in_idx.size(), R_all = (int)out_idx.size();
     if (n_tiles == 0 || R_all == 0) return HBEC_OK;
     if (sel_k > 0 && K_all > kStripeMaxK) return fail(HBEC_ERR_INVALID_ARG, "object plans take <= 8 inputs per pass");
+    if (sel_k > 0 && mirror) return fail(HBEC_ERR_INVALID_ARG, "object plans are not mirrored");
     for (int r0 = 0; r0 < R_all; r0 += 3) {
         const int R = std::min(3, R_all - r0);
         for (int c0 = 0; c0 < K_all; c0 += kStripeMaxK) {
@@ -112,6 +113,7 @@ int hbec::launch_stripe_passes(const TileRec* tiles, uint64_t n_tiles, const std
             a.n_tiles = (uint32_t)n_tiles;
             a.split = sel_k > 0 ? 1u : 0u;
             a.accumulate = c0 > 0 ? 1u : 0u;
+            a.mirror = mirror ? 1u : 0u;
             for (int j = 0; j < K; ++j) {
                 a.in_idx[j] = (uint32_t)in_idx[c0 + j];
                 if (sel_k > 0 && in_idx[c0 + j] >= sel_k) {  // parity shard: base B

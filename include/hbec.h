@@ -280,8 +280,15 @@ int hbec_reconstruct_host_devices(hbec_codec* codec, const hbec_stripe* stripes,
  * shard of every stripe, computed on the GPU while the stripe is in the device
  * slot (hashing of one chunk overlaps the copies of the next): digests (host)
  * receive n_stripes * (k+m) raw MD5s, shard i of stripe s at (s*(k+m)+i)*16.
- * Every stripe must fit one staging slot (k * shard_len <= HBEC_HOST_SLOT_MB). */
+ * Every stripe must fit one staging slot (k * shard_len <= HBEC_HOST_SLOT_MB).
+ * When every stripe is pinned and device-mapped (hbec_host_alloc), the stripes
+ * are coded in place over PCIe and the kernel copies their shards to a device
+ * hash arena as it goes (no staging copy, nothing read twice over PCIe);
+ * HBEC_MD5_ZEROCOPY=0 sends them through the ring instead.  Otherwise the
+ * whole batch takes the staging ring.  hbec_host_md5_stats: calls since load
+ * that took each way. */
 int hbec_encode_host_md5(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n_stripes, uint8_t* digests);
+int hbec_host_md5_stats(uint64_t* zero_copy_calls, uint64_t* ring_calls);
 
 /* Batching driver for concurrent callers (e.g. one cgo call per Stabilize):
  * each call submits ONE host stripe and blocks until it is coded; worker

@@ -223,3 +223,104 @@ def test_batcher_encode_md5_concurrent():
         t.join()
     bat.close()
     assert not errs, errs
+
+
+def _md5_stats():
+    import ctypes as C
+
+    from hummingbird_amd import _native as N
+
+    zc, ring = C.c_uint64(), C.c_uint64()
+    assert N.lib().hbec_host_md5_stats(C.byref(zc), C.byref(ring)) == 0
+    return zc.value, ring.value
+
+
+def _pinned_stripes(hb, k, m, sizes, rng):
+    """Stripes (ecSplit databuf layout) at 256-B aligned offsets of one
+    hbec_host_alloc buffer, data random, parity zero."""
+    stripes, off = [], 0
+    for s in sizes:
+        st = hb.array[off:off + (k + m) * s]
+        st[:k * s] = rng.integers(0, 256, k * s, dtype=np.uint8)
+        st[k * s:] = 0
+        stripes.append(st)
+        off += ((k + m) * s + 255) // 256 * 256
+    return stripes
+
+
+def _check_stripes(k, m, sizes, stripes, hashes):
+    mat = CO.build_matrix(k, m)
+    for st, s, hs in zip(stripes, sizes, hashes):
+        shards = [st[i * s:(i + 1) * s] for i in range(k + m)]
+        want = CO.apply(mat[k:], shards[:k])
+        for r in range(m):
+            assert np.array_equal(shards[k + r], want[r])
+        assert hs == [O.shard_hash(x) for x in shards]
+
+
+@pytest.mark.parametrize("k,m,sizes", [(4, 2, [1 << 18] * 40 + [16, 4096 * 3 + 16]), (8, 3, [512, 1 << 17] * 20),
+                                       (10, 4, [4096, 65536] * 6), (17, 3, [1024] * 10 + [48]),
+                                       (3, 5, [2048, 16, 8192] * 4), (1, 1, [16, 4096])])
+def test_encode_host_md5_pinned_zero_copy(k, m, sizes):
+    """Pinned stripes: coded in place over PCIe by the mirrored stripes kernel,
+    hashed from the device arena (k > 8: accumulate passes; m > 3: output
+    groups); parity and every digest against the oracle."""
+    enc = RS.New(k, m)
+    rng = np.random.default_rng(k * 100 + m)
+    total = sum(((k + m) * s + 255) // 256 * 256 for s in sizes)
+    hb = RS.HostBuffer(total)
+    try:
+        stripes = _pinned_stripes(hb, k, m, sizes, rng)
+        zc0, ring0 = _md5_stats()
+        hashes = enc.EncodeStripesMD5(stripes)
+        zc1, ring1 = _md5_stats()
+        assert (zc1 - zc0, ring1 - ring0) == (1, 0)
+        _check_stripes(k, m, sizes, stripes, hashes)
+        del stripes
+    finally:
+        hb.free()
+
+
+def test_encode_host_md5_mixed_pinned_and_pageable_takes_ring():
+    k, m = 4, 2
+    sizes = [4096, 1 << 16, 4096]
+    enc = RS.New(k, m)
+    rng = np.random.default_rng(5)
+    hb = RS.HostBuffer(sum(((k + m) * s + 255) // 256 * 256 for s in sizes))
+    try:
+        stripes = _pinned_stripes(hb, k, m, sizes, rng)
+        page = np.zeros((k + m) * 2048, np.uint8)
+        page[:k * 2048] = rng.integers(0, 256, k * 2048, dtype=np.uint8)
+        stripes.insert(1, page)
+        sizes.insert(1, 2048)
+        zc0, ring0 = _md5_stats()
+        hashes = enc.EncodeStripesMD5(stripes)
+        zc1, ring1 = _md5_stats()
+        assert (zc1 - zc0, ring1 - ring0) == (0, 1)
+        _check_stripes(k, m, sizes, stripes, hashes)
+        del stripes
+    finally:
+        hb.free()
+
+
+def test_encode_host_md5_pinned_many_small_stripes_switch_arenas():
+    """50 000 pinned 4+2 stripes of 1 KiB shards: 300 000 hash records, more
+    than one arena holds (256 K), so arenas alternate mid-batch."""
+    k, m, s, n = 4, 2, 1024, 50_000
+    enc = RS.New(k, m)
+    hb = RS.HostBuffer(n * (k + m) * s)
+    try:
+        rows = hb.array.reshape(n, (k + m) * s)
+        rows[:, :k * s] = np.random.default_rng(11).integers(0, 256, (n, k * s), dtype=np.uint8)
+        rows[:, k * s:] = 0
+        zc0, _ = _md5_stats()
+        hashes = enc.EncodeStripesMD5([rows[i] for i in range(n)])
+        assert _md5_stats()[0] == zc0 + 1
+        want, _ = CO.encode_batch(k, m, np.ascontiguousarray(rows[:, :k * s]), threads=CO.cpu_threads())
+        assert np.array_equal(rows[:, k * s:], want)
+        for i in range(0, n, 997):
+            assert hashes[i] == [O.shard_hash(rows[i, j * s:(j + 1) * s]) for j in range(k + m)]
+        assert hashes[-1] == [O.shard_hash(rows[-1, j * s:(j + 1) * s]) for j in range(k + m)]
+        del rows
+    finally:
+        hb.free()
