@@ -69,8 +69,9 @@ struct Ring {
     hbec::TileRec* dev_tiles[kSlots] = {};
     hipEvent_t ev_h2d[kSlots] = {}, ev_cmp[kSlots] = {}, ev_done[kSlots] = {};
     // ShardHash (hbec_encode_host_md5), created on first use: n_arenas device
-    // hash arenas (HBEC_HASH_ARENAS, default 4, of HBEC_HASH_ARENA_MB, default
-    // 512).  A chunk's shards land in the current arena (copied D2D after the
+    // hash arenas (HBEC_HASH_ARENAS, default 2, of HBEC_HASH_ARENA_MB, default
+    // 1024; 2 x 3 GiB: pinned 4+2 encode+hash 1.14 x encode alone instead of
+    // 1.21 x, profiles/r02_host_md5_arenas.jsonl).  A chunk's shards land in the current arena (copied D2D after the
     // ring's kernel, or written by the mirrored zero-copy kernel); a full
     // arena is hashed by ONE md5_list launch on its own stream while the next
     // arenas fill, so hashing hides behind the PCIe stream, and the hashes of
@@ -172,8 +173,8 @@ int ring_staging_init(Ring& r) {
 
 int ring_md5_init(Ring& r) {
     if (r.n_arenas > 0) return HBEC_OK;  // set last: everything below exists
-    const size_t cap = env_size("HBEC_HASH_ARENA_MB", 512) << 20;
-    const int n_arenas = (int)std::min<size_t>(Ring::kArenas, std::max<size_t>(2, env_size("HBEC_HASH_ARENAS", 4)));
+    const size_t cap = env_size("HBEC_HASH_ARENA_MB", 1024) << 20;
+    const int n_arenas = (int)std::min<size_t>(Ring::kArenas, std::max<size_t>(2, env_size("HBEC_HASH_ARENAS", 2)));
     r.arena_cap = std::max(cap, r.in_cap + r.out_cap);
     // MD5 records per arena (32 B pinned each; HBEC_HASH_ARENA_RECS, default
     // 256 K = 8 MiB): an arena is hashed early when its records run out, so
@@ -208,7 +209,6 @@ struct ArenaCursor {
     Ring* ring;
     hipStream_t producer;
     uint8_t* d_digest;
-    bool serial = false;  // hash on the producer stream, in order with the work that fills the arenas
     int cur = 0;
     uint64_t used = 0, recs = 0;
 
@@ -226,12 +226,9 @@ struct ArenaCursor {
     int flush() {  // hash the current arena, move to the next free one
         if (recs == 0) return HBEC_OK;
         const int a = cur;
-        hipStream_t hs = serial ? producer : ring->s_md5[a];
-        hipError_t e = hipSuccess;
-        if (!serial) {
-            e = hipEventRecord(ring->ev_arena_copied[a], producer);
-            if (e == hipSuccess) e = hipStreamWaitEvent(hs, ring->ev_arena_copied[a], 0);
-        }
+        hipStream_t hs = ring->s_md5[a];
+        hipError_t e = hipEventRecord(ring->ev_arena_copied[a], producer);
+        if (e == hipSuccess) e = hipStreamWaitEvent(hs, ring->ev_arena_copied[a], 0);
         if (e == hipSuccess)
             e = hipMemcpyAsync(ring->dev_md5rec[a], ring->pin_md5rec[a], recs * 32, hipMemcpyHostToDevice, hs);
         if (e == hipSuccess) e = hbec::launch_md5_list(ring->dev_md5rec[a], recs, d_digest, true, hs);
@@ -473,8 +470,6 @@ int zero_copy_run(Ring* ring, const std::vector<ZcStripe>& zs, const std::vector
 // launch on its own stream while the stripes kernel fills the next ones.
 // Stripe s's shard i lands at arena + its offset + i*S; its digest at
 // (s * n_shards + i) * 16 of d_digest.
-int md5_serial_mode();
-
 int zero_copy_md5_run(Ring* ring, const std::vector<ZcStripe>& zs, const std::vector<int>& in_idx,
                       const std::vector<int>& out_idx, const std::vector<uint8_t>& rows, uint8_t* d_digest,
                       int n_shards) {
@@ -482,7 +477,7 @@ int zero_copy_md5_run(Ring* ring, const std::vector<ZcStripe>& zs, const std::ve
     int rc = ring_md5_init(*ring);
     if (rc) return rc;
     const uint64_t tile = (uint64_t)hbec::stripes_tile_bytes(std::min(K, hbec::kStripeMaxK));
-    ArenaCursor ac{ring, ring->s_cmp, d_digest, md5_serial_mode() != 0};
+    ArenaCursor ac{ring, ring->s_cmp, d_digest};
     hipError_t e = hipSuccess;
     size_t si = 0;
     for (int c = 0; si < zs.size(); ++c) {
@@ -535,17 +530,6 @@ int zero_copy_md5_run(Ring* ring, const std::vector<ZcStripe>& zs, const std::ve
 }
 
 std::atomic<uint64_t> g_md5_zc_calls{0}, g_md5_ring_calls{0};
-
-// HBEC_MD5_SERIAL (tuning): "0" hash arenas beside the work that fills the
-// next ones, "1" in order with it, unset: in order for zero-copy, beside for
-// the ring.
-int md5_serial_mode() {
-    static const int v = [] {
-        const char* e = std::getenv("HBEC_MD5_SERIAL");
-        return e ? (e[0] == '1' ? 1 : 0) : -1;
-    }();
-    return v;
-}
 
 bool zero_copy_md5_enabled() {
     static const bool on = [] {
@@ -636,7 +620,7 @@ int host_run(const hbec_stripe* stripes, uint64_t n, const std::vector<int>& in_
         rc = ring_md5_init(*ring);
         if (rc) return rc;
     }
-    ArenaCursor ac{ring, ring->s_cmp, d_digest, md5_serial_mode() == 1};  // hash arenas (d_digest only)
+    ArenaCursor ac{ring, ring->s_cmp, d_digest};  // hash arenas (d_digest only)
 
     // Cut the batch into chunks of pieces that fit a slot.
     std::vector<std::vector<Piece>> chunks(1);
