@@ -28,7 +28,8 @@ on a bounded sample, rank 0 at N=1) and `config5` (BASELINE configs[4]: a
 65 536 x 1 MiB 4+2 batch partitioned contiguously over the N ranks, encoded
 device-resident, at every N including 1) and `small_objects` (the reference
 README's 4 KB shape: 65 536 x 4 KiB objects, 8+3 and 4+2, Encode /
-Reconstruct / Verify, rank 0).
+Reconstruct / Verify, rank 0) and `config4` (BASELINE configs[3]: 8+3 over
+mixed 4 KiB / 1 MiB objects, one object-plan launch per op, rank 0).
 
 `--gpus N` without a launcher (WORLD_SIZE unset) starts N rank processes
 itself through torch.distributed.run, before this process touches the GPU;
@@ -390,6 +391,64 @@ def small_objects(n=65536, obj_len=4096, reps=100, settle=200):
     return out
 
 
+def config4(n=4096, reps=20, settle=40):
+    """BASELINE configs[3]: 8+3 Encode + Reconstruct{0,1,2} of n objects of
+    4 KiB or 1 MiB (p = 0.5 each, by the splitmix64 byte stream of the base
+    seed) in one launch per op through an object plan (data
+    arena + parity arena, hbec_plan_objects).  Algorithmic
+    bytes: (k+m)*S per object for Encode, (k+3)*S for Reconstruct.  Check:
+    the reconstruct rebuilds shards 0-2 in place from the parity the encode
+    wrote, and the data arena must come back byte for byte."""
+    k, m, miss = 8, 3, (0, 1, 2)
+    present = [0 if i in miss else 1 for i in range(k + m)]
+    flags = torch.empty((1, n), dtype=torch.uint8, device="cuda")
+    B.fill_splitmix(flags, n)
+    sizes = [MiB if int(b) & 1 else 4096 for b in flags.cpu()[0].tolist()]
+    enc = RS.New(k, m)
+    dl, pl, doff, poff = [], [], 0, 0
+    for size in sizes:
+        s = size // k
+        dl.append((doff, s))
+        pl.append(poff)
+        doff += k * s
+        poff += m * s
+    data = torch.empty(doff, dtype=torch.uint8, device="cuda")
+    parity = torch.empty(poff, dtype=torch.uint8, device="cuda")
+    B.fill_splitmix(data.view(1, -1), doff, first=7)
+    want = data.clone()
+    plan = B.StripePlan(enc, objects=[(data.data_ptr() + o, parity.data_ptr() + po, s)
+                                      for (o, s), po in zip(dl, pl)])
+    stream = torch.cuda.current_stream()
+    for _ in range(settle):
+        plan.encode()
+    ms = {}
+    for name, fn in (("encode", plan.encode), ("reconstruct", lambda: plan.reconstruct(present))):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            fn()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        ms[name] = e0.elapsed_time(e1) / reps
+    plan.encode()
+    data[:dl[0][1] * 3].zero_()  # erase shards 0-2 of object 0 for real before the rebuild
+    plan.reconstruct(present)
+    torch.cuda.synchronize()
+    ok = bool(torch.equal(data, want))
+    enc_bytes = sum((k + m) * s for _, s in dl)
+    rec_bytes = sum((k + len(miss)) * s for _, s in dl)
+    total_ms = ms["encode"] + ms["reconstruct"]
+    gbs = (enc_bytes + rec_bytes) / (total_ms * 1e-3) / 1e9
+    n_big = sum(1 for x in sizes if x == MiB)
+    del plan, data, parity, want
+    torch.cuda.empty_cache()
+    return {"workload": f"8+3 Encode + Reconstruct{{0,1,2}} of {n} objects, {n_big} x 1 MiB + {n - n_big} x 4 KiB "
+                        "(BASELINE configs[3]), object plan, one launch per op, device-resident",
+            "encode_ms": round(ms["encode"], 4), "reconstruct_ms": round(ms["reconstruct"], 4),
+            "bytes_per_step": enc_bytes + rec_bytes, "GB_s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
+            "parity_ok": ok, "parity_check": "in-place rebuild of shards 0-2 from the encoded parity equals the data"}
+
+
 def host_path(k, m, obj_len, n_obj=2048, passes=5, all_devices=False):
     """The path as the object server runs it: stripes (ecSplit databuf layout,
     ecutils.go:31-35) in pinned host memory from hbec_host_alloc, coded in
@@ -460,7 +519,8 @@ def parse_args(argv):
     ap.add_argument("--objects", type=int, default=4096, help="objects per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
-    ap.add_argument("--no-small", action="store_true", help="skip the README 4 KB shape leg (small_objects)")
+    ap.add_argument("--no-small", action="store_true",
+                    help="skip the README 4 KB shape leg (small_objects) and the config4 leg")
     ap.add_argument("--no-host-path", action="store_true",
                     help="skip the PCIe-inclusive host-path line (pinned stripes, zero-copy)")
     ap.add_argument("--config5-objects", type=int, default=65536,
@@ -645,6 +705,10 @@ def main(argv=None):
             line["small_objects"] = small_objects()
         except Exception as e:  # noqa: BLE001 - reported; never blocks the other ranks
             line["small_objects"] = {"error": f"{type(e).__name__}: {e}"[:200]}
+        try:
+            line["config4"] = config4()
+        except Exception as e:  # noqa: BLE001 - reported; never blocks the other ranks
+            line["config4"] = {"error": f"{type(e).__name__}: {e}"[:200]}
     if world > 1 and backend == "nccl" and args.split_objects > 0:
         split = batch_split(pg, k, m, obj_len, args.split_objects, world, rank, ctl_device)
         if rank == 0:

@@ -543,18 +543,48 @@ bool zero_copy_md5_enabled() {
 // With d_digest (device, n * n_shards * 16 B), also hash every input and
 // output shard of every stripe while it is in the device slot: digest of
 // shard i of stripe s at (s * n_shards + i) * 16.
+int host_run_on(Ring* ring, const hbec_stripe* stripes, uint64_t n, const std::vector<int>& in_idx,
+                const std::vector<int>& out_idx, const std::vector<uint8_t>& rows, uint8_t* d_digest,
+                int n_shards);
+
+// A call that fails part-way may leave work queued on the ring's streams
+// (slot copies, kernels writing a hash arena, hashes); the next caller of
+// the ring reuses slots only after their events, but starts over at hash
+// arena 0, so a failed call drains every stream before the ring goes back.
+void ring_drain(Ring* r) {
+    hipStream_t all[4 + Ring::kArenas] = {r->s_h2d, r->s_cmp, r->s_d2h};
+    int n = 3;
+    for (int a = 0; a < Ring::kArenas; ++a) all[n++] = r->s_md5[a];
+    for (int i = 0; i < n; ++i)
+        if (all[i]) (void)hipStreamSynchronize(all[i]);
+    (void)hipGetLastError();
+}
+
 int host_run(const hbec_stripe* stripes, uint64_t n, const std::vector<int>& in_idx,
              const std::vector<int>& out_idx, const std::vector<uint8_t>& rows, uint8_t* d_digest = nullptr,
              int n_shards = 0) {
-    const int K = (int)in_idx.size(), R = (int)out_idx.size();
-    if (R == 0 || n == 0) return HBEC_OK;
+    if (out_idx.empty() || n == 0) return HBEC_OK;
     Ring* ring = nullptr;
     int rc = ring_acquire(&ring);
     if (rc) return rc;
     struct Releaser {
         Ring* r;
-        ~Releaser() { ring_release(r); }
+        bool ok = false;
+        ~Releaser() {
+            if (!ok) ring_drain(r);
+            ring_release(r);
+        }
     } rel{ring};
+    rc = host_run_on(ring, stripes, n, in_idx, out_idx, rows, d_digest, n_shards);
+    rel.ok = rc == HBEC_OK;
+    return rc;
+}
+
+int host_run_on(Ring* ring, const hbec_stripe* stripes, uint64_t n, const std::vector<int>& in_idx,
+                const std::vector<int>& out_idx, const std::vector<uint8_t>& rows, uint8_t* d_digest,
+                int n_shards) {
+    const int K = (int)in_idx.size(), R = (int)out_idx.size();
+    int rc = HBEC_OK;
     // Pinned stripes are coded in place (zero-copy); the rest take the ring.
     // Hashing needs every shard on the device: when every stripe is pinned,
     // the zero-copy kernel also copies them to a device hash arena
