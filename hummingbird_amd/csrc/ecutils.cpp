@@ -503,6 +503,54 @@ int hbec_ec_glue(int k, int m, hbec_read_fn read, void* const* bodies, int chunk
     });
 }
 
+namespace {
+// rangeBytesWriter (ecobj.go:826-850): passes on the bytes after the first
+// start_offset, up to `length` of them, and reports every write as whole.
+struct RangeWriter {
+    hbec_write_fn write;
+    void* ctx;
+    int64_t start_offset, length;
+};
+
+int range_write(void* c, const uint8_t* buf, size_t n) {
+    RangeWriter& r = *static_cast<RangeWriter*>(c);
+    if (r.start_offset > (int64_t)n) {
+        r.start_offset -= (int64_t)n;
+        return 0;
+    }
+    if (r.length <= 0) return 0;
+    buf += r.start_offset;
+    n -= (size_t)r.start_offset;
+    r.start_offset = 0;
+    if ((int64_t)n > r.length) n = (size_t)r.length;
+    r.length -= (int64_t)n;
+    return n ? r.write(r.ctx, buf, n) : 0;
+}
+}  // namespace
+
+int hbec_ec_glue_range(int k, int m, hbec_read_fn read, void* const* bodies, int chunk_size, int64_t content_length,
+                       int64_t start, int64_t end, hbec_write_fn write, void* const* dsts, int n_dsts) {
+    return hbec::guarded("hbec_ec_glue_range", [&]() -> int {
+        if (k <= 0 || chunk_size <= 0 || n_dsts < 0 || (n_dsts > 0 && !dsts))
+            return fail(HBEC_ERR_INVALID_ARG, "ecGlue range: bad arguments");
+        if (start < 0 || end < start || end > content_length)
+            return fail(HBEC_ERR_INVALID_ARG, "ecGlue range: need 0 <= start <= end <= content length");
+        if (start == end) return HBEC_OK;
+        // object bytes of the covered stripes: [obj0, obj1)
+        const int64_t stripe = (int64_t)k * chunk_size;
+        const int64_t obj0 = start / stripe * stripe;
+        const int64_t obj1 = std::min<int64_t>(content_length, (end + stripe - 1) / stripe * stripe);
+        std::vector<RangeWriter> rw((size_t)n_dsts);
+        std::vector<void*> ctx((size_t)n_dsts, nullptr);
+        for (int j = 0; j < n_dsts; ++j) {
+            rw[j] = RangeWriter{write, dsts[j], start - obj0, end - start};
+            if (dsts[j]) ctx[j] = &rw[j];  // nil stays nil
+        }
+        return hbec_ec_glue(k, m, read, bodies, chunk_size, obj1 - obj0, write ? range_write : nullptr,
+                            ctx.data(), n_dsts);
+    });
+}
+
 int hbec_parse_ec_scheme(const char* scheme, char* algo, size_t algo_cap, int64_t* data_shards,
                          int64_t* parity_shards, int64_t* chunk_size) {
     return hbec::guarded("hbec_parse_ec_scheme", [&]() -> int {

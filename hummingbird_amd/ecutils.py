@@ -5,6 +5,8 @@
     ec_reconstruct(k, m, bodies, chunk_size, content_length,
                    dsts, dst_chunk_num)                        ecutils.go:74-132
     ec_glue(k, m, bodies, chunk_size, content_length, *dsts)   ecutils.go:134-186
+    ec_glue_range(k, m, bodies, chunk_size, content_length,
+                  start, end, *dsts)                           ecobj.go:207-267 (CopyRange)
     parse_ec_scheme(scheme)                                    ecobj.go:82-98
     range_chunk_align(start, end, chunk_size, k)               ecobj.go:814-824
 
@@ -95,6 +97,20 @@ def ec_glue(data_chunks, parity_chunks, bodies, chunk_size, content_length, *dst
         check(N.lib().hbec_ec_glue(int(data_chunks), int(parity_chunks), _read_cb, _ctx_array(b_ids),
                                    int(chunk_size), int(content_length), _write_cb, _ctx_array(d_ids),
                                    len(d_ids)))
+    finally:
+        for i in b_ids + d_ids:
+            _objs.pop(i, None)
+
+
+def ec_glue_range(data_chunks, parity_chunks, bodies, chunk_size, content_length, start, end, *dsts):
+    """Object bytes [start, end) (CopyRange, ecobj.go:207-267): bodies are the
+    shard streams from rangeChunkAlign's shardStart on."""
+    b_ids = _register(bodies)
+    d_ids = _register(dsts)
+    try:
+        check(N.lib().hbec_ec_glue_range(int(data_chunks), int(parity_chunks), _read_cb, _ctx_array(b_ids),
+                                         int(chunk_size), int(content_length), int(start), int(end), _write_cb,
+                                         _ctx_array(d_ids), len(d_ids)))
     finally:
         for i in b_ids + d_ids:
             _objs.pop(i, None)

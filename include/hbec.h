@@ -340,6 +340,21 @@ int hbec_ec_reconstruct(int data_shards, int parity_shards, hbec_read_fn read, v
 int hbec_ec_glue(int data_shards, int parity_shards, hbec_read_fn read, void* const* bodies, int chunk_size,
                  int64_t content_length, hbec_write_fn write, void* const* dsts, int n_dsts);
 
+/* Range GET decode (ecObject.CopyRange, ecobj.go:207-267): object bytes
+ * [start, end) of an object of content_length bytes.  The bodies are the k+m
+ * shard streams positioned at the first shard byte of the stripe holding
+ * `start` (rangeChunkAlign's shardStart, the ranged shard GETs of
+ * ecobj.go:241-257); the stripes covering [start, end) are glued as ecGlue
+ * does and each dst receives exactly bytes [start, end) through a
+ * rangeBytesWriter (ecobj.go:826-850).  The reference passes the glue a
+ * shard-byte length and a start offset modulo chunk_size rather than modulo
+ * k * chunk_size (ecobj.go:238-265); this entry uses the object-byte
+ * quantities, so it returns the requested bytes for every range.  Returns
+ * HBEC_ERR_INVALID_ARG unless 0 <= start <= end <= content_length. */
+int hbec_ec_glue_range(int data_shards, int parity_shards, hbec_read_fn read, void* const* bodies, int chunk_size,
+                       int64_t content_length, int64_t start, int64_t end, hbec_write_fn write, void* const* dsts,
+                       int n_dsts);
+
 /* parseECScheme (ecobj.go:82-98): "reedsolomon/<k>/<m>/<chunk>". */
 int hbec_parse_ec_scheme(const char* scheme, char* algo, size_t algo_cap, int64_t* data_shards,
                          int64_t* parity_shards, int64_t* chunk_size);

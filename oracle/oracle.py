@@ -387,6 +387,48 @@ def ec_glue(k, m, shard_files, chunk_size, content_length):
     return bytes(out)
 
 
+class RangeBytesWriter:
+    """rangeBytesWriter (objectserver/ecobj.go:826-850): keeps the bytes after
+    the first start_offset, at most `length` of them."""
+
+    def __init__(self, start_offset: int, length: int):
+        self.start_offset, self.length, self.out = start_offset, length, bytearray()
+
+    def write(self, b: bytes) -> int:
+        n = len(b)
+        if self.start_offset > n:
+            self.start_offset -= n
+            return n
+        if self.length <= 0:
+            return n
+        b = b[self.start_offset:]
+        self.start_offset = 0
+        if len(b) > self.length:
+            b = b[:self.length]
+        self.length -= len(b)
+        self.out += b
+        return n
+
+
+def ec_glue_range(k, m, shard_files, chunk_size, content_length, start, end):
+    """Range GET decode (ecObject.CopyRange, objectserver/ecobj.go:207-267) in
+    object-byte units: glue the stripes covering [start, end) from the shard
+    bytes at rangeChunkAlign's shardStart on, then keep [start, end) through a
+    RangeBytesWriter.  (The reference passes a shard-byte length and start %
+    chunk_size, ecobj.go:238-265; restated here with the object-byte
+    quantities those stand for.)"""
+    stripe = k * chunk_size
+    obj0 = start // stripe * stripe
+    obj1 = min(content_length, -(-end // stripe) * stripe)
+    shard_start, _ = range_chunk_align(start, end, chunk_size, k)
+    files = [None if f is None else f[shard_start:] for f in shard_files]
+    w = RangeBytesWriter(start - obj0, end - start)
+    body = ec_glue(k, m, files, chunk_size, obj1 - obj0)
+    for i in range(0, len(body), chunk_size):  # the glue writes shard-sized pieces
+        w.write(body[i:i + chunk_size])
+    return bytes(w.out)
+
+
 def parse_ec_scheme(scheme: str):
     """objectserver/ecobj.go:82-98."""
     sections = scheme.split("/")

@@ -212,3 +212,67 @@ def test_stripe_loops_random_against_oracle(k, m, chunk, length, lost):
     E.ec_reconstruct(k, m, [None if i in lost else io.BytesIO(files[i]) for i in range(k + m)], chunk, length,
                      dsts, list(lost))
     assert [d.value() for d in dsts] == [bytes(files[i]) for i in lost]
+
+
+def _range_bodies(files, k, chunk, start, end):
+    shard_start, _ = O.range_chunk_align(start, end, chunk, k)
+    return [None if f is None else io.BytesIO(f[shard_start:]) for f in files]
+
+
+@pytest.mark.parametrize("k,m,chunk,length", [(4, 2, 1024, 40_000), (8, 3, 4096, 300_001), (2, 1, 10, 80),
+                                              (10, 4, 1003, 51_234)])
+def test_glue_range_is_the_slice(k, m, chunk, length):
+    """CopyRange decode (hbec_ec_glue_range) returns object[start:end] from
+    ranged shard bodies, healthy and with m shards lost (GPU ReconstructData),
+    and agrees with the oracle's restatement."""
+    body = bytes(O.object_bytes(k * 13 + m, length))
+    files = O.ec_split(k, m, body, chunk)
+    rng = np.random.default_rng(length)
+    stripe = k * chunk
+    ranges = [(0, length), (0, 1), (length - 1, length), (stripe, 2 * stripe), (stripe - 1, stripe + 1), (3, 3)]
+    ranges += [tuple(int(x) for x in sorted(rng.integers(0, length + 1, 2))) for _ in range(12)]
+    for start, end in ranges:
+        for lose in (False, True):
+            fs = list(files)
+            if lose:
+                for i in rng.choice(k + m, m, replace=False):
+                    fs[i] = None
+            out = Rec()
+            E.ec_glue_range(k, m, _range_bodies(fs, k, chunk, start, end), chunk, length, start, end, out)
+            assert out.value() == body[start:end]
+            assert out.value() == O.ec_glue_range(k, m, fs, chunk, length, start, end)
+
+
+def test_glue_range_reference_writer_kats(kats):
+    """TestRangeBytesWriter's vectors (ecobj_test.go:332-358) through the
+    library: a 1+1 object "THIS IS A TEST" glued with chunk sizes 1..19 (the
+    writer sees pieces of that size, as io.CopyBuffer's buffer)."""
+    rb = kats["range_bytes_writer"]
+    data = rb["data"].encode()
+    for chunk in rb["buffer_sizes"]:
+        files = O.ec_split(1, 1, data, chunk)
+        for off, length, want in rb["cases"]:
+            out = Rec()
+            E.ec_glue_range(1, 1, _range_bodies(files, 1, chunk, off, off + length), chunk, len(data), off,
+                            off + length, out)
+            assert out.value() == want.encode()
+            if chunk > 1:
+                assert all(len(c) <= chunk for c in out.calls)
+
+
+def test_glue_range_arguments_and_writers():
+    k, m, chunk, length = 4, 2, 100, 2_000
+    body = bytes(O.object_bytes(3, length))
+    files = O.ec_split(k, m, body, chunk)
+    for start, end in ((5, 4), (-1, 3), (0, length + 1)):
+        with pytest.raises(RS.ErrInvalidArg):
+            E.ec_glue_range(k, m, _range_bodies(files, k, chunk, 0, 1), chunk, length, start, end, Rec())
+
+    class Broken:
+        def write(self, b):
+            raise IOError("client went away")
+
+    good = Rec()
+    E.ec_glue_range(k, m, _range_bodies(files, k, chunk, 450, 1750), chunk, length, 450, 1750, Broken(), None,
+                    good)
+    assert good.value() == body[450:1750]  # a failing or nil writer does not stop the others

@@ -270,3 +270,36 @@ def test_auditor_size_rule_product_host(kats):
         _, ds, _, _ = E.parse_ec_scheme(c["ec_scheme"])
         size_ok = E.ec_shard_length(int(c["content_length"]), ds) == len(c["body"])
         assert size_ok == (c["test"] != "TestAuditShardFailLength"), c["test"]
+
+
+def test_range_bytes_writer_kats(kats):
+    """rangeBytesWriter restated (oracle) against the reference's own
+    TestRangeBytesWriter vectors, for every copy-buffer size it uses."""
+    rb = kats["range_bytes_writer"]
+    data = rb["data"].encode()
+    for bs in rb["buffer_sizes"]:
+        for off, length, want in rb["cases"]:
+            w = O.RangeBytesWriter(off, length)
+            for i in range(0, len(data), bs):
+                assert w.write(data[i:i + bs]) == len(data[i:i + bs])
+            assert bytes(w.out) == want.encode()
+
+
+@pytest.mark.parametrize("k,m,chunk,length", [(4, 2, 100, 3_001), (3, 2, 10, 95), (2, 1, 10, 80), (8, 3, 64, 5_000)])
+def test_oracle_ec_glue_range_is_the_slice(k, m, chunk, length):
+    """The oracle's range decode returns object[start:end] for every range
+    shape: inside one stripe, across stripes, on stripe boundaries, the
+    object's tail, empty; also with m shard files lost."""
+    body = bytes(O.object_bytes(k * 7 + m, length))
+    files = O.ec_split(k, m, body, chunk)
+    rng = np.random.default_rng(k + m + length)
+    stripe = k * chunk
+    ranges = [(0, length), (0, 1), (length - 1, length), (stripe, 2 * stripe), (stripe - 1, stripe + 1), (5, 5)]
+    ranges += [tuple(sorted(rng.integers(0, length + 1, 2))) for _ in range(40)]
+    for start, end in ranges:
+        start, end = int(start), int(min(end, length))
+        assert O.ec_glue_range(k, m, files, chunk, length, start, end) == body[start:end]
+        lost = list(files)
+        for i in rng.choice(k + m, m, replace=False):
+            lost[i] = None
+        assert O.ec_glue_range(k, m, lost, chunk, length, start, end) == body[start:end]
