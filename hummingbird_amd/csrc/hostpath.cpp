@@ -362,6 +362,20 @@ int zero_copy_blocks_per_cu() {
     return v;
 }
 
+// Grid cap of the zero-copy stripes kernel (HBEC_ZC_GRID blocks, 0 = CUs x
+// blocks per CU).  64 blocks of 4 waves keep ~1 MiB of PCIe reads in flight,
+// plenty for the link, where the whole chip (512 blocks) kept ~8 MiB queued
+// and streamed slower: 4096 x 1 MiB 4+2 pinned stripes 48.4-48.8 -> 52.2-52.5
+// GiB/s, 4 KiB stripes 42.2 -> 45.1 GiB/s; 32 and 128 blocks tie with 64
+// (profiles/r02_zc_grid.jsonl).
+int zero_copy_max_blocks() {
+    static const int v = [] {
+        const char* e = std::getenv("HBEC_ZC_GRID");
+        return e ? std::max(0, std::atoi(e)) : 64;
+    }();
+    return v;
+}
+
 bool zero_copy_enabled() {
     static const bool on = [] {
         const char* e = std::getenv("HBEC_ZEROCOPY");
@@ -452,7 +466,7 @@ int zero_copy_run(Ring* ring, const std::vector<ZcStripe>& zs, const std::vector
                            ring->s_cmp);
         if (e != hipSuccess) return hip_fail(e, "zero-copy records H2D");
         int rc = hbec::launch_stripe_passes(ring->dev_tiles[slot], nt, in_idx, out_idx, rows, 0, ring->s_cmp,
-                                            zero_copy_blocks_per_cu());
+                                            zero_copy_blocks_per_cu(), false, zero_copy_max_blocks());
         if (rc) return rc;
         e = hipEventRecord(ring->ev_cmp[slot], ring->s_cmp);
         if (e != hipSuccess) return hip_fail(e, "zero-copy event");
@@ -517,7 +531,7 @@ int zero_copy_md5_run(Ring* ring, const std::vector<ZcStripe>& zs, const std::ve
                            ring->s_cmp);
         if (e != hipSuccess) return hip_fail(e, "zero-copy records H2D");
         rc = hbec::launch_stripe_passes(ring->dev_tiles[slot], nt, in_idx, out_idx, rows, 0, ring->s_cmp,
-                                        zero_copy_blocks_per_cu(), true);
+                                        zero_copy_blocks_per_cu(), true, zero_copy_max_blocks());
         if (rc) return rc;
         e = hipEventRecord(ring->ev_cmp[slot], ring->s_cmp);
         if (e != hipSuccess) return hip_fail(e, "zero-copy event");

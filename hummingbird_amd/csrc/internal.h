@@ -69,13 +69,14 @@ struct TileRec;
 // Grid for a stripes launch of k inputs / r outputs over n_tiles records
 // (one block of 4 waves per CU at most, as the strided kernels).
 // blocks_per_cu > 0 overrides the HBM sweet spot (1 block per CU).
-int stripes_grid(int k, int r, uint64_t n_tiles, int* grid, int blocks_per_cu = 0);
+int stripes_grid(int k, int r, uint64_t n_tiles, int* grid, int blocks_per_cu = 0, int max_blocks = 0);
 // out (^)= rows x in over tile records, in launches of <= 3 outputs and
 // <= 8 inputs (k > 8: accumulate passes).  sel_k > 0: object-plan bases.
 // mirror: code in place at each record's in_addr and copy every input and
 // output column to the device arena at out_addr (StripeArgs::mirror).
+// max_blocks > 0 caps the grid (zero-copy launches over PCIe).
 int launch_stripe_passes(const TileRec* tiles, uint64_t n_tiles, const std::vector<int>& in_idx,
                          const std::vector<int>& out_idx, const std::vector<uint8_t>& rows, int sel_k,
-                         hipStream_t stream, int blocks_per_cu = 0, bool mirror = false);
+                         hipStream_t stream, int blocks_per_cu = 0, bool mirror = false, int max_blocks = 0);
 
 }  // namespace hbec

@@ -57,7 +57,7 @@ std::mutex g_occ_mu;
 
 }  // namespace
 
-int hbec::stripes_grid(int k, int r, uint64_t n_tiles, int* grid, int blocks_per_cu) {
+int hbec::stripes_grid(int k, int r, uint64_t n_tiles, int* grid, int blocks_per_cu, int max_blocks) {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
@@ -87,7 +87,8 @@ int hbec::stripes_grid(int k, int r, uint64_t n_tiles, int* grid, int blocks_per
         if (hbec::stripes_occupancy(k, r, &fit) != hipSuccess) fit = 1;
         bpc = std::max(1, std::min(fit, blocks_per_cu));
     }
-    const uint64_t cap = (uint64_t)cus[dev] * (uint64_t)bpc;
+    uint64_t cap = (uint64_t)cus[dev] * (uint64_t)bpc;
+    if (max_blocks > 0) cap = std::min<uint64_t>(cap, (uint64_t)max_blocks);
     *grid = (int)std::max<uint64_t>(1, std::min(want, cap));
     return HBEC_OK;
 }
@@ -98,7 +99,7 @@ int hbec::stripes_grid(int k, int r, uint64_t n_tiles, int* grid, int blocks_per
 // marks an object plan (split bases: shard indices >= sel_k are parity).
 int hbec::launch_stripe_passes(const TileRec* tiles, uint64_t n_tiles, const std::vector<int>& in_idx,
                                const std::vector<int>& out_idx, const std::vector<uint8_t>& rows, int sel_k,
-                               hipStream_t stream, int blocks_per_cu, bool mirror) {
+                               hipStream_t stream, int blocks_per_cu, bool mirror, int max_blocks) {
     const int K_all = (int)in_idx.size(), R_all = (int)out_idx.size();
     if (n_tiles == 0 || R_all == 0) return HBEC_OK;
     if (sel_k > 0 && K_all > kStripeMaxK) return fail(HBEC_ERR_INVALID_ARG, "object plans take <= 8 inputs per pass");
@@ -130,7 +131,7 @@ int hbec::launch_stripe_passes(const TileRec* tiles, uint64_t n_tiles, const std
                 for (int j = 0; j < K; ++j) perm_table(rows[(size_t)(r0 + r) * K_all + c0 + j], a.tab[r][j]);
             }
             int grid = 0;
-            int rc = stripes_grid(K, R, n_tiles, &grid, blocks_per_cu);
+            int rc = stripes_grid(K, R, n_tiles, &grid, blocks_per_cu, max_blocks);
             if (rc) return rc;
             hipError_t e = launch_stripes(K, R, a, grid, stream);
             if (e != hipSuccess) return hip_fail(e, "launch gf_apply_stripes");
