@@ -52,6 +52,12 @@ int hip_fail(hipError_t e, const char* what) {
 }
 
 static std::atomic<int> g_force_stream{0};
+// Views that are not all 16-B aligned (or shards not a multiple of 16 B):
+// gf_apply_unaligned (default) or, with HBEC_UNALIGNED=0, the byte kernel.
+static const std::atomic<int> g_unaligned_kernel{[] {
+    const char* e = std::getenv("HBEC_UNALIGNED");
+    return e ? std::atoi(e) : 1;
+}()};
 // Tuning knob: cap on resident blocks per CU used to size vec-kernel grids
 // (0 = the occupancy the compiler's register allocation allows).
 static const int g_blocks_per_cu_override = [] {
@@ -108,12 +114,14 @@ static int device_blocks(int dev, int k, int r, int pipe, int force_stream, int*
         if (e != hipSuccess) return hip_fail(e, "hipGetDeviceProperties");
         d.cus = p.multiProcessorCount;
     }
-    // pipe: 1 = pipelined kernel, 2 = packed kernel (short shards)
-    const int key_k = force_stream ? -k : (pipe == 2 ? 2000 + k : (pipe ? 1000 + k : k));
+    // pipe: 1 = pipelined kernel, 2 = packed kernel (short shards), 3 = unaligned kernel
+    const int key_k = pipe == 3 ? 3000 : (force_stream ? -k : (pipe == 2 ? 2000 + k : (pipe ? 1000 + k : k)));
     auto it = d.blocks_per_cu.find({key_k, r});
     if (it == d.blocks_per_cu.end()) {
         int b = 0;
-        hipError_t e = pipe == 2 ? packed_occupancy(k, r, &b) : vec_occupancy(k, r, pipe, force_stream, &b);
+        hipError_t e = pipe == 3   ? unaligned_occupancy(r, &b)
+                       : pipe == 2 ? packed_occupancy(k, r, &b)
+                                   : vec_occupancy(k, r, pipe, force_stream, &b);
         if (e != hipSuccess) return hip_fail(e, "occupancy query");
         if (b < 1) b = 1;
         it = d.blocks_per_cu.emplace(std::make_pair(key_k, r), b).first;
@@ -215,6 +223,27 @@ int apply_views(int rows, int cols, const uint8_t* coeffs, const hbec_view* in, 
                     if (g_grid_cap > 0) grid = std::min(grid, g_grid_cap);
                     hipError_t e = launch_vec(K, R, b, grid, stream, force_stream);
                     if (e != hipSuccess) return hip_fail(e, "launch gf_apply_vec");
+                }
+            } else if (g_unaligned_kernel.load()) {
+                // any alignment: aligned 16-B accesses with in-register shifts (gf_apply_unaligned)
+                int cus = 0, per_cu = 0;
+                rc = device_blocks(dev, K, R, 3, 0, &cus, &per_cu);
+                if (rc) return rc;
+                const uint64_t tpo = unaligned_tiles_per_obj(shard_len);
+                const uint64_t max_obj = std::max<uint64_t>(1, std::min<uint64_t>((1ull << 31), g_chunk_tiles) / tpo);
+                for (uint64_t o0 = 0; o0 < n_obj; o0 += max_obj) {
+                    const uint64_t no = std::min(max_obj, n_obj - o0);
+                    PassArgs b = a;
+                    for (int j = 0; j < K; ++j) b.in[j] = a.in[j] + o0 * a.in_stride[j];
+                    for (int r = 0; r < R; ++r) b.out[r] = a.out[r] + o0 * a.out_stride[r];
+                    b.n_obj = no;
+                    b.tiles_per_obj = (uint32_t)tpo;
+                    b.n_tiles = (uint32_t)(no * tpo);
+                    const uint64_t want_blocks = (b.n_tiles + kBlockThreads / 64 - 1) / (kBlockThreads / 64);
+                    int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want_blocks, (uint64_t)cus * per_cu));
+                    if (g_grid_cap > 0) grid = std::min(grid, g_grid_cap);
+                    hipError_t e = launch_unaligned(K, R, b, grid, stream);
+                    if (e != hipSuccess) return hip_fail(e, "launch gf_apply_unaligned");
                 }
             } else {
                 a.n_obj = n_obj;

@@ -98,6 +98,11 @@ __host__ __device__ constexpr int verify_u(int k) {
 
 hipError_t launch_vec(int k, int r, const PassArgs& a, int grid, hipStream_t stream, int force_stream);
 hipError_t launch_bytes(int k, int r, const PassArgs& a, int grid, hipStream_t stream);
+// Any alignment / stride / length with aligned 16-B accesses (gf_apply_unaligned):
+// wave tiles of 4 windows x 1008 B of one object's shard column.
+uint32_t unaligned_tiles_per_obj(uint64_t shard_len);
+hipError_t launch_unaligned(int k, int r, const PassArgs& a, int grid, hipStream_t stream);
+hipError_t unaligned_occupancy(int r, int* blocks_per_cu);
 hipError_t launch_fill(uint8_t* dst, uint64_t n_obj, uint64_t obj_len, uint64_t obj_stride, uint64_t base_seed,
                        uint64_t first, int grid, hipStream_t stream);
 hipError_t vec_occupancy(int k, int r, int pipe, int force_stream, int* blocks_per_cu);

@@ -590,6 +590,179 @@ __global__ __launch_bounds__(kBlockThreads) void gf_apply_bytes(PassArgs a, int 
     }
 }
 
+// ---------------------------------------------------------------------------
+// gf_apply_unaligned: any base alignment, any stride, any shard length.  ecSplit
+// sets S = ceil(len / k) (ecutils.go:14-24), so S is a multiple of 16 for only
+// 1 object size in 16, and its databuf puts shard i at i*S (ecutils.go:31-35):
+// an arbitrary object's shards start at arbitrary byte offsets.  The byte
+// kernel above codes them at ~20 % of HBM; this one keeps 16-B accesses, and
+// every access is 16-B ALIGNED:
+//  * input j of an object starts d_j = base & 15 bytes into an aligned block
+//    (d_j is wave-uniform: one object per wave tile).  A lane loads the two
+//    aligned blocks that cover its 16-B column and shifts the column out of
+//    them (v_alignbyte_b32).  Loads are clamped to the shard's last aligned
+//    block, so they stay inside blocks that hold shard bytes; clamped bytes
+//    feed only positions >= S, which are never stored.
+//  * output r's aligned blocks start at shard positions = e_r (mod 16),
+//    e_r = -base & 15.  Lane l stores the block [c_l + e_r, c_l + e_r + 16):
+//    the high bytes of its own column and the low bytes of lane l+1's
+//    (ds_bpermute).  So a window of 64 computed columns (1 KiB) stores 63
+//    blocks, and windows step 1008 B.  The shard head [0, e_r) is stored
+//    bytewise by lane 0 of window 0, and a block crossing the shard end
+//    bytewise by its lane.
+// Accumulate passes (inputs beyond kMaxK) read the old output the same way
+// as an input.  A window reads output bytes another window stores only in
+// the e_r bytes it does not use itself, so the passes are race-free.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kUnalignedWindow = 1008;  // stored bytes per 64-lane window (63 blocks)
+constexpr int kUnalignedU = 4;               // windows per wave tile (loads in flight)
+
+// bytes [d, d + 16) of the 32 bytes lo:hi, d wave-uniform in [0, 16)
+__device__ __forceinline__ u32x4 realign16(const u32x4& lo, const u32x4& hi, uint32_t d) {
+    const uint32_t sh = d & 3u;
+    uint32_t s0, s1, s2, s3, s4;
+    switch (d >> 2) {
+        case 0: s0 = lo[0]; s1 = lo[1]; s2 = lo[2]; s3 = lo[3]; s4 = hi[0]; break;
+        case 1: s0 = lo[1]; s1 = lo[2]; s2 = lo[3]; s3 = hi[0]; s4 = hi[1]; break;
+        case 2: s0 = lo[2]; s1 = lo[3]; s2 = hi[0]; s3 = hi[1]; s4 = hi[2]; break;
+        default: s0 = lo[3]; s1 = hi[0]; s2 = hi[1]; s3 = hi[2]; s4 = hi[3]; break;
+    }
+    // v_alignbyte_b32(a, b, s) = ({a, b} >> 8s)[31:0]
+    return u32x4{__builtin_amdgcn_alignbyte(s1, s0, sh), __builtin_amdgcn_alignbyte(s2, s1, sh),
+                 __builtin_amdgcn_alignbyte(s3, s2, sh), __builtin_amdgcn_alignbyte(s4, s3, sh)};
+}
+
+// A view of one object's shard: aligned base, misalignment, last aligned block.
+struct UView {
+    uint64_t abase;  // base & ~15
+    uint64_t last;   // (base + S - 1) & ~15
+    uint32_t d;      // base & 15 (wave-uniform)
+};
+
+__device__ __forceinline__ UView uview(const uint8_t* p, uint64_t stride, uint32_t obj, uint64_t s) {
+    const uint64_t b = reinterpret_cast<uint64_t>(p) + (uint64_t)obj * stride;
+    UView v;
+    v.abase = b & ~(uint64_t)15;
+    v.last = (b + s - 1u) & ~(uint64_t)15;
+    v.d = __builtin_amdgcn_readfirstlane((uint32_t)(b & 15u));
+    return v;
+}
+
+__device__ __forceinline__ void uload(u32x4& lo, u32x4& hi, const UView& v, uint64_t col) {
+    const uint64_t x = v.abase + col, y = x + 16u;
+    lo = ld16_addr(x < v.last ? x : v.last);
+    hi = ld16_addr(y < v.last ? y : v.last);
+}
+
+__device__ __forceinline__ void store_bytes(uint64_t addr, const u32x4& v, uint64_t n) {
+    uint8_t* p = reinterpret_cast<uint8_t*>(addr);
+#pragma unroll
+    for (int b = 0; b < 16; ++b)
+        if ((uint64_t)b < n) p[b] = (uint8_t)(v[b >> 2] >> (8 * (b & 3)));
+}
+
+template <int R>
+__global__ __launch_bounds__(kBlockThreads) void gf_apply_unaligned(PassArgs a, int K) {
+    constexpr int U = kUnalignedU;
+    constexpr uint32_t W = kUnalignedWindow;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave =
+        __builtin_amdgcn_readfirstlane(xcd_block() * (kBlockThreads / 64) + (threadIdx.x >> 6));
+    const uint32_t nwaves = gridDim.x * (kBlockThreads / 64);
+    const uint32_t tpo = a.tiles_per_obj;
+    const uint64_t S = a.shard_len;
+    for (uint32_t t = wave; t < a.n_tiles; t += nwaves) {
+        const uint32_t obj = t / tpo;
+        const uint64_t p0 = (uint64_t)(t - obj * tpo) * (U * W);  // first window's shard position
+        uint64_t col[U];
+        bool live[U];  // window-uniform
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            col[u] = p0 + (uint64_t)u * W + lane * 16u;
+            live[u] = p0 + (uint64_t)u * W < S;
+        }
+        u32x4 acc[R][U];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const UView ov = uview(a.out[r], a.out_stride[r], obj, S);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                acc[r][u] = u32x4{0, 0, 0, 0};
+                if (a.accumulate && live[u]) {
+                    u32x4 lo, hi;
+                    uload(lo, hi, ov, col[u]);
+                    acc[r][u] = realign16(lo, hi, ov.d);
+                }
+            }
+        }
+        u32x4 clo[U], chi[U];
+        UView cv = uview(a.in[0], a.in_stride[0], obj, S);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            clo[u] = chi[u] = u32x4{0, 0, 0, 0};
+            if (live[u]) uload(clo[u], chi[u], cv, col[u]);
+        }
+#pragma unroll 1
+        for (int j = 0; j < K; ++j) {
+            u32x4 nlo[U], nhi[U];
+            UView nv = cv;
+            if (j + 1 < K) {
+                nv = uview(a.in[j + 1], a.in_stride[j + 1], obj, S);
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    nlo[u] = nhi[u] = u32x4{0, 0, 0, 0};
+                    if (live[u]) uload(nlo[u], nhi[u], nv, col[u]);
+                }
+            }
+            uint32_t tb[R][5];
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+#pragma unroll
+                for (int q = 0; q < 5; ++q) tb[r][q] = a.tab[r][j][q];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const u32x4 x = realign16(clo[u], chi[u], cv.d);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const Sel sx = selectors(x[e]);
+#pragma unroll
+                    for (int r = 0; r < R; ++r)
+                        acc[r][u][e] ^= gf_mul_sel(sx, tb[r][0], tb[r][1], tb[r][2], tb[r][3], tb[r][4]);
+                }
+            }
+            if (j + 1 < K) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    clo[u] = nlo[u];
+                    chi[u] = nhi[u];
+                }
+                cv = nv;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint64_t ob = reinterpret_cast<uint64_t>(a.out[r]) + (uint64_t)obj * a.out_stride[r];
+            const uint32_t e = __builtin_amdgcn_readfirstlane((16u - (uint32_t)(ob & 15u)) & 15u);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (!live[u]) continue;  // window-uniform: every lane takes part in the shuffle
+                u32x4 nb;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) nb[i] = __shfl_down(acc[r][u][i], 1u, 64);
+                const u32x4 blk = realign16(acc[r][u], nb, e);
+                const uint64_t q = col[u] + e;  // block start (shard position); ob + q is 16-B aligned
+                if (lane < 63u && q < S) {
+                    if (q + 16u <= S)
+                        st16_addr(ob + q, blk);
+                    else
+                        store_bytes(ob + q, blk, S - q);
+                }
+                if (lane == 0u && col[u] == 0u && e > 0u) store_bytes(ob, acc[r][u], e < S ? e : S);  // head
+            }
+        }
+    }
+}
+
 // Synthetic objects: object i's bytes are the little-endian
 // splitmix64 stream seeded with base_seed ^ (i * golden).  splitmix64 is
 // counter based, so each 8-byte word is computed independently.
@@ -793,6 +966,34 @@ hipError_t launch_vec(int k, int r, const PassArgs& a, int grid, hipStream_t str
 hipError_t launch_bytes(int k, int r, const PassArgs& a, int grid, hipStream_t stream) {
     hipLaunchKernelGGL(gf_apply_bytes, dim3(grid), dim3(kBlockThreads), 0, stream, a, k, r);
     return hipGetLastError();
+}
+
+static const void* unaligned_kernel(int r) {
+    switch (r) {
+        case 1: return reinterpret_cast<const void*>(&gf_apply_unaligned<1>);
+        case 2: return reinterpret_cast<const void*>(&gf_apply_unaligned<2>);
+        case 3: return reinterpret_cast<const void*>(&gf_apply_unaligned<3>);
+        case 4: return reinterpret_cast<const void*>(&gf_apply_unaligned<4>);
+    }
+    return nullptr;
+}
+
+uint32_t unaligned_tiles_per_obj(uint64_t shard_len) {
+    const uint64_t windows = (shard_len + kUnalignedWindow - 1) / kUnalignedWindow;
+    return (uint32_t)((windows + kUnalignedU - 1) / kUnalignedU);
+}
+
+hipError_t launch_unaligned(int k, int r, const PassArgs& a, int grid, hipStream_t stream) {
+    const void* fn = unaligned_kernel(r);
+    if (!fn || k < 1 || k > kMaxK) return hipErrorInvalidValue;
+    void* args[] = {const_cast<PassArgs*>(&a), &k};
+    return hipLaunchKernel(fn, dim3(grid), dim3(kBlockThreads), args, 0, stream);
+}
+
+hipError_t unaligned_occupancy(int r, int* blocks_per_cu) {
+    const void* fn = unaligned_kernel(r);
+    if (!fn) return hipErrorInvalidValue;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, kBlockThreads, 0);
 }
 
 hipError_t launch_fill(uint8_t* dst, uint64_t n_obj, uint64_t obj_len, uint64_t obj_stride, uint64_t base_seed,
