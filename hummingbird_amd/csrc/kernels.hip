@@ -614,14 +614,35 @@ __global__ __launch_bounds__(kBlockThreads) void gf_apply_bytes(PassArgs a, int 
 // as an input.  A window reads output bytes another window stores only in
 // the e_r bytes it does not use itself, so the passes are race-free.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kUnalignedWindow = 1008;  // stored bytes per 64-lane window (63 blocks)
-constexpr int kUnalignedU = 4;               // windows per wave tile (loads in flight)
+#ifndef HBEC_UNALIGNED_U
+#define HBEC_UNALIGNED_U 2  // u2 ~ u4 > u8 (profiles/r02_tune_unaligned.jsonl)
+#endif
+#ifndef HBEC_REALIGN_SEL
+#define HBEC_REALIGN_SEL 1  // 1: select the 5 source dwords with v_cndmask; 0: a uniform switch
+#endif
+#ifndef HBEC_UNALIGNED_SHFL
+#define HBEC_UNALIGNED_SHFL 0  // 1: one load per input column, the upper block from lane l+1 (62 blocks/window)
+#endif
+// stored bytes per 64-lane window: 63 blocks (two loads per column), or 62
+// when the upper block comes from the next lane (lane 63's column is partial)
+constexpr uint32_t kUnalignedWindow = HBEC_UNALIGNED_SHFL ? 992 : 1008;
+constexpr uint32_t kUnalignedStoreLanes = HBEC_UNALIGNED_SHFL ? 62 : 63;
+constexpr int kUnalignedU = HBEC_UNALIGNED_U;  // windows per wave tile (loads in flight)
 
 // bytes [d, d + 16) of the 32 bytes lo:hi, d wave-uniform in [0, 16)
 __device__ __forceinline__ u32x4 realign16(const u32x4& lo, const u32x4& hi, uint32_t d) {
     const uint32_t sh = d & 3u;
     uint32_t s0, s1, s2, s3, s4;
-    switch (d >> 2) {
+    if (HBEC_REALIGN_SEL) {
+        const bool b2 = (d & 8u) != 0, b1 = (d & 4u) != 0;
+        const uint32_t t0 = b2 ? lo[2] : lo[0], t1 = b2 ? lo[3] : lo[1], t2 = b2 ? hi[0] : lo[2];
+        const uint32_t t3 = b2 ? hi[1] : lo[3], t4 = b2 ? hi[2] : hi[0], t5 = b2 ? hi[3] : hi[1];
+        s0 = b1 ? t1 : t0;
+        s1 = b1 ? t2 : t1;
+        s2 = b1 ? t3 : t2;
+        s3 = b1 ? t4 : t3;
+        s4 = b1 ? t5 : t4;
+    } else switch (d >> 2) {
         case 0: s0 = lo[0]; s1 = lo[1]; s2 = lo[2]; s3 = lo[3]; s4 = hi[0]; break;
         case 1: s0 = lo[1]; s1 = lo[2]; s2 = lo[3]; s3 = hi[0]; s4 = hi[1]; break;
         case 2: s0 = lo[2]; s1 = lo[3]; s2 = hi[0]; s3 = hi[1]; s4 = hi[2]; break;
@@ -649,13 +670,29 @@ __device__ __forceinline__ UView uview(const uint8_t* p, uint64_t stride, uint32
 }
 
 __device__ __forceinline__ void uload(u32x4& lo, u32x4& hi, const UView& v, uint64_t col) {
-    const uint64_t x = v.abase + col, y = x + 16u;
+    const uint64_t x = v.abase + col;
     lo = ld16_addr(x < v.last ? x : v.last);
-    hi = ld16_addr(y < v.last ? y : v.last);
+    if (HBEC_UNALIGNED_SHFL) {
+        hi = lo;  // replaced by lane l+1's block at use (ushift)
+    } else {
+        const uint64_t y = x + 16u;
+        hi = ld16_addr(y < v.last ? y : v.last);
+    }
 }
 
+// the column's upper block: loaded (two-load form) or lane l+1's lower block
+__device__ __forceinline__ u32x4 upper(const u32x4& lo, const u32x4& hi) {
+    if (!HBEC_UNALIGNED_SHFL) return hi;
+    u32x4 h;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) h[i] = __shfl_down(lo[i], 1u, 64);
+    return h;
+}
+
+typedef __attribute__((address_space(1))) uint8_t gu8;
+
 __device__ __forceinline__ void store_bytes(uint64_t addr, const u32x4& v, uint64_t n) {
-    uint8_t* p = reinterpret_cast<uint8_t*>(addr);
+    gu8* p = reinterpret_cast<gu8*>(addr);  // global, not flat: flat stores also count in lgkmcnt
 #pragma unroll
     for (int b = 0; b < 16; ++b)
         if ((uint64_t)b < n) p[b] = (uint8_t)(v[b >> 2] >> (8 * (b & 3)));
@@ -688,20 +725,17 @@ __global__ __launch_bounds__(kBlockThreads) void gf_apply_unaligned(PassArgs a, 
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 acc[r][u] = u32x4{0, 0, 0, 0};
-                if (a.accumulate && live[u]) {
+                if (a.accumulate) {  // kernel-uniform; clamped loads need no per-window branch
                     u32x4 lo, hi;
                     uload(lo, hi, ov, col[u]);
-                    acc[r][u] = realign16(lo, hi, ov.d);
+                    acc[r][u] = realign16(lo, upper(lo, hi), ov.d);
                 }
             }
         }
         u32x4 clo[U], chi[U];
         UView cv = uview(a.in[0], a.in_stride[0], obj, S);
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            clo[u] = chi[u] = u32x4{0, 0, 0, 0};
-            if (live[u]) uload(clo[u], chi[u], cv, col[u]);
-        }
+        for (int u = 0; u < U; ++u) uload(clo[u], chi[u], cv, col[u]);  // clamped: no branch
 #pragma unroll 1
         for (int j = 0; j < K; ++j) {
             u32x4 nlo[U], nhi[U];
@@ -709,10 +743,7 @@ __global__ __launch_bounds__(kBlockThreads) void gf_apply_unaligned(PassArgs a, 
             if (j + 1 < K) {
                 nv = uview(a.in[j + 1], a.in_stride[j + 1], obj, S);
 #pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    nlo[u] = nhi[u] = u32x4{0, 0, 0, 0};
-                    if (live[u]) uload(nlo[u], nhi[u], nv, col[u]);
-                }
+                for (int u = 0; u < U; ++u) uload(nlo[u], nhi[u], nv, col[u]);
             }
             uint32_t tb[R][5];
 #pragma unroll
@@ -721,7 +752,7 @@ __global__ __launch_bounds__(kBlockThreads) void gf_apply_unaligned(PassArgs a, 
                 for (int q = 0; q < 5; ++q) tb[r][q] = a.tab[r][j][q];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const u32x4 x = realign16(clo[u], chi[u], cv.d);
+                const u32x4 x = realign16(clo[u], upper(clo[u], chi[u]), cv.d);
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const Sel sx = selectors(x[e]);
@@ -751,7 +782,7 @@ __global__ __launch_bounds__(kBlockThreads) void gf_apply_unaligned(PassArgs a, 
                 for (int i = 0; i < 4; ++i) nb[i] = __shfl_down(acc[r][u][i], 1u, 64);
                 const u32x4 blk = realign16(acc[r][u], nb, e);
                 const uint64_t q = col[u] + e;  // block start (shard position); ob + q is 16-B aligned
-                if (lane < 63u && q < S) {
+                if (lane < kUnalignedStoreLanes && q < S) {
                     if (q + 16u <= S)
                         st16_addr(ob + q, blk);
                     else
