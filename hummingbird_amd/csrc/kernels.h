@@ -103,6 +103,27 @@ hipError_t launch_bytes(int k, int r, const PassArgs& a, int grid, hipStream_t s
 uint32_t unaligned_tiles_per_obj(uint64_t shard_len);
 hipError_t launch_unaligned(int k, int r, const PassArgs& a, int grid, hipStream_t stream);
 hipError_t unaligned_occupancy(int r, int* blocks_per_cu);
+// Unaligned plans (stripes / objects at any alignment, mixed lengths): one
+// record per wave tile of unaligned_tile_bytes() stored bytes of a stripe.
+// Input j of the tile's stripe starts at (bit j of in_sel ? b : a) +
+// in_idx[j] * shard_len; output r likewise with out_sel / out_idx.
+struct URec {
+    uint64_t a;          // stripe base (ecSplit databuf) or object data base
+    uint64_t b;          // object parity base (object plans)
+    uint64_t shard_len;
+    uint64_t p0;         // first window's shard position
+};
+struct UPlanArgs {
+    const URec* recs;
+    uint32_t n_recs;
+    uint32_t accumulate;      // 1: out ^= result (passes beyond kMaxK inputs)
+    uint32_t in_idx[kMaxK];
+    uint32_t out_idx[kMaxR];
+    uint32_t in_sel, out_sel;
+    uint32_t tab[kMaxR][kMaxK][5];
+};
+uint32_t unaligned_tile_bytes();
+hipError_t launch_unaligned_plan(int k, int r, const UPlanArgs& a, int grid, hipStream_t stream);
 hipError_t launch_fill(uint8_t* dst, uint64_t n_obj, uint64_t obj_len, uint64_t obj_stride, uint64_t base_seed,
                        uint64_t first, int grid, hipStream_t stream);
 hipError_t vec_occupancy(int k, int r, int pipe, int force_stream, int* blocks_per_cu);

@@ -615,13 +615,14 @@ __global__ __launch_bounds__(kBlockThreads) void gf_apply_bytes(PassArgs a, int 
 // the e_r bytes it does not use itself, so the passes are race-free.
 // ---------------------------------------------------------------------------
 #ifndef HBEC_UNALIGNED_U
-#define HBEC_UNALIGNED_U 2  // u2 ~ u4 > u8 (profiles/r02_tune_unaligned.jsonl)
+#define HBEC_UNALIGNED_U 4  // with SHFL: u4 > u2 (profiles/r02_tune_unaligned*.jsonl)
 #endif
 #ifndef HBEC_REALIGN_SEL
 #define HBEC_REALIGN_SEL 1  // 1: select the 5 source dwords with v_cndmask; 0: a uniform switch
 #endif
 #ifndef HBEC_UNALIGNED_SHFL
-#define HBEC_UNALIGNED_SHFL 0  // 1: one load per input column, the upper block from lane l+1 (62 blocks/window)
+#define HBEC_UNALIGNED_SHFL 1  // 1: one load per input column, the upper block from lane l+1 (62 blocks/window):
+                               // +3-9 % over two loads (profiles/r02_tune_unaligned_shfl.jsonl)
 #endif
 // stored bytes per 64-lane window: 63 blocks (two loads per column), or 62
 // when the upper block comes from the next lane (lane 63's column is partial)
@@ -660,8 +661,7 @@ struct UView {
     uint32_t d;      // base & 15 (wave-uniform)
 };
 
-__device__ __forceinline__ UView uview(const uint8_t* p, uint64_t stride, uint32_t obj, uint64_t s) {
-    const uint64_t b = reinterpret_cast<uint64_t>(p) + (uint64_t)obj * stride;
+__device__ __forceinline__ UView uview(uint64_t b, uint64_t s) {
     UView v;
     v.abase = b & ~(uint64_t)15;
     v.last = (b + s - 1u) & ~(uint64_t)15;
@@ -698,99 +698,131 @@ __device__ __forceinline__ void store_bytes(uint64_t addr, const u32x4& v, uint6
         if ((uint64_t)b < n) p[b] = (uint8_t)(v[b >> 2] >> (8 * (b & 3)));
 }
 
-template <int R>
-__global__ __launch_bounds__(kBlockThreads) void gf_apply_unaligned(PassArgs a, int K) {
+// One wave tile: U windows from shard position p0 of one object / stripe.
+// in_base(j) / out_base(r) give the byte address of that object's input j /
+// output r shard (wave-uniform); tab(r, j) its coefficient tables.
+template <int R, class InBase, class OutBase, class Tab>
+__device__ __forceinline__ void unaligned_tile(int K, uint64_t S, uint64_t p0, bool accumulate, uint32_t lane,
+                                               InBase in_base, OutBase out_base, Tab tab) {
     constexpr int U = kUnalignedU;
     constexpr uint32_t W = kUnalignedWindow;
+    uint64_t col[U];
+    bool live[U];  // window-uniform
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        col[u] = p0 + (uint64_t)u * W + lane * 16u;
+        live[u] = p0 + (uint64_t)u * W < S;
+    }
+    u32x4 acc[R][U];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const UView ov = uview(out_base(r), S);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            acc[r][u] = u32x4{0, 0, 0, 0};
+            if (accumulate) {  // kernel-uniform; clamped loads need no per-window branch
+                u32x4 lo, hi;
+                uload(lo, hi, ov, col[u]);
+                acc[r][u] = realign16(lo, upper(lo, hi), ov.d);
+            }
+        }
+    }
+    u32x4 clo[U], chi[U];
+    UView cv = uview(in_base(0), S);
+#pragma unroll
+    for (int u = 0; u < U; ++u) uload(clo[u], chi[u], cv, col[u]);  // clamped: no branch
+#pragma unroll 1
+    for (int j = 0; j < K; ++j) {
+        u32x4 nlo[U], nhi[U];
+        UView nv = cv;
+        if (j + 1 < K) {
+            nv = uview(in_base(j + 1), S);
+#pragma unroll
+            for (int u = 0; u < U; ++u) uload(nlo[u], nhi[u], nv, col[u]);
+        }
+        uint32_t tb[R][5];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int q = 0; q < 5; ++q) tb[r][q] = tab(r, j)[q];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const u32x4 x = realign16(clo[u], upper(clo[u], chi[u]), cv.d);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const Sel sx = selectors(x[e]);
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+                    acc[r][u][e] ^= gf_mul_sel(sx, tb[r][0], tb[r][1], tb[r][2], tb[r][3], tb[r][4]);
+            }
+        }
+        if (j + 1 < K) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                clo[u] = nlo[u];
+                chi[u] = nhi[u];
+            }
+            cv = nv;
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint64_t ob = out_base(r);
+        const uint32_t e = __builtin_amdgcn_readfirstlane((16u - (uint32_t)(ob & 15u)) & 15u);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!live[u]) continue;  // window-uniform: every lane takes part in the shuffle
+            u32x4 nb;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) nb[i] = __shfl_down(acc[r][u][i], 1u, 64);
+            const u32x4 blk = realign16(acc[r][u], nb, e);
+            const uint64_t q = col[u] + e;  // block start (shard position); ob + q is 16-B aligned
+            if (lane < kUnalignedStoreLanes && q < S) {
+                if (q + 16u <= S)
+                    st16_addr(ob + q, blk);
+                else
+                    store_bytes(ob + q, blk, S - q);
+            }
+            if (lane == 0u && col[u] == 0u && e > 0u) store_bytes(ob, acc[r][u], e < S ? e : S);  // head
+        }
+    }
+}
+
+template <int R>
+__global__ __launch_bounds__(kBlockThreads) void gf_apply_unaligned(PassArgs a, int K) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave =
         __builtin_amdgcn_readfirstlane(xcd_block() * (kBlockThreads / 64) + (threadIdx.x >> 6));
     const uint32_t nwaves = gridDim.x * (kBlockThreads / 64);
     const uint32_t tpo = a.tiles_per_obj;
-    const uint64_t S = a.shard_len;
     for (uint32_t t = wave; t < a.n_tiles; t += nwaves) {
         const uint32_t obj = t / tpo;
-        const uint64_t p0 = (uint64_t)(t - obj * tpo) * (U * W);  // first window's shard position
-        uint64_t col[U];
-        bool live[U];  // window-uniform
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            col[u] = p0 + (uint64_t)u * W + lane * 16u;
-            live[u] = p0 + (uint64_t)u * W < S;
-        }
-        u32x4 acc[R][U];
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const UView ov = uview(a.out[r], a.out_stride[r], obj, S);
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                acc[r][u] = u32x4{0, 0, 0, 0};
-                if (a.accumulate) {  // kernel-uniform; clamped loads need no per-window branch
-                    u32x4 lo, hi;
-                    uload(lo, hi, ov, col[u]);
-                    acc[r][u] = realign16(lo, upper(lo, hi), ov.d);
-                }
-            }
-        }
-        u32x4 clo[U], chi[U];
-        UView cv = uview(a.in[0], a.in_stride[0], obj, S);
-#pragma unroll
-        for (int u = 0; u < U; ++u) uload(clo[u], chi[u], cv, col[u]);  // clamped: no branch
-#pragma unroll 1
-        for (int j = 0; j < K; ++j) {
-            u32x4 nlo[U], nhi[U];
-            UView nv = cv;
-            if (j + 1 < K) {
-                nv = uview(a.in[j + 1], a.in_stride[j + 1], obj, S);
-#pragma unroll
-                for (int u = 0; u < U; ++u) uload(nlo[u], nhi[u], nv, col[u]);
-            }
-            uint32_t tb[R][5];
-#pragma unroll
-            for (int r = 0; r < R; ++r)
-#pragma unroll
-                for (int q = 0; q < 5; ++q) tb[r][q] = a.tab[r][j][q];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const u32x4 x = realign16(clo[u], upper(clo[u], chi[u]), cv.d);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const Sel sx = selectors(x[e]);
-#pragma unroll
-                    for (int r = 0; r < R; ++r)
-                        acc[r][u][e] ^= gf_mul_sel(sx, tb[r][0], tb[r][1], tb[r][2], tb[r][3], tb[r][4]);
-                }
-            }
-            if (j + 1 < K) {
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    clo[u] = nlo[u];
-                    chi[u] = nhi[u];
-                }
-                cv = nv;
-            }
-        }
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const uint64_t ob = reinterpret_cast<uint64_t>(a.out[r]) + (uint64_t)obj * a.out_stride[r];
-            const uint32_t e = __builtin_amdgcn_readfirstlane((16u - (uint32_t)(ob & 15u)) & 15u);
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (!live[u]) continue;  // window-uniform: every lane takes part in the shuffle
-                u32x4 nb;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) nb[i] = __shfl_down(acc[r][u][i], 1u, 64);
-                const u32x4 blk = realign16(acc[r][u], nb, e);
-                const uint64_t q = col[u] + e;  // block start (shard position); ob + q is 16-B aligned
-                if (lane < kUnalignedStoreLanes && q < S) {
-                    if (q + 16u <= S)
-                        st16_addr(ob + q, blk);
-                    else
-                        store_bytes(ob + q, blk, S - q);
-                }
-                if (lane == 0u && col[u] == 0u && e > 0u) store_bytes(ob, acc[r][u], e < S ? e : S);  // head
-            }
-        }
+        const uint64_t p0 = (uint64_t)(t - obj * tpo) * (kUnalignedU * kUnalignedWindow);
+        unaligned_tile<R>(
+            K, a.shard_len, p0, a.accumulate != 0, lane,
+            [&](int j) { return reinterpret_cast<uint64_t>(a.in[j]) + (uint64_t)obj * a.in_stride[j]; },
+            [&](int r) { return reinterpret_cast<uint64_t>(a.out[r]) + (uint64_t)obj * a.out_stride[r]; },
+            [&](int r, int j) { return a.tab[r][j]; });
+    }
+}
+
+// Plans over stripes / objects of mixed shard lengths at any alignment: one
+// record per wave tile (URec).  Input j of a tile's stripe starts at
+// (bit j of in_sel ? b : a) + in_idx[j] * S; outputs likewise.
+template <int R>
+__global__ __launch_bounds__(kBlockThreads) void gf_apply_unaligned_plan(UPlanArgs p, int K) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave =
+        __builtin_amdgcn_readfirstlane(xcd_block() * (kBlockThreads / 64) + (threadIdx.x >> 6));
+    const uint32_t nwaves = gridDim.x * (kBlockThreads / 64);
+    for (uint32_t t = wave; t < p.n_recs; t += nwaves) {
+        const URec rec = p.recs[t];
+        const uint64_t S = rec.shard_len;
+        unaligned_tile<R>(
+            K, S, rec.p0, p.accumulate != 0, lane,
+            [&](int j) { return (((p.in_sel >> j) & 1u) ? rec.b : rec.a) + (uint64_t)p.in_idx[j] * S; },
+            [&](int r) { return (((p.out_sel >> r) & 1u) ? rec.b : rec.a) + (uint64_t)p.out_idx[r] * S; },
+            [&](int r, int j) { return p.tab[r][j]; });
     }
 }
 
@@ -1018,6 +1050,25 @@ hipError_t launch_unaligned(int k, int r, const PassArgs& a, int grid, hipStream
     const void* fn = unaligned_kernel(r);
     if (!fn || k < 1 || k > kMaxK) return hipErrorInvalidValue;
     void* args[] = {const_cast<PassArgs*>(&a), &k};
+    return hipLaunchKernel(fn, dim3(grid), dim3(kBlockThreads), args, 0, stream);
+}
+
+static const void* unaligned_plan_kernel(int r) {
+    switch (r) {
+        case 1: return reinterpret_cast<const void*>(&gf_apply_unaligned_plan<1>);
+        case 2: return reinterpret_cast<const void*>(&gf_apply_unaligned_plan<2>);
+        case 3: return reinterpret_cast<const void*>(&gf_apply_unaligned_plan<3>);
+        case 4: return reinterpret_cast<const void*>(&gf_apply_unaligned_plan<4>);
+    }
+    return nullptr;
+}
+
+uint32_t unaligned_tile_bytes() { return (uint32_t)kUnalignedU * kUnalignedWindow; }
+
+hipError_t launch_unaligned_plan(int k, int r, const UPlanArgs& a, int grid, hipStream_t stream) {
+    const void* fn = unaligned_plan_kernel(r);
+    if (!fn || k < 1 || k > kMaxK) return hipErrorInvalidValue;
+    void* args[] = {const_cast<UPlanArgs*>(&a), &k};
     return hipLaunchKernel(fn, dim3(grid), dim3(kBlockThreads), args, 0, stream);
 }
 

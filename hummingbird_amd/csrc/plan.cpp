@@ -1,9 +1,10 @@
 // plan.cpp — stripe plans: a batch of stripes of mixed shard lengths coded in
 // one launch (stripes.hip).  A stripe is ecSplit's databuf layout
 // (objectserver/ecutils.go:31-35,55-58): k+m shards of shard_len bytes back
-// to back, data first.  Stripes the tiled kernel cannot take (unaligned; or
-// object plans beyond 8 inputs) go through the generic strided path one by
-// one; stripe plans with k > 8 run the tiled kernel in accumulate passes.
+// to back, data first.  Stripes the tiled kernel cannot take (unaligned:
+// S % 16 != 0 for 15 object sizes in 16; or object plans beyond 8 inputs) are
+// coded by one more launch per pass of gf_apply_unaligned_plan over their own
+// records; stripe plans with k > 8 run the tiled kernel in accumulate passes.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -33,6 +34,9 @@ struct hbec_plan {
     bool objects = false;
     std::vector<hbec_object> obj_tiled, obj_fallback;
     uint64_t shard_bytes = 0;           // sum of shard_len over all stripes
+    // stripes / objects the tiled kernel cannot take: unaligned-kernel records
+    hbec::URec* d_urecs = nullptr;
+    uint64_t n_urecs = 0;
 };
 
 namespace {
@@ -55,7 +59,77 @@ uint8_t* object_shard(const hbec_object& o, int k, int i) {
 
 std::mutex g_occ_mu;
 
+void add_urecs(std::vector<hbec::URec>& recs, const void* a, const void* b, uint64_t s) {
+    const uint64_t tile = hbec::unaligned_tile_bytes();
+    for (uint64_t p0 = 0; p0 < s; p0 += tile)
+        recs.push_back({reinterpret_cast<uint64_t>(a), reinterpret_cast<uint64_t>(b), s, p0});
+}
+
+template <class T>
+int upload(const std::vector<T>& recs, T** dst, const char* what) {
+    if (recs.empty()) return HBEC_OK;
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(dst), recs.size() * sizeof(T));
+    if (e != hipSuccess) return hip_fail(e, what);
+    e = hipMemcpy(*dst, recs.data(), recs.size() * sizeof(T), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        (void)hipFree(*dst);
+        *dst = nullptr;
+        return hip_fail(e, what);
+    }
+    return HBEC_OK;
+}
+
 }  // namespace
+
+// out rows (^)= rows x in over unaligned-kernel records, in passes of <= 4
+// outputs x <= kMaxK inputs (later input passes accumulate).  sel_k > 0:
+// object records (shard indices >= sel_k are parity, base b).
+static int launch_unaligned_passes(const hbec::URec* recs, uint64_t n_recs, const std::vector<int>& in_idx,
+                                   const std::vector<int>& out_idx, const std::vector<uint8_t>& rows, int sel_k,
+                                   hipStream_t stream) {
+    const int K_all = (int)in_idx.size(), R_all = (int)out_idx.size();
+    if (n_recs == 0 || R_all == 0) return HBEC_OK;
+    int dev = 0, cus = 0, per_cu = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+    e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess) return hip_fail(e, "hipDeviceGetAttribute");
+    for (int r0 = 0; r0 < R_all; r0 += hbec::kMaxR) {
+        const int R = std::min(hbec::kMaxR, R_all - r0);
+        e = hbec::unaligned_occupancy(R, &per_cu);
+        if (e != hipSuccess) return hip_fail(e, "unaligned occupancy");
+        for (int c0 = 0; c0 < K_all; c0 += hbec::kMaxK) {
+            const int K = std::min(hbec::kMaxK, K_all - c0);
+            hbec::UPlanArgs a;
+            std::memset(&a, 0, sizeof(a));
+            a.recs = recs;
+            a.n_recs = (uint32_t)n_recs;
+            a.accumulate = c0 > 0 ? 1u : 0u;
+            for (int j = 0; j < K; ++j) {
+                int i = in_idx[c0 + j];
+                if (sel_k > 0 && i >= sel_k) {
+                    a.in_sel |= 1u << j;
+                    i -= sel_k;
+                }
+                a.in_idx[j] = (uint32_t)i;
+            }
+            for (int r = 0; r < R; ++r) {
+                int i = out_idx[r0 + r];
+                if (sel_k > 0 && i >= sel_k) {
+                    a.out_sel |= 1u << r;
+                    i -= sel_k;
+                }
+                a.out_idx[r] = (uint32_t)i;
+                for (int j = 0; j < K; ++j) hbec::perm_table(rows[(size_t)(r0 + r) * K_all + c0 + j], a.tab[r][j]);
+            }
+            const uint64_t want = (n_recs + 3) / 4;  // 4 waves per block
+            const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cus * std::max(1, per_cu)));
+            e = hbec::launch_unaligned_plan(K, R, a, grid, stream);
+            if (e != hipSuccess) return hip_fail(e, "launch gf_apply_unaligned_plan");
+        }
+    }
+    return HBEC_OK;
+}
 
 int hbec::stripes_grid(int k, int r, uint64_t n_tiles, int* grid, int blocks_per_cu, int max_blocks) {
     int dev = 0;
@@ -142,18 +216,6 @@ int hbec::launch_stripe_passes(const TileRec* tiles, uint64_t n_tiles, const std
 
 namespace {
 
-// Codes one stripe through the generic strided path (any alignment / shape).
-int apply_one(const hbec_stripe& s, int n_shards, const std::vector<int>& in_idx, const std::vector<int>& out_idx,
-              const uint8_t* rows, hipStream_t stream) {
-    std::vector<hbec_view> vin(in_idx.size()), vout(out_idx.size());
-    uint8_t* base = static_cast<uint8_t*>(s.base);
-    for (size_t j = 0; j < in_idx.size(); ++j) vin[j] = {base + (uint64_t)in_idx[j] * s.shard_len, 0};
-    for (size_t r = 0; r < out_idx.size(); ++r) vout[r] = {base + (uint64_t)out_idx[r] * s.shard_len, 0};
-    (void)n_shards;
-    return hbec::apply_views((int)out_idx.size(), (int)in_idx.size(), rows, vin.data(), vout.data(), 1, s.shard_len,
-                             stream);
-}
-
 // Codes one object of an object plan through the generic strided path.
 int apply_one_object(const hbec_object& o, int k, const std::vector<int>& in_idx, const std::vector<int>& out_idx,
                      const uint8_t* rows, hipStream_t stream) {
@@ -185,24 +247,9 @@ int run_plan(const hbec_plan* p, const std::vector<int>& in_idx, const std::vect
                 if (rc) return rc;
             }
         }
-        for (const auto& o : p->obj_fallback) {
-            int rc = apply_one_object(o, p->k, in_idx, out_idx, rows.data(), stream);
-            if (rc) return rc;
-        }
-        return HBEC_OK;
+        return launch_unaligned_passes(p->d_urecs, p->n_urecs, in_idx, out_idx, rows, p->k, stream);
     }
-    const auto& singles = tiled_ok ? p->fallback : p->tiled;
-    for (const auto& s : singles) {
-        int rc = apply_one(s, p->k + p->m, in_idx, out_idx, rows.data(), stream);
-        if (rc) return rc;
-    }
-    if (!tiled_ok) {
-        for (const auto& s : p->fallback) {
-            int rc = apply_one(s, p->k + p->m, in_idx, out_idx, rows.data(), stream);
-            if (rc) return rc;
-        }
-    }
-    return HBEC_OK;
+    return launch_unaligned_passes(p->d_urecs, p->n_urecs, in_idx, out_idx, rows, 0, stream);
 }
 
 }  // namespace
@@ -220,6 +267,7 @@ int hbec_plan_stripes(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n,
         p->m = m;
         p->tile_bytes = hbec::stripes_tile_bytes(std::min(k, hbec::kStripeMaxK));
         std::vector<hbec::TileRec> recs;
+        std::vector<hbec::URec> urecs;
         for (uint64_t i = 0; i < n; ++i) {
             const hbec_stripe& s = stripes[i];
             if (s.shard_len == 0) continue;
@@ -227,6 +275,7 @@ int hbec_plan_stripes(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n,
             p->shard_bytes += s.shard_len;
             if (!aligned_stripe(s)) {
                 p->fallback.push_back(s);
+                add_urecs(urecs, s.base, nullptr, s.shard_len);
                 continue;
             }
             p->tiled.push_back(s);
@@ -251,6 +300,13 @@ int hbec_plan_stripes(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n,
                 return hip_fail(e, "hipMemcpy plan tiles");
             }
         }
+        if (urecs.size() >= (1ull << 31)) return fail(HBEC_ERR_INVALID_ARG, "plan too large (>= 2^31 tiles)");
+        int urc = upload(urecs, &p->d_urecs, "plan unaligned records");
+        if (urc) {
+            if (p->d_tiles) (void)hipFree(p->d_tiles);
+            return urc;
+        }
+        p->n_urecs = urecs.size();
         *out = p.release();
         return HBEC_OK;
     });
@@ -268,6 +324,7 @@ int hbec_plan_objects(hbec_codec* codec, const hbec_object* objects, uint64_t n,
         p->objects = true;
         p->tile_bytes = hbec::stripes_tile_bytes(std::min(k, hbec::kStripeMaxK));
         std::vector<hbec::TileRec> recs;
+        std::vector<hbec::URec> urecs;
         for (uint64_t i = 0; i < n; ++i) {
             const hbec_object& o = objects[i];
             if (o.shard_len == 0) continue;
@@ -275,6 +332,7 @@ int hbec_plan_objects(hbec_codec* codec, const hbec_object* objects, uint64_t n,
             p->shard_bytes += o.shard_len;
             if (!aligned_object(o)) {
                 p->obj_fallback.push_back(o);
+                add_urecs(urecs, o.data, o.parity, o.shard_len);
                 continue;
             }
             p->obj_tiled.push_back(o);
@@ -300,6 +358,13 @@ int hbec_plan_objects(hbec_codec* codec, const hbec_object* objects, uint64_t n,
                 return hip_fail(e, "hipMemcpy plan tiles");
             }
         }
+        if (urecs.size() >= (1ull << 31)) return fail(HBEC_ERR_INVALID_ARG, "plan too large (>= 2^31 tiles)");
+        int urc = upload(urecs, &p->d_urecs, "plan unaligned records");
+        if (urc) {
+            if (p->d_tiles) (void)hipFree(p->d_tiles);
+            return urc;
+        }
+        p->n_urecs = urecs.size();
         *out = p.release();
         return HBEC_OK;
     });
@@ -308,6 +373,7 @@ int hbec_plan_objects(hbec_codec* codec, const hbec_object* objects, uint64_t n,
 void hbec_plan_free(hbec_plan* plan) {
     if (!plan) return;
     if (plan->d_tiles) (void)hipFree(plan->d_tiles);
+    if (plan->d_urecs) (void)hipFree(plan->d_urecs);
     delete plan;
 }
 

@@ -65,6 +65,31 @@ def shape(k, m, n, obj_len, layout):
                       "verify_ok": ok}), flush=True)
 
 
+def plan_shape(k, m, n, odd):
+    """A stripe plan of n ecSplit databufs back to back, objects of 1 MiB
+    (odd=False) or 1 MiB - (1..15) B (odd=True: S % 16 != 0 for most, bases
+    at arbitrary offsets), as a batched stabilizer would hand them over."""
+    import numpy as np
+
+    rng = np.random.default_rng(k * 100 + m)
+    layout, off = [], 0
+    for _ in range(n):
+        size = (1 << 20) - (int(rng.integers(1, 16)) if odd else 0)
+        s = -(-size // k)
+        layout.append((off, s))
+        off += (k + m) * s
+    pool = torch.empty((1, off), dtype=torch.uint8, device="cuda")
+    B.fill_splitmix(pool, off)
+    enc = RS.New(k, m)
+    plan = B.StripePlan(enc, [(pool.data_ptr() + o, s) for o, s in layout])
+    ms = timeit(plan.encode)
+    nb = sum((k + m) * s for _, s in layout)
+    info = plan.info()
+    print(json.dumps({"k": k, "m": m, "n": n, "layout": "stripe plan, " + ("odd sizes" if odd else "1 MiB"),
+                      "encode_ms": round(ms, 4), "GB_s": round(nb / ms / 1e6, 1),
+                      "frac": round(nb / ms / 1e6 / PEAK, 4), "n_fallback": info["n_fallback"]}), flush=True)
+
+
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
     torch.cuda.set_device(0)
@@ -73,6 +98,9 @@ def main():
                     (10, 4, MiB), (10, 4, 10 * 104864), (12, 4, 12 * 87392), (16, 4, MiB), (17, 3, 17 * 61696)]:
         for layout in ("split", "databuf"):
             shape(k, m, n, L, layout)
+    for k, m in [(4, 2), (8, 3), (10, 4)]:
+        for odd in (False, True):
+            plan_shape(k, m, n, odd)
 
 
 if __name__ == "__main__":

@@ -18,12 +18,12 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 
 VARIANTS = {
-    "base": [],  # round-2 defaults: U = 2, v_cndmask selection
-    "shfl": ["HBEC_UNALIGNED_SHFL=1"],
-    "shflu4": ["HBEC_UNALIGNED_SHFL=1", "HBEC_UNALIGNED_U=4"],
-    "u4sw": ["HBEC_UNALIGNED_U=4", "HBEC_REALIGN_SEL=0"],
-    "u8": ["HBEC_UNALIGNED_U=8"],
+    "base": [],  # shipped: U = 4, single load + lane shuffle, v_cndmask selection
+    "twoload": ["HBEC_UNALIGNED_SHFL=0"],
+    "shflu2": ["HBEC_UNALIGNED_U=2"],
 }
+# second sweep (profiles/r02_tune_unaligned_shfl.jsonl) ran with U = 2, two
+# loads, v_cndmask as base: shfl, shflu4 (now shipped), u4sw, u8.
 # first sweep (profiles/r02_tune_unaligned.jsonl) ran with the defaults U = 4
 # and the uniform switch: base = u4 switch, sel, u2, u8, u2sel, u8sel.
 
