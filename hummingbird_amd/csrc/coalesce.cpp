@@ -161,14 +161,15 @@ int coalesced_call(hbec_codec* codec, int op, uint8_t* base, uint64_t s, const u
     }
     hipError_t e = hipGetDevice(&r.dev);
     if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
-    // Only stripes the GPU can code in place (pinned, device-mapped, 16-B
-    // aligned) are grouped: a group of those is ONE zero-copy launch with no
+    // Only stripes the GPU can code in place (pinned, device-mapped; 16-B
+    // aligned, or any alignment through the unaligned kernel) are grouped: a
+    // group of those is ONE zero-copy launch (per alignment class) with no
     // CPU copy.  Pageable stripes take the per-call path, whose bounce-buffer
     // copies then run in parallel on the callers' own threads — 64 concurrent
     // callers reach 30 GiB/s that way vs 9 GiB/s funnelled through one
     // leader's staging ring (profiles/r02_percall.jsonl).
-    const bool pinned = (reinterpret_cast<uintptr_t>(base) & 15u) == 0 && s % 16 == 0 &&
-                        pinned_device_addr(base, s * (uint64_t)n_shards) != 0;
+    const bool aligned = (reinterpret_cast<uintptr_t>(base) & 15u) == 0 && s % 16 == 0;
+    const bool pinned = (aligned || zero_copy_any_alignment()) && pinned_device_addr(base, s * (uint64_t)n_shards) != 0;
     if (!pinned) return op == 0 ? fn.encode(codec, base, s) : fn.reconstruct(codec, base, s, present, data_only);
     const uint64_t cap = group_cap_bytes();
     std::unique_lock<std::mutex> lk(g_co.mu);

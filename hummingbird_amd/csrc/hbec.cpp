@@ -523,7 +523,8 @@ static int host_apply(int rows, int cols, const uint8_t* coeffs, const uint8_t* 
     // Zero-copy: every shard in pinned, device-mapped memory -> the kernel
     // reads and writes them in place over PCIe (no staging copies).
     std::vector<hbec_view> zin(cols), zout(rows);
-    bool zero_copy = len > 0 && len % 16 == 0;
+    // (odd lengths / offsets too: apply_views takes them to gf_apply_unaligned)
+    bool zero_copy = len > 0 && (len % 16 == 0 || (g_unaligned_kernel.load() && zero_copy_any_alignment()));
     for (int j = 0; j < cols && zero_copy; ++j) {
         const uint64_t d = pinned_device_addr(in[j], len);
         zero_copy = d != 0;

@@ -362,6 +362,16 @@ int zero_copy_blocks_per_cu() {
     return v;
 }
 
+// Pinned stripes that are not 16-B aligned (or S % 16 != 0): zero-copy through
+// the unaligned kernel (default) or, with HBEC_ZC_UNALIGNED=0, the staged ring.
+bool zero_copy_unaligned_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("HBEC_ZC_UNALIGNED");
+        return !e || std::atoi(e) != 0;
+    }();
+    return on;
+}
+
 // Grid cap of the zero-copy stripes kernel (HBEC_ZC_GRID blocks, 0 = CUs x
 // blocks per CU).  64 blocks of 4 waves keep ~1 MiB of PCIe reads in flight,
 // plenty for the link, where the whole chip (512 blocks) kept ~8 MiB queued
@@ -390,6 +400,8 @@ bool zero_copy_enabled() {
 // pinned, device-mapped allocation; 0 otherwise.  hbec_host_alloc ranges are
 // looked up in the registry; other pinned memory is asked of the runtime at
 // both ends of the range.
+bool hbec::zero_copy_any_alignment() { return zero_copy_unaligned_enabled(); }
+
 uint64_t hbec::pinned_device_addr(const void* p, uint64_t len) {
     if (!zero_copy_enabled()) return 0;
     const uint64_t h = reinterpret_cast<uint64_t>(p);
@@ -467,6 +479,44 @@ int zero_copy_run(Ring* ring, const std::vector<ZcStripe>& zs, const std::vector
         if (e != hipSuccess) return hip_fail(e, "zero-copy records H2D");
         int rc = hbec::launch_stripe_passes(ring->dev_tiles[slot], nt, in_idx, out_idx, rows, 0, ring->s_cmp,
                                             zero_copy_blocks_per_cu(), false, zero_copy_max_blocks());
+        if (rc) return rc;
+        e = hipEventRecord(ring->ev_cmp[slot], ring->s_cmp);
+        if (e != hipSuccess) return hip_fail(e, "zero-copy event");
+    }
+    e = hipStreamSynchronize(ring->s_cmp);
+    if (e != hipSuccess) return hip_fail(e, "zero-copy drain");
+    return HBEC_OK;
+}
+
+// Pinned stripes at any alignment / shard length (S % 16 != 0 for most object
+// sizes): the same in-place PCIe coding through gf_apply_unaligned_plan
+// records (URec and TileRec are both 32 B, so the slot buffers are shared).
+int zero_copy_unaligned_run(Ring* ring, const std::vector<ZcStripe>& zs, const std::vector<int>& in_idx,
+                            const std::vector<int>& out_idx, const std::vector<uint8_t>& rows) {
+    static_assert(sizeof(hbec::URec) == sizeof(hbec::TileRec), "record slots are shared");
+    const uint64_t tile = hbec::unaligned_tile_bytes();
+    size_t si = 0;
+    uint64_t off = 0;
+    hipError_t e = hipSuccess;
+    for (int c = 0; si < zs.size(); ++c) {
+        const int slot = c % kSlots;
+        e = hipEventSynchronize(ring->ev_cmp[slot]);  // the slot's previous records are consumed
+        if (e != hipSuccess) return hip_fail(e, "zero-copy slot wait");
+        hbec::URec* rec = reinterpret_cast<hbec::URec*>(ring->pin_tiles[slot]);
+        uint64_t nt = 0;
+        while (si < zs.size() && nt < ring->tile_cap) {
+            const ZcStripe& z = zs[si];
+            rec[nt++] = {z.dev, 0, z.shard_len, off};
+            off += tile;
+            if (off >= z.shard_len) {
+                off = 0;
+                ++si;
+            }
+        }
+        e = hipMemcpyAsync(ring->dev_tiles[slot], rec, nt * sizeof(hbec::URec), hipMemcpyHostToDevice, ring->s_cmp);
+        if (e != hipSuccess) return hip_fail(e, "zero-copy records H2D");
+        int rc = hbec::launch_unaligned_passes(reinterpret_cast<const hbec::URec*>(ring->dev_tiles[slot]), nt, in_idx,
+                                               out_idx, rows, 0, ring->s_cmp, zero_copy_max_blocks());
         if (rc) return rc;
         e = hipEventRecord(ring->ev_cmp[slot], ring->s_cmp);
         if (e != hipSuccess) return hip_fail(e, "zero-copy event");
@@ -633,18 +683,23 @@ int host_run_on(Ring* ring, const hbec_stripe* stripes, uint64_t n, const std::v
         int top = 0;
         for (int i : in_idx) top = std::max(top, i);
         for (int i : out_idx) top = std::max(top, i);
-        std::vector<ZcStripe> zs;
+        std::vector<ZcStripe> zs, zu;  // aligned (stripes kernel) / any alignment (unaligned kernel)
         for (uint64_t s = 0; s < n; ++s) {
             const uint64_t S = stripes[s].shard_len;
             if (S == 0) continue;
+            const uint64_t d = stripes[s].base ? pinned_device_addr(stripes[s].base, (uint64_t)(top + 1) * S) : 0;
             const bool aligned = (reinterpret_cast<uintptr_t>(stripes[s].base) & 15u) == 0 && S % 16 == 0 &&
-                                 S < (1ull << 32);
-            const uint64_t d = aligned ? pinned_device_addr(stripes[s].base, (uint64_t)(top + 1) * S) : 0;
-            if (d && (d & 15u) == 0) zs.push_back({d, S});
+                                 S < (1ull << 32) && (d & 15u) == 0;
+            if (d && aligned) zs.push_back({d, S});
+            else if (d && zero_copy_unaligned_enabled()) zu.push_back({d, S});
             else staged.push_back(stripes[s]);
         }
         if (!zs.empty()) {
             rc = zero_copy_run(ring, zs, in_idx, out_idx, rows);
+            if (rc) return rc;
+        }
+        if (!zu.empty()) {
+            rc = zero_copy_unaligned_run(ring, zu, in_idx, out_idx, rows);
             if (rc) return rc;
         }
         if (staged.empty()) return HBEC_OK;

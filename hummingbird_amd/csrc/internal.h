@@ -44,6 +44,9 @@ void scratch_free(void* p, hipStream_t stream);
 // memory (hbec_host_alloc, hipHostMalloc, hipHostRegister), else 0 (also 0 when
 // HBEC_ZEROCOPY=0).  The zero-copy host paths code such memory in place.
 uint64_t pinned_device_addr(const void* p, uint64_t len);
+// Pinned stripes at any alignment / shard length are coded in place over PCIe
+// (gf_apply_unaligned_plan) unless HBEC_ZC_UNALIGNED=0.
+bool zero_copy_any_alignment();
 
 // ShardHash of a list of device chains: records {addr, len, slot, 0} (32 B
 // each, device memory), digest of record i at digest + slot * 16.
@@ -78,5 +81,14 @@ int stripes_grid(int k, int r, uint64_t n_tiles, int* grid, int blocks_per_cu = 
 int launch_stripe_passes(const TileRec* tiles, uint64_t n_tiles, const std::vector<int>& in_idx,
                          const std::vector<int>& out_idx, const std::vector<uint8_t>& rows, int sel_k,
                          hipStream_t stream, int blocks_per_cu = 0, bool mirror = false, int max_blocks = 0);
+
+struct URec;
+// out (^)= rows x in over unaligned-kernel records (any alignment, mixed
+// lengths), in launches of <= 4 outputs and <= kMaxK inputs (later input
+// passes accumulate).  sel_k > 0: object records (indices >= sel_k are
+// parity, base b).  max_blocks > 0 caps the grid (zero-copy over PCIe).
+int launch_unaligned_passes(const URec* recs, uint64_t n_recs, const std::vector<int>& in_idx,
+                            const std::vector<int>& out_idx, const std::vector<uint8_t>& rows, int sel_k,
+                            hipStream_t stream, int max_blocks = 0);
 
 }  // namespace hbec

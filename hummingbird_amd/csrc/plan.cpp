@@ -84,9 +84,9 @@ int upload(const std::vector<T>& recs, T** dst, const char* what) {
 // out rows (^)= rows x in over unaligned-kernel records, in passes of <= 4
 // outputs x <= kMaxK inputs (later input passes accumulate).  sel_k > 0:
 // object records (shard indices >= sel_k are parity, base b).
-static int launch_unaligned_passes(const hbec::URec* recs, uint64_t n_recs, const std::vector<int>& in_idx,
-                                   const std::vector<int>& out_idx, const std::vector<uint8_t>& rows, int sel_k,
-                                   hipStream_t stream) {
+int hbec::launch_unaligned_passes(const URec* recs, uint64_t n_recs, const std::vector<int>& in_idx,
+                                  const std::vector<int>& out_idx, const std::vector<uint8_t>& rows, int sel_k,
+                                  hipStream_t stream, int max_blocks) {
     const int K_all = (int)in_idx.size(), R_all = (int)out_idx.size();
     if (n_recs == 0 || R_all == 0) return HBEC_OK;
     int dev = 0, cus = 0, per_cu = 0;
@@ -123,7 +123,9 @@ static int launch_unaligned_passes(const hbec::URec* recs, uint64_t n_recs, cons
                 for (int j = 0; j < K; ++j) hbec::perm_table(rows[(size_t)(r0 + r) * K_all + c0 + j], a.tab[r][j]);
             }
             const uint64_t want = (n_recs + 3) / 4;  // 4 waves per block
-            const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cus * std::max(1, per_cu)));
+            uint64_t cap = (uint64_t)cus * std::max(1, per_cu);
+            if (max_blocks > 0) cap = std::min<uint64_t>(cap, (uint64_t)max_blocks);
+            const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, cap));
             e = hbec::launch_unaligned_plan(K, R, a, grid, stream);
             if (e != hipSuccess) return hip_fail(e, "launch gf_apply_unaligned_plan");
         }
@@ -247,9 +249,9 @@ int run_plan(const hbec_plan* p, const std::vector<int>& in_idx, const std::vect
                 if (rc) return rc;
             }
         }
-        return launch_unaligned_passes(p->d_urecs, p->n_urecs, in_idx, out_idx, rows, p->k, stream);
+        return hbec::launch_unaligned_passes(p->d_urecs, p->n_urecs, in_idx, out_idx, rows, p->k, stream);
     }
-    return launch_unaligned_passes(p->d_urecs, p->n_urecs, in_idx, out_idx, rows, 0, stream);
+    return hbec::launch_unaligned_passes(p->d_urecs, p->n_urecs, in_idx, out_idx, rows, 0, stream);
 }
 
 }  // namespace

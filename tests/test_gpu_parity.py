@@ -691,7 +691,7 @@ def _pinned_stripes(buf, k, m, sizes, seed, gap=0):
 
 
 @pytest.mark.parametrize("k,m,sizes", [
-    (4, 2, [MiB] * 40 + [4096, 1001, 16 * 7]),      # 1001 -> S=251: unaligned, takes the ring
+    (4, 2, [MiB] * 40 + [4096, 1001, 16 * 7]),      # 1001 -> S=251: unaligned, zero-copy via gf_apply_unaligned_plan
     (8, 3, [4096, MiB, 4096, 3 * MiB + 8, 1]),
     (3, 5, [3000 * 16, 30000 * 16]),                # more outputs than inputs, 2 row groups
 ])
@@ -782,7 +782,8 @@ def test_host_path_zero_copy_foreign_pinned_memory():
 @pytest.mark.parametrize("k,m,s", [(4, 2, MiB // 4), (8, 3, 4096), (3, 2, 48), (4, 2, 1001)])
 def test_per_call_encode_reconstruct_zero_copy(k, m, s):
     """klauspost Encode / Reconstruct on shards that live in pinned host memory:
-    coded in place by the GPU (no staging) when S % 16 == 0, staged otherwise."""
+    coded in place by the GPU (no staging); S % 16 != 0 (1001) through the
+    unaligned kernel."""
     hb = RS.HostBuffer((k + m) * (s + 16) + 16)
     pitch = (s + 15) // 16 * 16
     shards = [hb.array[i * pitch:i * pitch + s] for i in range(k + m)]

@@ -192,3 +192,56 @@ def test_plan_random_odd_stripes(k, m, n):
         [0 if i in lost else 1 for i in range(k + m)])
     torch.cuda.synchronize()
     assert np.array_equal(damaged.cpu().numpy(), want), lost
+
+
+@pytest.mark.parametrize("k,m", [(4, 2), (8, 3), (10, 4), (20, 4)])
+def test_host_pinned_odd_stripes_zero_copy(k, m):
+    """Pinned host stripes of odd sizes at odd byte offsets (ecSplit databufs
+    of arbitrary objects in a hbec_host_alloc pool): coded in place over PCIe
+    by the unaligned kernel, through the batched host path and through the
+    per-call databuf entry, against the oracle; bytes between stripes are
+    untouched."""
+    from oracle import oracle as O
+
+    rng = np.random.default_rng(k * 7 + m)
+    sizes = [int(x) for x in rng.integers(1, 300_000, size=24)] + [(1 << 20) - 3, 1001, 7]
+    layout, off = [], 0
+    for size in sizes:
+        s = O.ec_shard_length(size, k)
+        off += int(rng.integers(1, 16))
+        layout.append((off, s, size))
+        off += (k + m) * s
+    hb = RS.HostBuffer(off + 64)
+    a = hb.array
+    a[:] = GUARD
+    for i, (o, s, size) in enumerate(layout):
+        a[o:o + (k + m) * s] = 0
+        a[o:o + size] = CO.fill_objects(300 + i, 1, size)[0]
+    want = a.copy()
+    mat = CO.build_matrix(k, m)[k:]
+    for o, s, _ in layout:
+        for r, p in enumerate(CO.apply(mat, [want[o + j * s:o + (j + 1) * s] for j in range(k)])):
+            want[o + (k + r) * s:o + (k + r + 1) * s] = p
+    enc = RS.New(k, m)
+    stripes = [a[o:o + (k + m) * s] for o, s, _ in layout]
+    assert all(RS.host_device_addr(st) != 0 for st in stripes)
+    enc.EncodeStripes(stripes)
+    assert np.array_equal(a, want)
+    lost = sorted(rng.choice(k + m, size=m, replace=False).tolist())
+    for o, s, _ in layout:
+        for i in lost:
+            a[o + i * s:o + (i + 1) * s] = 0x5A
+    enc.ReconstructStripes(stripes, [0 if i in lost else 1 for i in range(k + m)])
+    assert np.array_equal(a, want), lost
+    # per-call databuf entries (the cgo shim's path), one stripe per call
+    for o, s, _ in layout:
+        a[o + k * s:o + (k + m) * s] = 0x77
+    for st, (o, s, _) in zip(stripes, layout):
+        enc.EncodeDatabuf(st, s)
+    assert np.array_equal(a, want)
+    for st, (o, s, _) in zip(stripes, layout):
+        st[:s] = 0x11
+        enc.ReconstructDatabuf(st, s, [0] + [1] * (k + m - 1))
+    assert np.array_equal(a, want)
+    del stripes
+    hb.free()
