@@ -22,12 +22,16 @@ VARIANTS = {
     "twoload": ["HBEC_UNALIGNED_SHFL=0"],
     "shflu2": ["HBEC_UNALIGNED_U=2"],
 }
+# third sweep (profiles/r02_tune_stream_clamp_rejected.jsonl): clamped loads in
+# the streaming kernel (K > 8, aligned) instead of loads under branches: equal
+# within 1 %, not adopted.
 # second sweep (profiles/r02_tune_unaligned_shfl.jsonl) ran with U = 2, two
 # loads, v_cndmask as base: shfl, shflu4 (now shipped), u4sw, u8.
 # first sweep (profiles/r02_tune_unaligned.jsonl) ran with the defaults U = 4
 # and the uniform switch: base = u4 switch, sel, u2, u8, u2sel, u8sel.
 
-SHAPES = [(4, 2, (1 << 20) - 4), (8, 3, (1 << 20) - 8), (6, 3, 1 << 20), (10, 4, 1 << 20)]
+SHAPES = [(4, 2, (1 << 20) - 4), (8, 3, (1 << 20) - 8), (6, 3, 1 << 20), (10, 4, 1 << 20),
+          (10, 4, 10 * 104864), (12, 4, 12 * 87392), (16, 4, 1 << 20)]  # the last three: aligned, streaming kernel
 
 
 def build(names=None):
