@@ -936,6 +936,46 @@ static int verify_views(hbec_codec* c, const hbec_view* views, uint64_t n_obj, u
         }
         return HBEC_OK;
     }
+    if (g_unaligned_kernel.load() && k <= kMaxK) {
+        // any alignment: recompute and compare in one pass (gf_verify_unaligned), <= 4 rows per launch
+        int dev = 0, cus = 0;
+        int rc = current_device(&dev);
+        if (rc) return rc;
+        const uint64_t tpo = unaligned_tiles_per_obj(shard_len);
+        const uint64_t max_obj = std::max<uint64_t>(1, std::min<uint64_t>((1ull << 31), g_chunk_tiles) / tpo);
+        for (int r0 = 0; r0 < m; r0 += kMaxR) {
+            const int R = std::min(kMaxR, m - r0);
+            int per_cu = 0;
+            rc = device_blocks(dev, k, R, 3, 0, &cus, &per_cu);
+            if (rc) return rc;
+            PassArgs a;
+            std::memset(&a, 0, sizeof(a));
+            for (int j = 0; j < k; ++j) {
+                a.in[j] = static_cast<const uint8_t*>(views[j].base);
+                a.in_stride[j] = views[j].obj_stride;
+            }
+            for (int r = 0; r < R; ++r) {
+                a.out[r] = static_cast<uint8_t*>(views[k + r0 + r].base);
+                a.out_stride[r] = views[k + r0 + r].obj_stride;
+                for (int j = 0; j < k; ++j) perm_table(prow[(size_t)(r0 + r) * k + j], a.tab[r][j]);
+            }
+            a.shard_len = shard_len;
+            for (uint64_t o0 = 0; o0 < n_obj; o0 += max_obj) {
+                const uint64_t no = std::min(max_obj, n_obj - o0);
+                PassArgs b = a;
+                for (int j = 0; j < k; ++j) b.in[j] = a.in[j] + o0 * a.in_stride[j];
+                for (int r = 0; r < R; ++r) b.out[r] = a.out[r] + o0 * a.out_stride[r];
+                b.n_obj = no;
+                b.tiles_per_obj = (uint32_t)tpo;
+                b.n_tiles = (uint32_t)(no * tpo);
+                const uint64_t want = (b.n_tiles + kBlockThreads / 64 - 1) / (kBlockThreads / 64);
+                const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cus * per_cu));
+                hipError_t e = launch_verify_unaligned(k, R, b, flags + o0, grid, stream);
+                if (e != hipSuccess) return hip_fail(e, "launch gf_verify_unaligned");
+            }
+        }
+        return HBEC_OK;
+    }
     // generic: recompute parity into scratch, then compare bytewise
     uint8_t* scratch = nullptr;
     const size_t bytes = (size_t)n_obj * m * shard_len;

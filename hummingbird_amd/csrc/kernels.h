@@ -123,6 +123,9 @@ struct UPlanArgs {
     uint32_t tab[kMaxR][kMaxK][5];
 };
 uint32_t unaligned_tile_bytes();
+// Verify at any alignment (k <= kMaxK, <= 4 parity rows per launch): OR 1 into
+// flags[obj] for every object whose stored parity differs from the recomputed.
+hipError_t launch_verify_unaligned(int k, int r, const PassArgs& a, uint32_t* flags, int grid, hipStream_t stream);
 hipError_t launch_unaligned_plan(int k, int r, const UPlanArgs& a, int grid, hipStream_t stream);
 hipError_t launch_fill(uint8_t* dst, uint64_t n_obj, uint64_t obj_len, uint64_t obj_stride, uint64_t base_seed,
                        uint64_t first, int grid, hipStream_t stream);

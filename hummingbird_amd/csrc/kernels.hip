@@ -701,9 +701,12 @@ __device__ __forceinline__ void store_bytes(uint64_t addr, const u32x4& v, uint6
 // One wave tile: U windows from shard position p0 of one object / stripe.
 // in_base(j) / out_base(r) give the byte address of that object's input j /
 // output r shard (wave-uniform); tab(r, j) its coefficient tables.
-template <int R, class InBase, class OutBase, class Tab>
+// VERIFY: compare the coded columns with the stored outputs instead of
+// storing them, and OR 1 into *flag on any mismatching byte (Encoder.Verify).
+template <int R, bool VERIFY = false, class InBase, class OutBase, class Tab>
 __device__ __forceinline__ void unaligned_tile(int K, uint64_t S, uint64_t p0, bool accumulate, uint32_t lane,
-                                               InBase in_base, OutBase out_base, Tab tab) {
+                                               InBase in_base, OutBase out_base, Tab tab,
+                                               uint32_t* flag = nullptr) {
     constexpr int U = kUnalignedU;
     constexpr uint32_t W = kUnalignedWindow;
     uint64_t col[U];
@@ -765,6 +768,33 @@ __device__ __forceinline__ void unaligned_tile(int K, uint64_t S, uint64_t p0, b
             cv = nv;
         }
     }
+    if constexpr (VERIFY) {
+        bool bad = false;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const UView ov = uview(out_base(r), S);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (!live[u]) continue;  // window-uniform (the upper block is a shuffle)
+                u32x4 lo, hi;
+                uload(lo, hi, ov, col[u]);
+                const u32x4 st = realign16(lo, upper(lo, hi), ov.d);
+                // columns [c, c + 16) of this window's lanes; bytes at or past S do not count
+                const uint64_t nv = col[u] < S ? S - col[u] : 0u;
+                if (lane < kUnalignedStoreLanes) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const uint64_t b0 = 4u * e;
+                        const uint32_t mask = nv >= b0 + 4u ? 0xFFFFFFFFu
+                                              : (nv <= b0 ? 0u : (0xFFFFFFFFu >> (8u * (uint32_t)(b0 + 4u - nv))));
+                        bad |= ((acc[r][u][e] ^ st[e]) & mask) != 0u;
+                    }
+                }
+            }
+        }
+        if (bad) atomicOr(flag, 1u);
+        return;
+    }
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const uint64_t ob = out_base(r);
@@ -803,6 +833,26 @@ __global__ __launch_bounds__(kBlockThreads) void gf_apply_unaligned(PassArgs a, 
             [&](int j) { return reinterpret_cast<uint64_t>(a.in[j]) + (uint64_t)obj * a.in_stride[j]; },
             [&](int r) { return reinterpret_cast<uint64_t>(a.out[r]) + (uint64_t)obj * a.out_stride[r]; },
             [&](int r, int j) { return a.tab[r][j]; });
+    }
+}
+
+// Encoder.Verify of views at any alignment: recompute every parity column
+// and compare it with the stored one in the same pass (nothing written).
+template <int R>
+__global__ __launch_bounds__(kBlockThreads) void gf_verify_unaligned(PassArgs a, int K, uint32_t* flags) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave =
+        __builtin_amdgcn_readfirstlane(xcd_block() * (kBlockThreads / 64) + (threadIdx.x >> 6));
+    const uint32_t nwaves = gridDim.x * (kBlockThreads / 64);
+    const uint32_t tpo = a.tiles_per_obj;
+    for (uint32_t t = wave; t < a.n_tiles; t += nwaves) {
+        const uint32_t obj = t / tpo;
+        const uint64_t p0 = (uint64_t)(t - obj * tpo) * (kUnalignedU * kUnalignedWindow);
+        unaligned_tile<R, true>(
+            K, a.shard_len, p0, false, lane,
+            [&](int j) { return reinterpret_cast<uint64_t>(a.in[j]) + (uint64_t)obj * a.in_stride[j]; },
+            [&](int r) { return reinterpret_cast<uint64_t>(a.out[r]) + (uint64_t)obj * a.out_stride[r]; },
+            [&](int r, int j) { return a.tab[r][j]; }, flags + obj);
     }
 }
 
@@ -1061,6 +1111,19 @@ static const void* unaligned_plan_kernel(int r) {
         case 4: return reinterpret_cast<const void*>(&gf_apply_unaligned_plan<4>);
     }
     return nullptr;
+}
+
+hipError_t launch_verify_unaligned(int k, int r, const PassArgs& a, uint32_t* flags, int grid, hipStream_t stream) {
+    const void* fn = nullptr;
+    switch (r) {
+        case 1: fn = reinterpret_cast<const void*>(&gf_verify_unaligned<1>); break;
+        case 2: fn = reinterpret_cast<const void*>(&gf_verify_unaligned<2>); break;
+        case 3: fn = reinterpret_cast<const void*>(&gf_verify_unaligned<3>); break;
+        case 4: fn = reinterpret_cast<const void*>(&gf_verify_unaligned<4>); break;
+    }
+    if (!fn || k < 1 || k > kMaxK) return hipErrorInvalidValue;
+    void* args[] = {const_cast<PassArgs*>(&a), &k, &flags};
+    return hipLaunchKernel(fn, dim3(grid), dim3(kBlockThreads), args, 0, stream);
 }
 
 uint32_t unaligned_tile_bytes() { return (uint32_t)kUnalignedU * kUnalignedWindow; }

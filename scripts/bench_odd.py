@@ -10,6 +10,7 @@ kind, and a Verify self-check (scripts/_common.py: no oracle here).
 from __future__ import annotations
 
 import json
+import os
 import statistics
 import sys
 from pathlib import Path
@@ -57,12 +58,14 @@ def shape(k, m, n, obj_len, layout):
     flags = torch.zeros(n, dtype=torch.int32, device="cuda")
     B.verify_views(enc, views, n, s, flags)
     ok = int(flags.count_nonzero().item()) == 0
+    vms = timeit(lambda: B.verify_views(enc, views, n, s, flags))  # read-only: (k+m)*S read
     nb = n * (k + m) * s
     info = B.kernel_info(k, m, s) if k <= 16 else {}
     print(json.dumps({"k": k, "m": m, "n": n, "obj_len": obj_len, "shard_len": s, "layout": layout,
                       "encode_ms": round(ms, 4), "GB_s": round(nb / ms / 1e6, 1),
                       "frac": round(nb / ms / 1e6 / PEAK, 4), "kind": info.get("kind"),
-                      "verify_ok": ok}), flush=True)
+                      "verify_ms": round(vms, 4), "verify_frac": round(nb / vms / 1e6 / PEAK, 4),
+                      "unaligned_kernel": os.environ.get("HBEC_UNALIGNED", "1"), "verify_ok": ok}), flush=True)
 
 
 def plan_shape(k, m, n, odd):

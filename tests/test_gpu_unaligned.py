@@ -245,3 +245,38 @@ def test_host_pinned_odd_stripes_zero_copy(k, m):
     assert np.array_equal(a, want)
     del stripes
     hb.free()
+
+
+@pytest.mark.parametrize("k,m,s,off", [(4, 2, 1001, 3), (8, 3, 131071, 0), (6, 3, 17, 5), (10, 4, 104858, 1),
+                                       (16, 6, 2015, 9), (17, 3, 333, 2), (3, 2, 1, 15)])
+def test_unaligned_verify_flags_exactly(k, m, s, off):
+    """Encoder.Verify over unaligned views (gf_verify_unaligned; k = 17 takes
+    the recompute-and-compare fallback): clean codewords from the oracle are
+    not flagged; a flipped first / last / middle byte of a parity shard, or of
+    a data shard, flags exactly that object."""
+    n = 12
+    rng = np.random.default_rng(k * 1000 + s)
+    row = (k + m) * s + 5
+    buf = rng.integers(0, 256, off + n * row + 16, dtype=np.uint8)
+    mat = CO.build_matrix(k, m)[k:]
+    for o in range(n):
+        b = off + o * row
+        for r, p in enumerate(CO.apply(mat, [buf[b + j * s:b + (j + 1) * s] for j in range(k)])):
+            buf[b + (k + r) * s:b + (k + r + 1) * s] = p
+    dev = torch.from_numpy(buf).cuda()
+    views = [(dev.data_ptr() + off + i * s, row) for i in range(k + m)]
+    enc = RS.New(k, m)
+    flags = torch.zeros(n, dtype=torch.int32, device="cuda")
+    B.verify_views(enc, views, n, s, flags)
+    torch.cuda.synchronize()
+    assert int(flags.count_nonzero().item()) == 0
+    flips = {1: off + 1 * row + k * s,                      # first byte of parity 0
+             4: off + 4 * row + (k + m) * s - 1,            # last byte of the last parity shard
+             7: off + 7 * row + (k + m - 1) * s + s // 2,   # middle of the last parity shard
+             10: off + 10 * row + s - 1}                    # last byte of data shard 0
+    for pos in flips.values():
+        dev[pos] ^= 0x40
+    flags.zero_()
+    B.verify_views(enc, views, n, s, flags)
+    torch.cuda.synchronize()
+    assert flags.nonzero().flatten().tolist() == sorted(flips)
