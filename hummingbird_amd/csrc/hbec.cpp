@@ -54,6 +54,11 @@ int hip_fail(hipError_t e, const char* what) {
 static std::atomic<int> g_force_stream{0};
 // Views that are not all 16-B aligned (or shards not a multiple of 16 B):
 // gf_apply_unaligned (default) or, with HBEC_UNALIGNED=0, the byte kernel.
+// Tuning knob: resident blocks per CU for the unaligned kernels' grids (0 = occupancy).
+static const int g_unaligned_bpc = [] {
+    const char* e = std::getenv("HBEC_UNALIGNED_BPC");
+    return e ? std::atoi(e) : 0;
+}();
 static const std::atomic<int> g_unaligned_kernel{[] {
     const char* e = std::getenv("HBEC_UNALIGNED");
     return e ? std::atoi(e) : 1;
@@ -229,6 +234,7 @@ int apply_views(int rows, int cols, const uint8_t* coeffs, const hbec_view* in, 
                 int cus = 0, per_cu = 0;
                 rc = device_blocks(dev, K, R, 3, 0, &cus, &per_cu);
                 if (rc) return rc;
+                if (g_unaligned_bpc > 0) per_cu = std::min(per_cu, g_unaligned_bpc);
                 const uint64_t tpo = unaligned_tiles_per_obj(shard_len);
                 const uint64_t max_obj = std::max<uint64_t>(1, std::min<uint64_t>((1ull << 31), g_chunk_tiles) / tpo);
                 for (uint64_t o0 = 0; o0 < n_obj; o0 += max_obj) {
@@ -948,6 +954,7 @@ static int verify_views(hbec_codec* c, const hbec_view* views, uint64_t n_obj, u
             int per_cu = 0;
             rc = device_blocks(dev, k, R, 3, 0, &cus, &per_cu);
             if (rc) return rc;
+            if (g_unaligned_bpc > 0) per_cu = std::min(per_cu, g_unaligned_bpc);
             PassArgs a;
             std::memset(&a, 0, sizeof(a));
             for (int j = 0; j < k; ++j) {

@@ -98,6 +98,8 @@ int hbec::launch_unaligned_passes(const URec* recs, uint64_t n_recs, const std::
         const int R = std::min(hbec::kMaxR, R_all - r0);
         e = hbec::unaligned_occupancy(R, &per_cu);
         if (e != hipSuccess) return hip_fail(e, "unaligned occupancy");
+        if (const char* env = std::getenv("HBEC_UNALIGNED_BPC"))  // tuning knob, as in apply_views
+            if (std::atoi(env) > 0) per_cu = std::min(per_cu, std::atoi(env));
         for (int c0 = 0; c0 < K_all; c0 += hbec::kMaxK) {
             const int K = std::min(hbec::kMaxK, K_all - c0);
             hbec::UPlanArgs a;
