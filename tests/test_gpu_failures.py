@@ -46,12 +46,20 @@ def test_pinned_host_alloc_failure_is_nomem_and_recovers():
 
 
 def test_device_oom_is_nomem_and_next_call_succeeds():
-    """Verify over unaligned views needs an n*m*S scratch buffer in HBM
-    (hbec.cpp verify_views, generic path).  With HBM nearly full that
-    allocation fails: ErrNoMem, no flag set.  With the memory back, the same
-    call and an aligned pipelined encode both succeed."""
-    k, m, n, s = 4, 2, 512, (1 << 20) + 1  # odd shard length: generic path, 1 GiB scratch
+    """Verify with more than 16 data shards over unaligned views needs an
+    n*m*S scratch buffer in HBM (hbec.cpp verify_views, generic path).  With
+    HBM nearly full that allocation fails: ErrNoMem, no flag set, while a
+    4+2 unaligned Verify (gf_verify_unaligned, no scratch) still succeeds.
+    With the memory back, the same call and an aligned pipelined encode both
+    succeed."""
+    k, m, n, s = 17, 2, 512, (1 << 20) + 1  # k > 16, odd shard length: generic path, 1 GiB scratch
     enc = RS.New(k, m)
+    e42, s42 = RS.New(4, 2), 1001
+    small = torch.empty((8, 6 * s42 + 3), dtype=torch.uint8, device="cuda")
+    B.fill_splitmix(small, 6 * s42 + 3)
+    v42 = [(small.data_ptr() + 3 + i * s42, small.stride(0)) for i in range(6)]
+    B.encode_views(e42, v42, 8, s42)
+    f42 = torch.zeros(8, dtype=torch.int32, device="cuda")
     objs = torch.empty((n, k * s + 1), dtype=torch.uint8, device="cuda")
     B.fill_splitmix(objs, k * s + 1)
     parity = torch.empty((n, m * s + 1), dtype=torch.uint8, device="cuda")
@@ -73,7 +81,9 @@ def test_device_oom_is_nomem_and_next_call_succeeds():
     try:
         with pytest.raises(RS.ErrNoMem):
             B.verify_views(enc, views, n, s, flags)
+        B.verify_views(e42, v42, 8, s42, f42)
         torch.cuda.synchronize()
+        assert int(f42.count_nonzero()) == 0
     finally:
         del hog
         torch.cuda.empty_cache()
