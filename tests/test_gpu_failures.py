@@ -95,7 +95,7 @@ def test_device_oom_is_nomem_and_next_call_succeeds():
     a = torch.empty((64, 4 << 18), dtype=torch.uint8, device="cuda")
     B.fill_splitmix(a, 4 << 18)
     p = torch.empty((64, 2 << 18), dtype=torch.uint8, device="cuda")
-    B.encode_objects(enc, a, p, 1 << 18)  # aligned: the pipelined kernel launch check
+    B.encode_objects(e42, a, p, 1 << 18)  # aligned 4+2: the pipelined kernel launch check
     torch.cuda.synchronize()
-    want, _ = CO.encode_batch(k, m, a[:2].cpu().numpy())
+    want, _ = CO.encode_batch(4, 2, a[:2].cpu().numpy())
     assert np.array_equal(p[:2].cpu().numpy(), want)
