@@ -15,7 +15,8 @@
  * After every write operation the stripe is verified (hbec_verify_databuf)
  * and every rebuilt shard compared with a saved copy, so a wrong byte, a
  * lost wake-up (hang: the run is under `timeout`) or a crash ends the run.
- * Sizes mix 4 KiB and 1 MiB objects, 4+2.  Prints one JSON line.
+ * Sizes mix 4 KiB and 1 MiB objects with odd-sized ones (S % 16 != 0:
+ * shards at odd offsets, the unaligned kernels), 4+2.  Prints one JSON line.
  *
  *   gcc -O2 -std=c11 -pthread -Iinclude scripts/soak.c -Lhummingbird_amd -lhbec \
  *       -Wl,-rpath,$PWD/hummingbird_amd -o gpurun_out/soak
@@ -160,7 +161,8 @@ int main(int argc, char** argv) {
         j->pinned = t % 2 == 0;
         j->rng = seed + (uint64_t)t * 7919u;
         for (int i = 0; i < PER; ++i) {
-            j->s[i] = (i % 3 == 0) ? (1u << 18) : 1024u;  /* 1 MiB or 4 KiB objects */
+            static const size_t sizes[PER] = {1u << 18, 1024u, 262141u, 1027u, 1024u, 333u};
+            j->s[i] = sizes[i];  /* 1 MiB, 4 KiB and odd-sized objects */
             const size_t bytes = N * j->s[i];
             if (j->pinned) {
                 if (hbec_host_alloc(bytes, (void**)&j->base[i])) {
