@@ -210,7 +210,8 @@ int hbec_fill_splitmix(void* dst, uint64_t n_objects, uint64_t obj_len, uint64_t
  * shard_len bytes back to back at base, data first.  The plan (built
  * synchronously, device memory) records the stripes' addresses: the buffers
  * must stay allocated while work queued with the plan runs.  Stripes whose
- * base or shard_len is not 16-B aligned are coded one by one.
+ * base or shard_len is not 16-B aligned (most object sizes) are coded by one
+ * more launch per pass of the unaligned kernel over their own records.
  * ------------------------------------------------------------------------- */
 typedef struct {
     void* base;
@@ -247,9 +248,10 @@ int hbec_reconstruct_plan(hbec_codec* codec, const hbec_plan* plan, const uint8_
  * caller's stripes.  Any k (k > 8 runs in accumulate passes).  Concurrent
  * calls share at most HBEC_HOST_RINGS (8) rings per device and wait for one
  * beyond that.  Env: HBEC_HOST_SLOT_MB (64), HBEC_HOST_THREADS.
- * Zero-copy: 16-B-aligned stripes in pinned, device-mapped host memory are
- * coded IN PLACE by the GPU over PCIe — no staging copies, no CPU
- * gather/scatter (HBEC_ZEROCOPY=0 sends them through the ring too).
+ * Zero-copy: stripes in pinned, device-mapped host memory are coded IN PLACE
+ * by the GPU over PCIe — no staging copies, no CPU gather/scatter — at any
+ * alignment and shard length (unaligned ones through the unaligned kernel;
+ * HBEC_ZC_UNALIGNED=0 stages those, HBEC_ZEROCOPY=0 stages every stripe).
  * hbec_host_alloc memory qualifies on every device; memory pinned elsewhere
  * (hipHostMalloc, hipHostRegister) on the device it was pinned for.  Not for
  * hbec_encode_host_md5. */
