@@ -391,6 +391,51 @@ def small_objects(n=65536, obj_len=4096, reps=100, settle=200):
     return out
 
 
+def odd_objects(n=4096, obj_len=(1 << 20) - 4, reps=20, settle=40):
+    """Objects of arbitrary size: ecSplit's S = ceil(len / k) is a multiple of
+    16 for one object size in 16 (objectserver/ecutils.go:14-24), and its
+    databuf puts shard i at i*S (ecutils.go:31-35), so most objects reach the
+    codec as shards at odd offsets.  n ecSplit databufs of 1 MiB - 4 B objects
+    (4+2, S = 262 143), device-resident: Encode, Reconstruct of shards {0,1}
+    in place, Verify (gf_apply_unaligned / gf_verify_unaligned).  Rebuilt
+    shards must equal the originals and Verify must pass every object."""
+    k, m = 4, 2
+    s = -(-obj_len // k)
+    enc = RS.New(k, m)
+    rows = torch.empty((n, (k + m) * s), dtype=torch.uint8, device="cuda")
+    B.fill_splitmix(rows, (k + m) * s, first=1 << 21)
+    views = B.shard_views(rows, k + m, s)
+    flags = torch.zeros(n, dtype=torch.int32, device="cuda")
+    present = [0, 0] + [1] * (k + m - 2)
+    nbytes = n * (k + m) * s
+    stream = torch.cuda.current_stream()
+    B.encode_views(enc, views, n, s)
+    keep = rows[:, :2 * s].clone()
+    ops = {"encode": lambda: B.encode_views(enc, views, n, s),
+           "reconstruct": lambda: B.reconstruct_views(enc, views, present, n, s),
+           "verify": lambda: B.verify_views(enc, views, n, s, flags)}
+    out = {"workload": f"4+2, {n} ecSplit databufs of {obj_len} B objects (S = {s}, shards at odd offsets), "
+                       "device-resident", "shard_bytes": s}
+    for _ in range(settle):
+        ops["encode"]()
+    for name, fn in ops.items():
+        for _ in range(3):
+            fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            fn()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        gbs = nbytes / (ms * 1e-3) / 1e9
+        out[name] = {"ms": round(ms, 4), "GB_s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
+    out["parity_ok"] = bool(int(flags.count_nonzero()) == 0 and torch.equal(rows[:, :2 * s], keep))
+    del rows, keep, flags
+    torch.cuda.empty_cache()
+    return out
+
+
 def config4(n=4096, reps=20, settle=40):
     """BASELINE configs[3]: 8+3 Encode + Reconstruct{0,1,2} of n objects of
     4 KiB or 1 MiB (p = 0.5 each, by the splitmix64 byte stream of the base
@@ -709,6 +754,10 @@ def main(argv=None):
             line["config4"] = config4()
         except Exception as e:  # noqa: BLE001 - reported; never blocks the other ranks
             line["config4"] = {"error": f"{type(e).__name__}: {e}"[:200]}
+        try:
+            line["odd_objects"] = odd_objects()
+        except Exception as e:  # noqa: BLE001 - reported; never blocks the other ranks
+            line["odd_objects"] = {"error": f"{type(e).__name__}: {e}"[:200]}
     if world > 1 and backend == "nccl" and args.split_objects > 0:
         split = batch_split(pg, k, m, obj_len, args.split_objects, world, rank, ctl_device)
         if rank == 0:

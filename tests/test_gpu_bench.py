@@ -27,3 +27,5 @@ def test_bench_line_small(capsys):
     assert d["config5"]["parity_ok"] and d["config5"]["objects"] == 512
     assert d["config4"]["parity_ok"] and 0 < d["config4"]["frac"] < 1
     assert all(sh["parity_ok"] for sh in d["small_objects"]["shapes"])
+    assert d["odd_objects"]["parity_ok"] and d["odd_objects"]["shard_bytes"] % 16 != 0
+    assert all(0 < d["odd_objects"][op]["frac"] < 1 for op in ("encode", "reconstruct", "verify"))
