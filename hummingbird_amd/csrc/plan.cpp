@@ -2,9 +2,10 @@
 // one launch (stripes.hip).  A stripe is ecSplit's databuf layout
 // (objectserver/ecutils.go:31-35,55-58): k+m shards of shard_len bytes back
 // to back, data first.  Stripes the tiled kernel cannot take (unaligned:
-// S % 16 != 0 for 15 object sizes in 16; or object plans beyond 8 inputs) are
-// coded by one more launch per pass of gf_apply_unaligned_plan over their own
-// records; stripe plans with k > 8 run the tiled kernel in accumulate passes.
+// S % 16 != 0 for 15 object sizes in 16; every object of an object plan with
+// k > 8) are coded by one more launch per pass of gf_apply_unaligned_plan over
+// their own records; stripe plans with k > 8 run the tiled kernel in
+// accumulate passes.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -49,12 +50,6 @@ bool aligned_stripe(const hbec_stripe& s) {
 bool aligned_object(const hbec_object& o) {
     return ((reinterpret_cast<uintptr_t>(o.data) | reinterpret_cast<uintptr_t>(o.parity)) & 15u) == 0 &&
            (o.shard_len % 16) == 0 && o.shard_len < (1ull << 32);
-}
-
-// Shard i of an object: data shard i (i < k) or parity shard i - k.
-uint8_t* object_shard(const hbec_object& o, int k, int i) {
-    return i < k ? static_cast<uint8_t*>(o.data) + (uint64_t)i * o.shard_len
-                 : static_cast<uint8_t*>(o.parity) + (uint64_t)(i - k) * o.shard_len;
 }
 
 std::mutex g_occ_mu;
@@ -220,16 +215,6 @@ int hbec::launch_stripe_passes(const TileRec* tiles, uint64_t n_tiles, const std
 
 namespace {
 
-// Codes one object of an object plan through the generic strided path.
-int apply_one_object(const hbec_object& o, int k, const std::vector<int>& in_idx, const std::vector<int>& out_idx,
-                     const uint8_t* rows, hipStream_t stream) {
-    std::vector<hbec_view> vin(in_idx.size()), vout(out_idx.size());
-    for (size_t j = 0; j < in_idx.size(); ++j) vin[j] = {object_shard(o, k, in_idx[j]), 0};
-    for (size_t r = 0; r < out_idx.size(); ++r) vout[r] = {object_shard(o, k, out_idx[r]), 0};
-    return hbec::apply_views((int)out_idx.size(), (int)in_idx.size(), rows, vin.data(), vout.data(), 1, o.shard_len,
-                             stream);
-}
-
 // out rows (given as shard indices + coefficient rows over in_idx) for every stripe
 int run_plan(const hbec_plan* p, const std::vector<int>& in_idx, const std::vector<int>& out_idx,
              const std::vector<uint8_t>& rows, hipStream_t stream) {
@@ -245,12 +230,7 @@ int run_plan(const hbec_plan* p, const std::vector<int>& in_idx, const std::vect
         if (rc) return rc;
     }
     if (p->objects) {
-        if (!tiled_ok) {
-            for (const auto& o : p->obj_tiled) {
-                int rc = apply_one_object(o, p->k, in_idx, out_idx, rows.data(), stream);
-                if (rc) return rc;
-            }
-        }
+        // with k > 8 every object is in the unaligned records (hbec_plan_objects)
         return hbec::launch_unaligned_passes(p->d_urecs, p->n_urecs, in_idx, out_idx, rows, p->k, stream);
     }
     return hbec::launch_unaligned_passes(p->d_urecs, p->n_urecs, in_idx, out_idx, rows, 0, stream);
@@ -336,6 +316,12 @@ int hbec_plan_objects(hbec_codec* codec, const hbec_object* objects, uint64_t n,
             p->shard_bytes += o.shard_len;
             if (!aligned_object(o)) {
                 p->obj_fallback.push_back(o);
+                add_urecs(urecs, o.data, o.parity, o.shard_len);
+                continue;
+            }
+            if (k > hbec::kStripeMaxK) {
+                // the object-plan tiled kernel takes <= 8 inputs: every object goes to
+                // the unaligned kernel's records (one launch per pass, not one per object)
                 add_urecs(urecs, o.data, o.parity, o.shard_len);
                 continue;
             }
