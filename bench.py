@@ -430,6 +430,13 @@ def odd_objects(n=4096, obj_len=(1 << 20) - 4, reps=20, settle=40):
         ms = e0.elapsed_time(e1) / reps
         gbs = nbytes / (ms * 1e-3) / 1e9
         out[name] = {"ms": round(ms, 4), "GB_s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
+    # the check: erase shards 0-1 of every object for real, rebuild them, and
+    # Verify every object (a reconstruct that wrote nothing would fail here)
+    rows[:, :2 * s].fill_(0x3C)
+    ops["reconstruct"]()
+    flags.zero_()
+    ops["verify"]()
+    torch.cuda.synchronize()
     out["parity_ok"] = bool(int(flags.count_nonzero()) == 0 and torch.equal(rows[:, :2 * s], keep))
     del rows, keep, flags
     torch.cuda.empty_cache()

@@ -107,7 +107,7 @@ _SIG = [
     ("hbec_set_force_stream", C.c_int, [C.c_int]),
     ("hbec_kernel_info", C.c_int,
      [C.c_int, C.c_int, C.c_uint64, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
-    ("hbec_ec_shard_length", C.c_int64, [C.c_int64, C.c_int]),
+    ("hbec_ec_shard_length", C.c_int64, [C.c_int64, C.c_int64]),
     ("hbec_ec_split", C.c_int, [C.c_int, C.c_int, READ_FN, _P, C.c_int, C.c_int64, WRITE_FN, C.POINTER(_P)]),
     ("hbec_ec_reconstruct", C.c_int,
      [C.c_int, C.c_int, READ_FN, C.POINTER(_P), C.c_int, C.c_int64, WRITE_FN, C.POINTER(_P),

@@ -246,7 +246,7 @@ int wait_slot(const Ring& r, int b) {
 
 extern "C" {
 
-int64_t hbec_ec_shard_length(int64_t length, int data_shards) {
+int64_t hbec_ec_shard_length(int64_t length, int64_t data_shards) {
     if (length < 0) return 0;
     if (data_shards <= 0) return 0;
     const int64_t shards = data_shards;

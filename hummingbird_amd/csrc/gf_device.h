@@ -79,6 +79,29 @@ __device__ __forceinline__ void st16_addr(uint64_t addr, u32x4 v) {
 #endif
 }
 
+// Lane l receives lane l+1's value (DPP wave_shl:1, a VALU move; lane 63
+// gets 0).  Replaces ds_bpermute, which goes through the LDS pipe.
+__device__ __forceinline__ uint32_t lane_next(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, true);
+}
+
+__device__ __forceinline__ u32x4 lane_next4(const u32x4& v) {
+    return u32x4{lane_next(v[0]), lane_next(v[1]), lane_next(v[2]), lane_next(v[3])};
+}
+
+// Bytes [d, d + 16) of the 32 bytes lo:hi, d wave-uniform in [0, 16): the
+// 5 source dwords are selected by d's bits 3 and 2 (v_cndmask on a uniform
+// condition), then v_alignbyte_b32(a, b, s) = ({a, b} >> 8s)[31:0] shifts.
+__device__ __forceinline__ u32x4 realign16(const u32x4& lo, const u32x4& hi, uint32_t d) {
+    const uint32_t sh = d & 3u;
+    const bool b2 = (d & 8u) != 0, b1 = (d & 4u) != 0;
+    const uint32_t t0 = b2 ? lo[2] : lo[0], t1 = b2 ? lo[3] : lo[1], t2 = b2 ? hi[0] : lo[2];
+    const uint32_t t3 = b2 ? hi[1] : lo[3], t4 = b2 ? hi[2] : hi[0], t5 = b2 ? hi[3] : hi[1];
+    const uint32_t s0 = b1 ? t1 : t0, s1 = b1 ? t2 : t1, s2 = b1 ? t3 : t2, s3 = b1 ? t4 : t3, s4 = b1 ? t5 : t4;
+    return u32x4{__builtin_amdgcn_alignbyte(s1, s0, sh), __builtin_amdgcn_alignbyte(s2, s1, sh),
+                 __builtin_amdgcn_alignbyte(s3, s2, sh), __builtin_amdgcn_alignbyte(s4, s3, sh)};
+}
+
 struct Sel {
     uint32_t s0, s1, s2;
 };
@@ -115,11 +138,14 @@ __device__ __forceinline__ uint32_t gf_mul_sel(const Sel& s, uint32_t t0, uint32
 #define HBEC_ALLVGPR_MIN 16  // K*R at or above which all 5 table words live in VGPRs (SGPR spills otherwise)
 #endif
 
-template <int K, int R>
+// VMIN: K*R at or above which the high words live in VGPRs too (kernels
+// with many scalar live values pass 1: all five words in VGPRs)
+template <int K, int R, int VMIN = HBEC_ALLVGPR_MIN>
 struct Tables {
+    static constexpr bool kAllV = K * R >= VMIN;
     uint32_t lo0[R][K];
     uint32_t lo2[R][K];
-    uint32_t hi[K * R >= HBEC_ALLVGPR_MIN ? R : 1][K * R >= HBEC_ALLVGPR_MIN ? K : 1][3];
+    uint32_t hi[kAllV ? R : 1][kAllV ? K : 1][3];
 };
 
 __device__ __forceinline__ uint32_t to_vgpr(uint32_t x) {
@@ -134,16 +160,16 @@ __device__ __forceinline__ uint32_t to_vgpr(uint32_t x) {
 
 typedef uint32_t TabArray[kMaxR][kMaxK][5];
 
-template <int K, int R>
-__device__ __forceinline__ Tables<K, R> load_tables(const TabArray& tab) {
-    Tables<K, R> t;
+template <int K, int R, int VMIN = HBEC_ALLVGPR_MIN>
+__device__ __forceinline__ Tables<K, R, VMIN> load_tables(const TabArray& tab) {
+    Tables<K, R, VMIN> t;
 #pragma unroll
     for (int r = 0; r < R; ++r)
 #pragma unroll
         for (int j = 0; j < K; ++j) {
             t.lo0[r][j] = to_vgpr(tab[r][j][0]);
             t.lo2[r][j] = to_vgpr(tab[r][j][2]);
-            if constexpr (K * R >= HBEC_ALLVGPR_MIN) {
+            if constexpr (Tables<K, R, VMIN>::kAllV) {
                 t.hi[r][j][0] = to_vgpr(tab[r][j][1]);
                 t.hi[r][j][1] = to_vgpr(tab[r][j][3]);
                 t.hi[r][j][2] = to_vgpr(tab[r][j][4]);
@@ -158,9 +184,9 @@ __device__ __forceinline__ Tables<K, R> load_tables(const TabArray& tab) {
 #ifndef HBEC_GF_NONE
 #define HBEC_GF_NONE 0  // tuning only: plain XOR of the inputs (same loads / stores, no field multiply)
 #endif
-template <int K, int R>
+template <int K, int R, int VMIN = HBEC_ALLVGPR_MIN>
 __device__ __forceinline__ void gf_dot(u32x4 (&acc)[R], const u32x4 (&x)[K], const TabArray& tab,
-                                       const Tables<K, R>& tb) {
+                                       const Tables<K, R, VMIN>& tb) {
     if constexpr (HBEC_GF_NONE != 0) {
 #pragma unroll
         for (int r = 0; r < R; ++r)
@@ -178,7 +204,7 @@ __device__ __forceinline__ void gf_dot(u32x4 (&acc)[R], const u32x4 (&x)[K], con
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 uint32_t h1, h3, h4;
-                if constexpr (K * R >= HBEC_ALLVGPR_MIN) {
+                if constexpr (Tables<K, R, VMIN>::kAllV) {
                     h1 = tb.hi[r][j][0];
                     h3 = tb.hi[r][j][1];
                     h4 = tb.hi[r][j][2];

@@ -137,6 +137,69 @@ static int device_blocks(int dev, int k, int r, int pipe, int force_stream, int*
 }
 
 // ---------------------------------------------------------------------------
+// Shards at any alignment (gf_odd, odd.hip)
+// ---------------------------------------------------------------------------
+static int cu_count(int dev, int* cus) {
+    std::lock_guard<std::mutex> g(g_dev_mu);
+    DeviceInfo& d = g_devs[dev];
+    if (d.cus == 0) {
+        hipDeviceProp_t p;
+        hipError_t e = hipGetDeviceProperties(&p, dev);
+        if (e != hipSuccess) return hip_fail(e, "hipGetDeviceProperties");
+        d.cus = p.multiProcessorCount;
+    }
+    *cus = d.cus;
+    return HBEC_OK;
+}
+
+// One pass of a (K <= kMaxK inputs, R <= kMaxR outputs) over strided views at
+// any alignment, as launches of <= kOddMaxK inputs: the first accumulates
+// only when `accumulate`, the later ones always.  mode 2 (verify) flags
+// objects instead of writing (K <= kOddMaxK).  One 4-wave block per CU (the
+// pipelined kernels' HBM sweet spot), launches of <= g_chunk_tiles tiles.
+static int odd_launches(const PassArgs& a, int K, int R, int mode, bool accumulate, uint64_t n_obj,
+                        uint64_t shard_len, uint32_t* flags, int dev, hipStream_t stream) {
+    int cus = 0;
+    int rc = cu_count(dev, &cus);
+    if (rc) return rc;
+    cus *= odd_blocks_per_cu();
+    for (int c1 = 0; c1 < K; c1 += kOddMaxK) {
+        const int K1 = std::min(kOddMaxK, K - c1);
+        PassArgs b = a;
+        for (int j = 0; j < K1; ++j) {
+            b.in[j] = a.in[c1 + j];
+            b.in_stride[j] = a.in_stride[c1 + j];
+            for (int r = 0; r < R; ++r)
+                for (int q = 0; q < 5; ++q) b.tab[r][j][q] = a.tab[r][c1 + j][q];
+        }
+        const int m = mode == 2 ? 2 : ((accumulate || c1 > 0) ? 1 : 0);
+        const uint64_t tpo = odd_tiles_per_obj(K1, shard_len);
+        const uint64_t max_obj = std::max<uint64_t>(1, std::min<uint64_t>((1ull << 31), g_chunk_tiles) / tpo);
+        for (uint64_t o0 = 0; o0 < n_obj; o0 += max_obj) {
+            const uint64_t no = std::min(max_obj, n_obj - o0);
+            PassArgs c = b;
+            for (int j = 0; j < K1; ++j) c.in[j] = b.in[j] + o0 * b.in_stride[j];
+            for (int r = 0; r < R; ++r) c.out[r] = b.out[r] + o0 * b.out_stride[r];
+            c.n_obj = no;
+            c.shard_len = shard_len;
+            c.tiles_per_obj = (uint32_t)tpo;
+            c.n_tiles = (uint32_t)(no * tpo);
+            const uint64_t want = (c.n_tiles + 3) / 4;
+            int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cus));
+            if (g_grid_cap > 0) grid = std::min(grid, g_grid_cap);
+            hipError_t e = launch_odd(K1, R, m, c, flags ? flags + o0 : nullptr, grid, stream);
+            if (e != hipSuccess) return hip_fail(e, "launch gf_odd");
+        }
+    }
+    return HBEC_OK;
+}
+
+static int apply_odd(const PassArgs& a, int K, int R, bool accumulate, uint64_t n_obj, uint64_t shard_len, int dev,
+                     hipStream_t stream) {
+    return odd_launches(a, K, R, 0, accumulate, n_obj, shard_len, nullptr, dev, stream);
+}
+
+// ---------------------------------------------------------------------------
 // Generic pass planner: out[R] (^)= C[R][K] x in[K] over strided views
 // ---------------------------------------------------------------------------
 static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
@@ -229,6 +292,11 @@ int apply_views(int rows, int cols, const uint8_t* coeffs, const hbec_view* in, 
                     hipError_t e = launch_vec(K, R, b, grid, stream, force_stream);
                     if (e != hipSuccess) return hip_fail(e, "launch gf_apply_vec");
                 }
+            } else if (g_unaligned_kernel.load() && odd_enabled()) {
+                // any alignment / length: gf_odd (odd.hip), passes of <= 8 inputs,
+                // later ones accumulating into the outputs
+                rc = apply_odd(a, K, R, c0 > 0, n_obj, shard_len, dev, stream);
+                if (rc) return rc;
             } else if (g_unaligned_kernel.load()) {
                 // any alignment: aligned 16-B accesses with in-register shifts (gf_apply_unaligned)
                 int cus = 0, per_cu = 0;
@@ -939,6 +1007,29 @@ static int verify_views(hbec_codec* c, const hbec_view* views, uint64_t n_obj, u
             const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cus * bpc));
             hipError_t e = launch_verify(k, m, b, flags + o0, grid, stream);
             if (e != hipSuccess) return hip_fail(e, "launch gf_verify_pipe");
+        }
+        return HBEC_OK;
+    }
+    if (g_unaligned_kernel.load() && odd_enabled() && k <= kOddMaxK) {
+        // any alignment: recompute and compare in one pass (gf_odd verify), <= 4 rows per launch
+        int dev = 0;
+        int rc = current_device(&dev);
+        if (rc) return rc;
+        for (int r0 = 0; r0 < m; r0 += kMaxR) {
+            const int R = std::min(kMaxR, m - r0);
+            PassArgs a;
+            std::memset(&a, 0, sizeof(a));
+            for (int j = 0; j < k; ++j) {
+                a.in[j] = static_cast<const uint8_t*>(views[j].base);
+                a.in_stride[j] = views[j].obj_stride;
+            }
+            for (int r = 0; r < R; ++r) {
+                a.out[r] = static_cast<uint8_t*>(views[k + r0 + r].base);
+                a.out_stride[r] = views[k + r0 + r].obj_stride;
+                for (int j = 0; j < k; ++j) perm_table(prow[(size_t)(r0 + r) * k + j], a.tab[r][j]);
+            }
+            rc = odd_launches(a, k, R, 2, false, n_obj, shard_len, flags, dev, stream);
+            if (rc) return rc;
         }
         return HBEC_OK;
     }

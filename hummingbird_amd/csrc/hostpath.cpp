@@ -494,7 +494,7 @@ int zero_copy_run(Ring* ring, const std::vector<ZcStripe>& zs, const std::vector
 int zero_copy_unaligned_run(Ring* ring, const std::vector<ZcStripe>& zs, const std::vector<int>& in_idx,
                             const std::vector<int>& out_idx, const std::vector<uint8_t>& rows) {
     static_assert(sizeof(hbec::URec) == sizeof(hbec::TileRec), "record slots are shared");
-    const uint64_t tile = hbec::unaligned_tile_bytes();
+    const uint64_t tile = hbec::urec_tile();
     size_t si = 0;
     uint64_t off = 0;
     hipError_t e = hipSuccess;
@@ -508,7 +508,7 @@ int zero_copy_unaligned_run(Ring* ring, const std::vector<ZcStripe>& zs, const s
             const ZcStripe& z = zs[si];
             rec[nt++] = {z.dev, 0, z.shard_len, off};
             off += tile;
-            if (off >= z.shard_len) {
+            if (off >= hbec::urec_span(z.shard_len)) {
                 off = 0;
                 ++si;
             }

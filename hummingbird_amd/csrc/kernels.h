@@ -127,6 +127,30 @@ uint32_t unaligned_tile_bytes();
 // flags[obj] for every object whose stored parity differs from the recomputed.
 hipError_t launch_verify_unaligned(int k, int r, const PassArgs& a, uint32_t* flags, int grid, hipStream_t stream);
 hipError_t launch_unaligned_plan(int k, int r, const UPlanArgs& a, int grid, hipStream_t stream);
+// ---- odd.hip: shards at any byte offset / of any length (round 3) ----
+// Aligned 16-B loads and stores only, shifted into one byte frame in
+// registers (DPP lane shift + v_alignbyte); compile-time K <= kOddMaxK,
+// <= kMaxR outputs; the gf_apply_vec_pipe2 schedule.  Modes: 0 apply,
+// 1 accumulate (out ^= ..., later passes of k > kOddMaxK), 2 verify (flag
+// objects whose stored parity differs; nothing written).
+constexpr int kOddMaxK = 8;
+// HBEC_ODD=1 / 0 selects gf_odd or the round-2 kernels (gf_apply_unaligned
+// family) for odd shards (default: HBEC_ODD_DEFAULT).
+bool odd_enabled();
+// 4-wave blocks per CU of the gf_odd grids (HBEC_ODD_BPC, tuning)
+int odd_blocks_per_cu();
+bool odd_supported(int k, int r);
+// Unaligned plan records (URec) of one stripe / object: p0 = 0, tile, 2*tile,
+// ... while p0 < urec_span(S), for whichever kernel family codes them.
+uint64_t urec_tile();
+uint64_t urec_span(uint64_t shard_len);
+uint32_t odd_tile_bytes(int k);       // shard bytes per wave tile of the strided kernel
+uint32_t odd_plan_tile_bytes();       // shard bytes per plan record
+uint32_t odd_tiles_per_obj(int k, uint64_t shard_len);
+hipError_t launch_odd(int k, int r, int mode, const PassArgs& a, uint32_t* flags, int grid, hipStream_t stream);
+// plan records: URec.p0 = first window * 992 (records cover positions [0, S + 32))
+hipError_t launch_odd_plan(int k, int r, int mode, const UPlanArgs& p, int grid, hipStream_t stream);
+
 hipError_t launch_fill(uint8_t* dst, uint64_t n_obj, uint64_t obj_len, uint64_t obj_stride, uint64_t base_seed,
                        uint64_t first, int grid, hipStream_t stream);
 hipError_t vec_occupancy(int k, int r, int pipe, int force_stream, int* blocks_per_cu);

@@ -630,26 +630,18 @@ constexpr uint32_t kUnalignedWindow = HBEC_UNALIGNED_SHFL ? 992 : 1008;
 constexpr uint32_t kUnalignedStoreLanes = HBEC_UNALIGNED_SHFL ? 62 : 63;
 constexpr int kUnalignedU = HBEC_UNALIGNED_U;  // windows per wave tile (loads in flight)
 
-// bytes [d, d + 16) of the 32 bytes lo:hi, d wave-uniform in [0, 16)
-__device__ __forceinline__ u32x4 realign16(const u32x4& lo, const u32x4& hi, uint32_t d) {
+// bytes [d, d + 16) of the 32 bytes lo:hi (gf_device.h realign16), or the
+// uniform-switch form of the same selection (tuning: HBEC_REALIGN_SEL=0)
+__device__ __forceinline__ u32x4 realign16_k(const u32x4& lo, const u32x4& hi, uint32_t d) {
+    if (HBEC_REALIGN_SEL) return realign16(lo, hi, d);
     const uint32_t sh = d & 3u;
     uint32_t s0, s1, s2, s3, s4;
-    if (HBEC_REALIGN_SEL) {
-        const bool b2 = (d & 8u) != 0, b1 = (d & 4u) != 0;
-        const uint32_t t0 = b2 ? lo[2] : lo[0], t1 = b2 ? lo[3] : lo[1], t2 = b2 ? hi[0] : lo[2];
-        const uint32_t t3 = b2 ? hi[1] : lo[3], t4 = b2 ? hi[2] : hi[0], t5 = b2 ? hi[3] : hi[1];
-        s0 = b1 ? t1 : t0;
-        s1 = b1 ? t2 : t1;
-        s2 = b1 ? t3 : t2;
-        s3 = b1 ? t4 : t3;
-        s4 = b1 ? t5 : t4;
-    } else switch (d >> 2) {
+    switch (d >> 2) {
         case 0: s0 = lo[0]; s1 = lo[1]; s2 = lo[2]; s3 = lo[3]; s4 = hi[0]; break;
         case 1: s0 = lo[1]; s1 = lo[2]; s2 = lo[3]; s3 = hi[0]; s4 = hi[1]; break;
         case 2: s0 = lo[2]; s1 = lo[3]; s2 = hi[0]; s3 = hi[1]; s4 = hi[2]; break;
         default: s0 = lo[3]; s1 = hi[0]; s2 = hi[1]; s3 = hi[2]; s4 = hi[3]; break;
     }
-    // v_alignbyte_b32(a, b, s) = ({a, b} >> 8s)[31:0]
     return u32x4{__builtin_amdgcn_alignbyte(s1, s0, sh), __builtin_amdgcn_alignbyte(s2, s1, sh),
                  __builtin_amdgcn_alignbyte(s3, s2, sh), __builtin_amdgcn_alignbyte(s4, s3, sh)};
 }
@@ -726,7 +718,7 @@ __device__ __forceinline__ void unaligned_tile(int K, uint64_t S, uint64_t p0, b
             if (accumulate) {  // kernel-uniform; clamped loads need no per-window branch
                 u32x4 lo, hi;
                 uload(lo, hi, ov, col[u]);
-                acc[r][u] = realign16(lo, upper(lo, hi), ov.d);
+                acc[r][u] = realign16_k(lo, upper(lo, hi), ov.d);
             }
         }
     }
@@ -750,7 +742,7 @@ __device__ __forceinline__ void unaligned_tile(int K, uint64_t S, uint64_t p0, b
             for (int q = 0; q < 5; ++q) tb[r][q] = tab(r, j)[q];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const u32x4 x = realign16(clo[u], upper(clo[u], chi[u]), cv.d);
+            const u32x4 x = realign16_k(clo[u], upper(clo[u], chi[u]), cv.d);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const Sel sx = selectors(x[e]);
@@ -778,7 +770,7 @@ __device__ __forceinline__ void unaligned_tile(int K, uint64_t S, uint64_t p0, b
                 if (!live[u]) continue;  // window-uniform (the upper block is a shuffle)
                 u32x4 lo, hi;
                 uload(lo, hi, ov, col[u]);
-                const u32x4 st = realign16(lo, upper(lo, hi), ov.d);
+                const u32x4 st = realign16_k(lo, upper(lo, hi), ov.d);
                 // columns [c, c + 16) of this window's lanes; bytes at or past S do not count
                 const uint64_t nv = col[u] < S ? S - col[u] : 0u;
                 if (lane < kUnalignedStoreLanes) {
@@ -805,7 +797,7 @@ __device__ __forceinline__ void unaligned_tile(int K, uint64_t S, uint64_t p0, b
             u32x4 nb;
 #pragma unroll
             for (int i = 0; i < 4; ++i) nb[i] = __shfl_down(acc[r][u][i], 1u, 64);
-            const u32x4 blk = realign16(acc[r][u], nb, e);
+            const u32x4 blk = realign16_k(acc[r][u], nb, e);
             const uint64_t q = col[u] + e;  // block start (shard position); ob + q is 16-B aligned
             if (lane < kUnalignedStoreLanes && q < S) {
                 if (q + 16u <= S)

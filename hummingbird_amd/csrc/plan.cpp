@@ -55,8 +55,8 @@ bool aligned_object(const hbec_object& o) {
 std::mutex g_occ_mu;
 
 void add_urecs(std::vector<hbec::URec>& recs, const void* a, const void* b, uint64_t s) {
-    const uint64_t tile = hbec::unaligned_tile_bytes();
-    for (uint64_t p0 = 0; p0 < s; p0 += tile)
+    const uint64_t tile = hbec::urec_tile(), span = hbec::urec_span(s);
+    for (uint64_t p0 = 0; p0 < span; p0 += tile)
         recs.push_back({reinterpret_cast<uint64_t>(a), reinterpret_cast<uint64_t>(b), s, p0});
 }
 
@@ -89,6 +89,46 @@ int hbec::launch_unaligned_passes(const URec* recs, uint64_t n_recs, const std::
     if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
     e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (e != hipSuccess) return hip_fail(e, "hipDeviceGetAttribute");
+    if (hbec::odd_enabled()) {
+        // gf_odd_plan: launches of <= 4 outputs x <= 8 inputs, later input
+        // launches accumulating; one 4-wave block per CU
+        for (int r0 = 0; r0 < R_all; r0 += hbec::kMaxR) {
+            const int R = std::min(hbec::kMaxR, R_all - r0);
+            for (int c0 = 0; c0 < K_all; c0 += hbec::kOddMaxK) {
+                const int K = std::min(hbec::kOddMaxK, K_all - c0);
+                hbec::UPlanArgs a;
+                std::memset(&a, 0, sizeof(a));
+                a.recs = recs;
+                a.n_recs = (uint32_t)n_recs;
+                a.accumulate = c0 > 0 ? 1u : 0u;
+                for (int j = 0; j < K; ++j) {
+                    int i = in_idx[c0 + j];
+                    if (sel_k > 0 && i >= sel_k) {
+                        a.in_sel |= 1u << j;
+                        i -= sel_k;
+                    }
+                    a.in_idx[j] = (uint32_t)i;
+                }
+                for (int r = 0; r < R; ++r) {
+                    int i = out_idx[r0 + r];
+                    if (sel_k > 0 && i >= sel_k) {
+                        a.out_sel |= 1u << r;
+                        i -= sel_k;
+                    }
+                    a.out_idx[r] = (uint32_t)i;
+                    for (int j = 0; j < K; ++j)
+                        hbec::perm_table(rows[(size_t)(r0 + r) * K_all + c0 + j], a.tab[r][j]);
+                }
+                const uint64_t want = (n_recs + 3) / 4;  // 4 waves per block
+                uint64_t cap = (uint64_t)cus * (uint64_t)hbec::odd_blocks_per_cu();
+                if (max_blocks > 0) cap = std::min<uint64_t>(cap, (uint64_t)max_blocks);
+                const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, cap));
+                e = hbec::launch_odd_plan(K, R, c0 > 0 ? 1 : 0, a, grid, stream);
+                if (e != hipSuccess) return hip_fail(e, "launch gf_odd_plan");
+            }
+        }
+        return HBEC_OK;
+    }
     for (int r0 = 0; r0 < R_all; r0 += hbec::kMaxR) {
         const int R = std::min(hbec::kMaxR, R_all - r0);
         e = hbec::unaligned_occupancy(R, &per_cu);
@@ -272,7 +312,9 @@ int hbec_plan_stripes(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n,
                 recs.push_back(r);
             }
         }
-        if (recs.size() >= (1ull << 31)) return fail(HBEC_ERR_INVALID_ARG, "plan too large (>= 2^31 tiles)");
+        // both record counts are checked before anything is allocated on the device
+        if (recs.size() >= (1ull << 31) || urecs.size() >= (1ull << 31))
+            return fail(HBEC_ERR_INVALID_ARG, "plan too large (>= 2^31 tiles)");
         p->n_tiles = recs.size();
         if (!recs.empty()) {
             hipError_t e = hipMalloc(&p->d_tiles, recs.size() * sizeof(hbec::TileRec));
@@ -284,7 +326,6 @@ int hbec_plan_stripes(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n,
                 return hip_fail(e, "hipMemcpy plan tiles");
             }
         }
-        if (urecs.size() >= (1ull << 31)) return fail(HBEC_ERR_INVALID_ARG, "plan too large (>= 2^31 tiles)");
         int urc = upload(urecs, &p->d_urecs, "plan unaligned records");
         if (urc) {
             if (p->d_tiles) (void)hipFree(p->d_tiles);
@@ -336,7 +377,9 @@ int hbec_plan_objects(hbec_codec* codec, const hbec_object* objects, uint64_t n,
                 recs.push_back(r);
             }
         }
-        if (recs.size() >= (1ull << 31)) return fail(HBEC_ERR_INVALID_ARG, "plan too large (>= 2^31 tiles)");
+        // both record counts are checked before anything is allocated on the device
+        if (recs.size() >= (1ull << 31) || urecs.size() >= (1ull << 31))
+            return fail(HBEC_ERR_INVALID_ARG, "plan too large (>= 2^31 tiles)");
         p->n_tiles = recs.size();
         if (!recs.empty()) {
             hipError_t e = hipMalloc(&p->d_tiles, recs.size() * sizeof(hbec::TileRec));
@@ -348,7 +391,6 @@ int hbec_plan_objects(hbec_codec* codec, const hbec_object* objects, uint64_t n,
                 return hip_fail(e, "hipMemcpy plan tiles");
             }
         }
-        if (urecs.size() >= (1ull << 31)) return fail(HBEC_ERR_INVALID_ARG, "plan too large (>= 2^31 tiles)");
         int urc = upload(urecs, &p->d_urecs, "plan unaligned records");
         if (urc) {
             if (p->d_tiles) (void)hipFree(p->d_tiles);

@@ -325,8 +325,9 @@ typedef int64_t (*hbec_read_fn)(void* ctx, uint8_t* buf, size_t n);
 /* io.Writer.Write: returns 0 when all n bytes were written, non-zero on error. */
 typedef int (*hbec_write_fn)(void* ctx, const uint8_t* buf, size_t n);
 
-/* ecShardLength (ecutils.go:14-24): ceil(length / k), 0 for length < 0. */
-int64_t hbec_ec_shard_length(int64_t length, int data_shards);
+/* ecShardLength (ecutils.go:14-24): ceil(length / k), 0 for length < 0.
+ * data_shards is Go's int (64-bit), as parseECScheme returns it. */
+int64_t hbec_ec_shard_length(int64_t length, int64_t data_shards);
 
 /* ecSplit (ecutils.go:26-72).  writers: k+m contexts, NULL = nil writer.  A
  * failing writer is dropped for the rest of the object, as in Go. */

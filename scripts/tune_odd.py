@@ -1,0 +1,109 @@
+#!/usr/bin/env python3
+"""A/B of gf_odd (odd.hip) build variants on odd shard lengths: one variant
+library per process (HBEC_LIB), processes alternated by scripts/tune_odd.sh.
+
+    python scripts/tune_odd.py build v1,v2        # CPU: tune_build/odd_<v>/libhbec.so
+    HBEC_LIB=tune_build/odd_<v>/libhbec.so python scripts/tune_odd.py run <v> [round]
+
+Prints one JSON line per (variant, shape): median ms and % of 8 TB/s for
+Encode, Verify and (databuf shapes) Reconstruct of two shards; every result
+is checked by Verify on the GPU.
+"""
+from __future__ import annotations
+
+import json
+import statistics
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+VARIANTS = {
+    "base": [],
+    "valu": ["HBEC_ODD_REALIGN=0"],
+    "u2": ["HBEC_ODD_U_SMALL=2"],
+    "sleep": ["HBEC_ODD_SLEEP=8"],
+    "u4": ["HBEC_ODD_U_SMALL=4"],
+    "valu_u2": ["HBEC_ODD_REALIGN=0", "HBEC_ODD_U_SMALL=2"],
+}
+
+MiB = 1 << 20
+SHAPES = [(4, 2, MiB - 4, "databuf"), (4, 2, MiB - 4, "split"), (4, 2, 1000001, "databuf"), (8, 3, MiB - 8, "databuf"),
+          (6, 3, MiB, "databuf"), (10, 4, MiB, "databuf"), (12, 4, 12 * 87392 - 5, "databuf")]
+
+
+def build(names=None):
+    from hummingbird_amd import build as Bd
+
+    for name, defs in VARIANTS.items():
+        if names and name not in names:
+            continue
+        out = ROOT / "tune_build" / f"odd_{name}"
+        Bd.build(defs=defs, lib=out / "libhbec.so", objdir=out / "obj", verbose=False)
+        print("built", out, flush=True)
+
+
+def run(label, rnd=0, n=2048):
+    import torch
+
+    from hummingbird_amd import batch as B
+    from hummingbird_amd import reedsolomon as RS
+
+    torch.cuda.set_device(0)
+
+    def timeit(fn, reps=15):
+        for _ in range(3):
+            fn()
+        ts = []
+        for _ in range(reps):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            fn()
+            b.record()
+            b.synchronize()
+            ts.append(a.elapsed_time(b))
+        return statistics.median(ts)
+
+    # clock settle
+    x = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
+    for _ in range(200):
+        x.add_(1)
+    del x
+    for k, m, L, layout in SHAPES:
+        s = -(-L // k)
+        enc = RS.New(k, m)
+        if layout == "databuf":
+            rows = torch.empty((n, (k + m) * s), dtype=torch.uint8, device="cuda")
+            B.fill_splitmix(rows, (k + m) * s)
+            views = B.shard_views(rows, k + m, s)
+        else:
+            objs = torch.empty((n, k * s), dtype=torch.uint8, device="cuda")
+            B.fill_splitmix(objs, k * s)
+            par = torch.empty((n, m * s), dtype=torch.uint8, device="cuda")
+            views = B.shard_views(objs, k, s) + B.shard_views(par, m, s)
+        flags = torch.zeros(n, dtype=torch.int32, device="cuda")
+        nb = n * (k + m) * s
+        row = {"variant": label, "round": rnd, "k": k, "m": m, "S": s, "layout": layout}
+        ms = timeit(lambda: B.encode_views(enc, views, n, s))
+        row["encode"] = round(nb / (ms * 1e-3) / 8e12, 4)
+        if layout == "databuf":
+            present = [0, 0] + [1] * (k + m - 2)
+            ms = timeit(lambda: B.reconstruct_views(enc, views, present, n, s))
+            row["reconstruct"] = round(n * (k + 2) * s / (ms * 1e-3) / 8e12, 4)
+        ms = timeit(lambda: B.verify_views(enc, views, n, s, flags))
+        row["verify"] = round(nb / (ms * 1e-3) / 8e12, 4)
+        flags.zero_()
+        B.verify_views(enc, views, n, s, flags)
+        torch.cuda.synchronize()
+        row["ok"] = int(flags.count_nonzero().item()) == 0
+        print(json.dumps(row), flush=True)
+        del views
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    if sys.argv[1:2] == ["build"]:
+        build(sys.argv[2].split(",") if len(sys.argv) > 2 else None)
+    else:
+        run(sys.argv[2] if len(sys.argv) > 2 else "default", int(sys.argv[3]) if len(sys.argv) > 3 else 0)

@@ -8,8 +8,8 @@ kernels.  Checks mirror what the reference path computes:
   * every erasure pattern of 4+2 and 8+3 (golden digests),
   * the ecutils stripe loops (ecSplit / ecReconstruct / ecGlue) against the
     golden shard files, including padding and multi-stripe objects,
-  * device batches at 64 x 1 MiB (full compare) and at the BASELINE size
-    4096 x 1 MiB (round-trip + sampled compare).
+  * device batches at 64 x 1 MiB and at the BASELINE size 4096 x 1 MiB
+    (every object compared with the oracle).
 """
 import hashlib
 import io
@@ -436,28 +436,25 @@ def test_apply_many_inputs_outputs():
 
 @pytest.mark.slow
 def test_baseline_size_4096x1mib_roundtrip():
-    """BASELINE configs 2+3 at full size: 4096 x 1 MiB, 4+2 encode then
-    reconstruct {0,1}; round trip must restore the data bit-exactly and
-    sampled objects must equal the CPU oracle."""
+    """BASELINE configs[1] + configs[2] at full size: 4096 x 1 MiB, 4+2
+    encode, then reconstruct {0,1} into a separate array.  EVERY object's
+    parity equals the CPU oracle's (klauspost restatement) and every rebuilt
+    shard equals the original data: no sampling."""
+    import fullcheck
+
     k, m, n = 4, 2, 4096
     s = MiB // k
     objs = _batch(n, k, MiB)
     parity = torch.empty((n, m * s), dtype=torch.uint8, device="cuda")
     enc = RS.New(k, m)
     B.encode_objects(enc, objs, parity, s)
-    rebuilt = torch.empty((n, 2 * s), dtype=torch.uint8, device="cuda")
+    rebuilt = torch.full((n, 2 * s), 0x3C, dtype=torch.uint8, device="cuda")
     views = [(rebuilt.data_ptr(), rebuilt.stride(0)), (rebuilt.data_ptr() + s, rebuilt.stride(0))]
     views += B.shard_views(objs, k, s)[2:] + B.shard_views(parity, m, s)
     B.reconstruct_views(enc, views, [0, 0, 1, 1, 1, 1], n, s)
     torch.cuda.synchronize()
-    assert torch.equal(rebuilt, objs[:, :2 * s])
-    idx = [0, 1, 2047, 4095]
-    want, _ = CO.encode_batch(k, m, objs[idx].cpu().numpy(), threads=CO.cpu_threads())
-    assert np.array_equal(parity[idx].cpu().numpy(), want)
-    # checksum of checksums over the whole batch: parity xor-fold vs the CPU encode of 64 sampled objects
-    sample = list(range(0, n, 64))
-    want, _ = CO.encode_batch(k, m, objs[sample].cpu().numpy(), threads=CO.cpu_threads())
-    assert np.array_equal(parity[sample].cpu().numpy(), want)
+    assert fullcheck.rows_match(rebuilt, objs[:, :2 * s])
+    assert fullcheck.encode_parity_matches(k, m, objs, parity) == n
 
 
 @pytest.mark.parametrize("k,m,s,n", [(4, 2, 5 * 4096 + 48, 7), (8, 3, 3 * 2048 + 16, 5), (2, 2, 4096 * 2 + 1024, 3),
