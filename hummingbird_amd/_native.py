@@ -117,6 +117,9 @@ _SIG = [
     ("hbec_ec_glue_range", C.c_int,
      [C.c_int, C.c_int, READ_FN, C.POINTER(_P), C.c_int, C.c_int64, C.c_int64, C.c_int64, WRITE_FN, C.POINTER(_P),
       C.c_int]),
+    ("hbec_ec_copy_range", C.c_int,
+     [C.c_int, C.c_int, READ_FN, C.POINTER(_P), C.c_int, C.c_int64, C.c_int64, C.c_int64, WRITE_FN, C.POINTER(_P),
+      C.c_int]),
     ("hbec_parse_ec_scheme", C.c_int,
      [C.c_char_p, C.c_char_p, C.c_size_t, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     ("hbec_range_chunk_align", None,

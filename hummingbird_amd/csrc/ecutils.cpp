@@ -551,6 +551,31 @@ int hbec_ec_glue_range(int k, int m, hbec_read_fn read, void* const* bodies, int
     });
 }
 
+// ecObject.CopyRange's decode exactly as the reference computes it
+// (ecobj.go:238-265): glue rangeChunkAlign's shard-byte span (shardEnd capped
+// at the object's content length) as if it were the content length, and pass
+// the glue through a rangeBytesWriter that starts at start % chunk_size.
+int hbec_ec_copy_range(int k, int m, hbec_read_fn read, void* const* bodies, int chunk_size, int64_t content_length,
+                       int64_t start, int64_t end, hbec_write_fn write, void* const* dsts, int n_dsts) {
+    return hbec::guarded("hbec_ec_copy_range", [&]() -> int {
+        if (k <= 0 || chunk_size <= 0 || n_dsts < 0 || (n_dsts > 0 && !dsts))
+            return fail(HBEC_ERR_INVALID_ARG, "CopyRange: bad arguments");
+        int64_t shard_start = 0, shard_end = 0;
+        hbec_range_chunk_align(start, end, chunk_size, k, &shard_start, &shard_end);
+        if (shard_end > content_length) shard_end = content_length;
+        std::vector<RangeWriter> rw((size_t)n_dsts);
+        std::vector<void*> ctx((size_t)n_dsts, nullptr);
+        for (int j = 0; j < n_dsts; ++j) {
+            // Go's % truncates toward zero, as C++'s does
+            rw[j] = RangeWriter{write, dsts[j], start % (int64_t)chunk_size, end - start};
+            if (dsts[j]) ctx[j] = &rw[j];
+        }
+        if (shard_end - shard_start <= 0) return HBEC_OK;  // ecGlue's loop does not run
+        return hbec_ec_glue(k, m, read, bodies, chunk_size, shard_end - shard_start, write ? range_write : nullptr,
+                            ctx.data(), n_dsts);
+    });
+}
+
 int hbec_parse_ec_scheme(const char* scheme, char* algo, size_t algo_cap, int64_t* data_shards,
                          int64_t* parity_shards, int64_t* chunk_size) {
     return hbec::guarded("hbec_parse_ec_scheme", [&]() -> int {

@@ -5,8 +5,10 @@
     ec_reconstruct(k, m, bodies, chunk_size, content_length,
                    dsts, dst_chunk_num)                        ecutils.go:74-132
     ec_glue(k, m, bodies, chunk_size, content_length, *dsts)   ecutils.go:134-186
+    ec_copy_range(k, m, bodies, chunk_size, content_length,
+                  start, end, *dsts)                           ecobj.go:207-267 (CopyRange, byte-exact)
     ec_glue_range(k, m, bodies, chunk_size, content_length,
-                  start, end, *dsts)                           ecobj.go:207-267 (CopyRange)
+                  start, end, *dsts)                           CopyRange decode, corrected units (opt-in)
     parse_ec_scheme(scheme)                                    ecobj.go:82-98
     range_chunk_align(start, end, chunk_size, k)               ecobj.go:814-824
 
@@ -111,6 +113,22 @@ def ec_glue_range(data_chunks, parity_chunks, bodies, chunk_size, content_length
         check(N.lib().hbec_ec_glue_range(int(data_chunks), int(parity_chunks), _read_cb, _ctx_array(b_ids),
                                          int(chunk_size), int(content_length), int(start), int(end), _write_cb,
                                          _ctx_array(d_ids), len(d_ids)))
+    finally:
+        for i in b_ids + d_ids:
+            _objs.pop(i, None)
+
+
+def ec_copy_range(data_chunks, parity_chunks, bodies, chunk_size, content_length, start, end, *dsts):
+    """ecObject.CopyRange's decode byte for byte as the reference does it
+    (ecobj.go:238-265, shard/object unit mix included): bodies are the ranged
+    shard streams "bytes=shardStart-shardEnd".  Returns the glue's status
+    code (the reference ignores it) instead of raising."""
+    b_ids = _register(bodies)
+    d_ids = _register(dsts)
+    try:
+        return int(N.lib().hbec_ec_copy_range(int(data_chunks), int(parity_chunks), _read_cb, _ctx_array(b_ids),
+                                              int(chunk_size), int(content_length), int(start), int(end), _write_cb,
+                                              _ctx_array(d_ids), len(d_ids)))
     finally:
         for i in b_ids + d_ids:
             _objs.pop(i, None)

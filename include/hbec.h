@@ -343,7 +343,8 @@ int hbec_ec_reconstruct(int data_shards, int parity_shards, hbec_read_fn read, v
 int hbec_ec_glue(int data_shards, int parity_shards, hbec_read_fn read, void* const* bodies, int chunk_size,
                  int64_t content_length, hbec_write_fn write, void* const* dsts, int n_dsts);
 
-/* Range GET decode (ecObject.CopyRange, ecobj.go:207-267): object bytes
+/* Corrected range GET decode (opt-in; the byte-exact drop-in for CopyRange
+ * is hbec_ec_copy_range below): object bytes
  * [start, end) of an object of content_length bytes.  The bodies are the k+m
  * shard streams positioned at the first shard byte of the stripe holding
  * `start` (rangeChunkAlign's shardStart, the ranged shard GETs of
@@ -352,9 +353,24 @@ int hbec_ec_glue(int data_shards, int parity_shards, hbec_read_fn read, void* co
  * rangeBytesWriter (ecobj.go:826-850).  The reference passes the glue a
  * shard-byte length and a start offset modulo chunk_size rather than modulo
  * k * chunk_size (ecobj.go:238-265); this entry uses the object-byte
- * quantities, so it returns the requested bytes for every range.  Returns
+ * quantities, so it returns the requested bytes for every range — which
+ * CHANGES the bytes on the wire compared with upstream.  Returns
  * HBEC_ERR_INVALID_ARG unless 0 <= start <= end <= content_length. */
 int hbec_ec_glue_range(int data_shards, int parity_shards, hbec_read_fn read, void* const* bodies, int chunk_size,
+                       int64_t content_length, int64_t start, int64_t end, hbec_write_fn write, void* const* dsts,
+                       int n_dsts);
+
+/* ecObject.CopyRange's decode, byte for byte as the reference computes it
+ * (ecobj.go:238-265): shardStart, shardEnd = rangeChunkAlign(start, end,
+ * chunk_size, k), shardEnd capped at content_length; the bodies (the ranged
+ * shard GETs "bytes=shardStart-shardEnd") are glued as ecGlue does with
+ * shardEnd - shardStart as the content length, through a rangeBytesWriter
+ * {start % chunk_size, end - start}.  The reference mixes shard and object
+ * units here, so for ranges that do not start in the first chunk of a stripe
+ * the bytes are not object[start, end) — this entry reproduces them anyway
+ * (the drop-in for ecobj.go:264-265; hbec_ec_glue_range is the corrected
+ * decode).  Returns the glue's status; CopyRange itself ignores it (:264). */
+int hbec_ec_copy_range(int data_shards, int parity_shards, hbec_read_fn read, void* const* bodies, int chunk_size,
                        int64_t content_length, int64_t start, int64_t end, hbec_write_fn write, void* const* dsts,
                        int n_dsts);
 

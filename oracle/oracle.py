@@ -27,6 +27,7 @@ plus the byte-level striping of the reference's own code:
 * ``ec_glue``          <- objectserver/ecutils.go:134-186
 * ``parse_ec_scheme``  <- objectserver/ecobj.go:82-98
 * ``range_chunk_align``<- objectserver/ecobj.go:814-824
+* ``ec_copy_range``     <- objectserver/ecobj.go:207-267 (CopyRange, byte-exact)
 * ``shard_hash``       <- objectserver/indexdb.go:746-753 (hex MD5 of a shard body)
 
 Parity pinning
@@ -427,6 +428,96 @@ def ec_glue_range(k, m, shard_files, chunk_size, content_length, start, end):
     for i in range(0, len(body), chunk_size):  # the glue writes shard-sized pieces
         w.write(body[i:i + chunk_size])
     return bytes(w.out)
+
+
+def http_range_body(f, first: int, last: int):
+    """The shard server's answer to "Range: bytes=first-last" (inclusive) over
+    shard file f, as CopyRange sees it (ecobj.go:241-257): bytes [first,
+    last] clipped at EOF, or None (no body: a 416 is skipped at :253-255)
+    when first is past the end of the file."""
+    if f is None or first >= len(f):
+        return None
+    return f[first:last + 1]
+
+
+def ec_copy_range(k, m, shard_files, chunk_size, content_length, start, end):
+    """ecObject.CopyRange (objectserver/ecobj.go:207-267) byte for byte, the
+    reference's unit mix included: rangeChunkAlign's shard-byte span (capped
+    at the object's content length, :239-241) is glued as if it were the
+    content length, through a rangeBytesWriter that starts at start %
+    chunk_size (:264-265).  ecGlue's error is ignored there (CopyRange
+    returns end - start, nil), so a stripe that cannot be rebuilt just ends
+    the output."""
+    shard_start, shard_end = range_chunk_align(start, end, chunk_size, k)
+    if shard_end > content_length:
+        shard_end = content_length
+    files = [http_range_body(f, shard_start, shard_end) for f in shard_files]
+    w = RangeBytesWriter(start % chunk_size, end - start)
+    glue_len = shard_end - shard_start
+    enc = Encoder(k, m)
+    written = 0
+    failed = [False] * (k + m)
+    off = 0
+    for s in _stripe_sizes(k, chunk_size, glue_len):  # ecutils.go:142-186
+        shards = []
+        for i in range(k + m):
+            f = files[i]
+            if f is not None and not failed[i] and len(f) >= off + s:
+                shards.append(np.frombuffer(f[off:off + s], dtype=np.uint8).copy())
+            else:
+                if f is not None:
+                    failed[i] = True
+                shards.append(np.zeros(0, dtype=np.uint8))
+        try:
+            enc.reconstruct_data(shards)
+        except ValueError:
+            break  # ecGlue returns the error; CopyRange drops it
+        for i in range(k):
+            d = shards[i].tobytes()[:glue_len - written]
+            w.write(d)
+            written += len(d)
+        off += s
+    return bytes(w.out)
+
+
+def _shard_positions(k, chunk_size, length):
+    """ecSplit's layout (ecutils.go:26-72) as index arithmetic: for every data
+    shard, the object position each shard byte holds (-1 = zero padding)."""
+    shards = [[] for _ in range(k)]
+    done = 0
+    while done < length:
+        e = chunk_size
+        if length - done < chunk_size * k:
+            e = (length - done) // k + (1 if (length - done) % k else 0)
+        for i in range(k):
+            shards[i] += [p if p < length else -1 for p in range(done + i * e, done + (i + 1) * e)]
+        done += min(e * k, length - done)
+    return shards
+
+
+def copy_range_positions(k, chunk_size, content_length, start, end):
+    """The object positions CopyRange (ec_copy_range, all shards healthy)
+    writes, in order: the same glue and writer arithmetic on position labels
+    instead of bytes (-1 = a padding byte)."""
+    pos = _shard_positions(k, chunk_size, content_length)
+    shard_start, shard_end = range_chunk_align(start, end, chunk_size, k)
+    if shard_end > content_length:
+        shard_end = content_length
+    glue_len = shard_end - shard_start
+    stream, off = [], 0
+    for s in _stripe_sizes(k, chunk_size, glue_len):
+        if any(shard_start + off + s > len(p) for p in pos):
+            break  # a short shard body: the stripe cannot be rebuilt from data alone (parity has the same length)
+        for i in range(k):
+            stream += pos[i][shard_start + off:shard_start + off + s][:glue_len - len(stream)]
+        off += s
+    a = start % chunk_size
+    return stream[a:a + (end - start)] if a <= len(stream) else []
+
+
+def copy_range_is_object_slice(k: int, chunk_size: int, content_length: int, start: int, end: int) -> bool:
+    """True where CopyRange's bytes equal object[start:end]."""
+    return copy_range_positions(k, chunk_size, content_length, start, end) == list(range(start, end))
 
 
 def parse_ec_scheme(scheme: str):

@@ -243,6 +243,44 @@ def test_glue_range_is_the_slice(k, m, chunk, length):
             assert out.value() == O.ec_glue_range(k, m, fs, chunk, length, start, end)
 
 
+@pytest.mark.parametrize("k,m,chunk,length", [(4, 2, 1024, 40_000), (8, 3, 4096, 300_001), (2, 1, 10, 80),
+                                              (10, 4, 1003, 51_234), (1, 1, 7, 50)])
+def test_copy_range_is_the_reference_bytes(k, m, chunk, length):
+    """hbec_ec_copy_range (the byte-exact CopyRange drop-in) returns what
+    ecObject.CopyRange writes (oracle.ec_copy_range, ecobj.go:207-267, the
+    shard/object unit mix included) for healthy and degraded shard sets, from
+    the ranged shard bodies "bytes=shardStart-shardEnd"; and it equals
+    object[start:end] exactly on the ranges the reference's arithmetic maps to
+    the object slice (oracle.copy_range_is_object_slice), where
+    hbec_ec_glue_range gives the same bytes."""
+    body = bytes(O.object_bytes(k * 17 + m, length))
+    files = O.ec_split(k, m, body, chunk)
+    rng = np.random.default_rng(length + k)
+    stripe = k * chunk
+    ranges = [(0, length), (0, 1), (0, chunk), (1, chunk // 2 + 1), (stripe, 2 * stripe), (stripe + 3, stripe + 9),
+              (length - 1, length), (3, 3)]
+    ranges += [tuple(int(x) for x in sorted(rng.integers(0, length + 1, 2))) for _ in range(16)]
+    n_agree = 0
+    for start, end in ranges:
+        for lose in (False, True):
+            fs = list(files)
+            if lose:
+                for i in rng.choice(k + m, m, replace=False):
+                    fs[i] = None
+            shard_start, shard_end = O.range_chunk_align(start, end, chunk, k)
+            shard_end = min(shard_end, length)
+            bodies = [None if b is None else io.BytesIO(b)
+                      for b in (O.http_range_body(f, shard_start, shard_end) for f in fs)]
+            out = Rec()
+            E.ec_copy_range(k, m, bodies, chunk, length, start, end, out)
+            want = O.ec_copy_range(k, m, fs, chunk, length, start, end)
+            assert out.value() == want, (start, end, lose)
+            if O.copy_range_is_object_slice(k, chunk, length, start, end):
+                assert want == body[start:end]
+                n_agree += not lose
+    assert n_agree > 0
+
+
 def test_glue_range_reference_writer_kats(kats):
     """TestRangeBytesWriter's vectors (ecobj_test.go:332-358) through the
     library: a 1+1 object "THIS IS A TEST" glued with chunk sizes 1..19 (the

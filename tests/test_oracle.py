@@ -303,3 +303,32 @@ def test_oracle_ec_glue_range_is_the_slice(k, m, chunk, length):
         for i in rng.choice(k + m, m, replace=False):
             lost[i] = None
         assert O.ec_glue_range(k, m, lost, chunk, length, start, end) == body[start:end]
+
+
+@pytest.mark.parametrize("k,m,chunk,length", [(4, 2, 100, 2_000), (3, 2, 7, 250), (1, 1, 5, 37), (8, 3, 64, 9_001)])
+def test_copy_range_reference_units_where_it_agrees(k, m, chunk, length):
+    """ecObject.CopyRange restated byte for byte (oracle.ec_copy_range,
+    ecobj.go:207-267): with every shard healthy it returns object[start:end]
+    exactly where oracle.copy_range_is_object_slice says so (the range starts
+    in the first chunk of its stripe and the glued shard-byte span still
+    covers it), and other bytes elsewhere.  The list of disagreeing ranges is
+    the reference's unit mix (start % chunk_size, a shard-byte content
+    length), not a codec difference."""
+    body = bytes(O.object_bytes(k * 31 + chunk, length))
+    files = O.ec_split(k, m, body, chunk)
+    stripe = k * chunk
+    rng = np.random.default_rng(k * 1000 + length)
+    ranges = [(0, length), (0, 1), (0, chunk), (chunk - 1, chunk + 1), (stripe, stripe + chunk),
+              (stripe + 1, stripe + 9), (length - 9, length)]
+    ranges += [tuple(int(x) for x in sorted(rng.integers(0, length + 1, 2))) for _ in range(40)]
+    agree = differ = 0
+    for start, end in ranges:
+        out = O.ec_copy_range(k, m, files, chunk, length, start, end)
+        pred = O.copy_range_is_object_slice(k, chunk, length, start, end)
+        if pred:
+            assert out == body[start:end], (start, end)
+            agree += 1
+        elif end - start >= 8:  # short ranges could coincide by chance
+            assert out != body[start:end], (start, end)
+            differ += 1
+    assert agree > 0 and (differ > 0 or k == 1)
