@@ -103,7 +103,9 @@ __device__ __forceinline__ int32_t odd_c0(uint64_t out0) { return (int32_t)((16u
 // as zero, so loads need no clamping.
 struct OddSrc {
     __amdgpu_buffer_rsrc_t rs;
-    int32_t g;  // block of the tile's first column
+    uint64_t base;  // base & ~15 (global-load variant)
+    int32_t nb;     // blocks holding shard bytes (global-load variant)
+    int32_t g;      // block of the tile's first column
 };
 
 __device__ __forceinline__ OddSrc odd_src(uint64_t base, int32_t S, int32_t c) {
@@ -112,11 +114,25 @@ __device__ __forceinline__ OddSrc odd_src(uint64_t base, int32_t S, int32_t c) {
     o.rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(base & ~(uint64_t)15), (short)0,
                                              (int)((uint32_t)(l + S + 15) & ~15u), 0x00020000);
     o.g = (l + c) >> 4;  // arithmetic: floor for c < 0
+    o.base = base & ~(uint64_t)15;
+    o.nb = (l + S + 15) >> 4;
     return o;
 }
 
+#ifndef HBEC_ODD_GLOBAL
+#define HBEC_ODD_GLOBAL 0  // 1: global loads at a clamped block index instead of buffer loads
+#endif
+
 __device__ __forceinline__ u32x4 odd_ld(const OddSrc& o, int32_t col) {
-    return __builtin_amdgcn_raw_buffer_load_b128(o.rs, (uint32_t)((col + o.g) * 16), 0, 2 /* nt */);
+    if constexpr (HBEC_ODD_GLOBAL) {
+        // blocks outside [0, nb) hold no shard byte: clamp to one that exists
+        const int32_t b = __builtin_amdgcn_readfirstlane(o.nb) - 1;
+        int32_t i = col + o.g;
+        i = i < 0 ? 0 : (i > b ? b : i);
+        return ld16_addr(o.base + (uint64_t)(uint32_t)(i * 16));
+    } else {
+        return __builtin_amdgcn_raw_buffer_load_b128(o.rs, (uint32_t)((col + o.g) * 16), 0, 2 /* nt */);
+    }
 }
 
 __device__ __forceinline__ uint32_t odd_d(uint64_t base, int32_t c) { return ((uint32_t)base + (uint32_t)c) & 15u; }

@@ -20,9 +20,20 @@
  *
  *   gcc -O2 -std=c11 -pthread -Iinclude scripts/soak.c -Lhummingbird_amd -lhbec \
  *       -Wl,-rpath,$PWD/hummingbird_amd -o gpurun_out/soak
- *   timeout -k 10 180 gpurun_out/soak THREADS SECONDS */
-#define _POSIX_C_SOURCE 199309L
+ *   timeout -k 10 180 gpurun_out/soak THREADS SECONDS
+ *
+ * Stall report: when no operation completes for STALL_S seconds, every task
+ * of the process (the soak threads, the library's pool and batcher workers
+ * and the HIP runtime's threads) prints its stack (SIGUSR1 handler,
+ * backtrace_symbols_fd; resolve libhbec.so+offset with addr2line) once. */
+#define _GNU_SOURCE
+#include <dirent.h>
+#include <execinfo.h>
 #include <pthread.h>
+#include <signal.h>
+#include <stdatomic.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -58,6 +69,38 @@ static uint64_t next(uint64_t* x) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
+}
+
+static atomic_flag g_dump_lock = ATOMIC_FLAG_INIT;
+
+static void dump_handler(int sig) {
+    (void)sig;
+    void* fr[64];
+    while (atomic_flag_test_and_set(&g_dump_lock)) {
+    }
+    char hdr[64];
+    const int n = snprintf(hdr, sizeof hdr, "--- task %ld\n", (long)syscall(SYS_gettid));
+    if (write(2, hdr, (size_t)n) < 0) {
+    }
+    const int d = backtrace(fr, 64);
+    backtrace_symbols_fd(fr, d, 2);
+    atomic_flag_clear(&g_dump_lock);
+}
+
+/* signal every task of the process in turn (each prints its own stack) */
+static void dump_all_tasks(void) {
+    DIR* dir = opendir("/proc/self/task");
+    if (!dir) return;
+    const pid_t pid = getpid();
+    struct dirent* e;
+    while ((e = readdir(dir)) != NULL) {
+        const long tid = atol(e->d_name);
+        if (tid <= 0) continue;
+        syscall(SYS_tgkill, pid, tid, SIGUSR1);
+        struct timespec ts = {0, 20 * 1000 * 1000};
+        nanosleep(&ts, NULL);
+    }
+    closedir(dir);
 }
 
 static int check(Job* j, int i) {
@@ -184,6 +227,19 @@ int main(int argc, char** argv) {
             memcpy(j->keep[i], j->base[i], bytes);
         }
     }
+    {
+        void* fr[4];
+        backtrace(fr, 4); /* load the unwinder before any signal */
+        struct sigaction sa;
+        memset(&sa, 0, sizeof sa);
+        sa.sa_handler = dump_handler;
+        sa.sa_flags = SA_RESTART;
+        sigaction(SIGUSR1, &sa, NULL);
+    }
+    const double stall_s = getenv("SOAK_STALL_S") ? atof(getenv("SOAK_STALL_S")) : 20.0;
+    double last_progress = now();
+    uint64_t last_ops = 0;
+    int dumped = 0;
     const double t0 = now();
     g_stop = t0 + secs;
     for (int t = 0; t < threads; ++t) pthread_create(&th[t], NULL, run, &jobs[t]);
@@ -212,6 +268,15 @@ int main(int argc, char** argv) {
                 hist[0], hist[1], hist[2], hist[3], hist[4], hist[5], hist[6], hist[10], hist[11], hist[12], hist[13],
                 hist[14], (unsigned long long)g, (unsigned long long)c, (unsigned long long)b, (unsigned long long)bs);
         fflush(stderr);
+        if (sofar != last_ops) {
+            last_ops = sofar;
+            last_progress = now();
+        } else if (!dumped && now() - last_progress >= stall_s) {
+            fprintf(stderr, "soak: no operation completed for %.0f s: stacks of every task follow\n", now() - last_progress);
+            fflush(stderr);
+            dump_all_tasks();
+            dumped = 1;
+        }
         if (bad) break;
     }
     int rc = 0, where = -1, who = -1;

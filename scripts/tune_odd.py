@@ -26,6 +26,9 @@ VARIANTS = {
     "sleep": ["HBEC_ODD_SLEEP=8"],
     "u4": ["HBEC_ODD_U_SMALL=4"],
     "valu_u2": ["HBEC_ODD_REALIGN=0", "HBEC_ODD_U_SMALL=2"],
+    "gl": ["HBEC_ODD_REALIGN=0", "HBEC_ODD_GLOBAL=1"],
+    "gl_lds": ["HBEC_ODD_GLOBAL=1"],
+    "nobar": ["HBEC_ODD_REALIGN=0", "HBEC_ODD_BARRIER=0"],
 }
 
 MiB = 1 << 20
