@@ -162,35 +162,43 @@ static int odd_launches(const PassArgs& a, int K, int R, int mode, bool accumula
     int cus = 0;
     int rc = cu_count(dev, &cus);
     if (rc) return rc;
-    cus *= odd_blocks_per_cu();
-    for (int c1 = 0; c1 < K; c1 += kOddMaxK) {
-        const int K1 = std::min(kOddMaxK, K - c1);
-        PassArgs b = a;
-        for (int j = 0; j < K1; ++j) {
-            b.in[j] = a.in[c1 + j];
-            b.in_stride[j] = a.in_stride[c1 + j];
-            for (int r = 0; r < R; ++r)
-                for (int q = 0; q < 5; ++q) b.tab[r][j][q] = a.tab[r][c1 + j][q];
-        }
-        const int m = mode == 2 ? 2 : ((accumulate || c1 > 0) ? 1 : 0);
-        const uint64_t tpo = odd_tiles_per_obj(K1, shard_len);
-        const uint64_t max_obj = std::max<uint64_t>(1, std::min<uint64_t>((1ull << 31), g_chunk_tiles) / tpo);
-        for (uint64_t o0 = 0; o0 < n_obj; o0 += max_obj) {
-            const uint64_t no = std::min(max_obj, n_obj - o0);
-            PassArgs c = b;
-            for (int j = 0; j < K1; ++j) c.in[j] = b.in[j] + o0 * b.in_stride[j];
-            for (int r = 0; r < R; ++r) c.out[r] = b.out[r] + o0 * b.out_stride[r];
-            c.n_obj = no;
-            c.shard_len = shard_len;
-            c.tiles_per_obj = (uint32_t)tpo;
-            c.n_tiles = (uint32_t)(no * tpo);
-            const uint64_t want = (c.n_tiles + 3) / 4;
-            int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cus));
-            if (g_grid_cap > 0) grid = std::min(grid, g_grid_cap);
-            hipError_t e = launch_odd(K1, R, m, c, flags ? flags + o0 : nullptr, grid, stream);
-            if (e != hipSuccess) return hip_fail(e, "launch gf_odd");
+    cus *= odd_blocks_per_cu(mode == 2 ? 2 : 0);
+    if (shard_len > odd_min_main()) {
+        for (int c1 = 0; c1 < K; c1 += kOddMaxK) {
+            const int K1 = std::min(kOddMaxK, K - c1);
+            PassArgs b = a;
+            for (int j = 0; j < K1; ++j) {
+                b.in[j] = a.in[c1 + j];
+                b.in_stride[j] = a.in_stride[c1 + j];
+                for (int r = 0; r < R; ++r)
+                    for (int q = 0; q < 5; ++q) b.tab[r][j][q] = a.tab[r][c1 + j][q];
+            }
+            const int m = mode == 2 ? 2 : ((accumulate || c1 > 0) ? 1 : 0);
+            const uint64_t tpo = odd_tiles_per_obj(K1, m, shard_len);
+            const uint64_t max_obj = std::max<uint64_t>(1, std::min<uint64_t>((1ull << 31), g_chunk_tiles) / tpo);
+            for (uint64_t o0 = 0; o0 < n_obj; o0 += max_obj) {
+                const uint64_t no = std::min(max_obj, n_obj - o0);
+                PassArgs c = b;
+                for (int j = 0; j < K1; ++j) c.in[j] = b.in[j] + o0 * b.in_stride[j];
+                for (int r = 0; r < R; ++r) c.out[r] = b.out[r] + o0 * b.out_stride[r];
+                c.n_obj = no;
+                c.shard_len = shard_len;
+                c.tiles_per_obj = (uint32_t)tpo;
+                c.n_tiles = (uint32_t)(no * tpo);
+                const uint64_t want = (c.n_tiles + 3) / 4;
+                int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cus));
+                if (g_grid_cap > 0) grid = std::min(grid, g_grid_cap);
+                hipError_t e = launch_odd(K1, R, m, c, flags ? flags + o0 : nullptr, grid, stream);
+                if (e != hipSuccess) return hip_fail(e, "launch gf_odd");
+            }
         }
     }
+    // the guard-band bytes of every shard, all K inputs of the pass at once
+    PassArgs g = a;
+    g.n_obj = n_obj;
+    g.shard_len = shard_len;
+    hipError_t e = launch_odd_edges(K, R, mode == 2 ? 2 : (accumulate ? 1 : 0), g, flags, stream);
+    if (e != hipSuccess) return hip_fail(e, "launch gf_odd_edges");
     return HBEC_OK;
 }
 
@@ -292,7 +300,7 @@ int apply_views(int rows, int cols, const uint8_t* coeffs, const hbec_view* in, 
                     hipError_t e = launch_vec(K, R, b, grid, stream, force_stream);
                     if (e != hipSuccess) return hip_fail(e, "launch gf_apply_vec");
                 }
-            } else if (g_unaligned_kernel.load() && odd_enabled()) {
+            } else if (g_unaligned_kernel.load() && odd_enabled() && cols <= kOddMaxK && shard_len < (1ull << 31)) {
                 // any alignment / length: gf_odd (odd.hip), passes of <= 8 inputs,
                 // later ones accumulating into the outputs
                 rc = apply_odd(a, K, R, c0 > 0, n_obj, shard_len, dev, stream);
@@ -1010,7 +1018,7 @@ static int verify_views(hbec_codec* c, const hbec_view* views, uint64_t n_obj, u
         }
         return HBEC_OK;
     }
-    if (g_unaligned_kernel.load() && odd_enabled() && k <= kOddMaxK) {
+    if (g_unaligned_kernel.load() && odd_enabled() && k <= kOddMaxK && shard_len < (1ull << 31)) {
         // any alignment: recompute and compare in one pass (gf_odd verify), <= 4 rows per launch
         int dev = 0;
         int rc = current_device(&dev);

@@ -504,19 +504,25 @@ int zero_copy_unaligned_run(Ring* ring, const std::vector<ZcStripe>& zs, const s
         if (e != hipSuccess) return hip_fail(e, "zero-copy slot wait");
         hbec::URec* rec = reinterpret_cast<hbec::URec*>(ring->pin_tiles[slot]);
         uint64_t nt = 0;
-        while (si < zs.size() && nt < ring->tile_cap) {
+        std::vector<hbec::URec> edges;  // gf_odd: one per stripe started in this slot, after the main records
+        while (si < zs.size() && nt + edges.size() + 1 < ring->tile_cap) {
             const ZcStripe& z = zs[si];
-            rec[nt++] = {z.dev, 0, z.shard_len, off};
+            const uint64_t span = hbec::urec_span(z.shard_len);
+            if (off == 0 && hbec::odd_enabled()) edges.push_back({z.dev, 0, z.shard_len, 0});
+            if (off < span) rec[nt++] = {z.dev, 0, z.shard_len, off};
             off += tile;
-            if (off >= hbec::urec_span(z.shard_len)) {
+            if (off >= span) {
                 off = 0;
                 ++si;
             }
         }
-        e = hipMemcpyAsync(ring->dev_tiles[slot], rec, nt * sizeof(hbec::URec), hipMemcpyHostToDevice, ring->s_cmp);
+        std::copy(edges.begin(), edges.end(), rec + nt);
+        e = hipMemcpyAsync(ring->dev_tiles[slot], rec, (nt + edges.size()) * sizeof(hbec::URec), hipMemcpyHostToDevice,
+                           ring->s_cmp);
         if (e != hipSuccess) return hip_fail(e, "zero-copy records H2D");
-        int rc = hbec::launch_unaligned_passes(reinterpret_cast<const hbec::URec*>(ring->dev_tiles[slot]), nt, in_idx,
-                                               out_idx, rows, 0, ring->s_cmp, zero_copy_max_blocks());
+        const hbec::URec* d_rec = reinterpret_cast<const hbec::URec*>(ring->dev_tiles[slot]);
+        int rc = hbec::launch_unaligned_passes(d_rec, nt, in_idx, out_idx, rows, 0, ring->s_cmp, zero_copy_max_blocks(),
+                                               d_rec + nt, edges.size());
         if (rc) return rc;
         e = hipEventRecord(ring->ev_cmp[slot], ring->s_cmp);
         if (e != hipSuccess) return hip_fail(e, "zero-copy event");

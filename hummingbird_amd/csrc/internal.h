@@ -87,8 +87,10 @@ struct URec;
 // lengths), in launches of <= 4 outputs and <= kMaxK inputs (later input
 // passes accumulate).  sel_k > 0: object records (indices >= sel_k are
 // parity, base b).  max_blocks > 0 caps the grid (zero-copy over PCIe).
+// erecs: gf_odd's one edge record per stripe (guard-band bytes; none for the round-2 kernels).
 int launch_unaligned_passes(const URec* recs, uint64_t n_recs, const std::vector<int>& in_idx,
                             const std::vector<int>& out_idx, const std::vector<uint8_t>& rows, int sel_k,
-                            hipStream_t stream, int max_blocks = 0);
+                            hipStream_t stream, int max_blocks = 0, const URec* erecs = nullptr,
+                            uint64_t n_erecs = 0);
 
 }  // namespace hbec

@@ -137,19 +137,27 @@ constexpr int kOddMaxK = 8;
 // HBEC_ODD=1 / 0 selects gf_odd or the round-2 kernels (gf_apply_unaligned
 // family) for odd shards (default: HBEC_ODD_DEFAULT).
 bool odd_enabled();
-// 4-wave blocks per CU of the gf_odd grids (HBEC_ODD_BPC, tuning)
-int odd_blocks_per_cu();
+// 4-wave blocks per CU of the gf_odd grids for a mode (HBEC_ODD_BPC overrides)
+int odd_blocks_per_cu(int mode);
 bool odd_supported(int k, int r);
 // Unaligned plan records (URec) of one stripe / object: p0 = 0, tile, 2*tile,
 // ... while p0 < urec_span(S), for whichever kernel family codes them.
 uint64_t urec_tile();
-uint64_t urec_span(uint64_t shard_len);
+uint64_t urec_span(uint64_t shard_len);  // 0: no main-kernel records (gf_odd: S <= odd_min_main())
 uint32_t odd_tile_bytes(int k);       // shard bytes per wave tile of the strided kernel
 uint32_t odd_plan_tile_bytes();       // shard bytes per plan record
-uint32_t odd_tiles_per_obj(int k, uint64_t shard_len);
+uint32_t odd_tiles_per_obj(int k, int mode, uint64_t shard_len);
+// shards of at most this many bytes are coded by gf_odd_edges alone
+uint64_t odd_min_main();
 hipError_t launch_odd(int k, int r, int mode, const PassArgs& a, uint32_t* flags, int grid, hipStream_t stream);
-// plan records: URec.p0 = first window * 992 (records cover positions [0, S + 32))
+// the guard-band bytes of every shard (after the main launches of a pass;
+// k <= kMaxK inputs, a.n_obj objects; verify flags mismatching objects)
+hipError_t launch_odd_edges(int k, int r, int mode, const PassArgs& a, uint32_t* flags, hipStream_t stream);
+// plan records: URec.p0 = first window * 992 (records cover positions [0, S + 32)),
+// only for stripes longer than odd_min_main(); plus one edge record per stripe
 hipError_t launch_odd_plan(int k, int r, int mode, const UPlanArgs& p, int grid, hipStream_t stream);
+hipError_t launch_odd_edges_plan(int k, int r, int mode, const UPlanArgs& p, const URec* erecs, uint32_t n_erecs,
+                                 hipStream_t stream);
 
 hipError_t launch_fill(uint8_t* dst, uint64_t n_obj, uint64_t obj_len, uint64_t obj_stride, uint64_t base_seed,
                        uint64_t first, int grid, hipStream_t stream);

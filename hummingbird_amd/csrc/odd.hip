@@ -7,41 +7,44 @@
 //
 // What the hardware prefers (scripts/unaligned_probe.hip, profiles/r03_unaligned_probe.jsonl):
 // 16-B loads and stores at byte-misaligned addresses stream at 52-55 % of
-// 8 TB/s for the 4+2 pattern against 70 % aligned, and misaligned STORES cost
-// most (a copy loses 11-14 % with misaligned stores, 4-9 % with misaligned
-// loads).  So every access here is a 16-B-aligned block, and the shift to a
-// common byte frame happens in registers:
+// 8 TB/s for the 4+2 pattern against 70 % aligned; a copy loses 4.5 % with
+// dword-aligned (not 16-B-aligned) loads, 9 % with byte-misaligned loads and
+// 11-14 % with misaligned stores.  So:
 //
 //  * Frame.  Column i of an object covers shard positions [c_i, c_i + 16),
-//    c_i = c0 + 16 i, with c0 = -32 + (-out0 mod 16): output 0's stores are
-//    then aligned as they are.  One wave window = 64 consecutive columns; it
+//    c_i = c0 + 16 i, with c0 = -32 + (-out0 mod 16): output 0's blocks are
+//    16-B aligned as they are.  One wave window = 64 consecutive columns; it
 //    STORES 62 blocks (the last two lanes only feed their neighbours), and
 //    windows step 62 columns = 992 B.
-//  * Inputs.  Lane i loads the aligned block of input j holding position c_i
-//    (buffer loads: the descriptor's range makes blocks outside the shard read
-//    as zero, no clamping), takes lane i+1's block by a DPP lane shift
-//    (v_mov_b32_dpp wave_shl:1, no LDS) and shifts its column out of the 32
-//    bytes (v_cndmask dword select + v_alignbyte, d_j = (in_j + c0) mod 16
-//    wave-uniform).
-//  * Outputs.  Output r's aligned blocks sit at positions c_i + delta_r,
-//    delta_r = (-(out_r + c0)) mod 16: lane i stores bytes [delta_r, delta_r
-//    + 16) of its column and lane i+1's (the same DPP shift), a 16-B-aligned
-//    store.  Blocks that straddle the shard's head or tail are stored bytewise
-//    (only the first and last window of a shard do that); every output byte
-//    has exactly one owner lane, so accumulate passes (k > 8: out ^= ...) read
-//    the old block and write it back race-free.
-//  * Verify.  The stored parity is loaded and shifted like an input and
-//    compared column by column with the recomputed one (bytes outside [0, S)
-//    masked); nothing is written but one flag per object.
+//  * Inputs are loaded as dword-aligned 16-B blocks (the block holding the
+//    column's first byte, rounded down to a dword): the column is then bytes
+//    [sh, sh + 16) of the lane's block and lane l+1's first dword, one DPP
+//    lane shift (v_mov_b32_dpp wave_shl:1) and four v_alignbyte_b32 with the
+//    wave-uniform shift sh_j = (in_j + c0) mod 4.
+//  * Outputs are stored as 16-B-aligned blocks only: output r's blocks sit at
+//    positions c_i + delta_r, delta_r = (-(out_r + c0)) mod 16, so lane i
+//    stores bytes [delta_r, delta_r + 16) of its column and lane i+1's (DPP
+//    shifts, a v_cndmask dword select and v_alignbyte; output 0 needs none).
+//  * Guard band.  The main kernel stores (compares) only blocks that lie in
+//    [G, S - G), G = 48 B: every column such a block needs is then read
+//    whole from inside the shard, so no load needs a clamp that matters and
+//    no store a byte mask, and every output byte has one owner lane (the
+//    accumulate passes of k > 8 read the old block and write it back
+//    race-free).  The < 64 head and < 64 tail bytes of each output shard (all
+//    of a shard of S <= 160 B) are coded byte by byte by gf_odd_edges, a
+//    second, tiny launch.
+//  * Verify: the stored parity is loaded and shifted like an input and
+//    compared column by column; nothing is written but one flag per object.
 //
 // Schedule: the one of gf_apply_vec_pipe2 — compile-time K <= 8 with the
-// coefficient tables hoisted once, one 4-wave block per CU, the next tile's
-// loads in flight while the current tile computes and stores, one block
-// barrier per tile with a block-uniform trip count (past-the-end waves load a
-// stand-in tile and store nothing), XCD-grouped block order.
+// coefficient tables hoisted once, 4-wave blocks, the next tile's loads in
+// flight while the current tile computes and stores, one block barrier per
+// tile with a block-uniform trip count (past-the-end waves load a stand-in
+// tile and store nothing), XCD-grouped block order.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <cstdlib>
 
 #include "gf_device.h"
@@ -51,12 +54,19 @@ namespace hbec {
 
 constexpr uint32_t kOddStore = 62;            // blocks stored per 64-lane window
 constexpr uint32_t kOddWin = kOddStore * 16;  // shard bytes per window (992)
+constexpr int32_t kOddGuard = 48;             // bytes at each end left to gf_odd_edges
+constexpr int32_t kOddEdgeSlots = 160;        // edge bytes handled per (shard, output): 80 head + 80 tail
+// the main kernel runs on shards longer than this (shorter ones: gf_odd_edges only)
+constexpr uint64_t kOddMinMain = (uint64_t)kOddEdgeSlots;
 
 #ifndef HBEC_ODD_SLEEP
 #define HBEC_ODD_SLEEP 0  // x 64 cycles after the next tile's loads
 #endif
 #ifndef HBEC_ODD_BARRIER
-#define HBEC_ODD_BARRIER 1
+#define HBEC_ODD_BARRIER 1  // apply: one block barrier per tile
+#endif
+#ifndef HBEC_ODD_VBARRIER
+#define HBEC_ODD_VBARRIER 0  // verify: none (8+3 57 -> 66 %, 6+3 63 -> 70 %, profiles/r03_tune_odd3.jsonl)
 #endif
 #ifndef HBEC_ODD_VMIN
 #define HBEC_ODD_VMIN 1  // K*R from which all table words live in VGPRs (1: always)
@@ -65,22 +75,20 @@ constexpr uint32_t kOddWin = kOddStore * 16;  // shard bytes per window (992)
 #define HBEC_ODD_LB 1  // launch_bounds min blocks per CU (register budget)
 #endif
 #ifndef HBEC_ODD_U_SMALL
-#define HBEC_ODD_U_SMALL 0  // windows per wave tile for K <= 4 (0: 4 / K)
+#define HBEC_ODD_U_SMALL 2  // windows per wave tile for K <= 4 (0: 4 / K); 2: 4+2 62.5 -> 65 % (r03_tune_odd3)
 #endif
-// How a column is shifted into the frame: 1 = through LDS (the block is
-// written at lane*16 and read back at lane*16 + d: one ds_write_b128 and one
-// unaligned ds_read_b128); 0 = in registers (DPP lane shift, v_cndmask dword
-// select, v_alignbyte: ~19 VALU per column).
-#ifndef HBEC_ODD_REALIGN
-#define HBEC_ODD_REALIGN 1
+#ifndef HBEC_ODD_U_VERIFY
+#define HBEC_ODD_U_VERIFY 0  // windows per wave tile of verify for K <= 4 (0: as apply)
 #endif
 
 enum : int { kOddApply = 0, kOddAcc = 1, kOddVerify = 2 };
 
 // windows per wave tile of the strided kernel: ~4 loads per lane in flight
 // for K <= 4 (as gf_apply_vec_pipe2's 1 KiB x 4 / K), one window above
-__host__ __device__ constexpr int odd_u(int k) {
-    return k <= 4 ? (HBEC_ODD_U_SMALL > 0 ? HBEC_ODD_U_SMALL : (4 / k)) : 1;
+__host__ __device__ constexpr int odd_u(int k, int mode = kOddApply) {
+    return (mode == kOddVerify && HBEC_ODD_U_VERIFY > 0 && k <= 4)
+               ? HBEC_ODD_U_VERIFY
+               : (k <= 4 ? (HBEC_ODD_U_SMALL > 0 ? HBEC_ODD_U_SMALL : (4 / k)) : 1);
 }
 constexpr int kOddPlanU = 1;  // plans: one window per record
 
@@ -91,61 +99,48 @@ struct OddTile {
     uint64_t in[K];   // input shard bases (any alignment)
     uint64_t out[R];  // output (or stored parity) shard bases
     int32_t S;
-    int32_t c;        // shard position of the tile's first column (>= -32)
+    int32_t c;        // shard position of the tile's first column
     uint32_t live;    // 0: past-the-end stand-in (loaded, never stored)
     uint32_t obj;     // flag index (verify)
 };
 
 __device__ __forceinline__ int32_t odd_c0(uint64_t out0) { return (int32_t)((16u - ((uint32_t)out0 & 15u)) & 15u) - 32; }
 
-// Buffer view of one shard: its 16-B blocks from base & ~15 on; a column's
-// block offset may be negative (wraps to huge) or past the end: both read
-// as zero, so loads need no clamping.
-struct OddSrc {
-    __amdgpu_buffer_rsrc_t rs;
-    uint64_t base;  // base & ~15 (global-load variant)
-    int32_t nb;     // blocks holding shard bytes (global-load variant)
-    int32_t g;      // block of the tile's first column
+// One shard's dword-aligned 16-B blocks for one tile: lane column col's block
+// starts off + 16 col bytes after base4, clamped into the shard's dwords
+// (the clamp only ever moves columns the guard band keeps from being stored).
+struct OddIn {
+    uint64_t base4;  // base & ~3
+    int32_t off;     // block start of the tile's first column, from base4
+    int32_t lim;     // last block start inside the shard's dwords
+    uint32_t sh;     // the column's first byte within the block (0..3)
 };
 
-__device__ __forceinline__ OddSrc odd_src(uint64_t base, int32_t S, int32_t c) {
-    const int32_t l = (int32_t)((uint32_t)base & 15u);
-    OddSrc o;
-    o.rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(base & ~(uint64_t)15), (short)0,
-                                             (int)((uint32_t)(l + S + 15) & ~15u), 0x00020000);
-    o.g = (l + c) >> 4;  // arithmetic: floor for c < 0
-    o.base = base & ~(uint64_t)15;
-    o.nb = (l + S + 15) >> 4;
+__device__ __forceinline__ OddIn odd_in(uint64_t base, int32_t S, int32_t c) {
+    const int32_t l4 = (int32_t)((uint32_t)base & 3u);
+    const int32_t t = l4 + c;
+    OddIn o;
+    o.base4 = base & ~(uint64_t)3;
+    o.sh = (uint32_t)t & 3u;
+    o.off = t - (int32_t)o.sh;
+    o.lim = ((l4 + S + 3) & ~3) - 16;
     return o;
 }
 
-#ifndef HBEC_ODD_GLOBAL
-#define HBEC_ODD_GLOBAL 0  // 1: global loads at a clamped block index instead of buffer loads
-#endif
-
-__device__ __forceinline__ u32x4 odd_ld(const OddSrc& o, int32_t col) {
-    if constexpr (HBEC_ODD_GLOBAL) {
-        // blocks outside [0, nb) hold no shard byte: clamp to one that exists
-        const int32_t b = __builtin_amdgcn_readfirstlane(o.nb) - 1;
-        int32_t i = col + o.g;
-        i = i < 0 ? 0 : (i > b ? b : i);
-        return ld16_addr(o.base + (uint64_t)(uint32_t)(i * 16));
-    } else {
-        return __builtin_amdgcn_raw_buffer_load_b128(o.rs, (uint32_t)((col + o.g) * 16), 0, 2 /* nt */);
-    }
+__device__ __forceinline__ u32x4 odd_ld(const OddIn& o, int32_t col) {
+    int32_t v = o.off + 16 * col;
+    v = v < 0 ? 0 : (v > o.lim ? o.lim : v);
+    return ld16_addr(o.base4 + (uint64_t)(uint32_t)v);
 }
 
-__device__ __forceinline__ uint32_t odd_d(uint64_t base, int32_t c) { return ((uint32_t)base + (uint32_t)c) & 15u; }
+// bytes [sh, sh + 16) of the lane's block and lane l+1's first dword
+__device__ __forceinline__ u32x4 odd_shift_in(const u32x4& v, uint32_t sh) {
+    const uint32_t n0 = lane_next(v[0]);
+    return u32x4{__builtin_amdgcn_alignbyte(v[1], v[0], sh), __builtin_amdgcn_alignbyte(v[2], v[1], sh),
+                 __builtin_amdgcn_alignbyte(v[3], v[2], sh), __builtin_amdgcn_alignbyte(n0, v[3], sh)};
+}
 
 typedef __attribute__((address_space(1))) uint8_t gu8_t;
-
-// bytes [lo, hi) of the block v to p (byte stores; head / tail blocks only)
-__device__ __forceinline__ void odd_store_part(uint64_t p, const u32x4& v, int32_t lo, int32_t hi) {
-    gu8_t* d = reinterpret_cast<gu8_t*>(p);
-#pragma unroll
-    for (int b = 0; b < 16; ++b)
-        if (b >= lo && b < hi) d[b] = (uint8_t)(v[b >> 2] >> (8 * (b & 3)));
-}
 
 // ---- tile sources ----
 // A source names tile t compactly (id(): a few scalars, carried one and two
@@ -205,26 +200,6 @@ struct OddPlan {
     }
 };
 
-// ---- shifting a column into the frame ----
-// LDS staging: per wave, one 1 KiB + 32 B slot per shard that is shifted.
-constexpr uint32_t kOddSlot = 1024 + 32;
-
-template <int NS>
-struct OddLds {
-    uint8_t* base;  // this wave's NS slots
-};
-
-// block v of lane l -> bytes [d, d + 16) of (v of lane l ++ v of lane l+1)
-template <int NS>
-__device__ __forceinline__ void odd_put(const OddLds<NS>& L, int slot, uint32_t lane, const u32x4& v) {
-    *reinterpret_cast<u32x4*>(L.base + slot * kOddSlot + lane * 16u) = v;
-}
-typedef u32x4 u32x4_u1 __attribute__((aligned(1)));
-template <int NS>
-__device__ __forceinline__ u32x4 odd_get(const OddLds<NS>& L, int slot, uint32_t lane, uint32_t d) {
-    return *reinterpret_cast<const u32x4_u1*>(L.base + slot * kOddSlot + lane * 16u + d);
-}
-
 // ---- one tile ----
 template <int K, int R, int U, int MODE>
 struct OddRegs {
@@ -234,130 +209,77 @@ struct OddRegs {
 
 template <int K, int R, int U, int MODE>
 __device__ __forceinline__ void odd_load(OddRegs<K, R, U, MODE>& X, const OddTile<K, R>& b, uint32_t lane) {
-    OddSrc src[OddRegs<K, R, U, MODE>::NL];
+    constexpr int NL = OddRegs<K, R, U, MODE>::NL;
+    OddIn src[NL];
 #pragma unroll
-    for (int j = 0; j < K; ++j) src[j] = odd_src(b.in[j], b.S, b.c);
+    for (int j = 0; j < K; ++j) src[j] = odd_in(b.in[j], b.S, b.c);
     if constexpr (MODE == kOddVerify) {
 #pragma unroll
-        for (int r = 0; r < R; ++r) src[K + r] = odd_src(b.out[r], b.S, b.c);
+        for (int r = 0; r < R; ++r) src[K + r] = odd_in(b.out[r], b.S, b.c);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-        for (int j = 0; j < OddRegs<K, R, U, MODE>::NL; ++j)
-            X.x[u][j] = odd_ld(src[j], (int32_t)(u * kOddStore + lane));
+        for (int j = 0; j < NL; ++j) X.x[u][j] = odd_ld(src[j], (int32_t)(u * kOddStore + lane));
 }
-
-// LDS slots per wave: K inputs (+ R stored parity for verify, + R outputs)
-template <int K, int R, int MODE>
-__host__ __device__ constexpr int odd_slots() { return K + R; }
 
 template <int K, int R, int U, int MODE>
 __device__ __forceinline__ void odd_finish(const OddRegs<K, R, U, MODE>& X, const OddTile<K, R>& b,
                                            const TabArray& tab, const Tables<K, R, HBEC_ODD_VMIN>& tb, uint32_t lane,
-                                           uint32_t* flags, const OddLds<odd_slots<K, R, MODE>()>& L) {
-    uint32_t d[K];
+                                           uint32_t* flags) {
+    constexpr int NL = OddRegs<K, R, U, MODE>::NL;
+    uint32_t sh[NL];
 #pragma unroll
-    for (int j = 0; j < K; ++j) d[j] = __builtin_amdgcn_readfirstlane(odd_d(b.in[j], b.c));
+    for (int j = 0; j < K; ++j) sh[j] = __builtin_amdgcn_readfirstlane(((uint32_t)b.in[j] + (uint32_t)b.c) & 3u);
+    if constexpr (MODE == kOddVerify) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            sh[K + r] = __builtin_amdgcn_readfirstlane(((uint32_t)b.out[r] + (uint32_t)b.c) & 3u);
+    }
     const int32_t S = b.S;
+    const int32_t hi = S - kOddGuard - 16;  // last block start the main kernel stores / compares
     bool bad = false;
-    OddSrc old[MODE == kOddAcc ? R : 1];
     uint32_t dl[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-        dl[r] = __builtin_amdgcn_readfirstlane((16u - odd_d(b.out[r], b.c)) & 15u);
-        if constexpr (MODE == kOddAcc) old[r] = odd_src(b.out[r], S, b.c + (int32_t)dl[r]);
-    }
+    for (int r = 0; r < R; ++r) dl[r] = __builtin_amdgcn_readfirstlane((16u - (((uint32_t)b.out[r] + (uint32_t)b.c) & 15u)) & 15u);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-        const int32_t w0 = b.c + (int32_t)(u * kOddWin);  // window's first column
-        const int32_t cpos = w0 + 16 * (int32_t)lane;
-        // window-uniform: every block this window stores (or compares) lies inside [0, S)
-        const bool interior = w0 >= 0 && w0 + (int32_t)kOddWin + 16 <= S;
+        const int32_t cpos = b.c + (int32_t)(u * kOddWin) + 16 * (int32_t)lane;  // this lane's column
         u32x4 x[K];
-        if constexpr (HBEC_ODD_REALIGN == 1) {
 #pragma unroll
-            for (int j = 0; j < K; ++j) odd_put(L, j, lane, X.x[u][j]);
-            if constexpr (MODE == kOddVerify) {
-#pragma unroll
-                for (int r = 0; r < R; ++r) odd_put(L, K + r, lane, X.x[u][K + r]);
-            }
-#pragma unroll
-            for (int j = 0; j < K; ++j) x[j] = odd_get(L, j, lane, d[j]);
-        } else {
-#pragma unroll
-            for (int j = 0; j < K; ++j) x[j] = realign16(X.x[u][j], lane_next4(X.x[u][j]), d[j]);
-        }
+        for (int j = 0; j < K; ++j) x[j] = odd_shift_in(X.x[u][j], sh[j]);
         u32x4 acc[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) acc[r] = u32x4{0, 0, 0, 0};
         gf_dot<K, R, HBEC_ODD_VMIN>(acc, x, tab, tb);
         if constexpr (MODE == kOddVerify) {
+            // frame columns = output 0's blocks: compare those inside the guard band
+            const bool mine = b.live != 0u && lane < kOddStore && cpos >= kOddGuard && cpos <= hi;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                const uint32_t dp = __builtin_amdgcn_readfirstlane(odd_d(b.out[r], b.c));
-                u32x4 st;
-                if constexpr (HBEC_ODD_REALIGN == 1)
-                    st = odd_get(L, K + r, lane, dp);
-                else
-                    st = realign16(X.x[u][K + r], lane_next4(X.x[u][K + r]), dp);
-                const u32x4 df = st ^ acc[r];
-                if (interior) {
-                    bad |= lane < kOddStore && (df[0] | df[1] | df[2] | df[3]) != 0u;
-                } else if (lane < kOddStore) {
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        // bytes of dword e at positions cpos + 4e .. + 3 that lie in [0, S)
-                        uint32_t m = 0;
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            const int32_t pos = cpos + 4 * e + q;
-                            m |= (pos >= 0 && pos < S) ? (0xFFu << (8 * q)) : 0u;
-                        }
-                        bad |= (df[e] & m) != 0u;
-                    }
-                }
+                const u32x4 df = odd_shift_in(X.x[u][K + r], sh[K + r]) ^ acc[r];
+                bad |= mine && (df[0] | df[1] | df[2] | df[3]) != 0u;
             }
         } else {
-            u32x4 blk[R];
-            if constexpr (HBEC_ODD_REALIGN == 1) {
 #pragma unroll
-                for (int r = 0; r < R; ++r)
-                    if (dl[r] != 0u) odd_put(L, K + r, lane, acc[r]);  // wave-uniform (r = 0 never)
-#pragma unroll
-                for (int r = 0; r < R; ++r) blk[r] = dl[r] == 0u ? acc[r] : odd_get(L, K + r, lane, dl[r]);
-            } else {
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    if (dl[r] == 0u)  // wave-uniform: output r is in the frame (always r = 0)
-                        blk[r] = acc[r];
-                    else
-                        blk[r] = realign16(acc[r], lane_next4(acc[r]), dl[r]);
+            for (int r = 0; r < R; ++r) {
+                u32x4 blk = acc[r];
+                if (dl[r] != 0u) blk = realign16(acc[r], lane_next4(acc[r]), dl[r]);  // wave-uniform (never r = 0)
+                const int32_t q = cpos + (int32_t)dl[r];  // block start: out[r] + q is 16-B aligned
+                const bool mine = b.live != 0u && lane < kOddStore && q >= kOddGuard && q <= hi;
+                if constexpr (MODE == kOddAcc) {
+                    // the old block; lanes that do not store read one inside the band instead
+                    const int32_t e = (int32_t)(((uint32_t)b.c + dl[r]) & 15u);  // q = e mod 16
+                    const int32_t qmin = kOddGuard + e, qmax = hi - ((hi - e) & 15);
+                    const int32_t qc = q < qmin ? qmin : (q > qmax ? qmax : q);
+                    blk ^= ld16_addr(b.out[r] + (uint64_t)(int64_t)qc);
                 }
-            }
-            if constexpr (MODE == kOddAcc) {
-#pragma unroll
-                for (int r = 0; r < R; ++r) blk[r] ^= odd_ld(old[r], (int32_t)(u * kOddStore + lane));
-            }
-            if (b.live != 0u) {
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    const int32_t q = cpos + (int32_t)dl[r];  // block start: out[r] + q is 16-B aligned
-                    const uint64_t p = b.out[r] + (uint64_t)(int64_t)q;
-                    if (interior) {
-                        if (lane < kOddStore) st16_addr(p, blk[r]);
-                    } else if (lane < kOddStore && q < S && q + 16 > 0) {
-                        if (q >= 0 && q + 16 <= S)
-                            st16_addr(p, blk[r]);
-                        else
-                            odd_store_part(p, blk[r], q < 0 ? -q : 0, q + 16 > S ? S - q : 16);
-                    }
-                }
+                if (mine) st16_addr(b.out[r] + (uint64_t)(int64_t)q, blk);
             }
         }
     }
     if constexpr (MODE == kOddVerify) {
-        if (b.live != 0u && __any(bad)) {
+        if (__any(bad)) {
             if (lane == 0u) atomicOr(flags + b.obj, 1u);
         }
     }
@@ -366,14 +288,11 @@ __device__ __forceinline__ void odd_finish(const OddRegs<K, R, U, MODE>& X, cons
 template <int K, int R, int U, int MODE, class Src>
 __device__ __forceinline__ void odd_body(const Src& src, uint32_t n, const TabArray& tab, uint32_t* flags) {
     constexpr uint32_t WPB = kPipeBlockThreads / 64;
-    constexpr int NS = odd_slots<K, R, MODE>();
-    __shared__ __attribute__((aligned(16))) uint8_t lds[HBEC_ODD_REALIGN == 1 ? WPB * NS * kOddSlot : 16];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t nw = gridDim.x * WPB;
     const uint32_t wave0 = __builtin_amdgcn_readfirstlane(xcd_block() * WPB);  // the block's first wave
     const uint32_t dw = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (wave0 >= n) return;  // whole blocks only: the loop below has block barriers
-    const OddLds<NS> L{lds + (HBEC_ODD_REALIGN == 1 ? dw * NS * kOddSlot : 0)};
     const Tables<K, R, HBEC_ODD_VMIN> tb = load_tables<K, R, HBEC_ODD_VMIN>(tab);
     typename Src::Id cur = src.id(wave0 + dw, n);
     OddRegs<K, R, U, MODE> X;
@@ -391,12 +310,12 @@ __device__ __forceinline__ void odd_body(const Src& src, uint32_t n, const TabAr
             odd_load<K, R, U, MODE>(Y, b, lane);
         }
         if (HBEC_ODD_SLEEP > 0) __builtin_amdgcn_s_sleep(HBEC_ODD_SLEEP);
-        if (HBEC_ODD_BARRIER) __builtin_amdgcn_s_barrier();
+        if (MODE == kOddVerify ? HBEC_ODD_VBARRIER : HBEC_ODD_BARRIER) __builtin_amdgcn_s_barrier();
         const typename Src::Id after = src.id(b0 + dw + nw, n);
         {
             OddTile<K, R> b;
             src.at(b, cur);
-            odd_finish<K, R, U, MODE>(X, b, tab, tb, lane, flags, L);
+            odd_finish<K, R, U, MODE>(X, b, tab, tb, lane, flags);
         }
         X = Y;
         cur = nxt;
@@ -404,18 +323,104 @@ __device__ __forceinline__ void odd_body(const Src& src, uint32_t n, const TabAr
     }
     OddTile<K, R> b;
     src.at(b, cur);
-    odd_finish<K, R, U, MODE>(X, b, tab, tb, lane, flags, L);
+    odd_finish<K, R, U, MODE>(X, b, tab, tb, lane, flags);
 }
 
 template <int K, int R, int MODE>
 __global__ __launch_bounds__(kPipeBlockThreads, HBEC_ODD_LB) void gf_odd(PassArgs a, uint32_t* flags) {
-    constexpr int U = odd_u(K);
+    constexpr int U = odd_u(K, MODE);
     odd_body<K, R, U, MODE>(OddStrided<K, R, U>{a}, a.n_tiles, a.tab, flags);
 }
 
 template <int K, int R, int MODE>
 __global__ __launch_bounds__(kPipeBlockThreads, HBEC_ODD_LB) void gf_odd_plan(UPlanArgs p, const URec* __restrict__ recs) {
     odd_body<K, R, kOddPlanU, MODE>(OddPlan<K, R>{p, recs}, p.n_recs, p.tab, nullptr);
+}
+
+// ---------------------------------------------------------------------------
+// gf_odd_edges: the bytes the main kernel leaves to the guard band, coded one
+// byte per thread: for output r of a shard of S bytes, positions [0, qmin_r)
+// and [qmax_r + 16, S), qmin_r / qmax_r the first / last 16-B-aligned block
+// of output r inside [G, S - G) (all of [0, S) when S <= kOddMinMain).  In
+// verify mode the compared columns are output 0's blocks for every r.  K <= 16
+// inputs, R <= 4 outputs per launch (one pass of apply_views).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool odd_edge_pos(int32_t S, uint64_t out_frame, int32_t slot, int32_t* pos) {
+    if (S <= kOddEdgeSlots) {
+        *pos = slot;
+        return slot < S;
+    }
+    const int32_t e = (int32_t)((16u - ((uint32_t)out_frame & 15u)) & 15u);  // aligned block positions = e mod 16
+    const int32_t qmin = kOddGuard + e;
+    const int32_t top = S - kOddGuard - 16;
+    const int32_t qmax = top - ((top - e) & 15);
+    if (slot < kOddEdgeSlots / 2) {
+        *pos = slot;
+        return slot < qmin;
+    }
+    *pos = S - kOddEdgeSlots + slot;
+    return *pos >= qmax + 16;
+}
+
+__device__ __forceinline__ uint32_t odd_edge_byte(const TabArray& tab, int r, int K, const uint64_t* in, int32_t p) {
+    uint32_t v = 0;
+    for (int j = 0; j < K; ++j) {
+        const uint32_t x = *reinterpret_cast<const gu8_t*>(in[j] + (uint64_t)p);
+        const uint32_t* t = tab[r][j];
+        v ^= gf_mul_sel(selectors(x), t[0], t[1], t[2], t[3], t[4]);
+    }
+    return v & 0xFFu;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kBlockThreads) void gf_odd_edges(PassArgs a, int K, int R, uint32_t* flags) {
+    const uint64_t per_obj = (uint64_t)R * kOddEdgeSlots;
+    const uint64_t total = a.n_obj * per_obj;
+    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < total; v += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t obj = v / per_obj;
+        const uint32_t rs = (uint32_t)(v - obj * per_obj);
+        const int r = (int)(rs / kOddEdgeSlots);
+        const int32_t slot = (int32_t)(rs - (uint32_t)r * kOddEdgeSlots);
+        uint64_t in[kMaxK];
+        for (int j = 0; j < K; ++j) in[j] = reinterpret_cast<uint64_t>(a.in[j]) + obj * a.in_stride[j];
+        const uint64_t out = reinterpret_cast<uint64_t>(a.out[r]) + obj * a.out_stride[r];
+        const uint64_t frame = MODE == kOddVerify ? reinterpret_cast<uint64_t>(a.out[0]) + obj * a.out_stride[0] : out;
+        int32_t p;
+        if (!odd_edge_pos((int32_t)a.shard_len, frame, slot, &p)) continue;
+        uint32_t val = odd_edge_byte(a.tab, r, K, in, p);
+        gu8_t* d = reinterpret_cast<gu8_t*>(out + (uint64_t)p);
+        if (MODE == kOddVerify) {
+            if (val != *d) atomicOr(flags + obj, 1u);
+        } else {
+            if (MODE == kOddAcc) val ^= *d;
+            *d = (uint8_t)val;
+        }
+    }
+}
+
+// plans: one edge record per stripe / object (URec, p0 unused)
+template <int MODE>
+__global__ __launch_bounds__(kBlockThreads) void gf_odd_edges_plan(UPlanArgs p, const URec* __restrict__ erecs,
+                                                                  uint32_t n_erecs, int K, int R) {
+    const uint64_t per = (uint64_t)R * kOddEdgeSlots;
+    const uint64_t total = (uint64_t)n_erecs * per;
+    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < total; v += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t e = v / per;
+        const uint32_t rs = (uint32_t)(v - e * per);
+        const int r = (int)(rs / kOddEdgeSlots);
+        const int32_t slot = (int32_t)(rs - (uint32_t)r * kOddEdgeSlots);
+        const URec rec = erecs[e];
+        const uint64_t S = rec.shard_len;
+        uint64_t in[kMaxK];
+        for (int j = 0; j < K; ++j) in[j] = (((p.in_sel >> j) & 1u) ? rec.b : rec.a) + (uint64_t)p.in_idx[j] * S;
+        const uint64_t out = (((p.out_sel >> r) & 1u) ? rec.b : rec.a) + (uint64_t)p.out_idx[r] * S;
+        int32_t q;
+        if (!odd_edge_pos((int32_t)S, out, slot, &q)) continue;
+        uint32_t val = odd_edge_byte(p.tab, r, K, in, q);
+        gu8_t* d = reinterpret_cast<gu8_t*>(out + (uint64_t)q);
+        if (MODE == kOddAcc) val ^= *d;
+        *d = (uint8_t)val;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -458,7 +463,7 @@ static const void* odd_kernel(int k, int r, int mode, bool plan) {
 }
 
 #ifndef HBEC_ODD_DEFAULT
-#define HBEC_ODD_DEFAULT 0  // until gf_odd beats the round-2 kernels on every odd shape
+#define HBEC_ODD_DEFAULT 1
 #endif
 bool odd_enabled() {
     static const bool on = [] {
@@ -468,29 +473,35 @@ bool odd_enabled() {
     return on;
 }
 
-#ifndef HBEC_ODD_BPC_DEFAULT
-#define HBEC_ODD_BPC_DEFAULT 1
+#ifndef HBEC_ODD_BPC_APPLY
+#define HBEC_ODD_BPC_APPLY 1
 #endif
-int odd_blocks_per_cu() {
+#ifndef HBEC_ODD_BPC_VERIFY
+#define HBEC_ODD_BPC_VERIFY 2  // read-only: 4+2 68.5 -> 81 % with 2 blocks per CU (r03_tune_odd3)
+#endif
+int odd_blocks_per_cu(int mode) {
     static const int v = [] {
         const char* e = std::getenv("HBEC_ODD_BPC");
-        const int x = e ? std::atoi(e) : 0;
-        return x > 0 ? x : HBEC_ODD_BPC_DEFAULT;
+        return e ? std::atoi(e) : 0;
     }();
-    return v;
+    return v > 0 ? v : (mode == kOddVerify ? HBEC_ODD_BPC_VERIFY : HBEC_ODD_BPC_APPLY);
 }
 
 uint64_t urec_tile() { return odd_enabled() ? (uint64_t)kOddPlanU * kOddWin : (uint64_t)unaligned_tile_bytes(); }
-uint64_t urec_span(uint64_t shard_len) { return odd_enabled() ? shard_len + 32u : shard_len; }
+uint64_t urec_span(uint64_t shard_len) {
+    if (!odd_enabled()) return shard_len;
+    return shard_len > kOddMinMain ? shard_len + 32u : 0u;
+}
 
 uint32_t odd_tile_bytes(int k) { return (uint32_t)odd_u(k) * kOddWin; }
+uint64_t odd_min_main() { return kOddMinMain; }
 uint32_t odd_plan_tile_bytes() { return (uint32_t)kOddPlanU * kOddWin; }
 
 // Tiles per shard: enough windows for every output block of the shard, from
 // the frame's first column (c0 >= -32) to position S.
-uint32_t odd_tiles_per_obj(int k, uint64_t shard_len) {
+uint32_t odd_tiles_per_obj(int k, int mode, uint64_t shard_len) {
     const uint64_t span = shard_len + 32u;
-    const uint64_t tile = odd_tile_bytes(k);
+    const uint64_t tile = (uint64_t)odd_u(k, mode) * kOddWin;
     return (uint32_t)((span + tile - 1) / tile);
 }
 
@@ -501,6 +512,27 @@ hipError_t launch_odd(int k, int r, int mode, const PassArgs& a, uint32_t* flags
     if (!fn) return hipErrorInvalidValue;
     void* args[] = {const_cast<PassArgs*>(&a), &flags};
     return hipLaunchKernel(fn, dim3(grid), dim3(kPipeBlockThreads), args, 0, stream);
+}
+
+hipError_t launch_odd_edges(int k, int r, int mode, const PassArgs& a, uint32_t* flags, hipStream_t stream) {
+    if (k < 1 || k > kMaxK || r < 1 || r > kMaxR || a.n_obj == 0) return a.n_obj == 0 ? hipSuccess : hipErrorInvalidValue;
+    const uint64_t total = a.n_obj * (uint64_t)r * kOddEdgeSlots;
+    const int grid = (int)std::min<uint64_t>((total + kBlockThreads - 1) / kBlockThreads, 4096);
+    const void* fn = mode == kOddVerify ? (const void*)&gf_odd_edges<kOddVerify>
+                                        : (mode == kOddAcc ? (const void*)&gf_odd_edges<kOddAcc> : (const void*)&gf_odd_edges<kOddApply>);
+    void* args[] = {const_cast<PassArgs*>(&a), &k, &r, &flags};
+    return hipLaunchKernel(fn, dim3(grid), dim3(kBlockThreads), args, 0, stream);
+}
+
+hipError_t launch_odd_edges_plan(int k, int r, int mode, const UPlanArgs& p, const URec* erecs, uint32_t n_erecs,
+                                 hipStream_t stream) {
+    if (n_erecs == 0) return hipSuccess;
+    if (k < 1 || k > kMaxK || r < 1 || r > kMaxR || mode == kOddVerify) return hipErrorInvalidValue;
+    const uint64_t total = (uint64_t)n_erecs * (uint64_t)r * kOddEdgeSlots;
+    const int grid = (int)std::min<uint64_t>((total + kBlockThreads - 1) / kBlockThreads, 4096);
+    const void* fn = mode == kOddAcc ? (const void*)&gf_odd_edges_plan<kOddAcc> : (const void*)&gf_odd_edges_plan<kOddApply>;
+    void* args[] = {const_cast<UPlanArgs*>(&p), &erecs, &n_erecs, &k, &r};
+    return hipLaunchKernel(fn, dim3(grid), dim3(kBlockThreads), args, 0, stream);
 }
 
 hipError_t launch_odd_plan(int k, int r, int mode, const UPlanArgs& p, int grid, hipStream_t stream) {

@@ -38,6 +38,9 @@ struct hbec_plan {
     // stripes / objects the tiled kernel cannot take: unaligned-kernel records
     hbec::URec* d_urecs = nullptr;
     uint64_t n_urecs = 0;
+    // gf_odd: one edge record per such stripe / object (its guard-band bytes)
+    hbec::URec* d_erecs = nullptr;
+    uint64_t n_erecs = 0;
 };
 
 namespace {
@@ -54,10 +57,12 @@ bool aligned_object(const hbec_object& o) {
 
 std::mutex g_occ_mu;
 
-void add_urecs(std::vector<hbec::URec>& recs, const void* a, const void* b, uint64_t s) {
+void add_urecs(std::vector<hbec::URec>& recs, std::vector<hbec::URec>& erecs, const void* a, const void* b,
+               uint64_t s) {
     const uint64_t tile = hbec::urec_tile(), span = hbec::urec_span(s);
     for (uint64_t p0 = 0; p0 < span; p0 += tile)
         recs.push_back({reinterpret_cast<uint64_t>(a), reinterpret_cast<uint64_t>(b), s, p0});
+    if (hbec::odd_enabled()) erecs.push_back({reinterpret_cast<uint64_t>(a), reinterpret_cast<uint64_t>(b), s, 0});
 }
 
 template <class T>
@@ -81,9 +86,9 @@ int upload(const std::vector<T>& recs, T** dst, const char* what) {
 // object records (shard indices >= sel_k are parity, base b).
 int hbec::launch_unaligned_passes(const URec* recs, uint64_t n_recs, const std::vector<int>& in_idx,
                                   const std::vector<int>& out_idx, const std::vector<uint8_t>& rows, int sel_k,
-                                  hipStream_t stream, int max_blocks) {
+                                  hipStream_t stream, int max_blocks, const URec* erecs, uint64_t n_erecs) {
     const int K_all = (int)in_idx.size(), R_all = (int)out_idx.size();
-    if (n_recs == 0 || R_all == 0) return HBEC_OK;
+    if ((n_recs == 0 && n_erecs == 0) || R_all == 0) return HBEC_OK;
     int dev = 0, cus = 0, per_cu = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
@@ -120,11 +125,16 @@ int hbec::launch_unaligned_passes(const URec* recs, uint64_t n_recs, const std::
                         hbec::perm_table(rows[(size_t)(r0 + r) * K_all + c0 + j], a.tab[r][j]);
                 }
                 const uint64_t want = (n_recs + 3) / 4;  // 4 waves per block
-                uint64_t cap = (uint64_t)cus * (uint64_t)hbec::odd_blocks_per_cu();
+                uint64_t cap = (uint64_t)cus * (uint64_t)hbec::odd_blocks_per_cu(0);
                 if (max_blocks > 0) cap = std::min<uint64_t>(cap, (uint64_t)max_blocks);
                 const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, cap));
-                e = hbec::launch_odd_plan(K, R, c0 > 0 ? 1 : 0, a, grid, stream);
-                if (e != hipSuccess) return hip_fail(e, "launch gf_odd_plan");
+                if (n_recs > 0) {
+                    e = hbec::launch_odd_plan(K, R, c0 > 0 ? 1 : 0, a, grid, stream);
+                    if (e != hipSuccess) return hip_fail(e, "launch gf_odd_plan");
+                }
+                // guard-band bytes of every stripe, this pass's inputs
+                e = hbec::launch_odd_edges_plan(K, R, c0 > 0 ? 1 : 0, a, erecs, (uint32_t)n_erecs, stream);
+                if (e != hipSuccess) return hip_fail(e, "launch gf_odd_edges_plan");
             }
         }
         return HBEC_OK;
@@ -271,9 +281,11 @@ int run_plan(const hbec_plan* p, const std::vector<int>& in_idx, const std::vect
     }
     if (p->objects) {
         // with k > 8 every object is in the unaligned records (hbec_plan_objects)
-        return hbec::launch_unaligned_passes(p->d_urecs, p->n_urecs, in_idx, out_idx, rows, p->k, stream);
+        return hbec::launch_unaligned_passes(p->d_urecs, p->n_urecs, in_idx, out_idx, rows, p->k, stream, 0,
+                                             p->d_erecs, p->n_erecs);
     }
-    return hbec::launch_unaligned_passes(p->d_urecs, p->n_urecs, in_idx, out_idx, rows, 0, stream);
+    return hbec::launch_unaligned_passes(p->d_urecs, p->n_urecs, in_idx, out_idx, rows, 0, stream, 0, p->d_erecs,
+                                         p->n_erecs);
 }
 
 }  // namespace
@@ -291,7 +303,7 @@ int hbec_plan_stripes(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n,
         p->m = m;
         p->tile_bytes = hbec::stripes_tile_bytes(std::min(k, hbec::kStripeMaxK));
         std::vector<hbec::TileRec> recs;
-        std::vector<hbec::URec> urecs;
+        std::vector<hbec::URec> urecs, erecs;
         for (uint64_t i = 0; i < n; ++i) {
             const hbec_stripe& s = stripes[i];
             if (s.shard_len == 0) continue;
@@ -299,7 +311,7 @@ int hbec_plan_stripes(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n,
             p->shard_bytes += s.shard_len;
             if (!aligned_stripe(s)) {
                 p->fallback.push_back(s);
-                add_urecs(urecs, s.base, nullptr, s.shard_len);
+                add_urecs(urecs, erecs, s.base, nullptr, s.shard_len);
                 continue;
             }
             p->tiled.push_back(s);
@@ -313,7 +325,7 @@ int hbec_plan_stripes(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n,
             }
         }
         // both record counts are checked before anything is allocated on the device
-        if (recs.size() >= (1ull << 31) || urecs.size() >= (1ull << 31))
+        if (recs.size() >= (1ull << 31) || urecs.size() >= (1ull << 31) || erecs.size() >= (1ull << 31))
             return fail(HBEC_ERR_INVALID_ARG, "plan too large (>= 2^31 tiles)");
         p->n_tiles = recs.size();
         if (!recs.empty()) {
@@ -327,11 +339,14 @@ int hbec_plan_stripes(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n,
             }
         }
         int urc = upload(urecs, &p->d_urecs, "plan unaligned records");
+        if (!urc) urc = upload(erecs, &p->d_erecs, "plan edge records");
         if (urc) {
             if (p->d_tiles) (void)hipFree(p->d_tiles);
+            if (p->d_urecs) (void)hipFree(p->d_urecs);
             return urc;
         }
         p->n_urecs = urecs.size();
+        p->n_erecs = erecs.size();
         *out = p.release();
         return HBEC_OK;
     });
@@ -349,7 +364,7 @@ int hbec_plan_objects(hbec_codec* codec, const hbec_object* objects, uint64_t n,
         p->objects = true;
         p->tile_bytes = hbec::stripes_tile_bytes(std::min(k, hbec::kStripeMaxK));
         std::vector<hbec::TileRec> recs;
-        std::vector<hbec::URec> urecs;
+        std::vector<hbec::URec> urecs, erecs;
         for (uint64_t i = 0; i < n; ++i) {
             const hbec_object& o = objects[i];
             if (o.shard_len == 0) continue;
@@ -357,13 +372,13 @@ int hbec_plan_objects(hbec_codec* codec, const hbec_object* objects, uint64_t n,
             p->shard_bytes += o.shard_len;
             if (!aligned_object(o)) {
                 p->obj_fallback.push_back(o);
-                add_urecs(urecs, o.data, o.parity, o.shard_len);
+                add_urecs(urecs, erecs, o.data, o.parity, o.shard_len);
                 continue;
             }
             if (k > hbec::kStripeMaxK) {
                 // the object-plan tiled kernel takes <= 8 inputs: every object goes to
                 // the unaligned kernel's records (one launch per pass, not one per object)
-                add_urecs(urecs, o.data, o.parity, o.shard_len);
+                add_urecs(urecs, erecs, o.data, o.parity, o.shard_len);
                 continue;
             }
             p->obj_tiled.push_back(o);
@@ -378,7 +393,7 @@ int hbec_plan_objects(hbec_codec* codec, const hbec_object* objects, uint64_t n,
             }
         }
         // both record counts are checked before anything is allocated on the device
-        if (recs.size() >= (1ull << 31) || urecs.size() >= (1ull << 31))
+        if (recs.size() >= (1ull << 31) || urecs.size() >= (1ull << 31) || erecs.size() >= (1ull << 31))
             return fail(HBEC_ERR_INVALID_ARG, "plan too large (>= 2^31 tiles)");
         p->n_tiles = recs.size();
         if (!recs.empty()) {
@@ -392,11 +407,14 @@ int hbec_plan_objects(hbec_codec* codec, const hbec_object* objects, uint64_t n,
             }
         }
         int urc = upload(urecs, &p->d_urecs, "plan unaligned records");
+        if (!urc) urc = upload(erecs, &p->d_erecs, "plan edge records");
         if (urc) {
             if (p->d_tiles) (void)hipFree(p->d_tiles);
+            if (p->d_urecs) (void)hipFree(p->d_urecs);
             return urc;
         }
         p->n_urecs = urecs.size();
+        p->n_erecs = erecs.size();
         *out = p.release();
         return HBEC_OK;
     });
@@ -406,6 +424,7 @@ void hbec_plan_free(hbec_plan* plan) {
     if (!plan) return;
     if (plan->d_tiles) (void)hipFree(plan->d_tiles);
     if (plan->d_urecs) (void)hipFree(plan->d_urecs);
+    if (plan->d_erecs) (void)hipFree(plan->d_erecs);
     delete plan;
 }
 

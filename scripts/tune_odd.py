@@ -21,14 +21,10 @@ sys.path.insert(0, str(ROOT))
 
 VARIANTS = {
     "base": [],
-    "valu": ["HBEC_ODD_REALIGN=0"],
     "u2": ["HBEC_ODD_U_SMALL=2"],
-    "sleep": ["HBEC_ODD_SLEEP=8"],
-    "u4": ["HBEC_ODD_U_SMALL=4"],
-    "valu_u2": ["HBEC_ODD_REALIGN=0", "HBEC_ODD_U_SMALL=2"],
-    "gl": ["HBEC_ODD_REALIGN=0", "HBEC_ODD_GLOBAL=1"],
-    "gl_lds": ["HBEC_ODD_GLOBAL=1"],
-    "nobar": ["HBEC_ODD_REALIGN=0", "HBEC_ODD_BARRIER=0"],
+    "uv4": ["HBEC_ODD_U_VERIFY=4"],
+    "nobar": ["HBEC_ODD_BARRIER=0"],
+    "sleep": ["HBEC_ODD_SLEEP=6"],
 }
 
 MiB = 1 << 20
