@@ -20,7 +20,7 @@ LIB = PKG / "libhbec.so"
 ROOT = PKG.parent
 INCLUDE = ROOT / "include"
 
-SOURCES = ["kernels.hip", "odd.hip", "stripes.hip", "verify.hip", "md5.hip", "shardhash.cpp", "hbec.cpp", "ecutils.cpp", "plan.cpp", "hostpath.cpp", "batcher.cpp", "coalesce.cpp"]
+SOURCES = ["kernels.hip", "odd.hip", "wide.hip", "stripes.hip", "verify.hip", "md5.hip", "shardhash.cpp", "hbec.cpp", "ecutils.cpp", "plan.cpp", "hostpath.cpp", "batcher.cpp", "coalesce.cpp"]
 HEADERS = ["kernels.h", "gf256.h", "internal.h", "gf_device.h", "pool.h"]
 ARCH = os.environ.get("HBEC_OFFLOAD_ARCH", "gfx950")
 

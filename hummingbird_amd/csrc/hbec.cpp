@@ -63,6 +63,7 @@ static const std::atomic<int> g_unaligned_kernel{[] {
     const char* e = std::getenv("HBEC_UNALIGNED");
     return e ? std::atoi(e) : 1;
 }()};
+bool unaligned_kernel_enabled() { return g_unaligned_kernel.load() != 0; }
 // Tuning knob: cap on resident blocks per CU used to size vec-kernel grids
 // (0 = the occupancy the compiler's register allocation allows).
 static const int g_blocks_per_cu_override = [] {
@@ -921,6 +922,86 @@ int hbec_fill_splitmix(void* dst, uint64_t n_objects, uint64_t obj_len, uint64_t
 }
 
 // ---- Encoder.Verify ------------------------------------------------------
+// Verify of k > kOddMaxK data shards (gf_verify_wide): HBEC_WIDE_VERIFY=0
+// falls back to the round-2 kernels (gf_verify_unaligned, k <= 16) and the
+// scratch recompute (k > 16).
+static bool wide_verify_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("HBEC_WIDE_VERIFY");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+static int verify_wide(const hbec_view* views, int k, int m, const uint8_t* prow, uint64_t n_obj,
+                       uint64_t shard_len, uint32_t* flags, hipStream_t stream) {
+    int dev = 0, cus = 0;
+    int rc = current_device(&dev);
+    if (rc) return rc;
+    rc = cu_count(dev, &cus);
+    if (rc) return rc;
+    const uint64_t main_len = wide_main_len(shard_len);
+    const uint64_t tpo = (main_len + wide_tile_bytes() - 1) / wide_tile_bytes();
+    for (int r0 = 0; r0 < m; r0 += kWideMaxR) {
+        const int R = std::min(kWideMaxR, m - r0);
+        const uint32_t tw = wide_tab_words(R);
+        // device block: in_base[k], in_stride[k], tables[k][tw]
+        const size_t words = (size_t)k * tw;
+        std::vector<uint64_t> blob((size_t)2 * k + (words + 1) / 2, 0);
+        for (int j = 0; j < k; ++j) {
+            blob[j] = reinterpret_cast<uint64_t>(views[j].base);
+            blob[(size_t)k + j] = views[j].obj_stride;
+        }
+        uint32_t* tab = reinterpret_cast<uint32_t*>(blob.data() + 2 * k);
+        for (int j = 0; j < k; ++j)
+            for (int r = 0; r < R; ++r) perm_table(prow[(size_t)(r0 + r) * k + j], tab + (size_t)j * tw + 5 * r);
+        void* d = nullptr;
+        rc = scratch_alloc(blob.size() * 8, stream, &d);
+        if (rc) return rc;
+        hipError_t e = hipMemcpyAsync(d, blob.data(), blob.size() * 8, hipMemcpyHostToDevice, stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(stream);  // blob is a host vector of this frame
+        if (e != hipSuccess) {
+            scratch_free(d, stream);
+            return hip_fail(e, "verify tables H2D");
+        }
+        WideArgs a;
+        std::memset(&a, 0, sizeof(a));
+        a.in_base = static_cast<const uint64_t*>(d);
+        a.in_stride = static_cast<const uint64_t*>(d) + k;
+        a.tab = reinterpret_cast<const uint32_t*>(static_cast<const uint64_t*>(d) + 2 * k);
+        a.K = (uint32_t)k;
+        a.shard_len = shard_len;
+        a.tiles_per_obj = (uint32_t)tpo;
+        // launches of whole objects, < 2^31 tiles each; object o0's views
+        // are reached through the in_base offsets below (one upload per row group)
+        const uint64_t max_obj = tpo ? std::max<uint64_t>(1, std::min<uint64_t>((1ull << 31), g_chunk_tiles) / tpo) : n_obj;
+        for (uint64_t o0 = 0; o0 < n_obj && e == hipSuccess; o0 += max_obj) {
+            const uint64_t no = std::min(max_obj, n_obj - o0);
+            WideArgs b = a;
+            for (int r = 0; r < R; ++r) {
+                b.out[r] = reinterpret_cast<uint64_t>(views[k + r0 + r].base) + o0 * views[k + r0 + r].obj_stride;
+                b.out_stride[r] = views[k + r0 + r].obj_stride;
+            }
+            b.n_obj = no;
+            b.n_tiles = (uint32_t)(no * tpo);
+            if (o0 > 0) {
+                // shift the input bases by o0 objects: a fresh upload for this chunk
+                std::vector<uint64_t> base(k);
+                for (int j = 0; j < k; ++j) base[j] = blob[j] + o0 * blob[(size_t)k + j];
+                e = hipMemcpyAsync(d, base.data(), (size_t)k * 8, hipMemcpyHostToDevice, stream);
+                if (e == hipSuccess) e = hipStreamSynchronize(stream);
+                if (e != hipSuccess) break;
+            }
+            const uint64_t want = (b.n_tiles + 3) / 4;
+            const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cus * 2));
+            e = launch_verify_wide(R, b, flags + o0, grid, stream);
+        }
+        scratch_free(d, stream);
+        if (e != hipSuccess) return hip_fail(e, "launch gf_verify_wide");
+    }
+    return HBEC_OK;
+}
+
 static int verify_views(hbec_codec* c, const hbec_view* views, uint64_t n_obj, uint64_t shard_len, uint32_t* flags,
                         hipStream_t stream) {
     const int k = c->k, m = c->m;
@@ -1040,6 +1121,11 @@ static int verify_views(hbec_codec* c, const hbec_view* views, uint64_t n_obj, u
             if (rc) return rc;
         }
         return HBEC_OK;
+    }
+    if (g_unaligned_kernel.load() && k > kOddMaxK && k <= 256 && shard_len < (1ull << 31) && wide_verify_enabled()) {
+        // k > 8 at any alignment (k > 16 included): one read-only pass per <= 8
+        // rows (gf_verify_wide, wide.hip), coefficient tables in LDS
+        return verify_wide(views, k, m, prow, n_obj, shard_len, flags, stream);
     }
     if (g_unaligned_kernel.load() && k <= kMaxK) {
         // any alignment: recompute and compare in one pass (gf_verify_unaligned), <= 4 rows per launch

@@ -400,7 +400,7 @@ bool zero_copy_enabled() {
 // pinned, device-mapped allocation; 0 otherwise.  hbec_host_alloc ranges are
 // looked up in the registry; other pinned memory is asked of the runtime at
 // both ends of the range.
-bool hbec::zero_copy_any_alignment() { return zero_copy_unaligned_enabled(); }
+bool hbec::zero_copy_any_alignment() { return zero_copy_unaligned_enabled() && unaligned_kernel_enabled(); }
 
 uint64_t hbec::pinned_device_addr(const void* p, uint64_t len) {
     if (!zero_copy_enabled()) return 0;
@@ -599,6 +599,73 @@ int zero_copy_md5_run(Ring* ring, const std::vector<ZcStripe>& zs, const std::ve
     return HBEC_OK;
 }
 
+// Zero-copy with ShardHash for pinned stripes at any alignment / shard length
+// (15 object sizes in 16: ecSplit's S = ceil(len / k)): the mirrored gf_odd
+// plan kernel codes each stripe in place over PCIe, as
+// zero_copy_unaligned_run, and stores every shard column it holds to the
+// stripe's hash arena, where shard i sits 16-B aligned at arena + i * P
+// (P = odd_mirror_pitch_host(S)); gf_odd_mirror_copy adds the guard-band
+// bytes (<= 160 per shard) afterwards.  The arena is then hashed by md5_list
+// exactly as in zero_copy_md5_run.
+int zero_copy_unaligned_md5_run(Ring* ring, const std::vector<ZcStripe>& zs, const std::vector<int>& in_idx,
+                                const std::vector<int>& out_idx, const std::vector<uint8_t>& rows, uint8_t* d_digest,
+                                int n_shards) {
+    static_assert(sizeof(hbec::URec) == sizeof(hbec::TileRec), "record slots are shared");
+    const int K = (int)in_idx.size(), R = (int)out_idx.size();
+    int rc = ring_md5_init(*ring);
+    if (rc) return rc;
+    const uint64_t tile = hbec::urec_tile();
+    ArenaCursor ac{ring, ring->s_cmp, d_digest};
+    hipError_t e = hipSuccess;
+    size_t si = 0;
+    for (int c = 0; si < zs.size(); ++c) {
+        const int slot = c % kSlots;
+        e = hipEventSynchronize(ring->ev_cmp[slot]);  // the slot's previous records are consumed
+        if (e != hipSuccess) return hip_fail(e, "zero-copy slot wait");
+        hbec::URec* rec = reinterpret_cast<hbec::URec*>(ring->pin_tiles[slot]);
+        uint64_t nt = 0;
+        std::vector<hbec::URec> edges;  // one per stripe of this slot, after the main records
+        while (si < zs.size()) {
+            const ZcStripe& z = zs[si];
+            const uint64_t S = z.shard_len;
+            const uint64_t span = hbec::urec_span(S);
+            const uint64_t tiles = (span + tile - 1) / tile;
+            const uint64_t bytes = ((uint64_t)n_shards * hbec::odd_mirror_pitch_host(S) + 255) & ~uint64_t(255);
+            if (tiles + 2 > ring->tile_cap || bytes > ring->arena_cap)
+                return fail(HBEC_ERR_INVALID_ARG, "stripe too large for a hash arena");
+            if (nt > 0 && nt + edges.size() + tiles + 1 > ring->tile_cap) break;
+            if (!ac.fits(bytes, (uint64_t)(K + R))) {
+                if (nt > 0 || !edges.empty()) break;  // launch this chunk first: the arena is hashed after its kernels
+                rc = ac.flush();
+                if (rc) return rc;
+            }
+            const uint64_t mbase = ac.base();  // 256-B aligned
+            for (uint64_t off = 0; off < span; off += tile) rec[nt++] = {z.dev, mbase, S, off};
+            edges.push_back({z.dev, mbase, S, 0});
+            const uint64_t P = hbec::odd_mirror_pitch_host(S);
+            for (int i : in_idx) ac.add(mbase + (uint64_t)i * P, S, (uint64_t)si * (uint64_t)n_shards + (uint64_t)i);
+            for (int i : out_idx) ac.add(mbase + (uint64_t)i * P, S, (uint64_t)si * (uint64_t)n_shards + (uint64_t)i);
+            ac.used += bytes;
+            ++si;
+        }
+        std::copy(edges.begin(), edges.end(), rec + nt);
+        e = hipMemcpyAsync(ring->dev_tiles[slot], rec, (nt + edges.size()) * sizeof(hbec::URec), hipMemcpyHostToDevice,
+                           ring->s_cmp);
+        if (e != hipSuccess) return hip_fail(e, "zero-copy records H2D");
+        const hbec::URec* d_rec = reinterpret_cast<const hbec::URec*>(ring->dev_tiles[slot]);
+        rc = hbec::launch_unaligned_passes(d_rec, nt, in_idx, out_idx, rows, 0, ring->s_cmp, zero_copy_max_blocks(),
+                                           d_rec + nt, edges.size(), true);
+        if (rc) return rc;
+        e = hipEventRecord(ring->ev_cmp[slot], ring->s_cmp);
+        if (e != hipSuccess) return hip_fail(e, "zero-copy event");
+    }
+    rc = ac.finish();
+    if (rc) return rc;
+    e = hipStreamSynchronize(ring->s_cmp);
+    if (e != hipSuccess) return hip_fail(e, "zero-copy drain");
+    return HBEC_OK;
+}
+
 std::atomic<uint64_t> g_md5_zc_calls{0}, g_md5_ring_calls{0};
 
 bool zero_copy_md5_enabled() {
@@ -665,13 +732,29 @@ int host_run_on(Ring* ring, const hbec_stripe* stripes, uint64_t n, const std::v
         for (int i : out_idx) top = std::max(top, i);
         std::vector<ZcStripe> zs;
         zs.reserve(n);
+        // every stripe pinned: the aligned mirror kernel when all are 16-B
+        // aligned with S % 16 == 0, else the mirrored gf_odd plan for all
+        const bool any_align = hbec::zero_copy_any_alignment() && hbec::odd_enabled();
+        bool all_aligned = true;
         for (uint64_t s = 0; s < n; ++s) {
             const uint64_t S = stripes[s].shard_len;
-            const bool aligned = stripes[s].base && (reinterpret_cast<uintptr_t>(stripes[s].base) & 15u) == 0 &&
-                                 S % 16 == 0 && S > 0 && S < (1ull << 32);
-            const uint64_t d = aligned ? pinned_device_addr(stripes[s].base, (uint64_t)(top + 1) * S) : 0;
-            if (!d || (d & 15u) != 0) break;
+            if (!stripes[s].base || S == 0) break;
+            const bool aligned = (reinterpret_cast<uintptr_t>(stripes[s].base) & 15u) == 0 && S % 16 == 0 &&
+                                 S < (1ull << 32);
+            if (!aligned && (!any_align || S >= (1ull << 31))) break;
+            const uint64_t d = pinned_device_addr(stripes[s].base, (uint64_t)(top + 1) * S);
+            if (!d) break;
+            all_aligned = all_aligned && aligned && (d & 15u) == 0;
             zs.push_back({d, S});
+        }
+        if (zs.size() == n && !all_aligned && !any_align) zs.clear();
+        if (zs.size() == n && !all_aligned) {
+            const uint64_t max_cols = (std::min(ring->in_cap / in_idx.size(), ring->out_cap / out_idx.size()) / 16) * 16;
+            for (const ZcStripe& z : zs)
+                if (z.shard_len > max_cols)
+                    return fail(HBEC_ERR_INVALID_ARG, "hashing needs every stripe to fit one staging slot");
+            g_md5_zc_calls.fetch_add(1, std::memory_order_relaxed);
+            return zero_copy_unaligned_md5_run(ring, zs, in_idx, out_idx, rows, d_digest, n_shards);
         }
         if (zs.size() == n) {
             // the same stripe bound as the ring (hbec.h: one staging slot)

@@ -45,8 +45,11 @@ void scratch_free(void* p, hipStream_t stream);
 // HBEC_ZEROCOPY=0).  The zero-copy host paths code such memory in place.
 uint64_t pinned_device_addr(const void* p, uint64_t len);
 // Pinned stripes at any alignment / shard length are coded in place over PCIe
-// (gf_apply_unaligned_plan) unless HBEC_ZC_UNALIGNED=0.
+// (gf_apply_unaligned_plan) unless HBEC_ZC_UNALIGNED=0 or HBEC_UNALIGNED=0.
 bool zero_copy_any_alignment();
+// The unaligned kernels (gf_odd / gf_apply_unaligned) are on unless
+// HBEC_UNALIGNED=0 (round-1 byte kernel; every path honours the same switch).
+bool unaligned_kernel_enabled();
 
 // ShardHash of a list of device chains: records {addr, len, slot, 0} (32 B
 // each, device memory), digest of record i at digest + slot * 16.
@@ -91,6 +94,6 @@ struct URec;
 int launch_unaligned_passes(const URec* recs, uint64_t n_recs, const std::vector<int>& in_idx,
                             const std::vector<int>& out_idx, const std::vector<uint8_t>& rows, int sel_k,
                             hipStream_t stream, int max_blocks = 0, const URec* erecs = nullptr,
-                            uint64_t n_erecs = 0);
+                            uint64_t n_erecs = 0, bool mirror = false);
 
 }  // namespace hbec

@@ -121,6 +121,10 @@ struct UPlanArgs {
     uint32_t out_idx[kMaxR];
     uint32_t in_sel, out_sel;
     uint32_t tab[kMaxR][kMaxK][5];
+    // gf_odd plans, zero-copy encode + ShardHash: bit 0 also stores every input
+    // column, bit 1 every output column (single input pass only) to the hash
+    // arena at rec.b (shard i at rec.b + i * odd_mirror_pitch_host(S))
+    uint32_t mirror;
 };
 uint32_t unaligned_tile_bytes();
 // Verify at any alignment (k <= kMaxK, <= 4 parity rows per launch): OR 1 into
@@ -133,7 +137,10 @@ hipError_t launch_unaligned_plan(int k, int r, const UPlanArgs& a, int grid, hip
 // <= kMaxR outputs; the gf_apply_vec_pipe2 schedule.  Modes: 0 apply,
 // 1 accumulate (out ^= ..., later passes of k > kOddMaxK), 2 verify (flag
 // objects whose stored parity differs; nothing written).
-constexpr int kOddMaxK = 8;
+#ifndef HBEC_ODD_MAXK
+#define HBEC_ODD_MAXK 8
+#endif
+constexpr int kOddMaxK = HBEC_ODD_MAXK;
 // HBEC_ODD=1 / 0 selects gf_odd or the round-2 kernels (gf_apply_unaligned
 // family) for odd shards (default: HBEC_ODD_DEFAULT).
 bool odd_enabled();
@@ -158,6 +165,39 @@ hipError_t launch_odd_edges(int k, int r, int mode, const PassArgs& a, uint32_t*
 hipError_t launch_odd_plan(int k, int r, int mode, const UPlanArgs& p, int grid, hipStream_t stream);
 hipError_t launch_odd_edges_plan(int k, int r, int mode, const UPlanArgs& p, const URec* erecs, uint32_t n_erecs,
                                  hipStream_t stream);
+// Mirrored plans: copy shard bytes the main kernel does not mirror (the guard
+// band, full = 0; whole shards, full = 1) from each edge record's stripe
+// (rec.a) to its arena (rec.b), for shards idx[0 .. n_idx).
+constexpr int kMirrorMaxIdx = 64;
+struct MirrorCopyArgs {
+    uint32_t idx[kMirrorMaxIdx];
+    uint32_t n_idx;
+    uint32_t full;
+};
+hipError_t launch_odd_mirror_copy(const URec* erecs, uint32_t n_erecs, const MirrorCopyArgs& a, hipStream_t stream);
+uint64_t odd_mirror_pitch_host(uint64_t shard_len);
+
+// ---- wide.hip: Verify of any k (k > 16 included) at any alignment, one read-only pass ----
+constexpr int kWideMaxR = 8;
+struct WideArgs {
+    const uint64_t* in_base;    // [K] device array: input shard bases of object 0
+    const uint64_t* in_stride;  // [K] object strides
+    const uint32_t* tab;        // [K][wide_tab_words(R)]: coefficient (r, j) tables at j * words + 5 r
+    uint64_t out[kWideMaxR];    // stored parity shard bases / strides
+    uint64_t out_stride[kWideMaxR];
+    uint32_t K;
+    uint32_t tiles_per_obj;     // ceil(wide_main_len(S) / wide_tile_bytes())
+    uint32_t n_tiles;
+    uint32_t pad_;
+    uint64_t shard_len;
+    uint64_t n_obj;
+};
+uint32_t wide_tab_words(int r);
+uint32_t wide_tile_bytes();
+uint64_t wide_main_len(uint64_t shard_len);
+// r <= kWideMaxR rows per launch; K <= 256; shard_len < 2^31.  Flags objects
+// (flags[obj] |= 1) whose stored parity differs.
+hipError_t launch_verify_wide(int r, const WideArgs& a, uint32_t* flags, int grid, hipStream_t stream);
 
 hipError_t launch_fill(uint8_t* dst, uint64_t n_obj, uint64_t obj_len, uint64_t obj_stride, uint64_t base_seed,
                        uint64_t first, int grid, hipStream_t stream);

@@ -80,6 +80,18 @@ constexpr uint64_t kOddMinMain = (uint64_t)kOddEdgeSlots;
 #ifndef HBEC_ODD_U_VERIFY
 #define HBEC_ODD_U_VERIFY 0  // windows per wave tile of verify for K <= 4 (0: as apply)
 #endif
+#ifndef HBEC_ODD_ALOAD
+#define HBEC_ODD_ALOAD 0  // 1: 16-B-aligned input loads, shifted by realign16 (0: dword-aligned loads, 1 DPP)
+#endif
+#ifndef HBEC_ODD_EDGE_PLAIN
+#define HBEC_ODD_EDGE_PLAIN 0  // 1: blocks in a 128-B line shared with the next / previous window: plain (L2) stores
+#endif
+#ifndef HBEC_ODD_NT_ST
+#define HBEC_ODD_NT_ST 1  // 0: plain stores for every output block
+#endif
+#ifndef HBEC_ODD_PLAN_U
+#define HBEC_ODD_PLAN_U 1  // windows per plan record
+#endif
 
 enum : int { kOddApply = 0, kOddAcc = 1, kOddVerify = 2 };
 
@@ -90,7 +102,7 @@ __host__ __device__ constexpr int odd_u(int k, int mode = kOddApply) {
                ? HBEC_ODD_U_VERIFY
                : (k <= 4 ? (HBEC_ODD_U_SMALL > 0 ? HBEC_ODD_U_SMALL : (4 / k)) : 1);
 }
-constexpr int kOddPlanU = 1;  // plans: one window per record
+constexpr int kOddPlanU = HBEC_ODD_PLAN_U;  // plans: windows per record
 
 // One tile, wave-uniform.  Positions are 32-bit: the host sends shards of
 // 2^31 bytes or more to the round-2 kernels.
@@ -102,7 +114,14 @@ struct OddTile {
     int32_t c;        // shard position of the tile's first column
     uint32_t live;    // 0: past-the-end stand-in (loaded, never stored)
     uint32_t obj;     // flag index (verify)
+    // mirrored plans (zero-copy encode + ShardHash): each shard's 16-B-aligned
+    // slot in the device hash arena, shard position p at slot + p
+    uint64_t m_in[K];
+    uint64_t m_out[R];
 };
+
+// hash-arena pitch of a mirrored stripe: shard i at arena + i * P (16-B aligned)
+__host__ __device__ __forceinline__ uint64_t odd_mirror_pitch(uint64_t S) { return (S + 31u) & ~(uint64_t)15; }
 
 __device__ __forceinline__ int32_t odd_c0(uint64_t out0) { return (int32_t)((16u - ((uint32_t)out0 & 15u)) & 15u) - 32; }
 
@@ -116,14 +135,17 @@ struct OddIn {
     uint32_t sh;     // the column's first byte within the block (0..3)
 };
 
+constexpr uint32_t kOddLdAlign = HBEC_ODD_ALOAD ? 16u : 4u;  // input block alignment
+
 __device__ __forceinline__ OddIn odd_in(uint64_t base, int32_t S, int32_t c) {
-    const int32_t l4 = (int32_t)((uint32_t)base & 3u);
+    constexpr uint32_t A = kOddLdAlign;
+    const int32_t l4 = (int32_t)((uint32_t)base & (A - 1u));
     const int32_t t = l4 + c;
     OddIn o;
-    o.base4 = base & ~(uint64_t)3;
-    o.sh = (uint32_t)t & 3u;
+    o.base4 = base & ~(uint64_t)(A - 1u);
+    o.sh = (uint32_t)t & (A - 1u);
     o.off = t - (int32_t)o.sh;
-    o.lim = ((l4 + S + 3) & ~3) - 16;
+    o.lim = ((l4 + S + (int32_t)A - 1) & ~((int32_t)A - 1)) - 16;
     return o;
 }
 
@@ -133,8 +155,10 @@ __device__ __forceinline__ u32x4 odd_ld(const OddIn& o, int32_t col) {
     return ld16_addr(o.base4 + (uint64_t)(uint32_t)v);
 }
 
-// bytes [sh, sh + 16) of the lane's block and lane l+1's first dword
+// bytes [sh, sh + 16) of the lane's block and lane l+1's first dword (or,
+// with 16-B-aligned loads, lane l+1's block)
 __device__ __forceinline__ u32x4 odd_shift_in(const u32x4& v, uint32_t sh) {
+    if constexpr (HBEC_ODD_ALOAD) return realign16(v, lane_next4(v), sh);
     const uint32_t n0 = lane_next(v[0]);
     return u32x4{__builtin_amdgcn_alignbyte(v[1], v[0], sh), __builtin_amdgcn_alignbyte(v[2], v[1], sh),
                  __builtin_amdgcn_alignbyte(v[3], v[2], sh), __builtin_amdgcn_alignbyte(n0, v[3], sh)};
@@ -180,7 +204,7 @@ struct OddIdP {
     uint32_t live;
 };
 
-template <int K, int R>
+template <int K, int R, bool MIR = false>
 struct OddPlan {
     using Id = OddIdP;
     const UPlanArgs& p;
@@ -197,13 +221,23 @@ struct OddPlan {
         b.c = odd_c0(b.out[0]) + (int32_t)i.rec.p0;
         b.live = i.live;
         b.obj = 0;
+        if constexpr (MIR) {
+            // rec.b = the stripe's arena (inputs and outputs are all at rec.a)
+            const uint64_t P = odd_mirror_pitch(S);
+#pragma unroll
+            for (int j = 0; j < K; ++j) b.m_in[j] = i.rec.b + (uint64_t)p.in_idx[j] * P;
+#pragma unroll
+            for (int r = 0; r < R; ++r) b.m_out[r] = i.rec.b + (uint64_t)p.out_idx[r] * P;
+        }
     }
 };
 
 // ---- one tile ----
 template <int K, int R, int U, int MODE>
 struct OddRegs {
-    static constexpr int NL = K + (MODE == kOddVerify ? R : 0);  // shards loaded per column
+    // shards loaded per column: verify loads the stored parity columns, the
+    // accumulate mode the old output blocks (with the inputs, one tile ahead)
+    static constexpr int NL = K + (MODE == kOddVerify || MODE == kOddAcc ? R : 0);
     u32x4 x[U][NL];
 };
 
@@ -220,21 +254,52 @@ __device__ __forceinline__ void odd_load(OddRegs<K, R, U, MODE>& X, const OddTil
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-        for (int j = 0; j < NL; ++j) X.x[u][j] = odd_ld(src[j], (int32_t)(u * kOddStore + lane));
+        for (int j = 0; j < (MODE == kOddAcc ? K : NL); ++j) X.x[u][j] = odd_ld(src[j], (int32_t)(u * kOddStore + lane));
+    if constexpr (MODE == kOddAcc) {
+        // the old output block each lane will rewrite: output r's aligned block
+        // at q = column + dl_r; lanes that store nothing read one inside the band
+        const int32_t hi = b.S - kOddGuard - 16;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint32_t dl = __builtin_amdgcn_readfirstlane((16u - (((uint32_t)b.out[r] + (uint32_t)b.c) & 15u)) & 15u);
+            const int32_t e = (int32_t)(((uint32_t)b.c + dl) & 15u);  // q = e mod 16
+            const int32_t qmin = kOddGuard + e, qmax = hi - ((hi - e) & 15);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int32_t q = b.c + (int32_t)(u * kOddWin) + 16 * (int32_t)lane + (int32_t)dl;
+                const int32_t qc = q < qmin ? qmin : (q > qmax ? qmax : q);
+                X.x[u][K + r] = ld16_addr(b.out[r] + (uint64_t)(int64_t)qc);
+            }
+        }
+    }
 }
 
-template <int K, int R, int U, int MODE>
+// output block store: non-temporal, or (HBEC_ODD_EDGE_PLAIN) plain for blocks
+// whose 128-B line the neighbouring window writes too, so L2 merges the halves
+__device__ __forceinline__ void odd_st(uint64_t addr, const u32x4& v, uint64_t win0, bool mine) {
+    if constexpr (HBEC_ODD_EDGE_PLAIN) {
+        const bool edge = (addr & ~(uint64_t)127) < win0 || (addr | 127u) >= win0 + kOddWin;
+        if (mine && edge) *reinterpret_cast<gu32x4*>(addr) = v;
+        if (mine && !edge) st16_addr(addr, v);
+    } else if constexpr (HBEC_ODD_NT_ST) {
+        if (mine) st16_addr(addr, v);
+    } else {
+        if (mine) *reinterpret_cast<gu32x4*>(addr) = v;
+    }
+}
+
+template <int K, int R, int U, int MODE, bool MIR = false>
 __device__ __forceinline__ void odd_finish(const OddRegs<K, R, U, MODE>& X, const OddTile<K, R>& b,
                                            const TabArray& tab, const Tables<K, R, HBEC_ODD_VMIN>& tb, uint32_t lane,
-                                           uint32_t* flags) {
+                                           uint32_t* flags, uint32_t mir = 0) {
     constexpr int NL = OddRegs<K, R, U, MODE>::NL;
-    uint32_t sh[NL];
+    uint32_t sh[K + (MODE == kOddVerify ? R : 0)];
 #pragma unroll
-    for (int j = 0; j < K; ++j) sh[j] = __builtin_amdgcn_readfirstlane(((uint32_t)b.in[j] + (uint32_t)b.c) & 3u);
+    for (int j = 0; j < K; ++j) sh[j] = __builtin_amdgcn_readfirstlane(((uint32_t)b.in[j] + (uint32_t)b.c) & (kOddLdAlign - 1u));
     if constexpr (MODE == kOddVerify) {
 #pragma unroll
         for (int r = 0; r < R; ++r)
-            sh[K + r] = __builtin_amdgcn_readfirstlane(((uint32_t)b.out[r] + (uint32_t)b.c) & 3u);
+            sh[K + r] = __builtin_amdgcn_readfirstlane(((uint32_t)b.out[r] + (uint32_t)b.c) & (kOddLdAlign - 1u));
     }
     const int32_t S = b.S;
     const int32_t hi = S - kOddGuard - 16;  // last block start the main kernel stores / compares
@@ -252,6 +317,28 @@ __device__ __forceinline__ void odd_finish(const OddRegs<K, R, U, MODE>& X, cons
 #pragma unroll
         for (int r = 0; r < R; ++r) acc[r] = u32x4{0, 0, 0, 0};
         gf_dot<K, R, HBEC_ODD_VMIN>(acc, x, tab, tb);
+        if constexpr (MIR && MODE != kOddVerify) {
+            // mirror: every arena slot is 16-B aligned, so column i's arena
+            // block starts at qm = cpos + dm, dm = -c mod 16; same guard band
+            // (the head and tail bytes are copied by gf_odd_mirror_copy)
+            const uint32_t dm = __builtin_amdgcn_readfirstlane((0u - (uint32_t)b.c) & 15u);
+            const int32_t qm = cpos + (int32_t)dm;
+            const bool mm = b.live != 0u && lane < kOddStore && qm >= kOddGuard && qm <= hi;
+            if (mir & 1u) {
+#pragma unroll
+                for (int j = 0; j < K; ++j) {
+                    const u32x4 v = realign16(x[j], lane_next4(x[j]), dm);
+                    if (mm) st16_addr(b.m_in[j] + (uint64_t)(int64_t)qm, v);
+                }
+            }
+            if (MODE == kOddApply && (mir & 2u)) {  // outputs are final only in a single input pass
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const u32x4 v = realign16(acc[r], lane_next4(acc[r]), dm);
+                    if (mm) st16_addr(b.m_out[r] + (uint64_t)(int64_t)qm, v);
+                }
+            }
+        }
         if constexpr (MODE == kOddVerify) {
             // frame columns = output 0's blocks: compare those inside the guard band
             const bool mine = b.live != 0u && lane < kOddStore && cpos >= kOddGuard && cpos <= hi;
@@ -267,14 +354,9 @@ __device__ __forceinline__ void odd_finish(const OddRegs<K, R, U, MODE>& X, cons
                 if (dl[r] != 0u) blk = realign16(acc[r], lane_next4(acc[r]), dl[r]);  // wave-uniform (never r = 0)
                 const int32_t q = cpos + (int32_t)dl[r];  // block start: out[r] + q is 16-B aligned
                 const bool mine = b.live != 0u && lane < kOddStore && q >= kOddGuard && q <= hi;
-                if constexpr (MODE == kOddAcc) {
-                    // the old block; lanes that do not store read one inside the band instead
-                    const int32_t e = (int32_t)(((uint32_t)b.c + dl[r]) & 15u);  // q = e mod 16
-                    const int32_t qmin = kOddGuard + e, qmax = hi - ((hi - e) & 15);
-                    const int32_t qc = q < qmin ? qmin : (q > qmax ? qmax : q);
-                    blk ^= ld16_addr(b.out[r] + (uint64_t)(int64_t)qc);
-                }
-                if (mine) st16_addr(b.out[r] + (uint64_t)(int64_t)q, blk);
+                if constexpr (MODE == kOddAcc) blk ^= X.x[u][K + r];  // the old block (odd_load)
+                const uint64_t win0 = b.out[r] + (uint64_t)(int64_t)(b.c + (int32_t)(u * kOddWin) + (int32_t)dl[r]);
+                odd_st(b.out[r] + (uint64_t)(int64_t)q, blk, win0, mine);
             }
         }
     }
@@ -285,8 +367,9 @@ __device__ __forceinline__ void odd_finish(const OddRegs<K, R, U, MODE>& X, cons
     }
 }
 
-template <int K, int R, int U, int MODE, class Src>
-__device__ __forceinline__ void odd_body(const Src& src, uint32_t n, const TabArray& tab, uint32_t* flags) {
+template <int K, int R, int U, int MODE, class Src, bool MIR = false>
+__device__ __forceinline__ void odd_body(const Src& src, uint32_t n, const TabArray& tab, uint32_t* flags,
+                                         uint32_t mir = 0) {
     constexpr uint32_t WPB = kPipeBlockThreads / 64;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t nw = gridDim.x * WPB;
@@ -315,7 +398,7 @@ __device__ __forceinline__ void odd_body(const Src& src, uint32_t n, const TabAr
         {
             OddTile<K, R> b;
             src.at(b, cur);
-            odd_finish<K, R, U, MODE>(X, b, tab, tb, lane, flags);
+            odd_finish<K, R, U, MODE, MIR>(X, b, tab, tb, lane, flags, mir);
         }
         X = Y;
         cur = nxt;
@@ -323,7 +406,7 @@ __device__ __forceinline__ void odd_body(const Src& src, uint32_t n, const TabAr
     }
     OddTile<K, R> b;
     src.at(b, cur);
-    odd_finish<K, R, U, MODE>(X, b, tab, tb, lane, flags);
+    odd_finish<K, R, U, MODE, MIR>(X, b, tab, tb, lane, flags, mir);
 }
 
 template <int K, int R, int MODE>
@@ -332,9 +415,41 @@ __global__ __launch_bounds__(kPipeBlockThreads, HBEC_ODD_LB) void gf_odd(PassArg
     odd_body<K, R, U, MODE>(OddStrided<K, R, U>{a}, a.n_tiles, a.tab, flags);
 }
 
-template <int K, int R, int MODE>
+template <int K, int R, int MODE, bool MIR = false>
 __global__ __launch_bounds__(kPipeBlockThreads, HBEC_ODD_LB) void gf_odd_plan(UPlanArgs p, const URec* __restrict__ recs) {
-    odd_body<K, R, kOddPlanU, MODE>(OddPlan<K, R>{p, recs}, p.n_recs, p.tab, nullptr);
+    odd_body<K, R, kOddPlanU, MODE, OddPlan<K, R, MIR>, MIR>(OddPlan<K, R, MIR>{p, recs}, p.n_recs, p.tab, nullptr,
+                                                            p.mirror);
+}
+
+// Mirror copies (zero-copy encode + ShardHash): for every edge record (one per
+// stripe, rec.a = stripe, rec.b = its arena) and shard idx[t], copy shard
+// bytes from the stripe to the arena slot: the guard-band head and tail the
+// main kernel leaves (positions [0, 80) and [S - 80, S): full == 0), or the
+// whole shard (full == 1: outputs of a k > kOddMaxK accumulate, final only
+// after the last pass).  One block per (record, shard), bytes by thread.
+__global__ __launch_bounds__(kBlockThreads) void gf_odd_mirror_copy(const URec* __restrict__ erecs, uint32_t n_erecs,
+                                                                    MirrorCopyArgs a) {
+    const uint32_t e = blockIdx.x / a.n_idx, t = blockIdx.x % a.n_idx;
+    if (e >= n_erecs) return;
+    const URec rec = erecs[e];
+    const uint64_t S = rec.shard_len, P = odd_mirror_pitch(S);
+    const gu8_t* src = reinterpret_cast<const gu8_t*>(rec.a + (uint64_t)a.idx[t] * S);
+    gu8_t* dst = reinterpret_cast<gu8_t*>(rec.b + (uint64_t)a.idx[t] * P);
+    if (a.full) {
+        for (uint64_t q = threadIdx.x; q < S; q += blockDim.x) dst[q] = src[q];
+        return;
+    }
+    for (uint32_t slot = threadIdx.x; slot < (uint32_t)kOddEdgeSlots; slot += blockDim.x) {
+        const uint64_t half = kOddEdgeSlots / 2;
+        uint64_t q;
+        if (S <= (uint64_t)kOddEdgeSlots) {
+            if (slot >= S) continue;
+            q = slot;
+        } else {
+            q = slot < half ? slot : S - kOddEdgeSlots + slot;
+        }
+        dst[q] = src[q];
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -426,38 +541,59 @@ __global__ __launch_bounds__(kBlockThreads) void gf_odd_edges_plan(UPlanArgs p, 
 // ---------------------------------------------------------------------------
 // launch table
 // ---------------------------------------------------------------------------
+template <int K, int R, int MODE>
+static const void* odd_pick(bool plan, bool mirror) {
+    if (!plan) return (const void*)&gf_odd<K, R, MODE>;
+    if constexpr (MODE != kOddVerify) {
+        if (mirror) return (const void*)&gf_odd_plan<K, R, MODE, true>;
+    }
+    return (const void*)&gf_odd_plan<K, R, MODE>;
+}
+
 template <int K, int MODE>
-static const void* odd_for_r(int r, bool plan) {
+static const void* odd_for_r(int r, bool plan, bool mirror) {
     switch (r) {
-        case 1: return plan ? (const void*)&gf_odd_plan<K, 1, MODE> : (const void*)&gf_odd<K, 1, MODE>;
-        case 2: return plan ? (const void*)&gf_odd_plan<K, 2, MODE> : (const void*)&gf_odd<K, 2, MODE>;
-        case 3: return plan ? (const void*)&gf_odd_plan<K, 3, MODE> : (const void*)&gf_odd<K, 3, MODE>;
-        case 4: return plan ? (const void*)&gf_odd_plan<K, 4, MODE> : (const void*)&gf_odd<K, 4, MODE>;
+        case 1: return odd_pick<K, 1, MODE>(plan, mirror);
+        case 2: return odd_pick<K, 2, MODE>(plan, mirror);
+        case 3: return odd_pick<K, 3, MODE>(plan, mirror);
+        case 4: return odd_pick<K, 4, MODE>(plan, mirror);
     }
     return nullptr;
 }
 
 template <int MODE>
-static const void* odd_kernel_(int k, int r, bool plan) {
+static const void* odd_kernel_(int k, int r, bool plan, bool mirror) {
     switch (k) {
-        case 1: return odd_for_r<1, MODE>(r, plan);
-        case 2: return odd_for_r<2, MODE>(r, plan);
-        case 3: return odd_for_r<3, MODE>(r, plan);
-        case 4: return odd_for_r<4, MODE>(r, plan);
-        case 5: return odd_for_r<5, MODE>(r, plan);
-        case 6: return odd_for_r<6, MODE>(r, plan);
-        case 7: return odd_for_r<7, MODE>(r, plan);
-        case 8: return odd_for_r<8, MODE>(r, plan);
+        case 1: return odd_for_r<1, MODE>(r, plan, mirror);
+        case 2: return odd_for_r<2, MODE>(r, plan, mirror);
+        case 3: return odd_for_r<3, MODE>(r, plan, mirror);
+        case 4: return odd_for_r<4, MODE>(r, plan, mirror);
+        case 5: return odd_for_r<5, MODE>(r, plan, mirror);
+        case 6: return odd_for_r<6, MODE>(r, plan, mirror);
+        case 7: return odd_for_r<7, MODE>(r, plan, mirror);
+        case 8: return odd_for_r<8, MODE>(r, plan, mirror);
+#if HBEC_ODD_MAXK > 8
+        case 9: return odd_for_r<9, MODE>(r, plan, mirror);
+        case 10: return odd_for_r<10, MODE>(r, plan, mirror);
+        case 11: return odd_for_r<11, MODE>(r, plan, mirror);
+        case 12: return odd_for_r<12, MODE>(r, plan, mirror);
+#endif
+#if HBEC_ODD_MAXK > 12
+        case 13: return odd_for_r<13, MODE>(r, plan, mirror);
+        case 14: return odd_for_r<14, MODE>(r, plan, mirror);
+        case 15: return odd_for_r<15, MODE>(r, plan, mirror);
+        case 16: return odd_for_r<16, MODE>(r, plan, mirror);
+#endif
     }
     return nullptr;
 }
 
-static const void* odd_kernel(int k, int r, int mode, bool plan) {
+static const void* odd_kernel(int k, int r, int mode, bool plan, bool mirror = false) {
     if (plan && mode == kOddVerify) return nullptr;
     switch (mode) {
-        case kOddApply: return odd_kernel_<kOddApply>(k, r, plan);
-        case kOddAcc: return odd_kernel_<kOddAcc>(k, r, plan);
-        case kOddVerify: return odd_kernel_<kOddVerify>(k, r, plan);
+        case kOddApply: return odd_kernel_<kOddApply>(k, r, plan, mirror);
+        case kOddAcc: return odd_kernel_<kOddAcc>(k, r, plan, mirror);
+        case kOddVerify: return odd_kernel_<kOddVerify>(k, r, plan, false);
     }
     return nullptr;
 }
@@ -536,11 +672,23 @@ hipError_t launch_odd_edges_plan(int k, int r, int mode, const UPlanArgs& p, con
 }
 
 hipError_t launch_odd_plan(int k, int r, int mode, const UPlanArgs& p, int grid, hipStream_t stream) {
-    const void* fn = odd_kernel(k, r, mode, true);
+    const void* fn = odd_kernel(k, r, mode, true, p.mirror != 0);
     if (!fn) return hipErrorInvalidValue;
     const URec* recs = p.recs;
     void* args[] = {const_cast<UPlanArgs*>(&p), &recs};
     return hipLaunchKernel(fn, dim3(grid), dim3(kPipeBlockThreads), args, 0, stream);
 }
+
+hipError_t launch_odd_mirror_copy(const URec* erecs, uint32_t n_erecs, const MirrorCopyArgs& a, hipStream_t stream) {
+    if (n_erecs == 0 || a.n_idx == 0) return hipSuccess;
+    if (a.n_idx > kMirrorMaxIdx) return hipErrorInvalidValue;
+    const uint64_t blocks = (uint64_t)n_erecs * a.n_idx;
+    if (blocks >= (1ull << 31)) return hipErrorInvalidValue;
+    MirrorCopyArgs c = a;
+    void* args[] = {&erecs, &n_erecs, &c};
+    return hipLaunchKernel((const void*)&gf_odd_mirror_copy, dim3((unsigned)blocks), dim3(kBlockThreads), args, 0, stream);
+}
+
+uint64_t odd_mirror_pitch_host(uint64_t shard_len) { return odd_mirror_pitch(shard_len); }
 
 }  // namespace hbec

@@ -86,9 +86,12 @@ int upload(const std::vector<T>& recs, T** dst, const char* what) {
 // object records (shard indices >= sel_k are parity, base b).
 int hbec::launch_unaligned_passes(const URec* recs, uint64_t n_recs, const std::vector<int>& in_idx,
                                   const std::vector<int>& out_idx, const std::vector<uint8_t>& rows, int sel_k,
-                                  hipStream_t stream, int max_blocks, const URec* erecs, uint64_t n_erecs) {
+                                  hipStream_t stream, int max_blocks, const URec* erecs, uint64_t n_erecs,
+                                  bool mirror) {
     const int K_all = (int)in_idx.size(), R_all = (int)out_idx.size();
     if ((n_recs == 0 && n_erecs == 0) || R_all == 0) return HBEC_OK;
+    if (mirror && (!hbec::odd_enabled() || sel_k > 0))
+        return fail(HBEC_ERR_INVALID_ARG, "mirrored unaligned plans need gf_odd and stripe records");
     int dev = 0, cus = 0, per_cu = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
@@ -106,6 +109,9 @@ int hbec::launch_unaligned_passes(const URec* recs, uint64_t n_recs, const std::
                 a.recs = recs;
                 a.n_recs = (uint32_t)n_recs;
                 a.accumulate = c0 > 0 ? 1u : 0u;
+                // mirror: each pass's inputs once (first output group), the
+                // outputs when one input pass makes them final
+                if (mirror) a.mirror = (r0 == 0 ? 1u : 0u) | (K_all <= hbec::kOddMaxK ? 2u : 0u);
                 for (int j = 0; j < K; ++j) {
                     int i = in_idx[c0 + j];
                     if (sel_k > 0 && i >= sel_k) {
@@ -135,6 +141,27 @@ int hbec::launch_unaligned_passes(const URec* recs, uint64_t n_recs, const std::
                 // guard-band bytes of every stripe, this pass's inputs
                 e = hbec::launch_odd_edges_plan(K, R, c0 > 0 ? 1 : 0, a, erecs, (uint32_t)n_erecs, stream);
                 if (e != hipSuccess) return hip_fail(e, "launch gf_odd_edges_plan");
+            }
+        }
+        if (mirror && n_erecs > 0) {
+            // the bytes the main kernel did not mirror, read back from the
+            // (final) stripes: guard bands of every shard, and whole outputs
+            // when k > kOddMaxK made them final only after the last pass
+            std::vector<int> all(in_idx);
+            all.insert(all.end(), out_idx.begin(), out_idx.end());
+            for (int pass = 0; pass < 2; ++pass) {
+                const bool full = pass == 1;
+                if (full && K_all <= hbec::kOddMaxK) break;
+                const std::vector<int>& idx = full ? out_idx : all;
+                for (size_t t0 = 0; t0 < idx.size(); t0 += hbec::kMirrorMaxIdx) {
+                    hbec::MirrorCopyArgs m;
+                    std::memset(&m, 0, sizeof(m));
+                    m.n_idx = (uint32_t)std::min<size_t>(hbec::kMirrorMaxIdx, idx.size() - t0);
+                    for (uint32_t t = 0; t < m.n_idx; ++t) m.idx[t] = (uint32_t)idx[t0 + t];
+                    m.full = full ? 1u : 0u;
+                    e = hbec::launch_odd_mirror_copy(erecs, (uint32_t)n_erecs, m, stream);
+                    if (e != hipSuccess) return hip_fail(e, "launch gf_odd_mirror_copy");
+                }
             }
         }
         return HBEC_OK;

@@ -7,7 +7,7 @@ One JSON line per shape.
     python scripts/bench_objplan_wide.py
 """
 import json, statistics, sys, torch
-sys.path.insert(0, '.')
+from pathlib import Path; sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 from hummingbird_amd import batch as B, reedsolomon as RS
 torch.cuda.set_device(0)
 def t(fn, reps=9):

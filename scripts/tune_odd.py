@@ -25,6 +25,13 @@ VARIANTS = {
     "uv4": ["HBEC_ODD_U_VERIFY=4"],
     "nobar": ["HBEC_ODD_BARRIER=0"],
     "sleep": ["HBEC_ODD_SLEEP=6"],
+    # round 3, second set
+    "aload": ["HBEC_ODD_ALOAD=1"],
+    "edge": ["HBEC_ODD_EDGE_PLAIN=1"],
+    "ntst0": ["HBEC_ODD_NT_ST=0"],
+    "planu2": ["HBEC_ODD_PLAN_U=2"],
+    "maxk12": ["HBEC_ODD_MAXK=12"],
+    "aedge": ["HBEC_ODD_ALOAD=1", "HBEC_ODD_EDGE_PLAIN=1"],
 }
 
 MiB = 1 << 20
@@ -98,6 +105,50 @@ def run(label, rnd=0, n=2048):
         row["ok"] = int(flags.count_nonzero().item()) == 0
         print(json.dumps(row), flush=True)
         del views
+        torch.cuda.empty_cache()
+    # plans: n ecSplit databufs of 1 MiB - (1..15) B back to back (stripe plan),
+    # and k > 8 object plans (data arena + parity arena)
+    import numpy as np
+
+    for k, m in [(4, 2), (8, 3), (10, 4)]:
+        rng = np.random.default_rng(k * 100 + m)
+        layout, off = [], 0
+        for _ in range(n):
+            s = -(-((1 << 20) - int(rng.integers(1, 16))) // k)
+            layout.append((off, s))
+            off += (k + m) * s
+        pool = torch.empty((1, off), dtype=torch.uint8, device="cuda")
+        B.fill_splitmix(pool, off)
+        enc = RS.New(k, m)
+        plan = B.StripePlan(enc, [(pool.data_ptr() + o, s) for o, s in layout])
+        ms = timeit(plan.encode)
+        nb = sum((k + m) * s for _, s in layout)
+        flags = torch.zeros(n, dtype=torch.int32, device="cuda")
+        for i, (o, s) in enumerate(layout[:64]):
+            v = [(pool.data_ptr() + o + j * s, 0) for j in range(k + m)]
+            B.verify_views(enc, v, 1, s, flags[i:i + 1])
+        torch.cuda.synchronize()
+        print(json.dumps({"variant": label, "round": rnd, "k": k, "m": m, "layout": "stripe plan odd",
+                          "encode": round(nb / (ms * 1e-3) / 8e12, 4),
+                          "ok": int(flags.count_nonzero().item()) == 0}), flush=True)
+        del pool, plan
+        torch.cuda.empty_cache()
+    for k, m, s in [(10, 4, 104858), (12, 4, 87392)]:
+        d = torch.empty((n, k * s), dtype=torch.uint8, device="cuda")
+        B.fill_splitmix(d, k * s)
+        par = torch.empty((n, m * s), dtype=torch.uint8, device="cuda")
+        enc = RS.New(k, m)
+        plan = B.StripePlan(enc, objects=[(d.data_ptr() + i * d.stride(0), par.data_ptr() + i * par.stride(0), s)
+                                          for i in range(n)])
+        ms = timeit(plan.encode)
+        nb = n * (k + m) * s
+        flags = torch.zeros(n, dtype=torch.int32, device="cuda")
+        B.verify_views(enc, B.shard_views(d, k, s) + B.shard_views(par, m, s), n, s, flags)
+        torch.cuda.synchronize()
+        print(json.dumps({"variant": label, "round": rnd, "k": k, "m": m, "S": s, "layout": "object plan",
+                          "encode": round(nb / (ms * 1e-3) / 8e12, 4),
+                          "ok": int(flags.count_nonzero().item()) == 0}), flush=True)
+        del d, par, plan
         torch.cuda.empty_cache()
 
 

@@ -324,3 +324,38 @@ def test_encode_host_md5_pinned_many_small_stripes_switch_arenas():
         del rows
     finally:
         hb.free()
+
+
+@pytest.mark.parametrize("k,m,sizes", [
+    (4, 2, [(1 << 18) - 1] * 24 + [(1 << 18) - 15, 161, 160, 159, 1, 7, 1001]),
+    (8, 3, [131071, 131065, 512 + 3, 200] * 6),
+    (10, 4, [104858, 4097, 65537] * 4),   # k > 8: outputs copied to the arena after the last pass
+    (17, 3, [1023] * 10 + [49]),
+    (3, 5, [2049, 17, 8193] * 4),          # m > 4: two output groups
+    (1, 1, [17, 4095])])
+def test_encode_host_md5_pinned_unaligned_zero_copy(k, m, sizes):
+    """Pinned stripes at odd byte offsets with S % 16 != 0 (ecSplit's S =
+    ceil(len / k) for 15 object sizes in 16, objectserver/ecutils.go:14-24):
+    coded in place over PCIe by the mirrored gf_odd plan kernel and hashed
+    from the device arena: the zero-copy path, parity
+    and every digest against the oracle."""
+    enc = RS.New(k, m)
+    rng = np.random.default_rng(k * 1000 + m)
+    total = sum((k + m) * s for s in sizes) + 64
+    hb = RS.HostBuffer(total)
+    try:
+        stripes, off = [], 3
+        for s in sizes:
+            st = hb.array[off:off + (k + m) * s]
+            st[:k * s] = rng.integers(0, 256, k * s, dtype=np.uint8)
+            st[k * s:] = 0x5A
+            stripes.append(st)
+            off += (k + m) * s + int(rng.integers(0, 16))
+        zc0, ring0 = _md5_stats()
+        hashes = enc.EncodeStripesMD5(stripes)
+        zc1, ring1 = _md5_stats()
+        assert (zc1 - zc0, ring1 - ring0) == (1, 0)
+        _check_stripes(k, m, sizes, stripes, hashes)
+        del stripes
+    finally:
+        hb.free()
