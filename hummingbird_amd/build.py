@@ -20,8 +20,8 @@ LIB = PKG / "libhbec.so"
 ROOT = PKG.parent
 INCLUDE = ROOT / "include"
 
-SOURCES = ["kernels.hip", "odd.hip", "wide.hip", "stripes.hip", "verify.hip", "md5.hip", "shardhash.cpp", "hbec.cpp", "ecutils.cpp", "plan.cpp", "hostpath.cpp", "batcher.cpp", "coalesce.cpp"]
-HEADERS = ["kernels.h", "gf256.h", "internal.h", "gf_device.h", "pool.h"]
+SOURCES = ["odd_k912.hip", "odd_k58.hip", "kernels.hip", "odd.hip", "wide.hip", "stripes.hip", "verify.hip", "md5.hip", "shardhash.cpp", "hbec.cpp", "ecutils.cpp", "plan.cpp", "hostpath.cpp", "batcher.cpp", "coalesce.cpp"]
+HEADERS = ["kernels.h", "gf256.h", "internal.h", "gf_device.h", "pool.h", "odd_impl.h"]
 ARCH = os.environ.get("HBEC_OFFLOAD_ARCH", "gfx950")
 
 

@@ -213,6 +213,10 @@ static int apply_odd(const PassArgs& a, int K, int R, bool accumulate, uint64_t 
 // ---------------------------------------------------------------------------
 static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
+static bool wide_apply_enabled();
+static int apply_wide(int rows, int cols, const uint8_t* coeffs, const hbec_view* in, const hbec_view* out,
+                      uint64_t n_obj, uint64_t shard_len, hipStream_t stream);
+
 int apply_views(int rows, int cols, const uint8_t* coeffs, const hbec_view* in, const hbec_view* out,
                 uint64_t n_obj, uint64_t shard_len, hipStream_t stream) {
     if (rows <= 0 || n_obj == 0 || shard_len == 0) return HBEC_OK;
@@ -228,6 +232,9 @@ int apply_views(int rows, int cols, const uint8_t* coeffs, const hbec_view* in, 
     int rc = current_device(&dev);
     if (rc) return rc;
     const int force_stream = g_force_stream.load();
+    if (!vec && g_unaligned_kernel.load() && cols > kOddMaxK && cols <= 256 && shard_len < (1ull << 31) &&
+        wide_apply_enabled())
+        return apply_wide(rows, cols, coeffs, in, out, n_obj, shard_len, stream);
 
     for (int r0 = 0; r0 < rows; r0 += kMaxR) {
         const int R = std::min(kMaxR, rows - r0);
@@ -933,37 +940,34 @@ static bool wide_verify_enabled() {
     return on;
 }
 
-static int verify_wide(const hbec_view* views, int k, int m, const uint8_t* prow, uint64_t n_obj,
-                       uint64_t shard_len, uint32_t* flags, hipStream_t stream) {
-    int dev = 0, cus = 0;
-    int rc = current_device(&dev);
-    if (rc) return rc;
-    rc = cu_count(dev, &cus);
-    if (rc) return rc;
-    const uint64_t main_len = wide_main_len(shard_len);
-    const uint64_t tpo = (main_len + wide_tile_bytes() - 1) / wide_tile_bytes();
-    for (int r0 = 0; r0 < m; r0 += kWideMaxR) {
-        const int R = std::min(kWideMaxR, m - r0);
+// gf_wide launches over n_obj objects of k input views: per group of <= 8
+// rows one device blob {in_base[k], in_stride[k], tables[k][words]} (the
+// input bases are re-uploaded, shifted, for each chunk of objects), then
+// launch(args, first object) per chunk of < 2^31 (and <= g_chunk_tiles) tiles.
+}  // extern "C"
+
+namespace hbec {  // gf_wide host side (templates need C++ linkage)
+
+template <class Launch>
+static int wide_launches(const hbec_view* in, int k, const uint8_t* coeffs, int rows, const hbec_view* out,
+                         uint64_t n_obj, uint64_t shard_len, uint64_t tpo, hipStream_t stream, Launch launch) {
+    for (int r0 = 0; r0 < rows; r0 += kWideMaxR) {
+        const int R = std::min(kWideMaxR, rows - r0);
         const uint32_t tw = wide_tab_words(R);
-        // device block: in_base[k], in_stride[k], tables[k][tw]
         const size_t words = (size_t)k * tw;
         std::vector<uint64_t> blob((size_t)2 * k + (words + 1) / 2, 0);
         for (int j = 0; j < k; ++j) {
-            blob[j] = reinterpret_cast<uint64_t>(views[j].base);
-            blob[(size_t)k + j] = views[j].obj_stride;
+            blob[j] = reinterpret_cast<uint64_t>(in[j].base);
+            blob[(size_t)k + j] = in[j].obj_stride;
         }
         uint32_t* tab = reinterpret_cast<uint32_t*>(blob.data() + 2 * k);
         for (int j = 0; j < k; ++j)
-            for (int r = 0; r < R; ++r) perm_table(prow[(size_t)(r0 + r) * k + j], tab + (size_t)j * tw + 5 * r);
+            for (int r = 0; r < R; ++r) perm_table(coeffs[(size_t)(r0 + r) * k + j], tab + (size_t)j * tw + 5 * r);
         void* d = nullptr;
-        rc = scratch_alloc(blob.size() * 8, stream, &d);
+        int rc = scratch_alloc(blob.size() * 8, stream, &d);
         if (rc) return rc;
         hipError_t e = hipMemcpyAsync(d, blob.data(), blob.size() * 8, hipMemcpyHostToDevice, stream);
         if (e == hipSuccess) e = hipStreamSynchronize(stream);  // blob is a host vector of this frame
-        if (e != hipSuccess) {
-            scratch_free(d, stream);
-            return hip_fail(e, "verify tables H2D");
-        }
         WideArgs a;
         std::memset(&a, 0, sizeof(a));
         a.in_base = static_cast<const uint64_t*>(d);
@@ -972,35 +976,75 @@ static int verify_wide(const hbec_view* views, int k, int m, const uint8_t* prow
         a.K = (uint32_t)k;
         a.shard_len = shard_len;
         a.tiles_per_obj = (uint32_t)tpo;
-        // launches of whole objects, < 2^31 tiles each; object o0's views
-        // are reached through the in_base offsets below (one upload per row group)
         const uint64_t max_obj = tpo ? std::max<uint64_t>(1, std::min<uint64_t>((1ull << 31), g_chunk_tiles) / tpo) : n_obj;
         for (uint64_t o0 = 0; o0 < n_obj && e == hipSuccess; o0 += max_obj) {
             const uint64_t no = std::min(max_obj, n_obj - o0);
             WideArgs b = a;
             for (int r = 0; r < R; ++r) {
-                b.out[r] = reinterpret_cast<uint64_t>(views[k + r0 + r].base) + o0 * views[k + r0 + r].obj_stride;
-                b.out_stride[r] = views[k + r0 + r].obj_stride;
+                b.out[r] = reinterpret_cast<uint64_t>(out[r0 + r].base) + o0 * out[r0 + r].obj_stride;
+                b.out_stride[r] = out[r0 + r].obj_stride;
             }
             b.n_obj = no;
             b.n_tiles = (uint32_t)(no * tpo);
             if (o0 > 0) {
-                // shift the input bases by o0 objects: a fresh upload for this chunk
                 std::vector<uint64_t> base(k);
                 for (int j = 0; j < k; ++j) base[j] = blob[j] + o0 * blob[(size_t)k + j];
                 e = hipMemcpyAsync(d, base.data(), (size_t)k * 8, hipMemcpyHostToDevice, stream);
                 if (e == hipSuccess) e = hipStreamSynchronize(stream);
                 if (e != hipSuccess) break;
             }
-            const uint64_t want = (b.n_tiles + 3) / 4;
-            const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cus * 2));
-            e = launch_verify_wide(R, b, flags + o0, grid, stream);
+            e = launch(b, R, o0);
         }
         scratch_free(d, stream);
-        if (e != hipSuccess) return hip_fail(e, "launch gf_verify_wide");
+        if (e != hipSuccess) return hip_fail(e, "launch gf_wide");
     }
     return HBEC_OK;
 }
+
+// 4-wave blocks per CU of the gf_wide grids (HBEC_WIDE_BPC): the kernel keeps
+// HBEC_WIDE_D loads in flight per lane, so it needs several waves per SIMD
+static int wide_grid(uint64_t n_tiles) {
+    static const int bpc = [] {
+        const char* e = std::getenv("HBEC_WIDE_BPC");
+        const int v = e ? std::atoi(e) : 0;
+        return v > 0 ? v : 4;
+    }();
+    int dev = 0, cus = 256;
+    if (current_device(&dev) == HBEC_OK) (void)cu_count(dev, &cus);
+    return (int)std::max<uint64_t>(1, std::min<uint64_t>((n_tiles + 3) / 4, (uint64_t)cus * bpc));
+}
+
+static int verify_wide(const hbec_view* views, int k, int m, const uint8_t* prow, uint64_t n_obj,
+                       uint64_t shard_len, uint32_t* flags, hipStream_t stream) {
+    const uint64_t tpo = (wide_main_len(shard_len) + wide_tile_bytes() - 1) / wide_tile_bytes();
+    return wide_launches(views, k, prow, m, views + k, n_obj, shard_len, tpo, stream,
+                         [&](const WideArgs& b, int R, uint64_t o0) {
+                             return launch_verify_wide(R, b, flags + o0, wide_grid(b.n_tiles), stream);
+                         });
+}
+
+// Apply of k > 8 inputs at any alignment in one pass (gf_wide apply):
+// HBEC_WIDE_APPLY=0 keeps the round-2 kernels (passes of <= 16 inputs).
+static bool wide_apply_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("HBEC_WIDE_APPLY");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+static int apply_wide(int rows, int cols, const uint8_t* coeffs, const hbec_view* in, const hbec_view* out,
+                      uint64_t n_obj, uint64_t shard_len, hipStream_t stream) {
+    const uint64_t tpo = wide_apply_tiles_per_obj(shard_len);
+    return wide_launches(in, cols, coeffs, rows, out, n_obj, shard_len, tpo, stream,
+                         [&](const WideArgs& b, int R, uint64_t) {
+                             return launch_apply_wide(R, b, wide_grid(b.n_tiles), stream);
+                         });
+}
+
+}  // namespace hbec
+
+extern "C" {
 
 static int verify_views(hbec_codec* c, const hbec_view* views, uint64_t n_obj, uint64_t shard_len, uint32_t* flags,
                         hipStream_t stream) {

@@ -140,6 +140,7 @@ hipError_t launch_unaligned_plan(int k, int r, const UPlanArgs& a, int grid, hip
 #ifndef HBEC_ODD_MAXK
 #define HBEC_ODD_MAXK 8
 #endif
+static_assert(HBEC_ODD_MAXK == 8 || HBEC_ODD_MAXK == 12, "gf_odd instances exist for K <= 8 (odd.hip, odd_k58.hip) and 9..12 (odd_k912.hip)");
 constexpr int kOddMaxK = HBEC_ODD_MAXK;
 // HBEC_ODD=1 / 0 selects gf_odd or the round-2 kernels (gf_apply_unaligned
 // family) for odd shards (default: HBEC_ODD_DEFAULT).
@@ -198,6 +199,11 @@ uint64_t wide_main_len(uint64_t shard_len);
 // r <= kWideMaxR rows per launch; K <= 256; shard_len < 2^31.  Flags objects
 // (flags[obj] |= 1) whose stored parity differs.
 hipError_t launch_verify_wide(int r, const WideArgs& a, uint32_t* flags, int grid, hipStream_t stream);
+// Apply of any k at any alignment in one pass (gf_wide apply + byte edges):
+// outputs out[0..r) of a.n_obj objects; a.tiles_per_obj =
+// wide_apply_tiles_per_obj(S) (0: the edge kernel codes every byte).
+uint32_t wide_apply_tiles_per_obj(uint64_t shard_len);
+hipError_t launch_apply_wide(int r, const WideArgs& a, int grid, hipStream_t stream);
 
 hipError_t launch_fill(uint8_t* dst, uint64_t n_obj, uint64_t obj_len, uint64_t obj_stride, uint64_t base_seed,
                        uint64_t first, int grid, hipStream_t stream);

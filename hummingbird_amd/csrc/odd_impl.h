@@ -1,0 +1,439 @@
+// odd_impl.h — the gf_odd kernel templates (see odd.hip for the design),
+// shared by the translation units that instantiate them: odd.hip (K <= 4,
+// launchers, edge and mirror kernels), odd_k58.hip (K 5..8), odd_k912.hip
+// (K 9..12 when HBEC_ODD_MAXK >= 12).  Every kernel instance lives in exactly
+// one translation unit, and the units compile in parallel.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <cstdlib>
+
+#include "gf_device.h"
+#include "kernels.h"
+
+namespace hbec {
+
+constexpr uint32_t kOddStore = 62;            // blocks stored per 64-lane window
+constexpr uint32_t kOddWin = kOddStore * 16;  // shard bytes per window (992)
+constexpr int32_t kOddGuard = 48;             // bytes at each end left to gf_odd_edges
+constexpr int32_t kOddEdgeSlots = 160;        // edge bytes handled per (shard, output): 80 head + 80 tail
+// the main kernel runs on shards longer than this (shorter ones: gf_odd_edges only)
+constexpr uint64_t kOddMinMain = (uint64_t)kOddEdgeSlots;
+
+#ifndef HBEC_ODD_SLEEP
+#define HBEC_ODD_SLEEP 0  // x 64 cycles after the next tile's loads
+#endif
+#ifndef HBEC_ODD_BARRIER
+#define HBEC_ODD_BARRIER 1  // apply: one block barrier per tile
+#endif
+#ifndef HBEC_ODD_VBARRIER
+#define HBEC_ODD_VBARRIER 0  // verify: none (8+3 57 -> 66 %, 6+3 63 -> 70 %, profiles/r03_tune_odd3.jsonl)
+#endif
+#ifndef HBEC_ODD_VMIN
+#define HBEC_ODD_VMIN 1  // K*R from which all table words live in VGPRs (1: always)
+#endif
+#ifndef HBEC_ODD_LB
+#define HBEC_ODD_LB 1  // launch_bounds min blocks per CU (register budget)
+#endif
+#ifndef HBEC_ODD_U_SMALL
+#define HBEC_ODD_U_SMALL 2  // windows per wave tile for K <= 4 (0: 4 / K); 2: 4+2 62.5 -> 65 % (r03_tune_odd3)
+#endif
+#ifndef HBEC_ODD_U_VERIFY
+#define HBEC_ODD_U_VERIFY 0  // windows per wave tile of verify for K <= 4 (0: as apply)
+#endif
+#ifndef HBEC_ODD_ALOAD
+#define HBEC_ODD_ALOAD 0  // 16-B-aligned input loads shifted by realign16: 1 for every K, 2 for K <= 4 (0: dword-aligned loads, 1 DPP)
+#endif
+#ifndef HBEC_ODD_EDGE_PLAIN
+#define HBEC_ODD_EDGE_PLAIN 0  // 1: blocks in a 128-B line shared with the next / previous window: plain (L2) stores
+#endif
+#ifndef HBEC_ODD_NT_ST
+#define HBEC_ODD_NT_ST 1  // 0: plain stores for every output block
+#endif
+#ifndef HBEC_ODD_PLAN_U
+#define HBEC_ODD_PLAN_U 2  // windows per plan record (2: odd 4+2 stripe plan 52.9 -> 59.5 %, r03b4)
+#endif
+
+enum : int { kOddApply = 0, kOddAcc = 1, kOddVerify = 2 };
+
+// windows per wave tile of the strided kernel: ~4 loads per lane in flight
+// for K <= 4 (as gf_apply_vec_pipe2's 1 KiB x 4 / K), one window above
+__host__ __device__ constexpr int odd_u(int k, int mode = kOddApply) {
+    return (mode == kOddVerify && HBEC_ODD_U_VERIFY > 0 && k <= 4)
+               ? HBEC_ODD_U_VERIFY
+               : (k <= 4 ? (HBEC_ODD_U_SMALL > 0 ? HBEC_ODD_U_SMALL : (4 / k)) : 1);
+}
+constexpr int kOddPlanU = HBEC_ODD_PLAN_U;  // plans: windows per record
+
+// One tile, wave-uniform.  Positions are 32-bit: the host sends shards of
+// 2^31 bytes or more to the round-2 kernels.
+template <int K, int R>
+struct OddTile {
+    uint64_t in[K];   // input shard bases (any alignment)
+    uint64_t out[R];  // output (or stored parity) shard bases
+    int32_t S;
+    int32_t c;        // shard position of the tile's first column
+    uint32_t live;    // 0: past-the-end stand-in (loaded, never stored)
+    uint32_t obj;     // flag index (verify)
+    // mirrored plans (zero-copy encode + ShardHash): each shard's 16-B-aligned
+    // slot in the device hash arena, shard position p at slot + p
+    uint64_t m_in[K];
+    uint64_t m_out[R];
+};
+
+// hash-arena pitch of a mirrored stripe: shard i at arena + i * P (16-B aligned)
+__host__ __device__ __forceinline__ uint64_t odd_mirror_pitch(uint64_t S) { return (S + 31u) & ~(uint64_t)15; }
+
+__device__ __forceinline__ int32_t odd_c0(uint64_t out0) { return (int32_t)((16u - ((uint32_t)out0 & 15u)) & 15u) - 32; }
+
+// One shard's dword-aligned 16-B blocks for one tile: lane column col's block
+// starts off + 16 col bytes after base4, clamped into the shard's dwords
+// (the clamp only ever moves columns the guard band keeps from being stored).
+struct OddIn {
+    uint64_t base4;  // base & ~3
+    int32_t off;     // block start of the tile's first column, from base4
+    int32_t lim;     // last block start inside the shard's dwords
+    uint32_t sh;     // the column's first byte within the block (0..3)
+};
+
+// input block alignment of a K-input kernel
+template <int K>
+__host__ __device__ constexpr uint32_t odd_ld_align() {
+    return (HBEC_ODD_ALOAD == 1 || (HBEC_ODD_ALOAD == 2 && K <= 4)) ? 16u : 4u;
+}
+
+template <uint32_t A>
+__device__ __forceinline__ OddIn odd_in(uint64_t base, int32_t S, int32_t c) {
+    const int32_t l4 = (int32_t)((uint32_t)base & (A - 1u));
+    const int32_t t = l4 + c;
+    OddIn o;
+    o.base4 = base & ~(uint64_t)(A - 1u);
+    o.sh = (uint32_t)t & (A - 1u);
+    o.off = t - (int32_t)o.sh;
+    o.lim = ((l4 + S + (int32_t)A - 1) & ~((int32_t)A - 1)) - 16;
+    return o;
+}
+
+__device__ __forceinline__ u32x4 odd_ld(const OddIn& o, int32_t col) {
+    int32_t v = o.off + 16 * col;
+    v = v < 0 ? 0 : (v > o.lim ? o.lim : v);
+    return ld16_addr(o.base4 + (uint64_t)(uint32_t)v);
+}
+
+// bytes [sh, sh + 16) of the lane's block and lane l+1's first dword (or,
+// with 16-B-aligned loads, lane l+1's block)
+template <uint32_t A>
+__device__ __forceinline__ u32x4 odd_shift_in(const u32x4& v, uint32_t sh) {
+    if constexpr (A == 16u) return realign16(v, lane_next4(v), sh);
+    const uint32_t n0 = lane_next(v[0]);
+    return u32x4{__builtin_amdgcn_alignbyte(v[1], v[0], sh), __builtin_amdgcn_alignbyte(v[2], v[1], sh),
+                 __builtin_amdgcn_alignbyte(v[3], v[2], sh), __builtin_amdgcn_alignbyte(n0, v[3], sh)};
+}
+
+typedef __attribute__((address_space(1))) uint8_t gu8_t;
+
+// ---- tile sources ----
+// A source names tile t compactly (id(): a few scalars, carried one and two
+// tiles ahead) and expands it to shard bases where they are used (at()), so
+// the pipeline does not hold three tiles of K + R 64-bit bases in SGPRs.
+// Strided batch (PassArgs): tile t = (object t / tpo, tile t % tpo).
+struct OddIdS {
+    uint32_t obj, ti, live;
+};
+
+template <int K, int R, int U>
+struct OddStrided {
+    using Id = OddIdS;
+    const PassArgs& a;
+    __device__ __forceinline__ Id id(uint32_t t, uint32_t n) const {
+        const uint32_t tt = t < n ? t : n - 1u;
+        const uint32_t tpo = a.tiles_per_obj;
+        const uint32_t obj = tt / tpo;
+        return Id{obj, tt - obj * tpo, t < n ? 1u : 0u};
+    }
+    __device__ __forceinline__ void at(OddTile<K, R>& b, const Id& i) const {
+#pragma unroll
+        for (int j = 0; j < K; ++j) b.in[j] = reinterpret_cast<uint64_t>(a.in[j]) + (uint64_t)i.obj * a.in_stride[j];
+#pragma unroll
+        for (int r = 0; r < R; ++r) b.out[r] = reinterpret_cast<uint64_t>(a.out[r]) + (uint64_t)i.obj * a.out_stride[r];
+        b.S = (int32_t)a.shard_len;
+        b.c = odd_c0(b.out[0]) + (int32_t)(i.ti * (uint32_t)(U * kOddWin));
+        b.live = i.live;
+        b.obj = i.obj;
+    }
+};
+
+// Plan records (URec): input j of the record's stripe at (bit j of in_sel ?
+// b : a) + in_idx[j] * S; rec.p0 = the record's first window * 992.
+struct OddIdP {
+    URec rec;
+    uint32_t live;
+};
+
+template <int K, int R, bool MIR = false>
+struct OddPlan {
+    using Id = OddIdP;
+    const UPlanArgs& p;
+    const URec* __restrict__ recs;
+    __device__ __forceinline__ Id id(uint32_t t, uint32_t n) const { return Id{recs[t < n ? t : n - 1u], t < n ? 1u : 0u}; }
+    __device__ __forceinline__ void at(OddTile<K, R>& b, const Id& i) const {
+        const uint64_t S = i.rec.shard_len;
+#pragma unroll
+        for (int j = 0; j < K; ++j) b.in[j] = (((p.in_sel >> j) & 1u) ? i.rec.b : i.rec.a) + (uint64_t)p.in_idx[j] * S;
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            b.out[r] = (((p.out_sel >> r) & 1u) ? i.rec.b : i.rec.a) + (uint64_t)p.out_idx[r] * S;
+        b.S = (int32_t)S;
+        b.c = odd_c0(b.out[0]) + (int32_t)i.rec.p0;
+        b.live = i.live;
+        b.obj = 0;
+        if constexpr (MIR) {
+            // rec.b = the stripe's arena (inputs and outputs are all at rec.a)
+            const uint64_t P = odd_mirror_pitch(S);
+#pragma unroll
+            for (int j = 0; j < K; ++j) b.m_in[j] = i.rec.b + (uint64_t)p.in_idx[j] * P;
+#pragma unroll
+            for (int r = 0; r < R; ++r) b.m_out[r] = i.rec.b + (uint64_t)p.out_idx[r] * P;
+        }
+    }
+};
+
+// ---- one tile ----
+template <int K, int R, int U, int MODE>
+struct OddRegs {
+    // shards loaded per column: verify loads the stored parity columns, the
+    // accumulate mode the old output blocks (with the inputs, one tile ahead)
+    static constexpr int NL = K + (MODE == kOddVerify || MODE == kOddAcc ? R : 0);
+    u32x4 x[U][NL];
+};
+
+template <int K, int R, int U, int MODE>
+__device__ __forceinline__ void odd_load(OddRegs<K, R, U, MODE>& X, const OddTile<K, R>& b, uint32_t lane) {
+    constexpr int NL = OddRegs<K, R, U, MODE>::NL;
+    OddIn src[NL];
+#pragma unroll
+    for (int j = 0; j < K; ++j) src[j] = odd_in<odd_ld_align<K>()>(b.in[j], b.S, b.c);
+    if constexpr (MODE == kOddVerify) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) src[K + r] = odd_in<odd_ld_align<K>()>(b.out[r], b.S, b.c);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int j = 0; j < (MODE == kOddAcc ? K : NL); ++j) X.x[u][j] = odd_ld(src[j], (int32_t)(u * kOddStore + lane));
+    if constexpr (MODE == kOddAcc) {
+        // the old output block each lane will rewrite: output r's aligned block
+        // at q = column + dl_r; lanes that store nothing read one inside the band
+        const int32_t hi = b.S - kOddGuard - 16;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint32_t dl = __builtin_amdgcn_readfirstlane((16u - (((uint32_t)b.out[r] + (uint32_t)b.c) & 15u)) & 15u);
+            const int32_t e = (int32_t)(((uint32_t)b.c + dl) & 15u);  // q = e mod 16
+            const int32_t qmin = kOddGuard + e, qmax = hi - ((hi - e) & 15);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int32_t q = b.c + (int32_t)(u * kOddWin) + 16 * (int32_t)lane + (int32_t)dl;
+                const int32_t qc = q < qmin ? qmin : (q > qmax ? qmax : q);
+                X.x[u][K + r] = ld16_addr(b.out[r] + (uint64_t)(int64_t)qc);
+            }
+        }
+    }
+}
+
+// output block store: non-temporal, or (HBEC_ODD_EDGE_PLAIN) plain for blocks
+// whose 128-B line the neighbouring window writes too, so L2 merges the halves
+__device__ __forceinline__ void odd_st(uint64_t addr, const u32x4& v, uint64_t win0, bool mine) {
+    if constexpr (HBEC_ODD_EDGE_PLAIN) {
+        const bool edge = (addr & ~(uint64_t)127) < win0 || (addr | 127u) >= win0 + kOddWin;
+        if (mine && edge) *reinterpret_cast<gu32x4*>(addr) = v;
+        if (mine && !edge) st16_addr(addr, v);
+    } else if constexpr (HBEC_ODD_NT_ST) {
+        if (mine) st16_addr(addr, v);
+    } else {
+        if (mine) *reinterpret_cast<gu32x4*>(addr) = v;
+    }
+}
+
+template <int K, int R, int U, int MODE, bool MIR = false>
+__device__ __forceinline__ void odd_finish(const OddRegs<K, R, U, MODE>& X, const OddTile<K, R>& b,
+                                           const TabArray& tab, const Tables<K, R, HBEC_ODD_VMIN>& tb, uint32_t lane,
+                                           uint32_t* flags, uint32_t mir = 0) {
+    constexpr int NL = OddRegs<K, R, U, MODE>::NL;
+    uint32_t sh[K + (MODE == kOddVerify ? R : 0)];
+#pragma unroll
+    for (int j = 0; j < K; ++j) sh[j] = __builtin_amdgcn_readfirstlane(((uint32_t)b.in[j] + (uint32_t)b.c) & (odd_ld_align<K>() - 1u));
+    if constexpr (MODE == kOddVerify) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            sh[K + r] = __builtin_amdgcn_readfirstlane(((uint32_t)b.out[r] + (uint32_t)b.c) & (odd_ld_align<K>() - 1u));
+    }
+    const int32_t S = b.S;
+    const int32_t hi = S - kOddGuard - 16;  // last block start the main kernel stores / compares
+    bool bad = false;
+    uint32_t dl[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) dl[r] = __builtin_amdgcn_readfirstlane((16u - (((uint32_t)b.out[r] + (uint32_t)b.c) & 15u)) & 15u);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int32_t cpos = b.c + (int32_t)(u * kOddWin) + 16 * (int32_t)lane;  // this lane's column
+        u32x4 x[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) x[j] = odd_shift_in<odd_ld_align<K>()>(X.x[u][j], sh[j]);
+        u32x4 acc[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r] = u32x4{0, 0, 0, 0};
+        gf_dot<K, R, HBEC_ODD_VMIN>(acc, x, tab, tb);
+        if constexpr (MIR && MODE != kOddVerify) {
+            // mirror: every arena slot is 16-B aligned, so column i's arena
+            // block starts at qm = cpos + dm, dm = -c mod 16; same guard band
+            // (the head and tail bytes are copied by gf_odd_mirror_copy)
+            const uint32_t dm = __builtin_amdgcn_readfirstlane((0u - (uint32_t)b.c) & 15u);
+            const int32_t qm = cpos + (int32_t)dm;
+            const bool mm = b.live != 0u && lane < kOddStore && qm >= kOddGuard && qm <= hi;
+            if (mir & 1u) {
+#pragma unroll
+                for (int j = 0; j < K; ++j) {
+                    const u32x4 v = realign16(x[j], lane_next4(x[j]), dm);
+                    if (mm) st16_addr(b.m_in[j] + (uint64_t)(int64_t)qm, v);
+                }
+            }
+            if (MODE == kOddApply && (mir & 2u)) {  // outputs are final only in a single input pass
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const u32x4 v = realign16(acc[r], lane_next4(acc[r]), dm);
+                    if (mm) st16_addr(b.m_out[r] + (uint64_t)(int64_t)qm, v);
+                }
+            }
+        }
+        if constexpr (MODE == kOddVerify) {
+            // frame columns = output 0's blocks: compare those inside the guard band
+            const bool mine = b.live != 0u && lane < kOddStore && cpos >= kOddGuard && cpos <= hi;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const u32x4 df = odd_shift_in<odd_ld_align<K>()>(X.x[u][K + r], sh[K + r]) ^ acc[r];
+                bad |= mine && (df[0] | df[1] | df[2] | df[3]) != 0u;
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                u32x4 blk = acc[r];
+                if (dl[r] != 0u) blk = realign16(acc[r], lane_next4(acc[r]), dl[r]);  // wave-uniform (never r = 0)
+                const int32_t q = cpos + (int32_t)dl[r];  // block start: out[r] + q is 16-B aligned
+                const bool mine = b.live != 0u && lane < kOddStore && q >= kOddGuard && q <= hi;
+                if constexpr (MODE == kOddAcc) blk ^= X.x[u][K + r];  // the old block (odd_load)
+                const uint64_t win0 = b.out[r] + (uint64_t)(int64_t)(b.c + (int32_t)(u * kOddWin) + (int32_t)dl[r]);
+                odd_st(b.out[r] + (uint64_t)(int64_t)q, blk, win0, mine);
+            }
+        }
+    }
+    if constexpr (MODE == kOddVerify) {
+        if (__any(bad)) {
+            if (lane == 0u) atomicOr(flags + b.obj, 1u);
+        }
+    }
+}
+
+template <int K, int R, int U, int MODE, class Src, bool MIR = false>
+__device__ __forceinline__ void odd_body(const Src& src, uint32_t n, const TabArray& tab, uint32_t* flags,
+                                         uint32_t mir = 0) {
+    constexpr uint32_t WPB = kPipeBlockThreads / 64;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t nw = gridDim.x * WPB;
+    const uint32_t wave0 = __builtin_amdgcn_readfirstlane(xcd_block() * WPB);  // the block's first wave
+    const uint32_t dw = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (wave0 >= n) return;  // whole blocks only: the loop below has block barriers
+    const Tables<K, R, HBEC_ODD_VMIN> tb = load_tables<K, R, HBEC_ODD_VMIN>(tab);
+    typename Src::Id cur = src.id(wave0 + dw, n);
+    OddRegs<K, R, U, MODE> X;
+    {
+        OddTile<K, R> b;
+        src.at(b, cur);
+        odd_load<K, R, U, MODE>(X, b, lane);
+    }
+    typename Src::Id nxt = src.id(wave0 + dw + nw, n);
+    for (uint32_t b0 = wave0 + nw; b0 < n; b0 += nw) {  // block-uniform trip count
+        OddRegs<K, R, U, MODE> Y;
+        {
+            OddTile<K, R> b;
+            src.at(b, nxt);
+            odd_load<K, R, U, MODE>(Y, b, lane);
+        }
+        if (HBEC_ODD_SLEEP > 0) __builtin_amdgcn_s_sleep(HBEC_ODD_SLEEP);
+        if (MODE == kOddVerify ? HBEC_ODD_VBARRIER : HBEC_ODD_BARRIER) __builtin_amdgcn_s_barrier();
+        const typename Src::Id after = src.id(b0 + dw + nw, n);
+        {
+            OddTile<K, R> b;
+            src.at(b, cur);
+            odd_finish<K, R, U, MODE, MIR>(X, b, tab, tb, lane, flags, mir);
+        }
+        X = Y;
+        cur = nxt;
+        nxt = after;
+    }
+    OddTile<K, R> b;
+    src.at(b, cur);
+    odd_finish<K, R, U, MODE, MIR>(X, b, tab, tb, lane, flags, mir);
+}
+
+template <int K, int R, int MODE>
+__global__ __launch_bounds__(kPipeBlockThreads, HBEC_ODD_LB) void gf_odd(PassArgs a, uint32_t* flags) {
+    constexpr int U = odd_u(K, MODE);
+    odd_body<K, R, U, MODE>(OddStrided<K, R, U>{a}, a.n_tiles, a.tab, flags);
+}
+
+template <int K, int R, int MODE, bool MIR = false>
+__global__ __launch_bounds__(kPipeBlockThreads, HBEC_ODD_LB) void gf_odd_plan(UPlanArgs p, const URec* __restrict__ recs) {
+    odd_body<K, R, kOddPlanU, MODE, OddPlan<K, R, MIR>, MIR>(OddPlan<K, R, MIR>{p, recs}, p.n_recs, p.tab, nullptr,
+                                                            p.mirror);
+}
+
+// ---------------------------------------------------------------------------
+// launch table: kernel of (K, r, mode, plan?, mirrored?)
+// ---------------------------------------------------------------------------
+template <int K, int R, int MODE>
+static const void* odd_pick(bool plan, bool mirror) {
+    if (!plan) return (const void*)&gf_odd<K, R, MODE>;
+    if constexpr (MODE != kOddVerify) {
+        if (mirror) return (const void*)&gf_odd_plan<K, R, MODE, true>;
+    }
+    return (const void*)&gf_odd_plan<K, R, MODE>;
+}
+
+template <int K, int MODE>
+static const void* odd_for_r(int r, bool plan, bool mirror) {
+    switch (r) {
+        case 1: return odd_pick<K, 1, MODE>(plan, mirror);
+        case 2: return odd_pick<K, 2, MODE>(plan, mirror);
+        case 3: return odd_pick<K, 3, MODE>(plan, mirror);
+        case 4: return odd_pick<K, 4, MODE>(plan, mirror);
+    }
+    return nullptr;
+}
+
+template <int K>
+static const void* odd_kernel_k(int r, int mode, bool plan, bool mirror) {
+    switch (mode) {
+        case kOddApply: return odd_for_r<K, kOddApply>(r, plan, mirror);
+        case kOddAcc: return odd_for_r<K, kOddAcc>(r, plan, mirror);
+        case kOddVerify: return plan ? nullptr : odd_for_r<K, kOddVerify>(r, false, false);
+    }
+    return nullptr;
+}
+
+template <int K0, int K1>
+static const void* odd_kernel_range(int k, int r, int mode, bool plan, bool mirror) {
+    if constexpr (K0 > K1) {
+        return nullptr;
+    } else {
+        if (k == K0) return odd_kernel_k<K0>(r, mode, plan, mirror);
+        return odd_kernel_range<K0 + 1, K1>(k, r, mode, plan, mirror);
+    }
+}
+
+// the other translation units' ranges
+const void* odd_kernel_k58(int k, int r, int mode, bool plan, bool mirror);
+const void* odd_kernel_k912(int k, int r, int mode, bool plan, bool mirror);
+
+}  // namespace hbec

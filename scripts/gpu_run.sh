@@ -23,7 +23,7 @@ step() {
 for s in "$@"; do
   case $s in
     build) step build 600 python -c "import __graft_entry__ as g; g.build()" ;;
-    tests) step tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
+    tests) step tests 900 python -u -m pytest tests -m gpu -x -v --tb=short --timeout 120 --timeout-method thread -p no:cacheprovider ;;
     testsall) step testsall 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --steps 50 --warmup 10 ;;

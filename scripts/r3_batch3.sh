@@ -5,7 +5,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out; mkdir -p $OUT
-timeout -k 10 400 python -u -m pytest tests/test_gpu_unaligned.py tests/test_gpu_md5.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $OUT/r3b3_tests.log 2>&1
+timeout -k 10 400 python -u -m pytest tests/test_gpu_unaligned.py tests/test_gpu_md5.py -x -q --tb=short --timeout 120 --timeout-method thread -p no:cacheprovider > $OUT/r3b3_tests.log 2>&1
 rc=$?; tail -5 $OUT/r3b3_tests.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 200 python scripts/bench_verify_wide.py > $OUT/r3b3_verify_wide.jsonl 2>&1 || exit $?
 HBEC_WIDE_VERIFY=0 timeout -k 10 200 python scripts/bench_verify_wide.py >> $OUT/r3b3_verify_wide.jsonl 2>&1 || exit $?

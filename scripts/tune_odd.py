@@ -32,6 +32,8 @@ VARIANTS = {
     "planu2": ["HBEC_ODD_PLAN_U=2"],
     "maxk12": ["HBEC_ODD_MAXK=12"],
     "aedge": ["HBEC_ODD_ALOAD=1", "HBEC_ODD_EDGE_PLAIN=1"],
+    "aload4": ["HBEC_ODD_ALOAD=2"],
+    "wd8": ["HBEC_WIDE_D=8"],
 }
 
 MiB = 1 << 20

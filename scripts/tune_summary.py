@@ -1,7 +1,25 @@
-import json, sys
-for l in open(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/tune.log"):
-    if l.startswith("{"):
-        d = json.loads(l)
-        print(f"{d['variant']:12s} enc {d['enc_ms_med']:.4f}/{d['enc_ms_min']:.4f} rec {d['rec_ms_med']:.4f}/{d['rec_ms_min']:.4f} "
-              f"GB/s {d['enc_GBs']:7.1f} {d['rec_GBs']:7.1f} frac {d['frac']:.4f} ok={d['parity_ok'] and d['rebuilt_ok']} "
-              f"tile={d.get('tile')} bpc={d.get('blocks_per_cu')}")
+#!/usr/bin/env python3
+"""Median per (shape, variant) of scripts/tune_odd.py JSON lines.
+
+    python scripts/tune_summary.py FILE.jsonl
+"""
+import collections
+import json
+import statistics
+import sys
+
+agg = collections.defaultdict(list)
+for line in open(sys.argv[1]):
+    line = line.strip()
+    if not line.startswith("{"):
+        continue
+    r = json.loads(line)
+    agg[(r["k"], r["m"], r.get("S") or 0, r["layout"], r["variant"])].append(r)
+for key in sorted(agg):
+    rows = agg[key]
+    out = []
+    for op in ("encode", "reconstruct", "verify"):
+        v = [x[op] for x in rows if x.get(op)]
+        if v:
+            out.append(f"{op[:3]} {statistics.median(v):.3f}")
+    print(key, " ".join(out), all(x.get("ok", True) for x in rows))

@@ -341,7 +341,7 @@ def test_encode_host_md5_pinned_unaligned_zero_copy(k, m, sizes):
     and every digest against the oracle."""
     enc = RS.New(k, m)
     rng = np.random.default_rng(k * 1000 + m)
-    total = sum((k + m) * s for s in sizes) + 64
+    total = sum((k + m) * s for s in sizes) + 16 * len(sizes) + 64  # stripes + gaps of < 16 B
     hb = RS.HostBuffer(total)
     try:
         stripes, off = [], 3
@@ -351,6 +351,7 @@ def test_encode_host_md5_pinned_unaligned_zero_copy(k, m, sizes):
             st[k * s:] = 0x5A
             stripes.append(st)
             off += (k + m) * s + int(rng.integers(0, 16))
+        assert off <= total and all(len(st) == (k + m) * s for st, s in zip(stripes, sizes))
         zc0, ring0 = _md5_stats()
         hashes = enc.EncodeStripesMD5(stripes)
         zc1, ring1 = _md5_stats()
