@@ -93,12 +93,19 @@ KERNEL_SOURCES = ("hummingbird_amd/csrc/kernels.hip", "hummingbird_amd/csrc/gf_d
                   "hummingbird_amd/csrc/kernels.h")
 
 
-def kernel_sources_sha256() -> str:
+def kernel_sources_sha256(sources=KERNEL_SOURCES) -> str:
     h = hashlib.sha256()
-    for rel in KERNEL_SOURCES:
+    for rel in sources:
         h.update(rel.encode())
         h.update((ROOT / rel).read_bytes())
     return h.hexdigest()
+
+
+# Sources of the odd_objects leg's kernels (gf_odd<4, 2, 0> / <4, 2, 2> and
+# gf_odd_edges): its traffic is reported only from a PMC summary collected
+# on exactly these sources (pmc_summary.py records both hashes).
+ODD_SOURCES = ("hummingbird_amd/csrc/odd.hip", "hummingbird_amd/csrc/odd_impl.h", "hummingbird_amd/csrc/gf_device.h",
+               "hummingbird_amd/csrc/kernels.h")
 
 
 def load_pmc(prefix_glob="profiles/r[0-9][0-9]_pmc.json"):
@@ -430,6 +437,22 @@ def odd_objects(n=4096, obj_len=(1 << 20) - 4, reps=20, settle=40):
         ms = e0.elapsed_time(e1) / reps
         gbs = nbytes / (ms * 1e-3) / 1e9
         out[name] = {"ms": round(ms, 4), "GB_s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
+    # HBM traffic per launch from the committed PMC summary (two separate
+    # --pmc passes over this bench), when it was collected on these sources
+    pmc_files = sorted(glob.glob(str(ROOT / "profiles/r[0-9][0-9]_pmc.json")))
+    pmc = json.loads(Path(pmc_files[-1]).read_text()) if pmc_files else {}
+    fresh = pmc.get("odd_sources_sha256") == kernel_sources_sha256(ODD_SOURCES)
+    kern = pmc.get("kernels", {})
+    for name, kname in (("encode", "gf_odd<4, 2, 0>"), ("reconstruct", "gf_odd<4, 2, 0>"), ("verify", "gf_odd<4, 2, 2>")):
+        edge = "gf_odd_edges<2>" if name == "verify" else "gf_odd_edges<0>"
+        t = kern.get(kname, {}).get("hbm_bytes_per_launch") if fresh else None
+        te = kern.get(edge, {}).get("hbm_bytes_per_launch") if fresh else None
+        if t is not None:
+            out[name]["traffic"] = int(t + (te or 0))
+            out[name]["traffic_ratio"] = round((t + (te or 0)) / nbytes, 4)
+    out["traffic_source"] = os.path.relpath(pmc_files[-1], ROOT) if (pmc_files and fresh) else None
+    if not fresh:
+        out["traffic_note"] = "no PMC summary collected on this tree's odd-kernel sources"
     # the check: erase shards 0-1 of every object for real, rebuild them, and
     # Verify every object (a reconstruct that wrote nothing would fail here)
     rows[:, :2 * s].fill_(0x3C)

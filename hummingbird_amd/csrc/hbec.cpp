@@ -232,7 +232,9 @@ int apply_views(int rows, int cols, const uint8_t* coeffs, const hbec_view* in, 
     int rc = current_device(&dev);
     if (rc) return rc;
     const int force_stream = g_force_stream.load();
-    if (!vec && g_unaligned_kernel.load() && cols > kOddMaxK && cols <= 256 && shard_len < (1ull << 31) &&
+    // k > 16 at any alignment: one gf_wide pass instead of accumulate passes
+    // (9..12 take gf_odd, 13..16 the round-2 one-pass gf_apply_unaligned)
+    if (!vec && g_unaligned_kernel.load() && cols > kMaxK && cols <= 256 && shard_len < (1ull << 31) &&
         wide_apply_enabled())
         return apply_wide(rows, cols, coeffs, in, out, n_obj, shard_len, stream);
 
@@ -929,7 +931,7 @@ int hbec_fill_splitmix(void* dst, uint64_t n_objects, uint64_t obj_len, uint64_t
 }
 
 // ---- Encoder.Verify ------------------------------------------------------
-// Verify of k > kOddMaxK data shards (gf_verify_wide): HBEC_WIDE_VERIFY=0
+// Verify of k > 8 data shards (gf_verify_wide): HBEC_WIDE_VERIFY=0
 // falls back to the round-2 kernels (gf_verify_unaligned, k <= 16) and the
 // scratch recompute (k > 16).
 static bool wide_verify_enabled() {
@@ -1001,14 +1003,15 @@ static int wide_launches(const hbec_view* in, int k, const uint8_t* coeffs, int 
     return HBEC_OK;
 }
 
-// 4-wave blocks per CU of the gf_wide grids (HBEC_WIDE_BPC): the kernel keeps
-// HBEC_WIDE_D loads in flight per lane, so it needs several waves per SIMD
-static int wide_grid(uint64_t n_tiles) {
-    static const int bpc = [] {
+// 4-wave blocks per CU of the gf_wide grids (HBEC_WIDE_BPC overrides): the
+// kernel keeps HBEC_WIDE_D loads in flight per lane, so it needs several waves
+// per SIMD; verify 8 (10+4 46 -> 49 %, r3b5), apply 4 (r3b6)
+static int wide_grid(uint64_t n_tiles, int dflt) {
+    static const int env = [] {
         const char* e = std::getenv("HBEC_WIDE_BPC");
-        const int v = e ? std::atoi(e) : 0;
-        return v > 0 ? v : 4;
+        return e ? std::atoi(e) : 0;
     }();
+    const int bpc = env > 0 ? env : dflt;
     int dev = 0, cus = 256;
     if (current_device(&dev) == HBEC_OK) (void)cu_count(dev, &cus);
     return (int)std::max<uint64_t>(1, std::min<uint64_t>((n_tiles + 3) / 4, (uint64_t)cus * bpc));
@@ -1019,7 +1022,7 @@ static int verify_wide(const hbec_view* views, int k, int m, const uint8_t* prow
     const uint64_t tpo = (wide_main_len(shard_len) + wide_tile_bytes() - 1) / wide_tile_bytes();
     return wide_launches(views, k, prow, m, views + k, n_obj, shard_len, tpo, stream,
                          [&](const WideArgs& b, int R, uint64_t o0) {
-                             return launch_verify_wide(R, b, flags + o0, wide_grid(b.n_tiles), stream);
+                             return launch_verify_wide(R, b, flags + o0, wide_grid(b.n_tiles, 8), stream);
                          });
 }
 
@@ -1038,7 +1041,7 @@ static int apply_wide(int rows, int cols, const uint8_t* coeffs, const hbec_view
     const uint64_t tpo = wide_apply_tiles_per_obj(shard_len);
     return wide_launches(in, cols, coeffs, rows, out, n_obj, shard_len, tpo, stream,
                          [&](const WideArgs& b, int R, uint64_t) {
-                             return launch_apply_wide(R, b, wide_grid(b.n_tiles), stream);
+                             return launch_apply_wide(R, b, wide_grid(b.n_tiles, 4), stream);
                          });
 }
 
@@ -1143,7 +1146,8 @@ static int verify_views(hbec_codec* c, const hbec_view* views, uint64_t n_obj, u
         }
         return HBEC_OK;
     }
-    if (g_unaligned_kernel.load() && odd_enabled() && k <= kOddMaxK && shard_len < (1ull << 31)) {
+    // k <= 8: gf_odd verify; above, gf_verify_wide (10+4 53 vs 55 %, 12+4 41 vs 54 %, r3b7)
+    if (g_unaligned_kernel.load() && odd_enabled() && k <= 8 && shard_len < (1ull << 31)) {
         // any alignment: recompute and compare in one pass (gf_odd verify), <= 4 rows per launch
         int dev = 0;
         int rc = current_device(&dev);
@@ -1166,7 +1170,7 @@ static int verify_views(hbec_codec* c, const hbec_view* views, uint64_t n_obj, u
         }
         return HBEC_OK;
     }
-    if (g_unaligned_kernel.load() && k > kOddMaxK && k <= 256 && shard_len < (1ull << 31) && wide_verify_enabled()) {
+    if (g_unaligned_kernel.load() && k > 8 && k <= 256 && shard_len < (1ull << 31) && wide_verify_enabled()) {
         // k > 8 at any alignment (k > 16 included): one read-only pass per <= 8
         // rows (gf_verify_wide, wide.hip), coefficient tables in LDS
         return verify_wide(views, k, m, prow, n_obj, shard_len, flags, stream);

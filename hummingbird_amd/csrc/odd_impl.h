@@ -170,14 +170,26 @@ struct OddStrided {
 struct OddIdP {
     URec rec;
     uint32_t live;
+    uint32_t sub;  // wave tile within the record (SUB > 1)
 };
+
+// A record covers kOddPlanU windows; kernels with fewer windows per wave tile
+// (U = odd_plan_u(K)) take each record as SUB = kOddPlanU / U wave tiles.
+template <int K>
+__host__ __device__ constexpr int odd_plan_u(int) {
+    return K <= 4 ? kOddPlanU : 1;  // K > 4: 2 windows of K inputs spill (10+4 object plan 42 -> 31 %, r3b7)
+}
 
 template <int K, int R, bool MIR = false>
 struct OddPlan {
     using Id = OddIdP;
+    static constexpr uint32_t SUB = (uint32_t)(kOddPlanU / odd_plan_u<K>(0));
     const UPlanArgs& p;
     const URec* __restrict__ recs;
-    __device__ __forceinline__ Id id(uint32_t t, uint32_t n) const { return Id{recs[t < n ? t : n - 1u], t < n ? 1u : 0u}; }
+    __device__ __forceinline__ Id id(uint32_t t, uint32_t n) const {
+        const uint32_t tt = t < n ? t : n - 1u;
+        return Id{recs[tt / SUB], t < n ? 1u : 0u, tt % SUB};
+    }
     __device__ __forceinline__ void at(OddTile<K, R>& b, const Id& i) const {
         const uint64_t S = i.rec.shard_len;
 #pragma unroll
@@ -186,7 +198,7 @@ struct OddPlan {
         for (int r = 0; r < R; ++r)
             b.out[r] = (((p.out_sel >> r) & 1u) ? i.rec.b : i.rec.a) + (uint64_t)p.out_idx[r] * S;
         b.S = (int32_t)S;
-        b.c = odd_c0(b.out[0]) + (int32_t)i.rec.p0;
+        b.c = odd_c0(b.out[0]) + (int32_t)i.rec.p0 + (int32_t)(i.sub * (uint32_t)odd_plan_u<K>(0) * kOddWin);
         b.live = i.live;
         b.obj = 0;
         if constexpr (MIR) {
@@ -385,8 +397,8 @@ __global__ __launch_bounds__(kPipeBlockThreads, HBEC_ODD_LB) void gf_odd(PassArg
 
 template <int K, int R, int MODE, bool MIR = false>
 __global__ __launch_bounds__(kPipeBlockThreads, HBEC_ODD_LB) void gf_odd_plan(UPlanArgs p, const URec* __restrict__ recs) {
-    odd_body<K, R, kOddPlanU, MODE, OddPlan<K, R, MIR>, MIR>(OddPlan<K, R, MIR>{p, recs}, p.n_recs, p.tab, nullptr,
-                                                            p.mirror);
+    using Src = OddPlan<K, R, MIR>;
+    odd_body<K, R, odd_plan_u<K>(0), MODE, Src, MIR>(Src{p, recs}, p.n_recs * Src::SUB, p.tab, nullptr, p.mirror);
 }
 
 // ---------------------------------------------------------------------------
@@ -395,10 +407,11 @@ __global__ __launch_bounds__(kPipeBlockThreads, HBEC_ODD_LB) void gf_odd_plan(UP
 template <int K, int R, int MODE>
 static const void* odd_pick(bool plan, bool mirror) {
     if (!plan) return (const void*)&gf_odd<K, R, MODE>;
-    if constexpr (MODE != kOddVerify) {
+    if constexpr (MODE != kOddVerify) {  // plans never verify
         if (mirror) return (const void*)&gf_odd_plan<K, R, MODE, true>;
+        return (const void*)&gf_odd_plan<K, R, MODE>;
     }
-    return (const void*)&gf_odd_plan<K, R, MODE>;
+    return nullptr;
 }
 
 template <int K, int MODE>

@@ -27,7 +27,12 @@
 namespace hbec {
 
 constexpr uint32_t kWideStore = 62;             // compared columns per 64-lane window
-constexpr uint32_t kWideWin = kWideStore * 16;  // shard bytes per tile
+constexpr uint32_t kWideWin = kWideStore * 16;  // shard bytes per window
+#ifndef HBEC_WIDE_U
+#define HBEC_WIDE_U 2  // windows per tile: each element's tables are read once for U columns (10+4 verify 51 -> 55 %, r3b7)
+#endif
+constexpr int kWideU = HBEC_WIDE_U;
+constexpr uint32_t kWideTile = kWideU * kWideWin;  // shard bytes per tile
 #ifndef HBEC_WIDE_D
 #define HBEC_WIDE_D 4  // loads in flight per lane (ring depth)
 #endif
@@ -69,9 +74,9 @@ __device__ __forceinline__ uint64_t wide_base(const uint32_t* e4, uint32_t obj) 
 // c0 = -32 + (-out0 mod 16)), windows of 62 stored blocks.
 template <bool APPLY>
 __device__ __forceinline__ int32_t wide_c(const uint32_t* lds_addr, uint32_t K, uint32_t obj, uint32_t ti) {
-    if constexpr (!APPLY) return (int32_t)(ti * kWideWin);
+    if constexpr (!APPLY) return (int32_t)(ti * kWideTile);
     const uint32_t o0 = (uint32_t)wide_base(lds_addr + 4 * K, obj);
-    return (int32_t)((16u - (o0 & 15u)) & 15u) - 32 + (int32_t)(ti * kWideWin);
+    return (int32_t)((16u - (o0 & 15u)) & 15u) - 32 + (int32_t)(ti * kWideTile);
 }
 
 // Element addresses and tables come from LDS (ds_read, in order with the
@@ -120,15 +125,18 @@ __global__ __launch_bounds__(kPipeBlockThreads) void gf_wide(WideArgs a, uint32_
     wide_set(cp, w, tpo);
     int32_t pc = wide_c<APPLY>(lds_addr, K, pp.obj, pp.ti);
     uint32_t issued = 0;
-    auto issue = [&](u32x4& buf, uint32_t& sh) {
+    auto issue = [&](u32x4 (&buf)[kWideU], uint32_t& sh) {
         const uint64_t base = wide_base(lds_addr + 4 * pp.j, pp.obj);
         const int32_t l4 = (int32_t)((uint32_t)base & 3u);
         const int32_t t = l4 + pc;
         sh = (uint32_t)t & 3u;
-        int32_t v = t - (int32_t)sh + 16 * (int32_t)lane;
         const int32_t lim = ((l4 + S + 3) & ~3) - 16;
-        v = v < 0 ? 0 : (v > lim ? lim : v);
-        buf = ld16_addr((base & ~(uint64_t)3) + (uint64_t)(uint32_t)v);
+#pragma unroll
+        for (int u = 0; u < kWideU; ++u) {
+            int32_t v = t - (int32_t)sh + 16 * (int32_t)lane + u * (int32_t)kWideWin;
+            v = v < 0 ? 0 : (v > lim ? lim : v);
+            buf[u] = ld16_addr((base & ~(uint64_t)3) + (uint64_t)(uint32_t)v);
+        }
         if (++issued < total) {
             if (++pp.j == L) {
                 wide_set(pp, pp.t + nw, tpo);
@@ -136,19 +144,23 @@ __global__ __launch_bounds__(kPipeBlockThreads) void gf_wide(WideArgs a, uint32_
             }
         }
     };
-    u32x4 ring[kWideD];
+    u32x4 ring[kWideD][kWideU];
     uint32_t rsh[kWideD];
 #pragma unroll
     for (int i = 0; i < kWideD; ++i) issue(ring[i], rsh[i]);
 
-    u32x4 acc[R];
+    u32x4 acc[kWideU][R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) acc[r] = u32x4{0, 0, 0, 0};
+    for (int u = 0; u < kWideU; ++u)
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[u][r] = u32x4{0, 0, 0, 0};
     bool bad = false;
     for (uint32_t p0 = 0; p0 < total; p0 += kWideD) {
 #pragma unroll
         for (int i = 0; i < kWideD; ++i) {
-            const u32x4 x = wide_shift(ring[i], rsh[i]);
+            u32x4 xs[kWideU];
+#pragma unroll
+            for (int u = 0; u < kWideU; ++u) xs[u] = wide_shift(ring[i][u], rsh[i]);
             // the reload reuses ring[i]'s registers only after x is computed:
             // a load hoisted above lands in fresh registers that the loop's
             // back edge must copy back, i.e. waits for (vmcnt(0) per turn)
@@ -168,43 +180,53 @@ __global__ __launch_bounds__(kPipeBlockThreads) void gf_wide(WideArgs a, uint32_
                         tw[4 * q + 3] = v[3];
                     }
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const Sel sx = selectors(x[e]);
+                    for (int u = 0; u < kWideU; ++u)
 #pragma unroll
-                        for (int r = 0; r < R; ++r)
-                            acc[r][e] ^= gf_mul_sel(sx, tw[5 * r], tw[5 * r + 1], tw[5 * r + 2], tw[5 * r + 3],
-                                                    tw[5 * r + 4]);
-                    }
+                        for (int e = 0; e < 4; ++e) {
+                            const Sel sx = selectors(xs[u][e]);
+#pragma unroll
+                            for (int r = 0; r < R; ++r)
+                                acc[u][r][e] ^= gf_mul_sel(sx, tw[5 * r], tw[5 * r + 1], tw[5 * r + 2], tw[5 * r + 3],
+                                                           tw[5 * r + 4]);
+                        }
                     if (APPLY && j == K - 1u) {
                         // tile done: each output's 16-B-aligned blocks in the band
                         const int32_t c = wide_c<APPLY>(lds_addr, K, cp.obj, cp.ti);
-                        const int32_t cpos = c + 16 * (int32_t)lane;
 #pragma unroll
                         for (int r = 0; r < R; ++r) {
                             const uint64_t ob = wide_base(lds_addr + 4 * (K + r), cp.obj);
                             const uint32_t dl = __builtin_amdgcn_readfirstlane((16u - (((uint32_t)ob + (uint32_t)c) & 15u)) & 15u);
-                            const u32x4 blk = realign16(acc[r], lane_next4(acc[r]), dl);
-                            const int32_t q = cpos + (int32_t)dl;
-                            if (lane < kWideStore && q >= kWideGuard && q <= hi) st16_addr(ob + (uint64_t)(int64_t)q, blk);
-                            acc[r] = u32x4{0, 0, 0, 0};
+#pragma unroll
+                            for (int u = 0; u < kWideU; ++u) {
+                                const u32x4 blk = realign16(acc[u][r], lane_next4(acc[u][r]), dl);
+                                const int32_t q = c + (int32_t)(u * kWideWin) + 16 * (int32_t)lane + (int32_t)dl;
+                                if (lane < kWideStore && q >= kWideGuard && q <= hi)
+                                    st16_addr(ob + (uint64_t)(int64_t)q, blk);
+                                acc[u][r] = u32x4{0, 0, 0, 0};
+                            }
                         }
                     }
                 } else if constexpr (!APPLY) {
                     // stored parity r0 = j - K against the recomputed column
                     const uint32_t r0 = j - K;
-                    const int32_t cpos = (int32_t)(cp.ti * kWideWin) + 16 * (int32_t)lane;
-                    const bool mine = lane < kWideStore && cpos + 16 <= main_end;
-                    u32x4 want = acc[0];
 #pragma unroll
-                    for (int r = 1; r < R; ++r)
-                        if (r0 == (uint32_t)r) want = acc[r];
-                    const u32x4 df = want ^ x;
-                    bad |= mine && (df[0] | df[1] | df[2] | df[3]) != 0u;
+                    for (int u = 0; u < kWideU; ++u) {
+                        const int32_t cpos = (int32_t)(cp.ti * kWideTile + u * kWideWin) + 16 * (int32_t)lane;
+                        const bool mine = lane < kWideStore && cpos + 16 <= main_end;
+                        u32x4 want = acc[u][0];
+#pragma unroll
+                        for (int r = 1; r < R; ++r)
+                            if (r0 == (uint32_t)r) want = acc[u][r];
+                        const u32x4 df = want ^ xs[u];
+                        bad |= mine && (df[0] | df[1] | df[2] | df[3]) != 0u;
+                    }
                     if (r0 == R - 1u) {
                         if (__any(bad) && lane == 0u) atomicOr(flags + cp.obj, 1u);
                         bad = false;
 #pragma unroll
-                        for (int r = 0; r < R; ++r) acc[r] = u32x4{0, 0, 0, 0};
+                        for (int u = 0; u < kWideU; ++u)
+#pragma unroll
+                            for (int r = 0; r < R; ++r) acc[u][r] = u32x4{0, 0, 0, 0};
                     }
                 }
                 if (++cp.j == L) wide_set(cp, cp.t + nw, tpo);
@@ -314,7 +336,7 @@ static hipError_t launch_apply_wide_r(const WideArgs& a, int grid, hipStream_t s
 }
 
 uint32_t wide_tab_words(int r) { return wide_tab_stride(r); }
-uint32_t wide_tile_bytes() { return kWideWin; }
+uint32_t wide_tile_bytes() { return kWideTile; }
 uint64_t wide_main_len(uint64_t shard_len) { return wide_main_bytes(shard_len); }
 
 hipError_t launch_verify_wide(int r, const WideArgs& a, uint32_t* flags, int grid, hipStream_t stream) {
@@ -333,7 +355,7 @@ hipError_t launch_verify_wide(int r, const WideArgs& a, uint32_t* flags, int gri
 }
 
 uint32_t wide_apply_tiles_per_obj(uint64_t shard_len) {
-    return shard_len > (uint64_t)kWideEdgeSlots ? (uint32_t)((shard_len + 32 + kWideWin - 1) / kWideWin) : 0u;
+    return shard_len > (uint64_t)kWideEdgeSlots ? (uint32_t)((shard_len + 32 + kWideTile - 1) / kWideTile) : 0u;
 }
 
 hipError_t launch_apply_wide(int r, const WideArgs& a, int grid, hipStream_t stream) {

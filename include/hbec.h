@@ -285,8 +285,11 @@ int hbec_reconstruct_host_devices(hbec_codec* codec, const hbec_stripe* stripes,
  * Every stripe must fit one staging slot (k * shard_len <= HBEC_HOST_SLOT_MB).
  * When every stripe is pinned and device-mapped (hbec_host_alloc), the stripes
  * are coded in place over PCIe and the kernel copies their shards to a device
- * hash arena as it goes (no staging copy, nothing read twice over PCIe);
- * HBEC_MD5_ZEROCOPY=0 sends them through the ring instead.  Otherwise the
+ * hash arena as it goes (no staging copy, nothing read twice over PCIe) — at
+ * any alignment and shard length (the mirrored gf_odd plan kernel when a
+ * stripe is not 16-B aligned or S % 16 != 0; k > 12: the outputs are read
+ * back once after the last pass); HBEC_MD5_ZEROCOPY=0 sends them through the
+ * ring instead.  Otherwise the
  * whole batch takes the staging ring.  hbec_host_md5_stats: calls since load
  * that took each way. */
 int hbec_encode_host_md5(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n_stripes, uint8_t* digests);

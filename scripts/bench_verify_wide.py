@@ -41,14 +41,14 @@ def main():
     for _ in range(100):
         x.add_(1)
     del x
-    for k, m, L in [(10, 4, 1 << 20), (10, 4, 10 * 104864), (12, 4, 1 << 20), (16, 4, 1 << 20), (20, 4, 1 << 20),
-                    (20, 4, 20 * 52432), (32, 8, 1 << 20), (32, 8, (1 << 20) - 5)]:
+    for k, m, L in [(10, 4, 1 << 20), (10, 4, 10 * 104864), (12, 4, 1 << 20), (16, 4, 1 << 20), (17, 3, 1 << 20),
+                    (20, 4, 1 << 20), (20, 4, 20 * 52432), (32, 8, 1 << 20), (32, 8, 32 * 32767)]:
         s = -(-L // k)
         enc = RS.New(k, m)
         rows = torch.empty((n, (k + m) * s), dtype=torch.uint8, device="cuda")
         B.fill_splitmix(rows, (k + m) * s)
         views = B.shard_views(rows, k + m, s)
-        B.encode_views(enc, views, n, s)
+        ems = t(lambda: B.encode_views(enc, views, n, s))  # k > 8 at odd offsets: gf_wide apply (HBEC_WIDE_APPLY)
         flags = torch.zeros(n, dtype=torch.int32, device="cuda")
         ms = t(lambda: B.verify_views(enc, views, n, s, flags))
         flags.zero_()
@@ -62,6 +62,8 @@ def main():
         exact = flags.nonzero().flatten().tolist() == [n // 3]
         nb = n * (k + m) * s
         print(json.dumps({"k": k, "m": m, "S": s, "n": n, "wide": os.environ.get("HBEC_WIDE_VERIFY", "1"),
+                          "wide_apply": os.environ.get("HBEC_WIDE_APPLY", "1"),
+                          "encode_ms": round(ems, 4), "encode_frac": round(nb / (ems * 1e-3) / 8e12, 4),
                           "verify_ms": round(ms, 4), "frac": round(nb / (ms * 1e-3) / 8e12, 4),
                           "clean_ok": clean, "flip_exact": exact}), flush=True)
         del rows, views

@@ -61,6 +61,7 @@ def main():
 
     res = {"source": [str(fetch_dir), str(write_dir)],
            "kernel_sources_sha256": bench.kernel_sources_sha256(),
+           "odd_sources_sha256": bench.kernel_sources_sha256(bench.ODD_SOURCES),
            "corrections": "read = 2 x FETCH_SIZE x 1024 (gfx950 half-count on wide streaming reads); "
                           "write = WRITE_SIZE x 1024",
            "kernels": kernels}

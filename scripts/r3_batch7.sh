@@ -8,5 +8,5 @@ timeout -k 10 500 python -u -m pytest tests/test_gpu_unaligned.py tests/test_gpu
 rc=$?; tail -3 $OUT/r3b7_tests.log; [ $rc -eq 0 ] || exit $rc
 HBEC_LIB=tune_build/odd_maxk12/libhbec.so timeout -k 10 300 python -u -m pytest tests/test_gpu_unaligned.py -x -q --tb=short --timeout 120 --timeout-method thread -p no:cacheprovider > $OUT/r3b7_tests_maxk12.log 2>&1
 rc=$?; tail -3 $OUT/r3b7_tests_maxk12.log; [ $rc -eq 0 ] || exit $rc
-bash scripts/tune_odd_env.sh $OUT/r3b7_tune.jsonl base maxk12 aload4 wd8 || exit $?
+bash scripts/tune_odd_env.sh $OUT/r3b7_tune.jsonl base maxk12 aload4 wd8 wu2 || exit $?
 echo done

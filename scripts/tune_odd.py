@@ -34,6 +34,7 @@ VARIANTS = {
     "aedge": ["HBEC_ODD_ALOAD=1", "HBEC_ODD_EDGE_PLAIN=1"],
     "aload4": ["HBEC_ODD_ALOAD=2"],
     "wd8": ["HBEC_WIDE_D=8"],
+    "wu2": ["HBEC_WIDE_U=2"],
 }
 
 MiB = 1 << 20
