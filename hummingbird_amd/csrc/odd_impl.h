@@ -46,12 +46,6 @@ constexpr uint64_t kOddMinMain = (uint64_t)kOddEdgeSlots;
 #ifndef HBEC_ODD_ALOAD
 #define HBEC_ODD_ALOAD 0  // 16-B-aligned input loads shifted by realign16: 1 for every K, 2 for K <= 4 (0: dword-aligned loads, 1 DPP)
 #endif
-#ifndef HBEC_ODD_EDGE_PLAIN
-#define HBEC_ODD_EDGE_PLAIN 0  // 1: blocks in a 128-B line shared with the next / previous window: plain (L2) stores
-#endif
-#ifndef HBEC_ODD_NT_ST
-#define HBEC_ODD_NT_ST 1  // 0: plain stores for every output block
-#endif
 #ifndef HBEC_ODD_PLAN_U
 #define HBEC_ODD_PLAN_U 2  // windows per plan record (2: odd 4+2 stripe plan 52.9 -> 59.5 %, r03b4)
 #endif
@@ -254,18 +248,11 @@ __device__ __forceinline__ void odd_load(OddRegs<K, R, U, MODE>& X, const OddTil
     }
 }
 
-// output block store: non-temporal, or (HBEC_ODD_EDGE_PLAIN) plain for blocks
-// whose 128-B line the neighbouring window writes too, so L2 merges the halves
-__device__ __forceinline__ void odd_st(uint64_t addr, const u32x4& v, uint64_t win0, bool mine) {
-    if constexpr (HBEC_ODD_EDGE_PLAIN) {
-        const bool edge = (addr & ~(uint64_t)127) < win0 || (addr | 127u) >= win0 + kOddWin;
-        if (mine && edge) *reinterpret_cast<gu32x4*>(addr) = v;
-        if (mine && !edge) st16_addr(addr, v);
-    } else if constexpr (HBEC_ODD_NT_ST) {
-        if (mine) st16_addr(addr, v);
-    } else {
-        if (mine) *reinterpret_cast<gu32x4*>(addr) = v;
-    }
+// output block store (non-temporal).  Measured and rejected (r03_tune_odd4):
+// plain stores for blocks whose 128-B line the neighbouring window also
+// writes (-1.5..-9 %), plain stores everywhere (-1..-12 %).
+__device__ __forceinline__ void odd_st(uint64_t addr, const u32x4& v, bool mine) {
+    if (mine) st16_addr(addr, v);
 }
 
 template <int K, int R, int U, int MODE, bool MIR = false>
@@ -335,8 +322,7 @@ __device__ __forceinline__ void odd_finish(const OddRegs<K, R, U, MODE>& X, cons
                 const int32_t q = cpos + (int32_t)dl[r];  // block start: out[r] + q is 16-B aligned
                 const bool mine = b.live != 0u && lane < kOddStore && q >= kOddGuard && q <= hi;
                 if constexpr (MODE == kOddAcc) blk ^= X.x[u][K + r];  // the old block (odd_load)
-                const uint64_t win0 = b.out[r] + (uint64_t)(int64_t)(b.c + (int32_t)(u * kOddWin) + (int32_t)dl[r]);
-                odd_st(b.out[r] + (uint64_t)(int64_t)q, blk, win0, mine);
+                odd_st(b.out[r] + (uint64_t)(int64_t)q, blk, mine);
             }
         }
     }

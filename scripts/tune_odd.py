@@ -27,11 +27,10 @@ VARIANTS = {
     "sleep": ["HBEC_ODD_SLEEP=6"],
     # round 3, second set
     "aload": ["HBEC_ODD_ALOAD=1"],
-    "edge": ["HBEC_ODD_EDGE_PLAIN=1"],
-    "ntst0": ["HBEC_ODD_NT_ST=0"],
+    # "edge" (HBEC_ODD_EDGE_PLAIN=1) and "ntst0" (HBEC_ODD_NT_ST=0): measured in
+    # profiles/r03_tune_odd4.jsonl, rejected, code removed
     "planu2": ["HBEC_ODD_PLAN_U=2"],
     "maxk12": ["HBEC_ODD_MAXK=12"],
-    "aedge": ["HBEC_ODD_ALOAD=1", "HBEC_ODD_EDGE_PLAIN=1"],
     "aload4": ["HBEC_ODD_ALOAD=2"],
     "wd8": ["HBEC_WIDE_D=8"],
     "wu2": ["HBEC_WIDE_U=2"],

@@ -46,13 +46,14 @@ def test_pinned_host_alloc_failure_is_nomem_and_recovers():
 
 
 def test_device_oom_is_nomem_and_next_call_succeeds():
-    """Verify with more than 16 data shards over unaligned views needs an
-    n*m*S scratch buffer in HBM (hbec.cpp verify_views, generic path).  With
-    HBM nearly full that allocation fails: ErrNoMem, no flag set, while a
-    4+2 unaligned Verify (gf_verify_unaligned, no scratch) still succeeds.
-    With the memory back, the same call and an aligned pipelined encode both
-    succeed."""
-    k, m, n, s = 17, 2, 512, (1 << 20) + 1  # k > 16, odd shard length: generic path, 1 GiB scratch
+    """A stripe plan's tile records live in HBM (hbec_plan_stripes, one 32-B
+    record per tile).  With HBM nearly full, a plan whose records need 1 GiB
+    fails with ErrNoMem and allocates nothing, while an unaligned 4+2 Verify
+    (gf_odd, no scratch) and a k = 17 Verify (gf_verify_wide, no scratch since
+    round 3) still succeed.  With the memory back, the same plan is made, and
+    an aligned pipelined encode succeeds (the launch check sees no stale
+    error from the failed allocation)."""
+    k, m, n, s = 17, 2, 64, (1 << 16) + 1  # k > 16, odd shard length: gf_verify_wide
     enc = RS.New(k, m)
     e42, s42 = RS.New(4, 2), 1001
     small = torch.empty((8, 6 * s42 + 3), dtype=torch.uint8, device="cuda")
@@ -68,10 +69,13 @@ def test_device_oom_is_nomem_and_next_call_succeeds():
     B.encode_views(enc, views, n, s)
     flags = torch.zeros(n, dtype=torch.int32, device="cuda")
     torch.cuda.synchronize()
+    # 512 aligned 4+2 stripes of 64 MiB shards: 32 Mi tile records = 1 GiB in
+    # HBM (the plan only records addresses; it is never run)
+    big = [(small.data_ptr() - (small.data_ptr() % 256), 64 << 20)] * 512
 
     free, _ = torch.cuda.mem_get_info()
     hog = None
-    for slack in (256 << 20, 512 << 20, 1 << 30):  # leave less than the 1 GiB scratch
+    for slack in (256 << 20, 512 << 20, 768 << 20):  # leave less than the plan's 1 GiB
         try:
             hog = torch.empty(free - slack, dtype=torch.uint8, device="cuda")
             break
@@ -80,16 +84,19 @@ def test_device_oom_is_nomem_and_next_call_succeeds():
     assert hog is not None, "could not fill HBM for the test"
     try:
         with pytest.raises(RS.ErrNoMem):
-            B.verify_views(enc, views, n, s, flags)
+            B.StripePlan(e42, big)
+        assert "hipMalloc plan tiles" in N.last_error()
         B.verify_views(e42, v42, 8, s42, f42)
+        B.verify_views(enc, views, n, s, flags)
         torch.cuda.synchronize()
-        assert int(f42.count_nonzero()) == 0
+        assert int(f42.count_nonzero()) == 0 and int(flags.count_nonzero()) == 0
     finally:
         del hog
         torch.cuda.empty_cache()
-    assert int(flags.count_nonzero()) == 0
 
-    B.verify_views(enc, views, n, s, flags)  # the same call, memory back
+    plan = B.StripePlan(e42, big)  # the same call, memory back
+    del plan
+    B.verify_views(enc, views, n, s, flags)
     torch.cuda.synchronize()
     assert int(flags.count_nonzero()) == 0
     a = torch.empty((64, 4 << 18), dtype=torch.uint8, device="cuda")
