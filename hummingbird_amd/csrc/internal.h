@@ -94,6 +94,6 @@ struct URec;
 int launch_unaligned_passes(const URec* recs, uint64_t n_recs, const std::vector<int>& in_idx,
                             const std::vector<int>& out_idx, const std::vector<uint8_t>& rows, int sel_k,
                             hipStream_t stream, int max_blocks = 0, const URec* erecs = nullptr,
-                            uint64_t n_erecs = 0, bool mirror = false);
+                            uint64_t n_erecs = 0, bool mirror = false, bool round2 = false);
 
 }  // namespace hbec

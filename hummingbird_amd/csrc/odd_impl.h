@@ -46,6 +46,9 @@ constexpr uint64_t kOddMinMain = (uint64_t)kOddEdgeSlots;
 #ifndef HBEC_ODD_ALOAD
 #define HBEC_ODD_ALOAD 0  // 16-B-aligned input loads shifted by realign16: 1 for every K, 2 for K <= 4 (0: dword-aligned loads, 1 DPP)
 #endif
+#ifndef HBEC_ODD_LDSTAB
+#define HBEC_ODD_LDSTAB 0  // 1: K > 8 read the coefficient tables from LDS per input (fewer VGPRs, more waves)
+#endif
 #ifndef HBEC_ODD_PLAN_U
 #define HBEC_ODD_PLAN_U 2  // windows per plan record (2: odd 4+2 stripe plan 52.9 -> 59.5 %, r03b4)
 #endif
@@ -127,6 +130,11 @@ __device__ __forceinline__ u32x4 odd_shift_in(const u32x4& v, uint32_t sh) {
 }
 
 typedef __attribute__((address_space(1))) uint8_t gu8_t;
+
+// K > 8 with HBEC_ODD_LDSTAB: coefficient tables in LDS (words per input, 16-B padded)
+template <int K>
+__host__ __device__ constexpr bool odd_lds_tables() { return HBEC_ODD_LDSTAB != 0 && K > 8; }
+__host__ __device__ constexpr uint32_t odd_lt_stride(int r) { return (uint32_t)((r * 5 + 3) & ~3); }
 
 // ---- tile sources ----
 // A source names tile t compactly (id(): a few scalars, carried one and two
@@ -258,7 +266,7 @@ __device__ __forceinline__ void odd_st(uint64_t addr, const u32x4& v, bool mine)
 template <int K, int R, int U, int MODE, bool MIR = false>
 __device__ __forceinline__ void odd_finish(const OddRegs<K, R, U, MODE>& X, const OddTile<K, R>& b,
                                            const TabArray& tab, const Tables<K, R, HBEC_ODD_VMIN>& tb, uint32_t lane,
-                                           uint32_t* flags, uint32_t mir = 0) {
+                                           uint32_t* flags, uint32_t mir = 0, const uint32_t* lt = nullptr) {
     constexpr int NL = OddRegs<K, R, U, MODE>::NL;
     uint32_t sh[K + (MODE == kOddVerify ? R : 0)];
 #pragma unroll
@@ -283,7 +291,31 @@ __device__ __forceinline__ void odd_finish(const OddRegs<K, R, U, MODE>& X, cons
         u32x4 acc[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) acc[r] = u32x4{0, 0, 0, 0};
-        gf_dot<K, R, HBEC_ODD_VMIN>(acc, x, tab, tb);
+        if constexpr (odd_lds_tables<K>()) {
+            // tables of input j: R x 5 words at lt + j * odd_lt_stride(R), broadcast LDS reads
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                const u32x4* tp = reinterpret_cast<const u32x4*>(lt + j * odd_lt_stride(R));
+                uint32_t tw[(R * 5 + 3) & ~3];
+#pragma unroll
+                for (int q = 0; q < (R * 5 + 3) / 4; ++q) {
+                    const u32x4 v = tp[q];
+                    tw[4 * q] = v[0];
+                    tw[4 * q + 1] = v[1];
+                    tw[4 * q + 2] = v[2];
+                    tw[4 * q + 3] = v[3];
+                }
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const Sel sx = selectors(x[j][e]);
+#pragma unroll
+                    for (int r = 0; r < R; ++r)
+                        acc[r][e] ^= gf_mul_sel(sx, tw[5 * r], tw[5 * r + 1], tw[5 * r + 2], tw[5 * r + 3], tw[5 * r + 4]);
+                }
+            }
+        } else {
+            gf_dot<K, R, HBEC_ODD_VMIN>(acc, x, tab, tb);
+        }
         if constexpr (MIR && MODE != kOddVerify) {
             // mirror: every arena slot is 16-B aligned, so column i's arena
             // block starts at qm = cpos + dm, dm = -c mod 16; same guard band
@@ -343,6 +375,16 @@ __device__ __forceinline__ void odd_body(const Src& src, uint32_t n, const TabAr
     const uint32_t dw = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (wave0 >= n) return;  // whole blocks only: the loop below has block barriers
     const Tables<K, R, HBEC_ODD_VMIN> tb = load_tables<K, R, HBEC_ODD_VMIN>(tab);
+    __shared__ __attribute__((aligned(16))) uint32_t lt[odd_lds_tables<K>() ? K * odd_lt_stride(R) : 4];
+    if constexpr (odd_lds_tables<K>()) {
+        // whole blocks reach this point (the early return above is per block)
+        const uint32_t ts = odd_lt_stride(R);
+        for (uint32_t i = threadIdx.x; i < (uint32_t)K * ts; i += blockDim.x) {
+            const uint32_t j = i / ts, w = i - j * ts;
+            lt[i] = w < (uint32_t)(R * 5) ? tab[w / 5][j][w % 5] : 0u;
+        }
+        __syncthreads();
+    }
     typename Src::Id cur = src.id(wave0 + dw, n);
     OddRegs<K, R, U, MODE> X;
     {
@@ -364,7 +406,7 @@ __device__ __forceinline__ void odd_body(const Src& src, uint32_t n, const TabAr
         {
             OddTile<K, R> b;
             src.at(b, cur);
-            odd_finish<K, R, U, MODE, MIR>(X, b, tab, tb, lane, flags, mir);
+            odd_finish<K, R, U, MODE, MIR>(X, b, tab, tb, lane, flags, mir, lt);
         }
         X = Y;
         cur = nxt;
@@ -372,7 +414,7 @@ __device__ __forceinline__ void odd_body(const Src& src, uint32_t n, const TabAr
     }
     OddTile<K, R> b;
     src.at(b, cur);
-    odd_finish<K, R, U, MODE, MIR>(X, b, tab, tb, lane, flags, mir);
+    odd_finish<K, R, U, MODE, MIR>(X, b, tab, tb, lane, flags, mir, lt);
 }
 
 template <int K, int R, int MODE>

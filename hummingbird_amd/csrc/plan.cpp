@@ -41,6 +41,10 @@ struct hbec_plan {
     // gf_odd: one edge record per such stripe / object (its guard-band bytes)
     hbec::URec* d_erecs = nullptr;
     uint64_t n_erecs = 0;
+    // shards of 2^31 bytes or more (gf_odd positions are 32-bit), or all of
+    // them with HBEC_ODD=0: round-2 gf_apply_unaligned_plan records
+    hbec::URec* d_brecs = nullptr;
+    uint64_t n_brecs = 0;
 };
 
 namespace {
@@ -57,12 +61,17 @@ bool aligned_object(const hbec_object& o) {
 
 std::mutex g_occ_mu;
 
-void add_urecs(std::vector<hbec::URec>& recs, std::vector<hbec::URec>& erecs, const void* a, const void* b,
-               uint64_t s) {
+void add_urecs(std::vector<hbec::URec>& recs, std::vector<hbec::URec>& erecs, std::vector<hbec::URec>& brecs,
+               const void* a, const void* b, uint64_t s) {
+    const uint64_t ua = reinterpret_cast<uint64_t>(a), ub = reinterpret_cast<uint64_t>(b);
+    if (!hbec::odd_enabled() || s >= (1ull << 31)) {
+        const uint64_t tile = (uint64_t)hbec::unaligned_tile_bytes();
+        for (uint64_t p0 = 0; p0 < s; p0 += tile) brecs.push_back({ua, ub, s, p0});
+        return;
+    }
     const uint64_t tile = hbec::urec_tile(), span = hbec::urec_span(s);
-    for (uint64_t p0 = 0; p0 < span; p0 += tile)
-        recs.push_back({reinterpret_cast<uint64_t>(a), reinterpret_cast<uint64_t>(b), s, p0});
-    if (hbec::odd_enabled()) erecs.push_back({reinterpret_cast<uint64_t>(a), reinterpret_cast<uint64_t>(b), s, 0});
+    for (uint64_t p0 = 0; p0 < span; p0 += tile) recs.push_back({ua, ub, s, p0});
+    erecs.push_back({ua, ub, s, 0});
 }
 
 template <class T>
@@ -87,18 +96,18 @@ int upload(const std::vector<T>& recs, T** dst, const char* what) {
 int hbec::launch_unaligned_passes(const URec* recs, uint64_t n_recs, const std::vector<int>& in_idx,
                                   const std::vector<int>& out_idx, const std::vector<uint8_t>& rows, int sel_k,
                                   hipStream_t stream, int max_blocks, const URec* erecs, uint64_t n_erecs,
-                                  bool mirror) {
+                                  bool mirror, bool round2) {
     const int K_all = (int)in_idx.size(), R_all = (int)out_idx.size();
     if ((n_recs == 0 && n_erecs == 0) || R_all == 0) return HBEC_OK;
-    if (mirror && (!hbec::odd_enabled() || sel_k > 0))
+    if (mirror && (!hbec::odd_enabled() || sel_k > 0 || round2))
         return fail(HBEC_ERR_INVALID_ARG, "mirrored unaligned plans need gf_odd and stripe records");
     int dev = 0, cus = 0, per_cu = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
     e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (e != hipSuccess) return hip_fail(e, "hipDeviceGetAttribute");
-    if (hbec::odd_enabled()) {
-        // gf_odd_plan: launches of <= 4 outputs x <= 8 inputs, later input
+    if (hbec::odd_enabled() && !round2) {
+        // gf_odd_plan: launches of <= 4 outputs x <= kOddMaxK inputs, later input
         // launches accumulating; one 4-wave block per CU
         for (int r0 = 0; r0 < R_all; r0 += hbec::kMaxR) {
             const int R = std::min(hbec::kMaxR, R_all - r0);
@@ -306,13 +315,13 @@ int run_plan(const hbec_plan* p, const std::vector<int>& in_idx, const std::vect
                                             stream);
         if (rc) return rc;
     }
-    if (p->objects) {
-        // with k > 8 every object is in the unaligned records (hbec_plan_objects)
-        return hbec::launch_unaligned_passes(p->d_urecs, p->n_urecs, in_idx, out_idx, rows, p->k, stream, 0,
-                                             p->d_erecs, p->n_erecs);
-    }
-    return hbec::launch_unaligned_passes(p->d_urecs, p->n_urecs, in_idx, out_idx, rows, 0, stream, 0, p->d_erecs,
-                                         p->n_erecs);
+    // with k > 8 every object is in the unaligned records (hbec_plan_objects)
+    const int sel_k = p->objects ? p->k : 0;
+    int rc = hbec::launch_unaligned_passes(p->d_urecs, p->n_urecs, in_idx, out_idx, rows, sel_k, stream, 0,
+                                           p->d_erecs, p->n_erecs);
+    if (rc || p->n_brecs == 0) return rc;
+    return hbec::launch_unaligned_passes(p->d_brecs, p->n_brecs, in_idx, out_idx, rows, sel_k, stream, 0, nullptr, 0,
+                                         false, true);
 }
 
 }  // namespace
@@ -330,7 +339,7 @@ int hbec_plan_stripes(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n,
         p->m = m;
         p->tile_bytes = hbec::stripes_tile_bytes(std::min(k, hbec::kStripeMaxK));
         std::vector<hbec::TileRec> recs;
-        std::vector<hbec::URec> urecs, erecs;
+        std::vector<hbec::URec> urecs, erecs, brecs;
         for (uint64_t i = 0; i < n; ++i) {
             const hbec_stripe& s = stripes[i];
             if (s.shard_len == 0) continue;
@@ -338,7 +347,7 @@ int hbec_plan_stripes(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n,
             p->shard_bytes += s.shard_len;
             if (!aligned_stripe(s)) {
                 p->fallback.push_back(s);
-                add_urecs(urecs, erecs, s.base, nullptr, s.shard_len);
+                add_urecs(urecs, erecs, brecs, s.base, nullptr, s.shard_len);
                 continue;
             }
             p->tiled.push_back(s);
@@ -352,7 +361,8 @@ int hbec_plan_stripes(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n,
             }
         }
         // both record counts are checked before anything is allocated on the device
-        if (recs.size() >= (1ull << 31) || urecs.size() >= (1ull << 31) || erecs.size() >= (1ull << 31))
+        if (recs.size() >= (1ull << 31) || urecs.size() >= (1ull << 31) || erecs.size() >= (1ull << 31) ||
+            brecs.size() >= (1ull << 31))
             return fail(HBEC_ERR_INVALID_ARG, "plan too large (>= 2^31 tiles)");
         p->n_tiles = recs.size();
         if (!recs.empty()) {
@@ -367,13 +377,16 @@ int hbec_plan_stripes(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n,
         }
         int urc = upload(urecs, &p->d_urecs, "plan unaligned records");
         if (!urc) urc = upload(erecs, &p->d_erecs, "plan edge records");
+        if (!urc) urc = upload(brecs, &p->d_brecs, "plan large-shard records");
         if (urc) {
             if (p->d_tiles) (void)hipFree(p->d_tiles);
             if (p->d_urecs) (void)hipFree(p->d_urecs);
+            if (p->d_erecs) (void)hipFree(p->d_erecs);
             return urc;
         }
         p->n_urecs = urecs.size();
         p->n_erecs = erecs.size();
+        p->n_brecs = brecs.size();
         *out = p.release();
         return HBEC_OK;
     });
@@ -391,7 +404,7 @@ int hbec_plan_objects(hbec_codec* codec, const hbec_object* objects, uint64_t n,
         p->objects = true;
         p->tile_bytes = hbec::stripes_tile_bytes(std::min(k, hbec::kStripeMaxK));
         std::vector<hbec::TileRec> recs;
-        std::vector<hbec::URec> urecs, erecs;
+        std::vector<hbec::URec> urecs, erecs, brecs;
         for (uint64_t i = 0; i < n; ++i) {
             const hbec_object& o = objects[i];
             if (o.shard_len == 0) continue;
@@ -399,13 +412,13 @@ int hbec_plan_objects(hbec_codec* codec, const hbec_object* objects, uint64_t n,
             p->shard_bytes += o.shard_len;
             if (!aligned_object(o)) {
                 p->obj_fallback.push_back(o);
-                add_urecs(urecs, erecs, o.data, o.parity, o.shard_len);
+                add_urecs(urecs, erecs, brecs, o.data, o.parity, o.shard_len);
                 continue;
             }
             if (k > hbec::kStripeMaxK) {
                 // the object-plan tiled kernel takes <= 8 inputs: every object goes to
                 // the unaligned kernel's records (one launch per pass, not one per object)
-                add_urecs(urecs, erecs, o.data, o.parity, o.shard_len);
+                add_urecs(urecs, erecs, brecs, o.data, o.parity, o.shard_len);
                 continue;
             }
             p->obj_tiled.push_back(o);
@@ -420,7 +433,8 @@ int hbec_plan_objects(hbec_codec* codec, const hbec_object* objects, uint64_t n,
             }
         }
         // both record counts are checked before anything is allocated on the device
-        if (recs.size() >= (1ull << 31) || urecs.size() >= (1ull << 31) || erecs.size() >= (1ull << 31))
+        if (recs.size() >= (1ull << 31) || urecs.size() >= (1ull << 31) || erecs.size() >= (1ull << 31) ||
+            brecs.size() >= (1ull << 31))
             return fail(HBEC_ERR_INVALID_ARG, "plan too large (>= 2^31 tiles)");
         p->n_tiles = recs.size();
         if (!recs.empty()) {
@@ -435,13 +449,16 @@ int hbec_plan_objects(hbec_codec* codec, const hbec_object* objects, uint64_t n,
         }
         int urc = upload(urecs, &p->d_urecs, "plan unaligned records");
         if (!urc) urc = upload(erecs, &p->d_erecs, "plan edge records");
+        if (!urc) urc = upload(brecs, &p->d_brecs, "plan large-shard records");
         if (urc) {
             if (p->d_tiles) (void)hipFree(p->d_tiles);
             if (p->d_urecs) (void)hipFree(p->d_urecs);
+            if (p->d_erecs) (void)hipFree(p->d_erecs);
             return urc;
         }
         p->n_urecs = urecs.size();
         p->n_erecs = erecs.size();
+        p->n_brecs = brecs.size();
         *out = p.release();
         return HBEC_OK;
     });
@@ -452,6 +469,7 @@ void hbec_plan_free(hbec_plan* plan) {
     if (plan->d_tiles) (void)hipFree(plan->d_tiles);
     if (plan->d_urecs) (void)hipFree(plan->d_urecs);
     if (plan->d_erecs) (void)hipFree(plan->d_erecs);
+    if (plan->d_brecs) (void)hipFree(plan->d_brecs);
     delete plan;
 }
 
