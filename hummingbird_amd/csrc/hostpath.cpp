@@ -780,7 +780,7 @@ int host_run_on(Ring* ring, const hbec_stripe* stripes, uint64_t n, const std::v
             const bool aligned = (reinterpret_cast<uintptr_t>(stripes[s].base) & 15u) == 0 && S % 16 == 0 &&
                                  S < (1ull << 32) && (d & 15u) == 0;
             if (d && aligned) zs.push_back({d, S});
-            else if (d && zero_copy_any_alignment() && S < (1ull << 31)) zu.push_back({d, S});  // gf_odd: 32-bit positions
+            else if (d && hbec::zero_copy_any_alignment() && S < (1ull << 31)) zu.push_back({d, S});  // gf_odd: 32-bit positions
             else staged.push_back(stripes[s]);
         }
         if (!zs.empty()) {

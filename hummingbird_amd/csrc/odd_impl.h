@@ -40,6 +40,9 @@ constexpr uint64_t kOddMinMain = (uint64_t)kOddEdgeSlots;
 #ifndef HBEC_ODD_U_SMALL
 #define HBEC_ODD_U_SMALL 2  // windows per wave tile for K <= 4 (0: 4 / K); 2: 4+2 62.5 -> 65 % (r03_tune_odd3)
 #endif
+#ifndef HBEC_ODD_U_MID
+#define HBEC_ODD_U_MID 1  // windows per wave tile for 5 <= K <= 8
+#endif
 #ifndef HBEC_ODD_U_VERIFY
 #define HBEC_ODD_U_VERIFY 0  // windows per wave tile of verify for K <= 4 (0: as apply)
 #endif
@@ -60,7 +63,7 @@ enum : int { kOddApply = 0, kOddAcc = 1, kOddVerify = 2 };
 __host__ __device__ constexpr int odd_u(int k, int mode = kOddApply) {
     return (mode == kOddVerify && HBEC_ODD_U_VERIFY > 0 && k <= 4)
                ? HBEC_ODD_U_VERIFY
-               : (k <= 4 ? (HBEC_ODD_U_SMALL > 0 ? HBEC_ODD_U_SMALL : (4 / k)) : 1);
+               : (k <= 4 ? (HBEC_ODD_U_SMALL > 0 ? HBEC_ODD_U_SMALL : (4 / k)) : (k <= 8 ? HBEC_ODD_U_MID : 1));
 }
 constexpr int kOddPlanU = HBEC_ODD_PLAN_U;  // plans: windows per record
 

@@ -34,6 +34,9 @@ VARIANTS = {
     "aload4": ["HBEC_ODD_ALOAD=2"],
     "wd8": ["HBEC_WIDE_D=8"],
     "wu2": ["HBEC_WIDE_U=2"],
+    "umid2": ["HBEC_ODD_U_MID=2"],
+    "umid3": ["HBEC_ODD_U_MID=3"],
+    "ldstab": ["HBEC_ODD_LDSTAB=1"],
 }
 
 MiB = 1 << 20
