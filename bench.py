@@ -404,7 +404,7 @@ def odd_objects(n=4096, obj_len=(1 << 20) - 4, reps=20, settle=40):
     databuf puts shard i at i*S (ecutils.go:31-35), so most objects reach the
     codec as shards at odd offsets.  n ecSplit databufs of 1 MiB - 4 B objects
     (4+2, S = 262 143), device-resident: Encode, Reconstruct of shards {0,1}
-    in place, Verify (gf_apply_unaligned / gf_verify_unaligned).  Rebuilt
+    in place, Verify (gf_odd<4, 2, 0> / gf_odd<4, 2, 2> + gf_odd_edges).  Rebuilt
     shards must equal the originals and Verify must pass every object."""
     k, m = 4, 2
     s = -(-obj_len // k)
