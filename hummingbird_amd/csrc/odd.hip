@@ -210,7 +210,7 @@ uint32_t odd_plan_tile_bytes() { return (uint32_t)kOddPlanU * kOddWin; }
 // the frame's first column (c0 >= -32) to position S.
 uint32_t odd_tiles_per_obj(int k, int mode, uint64_t shard_len) {
     const uint64_t span = shard_len + 32u;
-    const uint64_t tile = (uint64_t)odd_u(k, mode) * kOddWin;
+    const uint64_t tile = (uint64_t)odd_u(k, mode) * (mode == kOddVerify ? odd_win<kOddVerify>() : kOddWin);
     return (uint32_t)((span + tile - 1) / tile);
 }
 

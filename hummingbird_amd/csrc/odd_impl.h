@@ -17,6 +17,13 @@ namespace hbec {
 
 constexpr uint32_t kOddStore = 62;            // blocks stored per 64-lane window
 constexpr uint32_t kOddWin = kOddStore * 16;  // shard bytes per window (992)
+enum : int { kOddApply = 0, kOddAcc = 1, kOddVerify = 2 };
+// Verify stores nothing, so no output is realigned and lane 62's column is
+// compared too: 63 columns per window (1.6 % of the loads re-read, not 3.2 %)
+template <int MODE>
+__host__ __device__ constexpr uint32_t odd_store() { return MODE == kOddVerify ? 63u : kOddStore; }
+template <int MODE>
+__host__ __device__ constexpr uint32_t odd_win() { return odd_store<MODE>() * 16u; }
 constexpr int32_t kOddGuard = 48;             // bytes at each end left to gf_odd_edges
 constexpr int32_t kOddEdgeSlots = 160;        // edge bytes handled per (shard, output): 80 head + 80 tail
 // the main kernel runs on shards longer than this (shorter ones: gf_odd_edges only)
@@ -55,8 +62,6 @@ constexpr uint64_t kOddMinMain = (uint64_t)kOddEdgeSlots;
 #ifndef HBEC_ODD_PLAN_U
 #define HBEC_ODD_PLAN_U 2  // windows per plan record (2: odd 4+2 stripe plan 52.9 -> 59.5 %, r03b4)
 #endif
-
-enum : int { kOddApply = 0, kOddAcc = 1, kOddVerify = 2 };
 
 // windows per wave tile of the strided kernel: ~4 loads per lane in flight
 // for K <= 4 (as gf_apply_vec_pipe2's 1 KiB x 4 / K), one window above
@@ -148,7 +153,7 @@ struct OddIdS {
     uint32_t obj, ti, live;
 };
 
-template <int K, int R, int U>
+template <int K, int R, int U, int MODE>
 struct OddStrided {
     using Id = OddIdS;
     const PassArgs& a;
@@ -164,7 +169,7 @@ struct OddStrided {
 #pragma unroll
         for (int r = 0; r < R; ++r) b.out[r] = reinterpret_cast<uint64_t>(a.out[r]) + (uint64_t)i.obj * a.out_stride[r];
         b.S = (int32_t)a.shard_len;
-        b.c = odd_c0(b.out[0]) + (int32_t)(i.ti * (uint32_t)(U * kOddWin));
+        b.c = odd_c0(b.out[0]) + (int32_t)(i.ti * (uint32_t)(U * odd_win<MODE>()));
         b.live = i.live;
         b.obj = i.obj;
     }
@@ -239,7 +244,7 @@ __device__ __forceinline__ void odd_load(OddRegs<K, R, U, MODE>& X, const OddTil
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-        for (int j = 0; j < (MODE == kOddAcc ? K : NL); ++j) X.x[u][j] = odd_ld(src[j], (int32_t)(u * kOddStore + lane));
+        for (int j = 0; j < (MODE == kOddAcc ? K : NL); ++j) X.x[u][j] = odd_ld(src[j], (int32_t)(u * odd_store<MODE>() + lane));
     if constexpr (MODE == kOddAcc) {
         // the old output block each lane will rewrite: output r's aligned block
         // at q = column + dl_r; lanes that store nothing read one inside the band
@@ -287,7 +292,7 @@ __device__ __forceinline__ void odd_finish(const OddRegs<K, R, U, MODE>& X, cons
     for (int r = 0; r < R; ++r) dl[r] = __builtin_amdgcn_readfirstlane((16u - (((uint32_t)b.out[r] + (uint32_t)b.c) & 15u)) & 15u);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-        const int32_t cpos = b.c + (int32_t)(u * kOddWin) + 16 * (int32_t)lane;  // this lane's column
+        const int32_t cpos = b.c + (int32_t)(u * odd_win<MODE>()) + 16 * (int32_t)lane;  // this lane's column
         u32x4 x[K];
 #pragma unroll
         for (int j = 0; j < K; ++j) x[j] = odd_shift_in<odd_ld_align<K>()>(X.x[u][j], sh[j]);
@@ -343,7 +348,7 @@ __device__ __forceinline__ void odd_finish(const OddRegs<K, R, U, MODE>& X, cons
         }
         if constexpr (MODE == kOddVerify) {
             // frame columns = output 0's blocks: compare those inside the guard band
-            const bool mine = b.live != 0u && lane < kOddStore && cpos >= kOddGuard && cpos <= hi;
+            const bool mine = b.live != 0u && lane < odd_store<MODE>() && cpos >= kOddGuard && cpos <= hi;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const u32x4 df = odd_shift_in<odd_ld_align<K>()>(X.x[u][K + r], sh[K + r]) ^ acc[r];
@@ -423,7 +428,7 @@ __device__ __forceinline__ void odd_body(const Src& src, uint32_t n, const TabAr
 template <int K, int R, int MODE>
 __global__ __launch_bounds__(kPipeBlockThreads, HBEC_ODD_LB) void gf_odd(PassArgs a, uint32_t* flags) {
     constexpr int U = odd_u(K, MODE);
-    odd_body<K, R, U, MODE>(OddStrided<K, R, U>{a}, a.n_tiles, a.tab, flags);
+    odd_body<K, R, U, MODE>(OddStrided<K, R, U, MODE>{a}, a.n_tiles, a.tab, flags);
 }
 
 template <int K, int R, int MODE, bool MIR = false>

@@ -34,6 +34,8 @@ VARIANTS = {
     "aload4": ["HBEC_ODD_ALOAD=2"],
     "wd8": ["HBEC_WIDE_D=8"],
     "wu2": ["HBEC_WIDE_U=2"],
+    "wu1d8": ["HBEC_WIDE_U=1", "HBEC_WIDE_D=8"],
+    "wd8u2": ["HBEC_WIDE_D=8"],
     "umid2": ["HBEC_ODD_U_MID=2"],
     "umid3": ["HBEC_ODD_U_MID=3"],
     "ldstab": ["HBEC_ODD_LDSTAB=1"],
