@@ -202,7 +202,7 @@ uint64_t urec_span(uint64_t shard_len) {
     return shard_len > kOddMinMain ? shard_len + 32u : 0u;
 }
 
-uint32_t odd_tile_bytes(int k) { return (uint32_t)odd_u(k) * kOddWin; }
+uint32_t odd_tile_bytes(int k) { return odd_u(k) == 2 && HBEC_ODD_CARRY ? (64u + kOddStore) * 16u : (uint32_t)odd_u(k) * kOddWin; }
 uint64_t odd_min_main() { return kOddMinMain; }
 uint32_t odd_plan_tile_bytes() { return (uint32_t)kOddPlanU * kOddWin; }
 
@@ -210,7 +210,9 @@ uint32_t odd_plan_tile_bytes() { return (uint32_t)kOddPlanU * kOddWin; }
 // the frame's first column (c0 >= -32) to position S.
 uint32_t odd_tiles_per_obj(int k, int mode, uint64_t shard_len) {
     const uint64_t span = shard_len + 32u;
-    const uint64_t tile = (uint64_t)odd_u(k, mode) * (mode == kOddVerify ? odd_win<kOddVerify>() : kOddWin);
+    const uint64_t tile = mode == kOddVerify ? (uint64_t)odd_u(k, mode) * odd_win<kOddVerify>()
+                                             : (odd_u(k, mode) == 2 && HBEC_ODD_CARRY ? (uint64_t)(64 + kOddStore) * 16u
+                                                                                       : (uint64_t)odd_u(k, mode) * kOddWin);
     return (uint32_t)((span + tile - 1) / tile);
 }
 

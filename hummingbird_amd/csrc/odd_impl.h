@@ -15,6 +15,9 @@
 
 namespace hbec {
 
+#ifndef HBEC_ODD_CARRY
+#define HBEC_ODD_CARRY 0  // strided apply, 2 windows per wave tile: window 0 takes window 1's first column (126 of 128 stored)
+#endif
 constexpr uint32_t kOddStore = 62;            // blocks stored per 64-lane window
 constexpr uint32_t kOddWin = kOddStore * 16;  // shard bytes per window (992)
 enum : int { kOddApply = 0, kOddAcc = 1, kOddVerify = 2 };
@@ -24,6 +27,18 @@ template <int MODE>
 __host__ __device__ constexpr uint32_t odd_store() { return MODE == kOddVerify ? 63u : kOddStore; }
 template <int MODE>
 __host__ __device__ constexpr uint32_t odd_win() { return odd_store<MODE>() * 16u; }
+// Carry (HBEC_ODD_CARRY, strided apply with 2 windows per wave tile): the
+// windows are contiguous (columns 0..63 and 64..127 of the tile); window 0
+// gets its lane 63's missing next column from window 1's lane 0 (a readlane
+// + DPP with that value as the out-of-range fill) and stores 64 blocks,
+// window 1 stores 62: 126 of 128 loaded columns instead of 124.
+template <int U, int MODE>
+__host__ __device__ constexpr bool odd_carry() { return HBEC_ODD_CARRY != 0 && U == 2 && MODE != kOddVerify; }
+// first column of window u within a tile, and shard bytes per tile
+template <int U, int MODE, bool CARRY>
+__host__ __device__ constexpr uint32_t odd_wcol(int u) { return CARRY ? 64u * (uint32_t)u : odd_store<MODE>() * (uint32_t)u; }
+template <int U, int MODE, bool CARRY>
+__host__ __device__ constexpr uint32_t odd_tile_span() { return CARRY ? (64u + kOddStore) * 16u : U * odd_win<MODE>(); }
 constexpr int32_t kOddGuard = 48;             // bytes at each end left to gf_odd_edges
 constexpr int32_t kOddEdgeSlots = 160;        // edge bytes handled per (shard, output): 80 head + 80 tail
 // the main kernel runs on shards longer than this (shorter ones: gf_odd_edges only)
@@ -137,6 +152,31 @@ __device__ __forceinline__ u32x4 odd_shift_in(const u32x4& v, uint32_t sh) {
                  __builtin_amdgcn_alignbyte(v[3], v[2], sh), __builtin_amdgcn_alignbyte(n0, v[3], sh)};
 }
 
+// the same with lane 63's missing neighbour supplied (carry: the first dword
+// / block of the next window, wave-uniform): DPP wave_shl:1 without bound
+// control keeps `fill` in lane 63
+__device__ __forceinline__ uint32_t lane_next_fill(uint32_t v, uint32_t fill) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)v, 0x130, 0xF, 0xF, false);
+}
+
+__device__ __forceinline__ u32x4 lane_next4_fill(const u32x4& v, const u32x4& fill) {
+    return u32x4{lane_next_fill(v[0], fill[0]), lane_next_fill(v[1], fill[1]), lane_next_fill(v[2], fill[2]),
+                 lane_next_fill(v[3], fill[3])};
+}
+
+__device__ __forceinline__ u32x4 lane0(const u32x4& v) {
+    return u32x4{(uint32_t)__builtin_amdgcn_readlane((int)v[0], 0), (uint32_t)__builtin_amdgcn_readlane((int)v[1], 0),
+                 (uint32_t)__builtin_amdgcn_readlane((int)v[2], 0), (uint32_t)__builtin_amdgcn_readlane((int)v[3], 0)};
+}
+
+template <uint32_t A>
+__device__ __forceinline__ u32x4 odd_shift_in_fill(const u32x4& v, uint32_t sh, const u32x4& next0) {
+    if constexpr (A == 16u) return realign16(v, lane_next4_fill(v, next0), sh);
+    const uint32_t n0 = lane_next_fill(v[0], next0[0]);
+    return u32x4{__builtin_amdgcn_alignbyte(v[1], v[0], sh), __builtin_amdgcn_alignbyte(v[2], v[1], sh),
+                 __builtin_amdgcn_alignbyte(v[3], v[2], sh), __builtin_amdgcn_alignbyte(n0, v[3], sh)};
+}
+
 typedef __attribute__((address_space(1))) uint8_t gu8_t;
 
 // K > 8 with HBEC_ODD_LDSTAB: coefficient tables in LDS (words per input, 16-B padded)
@@ -156,6 +196,7 @@ struct OddIdS {
 template <int K, int R, int U, int MODE>
 struct OddStrided {
     using Id = OddIdS;
+    static constexpr bool kCarry = odd_carry<U, MODE>();
     const PassArgs& a;
     __device__ __forceinline__ Id id(uint32_t t, uint32_t n) const {
         const uint32_t tt = t < n ? t : n - 1u;
@@ -169,7 +210,7 @@ struct OddStrided {
 #pragma unroll
         for (int r = 0; r < R; ++r) b.out[r] = reinterpret_cast<uint64_t>(a.out[r]) + (uint64_t)i.obj * a.out_stride[r];
         b.S = (int32_t)a.shard_len;
-        b.c = odd_c0(b.out[0]) + (int32_t)(i.ti * (uint32_t)(U * odd_win<MODE>()));
+        b.c = odd_c0(b.out[0]) + (int32_t)(i.ti * odd_tile_span<U, MODE, kCarry>());
         b.live = i.live;
         b.obj = i.obj;
     }
@@ -193,6 +234,7 @@ __host__ __device__ constexpr int odd_plan_u(int) {
 template <int K, int R, bool MIR = false>
 struct OddPlan {
     using Id = OddIdP;
+    static constexpr bool kCarry = false;
     static constexpr uint32_t SUB = (uint32_t)(kOddPlanU / odd_plan_u<K>(0));
     const UPlanArgs& p;
     const URec* __restrict__ recs;
@@ -231,7 +273,7 @@ struct OddRegs {
     u32x4 x[U][NL];
 };
 
-template <int K, int R, int U, int MODE>
+template <int K, int R, int U, int MODE, bool CARRY = false>
 __device__ __forceinline__ void odd_load(OddRegs<K, R, U, MODE>& X, const OddTile<K, R>& b, uint32_t lane) {
     constexpr int NL = OddRegs<K, R, U, MODE>::NL;
     OddIn src[NL];
@@ -244,7 +286,8 @@ __device__ __forceinline__ void odd_load(OddRegs<K, R, U, MODE>& X, const OddTil
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-        for (int j = 0; j < (MODE == kOddAcc ? K : NL); ++j) X.x[u][j] = odd_ld(src[j], (int32_t)(u * odd_store<MODE>() + lane));
+        for (int j = 0; j < (MODE == kOddAcc ? K : NL); ++j)
+            X.x[u][j] = odd_ld(src[j], (int32_t)(odd_wcol<U, MODE, CARRY>(u) + lane));
     if constexpr (MODE == kOddAcc) {
         // the old output block each lane will rewrite: output r's aligned block
         // at q = column + dl_r; lanes that store nothing read one inside the band
@@ -256,7 +299,7 @@ __device__ __forceinline__ void odd_load(OddRegs<K, R, U, MODE>& X, const OddTil
             const int32_t qmin = kOddGuard + e, qmax = hi - ((hi - e) & 15);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const int32_t q = b.c + (int32_t)(u * kOddWin) + 16 * (int32_t)lane + (int32_t)dl;
+                const int32_t q = b.c + (int32_t)(16u * odd_wcol<U, MODE, CARRY>(u)) + 16 * (int32_t)lane + (int32_t)dl;
                 const int32_t qc = q < qmin ? qmin : (q > qmax ? qmax : q);
                 X.x[u][K + r] = ld16_addr(b.out[r] + (uint64_t)(int64_t)qc);
             }
@@ -271,7 +314,7 @@ __device__ __forceinline__ void odd_st(uint64_t addr, const u32x4& v, bool mine)
     if (mine) st16_addr(addr, v);
 }
 
-template <int K, int R, int U, int MODE, bool MIR = false>
+template <int K, int R, int U, int MODE, bool MIR = false, bool CARRY = false>
 __device__ __forceinline__ void odd_finish(const OddRegs<K, R, U, MODE>& X, const OddTile<K, R>& b,
                                            const TabArray& tab, const Tables<K, R, HBEC_ODD_VMIN>& tb, uint32_t lane,
                                            uint32_t* flags, uint32_t mir = 0, const uint32_t* lt = nullptr) {
@@ -290,6 +333,39 @@ __device__ __forceinline__ void odd_finish(const OddRegs<K, R, U, MODE>& X, cons
     uint32_t dl[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) dl[r] = __builtin_amdgcn_readfirstlane((16u - (((uint32_t)b.out[r] + (uint32_t)b.c) & 15u)) & 15u);
+    if constexpr (CARRY) {
+        static_assert(U == 2 && MODE != kOddVerify && !MIR, "carry: strided apply / accumulate, 2 windows");
+        // window 1 first: its lane 0 feeds window 0's lane 63
+        u32x4 x1[K], x0[K], acc1[R], acc0[R];
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            x1[j] = odd_shift_in<odd_ld_align<K>()>(X.x[1][j], sh[j]);
+            x0[j] = odd_shift_in_fill<odd_ld_align<K>()>(X.x[0][j], sh[j], lane0(X.x[1][j]));
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc1[r] = acc0[r] = u32x4{0, 0, 0, 0};
+        gf_dot<K, R, HBEC_ODD_VMIN>(acc1, x1, tab, tb);
+        gf_dot<K, R, HBEC_ODD_VMIN>(acc0, x0, tab, tb);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            u32x4 b0 = acc0[r], b1 = acc1[r];
+            if (dl[r] != 0u) {  // wave-uniform (never r = 0)
+                b0 = realign16(acc0[r], lane_next4_fill(acc0[r], lane0(acc1[r])), dl[r]);
+                b1 = realign16(acc1[r], lane_next4(acc1[r]), dl[r]);
+            }
+            const int32_t q0 = b.c + 16 * (int32_t)lane + (int32_t)dl[r];
+            const int32_t q1 = q0 + 1024;
+            const bool m0 = b.live != 0u && q0 >= kOddGuard && q0 <= hi;                      // all 64 lanes
+            const bool m1 = b.live != 0u && lane < kOddStore && q1 >= kOddGuard && q1 <= hi;  // 62
+            if constexpr (MODE == kOddAcc) {
+                b0 ^= X.x[0][K + r];
+                b1 ^= X.x[1][K + r];
+            }
+            odd_st(b.out[r] + (uint64_t)(int64_t)q0, b0, m0);
+            odd_st(b.out[r] + (uint64_t)(int64_t)q1, b1, m1);
+        }
+        return;
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const int32_t cpos = b.c + (int32_t)(u * odd_win<MODE>()) + 16 * (int32_t)lane;  // this lane's column
@@ -398,7 +474,7 @@ __device__ __forceinline__ void odd_body(const Src& src, uint32_t n, const TabAr
     {
         OddTile<K, R> b;
         src.at(b, cur);
-        odd_load<K, R, U, MODE>(X, b, lane);
+        odd_load<K, R, U, MODE, Src::kCarry>(X, b, lane);
     }
     typename Src::Id nxt = src.id(wave0 + dw + nw, n);
     for (uint32_t b0 = wave0 + nw; b0 < n; b0 += nw) {  // block-uniform trip count
@@ -406,7 +482,7 @@ __device__ __forceinline__ void odd_body(const Src& src, uint32_t n, const TabAr
         {
             OddTile<K, R> b;
             src.at(b, nxt);
-            odd_load<K, R, U, MODE>(Y, b, lane);
+            odd_load<K, R, U, MODE, Src::kCarry>(Y, b, lane);
         }
         if (HBEC_ODD_SLEEP > 0) __builtin_amdgcn_s_sleep(HBEC_ODD_SLEEP);
         if (MODE == kOddVerify ? HBEC_ODD_VBARRIER : HBEC_ODD_BARRIER) __builtin_amdgcn_s_barrier();
@@ -414,7 +490,7 @@ __device__ __forceinline__ void odd_body(const Src& src, uint32_t n, const TabAr
         {
             OddTile<K, R> b;
             src.at(b, cur);
-            odd_finish<K, R, U, MODE, MIR>(X, b, tab, tb, lane, flags, mir, lt);
+            odd_finish<K, R, U, MODE, MIR, Src::kCarry>(X, b, tab, tb, lane, flags, mir, lt);
         }
         X = Y;
         cur = nxt;
@@ -422,7 +498,7 @@ __device__ __forceinline__ void odd_body(const Src& src, uint32_t n, const TabAr
     }
     OddTile<K, R> b;
     src.at(b, cur);
-    odd_finish<K, R, U, MODE, MIR>(X, b, tab, tb, lane, flags, mir, lt);
+    odd_finish<K, R, U, MODE, MIR, Src::kCarry>(X, b, tab, tb, lane, flags, mir, lt);
 }
 
 template <int K, int R, int MODE>

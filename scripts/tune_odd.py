@@ -36,6 +36,7 @@ VARIANTS = {
     "wu2": ["HBEC_WIDE_U=2"],
     "wu1d8": ["HBEC_WIDE_U=1", "HBEC_WIDE_D=8"],
     "wd8u2": ["HBEC_WIDE_D=8"],
+    "carry": ["HBEC_ODD_CARRY=1"],
     "umid2": ["HBEC_ODD_U_MID=2"],
     "umid3": ["HBEC_ODD_U_MID=3"],
     "ldstab": ["HBEC_ODD_LDSTAB=1"],
