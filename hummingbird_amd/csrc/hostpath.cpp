@@ -494,7 +494,7 @@ int zero_copy_run(Ring* ring, const std::vector<ZcStripe>& zs, const std::vector
 int zero_copy_unaligned_run(Ring* ring, const std::vector<ZcStripe>& zs, const std::vector<int>& in_idx,
                             const std::vector<int>& out_idx, const std::vector<uint8_t>& rows) {
     static_assert(sizeof(hbec::URec) == sizeof(hbec::TileRec), "record slots are shared");
-    const uint64_t tile = hbec::urec_tile();
+    const uint64_t tile = hbec::urec_tile_for(std::min((int)in_idx.size(), hbec::kOddMaxK), false);
     size_t si = 0;
     uint64_t off = 0;
     hipError_t e = hipSuccess;
@@ -614,7 +614,7 @@ int zero_copy_unaligned_md5_run(Ring* ring, const std::vector<ZcStripe>& zs, con
     const int K = (int)in_idx.size(), R = (int)out_idx.size();
     int rc = ring_md5_init(*ring);
     if (rc) return rc;
-    const uint64_t tile = hbec::urec_tile();
+    const uint64_t tile = hbec::urec_tile_for(std::min(K, hbec::kOddMaxK), true);
     ArenaCursor ac{ring, ring->s_cmp, d_digest};
     hipError_t e = hipSuccess;
     size_t si = 0;

@@ -125,6 +125,9 @@ struct UPlanArgs {
     // column, bit 1 every output column (single input pass only) to the hash
     // arena at rec.b (shard i at rec.b + i * odd_mirror_pitch_host(S))
     uint32_t mirror;
+    // gf_odd plans: 1 when the records are carried 2-window tiles
+    // (urec_tile_for(k, false) == 2016 B, K <= 4 passes)
+    uint32_t carry;
 };
 uint32_t unaligned_tile_bytes();
 // Verify at any alignment (k <= kMaxK, <= 4 parity rows per launch): OR 1 into
@@ -151,6 +154,7 @@ bool odd_supported(int k, int r);
 // Unaligned plan records (URec) of one stripe / object: p0 = 0, tile, 2*tile,
 // ... while p0 < urec_span(S), for whichever kernel family codes them.
 uint64_t urec_tile();
+uint64_t urec_tile_for(int k, bool mirror);  // records read by a k-input pass (gf_odd carry for k <= 4)
 uint64_t urec_span(uint64_t shard_len);  // 0: no main-kernel records (gf_odd: S <= odd_min_main())
 uint32_t odd_tile_bytes(int k);       // shard bytes per wave tile of the strided kernel
 uint32_t odd_plan_tile_bytes();       // shard bytes per plan record

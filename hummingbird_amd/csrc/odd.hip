@@ -165,8 +165,8 @@ __global__ __launch_bounds__(kBlockThreads) void gf_odd_edges_plan(UPlanArgs p, 
     }
 }
 
-static const void* odd_kernel(int k, int r, int mode, bool plan, bool mirror = false) {
-    if (k <= 4) return odd_kernel_range<1, 4>(k, r, mode, plan, mirror);
+static const void* odd_kernel(int k, int r, int mode, bool plan, bool mirror = false, bool carry = false) {
+    if (k <= 4) return odd_kernel_range<1, 4>(k, r, mode, plan, mirror, carry);
     if (k <= 8) return odd_kernel_k58(k, r, mode, plan, mirror);
     return odd_kernel_k912(k, r, mode, plan, mirror);
 }
@@ -197,6 +197,15 @@ int odd_blocks_per_cu(int mode) {
 }
 
 uint64_t urec_tile() { return odd_enabled() ? (uint64_t)kOddPlanU * kOddWin : (uint64_t)unaligned_tile_bytes(); }
+// Record tile of a plan / zero-copy batch coded with k inputs per pass (the
+// gf_odd_plan instance that reads the records): K <= 4 plain kernels take a
+// record as one carried 2-window tile (2016 B), the others as 2 x 992 B
+// windows (mirrored, or K > 4 one window per wave tile).
+uint64_t urec_tile_for(int k, bool mirror) {
+    if (!odd_enabled()) return (uint64_t)unaligned_tile_bytes();
+    if (HBEC_ODD_CARRY && !mirror && k <= 4 && kOddPlanU == 2) return (uint64_t)(64 + kOddStore) * 16u;
+    return (uint64_t)kOddPlanU * kOddWin;
+}
 uint64_t urec_span(uint64_t shard_len) {
     if (!odd_enabled()) return shard_len;
     return shard_len > kOddMinMain ? shard_len + 32u : 0u;
@@ -247,7 +256,7 @@ hipError_t launch_odd_edges_plan(int k, int r, int mode, const UPlanArgs& p, con
 }
 
 hipError_t launch_odd_plan(int k, int r, int mode, const UPlanArgs& p, int grid, hipStream_t stream) {
-    const void* fn = odd_kernel(k, r, mode, true, p.mirror != 0);
+    const void* fn = odd_kernel(k, r, mode, true, p.mirror != 0, p.carry != 0);
     if (!fn) return hipErrorInvalidValue;
     const URec* recs = p.recs;
     void* args[] = {const_cast<UPlanArgs*>(&p), &recs};

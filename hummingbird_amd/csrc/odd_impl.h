@@ -16,7 +16,7 @@
 namespace hbec {
 
 #ifndef HBEC_ODD_CARRY
-#define HBEC_ODD_CARRY 0  // strided apply, 2 windows per wave tile: window 0 takes window 1's first column (126 of 128 stored)
+#define HBEC_ODD_CARRY 1  // 2-window apply tiles: window 0 takes window 1's first column, 126 of 128 stored (odd 4+2 65 -> 70 %, r03_tune_carry)
 #endif
 constexpr uint32_t kOddStore = 62;            // blocks stored per 64-lane window
 constexpr uint32_t kOddWin = kOddStore * 16;  // shard bytes per window (992)
@@ -231,10 +231,13 @@ __host__ __device__ constexpr int odd_plan_u(int) {
     return K <= 4 ? kOddPlanU : 1;  // K > 4: 2 windows of K inputs spill (10+4 object plan 42 -> 31 %, r3b7)
 }
 
-template <int K, int R, bool MIR = false>
+template <int K, int R, bool MIR = false, bool CARRY = false>
 struct OddPlan {
     using Id = OddIdP;
-    static constexpr bool kCarry = false;
+    // CARRY: the records hold one carried 2-window tile each (2016 B,
+    // urec_tile_for); otherwise 2 x 992 B windows
+    static constexpr bool kCarry = CARRY;
+    static_assert(!CARRY || (!MIR && odd_plan_u<K>(0) == 2), "carried plan records: K <= 4, not mirrored");
     static constexpr uint32_t SUB = (uint32_t)(kOddPlanU / odd_plan_u<K>(0));
     const UPlanArgs& p;
     const URec* __restrict__ recs;
@@ -507,9 +510,9 @@ __global__ __launch_bounds__(kPipeBlockThreads, HBEC_ODD_LB) void gf_odd(PassArg
     odd_body<K, R, U, MODE>(OddStrided<K, R, U, MODE>{a}, a.n_tiles, a.tab, flags);
 }
 
-template <int K, int R, int MODE, bool MIR = false>
+template <int K, int R, int MODE, bool MIR = false, bool CARRY = false>
 __global__ __launch_bounds__(kPipeBlockThreads, HBEC_ODD_LB) void gf_odd_plan(UPlanArgs p, const URec* __restrict__ recs) {
-    using Src = OddPlan<K, R, MIR>;
+    using Src = OddPlan<K, R, MIR, CARRY>;
     odd_body<K, R, odd_plan_u<K>(0), MODE, Src, MIR>(Src{p, recs}, p.n_recs * Src::SUB, p.tab, nullptr, p.mirror);
 }
 
@@ -517,43 +520,46 @@ __global__ __launch_bounds__(kPipeBlockThreads, HBEC_ODD_LB) void gf_odd_plan(UP
 // launch table: kernel of (K, r, mode, plan?, mirrored?)
 // ---------------------------------------------------------------------------
 template <int K, int R, int MODE>
-static const void* odd_pick(bool plan, bool mirror) {
+static const void* odd_pick(bool plan, bool mirror, bool carry) {
     if (!plan) return (const void*)&gf_odd<K, R, MODE>;
     if constexpr (MODE != kOddVerify) {  // plans never verify
         if (mirror) return (const void*)&gf_odd_plan<K, R, MODE, true>;
+        if constexpr (HBEC_ODD_CARRY != 0 && odd_plan_u<K>(0) == 2) {
+            if (carry) return (const void*)&gf_odd_plan<K, R, MODE, false, true>;
+        }
         return (const void*)&gf_odd_plan<K, R, MODE>;
     }
     return nullptr;
 }
 
 template <int K, int MODE>
-static const void* odd_for_r(int r, bool plan, bool mirror) {
+static const void* odd_for_r(int r, bool plan, bool mirror, bool carry) {
     switch (r) {
-        case 1: return odd_pick<K, 1, MODE>(plan, mirror);
-        case 2: return odd_pick<K, 2, MODE>(plan, mirror);
-        case 3: return odd_pick<K, 3, MODE>(plan, mirror);
-        case 4: return odd_pick<K, 4, MODE>(plan, mirror);
+        case 1: return odd_pick<K, 1, MODE>(plan, mirror, carry);
+        case 2: return odd_pick<K, 2, MODE>(plan, mirror, carry);
+        case 3: return odd_pick<K, 3, MODE>(plan, mirror, carry);
+        case 4: return odd_pick<K, 4, MODE>(plan, mirror, carry);
     }
     return nullptr;
 }
 
 template <int K>
-static const void* odd_kernel_k(int r, int mode, bool plan, bool mirror) {
+static const void* odd_kernel_k(int r, int mode, bool plan, bool mirror, bool carry) {
     switch (mode) {
-        case kOddApply: return odd_for_r<K, kOddApply>(r, plan, mirror);
-        case kOddAcc: return odd_for_r<K, kOddAcc>(r, plan, mirror);
-        case kOddVerify: return plan ? nullptr : odd_for_r<K, kOddVerify>(r, false, false);
+        case kOddApply: return odd_for_r<K, kOddApply>(r, plan, mirror, carry);
+        case kOddAcc: return odd_for_r<K, kOddAcc>(r, plan, mirror, carry);
+        case kOddVerify: return plan ? nullptr : odd_for_r<K, kOddVerify>(r, false, false, false);
     }
     return nullptr;
 }
 
 template <int K0, int K1>
-static const void* odd_kernel_range(int k, int r, int mode, bool plan, bool mirror) {
+static const void* odd_kernel_range(int k, int r, int mode, bool plan, bool mirror, bool carry = false) {
     if constexpr (K0 > K1) {
         return nullptr;
     } else {
-        if (k == K0) return odd_kernel_k<K0>(r, mode, plan, mirror);
-        return odd_kernel_range<K0 + 1, K1>(k, r, mode, plan, mirror);
+        if (k == K0) return odd_kernel_k<K0>(r, mode, plan, mirror, carry);
+        return odd_kernel_range<K0 + 1, K1>(k, r, mode, plan, mirror, carry);
     }
 }
 

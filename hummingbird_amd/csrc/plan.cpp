@@ -62,14 +62,14 @@ bool aligned_object(const hbec_object& o) {
 std::mutex g_occ_mu;
 
 void add_urecs(std::vector<hbec::URec>& recs, std::vector<hbec::URec>& erecs, std::vector<hbec::URec>& brecs,
-               const void* a, const void* b, uint64_t s) {
+               const void* a, const void* b, uint64_t s, int k) {
     const uint64_t ua = reinterpret_cast<uint64_t>(a), ub = reinterpret_cast<uint64_t>(b);
     if (!hbec::odd_enabled() || s >= (1ull << 31)) {
         const uint64_t tile = (uint64_t)hbec::unaligned_tile_bytes();
         for (uint64_t p0 = 0; p0 < s; p0 += tile) brecs.push_back({ua, ub, s, p0});
         return;
     }
-    const uint64_t tile = hbec::urec_tile(), span = hbec::urec_span(s);
+    const uint64_t tile = hbec::urec_tile_for(std::min(k, hbec::kOddMaxK), false), span = hbec::urec_span(s);
     for (uint64_t p0 = 0; p0 < span; p0 += tile) recs.push_back({ua, ub, s, p0});
     erecs.push_back({ua, ub, s, 0});
 }
@@ -121,6 +121,10 @@ int hbec::launch_unaligned_passes(const URec* recs, uint64_t n_recs, const std::
                 // mirror: each pass's inputs once (first output group), the
                 // outputs when one input pass makes them final
                 if (mirror) a.mirror = (r0 == 0 ? 1u : 0u) | (K_all <= hbec::kOddMaxK ? 2u : 0u);
+                // records built as carried tiles (K_all <= 4, not mirrored) take the carry kernel
+                a.carry = (!mirror && K <= 4 &&
+                           hbec::urec_tile_for(std::min(K_all, hbec::kOddMaxK), false) != hbec::urec_tile_for(K, true))
+                              ? 1u : 0u;
                 for (int j = 0; j < K; ++j) {
                     int i = in_idx[c0 + j];
                     if (sel_k > 0 && i >= sel_k) {
@@ -347,7 +351,7 @@ int hbec_plan_stripes(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n,
             p->shard_bytes += s.shard_len;
             if (!aligned_stripe(s)) {
                 p->fallback.push_back(s);
-                add_urecs(urecs, erecs, brecs, s.base, nullptr, s.shard_len);
+                add_urecs(urecs, erecs, brecs, s.base, nullptr, s.shard_len, k);
                 continue;
             }
             p->tiled.push_back(s);
@@ -412,13 +416,13 @@ int hbec_plan_objects(hbec_codec* codec, const hbec_object* objects, uint64_t n,
             p->shard_bytes += o.shard_len;
             if (!aligned_object(o)) {
                 p->obj_fallback.push_back(o);
-                add_urecs(urecs, erecs, brecs, o.data, o.parity, o.shard_len);
+                add_urecs(urecs, erecs, brecs, o.data, o.parity, o.shard_len, k);
                 continue;
             }
             if (k > hbec::kStripeMaxK) {
                 // the object-plan tiled kernel takes <= 8 inputs: every object goes to
                 // the unaligned kernel's records (one launch per pass, not one per object)
-                add_urecs(urecs, erecs, brecs, o.data, o.parity, o.shard_len);
+                add_urecs(urecs, erecs, brecs, o.data, o.parity, o.shard_len, k);
                 continue;
             }
             p->obj_tiled.push_back(o);
