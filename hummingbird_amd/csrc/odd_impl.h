@@ -219,7 +219,10 @@ struct OddStrided {
 // Plan records (URec): input j of the record's stripe at (bit j of in_sel ?
 // b : a) + in_idx[j] * S; rec.p0 = the record's first window * 992.
 struct OddIdP {
-    URec rec;
+    // the record's fields as scalars: holding the URec itself let the compiler
+    // index {a, b} by the in_sel bit and put the ids in LDS (r3 ISA check)
+    uint64_t a, b;
+    uint32_t S, p0;  // S < 2^31 on this path (larger shards take the brecs kernel)
     uint32_t live;
     uint32_t sub;  // wave tile within the record (SUB > 1)
 };
@@ -243,26 +246,29 @@ struct OddPlan {
     const URec* __restrict__ recs;
     __device__ __forceinline__ Id id(uint32_t t, uint32_t n) const {
         const uint32_t tt = t < n ? t : n - 1u;
-        return Id{recs[tt / SUB], t < n ? 1u : 0u, tt % SUB};
+        const URec& r = recs[tt / SUB];
+        return Id{r.a, r.b, (uint32_t)r.shard_len, (uint32_t)r.p0, t < n ? 1u : 0u, tt % SUB};
     }
     __device__ __forceinline__ void at(OddTile<K, R>& b, const Id& i) const {
-        const uint64_t S = i.rec.shard_len;
+        const uint64_t S = i.S;
+        const uint64_t d = i.b - i.a;  // base = a + (sel bit ? b - a : 0), no select between fields
 #pragma unroll
-        for (int j = 0; j < K; ++j) b.in[j] = (((p.in_sel >> j) & 1u) ? i.rec.b : i.rec.a) + (uint64_t)p.in_idx[j] * S;
+        for (int j = 0; j < K; ++j)
+            b.in[j] = i.a + (d & (0ull - (uint64_t)((p.in_sel >> j) & 1u))) + (uint64_t)p.in_idx[j] * S;
 #pragma unroll
         for (int r = 0; r < R; ++r)
-            b.out[r] = (((p.out_sel >> r) & 1u) ? i.rec.b : i.rec.a) + (uint64_t)p.out_idx[r] * S;
+            b.out[r] = i.a + (d & (0ull - (uint64_t)((p.out_sel >> r) & 1u))) + (uint64_t)p.out_idx[r] * S;
         b.S = (int32_t)S;
-        b.c = odd_c0(b.out[0]) + (int32_t)i.rec.p0 + (int32_t)(i.sub * (uint32_t)odd_plan_u<K>(0) * kOddWin);
+        b.c = odd_c0(b.out[0]) + (int32_t)i.p0 + (int32_t)(i.sub * (uint32_t)odd_plan_u<K>(0) * kOddWin);
         b.live = i.live;
         b.obj = 0;
         if constexpr (MIR) {
             // rec.b = the stripe's arena (inputs and outputs are all at rec.a)
             const uint64_t P = odd_mirror_pitch(S);
 #pragma unroll
-            for (int j = 0; j < K; ++j) b.m_in[j] = i.rec.b + (uint64_t)p.in_idx[j] * P;
+            for (int j = 0; j < K; ++j) b.m_in[j] = i.b + (uint64_t)p.in_idx[j] * P;
 #pragma unroll
-            for (int r = 0; r < R; ++r) b.m_out[r] = i.rec.b + (uint64_t)p.out_idx[r] * P;
+            for (int r = 0; r < R; ++r) b.m_out[r] = i.b + (uint64_t)p.out_idx[r] * P;
         }
     }
 };

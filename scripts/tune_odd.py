@@ -118,11 +118,11 @@ def run(label, rnd=0, n=2048):
     # and k > 8 object plans (data arena + parity arena)
     import numpy as np
 
-    for k, m in [(4, 2), (8, 3), (10, 4)]:
+    for k, m, uniform in [(4, 2, False), (4, 2, True), (8, 3, False), (10, 4, False)]:
         rng = np.random.default_rng(k * 100 + m)
         layout, off = [], 0
         for _ in range(n):
-            s = -(-((1 << 20) - int(rng.integers(1, 16))) // k)
+            s = -(-((1 << 20) - (4 if uniform else int(rng.integers(1, 16)))) // k)
             layout.append((off, s))
             off += (k + m) * s
         pool = torch.empty((1, off), dtype=torch.uint8, device="cuda")
@@ -136,7 +136,8 @@ def run(label, rnd=0, n=2048):
             v = [(pool.data_ptr() + o + j * s, 0) for j in range(k + m)]
             B.verify_views(enc, v, 1, s, flags[i:i + 1])
         torch.cuda.synchronize()
-        print(json.dumps({"variant": label, "round": rnd, "k": k, "m": m, "layout": "stripe plan odd",
+        print(json.dumps({"variant": label, "round": rnd, "k": k, "m": m,
+                          "layout": "stripe plan odd" + (" uniform S" if uniform else ""),
                           "encode": round(nb / (ms * 1e-3) / 8e12, 4),
                           "ok": int(flags.count_nonzero().item()) == 0}), flush=True)
         del pool, plan
