@@ -163,7 +163,6 @@ static int odd_launches(const PassArgs& a, int K, int R, int mode, bool accumula
     int cus = 0;
     int rc = cu_count(dev, &cus);
     if (rc) return rc;
-    cus *= odd_blocks_per_cu(mode == 2 ? 2 : 0);
     if (shard_len > odd_min_main()) {
         for (int c1 = 0; c1 < K; c1 += kOddMaxK) {
             const int K1 = std::min(kOddMaxK, K - c1);
@@ -187,7 +186,8 @@ static int odd_launches(const PassArgs& a, int K, int R, int mode, bool accumula
                 c.tiles_per_obj = (uint32_t)tpo;
                 c.n_tiles = (uint32_t)(no * tpo);
                 const uint64_t want = (c.n_tiles + 3) / 4;
-                int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cus));
+                const uint64_t cap = (uint64_t)cus * (uint64_t)odd_blocks_per_cu(m, K1, R);
+                int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, cap));
                 if (g_grid_cap > 0) grid = std::min(grid, g_grid_cap);
                 hipError_t e = launch_odd(K1, R, m, c, flags ? flags + o0 : nullptr, grid, stream);
                 if (e != hipSuccess) return hip_fail(e, "launch gf_odd");

@@ -149,7 +149,8 @@ constexpr int kOddMaxK = HBEC_ODD_MAXK;
 // family) for odd shards (default: HBEC_ODD_DEFAULT).
 bool odd_enabled();
 // 4-wave blocks per CU of the gf_odd grids for a mode (HBEC_ODD_BPC overrides)
-int odd_blocks_per_cu(int mode);
+// 4-wave blocks per CU of a gf_odd launch (mode 0 apply, 1 accumulate, 2 verify; K, R of the pass)
+int odd_blocks_per_cu(int mode, int k, int r, bool mirror = false);
 bool odd_supported(int k, int r);
 // Unaligned plan records (URec) of one stripe / object: p0 = 0, tile, 2*tile,
 // ... while p0 < urec_span(S), for whichever kernel family codes them.

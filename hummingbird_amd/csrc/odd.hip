@@ -188,12 +188,14 @@ bool odd_enabled() {
 #ifndef HBEC_ODD_BPC_VERIFY
 #define HBEC_ODD_BPC_VERIFY 2  // read-only: 4+2 68.5 -> 81 % with 2 blocks per CU (r03_tune_odd3)
 #endif
-int odd_blocks_per_cu(int mode) {
+int odd_blocks_per_cu(int mode, int k, int r, bool mirror) {
     static const int v = [] {
         const char* e = std::getenv("HBEC_ODD_BPC");
         return e ? std::atoi(e) : 0;
     }();
-    return v > 0 ? v : (mode == kOddVerify ? HBEC_ODD_BPC_VERIFY : HBEC_ODD_BPC_APPLY);
+    if (v > 0) return v;
+    if (mode == kOddVerify) return HBEC_ODD_BPC_VERIFY;
+    return odd_two_blocks(k, r, mode, mirror) ? 2 : HBEC_ODD_BPC_APPLY;  // launch bounds sized for it (odd_lb)
 }
 
 uint64_t urec_tile() { return odd_enabled() ? (uint64_t)kOddPlanU * kOddWin : (uint64_t)unaligned_tile_bytes(); }

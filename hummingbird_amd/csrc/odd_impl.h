@@ -184,6 +184,39 @@ template <int K>
 __host__ __device__ constexpr bool odd_lds_tables() { return HBEC_ODD_LDSTAB != 0 && K > 8; }
 __host__ __device__ constexpr uint32_t odd_lt_stride(int r) { return (uint32_t)((r * 5 + 3) & ~3); }
 
+// Pinned outputs (HBEC_ODD_PIN, default on): every output column is
+// materialised right after the field multiply (an empty asm that reads and
+// writes it).  Without it the compiler sinks each output row's products into
+// that row's store branch, r outer and j inner, keeping every input's
+// selectors live across the stores (8+3 275 VGPRs, 10+4 392; pinned 201 and
+// 267).  Measured per shape (profiles/r03_tune_pin.jsonl) and kept where it
+// pays: Verify 5 <= K <= 8 (2 blocks per CU then hold 2 waves per SIMD: 8+3
+// 67.7 -> 71.4 %), and plain apply passes with K <= 10 and K * R >= 36 (10+4
+// encode) together with launch bounds for 2 blocks per CU and a grid of 2
+// blocks per CU (odd_two_blocks): 10+4 encode 50.0 -> 53.9 %, plans 42.5 ->
+// 50.9 %.  Apply with fewer products (8+3, 6+3, reconstructs) lost 4-8 %
+// pinned, and 12+4 spills.
+#ifndef HBEC_ODD_PIN
+#define HBEC_ODD_PIN 1
+#endif
+__host__ __device__ constexpr bool odd_two_blocks(int k, int r, int mode, bool mir) {
+    return HBEC_ODD_PIN != 0 && !mir && mode == kOddApply && k <= 10 && k * r >= 36;
+}
+template <int K, int R, int MODE, bool MIR>
+__host__ __device__ constexpr bool odd_pin_on() {
+    return HBEC_ODD_PIN != 0 && !MIR && ((MODE == kOddVerify && K >= 5 && K <= 8) || odd_two_blocks(K, R, MODE, MIR));
+}
+template <int K, int R, int MODE, bool MIR>
+__device__ __forceinline__ void odd_pin(u32x4 (&acc)[R]) {
+    if constexpr (odd_pin_on<K, R, MODE, MIR>()) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) asm volatile("" : "+v"(acc[r]));
+    }
+}
+
+template <int K, int R, int MODE, bool MIR = false>
+__host__ __device__ constexpr int odd_lb() { return odd_two_blocks(K, R, MODE, MIR) ? 2 : HBEC_ODD_LB; }
+
 // ---- tile sources ----
 // A source names tile t compactly (id(): a few scalars, carried one and two
 // tiles ahead) and expands it to shard bases where they are used (at()), so
@@ -355,6 +388,8 @@ __device__ __forceinline__ void odd_finish(const OddRegs<K, R, U, MODE>& X, cons
         for (int r = 0; r < R; ++r) acc1[r] = acc0[r] = u32x4{0, 0, 0, 0};
         gf_dot<K, R, HBEC_ODD_VMIN>(acc1, x1, tab, tb);
         gf_dot<K, R, HBEC_ODD_VMIN>(acc0, x0, tab, tb);
+        odd_pin<K, R, MODE, MIR>(acc1);
+        odd_pin<K, R, MODE, MIR>(acc0);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             u32x4 b0 = acc0[r], b1 = acc1[r];
@@ -388,7 +423,12 @@ __device__ __forceinline__ void odd_finish(const OddRegs<K, R, U, MODE>& X, cons
             // tables of input j: R x 5 words at lt + j * odd_lt_stride(R), broadcast LDS reads
 #pragma unroll
             for (int j = 0; j < K; ++j) {
-                const u32x4* tp = reinterpret_cast<const u32x4*>(lt + j * odd_lt_stride(R));
+                uint32_t z = 0;
+                // LDSTAB 2: an opaque offset per input keeps each input's table
+                // reads inside the tile (hoisted out of the loop they sit in
+                // VGPRs again, 200 of them at 10+4)
+                if constexpr (HBEC_ODD_LDSTAB >= 2) asm volatile("" : "+v"(z)::"memory");
+                const u32x4* tp = reinterpret_cast<const u32x4*>(lt + z + j * odd_lt_stride(R));
                 uint32_t tw[(R * 5 + 3) & ~3];
 #pragma unroll
                 for (int q = 0; q < (R * 5 + 3) / 4; ++q) {
@@ -409,6 +449,7 @@ __device__ __forceinline__ void odd_finish(const OddRegs<K, R, U, MODE>& X, cons
         } else {
             gf_dot<K, R, HBEC_ODD_VMIN>(acc, x, tab, tb);
         }
+        odd_pin<K, R, MODE, MIR>(acc);
         if constexpr (MIR && MODE != kOddVerify) {
             // mirror: every arena slot is 16-B aligned, so column i's arena
             // block starts at qm = cpos + dm, dm = -c mod 16; same guard band
@@ -511,13 +552,13 @@ __device__ __forceinline__ void odd_body(const Src& src, uint32_t n, const TabAr
 }
 
 template <int K, int R, int MODE>
-__global__ __launch_bounds__(kPipeBlockThreads, HBEC_ODD_LB) void gf_odd(PassArgs a, uint32_t* flags) {
+__global__ __launch_bounds__(kPipeBlockThreads, (odd_lb<K, R, MODE>())) void gf_odd(PassArgs a, uint32_t* flags) {
     constexpr int U = odd_u(K, MODE);
     odd_body<K, R, U, MODE>(OddStrided<K, R, U, MODE>{a}, a.n_tiles, a.tab, flags);
 }
 
 template <int K, int R, int MODE, bool MIR = false, bool CARRY = false>
-__global__ __launch_bounds__(kPipeBlockThreads, HBEC_ODD_LB) void gf_odd_plan(UPlanArgs p, const URec* __restrict__ recs) {
+__global__ __launch_bounds__(kPipeBlockThreads, (odd_lb<K, R, MODE, MIR>())) void gf_odd_plan(UPlanArgs p, const URec* __restrict__ recs) {
     using Src = OddPlan<K, R, MIR, CARRY>;
     odd_body<K, R, odd_plan_u<K>(0), MODE, Src, MIR>(Src{p, recs}, p.n_recs * Src::SUB, p.tab, nullptr, p.mirror);
 }

@@ -144,7 +144,7 @@ int hbec::launch_unaligned_passes(const URec* recs, uint64_t n_recs, const std::
                         hbec::perm_table(rows[(size_t)(r0 + r) * K_all + c0 + j], a.tab[r][j]);
                 }
                 const uint64_t want = (n_recs + 3) / 4;  // 4 waves per block
-                uint64_t cap = (uint64_t)cus * (uint64_t)hbec::odd_blocks_per_cu(0);
+                uint64_t cap = (uint64_t)cus * (uint64_t)hbec::odd_blocks_per_cu(c0 > 0 ? 1 : 0, K, R, mirror);
                 if (max_blocks > 0) cap = std::min<uint64_t>(cap, (uint64_t)max_blocks);
                 const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, cap));
                 if (n_recs > 0) {

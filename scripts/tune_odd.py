@@ -40,6 +40,8 @@ VARIANTS = {
     "umid2": ["HBEC_ODD_U_MID=2"],
     "umid3": ["HBEC_ODD_U_MID=3"],
     "ldstab": ["HBEC_ODD_LDSTAB=1"],
+    "pin": ["HBEC_ODD_PIN=5"],
+    "pinlb2": ["HBEC_ODD_PIN=5", "HBEC_ODD_LB=2"],
 }
 
 MiB = 1 << 20
