@@ -560,6 +560,9 @@ int hbec_ec_copy_range(int k, int m, hbec_read_fn read, void* const* bodies, int
     return hbec::guarded("hbec_ec_copy_range", [&]() -> int {
         if (k <= 0 || chunk_size <= 0 || n_dsts < 0 || (n_dsts > 0 && !dsts))
             return fail(HBEC_ERR_INVALID_ARG, "CopyRange: bad arguments");
+        // Go's rangeBytesWriter would panic on b[negative:] (ecobj.go:826-850);
+        // here a negative start or an inverted range is refused before any read
+        if (start < 0 || end < start) return fail(HBEC_ERR_INVALID_ARG, "CopyRange: need 0 <= start <= end");
         int64_t shard_start = 0, shard_end = 0;
         hbec_range_chunk_align(start, end, chunk_size, k, &shard_start, &shard_end);
         if (shard_end > content_length) shard_end = content_length;

@@ -234,7 +234,7 @@ int apply_views(int rows, int cols, const uint8_t* coeffs, const hbec_view* in, 
     const int force_stream = g_force_stream.load();
     // k > 16 at any alignment: one gf_wide pass instead of accumulate passes
     // (9..12 take gf_odd, 13..16 the round-2 one-pass gf_apply_unaligned)
-    if (!vec && g_unaligned_kernel.load() && cols > kMaxK && cols <= 256 && shard_len < (1ull << 31) &&
+    if (!vec && g_unaligned_kernel.load() && cols > kMaxK && cols <= 256 && pos32_shard(shard_len) &&
         wide_apply_enabled())
         return apply_wide(rows, cols, coeffs, in, out, n_obj, shard_len, stream);
 
@@ -310,7 +310,7 @@ int apply_views(int rows, int cols, const uint8_t* coeffs, const hbec_view* in, 
                     hipError_t e = launch_vec(K, R, b, grid, stream, force_stream);
                     if (e != hipSuccess) return hip_fail(e, "launch gf_apply_vec");
                 }
-            } else if (g_unaligned_kernel.load() && odd_enabled() && cols <= kOddMaxK && shard_len < (1ull << 31)) {
+            } else if (g_unaligned_kernel.load() && odd_enabled() && cols <= kOddMaxK && pos32_shard(shard_len)) {
                 // any alignment / length: gf_odd (odd.hip), passes of <= 8 inputs,
                 // later ones accumulating into the outputs
                 rc = apply_odd(a, K, R, c0 > 0, n_obj, shard_len, dev, stream);
@@ -1147,7 +1147,7 @@ static int verify_views(hbec_codec* c, const hbec_view* views, uint64_t n_obj, u
         return HBEC_OK;
     }
     // k <= 8: gf_odd verify; above, gf_verify_wide (10+4 53 vs 55 %, 12+4 41 vs 54 %, r3b7)
-    if (g_unaligned_kernel.load() && odd_enabled() && k <= 8 && shard_len < (1ull << 31)) {
+    if (g_unaligned_kernel.load() && odd_enabled() && k <= 8 && pos32_shard(shard_len)) {
         // any alignment: recompute and compare in one pass (gf_odd verify), <= 4 rows per launch
         int dev = 0;
         int rc = current_device(&dev);
@@ -1170,7 +1170,7 @@ static int verify_views(hbec_codec* c, const hbec_view* views, uint64_t n_obj, u
         }
         return HBEC_OK;
     }
-    if (g_unaligned_kernel.load() && k > 8 && k <= 256 && shard_len < (1ull << 31) && wide_verify_enabled()) {
+    if (g_unaligned_kernel.load() && k > 8 && k <= 256 && pos32_shard(shard_len) && wide_verify_enabled()) {
         // k > 8 at any alignment (k > 16 included): one read-only pass per <= 8
         // rows (gf_verify_wide, wide.hip), coefficient tables in LDS
         return verify_wide(views, k, m, prow, n_obj, shard_len, flags, stream);

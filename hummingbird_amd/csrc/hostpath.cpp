@@ -633,9 +633,13 @@ int zero_copy_unaligned_md5_run(Ring* ring, const std::vector<ZcStripe>& zs, con
             const uint64_t bytes = ((uint64_t)n_shards * hbec::odd_mirror_pitch_host(S) + 255) & ~uint64_t(255);
             if (tiles + 2 > ring->tile_cap || bytes > ring->arena_cap)
                 return fail(HBEC_ERR_INVALID_ARG, "stripe too large for a hash arena");
-            if (nt > 0 && nt + edges.size() + tiles + 1 > ring->tile_cap) break;
+            // a stripe of S <= 160 adds an edge record and no main record, so
+            // the slot is full when main + edge records would pass tile_cap,
+            // whether or not a main record exists yet
+            const bool any = nt > 0 || !edges.empty();
+            if (any && nt + edges.size() + tiles + 1 > ring->tile_cap) break;
             if (!ac.fits(bytes, (uint64_t)(K + R))) {
-                if (nt > 0 || !edges.empty()) break;  // launch this chunk first: the arena is hashed after its kernels
+                if (any) break;  // launch this chunk first: the arena is hashed after its kernels
                 rc = ac.flush();
                 if (rc) return rc;
             }
@@ -741,7 +745,7 @@ int host_run_on(Ring* ring, const hbec_stripe* stripes, uint64_t n, const std::v
             if (!stripes[s].base || S == 0) break;
             const bool aligned = (reinterpret_cast<uintptr_t>(stripes[s].base) & 15u) == 0 && S % 16 == 0 &&
                                  S < (1ull << 32);
-            if (!aligned && (!any_align || S >= (1ull << 31))) break;
+            if (!aligned && (!any_align || !hbec::pos32_shard(S))) break;
             const uint64_t d = pinned_device_addr(stripes[s].base, (uint64_t)(top + 1) * S);
             if (!d) break;
             all_aligned = all_aligned && aligned && (d & 15u) == 0;
@@ -780,7 +784,7 @@ int host_run_on(Ring* ring, const hbec_stripe* stripes, uint64_t n, const std::v
             const bool aligned = (reinterpret_cast<uintptr_t>(stripes[s].base) & 15u) == 0 && S % 16 == 0 &&
                                  S < (1ull << 32) && (d & 15u) == 0;
             if (d && aligned) zs.push_back({d, S});
-            else if (d && hbec::zero_copy_any_alignment() && S < (1ull << 31)) zu.push_back({d, S});  // gf_odd: 32-bit positions
+            else if (d && hbec::zero_copy_any_alignment() && hbec::pos32_shard(S)) zu.push_back({d, S});  // gf_odd: 32-bit positions
             else staged.push_back(stripes[s]);
         }
         if (!zs.empty()) {

@@ -145,6 +145,13 @@ hipError_t launch_unaligned_plan(int k, int r, const UPlanArgs& a, int grid, hip
 #endif
 static_assert(HBEC_ODD_MAXK == 8 || HBEC_ODD_MAXK == 12, "gf_odd instances exist for K <= 8 (odd.hip, odd_k58.hip) and 9..12 (odd_k912.hip)");
 constexpr int kOddMaxK = HBEC_ODD_MAXK;
+// Longest shard the 32-bit-position kernels (gf_odd, gf_odd_plan, gf_wide)
+// take.  They form shard positions in int32: column block starts, load
+// limits ((l4 + S + A - 1) & ~(A - 1)) - 16, window and tile offsets, all
+// below S + 4 KiB.  2^31 - 64 KiB keeps every one of them positive; longer
+// shards take the 64-bit round-2 kernels (gf_apply_unaligned family).
+constexpr uint64_t kPos32MaxShard = (1ull << 31) - (1ull << 16);
+__host__ __device__ constexpr bool pos32_shard(uint64_t shard_len) { return shard_len <= kPos32MaxShard; }
 // HBEC_ODD=1 / 0 selects gf_odd or the round-2 kernels (gf_apply_unaligned
 // family) for odd shards (default: HBEC_ODD_DEFAULT).
 bool odd_enabled();

@@ -230,6 +230,7 @@ uint32_t odd_tiles_per_obj(int k, int mode, uint64_t shard_len) {
 bool odd_supported(int k, int r) { return k >= 1 && k <= kOddMaxK && r >= 1 && r <= kMaxR; }
 
 hipError_t launch_odd(int k, int r, int mode, const PassArgs& a, uint32_t* flags, int grid, hipStream_t stream) {
+    if (!pos32_shard(a.shard_len)) return hipErrorInvalidValue;  // 32-bit shard positions
     const void* fn = odd_kernel(k, r, mode, false);
     if (!fn) return hipErrorInvalidValue;
     void* args[] = {const_cast<PassArgs*>(&a), &flags};
@@ -238,6 +239,7 @@ hipError_t launch_odd(int k, int r, int mode, const PassArgs& a, uint32_t* flags
 
 hipError_t launch_odd_edges(int k, int r, int mode, const PassArgs& a, uint32_t* flags, hipStream_t stream) {
     if (k < 1 || k > kMaxK || r < 1 || r > kMaxR || a.n_obj == 0) return a.n_obj == 0 ? hipSuccess : hipErrorInvalidValue;
+    if (!pos32_shard(a.shard_len)) return hipErrorInvalidValue;
     const uint64_t total = a.n_obj * (uint64_t)r * kOddEdgeSlots;
     const int grid = (int)std::min<uint64_t>((total + kBlockThreads - 1) / kBlockThreads, 4096);
     const void* fn = mode == kOddVerify ? (const void*)&gf_odd_edges<kOddVerify>

@@ -64,7 +64,7 @@ std::mutex g_occ_mu;
 void add_urecs(std::vector<hbec::URec>& recs, std::vector<hbec::URec>& erecs, std::vector<hbec::URec>& brecs,
                const void* a, const void* b, uint64_t s, int k) {
     const uint64_t ua = reinterpret_cast<uint64_t>(a), ub = reinterpret_cast<uint64_t>(b);
-    if (!hbec::odd_enabled() || s >= (1ull << 31)) {
+    if (!hbec::odd_enabled() || !hbec::pos32_shard(s)) {
         const uint64_t tile = (uint64_t)hbec::unaligned_tile_bytes();
         for (uint64_t p0 = 0; p0 < s; p0 += tile) brecs.push_back({ua, ub, s, p0});
         return;

@@ -340,7 +340,7 @@ uint32_t wide_tile_bytes() { return kWideTile; }
 uint64_t wide_main_len(uint64_t shard_len) { return wide_main_bytes(shard_len); }
 
 hipError_t launch_verify_wide(int r, const WideArgs& a, uint32_t* flags, int grid, hipStream_t stream) {
-    if (a.K < 1 || a.K > 256 || a.shard_len >= (1ull << 31)) return hipErrorInvalidValue;
+    if (a.K < 1 || a.K > 256 || !pos32_shard(a.shard_len)) return hipErrorInvalidValue;
     switch (r) {
         case 1: return launch_wide_r<1>(a, flags, grid, stream);
         case 2: return launch_wide_r<2>(a, flags, grid, stream);
@@ -359,7 +359,7 @@ uint32_t wide_apply_tiles_per_obj(uint64_t shard_len) {
 }
 
 hipError_t launch_apply_wide(int r, const WideArgs& a, int grid, hipStream_t stream) {
-    if (a.K < 1 || a.K > 256 || a.shard_len >= (1ull << 31)) return hipErrorInvalidValue;
+    if (a.K < 1 || a.K > 256 || !pos32_shard(a.shard_len)) return hipErrorInvalidValue;
     switch (r) {
         case 1: return launch_apply_wide_r<1>(a, grid, stream);
         case 2: return launch_apply_wide_r<2>(a, grid, stream);

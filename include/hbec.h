@@ -30,7 +30,12 @@
 extern "C" {
 #endif
 
-#define HBEC_VERSION 1
+/* ABI version.  2: hbec_ec_shard_length's data_shards became int64_t (Go's
+ * int, as parseECScheme returns it); it was int in version 1, so a caller
+ * compiled against a version-1 header must be rebuilt (a 32-bit argument
+ * leaves the register's upper half undefined).  Callers may check
+ * hbec_version() == HBEC_VERSION at start-up. */
+#define HBEC_VERSION 2
 
 enum {
     HBEC_OK = 0,
@@ -372,7 +377,9 @@ int hbec_ec_glue_range(int data_shards, int parity_shards, hbec_read_fn read, vo
  * units here, so for ranges that do not start in the first chunk of a stripe
  * the bytes are not object[start, end) — this entry reproduces them anyway
  * (the drop-in for ecobj.go:264-265; hbec_ec_glue_range is the corrected
- * decode).  Returns the glue's status; CopyRange itself ignores it (:264). */
+ * decode).  Returns the glue's status; CopyRange itself ignores it (:264).
+ * HBEC_ERR_INVALID_ARG, before any read, when start < 0 or end < start (Go
+ * would panic slicing with a negative offset). */
 int hbec_ec_copy_range(int data_shards, int parity_shards, hbec_read_fn read, void* const* bodies, int chunk_size,
                        int64_t content_length, int64_t start, int64_t end, hbec_write_fn write, void* const* dsts,
                        int n_dsts);

@@ -1,0 +1,116 @@
+#!/usr/bin/env python3
+"""Driver for per-kernel counter passes over the odd-shard kernel families
+(VERDICT r03 item 1): each shape is launched `reps` times back to back after
+a clock settle, so a rocprofv3 --pmc pass sees runs of one kernel at a time.
+
+    python scripts/odd_sq.py [reps] [n_objects] [shape,...]
+
+Shapes (ecSplit databufs, device-resident, 2048 objects by default):
+  a42   aligned 4+2 @ 1 MiB            gf_apply_vec_pipe2<4,2>   (reference point)
+  o42   4+2,  S = 262 143              gf_odd<4,2,0>
+  a83   aligned 8+3 @ 1 MiB            gf_apply_vec_pipe<8,3>
+  o83   8+3,  S = 131 071              gf_odd<8,3,0>
+  r83   8+3 reconstruct {0,1}          gf_odd<8,2,0>
+  v83   8+3 Verify                     gf_odd<8,3,2>
+  o104  10+4, S = 104 858              gf_odd<10,4,0>
+  p124  12+4 object plan, S = 87 392   gf_odd_plan<12,4,...>
+  v328  32+8 Verify, S = 32 768 + 3    gf_wide<8,...> verify
+One JSON line per shape (median ms, % of 8 TB/s on the algorithmic bytes);
+every encode is checked with the product's Verify.
+"""
+from __future__ import annotations
+
+import json
+import os
+import statistics
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+MiB = 1 << 20
+ALL = ["a42", "o42", "a83", "o83", "r83", "v83", "o104", "p124", "v328"]
+
+
+def main():
+    import torch
+
+    from hummingbird_amd import batch as B
+    from hummingbird_amd import reedsolomon as RS
+
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+    n = int(sys.argv[2]) if len(sys.argv) > 2 else 2048
+    names = sys.argv[3].split(",") if len(sys.argv) > 3 else ALL
+    torch.cuda.set_device(0)
+
+    def timeit(fn):
+        fn()
+        ts = []
+        for _ in range(reps):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            fn()
+            b.record()
+            b.synchronize()
+            ts.append(a.elapsed_time(b))
+        return statistics.median(ts)
+
+    x = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
+    for _ in range(200):
+        x.add_(1)
+    del x
+
+    def databuf(k, m, s):
+        rows = torch.empty((n, (k + m) * s), dtype=torch.uint8, device="cuda")
+        B.fill_splitmix(rows, (k + m) * s)
+        return rows, B.shard_views(rows, k + m, s)
+
+    def check(enc, views, s):
+        flags = torch.zeros(n, dtype=torch.int32, device="cuda")
+        B.verify_views(enc, views, n, s, flags)
+        torch.cuda.synchronize()
+        return int(flags.count_nonzero().item()) == 0
+
+    for name in names:
+        k, m, s, op = {"a42": (4, 2, MiB // 4, "enc"), "o42": (4, 2, 262143, "enc"), "a83": (8, 3, MiB // 8, "enc"),
+                       "o83": (8, 3, 131071, "enc"), "r83": (8, 3, 131071, "rec"), "v83": (8, 3, 131071, "ver"),
+                       "o104": (10, 4, 104858, "enc"), "p124": (12, 4, 87392, "plan"),
+                       "v328": (32, 8, 32771, "ver")}[name]
+        enc = RS.New(k, m)
+        row = {"lib": os.environ.get("HBEC_LIB", "default"), "label": os.environ.get("AB_LABEL", ""), "round": int(os.environ.get("AB_ROUND", "0")),
+               "shape": name, "k": k, "m": m, "S": s, "n": n, "op": op}
+        if op == "plan":
+            d = torch.empty((n, k * s), dtype=torch.uint8, device="cuda")
+            B.fill_splitmix(d, k * s)
+            par = torch.empty((n, m * s), dtype=torch.uint8, device="cuda")
+            plan = B.StripePlan(enc, objects=[(d.data_ptr() + i * d.stride(0), par.data_ptr() + i * par.stride(0), s)
+                                              for i in range(n)])
+            ms = timeit(plan.encode)
+            nb = n * (k + m) * s
+            row["ok"] = check(enc, B.shard_views(d, k, s) + B.shard_views(par, m, s), s)
+            del plan, d, par
+        else:
+            rows, views = databuf(k, m, s)
+            B.encode_views(enc, views, n, s)
+            if op == "enc":
+                ms = timeit(lambda: B.encode_views(enc, views, n, s))
+                nb = n * (k + m) * s
+            elif op == "rec":
+                present = [0, 0] + [1] * (k + m - 2)
+                ms = timeit(lambda: B.reconstruct_views(enc, views, present, n, s))
+                nb = n * (k + 2) * s
+            else:
+                flags = torch.zeros(n, dtype=torch.int32, device="cuda")
+                ms = timeit(lambda: B.verify_views(enc, views, n, s, flags))
+                nb = n * (k + m) * s
+            row["ok"] = check(enc, views, s)
+            del rows, views
+        row["ms"] = round(ms, 4)
+        row["frac"] = round(nb / (ms * 1e-3) / 8e12, 4)
+        print(json.dumps(row), flush=True)
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

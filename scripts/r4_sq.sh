@@ -1,0 +1,19 @@
+#!/bin/bash
+# GPU batch: counter list, odd-shape timings, one SQ issue pass and a
+# kernel-trace stats pass over scripts/odd_sq.py.
+# usage: scripts/r4_sq.sh TAG [SHAPES]
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+ROOT=$(pwd); OUT=$ROOT/gpurun_out; mkdir -p $OUT; export TMPDIR=/tmp
+tag=${1:-r4sq}
+shapes=${2:-a42,o42,a83,o83,r83,v83,o104,p124,v328}
+if [ ! -s $OUT/r4_counters.txt ]; then
+  (cd /tmp && timeout -k 10 60 rocprofv3 -L > $OUT/r4_counters.txt 2>&1) || echo "counter list rc=$?"
+fi
+timeout -k 10 200 python scripts/odd_sq.py 10 2048 $shapes > $OUT/${tag}_times.jsonl 2> $OUT/${tag}_times.err || exit $?
+cat $OUT/${tag}_times.jsonl
+mkdir -p $OUT/${tag}_sq1 $OUT/${tag}_prof
+(cd /tmp && timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU --kernel-trace --output-format csv -d $OUT/${tag}_sq1 -o run -- python3 $ROOT/scripts/odd_sq.py 3 2048 $shapes > $OUT/${tag}_sq1.log 2>&1) || exit $?
+(cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/${tag}_prof -o run -- python3 $ROOT/scripts/odd_sq.py 10 2048 $shapes > $OUT/${tag}_prof.log 2>&1) || exit $?
+python scripts/sq_summary.py $OUT/${tag}_sq1.json $OUT/${tag}_sq1 --only gf_ || exit $?
+echo done

@@ -37,7 +37,7 @@ def test_library_exports_every_header_symbol():
 
 
 def test_version_and_strerror():
-    assert N.lib().hbec_version() == 1
+    assert N.lib().hbec_version() == 2  # 2: int64 data_shards in hbec_ec_shard_length
     assert N.strerror(N.ERR_TOO_FEW_SHARDS) == "too few shards given"
     assert N.strerror(N.ERR_SHARD_SIZE) == "shard sizes do not match"
 
@@ -152,6 +152,26 @@ def test_ec_split_zero_length_needs_no_device():
     assert out == []
 
 
+def test_copy_range_refuses_negative_or_inverted_ranges():
+    """A negative start (Go would panic on b[negative:], ecobj.go:826-850) or
+    end < start is an argument error before any body is read (advisor r03)."""
+    read = []
+
+    class Body:
+        def read(self, n):
+            read.append(n)
+            return b""
+
+    class W:
+        def write(self, b):
+            raise AssertionError("nothing may be written")
+
+    for start, end in [(-1, 10), (-4096, 0), (10, 5)]:
+        rc = E.ec_copy_range(4, 2, [Body() for _ in range(6)], 1 << 20, 100, start, end, W())
+        assert rc == N.ERR_INVALID_ARG, (start, end)
+    assert read == []
+
+
 def test_ec_split_short_read_is_unexpected_eof():
     import io
     with pytest.raises(RS.ErrUnexpectedEOF):
@@ -187,7 +207,7 @@ def test_pure_c_client(tmp_path):
                     f"-Wl,-rpath,{lib_dir}", "-o", str(exe)], check=True, capture_output=True)
     out = subprocess.run([str(exe)], capture_output=True, text=True)
     assert out.returncode == 0, (out.returncode, out.stderr)
-    assert "abi ok v1" in out.stdout
+    assert "abi ok v2" in out.stdout
 
 
 def test_shardhash_validation_before_device():

@@ -100,3 +100,90 @@ def test_stripe_plan_with_a_stripe_over_4gib():
             d = stripe[:k * s].cpu().numpy().reshape(1, -1)
             want, _ = CO.encode_batch(k, m, d)
             assert np.array_equal(stripe[k * s:].cpu().numpy(), want.reshape(-1)), s
+
+
+# Shards at the top of the 32-bit-position kernels' range (VERDICT r03 item
+# 2): gf_odd / gf_odd_plan / gf_wide form shard positions in int32 and take
+# S <= kPos32MaxShard = 2^31 - 64 KiB (kernels.h); 2^31 - 1 and 2^31 - 5 go
+# to the 64-bit round-2 kernels.  Before the routing fix, S = 2^31 - 1 at an
+# odd base made gf_odd's load limit negative and every column load hit one
+# block (silently wrong parity).
+POS32_MAX = (1 << 31) - (1 << 16)
+
+
+def _pos32_windows(s):
+    mid = min((1 << 31) - 4096 - WIN // 2, s - WIN)
+    return sorted({0, mid, s - 65536 - WIN // 2, s - WIN})
+
+
+def _check_databuf_windows(k, m, buf, base, s):
+    for off in _pos32_windows(s):
+        d = np.stack([buf[base + j * s + off: base + j * s + off + WIN].cpu().numpy() for j in range(k)])
+        want, _ = CO.encode_batch(k, m, np.ascontiguousarray(d.reshape(1, k * WIN)))
+        got = np.concatenate([buf[base + (k + r) * s + off: base + (k + r) * s + off + WIN].cpu().numpy()
+                              for r in range(m)])
+        assert np.array_equal(got, want.reshape(-1)), (s, off)
+
+
+@pytest.mark.parametrize("k,m,s,base", [(2, 1, (1 << 31) - 1, 1), (2, 1, (1 << 31) - 5, 3),
+                                        (2, 1, POS32_MAX - 3, 3), (3, 2, POS32_MAX, 1),
+                                        (9, 1, POS32_MAX - 1, 3)])
+def test_shard_near_2gib_encode_rebuild_verify(k, m, s, base):
+    """ecSplit databuf (shard i at base + i * S, ecutils.go:31-35) with S just
+    below 2^31 at an odd byte offset: encode against the oracle on windows at
+    0, across 2^31 - 4096, 64 KiB before the end and the last 4 KiB; rebuild
+    of shard 0 bit-identical; Verify clean, then flags a flipped last byte."""
+    enc = RS.New(k, m)
+    n = k + m
+    buf = torch.empty(base + n * s + 16, dtype=torch.uint8, device="cuda")
+    B.fill_splitmix(buf.view(1, -1), buf.numel(), first=s & 0xFFFF)
+    views = [(buf.data_ptr() + base + i * s, 0) for i in range(n)]
+    B.encode_views(enc, views, 1, s)
+    torch.cuda.synchronize()
+    _check_databuf_windows(k, m, buf, base, s)
+
+    reb = torch.empty(s + 8, dtype=torch.uint8, device="cuda")
+    rv = list(views)
+    rv[0] = (reb.data_ptr() + 5, 0)
+    B.reconstruct_views(enc, rv, [0] + [1] * (n - 1), 1, s)
+    torch.cuda.synchronize()
+    assert torch.equal(reb[5:5 + s], buf[base:base + s])
+    del reb
+
+    flags = torch.zeros(1, dtype=torch.int32, device="cuda")
+    B.verify_views(enc, views, 1, s, flags)
+    torch.cuda.synchronize()
+    assert int(flags.item()) == 0
+    last = base + n * s - 1  # last byte of the last parity shard
+    buf[last] ^= 0x40
+    B.verify_views(enc, views, 1, s, flags)
+    torch.cuda.synchronize()
+    assert int(flags.item()) == 1
+    del buf
+    torch.cuda.empty_cache()
+
+
+def test_stripe_plan_near_2gib():
+    """A stripe plan with one stripe the 32-bit plan kernel takes (S = 2^31 -
+    64 KiB - 3) and one it must not (S = 2^31 - 5), both at odd offsets."""
+    k, m = 2, 1
+    enc = RS.New(k, m)
+    sizes = [POS32_MAX - 3, (1 << 31) - 5, 4097]
+    offs, off = [], 3
+    for s in sizes:
+        offs.append(off)
+        off += (k + m) * s + 7
+    pool = torch.empty(off + 16, dtype=torch.uint8, device="cuda")
+    B.fill_splitmix(pool.view(1, -1), pool.numel(), first=77)
+    plan = B.StripePlan(enc, [(pool.data_ptr() + o, s) for o, s in zip(offs, sizes)])
+    plan.encode()
+    torch.cuda.synchronize()
+    for o, s in zip(offs, sizes):
+        if s > (1 << 20):
+            _check_databuf_windows(k, m, pool, o, s)
+        else:
+            d = pool[o:o + k * s].cpu().numpy().reshape(1, -1)
+            want, _ = CO.encode_batch(k, m, d)
+            assert np.array_equal(pool[o + k * s:o + (k + m) * s].cpu().numpy(), want.reshape(-1))
+    del pool, plan
+    torch.cuda.empty_cache()

@@ -360,3 +360,49 @@ def test_encode_host_md5_pinned_unaligned_zero_copy(k, m, sizes):
         del stripes
     finally:
         hb.free()
+
+
+def test_encode_host_md5_pinned_many_tiny_unaligned_stripes():
+    """More pinned, unaligned stripes of S <= 160 than one ring slot holds
+    records for (tile_cap = 66 560 at the default 64 MiB slot), k + m = 3.
+    Such stripes add an edge record and no main record, so the slot-full test
+    must count the edge records too (advisor r03, hostpath.cpp
+    zero_copy_unaligned_md5_run): parity and every digest against the oracle."""
+    k, m, n = 2, 1, 70_000
+    sizes = [(1, 7, 100, 159, 160, 17)[i % 6] for i in range(n)]
+    enc = RS.New(k, m)
+    rng = np.random.default_rng(99)
+    gaps = rng.integers(0, 16, n)
+    total = sum((k + m) * s for s in sizes) + int(gaps.sum()) + 64
+    hb = RS.HostBuffer(total)
+    try:
+        stripes, offs, off = [], [], 3
+        data = rng.integers(0, 256, total, dtype=np.uint8)
+        hb.array[:] = data
+        for s, g in zip(sizes, gaps):
+            st = hb.array[off:off + (k + m) * s]
+            st[k * s:] = 0xA5
+            stripes.append(st)
+            offs.append(off)
+            off += (k + m) * s + int(g)
+        zc0, ring0 = _md5_stats()
+        hashes = enc.EncodeStripesMD5(stripes)
+        zc1, ring1 = _md5_stats()
+        assert (zc1 - zc0, ring1 - ring0) == (1, 0)
+        for s in sorted(set(sizes)):
+            idx = [i for i in range(n) if sizes[i] == s]
+            objs = np.stack([np.asarray(stripes[i][:k * s]) for i in idx])
+            want, _ = CO.encode_batch(k, m, np.ascontiguousarray(objs))
+            got = np.stack([np.asarray(stripes[i][k * s:]) for i in idx])
+            assert np.array_equal(got, want), s
+        for i in range(n):
+            s = sizes[i]
+            assert hashes[i] == [O.shard_hash(stripes[i][j * s:(j + 1) * s]) for j in range(k + m)], i
+        # bytes between the stripes are untouched
+        mask = np.ones(total, bool)
+        for o, s in zip(offs, sizes):
+            mask[o:o + (k + m) * s] = False
+        assert np.array_equal(hb.array[mask], data[mask])
+        del stripes
+    finally:
+        hb.free()
