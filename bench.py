@@ -86,6 +86,16 @@ def max_over_ranks(pg, values, device):
     return t.tolist()
 
 
+def gather_ranks(pg, values, device):
+    """Every rank's list of floats, in rank order (control traffic only)."""
+    if pg is None:
+        return [list(values)]
+    t = torch.tensor(list(values), dtype=torch.float64, device=device)
+    out = [torch.empty_like(t) for _ in range(pg.get_world_size())]
+    pg.all_gather(out, t)
+    return [o.tolist() for o in out]
+
+
 # Sources whose compiled code the dominant kernel is (gf_apply_vec_pipe2 and
 # its device helpers): a PMC summary is only reported as this run's traffic
 # when it was collected on exactly these sources.
@@ -158,8 +168,12 @@ class Workload:
         return bool(torch.equal(self.rebuilt, want))
 
 
-def cpu_baseline(k, m, obj_len, erased, budget_s=12.0, sample_objs=512):
-    """Oracle AVX2 port over the host threads, bounded sample, same two ops."""
+def cpu_baseline(k, m, obj_len, erased, budget_s=12.0, sample_objs=512, gpu=None):
+    """Oracle AVX2 port over the host threads, bounded sample, same two ops.
+    gpu: (objects, parity, rebuilt) of the timed headline batch's first
+    sample_objs objects (host copies, taken after the timed region); the CPU
+    sample is the same splitmix objects, so the oracle's parity and rebuilt
+    shards are compared with the GPU's byte for byte (`oracle_match`)."""
     import numpy as np
 
     from oracle import coracle as CO
@@ -187,6 +201,10 @@ def cpu_baseline(k, m, obj_len, erased, budget_s=12.0, sample_objs=512):
         if passes >= 20000:
             break
     assert np.array_equal(rebuilt, np.concatenate([objs[:, i * s:(i + 1) * s] for i in erased], axis=1))
+    match = None
+    if gpu is not None:
+        g_objs, g_par, g_reb = gpu
+        match = bool(np.array_equal(g_objs, objs) and np.array_equal(g_par, parity) and np.array_equal(g_reb, rebuilt))
     nbytes = passes * sample_objs * ((k + m) * s + (k + len(erased)) * s)
     # single thread, same two ops, bounded (~2 s)
     t1, p1 = 0.0, 0
@@ -212,6 +230,9 @@ def cpu_baseline(k, m, obj_len, erased, budget_s=12.0, sample_objs=512):
         "single_thread_GiB_s": round(single, 3),
         "config1_ecsplit_1mib_single_thread_ms": round(reps[len(reps) // 2] * 1e3, 4),
         "config1_kernel_only_single_thread_ms": round(reps_k[len(reps_k) // 2] * 1e3, 4),
+        "oracle_match": match,
+        "oracle_match_sample": (f"objects 0..{sample_objs - 1} of the timed batch: GPU parity and rebuilt shards "
+                                f"{{{','.join(map(str, erased))}}} vs the oracle's, byte for byte") if gpu is not None else None,
     }
 
 
@@ -618,9 +639,10 @@ def dry_run(world, rank):
         dist.init_process_group("gloo")
         pg = dist
     (seen,) = max_over_ranks(pg, [float(rank + 1)], "cpu")
+    per_rank = gather_ranks(pg, [float(rank), float(10 * rank)], "cpu")
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": world,
-                          "ranks_seen": int(seen), "dry_run": True}), flush=True)
+                          "ranks_seen": int(seen), "per_rank": per_rank, "dry_run": True}), flush=True)
     if pg:
         pg.destroy_process_group()
     return 0
@@ -705,6 +727,7 @@ def main(argv=None):
 
     enc_ms = sum(e0.elapsed_time(e1) for e0, e1, _ in ev) / args.steps
     rec_ms = sum(e1.elapsed_time(e2) for _, e1, e2 in ev) / args.steps
+    per_rank = gather_ranks(pg, [enc_ms, rec_ms], ctl_device) if world > 1 else None
     elapsed, enc_ms, rec_ms, bad = max_over_ranks(pg, [elapsed, enc_ms, rec_ms, 0.0 if ok else 1.0], ctl_device)
     ok = bad == 0.0
 
@@ -761,13 +784,22 @@ def main(argv=None):
                 "kernel_sources_sha256": kernel_sources_sha256(),
                 "tile_bytes": info["tile_bytes"], "kernel_kind": info["kind"],
                 "blocks_per_cu": info["blocks_per_cu"],
+                # N > 1: each rank's own launches (the fields above use the max over ranks)
+                "per_rank": None if per_rank is None else [
+                    {"rank": r, "encode_ms_per_launch": round(e, 4), "reconstruct_ms_per_launch": round(c, 4),
+                     "frac": round(launch_bytes / ((e + c) / 2 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+                    for r, (e, c) in enumerate(per_rank)],
             },
             "object_data_gib_s": round(value * k / (k + m), 2),
             "parity_ok": ok,
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(k, m, obj_len, erased, budget_s=args.cpu_budget)
+            ns = min(512, n)
+            gpu = (w.objs[:ns].cpu().numpy(), w.parity[:ns].cpu().numpy(), w.rebuilt[:ns].cpu().numpy())
+            line["cpu_baseline"] = cpu_baseline(k, m, obj_len, erased, budget_s=args.cpu_budget, sample_objs=ns,
+                                                gpu=gpu if first == 0 else None)
+            del gpu
     del w  # free this rank's headline batch before the partition / split buffers
     torch.cuda.empty_cache()
     if args.config5_objects > 0:

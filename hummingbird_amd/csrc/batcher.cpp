@@ -248,12 +248,9 @@ int hbec_batcher_new(hbec_codec* codec, uint64_t max_batch_bytes, uint32_t max_w
         b->codec = codec;
         b->max_batch_bytes = max_batch_bytes ? max_batch_bytes : (256ull << 20);
         b->max_wait = std::chrono::microseconds(max_wait_us);
-        const char* envq = std::getenv("HBEC_BATCHER_QUIET_US");
-        b->quiet = std::chrono::microseconds(envq ? std::max(1, std::atoi(envq)) : 20);
-        const char* env = std::getenv("HBEC_BATCHER_WORKERS");
-        const int n_workers = std::min(8, std::max(1, env ? std::atoi(env) : 2));
-        const char* env5 = std::getenv("HBEC_BATCHER_MD5_WORKERS");
-        b->md5_workers = std::min(16, std::max(0, env5 ? std::atoi(env5) : 4));
+        b->quiet = std::chrono::microseconds(std::max(1LL, hbec::tune_knob("HBEC_BATCHER_QUIET_US", 20)));
+        const int n_workers = (int)std::min(8LL, std::max(1LL, hbec::env_knob("HBEC_BATCHER_WORKERS", 2)));
+        b->md5_workers = (int)std::min(16LL, std::max(0LL, hbec::env_knob("HBEC_BATCHER_MD5_WORKERS", 4)));
         b->batch_cap = std::max<uint64_t>(1, b->max_batch_bytes / (uint64_t)n_workers);
         b->md5_cap = std::max<uint64_t>(1, b->max_batch_bytes / (uint64_t)std::max(1, b->md5_workers));
         hbec_batcher* raw = b.get();

@@ -59,8 +59,7 @@ struct CoReq {
 // the slot on, so at most this many groups ever run.
 int max_in_flight() {
     static const int v = [] {
-        const char* e = std::getenv("HBEC_COALESCE_INFLIGHT");
-        const int x = e ? std::atoi(e) : 0;
+        const int x = (int)hbec::tune_knob("HBEC_COALESCE_INFLIGHT", 0);
         return x > 0 ? x : 2;
     }();
     return v;
@@ -72,10 +71,7 @@ int max_in_flight() {
 // grouping (1 MiB: 35 vs 25-29 GiB/s at 16 callers); from ~64 callers,
 // grouping wins (38-42 vs 35 GiB/s) (profiles/r02_coalesce_direct.jsonl).
 int direct_limit() {
-    static const int v = [] {
-        const char* e = std::getenv("HBEC_COALESCE_DIRECT");
-        return e ? std::max(0, std::atoi(e)) : 16;
-    }();
+    static const int v = (int)std::max(0LL, hbec::tune_knob("HBEC_COALESCE_DIRECT", 16));
     return v;
 }
 
@@ -91,8 +87,7 @@ Coalescer g_co;
 
 uint64_t group_cap_bytes() {
     static const uint64_t cap = [] {
-        const char* e = std::getenv("HBEC_COALESCE_MB");
-        const long long v = e ? std::atoll(e) : 0;
+        const long long v = hbec::tune_knob("HBEC_COALESCE_MB", 0);
         return (uint64_t)(v > 0 ? v : 256) << 20;
     }();
     return cap;
@@ -140,10 +135,7 @@ void fail_group(CoReq* head, int code, const char* msg) noexcept {
 }  // namespace
 
 bool coalesce_enabled() {
-    static const bool on = [] {
-        const char* e = std::getenv("HBEC_COALESCE");
-        return !(e && e[0] == '0');
-    }();
+    static const bool on = hbec::env_knob("HBEC_COALESCE", 1) != 0;
     return on;
 }
 

@@ -51,30 +51,26 @@ int hip_fail(hipError_t e, const char* what) {
     return fail(e == hipErrorOutOfMemory ? HBEC_ERR_NOMEM : HBEC_ERR_DEVICE, m);
 }
 
+long long hbec::env_knob(const char* name, long long dflt) {
+    const char* e = std::getenv(name);
+    return e && *e ? std::atoll(e) : dflt;
+}
+
 static std::atomic<int> g_force_stream{0};
 // Views that are not all 16-B aligned (or shards not a multiple of 16 B):
-// gf_apply_unaligned (default) or, with HBEC_UNALIGNED=0, the byte kernel.
+// gf_odd (k <= 12), gf_wide (k > 16), gf_apply_unaligned (13..16, S > 2^31).
 // Tuning knob: resident blocks per CU for the unaligned kernels' grids (0 = occupancy).
-static const int g_unaligned_bpc = [] {
-    const char* e = std::getenv("HBEC_UNALIGNED_BPC");
-    return e ? std::atoi(e) : 0;
-}();
-static const std::atomic<int> g_unaligned_kernel{[] {
-    const char* e = std::getenv("HBEC_UNALIGNED");
-    return e ? std::atoi(e) : 1;
-}()};
-bool unaligned_kernel_enabled() { return g_unaligned_kernel.load() != 0; }
+static const int g_unaligned_bpc = (int)tune_knob("HBEC_UNALIGNED_BPC", 0);
 // Tuning knob: cap on resident blocks per CU used to size vec-kernel grids
 // (0 = the occupancy the compiler's register allocation allows).
-static const int g_blocks_per_cu_override = [] {
-    const char* e = std::getenv("HBEC_BLOCKS_PER_CU");
-    return e ? std::atoi(e) : 0;
-}();
+static const int g_blocks_per_cu_override = (int)tune_knob("HBEC_BLOCKS_PER_CU", 0);
 // Tuning knob: absolute cap on vec-kernel grids (0 = none), to run fewer CUs.
-static const int g_grid_cap = [] {
-    const char* e = std::getenv("HBEC_GRID_CAP");
-    return e ? std::atoi(e) : 0;
-}();
+static const int g_grid_cap_env = (int)tune_knob("HBEC_GRID_CAP", 0);
+// Per-thread grid cap set by a caller that shares the GPU with its own side
+// work (the encode + ShardHash pipeline); 0 = none.
+thread_local int t_grid_cap = 0;
+void set_thread_grid_cap(int blocks) { t_grid_cap = blocks; }
+#define g_grid_cap (t_grid_cap > 0 ? (g_grid_cap_env > 0 ? std::min(t_grid_cap, g_grid_cap_env) : t_grid_cap) : g_grid_cap_env)
 // Tiles per launch of the pipelined / packed kernels (HBEC_CHUNK_TILES):
 // a batch is split into launches of whole objects of at most this many
 // tiles.  Over one very long launch the blocks' grid-stride fronts drift
@@ -82,8 +78,7 @@ static const int g_grid_cap = [] {
 // 72.6 % of 8 TB/s, in 16 launches of 4096 objects at 76.0 %
 // (profiles/r02_config5_tune.jsonl).
 static const uint64_t g_chunk_tiles = [] {
-    const char* e = std::getenv("HBEC_CHUNK_TILES");
-    const long long v = e ? std::atoll(e) : 0;
+    const long long v = tune_knob("HBEC_CHUNK_TILES", 0);
     return (uint64_t)(v > 0 ? v : (1ll << 20));
 }();
 
@@ -176,6 +171,21 @@ static int odd_launches(const PassArgs& a, int K, int R, int mode, bool accumula
             const int m = mode == 2 ? 2 : ((accumulate || c1 > 0) ? 1 : 0);
             const uint64_t tpo = odd_tiles_per_obj(K1, m, shard_len);
             const uint64_t max_obj = std::max<uint64_t>(1, std::min<uint64_t>((1ull << 31), g_chunk_tiles) / tpo);
+            // per-object records of this pass (stream-ordered scratch, freed after its launches)
+            uint32_t* recs = nullptr;
+            const uint64_t rw = odd_rec_words(K1, R, m);
+            if (odd_uses_records()) {
+                rc = scratch_alloc(n_obj * rw * 4, stream, reinterpret_cast<void**>(&recs));
+                if (rc) return rc;
+                PassArgs p = b;
+                p.n_obj = n_obj;
+                p.shard_len = shard_len;
+                hipError_t e = launch_odd_objrec(K1, R, m, p, recs, stream);
+                if (e != hipSuccess) {
+                    scratch_free(recs, stream);
+                    return hip_fail(e, "launch gf_odd_objrec");
+                }
+            }
             for (uint64_t o0 = 0; o0 < n_obj; o0 += max_obj) {
                 const uint64_t no = std::min(max_obj, n_obj - o0);
                 PassArgs c = b;
@@ -189,9 +199,14 @@ static int odd_launches(const PassArgs& a, int K, int R, int mode, bool accumula
                 const uint64_t cap = (uint64_t)cus * (uint64_t)odd_blocks_per_cu(m, K1, R);
                 int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, cap));
                 if (g_grid_cap > 0) grid = std::min(grid, g_grid_cap);
-                hipError_t e = launch_odd(K1, R, m, c, flags ? flags + o0 : nullptr, grid, stream);
-                if (e != hipSuccess) return hip_fail(e, "launch gf_odd");
+                hipError_t e = launch_odd(K1, R, m, c, flags ? flags + o0 : nullptr, recs ? recs + o0 * rw : nullptr, grid,
+                                          stream);
+                if (e != hipSuccess) {
+                    scratch_free(recs, stream);
+                    return hip_fail(e, "launch gf_odd");
+                }
             }
+            scratch_free(recs, stream);
         }
     }
     // the guard-band bytes of every shard, all K inputs of the pass at once
@@ -213,7 +228,6 @@ static int apply_odd(const PassArgs& a, int K, int R, bool accumulate, uint64_t 
 // ---------------------------------------------------------------------------
 static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
-static bool wide_apply_enabled();
 static int apply_wide(int rows, int cols, const uint8_t* coeffs, const hbec_view* in, const hbec_view* out,
                       uint64_t n_obj, uint64_t shard_len, hipStream_t stream);
 
@@ -234,8 +248,7 @@ int apply_views(int rows, int cols, const uint8_t* coeffs, const hbec_view* in, 
     const int force_stream = g_force_stream.load();
     // k > 16 at any alignment: one gf_wide pass instead of accumulate passes
     // (9..12 take gf_odd, 13..16 the round-2 one-pass gf_apply_unaligned)
-    if (!vec && g_unaligned_kernel.load() && cols > kMaxK && cols <= 256 && pos32_shard(shard_len) &&
-        wide_apply_enabled())
+    if (!vec && cols > kMaxK && cols <= 256 && pos32_shard(shard_len))
         return apply_wide(rows, cols, coeffs, in, out, n_obj, shard_len, stream);
 
     for (int r0 = 0; r0 < rows; r0 += kMaxR) {
@@ -310,12 +323,12 @@ int apply_views(int rows, int cols, const uint8_t* coeffs, const hbec_view* in, 
                     hipError_t e = launch_vec(K, R, b, grid, stream, force_stream);
                     if (e != hipSuccess) return hip_fail(e, "launch gf_apply_vec");
                 }
-            } else if (g_unaligned_kernel.load() && odd_enabled() && cols <= kOddMaxK && pos32_shard(shard_len)) {
+            } else if (odd_enabled() && cols <= kOddMaxK && pos32_shard(shard_len)) {
                 // any alignment / length: gf_odd (odd.hip), passes of <= 8 inputs,
                 // later ones accumulating into the outputs
                 rc = apply_odd(a, K, R, c0 > 0, n_obj, shard_len, dev, stream);
                 if (rc) return rc;
-            } else if (g_unaligned_kernel.load()) {
+            } else {
                 // any alignment: aligned 16-B accesses with in-register shifts (gf_apply_unaligned)
                 int cus = 0, per_cu = 0;
                 rc = device_blocks(dev, K, R, 3, 0, &cus, &per_cu);
@@ -337,13 +350,6 @@ int apply_views(int rows, int cols, const uint8_t* coeffs, const hbec_view* in, 
                     hipError_t e = launch_unaligned(K, R, b, grid, stream);
                     if (e != hipSuccess) return hip_fail(e, "launch gf_apply_unaligned");
                 }
-            } else {
-                a.n_obj = n_obj;
-                const uint64_t words = ((shard_len + 3) / 4) * n_obj;
-                const uint64_t want = (words + kBlockThreads - 1) / kBlockThreads;
-                const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, 8192));
-                hipError_t e = launch_bytes(K, R, a, grid, stream);
-                if (e != hipSuccess) return hip_fail(e, "launch gf_apply_bytes");
             }
         }
     }
@@ -366,17 +372,14 @@ struct Staging {
     std::vector<hipEvent_t> ev;
 };
 
-// Per-call host path for pageable shards (HBEC_PERCALL_MODE):
+// Per-call host path for pageable shards (tuning knob HBEC_PERCALL_DMA):
 //   "mapped" (default): the calling thread copies the inputs into a pinned,
 //     device-mapped bounce buffer, the kernel reads them and writes the
 //     outputs there over PCIe, and the thread copies the outputs back;
 //   "dma": one hipMemcpyAsync per shard through a device buffer (the runtime
 //     stages each pageable copy itself).
 // One 1 MiB 4+2 Encode: 87 us mapped vs 131 us dma (profiles/r01_host_path.jsonl).
-static const bool g_percall_mapped = [] {
-    const char* e = std::getenv("HBEC_PERCALL_MODE");
-    return !(e && std::string(e) == "dma");
-}();
+static const bool g_percall_mapped = tune_knob("HBEC_PERCALL_DMA", 0) == 0;
 
 // Column pieces of one per-call apply in mapped mode (HBEC_PERCALL_PIECES,
 // default 2; shards shorter than 64 KiB are one piece): the calling thread
@@ -384,11 +387,7 @@ static const bool g_percall_mapped = [] {
 // PCIe, then copies each piece's outputs back as soon as its kernel is done.
 // 1 MiB 4+2 Encode from pageable memory, one caller: 77 us in one piece,
 // 66 us in 2, 86 us in 4 (per-piece launch cost; profiles/r02_percall_pieces.jsonl).
-static const int g_percall_pieces = [] {
-    const char* e = std::getenv("HBEC_PERCALL_PIECES");
-    const int v = e ? std::atoi(e) : 2;
-    return std::max(1, std::min(16, v));
-}();
+static const int g_percall_pieces = (int)std::max(1LL, std::min(16LL, tune_knob("HBEC_PERCALL_PIECES", 2)));
 
 // Per-call applies running at once (HBEC_PERCALL_CONCURRENCY, default 16;
 // 0 = no limit).  Callers past the limit block on a condition variable
@@ -441,8 +440,7 @@ class PercallGate {
 };
 
 static PercallGate g_percall_gate([] {
-    const char* e = std::getenv("HBEC_PERCALL_CONCURRENCY");
-    return e ? std::max(0, std::atoi(e)) : 16;
+    return (int)std::max(0LL, env_knob("HBEC_PERCALL_CONCURRENCY", 16));
 }());
 
 struct PercallSlot {
@@ -616,7 +614,7 @@ static int host_apply(int rows, int cols, const uint8_t* coeffs, const uint8_t* 
     // reads and writes them in place over PCIe (no staging copies).
     std::vector<hbec_view> zin(cols), zout(rows);
     // (odd lengths / offsets too: apply_views takes them to gf_apply_unaligned)
-    bool zero_copy = len > 0 && (len % 16 == 0 || (g_unaligned_kernel.load() && zero_copy_any_alignment()));
+    bool zero_copy = len > 0 && (len % 16 == 0 || (zero_copy_any_alignment()));
     for (int j = 0; j < cols && zero_copy; ++j) {
         const uint64_t d = pinned_device_addr(in[j], len);
         zero_copy = d != 0;
@@ -931,16 +929,9 @@ int hbec_fill_splitmix(void* dst, uint64_t n_objects, uint64_t obj_len, uint64_t
 }
 
 // ---- Encoder.Verify ------------------------------------------------------
-// Verify of k > 8 data shards (gf_verify_wide): HBEC_WIDE_VERIFY=0
-// falls back to the round-2 kernels (gf_verify_unaligned, k <= 16) and the
+// Verify of k > 8 data shards: gf_verify_wide in one read-only pass; shards
+// beyond the 32-bit kernels' range take gf_verify_unaligned (k <= 16) or the
 // scratch recompute (k > 16).
-static bool wide_verify_enabled() {
-    static const bool on = [] {
-        const char* e = std::getenv("HBEC_WIDE_VERIFY");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
 
 // gf_wide launches over n_obj objects of k input views: per group of <= 8
 // rows one device blob {in_base[k], in_stride[k], tables[k][words]} (the
@@ -1007,10 +998,7 @@ static int wide_launches(const hbec_view* in, int k, const uint8_t* coeffs, int 
 // kernel keeps HBEC_WIDE_D loads in flight per lane, so it needs several waves
 // per SIMD; verify 8 (10+4 46 -> 49 %, r3b5), apply 4 (r3b6)
 static int wide_grid(uint64_t n_tiles, int dflt) {
-    static const int env = [] {
-        const char* e = std::getenv("HBEC_WIDE_BPC");
-        return e ? std::atoi(e) : 0;
-    }();
+    static const int env = (int)tune_knob("HBEC_WIDE_BPC", 0);
     const int bpc = env > 0 ? env : dflt;
     int dev = 0, cus = 256;
     if (current_device(&dev) == HBEC_OK) (void)cu_count(dev, &cus);
@@ -1028,13 +1016,6 @@ static int verify_wide(const hbec_view* views, int k, int m, const uint8_t* prow
 
 // Apply of k > 8 inputs at any alignment in one pass (gf_wide apply):
 // HBEC_WIDE_APPLY=0 keeps the round-2 kernels (passes of <= 16 inputs).
-static bool wide_apply_enabled() {
-    static const bool on = [] {
-        const char* e = std::getenv("HBEC_WIDE_APPLY");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
 
 static int apply_wide(int rows, int cols, const uint8_t* coeffs, const hbec_view* in, const hbec_view* out,
                       uint64_t n_obj, uint64_t shard_len, hipStream_t stream) {
@@ -1147,7 +1128,7 @@ static int verify_views(hbec_codec* c, const hbec_view* views, uint64_t n_obj, u
         return HBEC_OK;
     }
     // k <= 8: gf_odd verify; above, gf_verify_wide (10+4 53 vs 55 %, 12+4 41 vs 54 %, r3b7)
-    if (g_unaligned_kernel.load() && odd_enabled() && k <= 8 && pos32_shard(shard_len)) {
+    if (odd_enabled() && k <= 8 && pos32_shard(shard_len)) {
         // any alignment: recompute and compare in one pass (gf_odd verify), <= 4 rows per launch
         int dev = 0;
         int rc = current_device(&dev);
@@ -1170,12 +1151,12 @@ static int verify_views(hbec_codec* c, const hbec_view* views, uint64_t n_obj, u
         }
         return HBEC_OK;
     }
-    if (g_unaligned_kernel.load() && k > 8 && k <= 256 && pos32_shard(shard_len) && wide_verify_enabled()) {
+    if (k > 8 && k <= 256 && pos32_shard(shard_len)) {
         // k > 8 at any alignment (k > 16 included): one read-only pass per <= 8
         // rows (gf_verify_wide, wide.hip), coefficient tables in LDS
         return verify_wide(views, k, m, prow, n_obj, shard_len, flags, stream);
     }
-    if (g_unaligned_kernel.load() && k <= kMaxK) {
+    if (k <= kMaxK) {
         // any alignment: recompute and compare in one pass (gf_verify_unaligned), <= 4 rows per launch
         int dev = 0, cus = 0;
         int rc = current_device(&dev);

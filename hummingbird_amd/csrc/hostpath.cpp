@@ -114,9 +114,11 @@ struct Ring {
 };
 
 size_t env_size(const char* name, size_t dflt) {
-    const char* e = std::getenv(name);
-    if (!e) return dflt;
-    long long v = std::atoll(e);
+    const long long v = hbec::env_knob(name, 0);
+    return v > 0 ? (size_t)v : dflt;
+}
+size_t tune_size(const char* name, size_t dflt) {
+    const long long v = hbec::tune_knob(name, 0);
     return v > 0 ? (size_t)v : dflt;
 }
 
@@ -174,13 +176,13 @@ int ring_staging_init(Ring& r) {
 int ring_md5_init(Ring& r) {
     if (r.n_arenas > 0) return HBEC_OK;  // set last: everything below exists
     const size_t cap = env_size("HBEC_HASH_ARENA_MB", 1024) << 20;
-    const int n_arenas = (int)std::min<size_t>(Ring::kArenas, std::max<size_t>(2, env_size("HBEC_HASH_ARENAS", 2)));
+    const int n_arenas = (int)std::min<size_t>(Ring::kArenas, std::max<size_t>(2, tune_size("HBEC_HASH_ARENAS", 2)));
     r.arena_cap = std::max(cap, r.in_cap + r.out_cap);
     // MD5 records per arena (32 B pinned each; HBEC_HASH_ARENA_RECS, default
     // 256 K = 8 MiB): an arena is hashed early when its records run out, so
     // this bounds pinned memory, not batch size (one record per 16-B shard
     // would pin 2 GiB per arena)
-    r.arena_rec_cap = std::min<size_t>(r.arena_cap / 16 + 1024, env_size("HBEC_HASH_ARENA_RECS", 1u << 18));
+    r.arena_rec_cap = std::min<size_t>(r.arena_cap / 16 + 1024, tune_size("HBEC_HASH_ARENA_RECS", 1u << 18));
     hipError_t e = hipSuccess;
     for (int a = 0; a < n_arenas && e == hipSuccess; ++a) {  // a failed earlier attempt keeps what it got
         if (!r.s_md5[a]) e = hipStreamCreateWithFlags(&r.s_md5[a], hipStreamNonBlocking);
@@ -264,11 +266,7 @@ std::vector<Ring*> g_free_rings;
 std::map<int, int> g_rings_made;  // per device
 
 int ring_limit() {
-    static const int v = [] {
-        const char* e = std::getenv("HBEC_HOST_RINGS");
-        const int x = e ? std::atoi(e) : 0;
-        return x > 0 ? x : 8;
-    }();
+    static const int v = (int)env_size("HBEC_HOST_RINGS", 8);
     return v;
 }
 
@@ -354,21 +352,15 @@ std::map<uint64_t, PinnedRange> g_pinned;  // host base -> range (hbec_host_allo
 // it streams over PCIe, whose latency wants more requests in flight than
 // HBM's sweet spot of one 4-wave block per CU.
 int zero_copy_blocks_per_cu() {
-    static const int v = [] {
-        const char* e = std::getenv("HBEC_ZC_BLOCKS_PER_CU");
-        const int x = e ? std::atoi(e) : 0;
-        return x > 0 ? x : 2;  // 1: 45.9, 2: 46.7, 4: 46.6, 8: 46.8 GiB/s (profiles/r02_zc_bpc.jsonl)
-    }();
+    // 1: 45.9, 2: 46.7, 4: 46.6, 8: 46.8 GiB/s (profiles/r02_zc_bpc.jsonl)
+    static const int v = (int)tune_size("HBEC_ZC_BLOCKS_PER_CU", 2);
     return v;
 }
 
 // Pinned stripes that are not 16-B aligned (or S % 16 != 0): zero-copy through
 // the unaligned kernel (default) or, with HBEC_ZC_UNALIGNED=0, the staged ring.
 bool zero_copy_unaligned_enabled() {
-    static const bool on = [] {
-        const char* e = std::getenv("HBEC_ZC_UNALIGNED");
-        return !e || std::atoi(e) != 0;
-    }();
+    static const bool on = hbec::tune_knob("HBEC_ZC_UNALIGNED", 1) != 0;
     return on;
 }
 
@@ -379,18 +371,12 @@ bool zero_copy_unaligned_enabled() {
 // GiB/s, 4 KiB stripes 42.2 -> 45.1 GiB/s; 32 and 128 blocks tie with 64
 // (profiles/r02_zc_grid.jsonl).
 int zero_copy_max_blocks() {
-    static const int v = [] {
-        const char* e = std::getenv("HBEC_ZC_GRID");
-        return e ? std::max(0, std::atoi(e)) : 64;
-    }();
+    static const int v = (int)std::max(0LL, hbec::tune_knob("HBEC_ZC_GRID", 64));
     return v;
 }
 
 bool zero_copy_enabled() {
-    static const bool on = [] {
-        const char* e = std::getenv("HBEC_ZEROCOPY");
-        return !(e && e[0] == '0');
-    }();
+    static const bool on = hbec::env_knob("HBEC_ZEROCOPY", 1) != 0;
     return on;
 }
 
@@ -400,7 +386,7 @@ bool zero_copy_enabled() {
 // pinned, device-mapped allocation; 0 otherwise.  hbec_host_alloc ranges are
 // looked up in the registry; other pinned memory is asked of the runtime at
 // both ends of the range.
-bool hbec::zero_copy_any_alignment() { return zero_copy_unaligned_enabled() && unaligned_kernel_enabled(); }
+bool hbec::zero_copy_any_alignment() { return zero_copy_unaligned_enabled(); }
 
 uint64_t hbec::pinned_device_addr(const void* p, uint64_t len) {
     if (!zero_copy_enabled()) return 0;
@@ -673,10 +659,7 @@ int zero_copy_unaligned_md5_run(Ring* ring, const std::vector<ZcStripe>& zs, con
 std::atomic<uint64_t> g_md5_zc_calls{0}, g_md5_ring_calls{0};
 
 bool zero_copy_md5_enabled() {
-    static const bool on = [] {
-        const char* e = std::getenv("HBEC_MD5_ZEROCOPY");
-        return !(e && e[0] == '0');
-    }();
+    static const bool on = hbec::tune_knob("HBEC_MD5_ZEROCOPY", 1) != 0;
     return on;
 }
 

@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "../../include/hbec.h"
+#include "kernels.h"
 
 namespace hbec {
 
@@ -32,6 +33,9 @@ int guarded(const char* entry, F&& body) noexcept {
 }
 
 // Queue out[r] (^)= XOR_c coeffs[r][c] * in[c] over n_obj strided objects.
+// Caps the grids of this thread's apply launches (0 = none); used around the
+// encode launches of the encode + ShardHash pipeline.
+void set_thread_grid_cap(int blocks);
 int apply_views(int rows, int cols, const uint8_t* coeffs, const hbec_view* in, const hbec_view* out,
                 uint64_t n_obj, uint64_t shard_len, hipStream_t stream);
 
@@ -45,11 +49,8 @@ void scratch_free(void* p, hipStream_t stream);
 // HBEC_ZEROCOPY=0).  The zero-copy host paths code such memory in place.
 uint64_t pinned_device_addr(const void* p, uint64_t len);
 // Pinned stripes at any alignment / shard length are coded in place over PCIe
-// (gf_apply_unaligned_plan) unless HBEC_ZC_UNALIGNED=0 or HBEC_UNALIGNED=0.
+// (the gf_odd plan kernel) unless HBEC_ZC_UNALIGNED=0.
 bool zero_copy_any_alignment();
-// The unaligned kernels (gf_odd / gf_apply_unaligned) are on unless
-// HBEC_UNALIGNED=0 (round-1 byte kernel; every path honours the same switch).
-bool unaligned_kernel_enabled();
 
 // ShardHash of a list of device chains: records {addr, len, slot, 0} (32 B
 // each, device memory), digest of record i at digest + slot * 16.

@@ -5,6 +5,26 @@
 
 namespace hbec {
 
+// ---- Environment knobs ----
+// env_knob is the library's one reader of the environment (hbec.cpp): the
+// value of `name` as an integer, dflt when unset or empty.  Operational knobs
+// (the table in include/hbec.h) call it directly.  Tuning knobs call
+// tune_knob, which reads the environment only in tuning builds
+// (-DHBEC_TUNE=1, scripts/tune*.py); the product build compiles each to its
+// default.
+long long env_knob(const char* name, long long dflt);
+#ifndef HBEC_TUNE
+#define HBEC_TUNE 0
+#endif
+inline long long tune_knob(const char* name, long long dflt) {
+#if HBEC_TUNE
+    return env_knob(name, dflt);
+#else
+    (void)name;
+    return dflt;
+#endif
+}
+
 constexpr int kMaxK = 16;         // inputs per kernel pass
 constexpr int kMaxR = 4;          // outputs per kernel pass
 constexpr int kBlockThreads = 256;
@@ -97,7 +117,6 @@ __host__ __device__ constexpr int verify_u(int k) {
 }
 
 hipError_t launch_vec(int k, int r, const PassArgs& a, int grid, hipStream_t stream, int force_stream);
-hipError_t launch_bytes(int k, int r, const PassArgs& a, int grid, hipStream_t stream);
 // Any alignment / stride / length with aligned 16-B accesses (gf_apply_unaligned):
 // wave tiles of 4 windows x 1008 B of one object's shard column.
 uint32_t unaligned_tiles_per_obj(uint64_t shard_len);
@@ -169,7 +188,15 @@ uint32_t odd_plan_tile_bytes();       // shard bytes per plan record
 uint32_t odd_tiles_per_obj(int k, int mode, uint64_t shard_len);
 // shards of at most this many bytes are coded by gf_odd_edges alone
 uint64_t odd_min_main();
-hipError_t launch_odd(int k, int r, int mode, const PassArgs& a, uint32_t* flags, int grid, hipStream_t stream);
+// Strided passes code from per-object records (gf_odd_rec): launch_odd_objrec
+// writes odd_rec_words(k, r, mode) words per object of a.n_obj objects into
+// recs (device), before the main launches, whose `recs` point at their first
+// object's record.  Without records (odd_uses_records() false) recs is unused.
+bool odd_uses_records();
+uint32_t odd_rec_words(int k, int r, int mode);
+hipError_t launch_odd_objrec(int k, int r, int mode, const PassArgs& a, uint32_t* recs, hipStream_t stream);
+hipError_t launch_odd(int k, int r, int mode, const PassArgs& a, uint32_t* flags, const uint32_t* recs, int grid,
+                      hipStream_t stream);
 // the guard-band bytes of every shard (after the main launches of a pass;
 // k <= kMaxK inputs, a.n_obj objects; verify flags mismatching objects)
 hipError_t launch_odd_edges(int k, int r, int mode, const PassArgs& a, uint32_t* flags, hipStream_t stream);

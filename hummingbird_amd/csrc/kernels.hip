@@ -554,48 +554,12 @@ __global__ __launch_bounds__(kBlockThreads, kVecWavesPerSimd) void gf_apply_vec_
     }
 }
 
-// Byte path: any alignment / length (small or odd shards).  Each thread owns
-// 4 consecutive bytes of one shard column.
-__global__ __launch_bounds__(kBlockThreads) void gf_apply_bytes(PassArgs a, int K, int R) {
-    const uint64_t words = (a.shard_len + 3) / 4;
-    const uint64_t total = words * a.n_obj;
-    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < total;
-         v += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t obj = v / words;
-        const uint64_t off = (v - obj * words) * 4;
-        const int nb = (a.shard_len - off) >= 4 ? 4 : (int)(a.shard_len - off);
-        uint32_t acc[kMaxR] = {0, 0, 0, 0};
-        if (a.accumulate) {
-            for (int r = 0; r < R; ++r) {
-                const uint8_t* d = a.out[r] + obj * a.out_stride[r] + off;
-                uint32_t w = 0;
-                for (int b = 0; b < nb; ++b) w |= (uint32_t)d[b] << (8 * b);
-                acc[r] = w;
-            }
-        }
-        for (int j = 0; j < K; ++j) {
-            const uint8_t* s = a.in[j] + obj * a.in_stride[j] + off;
-            uint32_t w = 0;
-            for (int b = 0; b < nb; ++b) w |= (uint32_t)s[b] << (8 * b);
-            const Sel sx = selectors(w);
-            for (int r = 0; r < R; ++r) {
-                const uint32_t* t = a.tab[r][j];
-                acc[r] ^= gf_mul_sel(sx, t[0], t[1], t[2], t[3], t[4]);
-            }
-        }
-        for (int r = 0; r < R; ++r) {
-            uint8_t* d = a.out[r] + obj * a.out_stride[r] + off;
-            for (int b = 0; b < nb; ++b) d[b] = (uint8_t)(acc[r] >> (8 * b));
-        }
-    }
-}
-
 // ---------------------------------------------------------------------------
 // gf_apply_unaligned: any base alignment, any stride, any shard length.  ecSplit
 // sets S = ceil(len / k) (ecutils.go:14-24), so S is a multiple of 16 for only
 // 1 object size in 16, and its databuf puts shard i at i*S (ecutils.go:31-35):
-// an arbitrary object's shards start at arbitrary byte offsets.  The byte
-// kernel above codes them at ~20 % of HBM; this one keeps 16-B accesses, and
+// an arbitrary object's shards start at arbitrary byte offsets.  Round 1's
+// byte-per-lane kernel coded them at ~20 % of HBM; this one keeps 16-B accesses, and
 // every access is 16-B ALIGNED:
 //  * input j of an object starts d_j = base & 15 bytes into an aligned block
 //    (d_j is wave-uniform: one object per wave tile).  A lane loads the two
@@ -989,14 +953,8 @@ static uint64_t packed_max_shard(int k) {
 // Tuning knobs: HBEC_PACKED=0 sends short shards back to gf_apply_vec (A/B);
 // HBEC_PACKED_MAX_SHARD=B takes shards shorter than B bytes (instead of
 // shorter than one pipelined tile) through the packed kernel.
-static const bool g_packed_on = [] {
-    const char* e = std::getenv("HBEC_PACKED");
-    return !(e && e[0] == '0');
-}();
-static const uint64_t g_packed_max = [] {
-    const char* e = std::getenv("HBEC_PACKED_MAX_SHARD");
-    return e ? (uint64_t)std::atoll(e) : 0ull;
-}();
+static const bool g_packed_on = tune_knob("HBEC_PACKED", 1) != 0;
+static const uint64_t g_packed_max = (uint64_t)std::max(0LL, tune_knob("HBEC_PACKED_MAX_SHARD", 0));
 
 int is_packed_shape(int k, int r, uint64_t shard_len, int accumulate, int force_stream) {
     return (HBEC_USE_PACKED && g_packed_on && !force_stream && !accumulate && shard_len >= 16 && shard_len % 16 == 0 &&
@@ -1068,10 +1026,6 @@ hipError_t launch_vec(int k, int r, const PassArgs& a, int grid, hipStream_t str
     return hipLaunchKernel(fn, dim3(grid), dim3(kBlockThreads), args, 0, stream);
 }
 
-hipError_t launch_bytes(int k, int r, const PassArgs& a, int grid, hipStream_t stream) {
-    hipLaunchKernelGGL(gf_apply_bytes, dim3(grid), dim3(kBlockThreads), 0, stream, a, k, r);
-    return hipGetLastError();
-}
 
 static const void* unaligned_kernel(int r) {
     switch (r) {

@@ -165,6 +165,81 @@ __global__ __launch_bounds__(kBlockThreads) void gf_odd_edges_plan(UPlanArgs p, 
     }
 }
 
+// ---------------------------------------------------------------------------
+// gf_odd_objrec: the object records gf_odd_rec reads (layout: OddRec,
+// odd_impl.h), one thread per object of a strided pass.  mode 2 (verify)
+// records the stored parity as loaded shards K..K+R-1 and the compared band.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int32_t ceil16(int32_t x) { return (x + 15) & ~15; }
+__device__ __forceinline__ int32_t floor16(int32_t x) { return x & ~15; }
+
+__global__ __launch_bounds__(kBlockThreads) void gf_odd_objrec(PassArgs a, int K, int R, int mode, uint32_t fw,
+                                                              uint32_t rw, uint32_t* __restrict__ recs) {
+    const uint64_t obj = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (obj >= a.n_obj) return;
+    const int32_t S = (int32_t)a.shard_len;
+    // frame: output 0's 16-B grid, first column at c0 in [0, 16)
+    const int32_t c0 = (int32_t)((0u - (uint32_t)(reinterpret_cast<uint64_t>(a.out[0]) + obj * a.out_stride[0])) & 15u);
+    const int32_t hi = S - kOddGuard - 16;  // last block start stored / compared
+    const int NL = K + (mode == kOddVerify ? R : 0), NO = mode == kOddVerify ? 0 : R;
+    uint32_t* f = recs + obj * rw;
+    uint32_t* l = f + fw;
+    uint32_t shp = 0, dlp = 0;
+    for (int s = 0; s < NL; ++s) {
+        const uint64_t b = s < K ? reinterpret_cast<uint64_t>(a.in[s]) + obj * a.in_stride[s]
+                                 : reinterpret_cast<uint64_t>(a.out[s - K]) + obj * a.out_stride[s - K];
+        const int32_t t0 = (int32_t)(b & 3u) + c0;  // column 0's first byte, from the shard's dword base
+        const uint64_t base = (b & ~(uint64_t)3) + (uint64_t)(t0 & ~3);
+        l[3 * s] = (uint32_t)base;
+        l[3 * s + 1] = (uint32_t)(base >> 32);
+        l[3 * s + 2] = (uint32_t)(S - 16 - (t0 & ~3));  // blocks end inside the shard's dwords
+        shp |= ((uint32_t)t0 & 3u) << (2 * s);
+    }
+    for (int r = 0; r < NO; ++r) {
+        const uint64_t o = reinterpret_cast<uint64_t>(a.out[r]) + obj * a.out_stride[r];
+        const uint32_t dl = (0u - ((uint32_t)o + (uint32_t)c0)) & 15u;
+        const uint64_t q = o + (uint64_t)(c0 + (int32_t)dl);  // 16-B aligned
+        const int32_t lo = ceil16(kOddGuard - c0 - (int32_t)dl), top = floor16(hi - c0 - (int32_t)dl);
+        const uint32_t width = (uint32_t)(top >= lo ? top - lo : 0);  // S > kOddMinMain: never empty
+        f[4 + 4 * r] = (uint32_t)q;
+        f[5 + 4 * r] = (uint32_t)(q >> 32);
+        f[6 + 4 * r] = (uint32_t)lo;
+        f[7 + 4 * r] = width;
+        if (mode == kOddAcc) {  // the old blocks, loaded with the inputs
+            l[3 * NL + 4 * r] = (uint32_t)q;
+            l[3 * NL + 4 * r + 1] = (uint32_t)(q >> 32);
+            l[3 * NL + 4 * r + 2] = (uint32_t)lo;
+            l[3 * NL + 4 * r + 3] = (uint32_t)lo + width;
+        }
+        dlp |= dl << (4 * r);
+    }
+    const int32_t vlo = ceil16(kOddGuard - c0), vtop = floor16(hi - c0);
+    f[0] = shp;
+    f[1] = dlp;
+    f[2] = (uint32_t)vlo;
+    f[3] = (uint32_t)(vtop >= vlo ? vtop - vlo : 0);
+}
+
+static uint32_t odd_rec_fw(int r, int mode) { return (uint32_t)((4 + 4 * (mode == kOddVerify ? 0 : r) + 7) & ~7); }
+
+uint32_t odd_rec_words(int k, int r, int mode) {
+    const int nl = k + (mode == kOddVerify ? r : 0), la = mode == kOddAcc ? 4 * r : 0;
+    return odd_rec_fw(r, mode) + (uint32_t)((3 * nl + la + 7) & ~7);
+}
+
+bool odd_uses_records() { return HBEC_ODD_REC != 0; }
+
+hipError_t launch_odd_objrec(int k, int r, int mode, const PassArgs& a, uint32_t* recs, hipStream_t stream) {
+    if (a.n_obj == 0) return hipSuccess;
+    if (k < 1 || k > kOddMaxK || r < 1 || r > kMaxR || !pos32_shard(a.shard_len) || a.shard_len <= kOddMinMain)
+        return hipErrorInvalidValue;
+    const uint64_t grid = (a.n_obj + kBlockThreads - 1) / kBlockThreads;
+    if (grid >= (1ull << 31)) return hipErrorInvalidValue;
+    uint32_t fw = odd_rec_fw(r, mode), rw = odd_rec_words(k, r, mode);
+    void* args[] = {const_cast<PassArgs*>(&a), &k, &r, &mode, &fw, &rw, &recs};
+    return hipLaunchKernel((const void*)&gf_odd_objrec, dim3((unsigned)grid), dim3(kBlockThreads), args, 0, stream);
+}
+
 static const void* odd_kernel(int k, int r, int mode, bool plan, bool mirror = false, bool carry = false) {
     if (k <= 4) return odd_kernel_range<1, 4>(k, r, mode, plan, mirror, carry);
     if (k <= 8) return odd_kernel_k58(k, r, mode, plan, mirror);
@@ -175,10 +250,7 @@ static const void* odd_kernel(int k, int r, int mode, bool plan, bool mirror = f
 #define HBEC_ODD_DEFAULT 1
 #endif
 bool odd_enabled() {
-    static const bool on = [] {
-        const char* e = std::getenv("HBEC_ODD");
-        return e ? e[0] != '0' : HBEC_ODD_DEFAULT != 0;
-    }();
+    static const bool on = tune_knob("HBEC_ODD", HBEC_ODD_DEFAULT) != 0;
     return on;
 }
 
@@ -189,10 +261,7 @@ bool odd_enabled() {
 #define HBEC_ODD_BPC_VERIFY 2  // read-only: 4+2 68.5 -> 81 % with 2 blocks per CU (r03_tune_odd3)
 #endif
 int odd_blocks_per_cu(int mode, int k, int r, bool mirror) {
-    static const int v = [] {
-        const char* e = std::getenv("HBEC_ODD_BPC");
-        return e ? std::atoi(e) : 0;
-    }();
+    static const int v = (int)tune_knob("HBEC_ODD_BPC", 0);
     if (v > 0) return v;
     if (mode == kOddVerify) return HBEC_ODD_BPC_VERIFY;
     return odd_two_blocks(k, r, mode, mirror) ? 2 : HBEC_ODD_BPC_APPLY;  // launch bounds sized for it (odd_lb)
@@ -221,19 +290,22 @@ uint32_t odd_plan_tile_bytes() { return (uint32_t)kOddPlanU * kOddWin; }
 // the frame's first column (c0 >= -32) to position S.
 uint32_t odd_tiles_per_obj(int k, int mode, uint64_t shard_len) {
     const uint64_t span = shard_len + 32u;
-    const uint64_t tile = mode == kOddVerify ? (uint64_t)odd_u(k, mode) * odd_win<kOddVerify>()
-                                             : (odd_u(k, mode) == 2 && HBEC_ODD_CARRY ? (uint64_t)(64 + kOddStore) * 16u
-                                                                                       : (uint64_t)odd_u(k, mode) * kOddWin);
+    const uint64_t tile = HBEC_ODD_REC ? (uint64_t)odd_rec_span(odd_u(k, mode), mode)
+                          : mode == kOddVerify ? (uint64_t)odd_u(k, mode) * odd_win<kOddVerify>()
+                                               : (odd_u(k, mode) == 2 && HBEC_ODD_CARRY ? (uint64_t)(64 + kOddStore) * 16u
+                                                                                         : (uint64_t)odd_u(k, mode) * kOddWin);
     return (uint32_t)((span + tile - 1) / tile);
 }
 
 bool odd_supported(int k, int r) { return k >= 1 && k <= kOddMaxK && r >= 1 && r <= kMaxR; }
 
-hipError_t launch_odd(int k, int r, int mode, const PassArgs& a, uint32_t* flags, int grid, hipStream_t stream) {
+hipError_t launch_odd(int k, int r, int mode, const PassArgs& a, uint32_t* flags, const uint32_t* recs, int grid,
+                      hipStream_t stream) {
     if (!pos32_shard(a.shard_len)) return hipErrorInvalidValue;  // 32-bit shard positions
+    if (HBEC_ODD_REC && !recs) return hipErrorInvalidValue;
     const void* fn = odd_kernel(k, r, mode, false);
     if (!fn) return hipErrorInvalidValue;
-    void* args[] = {const_cast<PassArgs*>(&a), &flags};
+    void* args[] = {const_cast<PassArgs*>(&a), &flags, &recs};
     return hipLaunchKernel(fn, dim3(grid), dim3(kPipeBlockThreads), args, 0, stream);
 }
 

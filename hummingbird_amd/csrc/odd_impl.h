@@ -74,6 +74,9 @@ constexpr uint64_t kOddMinMain = (uint64_t)kOddEdgeSlots;
 #ifndef HBEC_ODD_LDSTAB
 #define HBEC_ODD_LDSTAB 0  // 1: K > 8 read the coefficient tables from LDS per input (fewer VGPRs, more waves)
 #endif
+#ifndef HBEC_ODD_SCHED
+#define HBEC_ODD_SCHED 1  // record kernels: scheduling barrier after the next tile's loads
+#endif
 #ifndef HBEC_ODD_PLAN_U
 #define HBEC_ODD_PLAN_U 2  // windows per plan record (2: odd 4+2 stripe plan 52.9 -> 59.5 %, r03b4)
 #endif
@@ -86,6 +89,35 @@ __host__ __device__ constexpr int odd_u(int k, int mode = kOddApply) {
                : (k <= 4 ? (HBEC_ODD_U_SMALL > 0 ? HBEC_ODD_U_SMALL : (4 / k)) : (k <= 8 ? HBEC_ODD_U_MID : 1));
 }
 constexpr int kOddPlanU = HBEC_ODD_PLAN_U;  // plans: windows per record
+
+// Record kernels (gf_odd_rec): the windows of a wave tile are contiguous
+// columns, and each window but the last takes its lane 63's missing next
+// dword from the following window's lane 0.  Apply / accumulate (U == 2):
+// window 0 stores 64 blocks, window 1 62 (its outputs are realigned, which
+// needs lane l+1's column).  Verify (HBEC_ODD_VCARRY, any U >= 2): windows
+// 0..U-2 compare 64 columns, the last 63, so a tile of 64 U loaded blocks
+// compares 64 U - 1 and neighbouring tiles share one column instead of one
+// per window (odd Verify read 1.067 x its bytes with 63-column windows).
+#ifndef HBEC_ODD_VCARRY
+#define HBEC_ODD_VCARRY 1
+#endif
+__host__ __device__ constexpr bool odd_rec_carry(int u, int mode) {
+    return mode == kOddVerify ? (HBEC_ODD_VCARRY != 0 && u >= 2) : (HBEC_ODD_CARRY != 0 && u == 2);
+}
+// unrolled by two (no register copies between tiles) unless two live tile
+// buffers would not fit: the 2-block pinned shapes (10+4: 175 VGPRs spilled)
+#ifndef HBEC_ODD_UNROLL
+#define HBEC_ODD_UNROLL 1
+#endif
+__host__ __device__ constexpr bool odd_two_blocks(int k, int r, int mode, bool mir);
+__host__ __device__ constexpr bool odd_rec_unroll(int k, int r, int mode) {
+    return HBEC_ODD_UNROLL != 0 && !odd_two_blocks(k, r, mode, false);
+}
+// shard bytes per wave tile of the record kernel
+__host__ __device__ constexpr uint32_t odd_rec_span(int u, int mode) {
+    return odd_rec_carry(u, mode) ? (mode == kOddVerify ? (64u * (uint32_t)u - 1u) * 16u : (64u + kOddStore) * 16u)
+                                  : (uint32_t)u * (mode == kOddVerify ? 63u : kOddStore) * 16u;
+}
 
 // One tile, wave-uniform.  Positions are 32-bit: the host sends shards of
 // 2^31 bytes or more to the round-2 kernels.
@@ -557,6 +589,327 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_lb<K, R, MODE>())) void gf_
     odd_body<K, R, U, MODE>(OddStrided<K, R, U, MODE>{a}, a.n_tiles, a.tab, flags);
 }
 
+// ---------------------------------------------------------------------------
+// Object records (strided batches).  Everything gf_odd's loads and finish need
+// of an object's shards is fixed per object: the column frame, each loaded
+// shard's dword-aligned block base and byte shift, each output's aligned block
+// grid and guard band.  gf_odd_objrec (odd.hip) writes it once per object; the
+// tile loop (gf_odd_rec) reads it with scalar loads issued a tile or two ahead
+// and adds only the tile position.  The per-tile arithmetic this replaces
+// (64-bit object bases of K + R shards and their alignment: ~250 SALU per tile
+// at 8+3, profiles/r04_sq_odd.json) issued in the same slots as the field
+// arithmetic at one wave per SIMD.
+//
+// Frame: columns at shard positions c0 + V, c0 = (-out0) mod 16 (output 0's
+// 16-B grid), V = ti * span + 16 * column >= 0.
+// Record (OddRec::RW words, 32-B multiples):
+//   F part (finish), words [0, FW): [0] shifts (2 bits per loaded shard),
+//     [1] realigns (4 bits per output), [2], [3] verify band (lo, width on V);
+//     then per output r (apply / accumulate): Q lo, Q hi, lo, width.
+//   L part (loads), words [FW, FW + LW): per loaded shard s (inputs, then
+//     verify's stored parity): B lo, B hi, lim; accumulate passes then per
+//     output: Q lo, Q hi, lo, lo + width (the old blocks are loaded too).
+// Loaded shard s: the dword-aligned block holding column V's first byte is at
+// B + min_u32(V, lim) (B = base + c0 rounded down to a dword, lim = S - 16 - t0
+// keeps every block inside the shard; the clamp only moves columns the guard
+// band keeps from any store).  Output r: block at Q + V, stored when
+// (V - lo) <= width (unsigned).
+// ---------------------------------------------------------------------------
+template <int U, int MODE, bool CARRY>
+__host__ __device__ constexpr uint32_t odd_rec_wcol(int u) { return CARRY ? 64u * (uint32_t)u : odd_store<MODE>() * (uint32_t)u; }
+
+template <int K, int R, int MODE>
+struct OddRec {
+    static constexpr int NL = K + (MODE == kOddVerify ? R : 0);
+    static constexpr int NO = MODE == kOddVerify ? 0 : R;
+    static constexpr int FW = (4 + 4 * NO + 7) & ~7;
+    // accumulate passes also load the old output blocks: Q lo, Q hi, lo, hi per output
+    static constexpr int LA = MODE == kOddAcc ? 4 * R : 0;
+    static constexpr int LW = (3 * NL + LA + 7) & ~7;
+    static constexpr int RW = FW + LW;
+};
+
+typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
+
+// Scalar loads issued by hand: the compiler re-issues loads of read-only
+// memory right before their use (to save SGPRs), which exposed their latency
+// once per tile.  odd_sload only issues; odd_swait (lgkmcnt(0), then an empty
+// asm per vector) orders every use after the data has landed.
+template <int N>
+__device__ __forceinline__ void odd_sload(u32x8 (&v)[N], const uint32_t* p) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) asm volatile("s_load_dwordx8 %0, %1, %2" : "=s"(v[i]) : "s"(p), "n"(32 * i));
+}
+template <int N>
+__device__ __forceinline__ void odd_swait_pin(u32x8 (&v)[N]) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) asm volatile("" : "+s"(v[i]));
+}
+__device__ __forceinline__ void odd_swait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+template <int N>
+__device__ __forceinline__ uint32_t odd_w(const u32x8 (&v)[N], int i) { return v[i / 8][i % 8]; }
+
+template <int K, int R, int MODE>
+struct OddRT {  // the finish's scalars of one tile
+    u32x8 f[OddRec<K, R, MODE>::FW / 8];
+    uint32_t v0;  // ti * span
+    uint32_t obj, live;
+};
+
+template <int K, int R, int U, int MODE, bool CARRY>
+__device__ __forceinline__ void odd_rec_load(OddRegs<K, R, U, MODE>& X, const u32x8 (&l)[OddRec<K, R, MODE>::LW / 8],
+                                             uint32_t v0, uint32_t lane) {
+    using RC = OddRec<K, R, MODE>;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint32_t v = v0 + 16u * odd_rec_wcol<U, MODE, CARRY>(u) + 16u * lane;
+#pragma unroll
+        for (int j = 0; j < RC::NL; ++j) {
+            const uint64_t b = (uint64_t)odd_w(l, 3 * j) | ((uint64_t)odd_w(l, 3 * j + 1) << 32);
+            X.x[u][j] = ld16_addr(b + __builtin_elementwise_min(v, odd_w(l, 3 * j + 2)));
+        }
+    }
+    if constexpr (MODE == kOddAcc) {
+        // the old output block each lane will rewrite, clamped into the band
+        // (lanes that store nothing read one inside it)
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            constexpr int o = 3 * RC::NL;
+            const uint64_t q = (uint64_t)odd_w(l, o + 4 * r) | ((uint64_t)odd_w(l, o + 1 + 4 * r) << 32);
+            const uint32_t lo = odd_w(l, o + 2 + 4 * r), hi = odd_w(l, o + 3 + 4 * r);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t v = v0 + 16u * odd_rec_wcol<U, MODE, CARRY>(u) + 16u * lane;
+                X.x[u][K + r] = ld16_addr(q + __builtin_elementwise_min(__builtin_elementwise_max(v, lo), hi));
+            }
+        }
+    }
+}
+
+template <int K, int R, int U, int MODE, bool CARRY>
+__device__ __forceinline__ void odd_rec_finish(const OddRegs<K, R, U, MODE>& X, const OddRT<K, R, MODE>& t,
+                                               const TabArray& tab, const Tables<K, R, HBEC_ODD_VMIN>& tb,
+                                               uint32_t lane, uint32_t* flags) {
+    constexpr int NL = OddRec<K, R, MODE>::NL;
+    const uint32_t shp = odd_w(t.f, 0), dlp = odd_w(t.f, 1);
+    // v_alignbyte reads bits [1:0] of its shift: the packed shifts need no mask
+    uint32_t sh[NL];
+#pragma unroll
+    for (int j = 0; j < NL; ++j) sh[j] = shp >> (2 * j);
+    uint32_t dl[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) dl[r] = (dlp >> (4 * r)) & 15u;
+    auto st_mask = [&](int r, uint32_t v, uint32_t lanes) {
+        return t.live != 0u && lane < lanes && (v - odd_w(t.f, 6 + 4 * r)) <= odd_w(t.f, 7 + 4 * r);
+    };
+    auto q_addr = [&](int r, uint32_t v) {
+        return ((uint64_t)odd_w(t.f, 4 + 4 * r) | ((uint64_t)odd_w(t.f, 5 + 4 * r) << 32)) + v;
+    };
+    if constexpr (CARRY && MODE == kOddVerify) {
+        // chained windows: window u < U-1 compares all 64 columns (lane 63
+        // borrows window u+1's first dword), the last window 63
+        bool bad = false;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t v = t.v0 + 16u * 64u * (uint32_t)u + 16u * lane;
+            u32x4 x[K];
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+                x[j] = u + 1 < U ? odd_shift_in_fill<4u>(X.x[u][j], sh[j], lane0(X.x[u + 1 < U ? u + 1 : u][j]))
+                                 : odd_shift_in<4u>(X.x[u][j], sh[j]);
+            u32x4 acc[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) acc[r] = u32x4{0, 0, 0, 0};
+            gf_dot<K, R, HBEC_ODD_VMIN>(acc, x, tab, tb);
+            odd_pin<K, R, MODE, false>(acc);
+            const bool mine = t.live != 0u && (u + 1 < U || lane < 63u) && (v - odd_w(t.f, 2)) <= odd_w(t.f, 3);
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const u32x4 st = u + 1 < U ? odd_shift_in_fill<4u>(X.x[u][K + r], sh[K + r], lane0(X.x[u + 1 < U ? u + 1 : u][K + r]))
+                                           : odd_shift_in<4u>(X.x[u][K + r], sh[K + r]);
+                const u32x4 df = st ^ acc[r];
+                bad |= mine && (df[0] | df[1] | df[2] | df[3]) != 0u;
+            }
+        }
+        if (__any(bad)) {
+            if (lane == 0u) atomicOr(flags + t.obj, 1u);
+        }
+        return;
+    } else if constexpr (CARRY) {
+        static_assert(U == 2, "apply carry: 2 windows");
+        u32x4 x1[K], x0[K], acc1[R], acc0[R];
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            x1[j] = odd_shift_in<4u>(X.x[1][j], sh[j]);
+            x0[j] = odd_shift_in_fill<4u>(X.x[0][j], sh[j], lane0(X.x[1][j]));
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc1[r] = acc0[r] = u32x4{0, 0, 0, 0};
+        gf_dot<K, R, HBEC_ODD_VMIN>(acc1, x1, tab, tb);
+        gf_dot<K, R, HBEC_ODD_VMIN>(acc0, x0, tab, tb);
+        odd_pin<K, R, MODE, false>(acc1);
+        odd_pin<K, R, MODE, false>(acc0);
+        const uint32_t v0 = t.v0 + 16u * lane, v1 = v0 + 1024u;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            u32x4 b0 = acc0[r], b1 = acc1[r];
+            if (dl[r] != 0u) {  // wave-uniform (never r = 0)
+                b0 = realign16(acc0[r], lane_next4_fill(acc0[r], lane0(acc1[r])), dl[r]);
+                b1 = realign16(acc1[r], lane_next4(acc1[r]), dl[r]);
+            }
+            if constexpr (MODE == kOddAcc) {
+                b0 ^= X.x[0][K + r];
+                b1 ^= X.x[1][K + r];
+            }
+            odd_st(q_addr(r, v0), b0, st_mask(r, v0, 64u));
+            odd_st(q_addr(r, v1), b1, st_mask(r, v1, kOddStore));
+        }
+        return;
+    }
+    bool bad = false;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint32_t v = t.v0 + 16u * odd_rec_wcol<U, MODE, CARRY>(u) + 16u * lane;  // this lane's column
+        u32x4 x[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) x[j] = odd_shift_in<4u>(X.x[u][j], sh[j]);
+        u32x4 acc[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r] = u32x4{0, 0, 0, 0};
+        gf_dot<K, R, HBEC_ODD_VMIN>(acc, x, tab, tb);
+        odd_pin<K, R, MODE, false>(acc);
+        if constexpr (MODE == kOddVerify) {
+            const bool mine = t.live != 0u && lane < odd_store<MODE>() && (v - odd_w(t.f, 2)) <= odd_w(t.f, 3);
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const u32x4 df = odd_shift_in<4u>(X.x[u][K + r], sh[K + r]) ^ acc[r];
+                bad |= mine && (df[0] | df[1] | df[2] | df[3]) != 0u;
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                u32x4 blk = acc[r];
+                if (dl[r] != 0u) blk = realign16(acc[r], lane_next4(acc[r]), dl[r]);  // wave-uniform (never r = 0)
+                if constexpr (MODE == kOddAcc) blk ^= X.x[u][K + r];
+                odd_st(q_addr(r, v), blk, st_mask(r, v, kOddStore));
+            }
+        }
+    }
+    if constexpr (MODE == kOddVerify) {
+        if (__any(bad)) {
+            if (lane == 0u) atomicOr(flags + t.obj, 1u);
+        }
+    }
+}
+
+// A wave's tiles t0, t0 + nw, ...: (object, tile in object), stepped by
+// (qq, rr) = divmod(nw, tpo).  Stand-in tiles past the end (obj >= n_obj)
+// load the last tile and store nothing.
+struct OddPos {
+    uint32_t obj, ti;
+};
+
+template <int K, int R, int MODE>
+__global__ __launch_bounds__(kPipeBlockThreads, (odd_lb<K, R, MODE>())) void gf_odd_rec(PassArgs a, uint32_t* flags,
+                                                                                        const uint32_t* __restrict__ recs) {
+    using RC = OddRec<K, R, MODE>;
+    constexpr int U = odd_u(K, MODE);
+    constexpr bool CARRY = odd_rec_carry(U, MODE);
+    constexpr uint32_t SPAN = odd_rec_span(U, MODE);
+    static_assert(odd_ld_align<K>() == 4u, "records hold dword-aligned block bases");
+    constexpr uint32_t WPB = kPipeBlockThreads / 64;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t nw = gridDim.x * WPB;
+    const uint32_t n = a.n_tiles, tpo = a.tiles_per_obj, n_obj = (uint32_t)a.n_obj;
+    const uint32_t wave0 = __builtin_amdgcn_readfirstlane(xcd_block() * WPB);
+    const uint32_t dw = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (wave0 >= n) return;  // whole blocks only: the loop below has block barriers
+    const Tables<K, R, HBEC_ODD_VMIN> tb = load_tables<K, R, HBEC_ODD_VMIN>(a.tab);
+    const uint32_t qq = nw / tpo, rr = nw - qq * tpo;
+    auto step = [&](OddPos p) {
+        p.ti += rr;
+        p.obj += qq;
+        if (p.ti >= tpo) {
+            p.ti -= tpo;
+            p.obj += 1u;
+        }
+        return p;
+    };
+    auto rec = [&](const OddPos& p) {
+        return recs + (size_t)__builtin_amdgcn_readfirstlane(p.obj < n_obj ? p.obj : n_obj - 1u) * RC::RW;
+    };
+    auto v0 = [&](const OddPos& p) { return (p.obj < n_obj ? p.ti : tpo - 1u) * SPAN; };
+    // Unrolled by two over buffers X and Y, so no tile's registers are
+    // copied: each half issues one buffer's loads (tile P, L = its load
+    // record, waited), fetches the next tile's load record into L and P's
+    // finish record, then codes the other buffer's tile.
+    OddPos p;
+    {
+        const uint32_t t = wave0 + dw;
+        p.obj = t / tpo;
+        p.ti = t - p.obj * tpo;
+    }
+    u32x8 L[RC::LW / 8];
+    OddRT<K, R, MODE> tx, ty;
+    OddRegs<K, R, U, MODE> X, Y;
+    auto fill = [&](OddRT<K, R, MODE>& tt, const OddPos& q) {
+        tt.v0 = v0(q);
+        tt.obj = q.obj;
+        tt.live = q.obj < n_obj;
+    };
+    odd_sload(L, rec(p) + RC::FW);
+    odd_swait();
+    odd_swait_pin(L);
+    fill(tx, p);
+    odd_rec_load<K, R, U, MODE, CARRY>(X, L, tx.v0, lane);
+    odd_sload(tx.f, rec(p));
+    p = step(p);
+    odd_sload(L, rec(p) + RC::FW);
+    odd_swait();
+    odd_swait_pin(L);
+    odd_swait_pin(tx.f);
+    auto half = [&](OddRegs<K, R, U, MODE>& Z, OddRT<K, R, MODE>& tz, const OddRegs<K, R, U, MODE>& W,
+                    const OddRT<K, R, MODE>& tw) {
+        fill(tz, p);
+        odd_rec_load<K, R, U, MODE, CARRY>(Z, L, tz.v0, lane);
+        odd_sload(tz.f, rec(p));
+        p = step(p);
+        odd_sload(L, rec(p) + RC::FW);
+        // keep the loads ahead of the arithmetic below (left to itself the
+        // scheduler sinks most of them below the current tile's selector work)
+        if (HBEC_ODD_SCHED && odd_rec_unroll(K, R, MODE)) __builtin_amdgcn_sched_barrier(0);
+        if (MODE == kOddVerify ? HBEC_ODD_VBARRIER : HBEC_ODD_BARRIER) __builtin_amdgcn_s_barrier();
+        odd_rec_finish<K, R, U, MODE, CARRY>(W, tw, a.tab, tb, lane, flags);
+        odd_swait();
+        odd_swait_pin(L);
+        odd_swait_pin(tz.f);
+    };
+    if constexpr (odd_rec_unroll(K, R, MODE)) {
+        for (uint32_t b0 = wave0 + nw;; b0 += 2u * nw) {  // block-uniform trip count
+            if (b0 >= n) {
+                odd_rec_finish<K, R, U, MODE, CARRY>(X, tx, a.tab, tb, lane, flags);
+                break;
+            }
+            half(Y, ty, X, tx);
+            if (b0 + nw >= n) {
+                odd_rec_finish<K, R, U, MODE, CARRY>(Y, ty, a.tab, tb, lane, flags);
+                break;
+            }
+            half(X, tx, Y, ty);
+        }
+    } else {
+        // one buffer pair, the next tile copied over the current one (the
+        // register-bound shapes, where two live buffers spill)
+        for (uint32_t b0 = wave0 + nw; b0 < n; b0 += nw) {  // block-uniform trip count
+            half(Y, ty, X, tx);
+            X = Y;
+            tx = ty;
+        }
+        odd_rec_finish<K, R, U, MODE, CARRY>(X, tx, a.tab, tb, lane, flags);
+    }
+}
+
 template <int K, int R, int MODE, bool MIR = false, bool CARRY = false>
 __global__ __launch_bounds__(kPipeBlockThreads, (odd_lb<K, R, MODE, MIR>())) void gf_odd_plan(UPlanArgs p, const URec* __restrict__ recs) {
     using Src = OddPlan<K, R, MIR, CARRY>;
@@ -566,9 +919,12 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_lb<K, R, MODE, MIR>())) voi
 // ---------------------------------------------------------------------------
 // launch table: kernel of (K, r, mode, plan?, mirrored?)
 // ---------------------------------------------------------------------------
+#ifndef HBEC_ODD_REC
+#define HBEC_ODD_REC 1  // strided batches: object records (gf_odd_rec) instead of per-tile base arithmetic (gf_odd)
+#endif
 template <int K, int R, int MODE>
 static const void* odd_pick(bool plan, bool mirror, bool carry) {
-    if (!plan) return (const void*)&gf_odd<K, R, MODE>;
+    if (!plan) return HBEC_ODD_REC ? (const void*)&gf_odd_rec<K, R, MODE> : (const void*)&gf_odd<K, R, MODE>;
     if constexpr (MODE != kOddVerify) {  // plans never verify
         if (mirror) return (const void*)&gf_odd_plan<K, R, MODE, true>;
         if constexpr (HBEC_ODD_CARRY != 0 && odd_plan_u<K>(0) == 2) {

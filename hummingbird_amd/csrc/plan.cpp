@@ -183,8 +183,7 @@ int hbec::launch_unaligned_passes(const URec* recs, uint64_t n_recs, const std::
         const int R = std::min(hbec::kMaxR, R_all - r0);
         e = hbec::unaligned_occupancy(R, &per_cu);
         if (e != hipSuccess) return hip_fail(e, "unaligned occupancy");
-        if (const char* env = std::getenv("HBEC_UNALIGNED_BPC"))  // tuning knob, as in apply_views
-            if (std::atoi(env) > 0) per_cu = std::min(per_cu, std::atoi(env));
+        if (const long long v = hbec::tune_knob("HBEC_UNALIGNED_BPC", 0); v > 0) per_cu = std::min(per_cu, (int)v);
         for (int c0 = 0; c0 < K_all; c0 += hbec::kMaxK) {
             const int K = std::min(hbec::kMaxK, K_all - c0);
             hbec::UPlanArgs a;
@@ -240,7 +239,7 @@ int hbec::stripes_grid(int k, int r, uint64_t n_tiles, int* grid, int blocks_per
         if (e != hipSuccess) return hip_fail(e, "stripes occupancy");
         b = std::max(1, b);
         if (hbec::kPipeBlocksPerCu > 0) b = std::min(b, hbec::kPipeBlocksPerCu);  // same HBM sweet spot
-        if (const char* env = std::getenv("HBEC_STRIPE_BLOCKS_PER_CU")) b = std::max(1, std::min(b, std::atoi(env)));
+        if (const long long v = hbec::tune_knob("HBEC_STRIPE_BLOCKS_PER_CU", 0); v > 0) b = std::max(1, std::min(b, (int)v));
         occ[dev][k][r] = b;
     }
     const uint64_t want = (n_tiles + 3) / 4;  // 4 waves per block

@@ -93,7 +93,15 @@ int side_stream_get(int dev, hipStream_t* s) {
                 return HBEC_OK;
             }
     }
-    hipError_t e = hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+    static const bool prio = tune_knob("HBEC_MD5_SIDE_PRIO", 0) == 1;
+    hipError_t e;
+    if (prio) {
+        int lo = 0, hi = 0;
+        e = hipDeviceGetStreamPriorityRange(&lo, &hi);
+        if (e == hipSuccess) e = hipStreamCreateWithPriority(s, hipStreamNonBlocking, hi);
+    } else {
+        e = hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+    }
     if (e != hipSuccess) return hip_fail(e, "hipStreamCreate");
     return HBEC_OK;
 }
@@ -192,8 +200,7 @@ std::map<int, int> g_hash_made;
 
 int hash_ring_limit() {
     static const int v = [] {
-        const char* e = std::getenv("HBEC_HOST_RINGS");
-        const int x = e ? std::atoi(e) : 0;
+        const int x = (int)env_knob("HBEC_HOST_RINGS", 0);
         return x > 0 ? x : 8;
     }();
     return v;
@@ -235,8 +242,7 @@ int hash_ring_make(int dev, HashRing** out) {
     std::unique_ptr<HashRing> r(new (std::nothrow) HashRing());
     if (!r) return fail(HBEC_ERR_NOMEM, "hash ring");
     r->dev = dev;
-    const char* env = std::getenv("HBEC_HOST_SLOT_MB");
-    const long long mb = env ? std::atoll(env) : 64;
+    const long long mb = env_knob("HBEC_HOST_SLOT_MB", 64);
     r->cap = (size_t)(mb > 0 ? mb : 64) << 20;
     r->rec_cap = 65536;
     for (int i = 0; i < kHashSlots && e == hipSuccess; ++i) {
@@ -288,10 +294,7 @@ void scratch_free(void* p, hipStream_t stream) {
 // so co-resident MD5 waves block their launch and the overlap turns into
 // serialisation (profiles/r01_md5_sweep.jsonl: 8+3 pipelined 3.4 ms vs 2.45
 // sequential; 4+2 3.13 vs 3.87).  HBEC_MD5_SEGMENTS overrides n.
-static const int g_md5_segments = [] {
-    const char* e = std::getenv("HBEC_MD5_SEGMENTS");
-    return e ? std::max(1, std::atoi(e)) : 0;
-}();
+static const int g_md5_segments = (int)std::max(0LL, tune_knob("HBEC_MD5_SEGMENTS", 0));
 
 static uint64_t md5_segment(uint64_t shard_len, int k) {
     const int n = g_md5_segments ? g_md5_segments : (k <= 4 ? 8 : 1);
@@ -552,15 +555,21 @@ int hbec_encode_md5_batch(hbec_codec* codec, const hbec_view* views, uint64_t n_
             return rc;
         }
         std::vector<hbec_view> sv((size_t)n);
-        for (uint64_t off = 0; off < shard_len && rc == HBEC_OK; off += seg) {
-            const uint64_t len = std::min(seg, shard_len - off);
+        static const uint64_t head = (uint64_t)std::max(0LL, tune_knob("HBEC_MD5_HEAD_KIB", 0)) * 1024u;
+        static const int enc_grid = (int)tune_knob("HBEC_MD5_ENC_GRID", 0);
+        for (uint64_t off = 0; off < shard_len && rc == HBEC_OK;) {
+            const uint64_t want = (off == 0 && head > 0) ? std::min(head, seg) : seg;
+            const uint64_t len = std::min(want, shard_len - off);
             for (int i = 0; i < n; ++i) sv[i] = hbec_view{static_cast<uint8_t*>(views[i].base) + off, views[i].obj_stride};
+            set_thread_grid_cap(off > 0 ? enc_grid : 0);
             rc = hbec_encode_batch(codec, sv.data(), n_objects, len, hip_stream);
+            set_thread_grid_cap(0);
             if (rc) break;
             rc = order_after(side, main);  // segment encoded (and, first time, state allocated)
             if (rc) break;
             const uint32_t flags = (off == 0 ? kInit : 0u) | (off + len == shard_len ? kFinal : 0u);
             rc = md5_step(sv.data(), n, n_objects, len, off, flags, state, d_digests, side);
+            off += len;
         }
         const int rc2 = order_after(main, side);  // caller's stream: digests ready
         hipFreeAsync(state, main);

@@ -270,14 +270,8 @@ int verify_tile_bytes(int k) { return verify_u(k) * 1024; }
 // Shards shorter than max(one verify tile, 2 KiB) take the packed verify
 // (HBEC_VERIFY_PACKED=0 turns it off for A/B; HBEC_VERIFY_PACKED_MAX_SHARD=B
 // moves the threshold).
-static const bool g_verify_packed_on = [] {
-    const char* e = std::getenv("HBEC_VERIFY_PACKED");
-    return !(e && e[0] == '0');
-}();
-static const uint64_t g_verify_packed_max = [] {
-    const char* e = std::getenv("HBEC_VERIFY_PACKED_MAX_SHARD");
-    return e ? (uint64_t)std::atoll(e) : 0ull;
-}();
+static const bool g_verify_packed_on = tune_knob("HBEC_VERIFY_PACKED", 1) != 0;
+static const uint64_t g_verify_packed_max = (uint64_t)std::max(0LL, tune_knob("HBEC_VERIFY_PACKED_MAX_SHARD", 0));
 
 int is_verify_packed_shape(int k, int r, uint64_t shard_len) {
     const uint64_t tile = (uint64_t)verify_tile_bytes(k);

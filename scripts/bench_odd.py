@@ -65,7 +65,7 @@ def shape(k, m, n, obj_len, layout):
                       "encode_ms": round(ms, 4), "GB_s": round(nb / ms / 1e6, 1),
                       "frac": round(nb / ms / 1e6 / PEAK, 4), "kind": info.get("kind"),
                       "verify_ms": round(vms, 4), "verify_frac": round(nb / vms / 1e6 / PEAK, 4),
-                      "unaligned_kernel": os.environ.get("HBEC_UNALIGNED", "1"), "verify_ok": ok}), flush=True)
+                      "verify_ok": ok}), flush=True)
 
 
 def plan_shape(k, m, n, odd):

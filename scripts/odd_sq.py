@@ -8,6 +8,8 @@ a clock settle, so a rocprofv3 --pmc pass sees runs of one kernel at a time.
 Shapes (ecSplit databufs, device-resident, 2048 objects by default):
   a42   aligned 4+2 @ 1 MiB            gf_apply_vec_pipe2<4,2>   (reference point)
   o42   4+2,  S = 262 143              gf_odd<4,2,0>
+  v42   4+2 Verify                     gf_odd<4,2,2>
+  r42   4+2 reconstruct {0,1}          gf_odd<4,2,0>
   a83   aligned 8+3 @ 1 MiB            gf_apply_vec_pipe<8,3>
   o83   8+3,  S = 131 071              gf_odd<8,3,0>
   r83   8+3 reconstruct {0,1}          gf_odd<8,2,0>
@@ -73,7 +75,7 @@ def main():
         return int(flags.count_nonzero().item()) == 0
 
     for name in names:
-        k, m, s, op = {"a42": (4, 2, MiB // 4, "enc"), "o42": (4, 2, 262143, "enc"), "a83": (8, 3, MiB // 8, "enc"),
+        k, m, s, op = {"a42": (4, 2, MiB // 4, "enc"), "o42": (4, 2, 262143, "enc"), "v42": (4, 2, 262143, "ver"), "r42": (4, 2, 262143, "rec"), "a83": (8, 3, MiB // 8, "enc"),
                        "o83": (8, 3, 131071, "enc"), "r83": (8, 3, 131071, "rec"), "v83": (8, 3, 131071, "ver"),
                        "o104": (10, 4, 104858, "enc"), "p124": (12, 4, 87392, "plan"),
                        "v328": (32, 8, 32771, "ver")}[name]

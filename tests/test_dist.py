@@ -151,6 +151,7 @@ def test_bench_gpus_without_launcher_spawns_ranks():
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, r.stdout  # rank 0 alone prints
     assert lines[0]["n_gpus"] == 2 and lines[0]["ranks_seen"] == 2
+    assert lines[0]["per_rank"] == [[0.0, 0.0], [1.0, 10.0]]  # every rank's launch times, in rank order
 
 
 def test_bench_single_gpu_dry_run():
