@@ -111,11 +111,11 @@ def kernel_sources_sha256(sources=KERNEL_SOURCES) -> str:
     return h.hexdigest()
 
 
-# Sources of the odd_objects leg's kernels (gf_odd<4, 2, 0> / <4, 2, 2> and
-# gf_odd_edges): its traffic is reported only from a PMC summary collected
-# on exactly these sources (pmc_summary.py records both hashes).
+# Sources of the odd_objects legs' kernels (gf_odd_rec / gf_odd of 4+2, 8+3,
+# 10+4 and gf_odd_edges): their traffic is reported only from a PMC summary
+# collected on exactly these sources (pmc_summary.py records both hashes).
 ODD_SOURCES = ("hummingbird_amd/csrc/odd.hip", "hummingbird_amd/csrc/odd_impl.h", "hummingbird_amd/csrc/gf_device.h",
-               "hummingbird_amd/csrc/kernels.h")
+               "hummingbird_amd/csrc/kernels.h", "hummingbird_amd/csrc/odd_k58.hip", "hummingbird_amd/csrc/odd_k912.hip")
 
 
 def load_pmc(prefix_glob="profiles/r[0-9][0-9]_pmc.json"):
@@ -419,30 +419,34 @@ def small_objects(n=65536, obj_len=4096, reps=100, settle=200):
     return out
 
 
-def odd_objects(n=4096, obj_len=(1 << 20) - 4, reps=20, settle=40):
-    """Objects of arbitrary size: ecSplit's S = ceil(len / k) is a multiple of
-    16 for one object size in 16 (objectserver/ecutils.go:14-24), and its
-    databuf puts shard i at i*S (ecutils.go:31-35), so most objects reach the
-    codec as shards at odd offsets.  n ecSplit databufs of 1 MiB - 4 B objects
-    (4+2, S = 262 143), device-resident: Encode, Reconstruct of shards {0,1}
-    in place, Verify (gf_odd<4, 2, 0> / gf_odd<4, 2, 2> + gf_odd_edges).  Rebuilt
-    shards must equal the originals and Verify must pass every object."""
-    k, m = 4, 2
+def _odd_kernel_traffic(kern, k, r, mode):
+    """PMC bytes per launch of the odd-shard kernel coding (k, r, mode), by the
+    name it runs under (gf_odd_rec for strided batches, gf_odd before)."""
+    for name in (f"gf_odd_rec<{k}, {r}, {mode}>", f"gf_odd<{k}, {r}, {mode}>"):
+        if name in kern:
+            return name, kern[name].get("hbm_bytes_per_launch")
+    return None, None
+
+
+def odd_leg(k, m, n, obj_len, first, reps=20, settle=40, pmc=None):
+    """One odd-shard shape: n ecSplit databufs of obj_len-byte objects,
+    device-resident: Encode, Reconstruct of shards {0,1} in place, Verify.
+    Rebuilt shards must equal the originals and Verify must pass every object."""
     s = -(-obj_len // k)
     enc = RS.New(k, m)
     rows = torch.empty((n, (k + m) * s), dtype=torch.uint8, device="cuda")
-    B.fill_splitmix(rows, (k + m) * s, first=1 << 21)
+    B.fill_splitmix(rows, (k + m) * s, first=first)
     views = B.shard_views(rows, k + m, s)
     flags = torch.zeros(n, dtype=torch.int32, device="cuda")
     present = [0, 0] + [1] * (k + m - 2)
-    nbytes = n * (k + m) * s
+    nbytes = {"encode": n * (k + m) * s, "reconstruct": n * (k + 2) * s, "verify": n * (k + m) * s}
     stream = torch.cuda.current_stream()
     B.encode_views(enc, views, n, s)
     keep = rows[:, :2 * s].clone()
     ops = {"encode": lambda: B.encode_views(enc, views, n, s),
            "reconstruct": lambda: B.reconstruct_views(enc, views, present, n, s),
            "verify": lambda: B.verify_views(enc, views, n, s, flags)}
-    out = {"workload": f"4+2, {n} ecSplit databufs of {obj_len} B objects (S = {s}, shards at odd offsets), "
+    out = {"workload": f"{k}+{m}, {n} ecSplit databufs of {obj_len} B objects (S = {s}, shards at odd offsets), "
                        "device-resident", "shard_bytes": s}
     for _ in range(settle):
         ops["encode"]()
@@ -456,24 +460,19 @@ def odd_objects(n=4096, obj_len=(1 << 20) - 4, reps=20, settle=40):
         e1.record(stream)
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / reps
-        gbs = nbytes / (ms * 1e-3) / 1e9
+        gbs = nbytes[name] / (ms * 1e-3) / 1e9
         out[name] = {"ms": round(ms, 4), "GB_s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
-    # HBM traffic per launch from the committed PMC summary (two separate
-    # --pmc passes over this bench), when it was collected on these sources
-    pmc_files = sorted(glob.glob(str(ROOT / "profiles/r[0-9][0-9]_pmc.json")))
-    pmc = json.loads(Path(pmc_files[-1]).read_text()) if pmc_files else {}
-    fresh = pmc.get("odd_sources_sha256") == kernel_sources_sha256(ODD_SOURCES)
-    kern = pmc.get("kernels", {})
-    for name, kname in (("encode", "gf_odd<4, 2, 0>"), ("reconstruct", "gf_odd<4, 2, 0>"), ("verify", "gf_odd<4, 2, 2>")):
-        edge = "gf_odd_edges<2>" if name == "verify" else "gf_odd_edges<0>"
-        t = kern.get(kname, {}).get("hbm_bytes_per_launch") if fresh else None
-        te = kern.get(edge, {}).get("hbm_bytes_per_launch") if fresh else None
-        if t is not None:
-            out[name]["traffic"] = int(t + (te or 0))
-            out[name]["traffic_ratio"] = round((t + (te or 0)) / nbytes, 4)
-    out["traffic_source"] = os.path.relpath(pmc_files[-1], ROOT) if (pmc_files and fresh) else None
-    if not fresh:
-        out["traffic_note"] = "no PMC summary collected on this tree's odd-kernel sources"
+    if pmc is not None:
+        kern = pmc.get("kernels", {})
+        for name, (r, mode) in (("encode", (m, 0)), ("reconstruct", (2, 0)), ("verify", (m, 2))):
+            if name == "verify" and k > 8:
+                continue  # k > 8 Verify is gf_wide
+            kname, t = _odd_kernel_traffic(kern, k, r, mode)
+            te = kern.get("gf_odd_edges<2>" if name == "verify" else "gf_odd_edges<0>", {}).get("hbm_bytes_per_launch")
+            if t is not None:
+                out[name]["kernel"] = kname
+                out[name]["traffic"] = int(t + (te or 0))
+                out[name]["traffic_ratio"] = round((t + (te or 0)) / nbytes[name], 4)
     # the check: erase shards 0-1 of every object for real, rebuild them, and
     # Verify every object (a reconstruct that wrote nothing would fail here)
     rows[:, :2 * s].fill_(0x3C)
@@ -484,6 +483,28 @@ def odd_objects(n=4096, obj_len=(1 << 20) - 4, reps=20, settle=40):
     out["parity_ok"] = bool(int(flags.count_nonzero()) == 0 and torch.equal(rows[:, :2 * s], keep))
     del rows, keep, flags
     torch.cuda.empty_cache()
+    return out
+
+
+def odd_objects(n=4096):
+    """Objects of arbitrary size: ecSplit's S = ceil(len / k) is a multiple of
+    16 for one object size in 16 (objectserver/ecutils.go:14-24), and its
+    databuf puts shard i at i*S (ecutils.go:31-35), so most objects reach the
+    codec as shards at odd offsets.  The 4+2 leg (1 MiB - 4 B objects, S =
+    262 143) at the top level; 8+3 (1 MiB - 8 B, S = 131 071: BASELINE
+    configs[3]'s shape) and 10+4 (1 MiB, S = 104 858) under `shapes`.  HBM
+    traffic per launch comes from the committed PMC summary (two --pmc passes
+    over this bench) when it was collected on these sources."""
+    pmc_files = sorted(glob.glob(str(ROOT / "profiles/r[0-9][0-9]_pmc.json")))
+    pmc = json.loads(Path(pmc_files[-1]).read_text()) if pmc_files else {}
+    fresh = pmc.get("odd_sources_sha256") == kernel_sources_sha256(ODD_SOURCES)
+    out = odd_leg(4, 2, n, (1 << 20) - 4, 1 << 21, pmc=pmc if fresh else None)
+    out["shapes"] = {"8+3": odd_leg(8, 3, n, (1 << 20) - 8, 1 << 22, pmc=pmc if fresh else None),
+                     "10+4": odd_leg(10, 4, n, 1 << 20, 1 << 23, pmc=pmc if fresh else None)}
+    out["traffic_source"] = os.path.relpath(pmc_files[-1], ROOT) if (pmc_files and fresh) else None
+    if not fresh:
+        out["traffic_note"] = "no PMC summary collected on this tree's odd-kernel sources"
+    out["parity_ok"] = out["parity_ok"] and all(v["parity_ok"] for v in out["shapes"].values())
     return out
 
 

@@ -21,7 +21,7 @@ ROOT = PKG.parent
 INCLUDE = ROOT / "include"
 
 SOURCES = ["odd_k912.hip", "odd_k58.hip", "kernels.hip", "odd.hip", "wide.hip", "stripes.hip", "verify.hip", "md5.hip", "shardhash.cpp", "hbec.cpp", "ecutils.cpp", "plan.cpp", "hostpath.cpp", "batcher.cpp", "coalesce.cpp"]
-HEADERS = ["kernels.h", "gf256.h", "internal.h", "gf_device.h", "pool.h", "odd_impl.h", "gf_tune.h"]
+HEADERS = ["kernels.h", "gf256.h", "internal.h", "gf_device.h", "pool.h", "odd_impl.h", "tuning.h"]
 ARCH = os.environ.get("HBEC_OFFLOAD_ARCH", "gfx950")
 
 

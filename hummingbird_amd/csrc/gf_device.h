@@ -7,23 +7,17 @@
 #include <stdint.h>
 
 #include "kernels.h"
+#include "tuning.h"
 
 namespace hbec {
 
-#ifndef HBEC_XCD_MAP
-#define HBEC_XCD_MAP 1
-#endif
 // Workgroups are dispatched round-robin over MI355X's 8 XCDs (block b runs on
 // XCD b % 8).  Renumber them so the blocks resident on one XCD take adjacent
 // tiles of every grid-stride front (one contiguous run per XCD and L2).
 // 8+3: +1.4-1.8 %, 4+2: +0.3-0.5 % vs. the raw block id (profiles/r01_tune_xcd.jsonl).
 __device__ __forceinline__ uint32_t xcd_block() {
-#if HBEC_XCD_MAP
     const uint32_t nb = gridDim.x;
     return (nb % 8u == 0u) ? (blockIdx.x % 8u) * (nb / 8u) + blockIdx.x / 8u : blockIdx.x;
-#else
-    return blockIdx.x;
-#endif
 }
 
 __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
@@ -34,27 +28,14 @@ __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel)
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-#ifndef HBEC_NT_LOADS
-#define HBEC_NT_LOADS 1
-#endif
-#ifndef HBEC_NT_STORES
-#define HBEC_NT_STORES 1
-#endif
-
+// Shard streams are touched once: non-temporal loads and stores (plain ones
+// lost 2-3 %, profiles/r01_tune_*.jsonl).
 __device__ __forceinline__ u32x4 ld16(const uint8_t* p) {
-#if HBEC_NT_LOADS
     return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
-#else
-    return *reinterpret_cast<const u32x4*>(p);
-#endif
 }
 
 __device__ __forceinline__ void st16(uint8_t* p, u32x4 v) {
-#if HBEC_NT_STORES
     __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
-#else
-    *reinterpret_cast<u32x4*>(p) = v;
-#endif
 }
 
 // Global-address-space (addrspace 1) views for addresses built from integers
@@ -64,19 +45,11 @@ typedef __attribute__((address_space(1))) const u32x4 gu32x4_c;
 typedef __attribute__((address_space(1))) u32x4 gu32x4;
 
 __device__ __forceinline__ u32x4 ld16_addr(uint64_t addr) {
-#if HBEC_NT_LOADS
     return __builtin_nontemporal_load(reinterpret_cast<gu32x4_c*>(addr));
-#else
-    return *reinterpret_cast<gu32x4_c*>(addr);
-#endif
 }
 
 __device__ __forceinline__ void st16_addr(uint64_t addr, u32x4 v) {
-#if HBEC_NT_STORES
     __builtin_nontemporal_store(v, reinterpret_cast<gu32x4*>(addr));
-#else
-    *reinterpret_cast<gu32x4*>(addr) = v;
-#endif
 }
 
 // Lane l receives lane l+1's value (DPP wave_shl:1, a VALU move; lane 63
@@ -114,10 +87,6 @@ __device__ __forceinline__ Sel selectors(uint32_t x) {
     return s;
 }
 
-#ifndef HBEC_XOR3
-#define HBEC_XOR3 1
-#endif
-
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // v_bitop3_b32: a ^ b ^ c
 }
@@ -127,16 +96,10 @@ __device__ __forceinline__ uint32_t gf_mul_sel(const Sel& s, uint32_t t0, uint32
     return perm(t1, t0, s.s0) ^ perm(t3, t2, s.s1) ^ perm(t4, t4, s.s2);
 }
 
-#ifndef HBEC_VGPR_TABLES
-#define HBEC_VGPR_TABLES 1
-#endif
-
 // Coefficient tables of one pass.  v_perm_b32 may read only one SGPR (GFX9
 // constant-bus limit), so the low halves t[0] and t[2] are copied to VGPRs
-// once per kernel instead of by a v_mov before every perm.
-#ifndef HBEC_ALLVGPR_MIN
-#define HBEC_ALLVGPR_MIN 16  // K*R at or above which all 5 table words live in VGPRs (SGPR spills otherwise)
-#endif
+// once per kernel instead of by a v_mov before every perm; from K*R =
+// HBEC_ALLVGPR_MIN (tuning.h) the high words too (SGPR spills otherwise).
 
 // VMIN: K*R at or above which the high words live in VGPRs too (kernels
 // with many scalar live values pass 1: all five words in VGPRs)
@@ -149,13 +112,9 @@ struct Tables {
 };
 
 __device__ __forceinline__ uint32_t to_vgpr(uint32_t x) {
-#if HBEC_VGPR_TABLES
     uint32_t r;
     asm("v_mov_b32 %0, %1" : "=v"(r) : "s"(x));
     return r;
-#else
-    return x;
-#endif
 }
 
 typedef uint32_t TabArray[kMaxR][kMaxK][5];
@@ -181,19 +140,9 @@ __device__ __forceinline__ Tables<K, R, VMIN> load_tables(const TabArray& tab) {
 // acc[r] ^= XOR_j C[r][j] * x[j] for one 16-B column of K inputs.  The 3K
 // perm terms per (row, dword) are folded by v_bitop3 XOR3s; a pending odd
 // term is carried so every XOR3 retires two terms.
-#ifndef HBEC_GF_NONE
-#define HBEC_GF_NONE 0  // tuning only: plain XOR of the inputs (same loads / stores, no field multiply)
-#endif
 template <int K, int R, int VMIN = HBEC_ALLVGPR_MIN>
 __device__ __forceinline__ void gf_dot(u32x4 (&acc)[R], const u32x4 (&x)[K], const TabArray& tab,
                                        const Tables<K, R, VMIN>& tb) {
-    if constexpr (HBEC_GF_NONE != 0) {
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-#pragma unroll
-            for (int j = 0; j < K; ++j) acc[r] ^= x[(j + r) % K];
-        return;
-    }
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
         uint32_t pend[R];
@@ -265,25 +214,4 @@ __device__ __forceinline__ void packed_coords(PackedCoord<U>& c, uint32_t t, uin
     }
 }
 
-// ---- Tuning only: field multiply through LDS tables ----
-// HBEC_GF_LDS = 1 / 2 (tuning builds) pull in gf_tune.h; the product keeps
-// these declarations only, so the kernels' `if constexpr (HBEC_GF_LDS != 0)`
-// branches name something (they are discarded, never instantiated).
-#ifndef HBEC_GF_LDS
-#define HBEC_GF_LDS 0
-#endif
-#if HBEC_GF_LDS == 0
-__host__ __device__ constexpr int gf_lds_bytes(int, int) { return 16; }
-template <int K, int R>
-struct LdsGf {};
-template <int K, int R>
-__device__ LdsGf<K, R> gf_lds_init(uint8_t* lt, const TabArray& tab);
-template <int K, int R>
-__device__ void gf_dot_lds(u32x4 (&acc)[R], const u32x4 (&x)[K], const LdsGf<K, R>& g);
-#endif
-
 }  // namespace hbec
-
-#if HBEC_GF_LDS != 0
-#include "gf_tune.h"
-#endif

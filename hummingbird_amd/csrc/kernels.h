@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "tuning.h"
+
 namespace hbec {
 
 // ---- Environment knobs ----
@@ -13,9 +15,6 @@ namespace hbec {
 // (-DHBEC_TUNE=1, scripts/tune*.py); the product build compiles each to its
 // default.
 long long env_knob(const char* name, long long dflt);
-#ifndef HBEC_TUNE
-#define HBEC_TUNE 0
-#endif
 inline long long tune_knob(const char* name, long long dflt) {
 #if HBEC_TUNE
     return env_knob(name, dflt);
@@ -28,18 +27,9 @@ inline long long tune_knob(const char* name, long long dflt) {
 constexpr int kMaxK = 16;         // inputs per kernel pass
 constexpr int kMaxR = 4;          // outputs per kernel pass
 constexpr int kBlockThreads = 256;
-#ifndef HBEC_PIPE_BLOCK
-#define HBEC_PIPE_BLOCK 256
-#endif
-#ifndef HBEC_PIPE_BLOCKS_PER_CU
-#define HBEC_PIPE_BLOCKS_PER_CU 1  // one 4-wave block per CU (0: occupancy limit)
-#endif
 constexpr int kPipeBlockThreads = HBEC_PIPE_BLOCK;  // pipelined kernel block size
 constexpr int kPipeBlocksPerCu = HBEC_PIPE_BLOCKS_PER_CU;
 
-#ifndef HBEC_WAVES_PER_SIMD
-#define HBEC_WAVES_PER_SIMD 4
-#endif
 constexpr int kVecWavesPerSimd = HBEC_WAVES_PER_SIMD;  // occupancy floor for the vec kernels
 
 // One pass: out[r] (^)= XOR_{j<K} C[r][j] * in[j] over n_obj objects.
@@ -81,40 +71,17 @@ int vec_block_threads(int k, int r, uint64_t shard_len, int accumulate, int forc
 // from A/B sweeps on MI355X (profiles/r01_tune_*.jsonl): HBM streams best with
 // few outstanding requests per CU — 4+2 peaks at 1 KiB tiles (4 loads per
 // wave, 32 KiB in flight per CU), while 8+3 (more inputs per output byte)
-// peaks at 3 KiB tiles.  HBEC_PIPE_LOADS overrides with K*U ~= that value.
-#ifndef HBEC_PIPE_LOADS
-#define HBEC_PIPE_LOADS 0
-#endif
-#ifndef HBEC_PIPE_U_BIG
-#define HBEC_PIPE_U_BIG 3  // KiB per input per wave tile for 5 <= K <= 8
-#endif
-__host__ __device__ constexpr int pipe_u(int k) {
-    if (HBEC_PIPE_LOADS > 0) return k >= HBEC_PIPE_LOADS ? 1 : (HBEC_PIPE_LOADS / k > 4 ? 4 : HBEC_PIPE_LOADS / k);
-    return k <= 4 ? (4 / k) : (k <= 8 ? HBEC_PIPE_U_BIG : 1);
-}
+// peaks at 3 KiB tiles (tuning.h).
+__host__ __device__ constexpr int pipe_u(int k) { return k <= 4 ? (4 / k) : (k <= 8 ? HBEC_PIPE_U_BIG : 1); }
 
 // Tile depth of the stripe-plan and verify kernels, from A/B runs on MI355X
-// (profiles/r01_tune_plan_verify.jsonl; HBEC_STRIPE_LOADS / HBEC_VERIFY_LOADS
-// override with K*U ~= that value):
+// (profiles/r01_tune_plan_verify.jsonl):
 //  * stripes: pipe_u for K <= 4, 1 KiB for K >= 5 — config 4's 4 KiB objects
 //    (512-B shards) waste less of a shallow tile: 67.2 % vs 63.7 % at 3 KiB;
 //  * verify (read-only): 4 KiB for K <= 4 (85.1 % vs 81.9 % at 1 KiB),
 //    1 KiB for K >= 5 (82.0 % vs 79.8 % at 3 KiB).
-#ifndef HBEC_STRIPE_LOADS
-#define HBEC_STRIPE_LOADS 0
-#endif
-#ifndef HBEC_VERIFY_LOADS
-#define HBEC_VERIFY_LOADS 0
-#endif
-__host__ __device__ constexpr int loads_u(int k, int loads) {
-    return k >= loads ? 1 : (loads / k > 4 ? 4 : loads / k);
-}
-__host__ __device__ constexpr int stripes_u(int k) {
-    return HBEC_STRIPE_LOADS > 0 ? loads_u(k, HBEC_STRIPE_LOADS) : (k <= 4 ? pipe_u(k) : 1);
-}
-__host__ __device__ constexpr int verify_u(int k) {
-    return HBEC_VERIFY_LOADS > 0 ? loads_u(k, HBEC_VERIFY_LOADS) : (k <= 4 ? 4 : 1);
-}
+__host__ __device__ constexpr int stripes_u(int k) { return k <= 4 ? pipe_u(k) : 1; }
+__host__ __device__ constexpr int verify_u(int k) { return k <= 4 ? 4 : 1; }
 
 hipError_t launch_vec(int k, int r, const PassArgs& a, int grid, hipStream_t stream, int force_stream);
 // Any alignment / stride / length with aligned 16-B accesses (gf_apply_unaligned):
@@ -159,11 +126,9 @@ hipError_t launch_unaligned_plan(int k, int r, const UPlanArgs& a, int grid, hip
 // <= kMaxR outputs; the gf_apply_vec_pipe2 schedule.  Modes: 0 apply,
 // 1 accumulate (out ^= ..., later passes of k > kOddMaxK), 2 verify (flag
 // objects whose stored parity differs; nothing written).
-#ifndef HBEC_ODD_MAXK
-#define HBEC_ODD_MAXK 12  // 10+4 odd reconstruct 51-58 -> 67 % of 8 TB/s in one pass (r3b7)
-#endif
-static_assert(HBEC_ODD_MAXK == 8 || HBEC_ODD_MAXK == 12, "gf_odd instances exist for K <= 8 (odd.hip, odd_k58.hip) and 9..12 (odd_k912.hip)");
-constexpr int kOddMaxK = HBEC_ODD_MAXK;
+// gf_odd instances exist for K <= 8 (odd.hip, odd_k58.hip) and 9..12
+// (odd_k912.hip): 10+4 odd reconstruct 51-58 -> 67 % of 8 TB/s in one pass (r3b7)
+constexpr int kOddMaxK = 12;
 // Longest shard the 32-bit-position kernels (gf_odd, gf_odd_plan, gf_wide)
 // take.  They form shard positions in int32: column block starts, load
 // limits ((l4 + S + A - 1) & ~(A - 1)) - 16, window and tile offsets, all
@@ -171,12 +136,12 @@ constexpr int kOddMaxK = HBEC_ODD_MAXK;
 // shards take the 64-bit round-2 kernels (gf_apply_unaligned family).
 constexpr uint64_t kPos32MaxShard = (1ull << 31) - (1ull << 16);
 __host__ __device__ constexpr bool pos32_shard(uint64_t shard_len) { return shard_len <= kPos32MaxShard; }
-// HBEC_ODD=1 / 0 selects gf_odd or the round-2 kernels (gf_apply_unaligned
-// family) for odd shards (default: HBEC_ODD_DEFAULT).
+// gf_odd for odd shards (true; a tuning build's HBEC_ODD=0 takes the round-2
+// gf_apply_unaligned family instead, for A/B)
 bool odd_enabled();
-// 4-wave blocks per CU of the gf_odd grids for a mode (HBEC_ODD_BPC overrides)
-// 4-wave blocks per CU of a gf_odd launch (mode 0 apply, 1 accumulate, 2 verify; K, R of the pass)
-int odd_blocks_per_cu(int mode, int k, int r, bool mirror = false);
+// 4-wave blocks per CU of a gf_odd launch (mode 0 apply, 1 accumulate, 2
+// verify; K, R of the pass; strided: a gf_odd_rec launch)
+int odd_blocks_per_cu(int mode, int k, int r, bool mirror = false, bool strided = false);
 bool odd_supported(int k, int r);
 // Unaligned plan records (URec) of one stripe / object: p0 = 0, tile, 2*tile,
 // ... while p0 < urec_span(S), for whichever kernel family codes them.
@@ -195,6 +160,10 @@ uint64_t odd_min_main();
 bool odd_uses_records();
 uint32_t odd_rec_words(int k, int r, int mode);
 hipError_t launch_odd_objrec(int k, int r, int mode, const PassArgs& a, uint32_t* recs, hipStream_t stream);
+// Plans: the same records for n stripes / objects of orecs (shard lengths
+// > odd_min_main(), coded with p's shard indices and tables) into recs.
+hipError_t launch_odd_planrec(int k, int r, int mode, const UPlanArgs& p, const URec* orecs, uint32_t n,
+                              uint32_t* recs, hipStream_t stream);
 hipError_t launch_odd(int k, int r, int mode, const PassArgs& a, uint32_t* flags, const uint32_t* recs, int grid,
                       hipStream_t stream);
 // the guard-band bytes of every shard (after the main launches of a pass;

@@ -62,27 +62,12 @@ __device__ __forceinline__ void process_tile(const PassArgs& a, const Tables<K, 
         u32x4 acc[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) acc[r] = accumulate ? old[u][r] : u32x4{0, 0, 0, 0};
-#if HBEC_XOR3
         {
             u32x4 xs[K];
 #pragma unroll
             for (int j = 0; j < K; ++j) xs[j] = x[u][j];
             gf_dot<K, R>(acc, xs, a.tab, tb);
         }
-#else
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const Sel sx = selectors(x[u][j][e]);
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    const uint32_t* t = a.tab[r][j];
-                    acc[r][e] ^= gf_mul_sel(sx, tb.lo0[r][j], t[1], tb.lo2[r][j], t[3], t[4]);
-                }
-            }
-        }
-#endif
         if (live) {
 #pragma unroll
             for (int r = 0; r < R; ++r) st16(a.out[r] + obj * a.out_stride[r] + off, acc[r]);
@@ -90,16 +75,7 @@ __device__ __forceinline__ void process_tile(const PassArgs& a, const Tables<K, 
     }
 }
 
-// Sub-tiles (1 KiB each) per wave tile: keeps K*U*4 load VGPRs <= 32.
-#ifndef HBEC_TILE_SMALL
-#define HBEC_TILE_SMALL 4
-#endif
-#ifndef HBEC_TILE_MID
-#define HBEC_TILE_MID 1
-#endif
-#ifndef HBEC_TILE_BIG
-#define HBEC_TILE_BIG 1
-#endif
+// Sub-tiles (1 KiB each) per wave tile: keeps K*U*4 load VGPRs <= 32 (tuning.h).
 __host__ __device__ constexpr int tile_kib(int k) {
     return k <= 2 ? HBEC_TILE_SMALL : (k <= 4 ? HBEC_TILE_MID : HBEC_TILE_BIG);
 }
@@ -165,18 +141,8 @@ __device__ __forceinline__ void compute_store_tile(const u32x4 (&x)[U][K], const
     }
 }
 
-#ifndef HBEC_USE_PIPE
-#define HBEC_USE_PIPE 1
-#endif
-#ifndef HBEC_PIPE_WAVES_PER_SIMD
-#define HBEC_PIPE_WAVES_PER_SIMD 1
-#endif
-#ifndef HBEC_PIPE_SLEEP
-#define HBEC_PIPE_SLEEP 6  // x 64 cycles
-#endif
-
 template <int K, int R>
-__global__ __launch_bounds__(kPipeBlockThreads, HBEC_PIPE_WAVES_PER_SIMD) void gf_apply_vec_pipe(PassArgs a) {
+__global__ __launch_bounds__(kPipeBlockThreads, 1) void gf_apply_vec_pipe(PassArgs a) {
     // never launched with a.accumulate (launch_vec routes those to gf_apply_vec)
     constexpr int U = pipe_u(K);
     constexpr uint64_t TILE = (uint64_t)U * 1024u;
@@ -201,7 +167,7 @@ __global__ __launch_bounds__(kPipeBlockThreads, HBEC_PIPE_WAVES_PER_SIMD) void g
         // loads lowers the requests in flight at the HBM; 4+2: +1.0-1.5 %
         // (flat from 6 to 8, a cliff from 12), 8+3 (longer tiles): no effect
         // (profiles/r01_tune_sleep.jsonl)
-        if (HBEC_PIPE_SLEEP > 0 && K <= 4) __builtin_amdgcn_s_sleep(HBEC_PIPE_SLEEP);
+        if (K <= 4) __builtin_amdgcn_s_sleep(HBEC_PIPE_SLEEP);
         if (base + TILE <= a.shard_len)
             compute_store_tile<K, R, U>(cur, a, tb, obj, base + lane * 16u, true);
         else
@@ -219,12 +185,6 @@ __global__ __launch_bounds__(kPipeBlockThreads, HBEC_PIPE_WAVES_PER_SIMD) void g
         compute_store_tile<K, R, U>(cur, a, tb, obj, base + lane * 16u, false);
 }
 
-#ifndef HBEC_PIPE_V2
-#define HBEC_PIPE_V2 1
-#endif
-#ifndef HBEC_PIPE_V2_MAXK
-#define HBEC_PIPE_V2_MAXK 4
-#endif
 // gf_apply_vec_pipe2: the pipelined kernel in the stripe-plan kernel's loop
 // shape -- every tile's shard bases are scalar values computed one tile ahead
 // (the plan kernel loads them as records) and full / partial tiles are a
@@ -239,30 +199,11 @@ struct PipeTile {
     uint32_t live;   // bytes stored: valid, or 0 for a past-the-end stand-in tile
 };
 
-// Tuning knob (tile order): with HBEC_SWZ_G > 0, runs of HBEC_SWZ_C tiles
-// of HBEC_SWZ_G objects are interleaved, so the tiles in flight at one time
-// span G objects instead of ~4 (only when both divide the batch evenly).
-#ifndef HBEC_SWZ_G
-#define HBEC_SWZ_G 0  // off: never faster (profiles/r01_tune_swizzle.jsonl)
-#endif
-#ifndef HBEC_SWZ_C
-#define HBEC_SWZ_C 16
-#endif
-
 template <int K, int R, int U>
 __device__ __forceinline__ void pipe_tile_coords(PipeTile<K, R>& b, const PassArgs& a, uint32_t t, uint32_t tpo) {
     constexpr uint64_t TILE = (uint64_t)U * 1024u;
-    uint32_t obj = t / tpo;
-    uint64_t off = (uint64_t)(t - obj * tpo) * TILE;
-    if (HBEC_SWZ_G > 0 && tpo % HBEC_SWZ_C == 0 && (a.n_tiles / tpo) % HBEC_SWZ_G == 0) {
-        const uint32_t ci = t % HBEC_SWZ_C;
-        const uint32_t oi = (t / HBEC_SWZ_C) % HBEC_SWZ_G;
-        const uint32_t rest = t / (HBEC_SWZ_C * HBEC_SWZ_G);
-        const uint32_t ncg = tpo / HBEC_SWZ_C;
-        const uint32_t og = rest / ncg;
-        obj = og * HBEC_SWZ_G + oi;
-        off = (uint64_t)((rest - og * ncg) * HBEC_SWZ_C + ci) * TILE;
-    }
+    const uint32_t obj = t / tpo;
+    const uint64_t off = (uint64_t)(t - obj * tpo) * TILE;
 #pragma unroll
     for (int j = 0; j < K; ++j) b.in[j] = reinterpret_cast<uint64_t>(a.in[j]) + obj * a.in_stride[j] + off;
 #pragma unroll
@@ -286,17 +227,14 @@ __device__ __forceinline__ void pipe2_load(u32x4 (&x)[U][K], const PipeTile<K, R
 
 template <int K, int R, int U, bool FULL>
 __device__ __forceinline__ void pipe2_store_(const u32x4 (&x)[U][K], const PassArgs& a, const Tables<K, R>& tb,
-                                             const PipeTile<K, R>& b, uint32_t lane, const LdsGf<K, R>& lg) {
+                                             const PipeTile<K, R>& b, uint32_t lane) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const uint64_t off = (uint64_t)lane * 16u + (uint64_t)u * 1024u;
         u32x4 acc[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) acc[r] = u32x4{0, 0, 0, 0};
-        if constexpr (HBEC_GF_LDS != 0)
-            gf_dot_lds<K, R>(acc, x[u], lg);
-        else
-            gf_dot<K, R>(acc, x[u], a.tab, tb);
+        gf_dot<K, R>(acc, x[u], a.tab, tb);
         if (FULL || off < b.live) {
 #pragma unroll
             for (int r = 0; r < R; ++r) st16_addr(b.out[r] + off, acc[r]);
@@ -319,11 +257,11 @@ __device__ __forceinline__ void pipe_tile_at(PipeTile<K, R>& b, const PassArgs& 
 
 template <int K, int R, int U>
 __device__ __forceinline__ void pipe2_finish(const u32x4 (&x)[U][K], const PassArgs& a, const Tables<K, R>& tb,
-                                             const PipeTile<K, R>& cur, uint32_t lane, const LdsGf<K, R>& lg) {
+                                             const PipeTile<K, R>& cur, uint32_t lane) {
     if (cur.live >= (uint32_t)U * 1024u)
-        pipe2_store_<K, R, U, true>(x, a, tb, cur, lane, lg);
+        pipe2_store_<K, R, U, true>(x, a, tb, cur, lane);
     else
-        pipe2_store_<K, R, U, false>(x, a, tb, cur, lane, lg);
+        pipe2_store_<K, R, U, false>(x, a, tb, cur, lane);
 }
 
 // Block barrier once per tile, after the next tile's loads are issued and the
@@ -333,18 +271,9 @@ __device__ __forceinline__ void pipe2_finish(const u32x4 (&x)[U][K], const PassA
 // the same number of iterations (the loop bound is the block's first wave's
 // tile; a wave past the end re-codes the last tile), so the barrier counts
 // always match.
-#ifndef HBEC_PIPE_BARRIER
-#define HBEC_PIPE_BARRIER 1
-#endif
-#ifndef HBEC_PIPE2_SLEEP
-#define HBEC_PIPE2_SLEEP 8  // x 64 cycles, K <= 4
-#endif
-#ifndef HBEC_PIPE2_SLEEP_BIG
-#define HBEC_PIPE2_SLEEP_BIG 0  // x 64 cycles, K > 4
-#endif
 
 template <int K, int R>
-__global__ __launch_bounds__(kPipeBlockThreads, HBEC_PIPE_WAVES_PER_SIMD) void gf_apply_vec_pipe2(PassArgs a) {
+__global__ __launch_bounds__(kPipeBlockThreads, 1) void gf_apply_vec_pipe2(PassArgs a) {
     constexpr int U = pipe_u(K);
     constexpr uint32_t WPB = kPipeBlockThreads / 64;
     const uint32_t lane = threadIdx.x & 63u;
@@ -354,11 +283,6 @@ __global__ __launch_bounds__(kPipeBlockThreads, HBEC_PIPE_WAVES_PER_SIMD) void g
     const uint32_t wave = wave0 + dw;
     const uint32_t tpo = a.tiles_per_obj;
     const uint32_t n = a.n_tiles;
-    LdsGf<K, R> lg{};
-    if constexpr (HBEC_GF_LDS != 0) {
-        __shared__ uint8_t lt[gf_lds_bytes(K, R)];
-        lg = gf_lds_init<K, R>(lt, a.tab);  // block-wide barrier: before any wave returns
-    }
     if (wave0 >= n) return;  // whole blocks only: the loop below has block barriers
     const Tables<K, R> tb = load_tables<K, R>(a.tab);
     PipeTile<K, R> cur, nxt;
@@ -369,12 +293,11 @@ __global__ __launch_bounds__(kPipeBlockThreads, HBEC_PIPE_WAVES_PER_SIMD) void g
     for (uint32_t b0 = wave0 + nw; b0 < n; b0 += nw) {  // block-uniform trip count
         u32x4 y[U][K];
         pipe2_load<K, R, U>(y, nxt, lane);
-        if (HBEC_PIPE2_SLEEP > 0 && K <= 4) __builtin_amdgcn_s_sleep(HBEC_PIPE2_SLEEP);
-        if (HBEC_PIPE2_SLEEP_BIG > 0 && K > 4) __builtin_amdgcn_s_sleep(HBEC_PIPE2_SLEEP_BIG);
-        if (HBEC_PIPE_BARRIER) __builtin_amdgcn_s_barrier();
+        if (K <= 4) __builtin_amdgcn_s_sleep(HBEC_PIPE2_SLEEP);
+        __builtin_amdgcn_s_barrier();
         PipeTile<K, R> after;
         pipe_tile_at<K, R, U>(after, a, b0 + dw + nw, n, tpo);
-        pipe2_finish<K, R, U>(x, a, tb, cur, lane, lg);
+        pipe2_finish<K, R, U>(x, a, tb, cur, lane);
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -382,7 +305,7 @@ __global__ __launch_bounds__(kPipeBlockThreads, HBEC_PIPE_WAVES_PER_SIMD) void g
         cur = nxt;
         nxt = after;
     }
-    pipe2_finish<K, R, U>(x, a, tb, cur, lane, lg);
+    pipe2_finish<K, R, U>(x, a, tb, cur, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -432,25 +355,13 @@ __device__ __forceinline__ void packed_finish(const u32x4 (&x)[U][K], const Pass
         packed_store_<K, R, U, false>(x, a, tb, c, t, lane, live);
 }
 
-#ifndef HBEC_PACKED_SLEEP
-#define HBEC_PACKED_SLEEP 0  // x 64 cycles, K <= 4
-#endif
-#ifndef HBEC_PACKED_SLEEP_BIG
-#define HBEC_PACKED_SLEEP_BIG 0  // x 64 cycles, K > 4
-#endif
 
-#ifndef HBEC_PACKED_U_BIG
-#define HBEC_PACKED_U_BIG 1  // KiB per input per wave tile for K > 4 (0: pipe_u's 3 KiB)
-#endif
-#ifndef HBEC_PACKED_BARRIER
-#define HBEC_PACKED_BARRIER 1
-#endif
 __host__ __device__ constexpr int packed_u(int k) {
-    return (k > 4 && HBEC_PACKED_U_BIG > 0) ? HBEC_PACKED_U_BIG : pipe_u(k);
+    return k > 4 ? HBEC_PACKED_U_BIG : pipe_u(k);
 }
 
 template <int K, int R>
-__global__ __launch_bounds__(kPipeBlockThreads, HBEC_PIPE_WAVES_PER_SIMD) void gf_apply_packed(PassArgs a) {
+__global__ __launch_bounds__(kPipeBlockThreads, 1) void gf_apply_packed(PassArgs a) {
     constexpr int U = packed_u(K);
     constexpr uint32_t WPB = kPipeBlockThreads / 64;
     const uint32_t lane = threadIdx.x & 63u;
@@ -473,9 +384,7 @@ __global__ __launch_bounds__(kPipeBlockThreads, HBEC_PIPE_WAVES_PER_SIMD) void g
         packed_coords<U>(nxt, tn < n ? tn : n - 1u, lane, a.n_elems, spo, inv);
         u32x4 y[U][K];
         packed_load<K, U>(y, a, nxt);
-        if (HBEC_PACKED_SLEEP > 0 && K <= 4) __builtin_amdgcn_s_sleep(HBEC_PACKED_SLEEP);
-        if (HBEC_PACKED_SLEEP_BIG > 0 && K > 4) __builtin_amdgcn_s_sleep(HBEC_PACKED_SLEEP_BIG);
-        if (HBEC_PACKED_BARRIER) __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_barrier();
         packed_finish<K, R, U>(x, a, tb, cur, t, n, lane);
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -578,37 +487,12 @@ __global__ __launch_bounds__(kBlockThreads, kVecWavesPerSimd) void gf_apply_vec_
 // as an input.  A window reads output bytes another window stores only in
 // the e_r bytes it does not use itself, so the passes are race-free.
 // ---------------------------------------------------------------------------
-#ifndef HBEC_UNALIGNED_U
-#define HBEC_UNALIGNED_U 4  // with SHFL: u4 > u2 (profiles/r02_tune_unaligned*.jsonl)
-#endif
-#ifndef HBEC_REALIGN_SEL
-#define HBEC_REALIGN_SEL 1  // 1: select the 5 source dwords with v_cndmask; 0: a uniform switch
-#endif
-#ifndef HBEC_UNALIGNED_SHFL
-#define HBEC_UNALIGNED_SHFL 1  // 1: one load per input column, the upper block from lane l+1 (62 blocks/window):
-                               // +3-9 % over two loads (profiles/r02_tune_unaligned_shfl.jsonl)
-#endif
-// stored bytes per 64-lane window: 63 blocks (two loads per column), or 62
-// when the upper block comes from the next lane (lane 63's column is partial)
-constexpr uint32_t kUnalignedWindow = HBEC_UNALIGNED_SHFL ? 992 : 1008;
-constexpr uint32_t kUnalignedStoreLanes = HBEC_UNALIGNED_SHFL ? 62 : 63;
+// stored bytes per 64-lane window: 62 blocks, the column's upper block from
+// lane l+1 (lane 63's column is partial); one load per input column, +3-9 %
+// over two (profiles/r02_tune_unaligned_shfl.jsonl)
+constexpr uint32_t kUnalignedWindow = 992;
+constexpr uint32_t kUnalignedStoreLanes = 62;
 constexpr int kUnalignedU = HBEC_UNALIGNED_U;  // windows per wave tile (loads in flight)
-
-// bytes [d, d + 16) of the 32 bytes lo:hi (gf_device.h realign16), or the
-// uniform-switch form of the same selection (tuning: HBEC_REALIGN_SEL=0)
-__device__ __forceinline__ u32x4 realign16_k(const u32x4& lo, const u32x4& hi, uint32_t d) {
-    if (HBEC_REALIGN_SEL) return realign16(lo, hi, d);
-    const uint32_t sh = d & 3u;
-    uint32_t s0, s1, s2, s3, s4;
-    switch (d >> 2) {
-        case 0: s0 = lo[0]; s1 = lo[1]; s2 = lo[2]; s3 = lo[3]; s4 = hi[0]; break;
-        case 1: s0 = lo[1]; s1 = lo[2]; s2 = lo[3]; s3 = hi[0]; s4 = hi[1]; break;
-        case 2: s0 = lo[2]; s1 = lo[3]; s2 = hi[0]; s3 = hi[1]; s4 = hi[2]; break;
-        default: s0 = lo[3]; s1 = hi[0]; s2 = hi[1]; s3 = hi[2]; s4 = hi[3]; break;
-    }
-    return u32x4{__builtin_amdgcn_alignbyte(s1, s0, sh), __builtin_amdgcn_alignbyte(s2, s1, sh),
-                 __builtin_amdgcn_alignbyte(s3, s2, sh), __builtin_amdgcn_alignbyte(s4, s3, sh)};
-}
 
 // A view of one object's shard: aligned base, misalignment, last aligned block.
 struct UView {
@@ -628,17 +512,12 @@ __device__ __forceinline__ UView uview(uint64_t b, uint64_t s) {
 __device__ __forceinline__ void uload(u32x4& lo, u32x4& hi, const UView& v, uint64_t col) {
     const uint64_t x = v.abase + col;
     lo = ld16_addr(x < v.last ? x : v.last);
-    if (HBEC_UNALIGNED_SHFL) {
-        hi = lo;  // replaced by lane l+1's block at use (ushift)
-    } else {
-        const uint64_t y = x + 16u;
-        hi = ld16_addr(y < v.last ? y : v.last);
-    }
+    hi = lo;  // replaced by lane l+1's block at use (upper)
 }
 
-// the column's upper block: loaded (two-load form) or lane l+1's lower block
+// the column's upper block: lane l+1's lower block
 __device__ __forceinline__ u32x4 upper(const u32x4& lo, const u32x4& hi) {
-    if (!HBEC_UNALIGNED_SHFL) return hi;
+    (void)hi;
     u32x4 h;
 #pragma unroll
     for (int i = 0; i < 4; ++i) h[i] = __shfl_down(lo[i], 1u, 64);
@@ -682,7 +561,7 @@ __device__ __forceinline__ void unaligned_tile(int K, uint64_t S, uint64_t p0, b
             if (accumulate) {  // kernel-uniform; clamped loads need no per-window branch
                 u32x4 lo, hi;
                 uload(lo, hi, ov, col[u]);
-                acc[r][u] = realign16_k(lo, upper(lo, hi), ov.d);
+                acc[r][u] = realign16(lo, upper(lo, hi), ov.d);
             }
         }
     }
@@ -706,7 +585,7 @@ __device__ __forceinline__ void unaligned_tile(int K, uint64_t S, uint64_t p0, b
             for (int q = 0; q < 5; ++q) tb[r][q] = tab(r, j)[q];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const u32x4 x = realign16_k(clo[u], upper(clo[u], chi[u]), cv.d);
+            const u32x4 x = realign16(clo[u], upper(clo[u], chi[u]), cv.d);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const Sel sx = selectors(x[e]);
@@ -734,7 +613,7 @@ __device__ __forceinline__ void unaligned_tile(int K, uint64_t S, uint64_t p0, b
                 if (!live[u]) continue;  // window-uniform (the upper block is a shuffle)
                 u32x4 lo, hi;
                 uload(lo, hi, ov, col[u]);
-                const u32x4 st = realign16_k(lo, upper(lo, hi), ov.d);
+                const u32x4 st = realign16(lo, upper(lo, hi), ov.d);
                 // columns [c, c + 16) of this window's lanes; bytes at or past S do not count
                 const uint64_t nv = col[u] < S ? S - col[u] : 0u;
                 if (lane < kUnalignedStoreLanes) {
@@ -761,7 +640,7 @@ __device__ __forceinline__ void unaligned_tile(int K, uint64_t S, uint64_t p0, b
             u32x4 nb;
 #pragma unroll
             for (int i = 0; i < 4; ++i) nb[i] = __shfl_down(acc[r][u][i], 1u, 64);
-            const u32x4 blk = realign16_k(acc[r][u], nb, e);
+            const u32x4 blk = realign16(acc[r][u], nb, e);
             const uint64_t q = col[u] + e;  // block start (shard position); ob + q is 16-B aligned
             if (lane < kUnalignedStoreLanes && q < S) {
                 if (q + 16u <= S)
@@ -865,7 +744,7 @@ __global__ __launch_bounds__(kBlockThreads) void fill_splitmix(uint8_t* dst, uin
 // ---------------------------------------------------------------------------
 template <int K, int R>
 static const void* vec_kernel_ptr(bool pipe) {
-    if (pipe) return (HBEC_PIPE_V2 && K <= HBEC_PIPE_V2_MAXK) ? reinterpret_cast<const void*>(&gf_apply_vec_pipe2<K, R>)
+    if (pipe) return K <= HBEC_PIPE_V2_MAXK ? reinterpret_cast<const void*>(&gf_apply_vec_pipe2<K, R>)
                                               : reinterpret_cast<const void*>(&gf_apply_vec_pipe<K, R>);
     return reinterpret_cast<const void*>(&gf_apply_vec<K, R>);
 }
@@ -910,9 +789,6 @@ int is_streaming_shape(int k, int r, int force_stream) {
     return (force_stream || !unrolled_kernel(k, r, false)) ? 1 : 0;
 }
 
-#ifndef HBEC_USE_PACKED
-#define HBEC_USE_PACKED 1
-#endif
 
 template <int K>
 static const void* packed_for_r(int r) {
@@ -957,7 +833,7 @@ static const bool g_packed_on = tune_knob("HBEC_PACKED", 1) != 0;
 static const uint64_t g_packed_max = (uint64_t)std::max(0LL, tune_knob("HBEC_PACKED_MAX_SHARD", 0));
 
 int is_packed_shape(int k, int r, uint64_t shard_len, int accumulate, int force_stream) {
-    return (HBEC_USE_PACKED && g_packed_on && !force_stream && !accumulate && shard_len >= 16 && shard_len % 16 == 0 &&
+    return (g_packed_on && !force_stream && !accumulate && shard_len >= 16 && shard_len % 16 == 0 &&
             shard_len < (g_packed_max ? g_packed_max : packed_max_shard(k)) &&
             packed_kernel(k, r) != nullptr)
                ? 1
@@ -974,12 +850,6 @@ hipError_t launch_packed(int k, int r, const PassArgs& a, int grid, hipStream_t 
 // Resident 4-wave blocks per CU for the packed kernel: K <= 4 streams best
 // with 2 (short tiles: more waves keep enough bytes in flight), K > 4 with 1
 // (profiles/r02_tune_packed*.jsonl).
-#ifndef HBEC_PACKED_BLOCKS_SMALL
-#define HBEC_PACKED_BLOCKS_SMALL 2
-#endif
-#ifndef HBEC_PACKED_BLOCKS_BIG
-#define HBEC_PACKED_BLOCKS_BIG 1
-#endif
 
 hipError_t packed_occupancy(int k, int r, int* blocks_per_cu) {
     const void* fn = packed_kernel(k, r);
@@ -993,7 +863,7 @@ hipError_t packed_occupancy(int k, int r, int* blocks_per_cu) {
 // The pipelined kernel wants whole tiles; short shards (e.g. 8+3 of a 4 KiB
 // object: 512 B) take the 1 KiB-tile kernel so fewer lanes idle.
 static bool use_pipe(int k, uint64_t shard_len, bool accumulate) {
-    return HBEC_USE_PIPE && !accumulate && shard_len >= (uint64_t)pipe_u(k) * 1024u;
+    return !accumulate && shard_len >= (uint64_t)pipe_u(k) * 1024u;
 }
 
 int is_pipe_shape(int k, int r, uint64_t shard_len, int force_stream) {

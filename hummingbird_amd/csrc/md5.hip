@@ -133,15 +133,10 @@ struct Md5Args {
     uint32_t pad_;
 };
 
-#ifndef HBEC_MD5_PINGPONG
-#define HBEC_MD5_PINGPONG 1
-#endif
-#ifndef HBEC_MD5_DEPTH_LIST
-#define HBEC_MD5_DEPTH_LIST 2
-#endif
 
 template <bool ALIGNED, int D>
 __global__ __launch_bounds__(64) void md5_chains(Md5Args a) {
+    if (HBEC_MD5_PRIO > 0) __builtin_amdgcn_s_setprio(HBEC_MD5_PRIO);
     const uint32_t v = blockIdx.y;
     const uint64_t o = (uint64_t)blockIdx.x * 64u + threadIdx.x;
     if (o >= a.n_obj) return;
@@ -204,7 +199,6 @@ __global__ __launch_bounds__(64) void md5_chains(Md5Args a) {
                 }
             }
         };
-#if HBEC_MD5_PINGPONG
         // ping-pong between two register groups: group g+1 loads while g
         // compresses, without copying registers; loads past the end re-read
         // the last group (clamped), compressions past it are skipped.
@@ -220,22 +214,7 @@ __global__ __launch_bounds__(64) void md5_chains(Md5Args a) {
             for (int j = 0; j < D; ++j)
                 if ((g + 1) * D + j < nb) md5_compress4(h, grp_b[j]);
         }
-#else
-        // one compression site per block of the group (half the code of the
-        // ping-pong), 16 register moves per block to rotate the buffers
-        load_group(cur, 0);
-        for (uint64_t g = 0; g < groups; ++g) {
-            u32x4 nxt[D][4];
-            load_group(nxt, g + 1 < groups ? g + 1 : g);
-#pragma unroll
-            for (int j = 0; j < D; ++j)
-                if (g * D + j < nb) md5_compress4(h, cur[j]);
-#pragma unroll
-            for (int j = 0; j < D; ++j)
-#pragma unroll
-                for (int w = 0; w < 4; ++w) cur[j][w] = nxt[j][w];
-        }
-#endif
+
     }
     const uint32_t rv = (uint32_t)(lv - nv * 64u);  // pending bytes left (< 64)
     if (a.flags & kMd5Final) {
@@ -372,9 +351,6 @@ __global__ __launch_bounds__(64) void md5_list(const Md5ListRec* __restrict__ re
 
 // Blocks per load group and the buffer scheme, from the depth sweep on MI355X
 // (profiles/r01_md5_sweep.jsonl).
-#ifndef HBEC_MD5_DEPTH
-#define HBEC_MD5_DEPTH 2
-#endif
 
 uint64_t md5_state_bytes() { return sizeof(Md5State); }
 

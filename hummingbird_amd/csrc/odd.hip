@@ -166,41 +166,41 @@ __global__ __launch_bounds__(kBlockThreads) void gf_odd_edges_plan(UPlanArgs p, 
 }
 
 // ---------------------------------------------------------------------------
-// gf_odd_objrec: the object records gf_odd_rec reads (layout: OddRec,
-// odd_impl.h), one thread per object of a strided pass.  mode 2 (verify)
-// records the stored parity as loaded shards K..K+R-1 and the compared band.
+// gf_odd_objrec / gf_odd_planrec: the object records gf_odd_rec reads (layout:
+// OddRec, odd_impl.h), one thread per object of a strided pass or per stripe
+// of a plan.  mode 2 (verify) records the stored parity as loaded shards
+// K..K+R-1 and the compared band.  A shard of S <= kOddMinMain (plans only)
+// gets empty bands: its tiles store nothing.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ int32_t ceil16(int32_t x) { return (x + 15) & ~15; }
 __device__ __forceinline__ int32_t floor16(int32_t x) { return x & ~15; }
 
-__global__ __launch_bounds__(kBlockThreads) void gf_odd_objrec(PassArgs a, int K, int R, int mode, uint32_t fw,
-                                                              uint32_t rw, uint32_t* __restrict__ recs) {
-    const uint64_t obj = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (obj >= a.n_obj) return;
-    const int32_t S = (int32_t)a.shard_len;
+// in_b(s) / out_b(r): the byte address of loaded shard s / output r
+template <class InB, class OutB>
+__device__ __forceinline__ void odd_rec_write(int K, int R, int mode, int32_t S, InB in_b, OutB out_b, uint32_t* f,
+                                              uint32_t* l) {
     // frame: output 0's 16-B grid, first column at c0 in [0, 16)
-    const int32_t c0 = (int32_t)((0u - (uint32_t)(reinterpret_cast<uint64_t>(a.out[0]) + obj * a.out_stride[0])) & 15u);
+    const int32_t c0 = (int32_t)((0u - (uint32_t)out_b(0)) & 15u);
     const int32_t hi = S - kOddGuard - 16;  // last block start stored / compared
+    const bool main = S > kOddMinMain;
     const int NL = K + (mode == kOddVerify ? R : 0), NO = mode == kOddVerify ? 0 : R;
-    uint32_t* f = recs + obj * rw;
-    uint32_t* l = f + fw;
     uint32_t shp = 0, dlp = 0;
     for (int s = 0; s < NL; ++s) {
-        const uint64_t b = s < K ? reinterpret_cast<uint64_t>(a.in[s]) + obj * a.in_stride[s]
-                                 : reinterpret_cast<uint64_t>(a.out[s - K]) + obj * a.out_stride[s - K];
+        const uint64_t b = s < K ? in_b(s) : out_b(s - K);
         const int32_t t0 = (int32_t)(b & 3u) + c0;  // column 0's first byte, from the shard's dword base
         const uint64_t base = (b & ~(uint64_t)3) + (uint64_t)(t0 & ~3);
         l[3 * s] = (uint32_t)base;
         l[3 * s + 1] = (uint32_t)(base >> 32);
-        l[3 * s + 2] = (uint32_t)(S - 16 - (t0 & ~3));  // blocks end inside the shard's dwords
+        l[3 * s + 2] = main ? (uint32_t)(S - 16 - (t0 & ~3)) : 0u;  // blocks end inside the shard's dwords
         shp |= ((uint32_t)t0 & 3u) << (2 * s);
     }
     for (int r = 0; r < NO; ++r) {
-        const uint64_t o = reinterpret_cast<uint64_t>(a.out[r]) + obj * a.out_stride[r];
+        const uint64_t o = out_b(r);
         const uint32_t dl = (0u - ((uint32_t)o + (uint32_t)c0)) & 15u;
         const uint64_t q = o + (uint64_t)(c0 + (int32_t)dl);  // 16-B aligned
-        const int32_t lo = ceil16(kOddGuard - c0 - (int32_t)dl), top = floor16(hi - c0 - (int32_t)dl);
-        const uint32_t width = (uint32_t)(top >= lo ? top - lo : 0);  // S > kOddMinMain: never empty
+        int32_t lo = ceil16(kOddGuard - c0 - (int32_t)dl), top = floor16(hi - c0 - (int32_t)dl);
+        if (!main) lo = -16, top = -32;  // (V - lo) <= width holds for no V < 2^31
+        const uint32_t width = (uint32_t)(top >= lo ? top - lo : 0);
         f[4 + 4 * r] = (uint32_t)q;
         f[5 + 4 * r] = (uint32_t)(q >> 32);
         f[6 + 4 * r] = (uint32_t)lo;
@@ -208,16 +208,44 @@ __global__ __launch_bounds__(kBlockThreads) void gf_odd_objrec(PassArgs a, int K
         if (mode == kOddAcc) {  // the old blocks, loaded with the inputs
             l[3 * NL + 4 * r] = (uint32_t)q;
             l[3 * NL + 4 * r + 1] = (uint32_t)(q >> 32);
-            l[3 * NL + 4 * r + 2] = (uint32_t)lo;
-            l[3 * NL + 4 * r + 3] = (uint32_t)lo + width;
+            l[3 * NL + 4 * r + 2] = main ? (uint32_t)lo : 0u;
+            l[3 * NL + 4 * r + 3] = main ? (uint32_t)lo + width : 0u;
         }
         dlp |= dl << (4 * r);
     }
-    const int32_t vlo = ceil16(kOddGuard - c0), vtop = floor16(hi - c0);
+    int32_t vlo = ceil16(kOddGuard - c0), vtop = floor16(hi - c0);
+    if (!main) vlo = -16, vtop = -32;
     f[0] = shp;
     f[1] = dlp;
     f[2] = (uint32_t)vlo;
     f[3] = (uint32_t)(vtop >= vlo ? vtop - vlo : 0);
+}
+
+__global__ __launch_bounds__(kBlockThreads) void gf_odd_objrec(PassArgs a, int K, int R, int mode, uint32_t fw,
+                                                              uint32_t rw, uint32_t* __restrict__ recs) {
+    const uint64_t obj = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (obj >= a.n_obj) return;
+    uint32_t* f = recs + obj * rw;
+    odd_rec_write(
+        K, R, mode, (int32_t)a.shard_len,
+        [&](int s) { return reinterpret_cast<uint64_t>(a.in[s]) + obj * a.in_stride[s]; },
+        [&](int r) { return reinterpret_cast<uint64_t>(a.out[r]) + obj * a.out_stride[r]; }, f, f + fw);
+}
+
+// plans: one record per stripe / object record (URec: a = stripe or data
+// arena, b = parity arena, shard i of a base at i * S)
+__global__ __launch_bounds__(kBlockThreads) void gf_odd_planrec(UPlanArgs p, const URec* __restrict__ orecs,
+                                                               uint32_t n, int K, int R, int mode, uint32_t fw,
+                                                               uint32_t rw, uint32_t* __restrict__ recs) {
+    const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n) return;
+    const URec rec = orecs[e];
+    const uint64_t S = rec.shard_len;
+    uint32_t* f = recs + (uint64_t)e * rw;
+    odd_rec_write(
+        K, R, mode, (int32_t)S,
+        [&](int s) { return (((p.in_sel >> s) & 1u) ? rec.b : rec.a) + (uint64_t)p.in_idx[s] * S; },
+        [&](int r) { return (((p.out_sel >> r) & 1u) ? rec.b : rec.a) + (uint64_t)p.out_idx[r] * S; }, f, f + fw);
 }
 
 static uint32_t odd_rec_fw(int r, int mode) { return (uint32_t)((4 + 4 * (mode == kOddVerify ? 0 : r) + 7) & ~7); }
@@ -240,6 +268,16 @@ hipError_t launch_odd_objrec(int k, int r, int mode, const PassArgs& a, uint32_t
     return hipLaunchKernel((const void*)&gf_odd_objrec, dim3((unsigned)grid), dim3(kBlockThreads), args, 0, stream);
 }
 
+hipError_t launch_odd_planrec(int k, int r, int mode, const UPlanArgs& p, const URec* orecs, uint32_t n,
+                              uint32_t* recs, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    if (k < 1 || k > kOddMaxK || r < 1 || r > kMaxR || mode == kOddVerify) return hipErrorInvalidValue;
+    const uint32_t grid = (n + kBlockThreads - 1) / kBlockThreads;
+    uint32_t fw = odd_rec_fw(r, mode), rw = odd_rec_words(k, r, mode);
+    void* args[] = {const_cast<UPlanArgs*>(&p), &orecs, &n, &k, &r, &mode, &fw, &rw, &recs};
+    return hipLaunchKernel((const void*)&gf_odd_planrec, dim3(grid), dim3(kBlockThreads), args, 0, stream);
+}
+
 static const void* odd_kernel(int k, int r, int mode, bool plan, bool mirror = false, bool carry = false) {
     if (k <= 4) return odd_kernel_range<1, 4>(k, r, mode, plan, mirror, carry);
     if (k <= 8) return odd_kernel_k58(k, r, mode, plan, mirror);
@@ -260,10 +298,11 @@ bool odd_enabled() {
 #ifndef HBEC_ODD_BPC_VERIFY
 #define HBEC_ODD_BPC_VERIFY 2  // read-only: 4+2 68.5 -> 81 % with 2 blocks per CU (r03_tune_odd3)
 #endif
-int odd_blocks_per_cu(int mode, int k, int r, bool mirror) {
+int odd_blocks_per_cu(int mode, int k, int r, bool mirror, bool strided) {
     static const int v = (int)tune_knob("HBEC_ODD_BPC", 0);
     if (v > 0) return v;
     if (mode == kOddVerify) return HBEC_ODD_BPC_VERIFY;
+    if (strided && HBEC_ODD_REC && odd_rec_lds(k)) return 2;  // LDS-table record kernels: 2 waves per SIMD (odd_rec_lb)
     return odd_two_blocks(k, r, mode, mirror) ? 2 : HBEC_ODD_BPC_APPLY;  // launch bounds sized for it (odd_lb)
 }
 

@@ -1,7 +1,7 @@
 // odd_impl.h — the gf_odd kernel templates (see odd.hip for the design),
 // shared by the translation units that instantiate them: odd.hip (K <= 4,
 // launchers, edge and mirror kernels), odd_k58.hip (K 5..8), odd_k912.hip
-// (K 9..12 when HBEC_ODD_MAXK >= 12).  Every kernel instance lives in exactly
+// (K 9..12).  Every kernel instance lives in exactly
 // one translation unit, and the units compile in parallel.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -109,9 +109,13 @@ __host__ __device__ constexpr bool odd_rec_carry(int u, int mode) {
 #ifndef HBEC_ODD_UNROLL
 #define HBEC_ODD_UNROLL 1
 #endif
+#ifndef HBEC_ODD_LDS_UNROLL
+#define HBEC_ODD_LDS_UNROLL 1
+#endif
 __host__ __device__ constexpr bool odd_two_blocks(int k, int r, int mode, bool mir);
+__host__ __device__ constexpr bool odd_rec_lds(int k);
 __host__ __device__ constexpr bool odd_rec_unroll(int k, int r, int mode) {
-    return HBEC_ODD_UNROLL != 0 && !odd_two_blocks(k, r, mode, false);
+    return HBEC_ODD_UNROLL != 0 && (odd_rec_lds(k) ? HBEC_ODD_LDS_UNROLL != 0 : !odd_two_blocks(k, r, mode, false));
 }
 // shard bytes per wave tile of the record kernel
 __host__ __device__ constexpr uint32_t odd_rec_span(int u, int mode) {
@@ -618,6 +622,61 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_lb<K, R, MODE>())) void gf_
 template <int U, int MODE, bool CARRY>
 __host__ __device__ constexpr uint32_t odd_rec_wcol(int u) { return CARRY ? 64u * (uint32_t)u : odd_store<MODE>() * (uint32_t)u; }
 
+// Record kernels with K >= HBEC_ODD_LDS_MINK read the coefficient tables from
+// LDS, one input at a time, instead of holding all 5 K R words in VGPRs
+// (12+4: 240 words; the register-resident kernel spilled 134 SGPRs and ran
+// at 40 % of 8 TB/s).
+#ifndef HBEC_ODD_LDS_MINK
+#define HBEC_ODD_LDS_MINK 9
+#endif
+__host__ __device__ constexpr bool odd_rec_lds(int k) { return k >= HBEC_ODD_LDS_MINK; }
+
+// acc[r] ^= XOR_j C[r][j] x[j], input j's R tables (5 words each) at LDS byte
+// address lt + 4 j odd_lt_stride(R): broadcast ds_read_b128 issued by asm
+// right before the input is used and waited for there, so they are neither
+// hoisted out of the loop into VGPRs nor left to the waitcnt pass (which does
+// not see them).  The 3 K products per output dword are folded as in gf_dot.
+template <int K, int R>
+__device__ __forceinline__ void gf_dot_lds(u32x4 (&acc)[R], const u32x4 (&x)[K], uint32_t lt) {
+    constexpr int TQ = (int)odd_lt_stride(R) / 4;
+    uint32_t pend[4][R];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        u32x4 t[TQ];
+#pragma unroll
+        for (int q = 0; q < TQ; ++q)
+            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(t[q]) : "v"(lt), "i"((j * TQ + q) * 16));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int q = 0; q < TQ; ++q) asm volatile("" : "+v"(t[q]));
+        const bool has = (j & 1) != 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const Sel sx = selectors(x[j][e]);
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const uint32_t p0 = perm(t[(5 * r + 1) / 4][(5 * r + 1) % 4], t[(5 * r) / 4][(5 * r) % 4], sx.s0);
+                const uint32_t p1 = perm(t[(5 * r + 3) / 4][(5 * r + 3) % 4], t[(5 * r + 2) / 4][(5 * r + 2) % 4], sx.s1);
+                const uint32_t h4 = t[(5 * r + 4) / 4][(5 * r + 4) % 4];
+                const uint32_t p2 = perm(h4, h4, sx.s2);
+                if (!has) {
+                    acc[r][e] = xor3(acc[r][e], p0, p1);
+                    pend[e][r] = p2;
+                } else {
+                    acc[r][e] = xor3(acc[r][e], pend[e][r], p0);
+                    acc[r][e] = xor3(acc[r][e], p1, p2);
+                }
+            }
+        }
+    }
+    if constexpr ((K & 1) != 0) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int r = 0; r < R; ++r) acc[r][e] ^= pend[e][r];
+    }
+}
+
 template <int K, int R, int MODE>
 struct OddRec {
     static constexpr int NL = K + (MODE == kOddVerify ? R : 0);
@@ -687,10 +746,20 @@ __device__ __forceinline__ void odd_rec_load(OddRegs<K, R, U, MODE>& X, const u3
     }
 }
 
+// outputs pinned after the multiply: the gf_odd choice, and always with LDS
+// tables (unpinned, 12+4 spilled 218 VGPRs at 2 blocks per CU)
+template <int K, int R, int MODE>
+__device__ __forceinline__ void odd_rec_pin(u32x4 (&acc)[R]) {
+    if constexpr (odd_pin_on<K, R, MODE, false>() || odd_rec_lds(K)) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) asm volatile("" : "+v"(acc[r]));
+    }
+}
+
 template <int K, int R, int U, int MODE, bool CARRY>
 __device__ __forceinline__ void odd_rec_finish(const OddRegs<K, R, U, MODE>& X, const OddRT<K, R, MODE>& t,
                                                const TabArray& tab, const Tables<K, R, HBEC_ODD_VMIN>& tb,
-                                               uint32_t lane, uint32_t* flags) {
+                                               uint32_t lane, uint32_t* flags, uint32_t lt) {
     constexpr int NL = OddRec<K, R, MODE>::NL;
     const uint32_t shp = odd_w(t.f, 0), dlp = odd_w(t.f, 1);
     // v_alignbyte reads bits [1:0] of its shift: the packed shifts need no mask
@@ -722,7 +791,7 @@ __device__ __forceinline__ void odd_rec_finish(const OddRegs<K, R, U, MODE>& X, 
 #pragma unroll
             for (int r = 0; r < R; ++r) acc[r] = u32x4{0, 0, 0, 0};
             gf_dot<K, R, HBEC_ODD_VMIN>(acc, x, tab, tb);
-            odd_pin<K, R, MODE, false>(acc);
+            odd_rec_pin<K, R, MODE>(acc);
             const bool mine = t.live != 0u && (u + 1 < U || lane < 63u) && (v - odd_w(t.f, 2)) <= odd_w(t.f, 3);
 #pragma unroll
             for (int r = 0; r < R; ++r) {
@@ -748,8 +817,8 @@ __device__ __forceinline__ void odd_rec_finish(const OddRegs<K, R, U, MODE>& X, 
         for (int r = 0; r < R; ++r) acc1[r] = acc0[r] = u32x4{0, 0, 0, 0};
         gf_dot<K, R, HBEC_ODD_VMIN>(acc1, x1, tab, tb);
         gf_dot<K, R, HBEC_ODD_VMIN>(acc0, x0, tab, tb);
-        odd_pin<K, R, MODE, false>(acc1);
-        odd_pin<K, R, MODE, false>(acc0);
+        odd_rec_pin<K, R, MODE>(acc1);
+        odd_rec_pin<K, R, MODE>(acc0);
         const uint32_t v0 = t.v0 + 16u * lane, v1 = v0 + 1024u;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
@@ -777,8 +846,12 @@ __device__ __forceinline__ void odd_rec_finish(const OddRegs<K, R, U, MODE>& X, 
         u32x4 acc[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) acc[r] = u32x4{0, 0, 0, 0};
-        gf_dot<K, R, HBEC_ODD_VMIN>(acc, x, tab, tb);
-        odd_pin<K, R, MODE, false>(acc);
+        if constexpr (odd_rec_lds(K)) {
+            gf_dot_lds<K, R>(acc, x, lt);
+        } else {
+            gf_dot<K, R, HBEC_ODD_VMIN>(acc, x, tab, tb);
+        }
+        odd_rec_pin<K, R, MODE>(acc);
         if constexpr (MODE == kOddVerify) {
             const bool mine = t.live != 0u && lane < odd_store<MODE>() && (v - odd_w(t.f, 2)) <= odd_w(t.f, 3);
 #pragma unroll
@@ -810,8 +883,12 @@ struct OddPos {
     uint32_t obj, ti;
 };
 
+// LDS-table record kernels fit 2 blocks per CU (2 waves per SIMD)
 template <int K, int R, int MODE>
-__global__ __launch_bounds__(kPipeBlockThreads, (odd_lb<K, R, MODE>())) void gf_odd_rec(PassArgs a, uint32_t* flags,
+__host__ __device__ constexpr int odd_rec_lb() { return odd_rec_lds(K) ? 2 : odd_lb<K, R, MODE>(); }
+
+template <int K, int R, int MODE>
+__global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE>())) void gf_odd_rec(PassArgs a, uint32_t* flags,
                                                                                         const uint32_t* __restrict__ recs) {
     using RC = OddRec<K, R, MODE>;
     constexpr int U = odd_u(K, MODE);
@@ -825,6 +902,17 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_lb<K, R, MODE>())) void gf_
     const uint32_t wave0 = __builtin_amdgcn_readfirstlane(xcd_block() * WPB);
     const uint32_t dw = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (wave0 >= n) return;  // whole blocks only: the loop below has block barriers
+    __shared__ __attribute__((aligned(16))) uint32_t ltab[odd_rec_lds(K) ? K * odd_lt_stride(R) : 4];
+    if constexpr (odd_rec_lds(K)) {
+        // whole blocks reach this point (the early return above is per block)
+        const uint32_t ts = odd_lt_stride(R);
+        for (uint32_t i = threadIdx.x; i < (uint32_t)K * ts; i += blockDim.x) {
+            const uint32_t j = i / ts, w = i - j * ts;
+            ltab[i] = w < (uint32_t)(R * 5) ? a.tab[w / 5][j][w % 5] : 0u;
+        }
+        __syncthreads();
+    }
+    const uint32_t lt = (uint32_t)reinterpret_cast<uintptr_t>(&ltab[0]);  // LDS offset (low half of the flat address)
     const Tables<K, R, HBEC_ODD_VMIN> tb = load_tables<K, R, HBEC_ODD_VMIN>(a.tab);
     const uint32_t qq = nw / tpo, rr = nw - qq * tpo;
     auto step = [&](OddPos p) {
@@ -880,7 +968,7 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_lb<K, R, MODE>())) void gf_
         // scheduler sinks most of them below the current tile's selector work)
         if (HBEC_ODD_SCHED && odd_rec_unroll(K, R, MODE)) __builtin_amdgcn_sched_barrier(0);
         if (MODE == kOddVerify ? HBEC_ODD_VBARRIER : HBEC_ODD_BARRIER) __builtin_amdgcn_s_barrier();
-        odd_rec_finish<K, R, U, MODE, CARRY>(W, tw, a.tab, tb, lane, flags);
+        odd_rec_finish<K, R, U, MODE, CARRY>(W, tw, a.tab, tb, lane, flags, lt);
         odd_swait();
         odd_swait_pin(L);
         odd_swait_pin(tz.f);
@@ -888,12 +976,12 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_lb<K, R, MODE>())) void gf_
     if constexpr (odd_rec_unroll(K, R, MODE)) {
         for (uint32_t b0 = wave0 + nw;; b0 += 2u * nw) {  // block-uniform trip count
             if (b0 >= n) {
-                odd_rec_finish<K, R, U, MODE, CARRY>(X, tx, a.tab, tb, lane, flags);
+                odd_rec_finish<K, R, U, MODE, CARRY>(X, tx, a.tab, tb, lane, flags, lt);
                 break;
             }
             half(Y, ty, X, tx);
             if (b0 + nw >= n) {
-                odd_rec_finish<K, R, U, MODE, CARRY>(Y, ty, a.tab, tb, lane, flags);
+                odd_rec_finish<K, R, U, MODE, CARRY>(Y, ty, a.tab, tb, lane, flags, lt);
                 break;
             }
             half(X, tx, Y, ty);
@@ -906,7 +994,7 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_lb<K, R, MODE>())) void gf_
             X = Y;
             tx = ty;
         }
-        odd_rec_finish<K, R, U, MODE, CARRY>(X, tx, a.tab, tb, lane, flags);
+        odd_rec_finish<K, R, U, MODE, CARRY>(X, tx, a.tab, tb, lane, flags, lt);
     }
 }
 

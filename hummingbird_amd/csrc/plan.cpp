@@ -45,6 +45,9 @@ struct hbec_plan {
     // them with HBEC_ODD=0: round-2 gf_apply_unaligned_plan records
     hbec::URec* d_brecs = nullptr;
     uint64_t n_brecs = 0;
+    // gf_odd_rec: one record per stripe / object with a main-kernel part
+    hbec::URec* d_orecs = nullptr;
+    hbec::OddStripeRecs orecs;
 };
 
 namespace {
@@ -62,7 +65,7 @@ bool aligned_object(const hbec_object& o) {
 std::mutex g_occ_mu;
 
 void add_urecs(std::vector<hbec::URec>& recs, std::vector<hbec::URec>& erecs, std::vector<hbec::URec>& brecs,
-               const void* a, const void* b, uint64_t s, int k) {
+               std::vector<hbec::URec>& orecs, const void* a, const void* b, uint64_t s, int k) {
     const uint64_t ua = reinterpret_cast<uint64_t>(a), ub = reinterpret_cast<uint64_t>(b);
     if (!hbec::odd_enabled() || !hbec::pos32_shard(s)) {
         const uint64_t tile = (uint64_t)hbec::unaligned_tile_bytes();
@@ -72,6 +75,18 @@ void add_urecs(std::vector<hbec::URec>& recs, std::vector<hbec::URec>& erecs, st
     const uint64_t tile = hbec::urec_tile_for(std::min(k, hbec::kOddMaxK), false), span = hbec::urec_span(s);
     for (uint64_t p0 = 0; p0 < span; p0 += tile) recs.push_back({ua, ub, s, p0});
     erecs.push_back({ua, ub, s, 0});
+    if (span > 0) orecs.push_back({ua, ub, s, 0});
+}
+
+void set_orecs(hbec_plan* p, const std::vector<hbec::URec>& orecs) {
+    p->orecs.recs = p->d_orecs;
+    p->orecs.n = orecs.size();
+    p->orecs.s_min = p->orecs.s_max = 0;
+    for (size_t i = 0; i < orecs.size(); ++i) {
+        const uint64_t s = orecs[i].shard_len;
+        p->orecs.s_min = i ? std::min(p->orecs.s_min, s) : s;
+        p->orecs.s_max = std::max(p->orecs.s_max, s);
+    }
 }
 
 template <class T>
@@ -88,6 +103,37 @@ int upload(const std::vector<T>& recs, T** dst, const char* what) {
     return HBEC_OK;
 }
 
+// One pass of a plan over per-stripe records: the records (stream-ordered
+// scratch), then gf_odd_rec with the longest stripe's tile count.
+int odd_stripe_rec_pass(int K, int R, int mode, const hbec::UPlanArgs& a, const hbec::OddStripeRecs& o, int cus,
+                        int max_blocks, hipStream_t stream) {
+    const uint64_t rw = hbec::odd_rec_words(K, R, mode);
+    uint32_t* recs = nullptr;
+    int rc = hbec::scratch_alloc(o.n * rw * 4, stream, reinterpret_cast<void**>(&recs));
+    if (rc) return rc;
+    hipError_t e = hbec::launch_odd_planrec(K, R, mode, a, o.recs, (uint32_t)o.n, recs, stream);
+    if (e != hipSuccess) {
+        hbec::scratch_free(recs, stream);
+        return hip_fail(e, "launch gf_odd_planrec");
+    }
+    hbec::PassArgs c;
+    std::memset(&c, 0, sizeof(c));
+    std::memcpy(c.tab, a.tab, sizeof(c.tab));
+    const uint64_t tpo = hbec::odd_tiles_per_obj(K, mode, o.s_max);
+    c.n_obj = o.n;
+    c.shard_len = o.s_max;
+    c.tiles_per_obj = (uint32_t)tpo;
+    c.n_tiles = (uint32_t)(o.n * tpo);
+    const uint64_t want = (c.n_tiles + 3) / 4;
+    uint64_t cap = (uint64_t)cus * (uint64_t)hbec::odd_blocks_per_cu(mode, K, R, false, true);
+    if (max_blocks > 0) cap = std::min<uint64_t>(cap, (uint64_t)max_blocks);
+    const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, cap));
+    e = hbec::launch_odd(K, R, mode, c, nullptr, recs, grid, stream);
+    hbec::scratch_free(recs, stream);
+    if (e != hipSuccess) return hip_fail(e, "launch gf_odd_rec (plan)");
+    return HBEC_OK;
+}
+
 }  // namespace
 
 // out rows (^)= rows x in over unaligned-kernel records, in passes of <= 4
@@ -96,7 +142,7 @@ int upload(const std::vector<T>& recs, T** dst, const char* what) {
 int hbec::launch_unaligned_passes(const URec* recs, uint64_t n_recs, const std::vector<int>& in_idx,
                                   const std::vector<int>& out_idx, const std::vector<uint8_t>& rows, int sel_k,
                                   hipStream_t stream, int max_blocks, const URec* erecs, uint64_t n_erecs,
-                                  bool mirror, bool round2) {
+                                  bool mirror, bool round2, const OddStripeRecs* orecs) {
     const int K_all = (int)in_idx.size(), R_all = (int)out_idx.size();
     if ((n_recs == 0 && n_erecs == 0) || R_all == 0) return HBEC_OK;
     if (mirror && (!hbec::odd_enabled() || sel_k > 0 || round2))
@@ -107,6 +153,18 @@ int hbec::launch_unaligned_passes(const URec* recs, uint64_t n_recs, const std::
     e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (e != hipSuccess) return hip_fail(e, "hipDeviceGetAttribute");
     if (hbec::odd_enabled() && !round2) {
+        // per-stripe records when every stripe's tile count is within 1/32 of
+        // the longest one's (the shorter stripes' extra tiles store nothing)
+        bool use_orecs = false;
+        if (orecs && orecs->n > 0 && !mirror && hbec::odd_uses_records()) {
+            use_orecs = true;
+            for (int c0 = 0; c0 < K_all && use_orecs; c0 += hbec::kOddMaxK) {
+                const int K = std::min(hbec::kOddMaxK, K_all - c0), mode = c0 > 0 ? 1 : 0;
+                const uint64_t t_max = hbec::odd_tiles_per_obj(K, mode, orecs->s_max);
+                const uint64_t t_min = hbec::odd_tiles_per_obj(K, mode, orecs->s_min);
+                use_orecs = t_max * 32 <= t_min * 33 && orecs->n * t_max < (1ull << 31);
+            }
+        }
         // gf_odd_plan: launches of <= 4 outputs x <= kOddMaxK inputs, later input
         // launches accumulating; one 4-wave block per CU
         for (int r0 = 0; r0 < R_all; r0 += hbec::kMaxR) {
@@ -147,8 +205,12 @@ int hbec::launch_unaligned_passes(const URec* recs, uint64_t n_recs, const std::
                 uint64_t cap = (uint64_t)cus * (uint64_t)hbec::odd_blocks_per_cu(c0 > 0 ? 1 : 0, K, R, mirror);
                 if (max_blocks > 0) cap = std::min<uint64_t>(cap, (uint64_t)max_blocks);
                 const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, cap));
-                if (n_recs > 0) {
-                    e = hbec::launch_odd_plan(K, R, c0 > 0 ? 1 : 0, a, grid, stream);
+                const int mode = c0 > 0 ? 1 : 0;
+                if (use_orecs) {
+                    int rc = odd_stripe_rec_pass(K, R, mode, a, *orecs, cus, max_blocks, stream);
+                    if (rc) return rc;
+                } else if (n_recs > 0) {
+                    e = hbec::launch_odd_plan(K, R, mode, a, grid, stream);
                     if (e != hipSuccess) return hip_fail(e, "launch gf_odd_plan");
                 }
                 // guard-band bytes of every stripe, this pass's inputs
@@ -321,7 +383,7 @@ int run_plan(const hbec_plan* p, const std::vector<int>& in_idx, const std::vect
     // with k > 8 every object is in the unaligned records (hbec_plan_objects)
     const int sel_k = p->objects ? p->k : 0;
     int rc = hbec::launch_unaligned_passes(p->d_urecs, p->n_urecs, in_idx, out_idx, rows, sel_k, stream, 0,
-                                           p->d_erecs, p->n_erecs);
+                                           p->d_erecs, p->n_erecs, false, false, &p->orecs);
     if (rc || p->n_brecs == 0) return rc;
     return hbec::launch_unaligned_passes(p->d_brecs, p->n_brecs, in_idx, out_idx, rows, sel_k, stream, 0, nullptr, 0,
                                          false, true);
@@ -342,7 +404,7 @@ int hbec_plan_stripes(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n,
         p->m = m;
         p->tile_bytes = hbec::stripes_tile_bytes(std::min(k, hbec::kStripeMaxK));
         std::vector<hbec::TileRec> recs;
-        std::vector<hbec::URec> urecs, erecs, brecs;
+        std::vector<hbec::URec> urecs, erecs, brecs, orecs;
         for (uint64_t i = 0; i < n; ++i) {
             const hbec_stripe& s = stripes[i];
             if (s.shard_len == 0) continue;
@@ -350,7 +412,7 @@ int hbec_plan_stripes(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n,
             p->shard_bytes += s.shard_len;
             if (!aligned_stripe(s)) {
                 p->fallback.push_back(s);
-                add_urecs(urecs, erecs, brecs, s.base, nullptr, s.shard_len, k);
+                add_urecs(urecs, erecs, brecs, orecs, s.base, nullptr, s.shard_len, k);
                 continue;
             }
             p->tiled.push_back(s);
@@ -381,12 +443,15 @@ int hbec_plan_stripes(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n,
         int urc = upload(urecs, &p->d_urecs, "plan unaligned records");
         if (!urc) urc = upload(erecs, &p->d_erecs, "plan edge records");
         if (!urc) urc = upload(brecs, &p->d_brecs, "plan large-shard records");
+        if (!urc) urc = upload(orecs, &p->d_orecs, "plan stripe records");
         if (urc) {
             if (p->d_tiles) (void)hipFree(p->d_tiles);
             if (p->d_urecs) (void)hipFree(p->d_urecs);
             if (p->d_erecs) (void)hipFree(p->d_erecs);
+            if (p->d_brecs) (void)hipFree(p->d_brecs);
             return urc;
         }
+        set_orecs(p.get(), orecs);
         p->n_urecs = urecs.size();
         p->n_erecs = erecs.size();
         p->n_brecs = brecs.size();
@@ -407,7 +472,7 @@ int hbec_plan_objects(hbec_codec* codec, const hbec_object* objects, uint64_t n,
         p->objects = true;
         p->tile_bytes = hbec::stripes_tile_bytes(std::min(k, hbec::kStripeMaxK));
         std::vector<hbec::TileRec> recs;
-        std::vector<hbec::URec> urecs, erecs, brecs;
+        std::vector<hbec::URec> urecs, erecs, brecs, orecs;
         for (uint64_t i = 0; i < n; ++i) {
             const hbec_object& o = objects[i];
             if (o.shard_len == 0) continue;
@@ -415,13 +480,13 @@ int hbec_plan_objects(hbec_codec* codec, const hbec_object* objects, uint64_t n,
             p->shard_bytes += o.shard_len;
             if (!aligned_object(o)) {
                 p->obj_fallback.push_back(o);
-                add_urecs(urecs, erecs, brecs, o.data, o.parity, o.shard_len, k);
+                add_urecs(urecs, erecs, brecs, orecs, o.data, o.parity, o.shard_len, k);
                 continue;
             }
             if (k > hbec::kStripeMaxK) {
                 // the object-plan tiled kernel takes <= 8 inputs: every object goes to
                 // the unaligned kernel's records (one launch per pass, not one per object)
-                add_urecs(urecs, erecs, brecs, o.data, o.parity, o.shard_len, k);
+                add_urecs(urecs, erecs, brecs, orecs, o.data, o.parity, o.shard_len, k);
                 continue;
             }
             p->obj_tiled.push_back(o);
@@ -453,12 +518,15 @@ int hbec_plan_objects(hbec_codec* codec, const hbec_object* objects, uint64_t n,
         int urc = upload(urecs, &p->d_urecs, "plan unaligned records");
         if (!urc) urc = upload(erecs, &p->d_erecs, "plan edge records");
         if (!urc) urc = upload(brecs, &p->d_brecs, "plan large-shard records");
+        if (!urc) urc = upload(orecs, &p->d_orecs, "plan stripe records");
         if (urc) {
             if (p->d_tiles) (void)hipFree(p->d_tiles);
             if (p->d_urecs) (void)hipFree(p->d_urecs);
             if (p->d_erecs) (void)hipFree(p->d_erecs);
+            if (p->d_brecs) (void)hipFree(p->d_brecs);
             return urc;
         }
+        set_orecs(p.get(), orecs);
         p->n_urecs = urecs.size();
         p->n_erecs = erecs.size();
         p->n_brecs = brecs.size();
@@ -473,6 +541,7 @@ void hbec_plan_free(hbec_plan* plan) {
     if (plan->d_urecs) (void)hipFree(plan->d_urecs);
     if (plan->d_erecs) (void)hipFree(plan->d_erecs);
     if (plan->d_brecs) (void)hipFree(plan->d_brecs);
+    if (plan->d_orecs) (void)hipFree(plan->d_orecs);
     delete plan;
 }
 

@@ -156,12 +156,6 @@ __device__ __forceinline__ TileRec load_rec(const TileRec* __restrict__ recs, ui
 // block's 4 waves load and store in step, and an optional s_sleep (x 64
 // cycles) before it.  The trip count is block-uniform: waves past the end
 // load a stand-in tile (the last one) and store nothing.
-#ifndef HBEC_STRIPES_BARRIER
-#define HBEC_STRIPES_BARRIER 1
-#endif
-#ifndef HBEC_STRIPES_SLEEP
-#define HBEC_STRIPES_SLEEP 0
-#endif
 
 template <int K, int R, bool SPLIT, bool ACC = false, bool MIRROR = false>
 __global__ __launch_bounds__(kBlockThreads, 1) void gf_apply_stripes(StripeArgs a,
@@ -205,8 +199,7 @@ __global__ __launch_bounds__(kBlockThreads, 1) void gf_apply_stripes(StripeArgs 
         // return out of order, so waiting for `nxt` is an lgkmcnt(0)
         const uint32_t t2 = tn + nw;
         const TileRec after = load_rec(tiles, t2 < n ? t2 : n - 1u);
-        if (HBEC_STRIPES_SLEEP > 0) __builtin_amdgcn_s_sleep(HBEC_STRIPES_SLEEP);
-        if (HBEC_STRIPES_BARRIER) __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_barrier();
         if constexpr (MIRROR) {
             store_mirror_tile<K, R, U, ACC>(x, a, tb, dst, min_, mout, cur.valid, t < n ? cur.valid : 0u, lane);
             mirror_bases<K, R>(min_, mout, a, nxt);

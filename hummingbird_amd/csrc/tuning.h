@@ -1,0 +1,99 @@
+// tuning.h — the tuned constants of the gfx950 kernels, in one table.
+//
+// Every value was chosen by an interleaved A/B on MI355X (the profile cited
+// beside it).  Kernels use them as constants: there is no alternative code
+// path behind any of them.  A tuning build may override one with -D
+// (hummingbird_amd/build.py build(defs=...), scripts/tune*.py); the product
+// build compiles exactly these values.  Runtime tuning knobs are read only in
+// tuning builds (HBEC_TUNE, kernels.h tune_knob).
+#pragma once
+
+#ifndef HBEC_TUNE
+#define HBEC_TUNE 0  // 1: tune_knob() reads the environment (tuning builds only)
+#endif
+
+// ---- pipelined strided kernels (gf_apply_vec_pipe / pipe2, kernels.hip) ----
+#ifndef HBEC_PIPE_BLOCK
+#define HBEC_PIPE_BLOCK 256  // threads per block: 4 waves, one per SIMD
+#endif
+#ifndef HBEC_PIPE_BLOCKS_PER_CU
+#define HBEC_PIPE_BLOCKS_PER_CU 1  // 2-3 blocks per CU: 49-64 % vs 70.75 % (profiles/r01_tune_grid.jsonl)
+#endif
+#ifndef HBEC_PIPE_U_BIG
+#define HBEC_PIPE_U_BIG 3  // KiB per input per wave tile, 5 <= K <= 8: 8+3 74.0 % vs 72.9 % at 2 KiB
+#endif
+#ifndef HBEC_PIPE_SLEEP
+#define HBEC_PIPE_SLEEP 6  // x 64 cycles after the next tile's loads, K <= 4 (profiles/r01_tune_sleep*.jsonl)
+#endif
+#ifndef HBEC_PIPE2_SLEEP
+#define HBEC_PIPE2_SLEEP 8  // pipe2 with its block barrier: 6 and 8 tie, 12 loses 4 % (r01_tune_sleep_pipe2)
+#endif
+#ifndef HBEC_PIPE_V2_MAXK
+#define HBEC_PIPE_V2_MAXK 4  // pipe2 up to K = 4: +1.6 % at 4+2, -7 % at 8+3 (profiles/r01_tune_pipe2.jsonl)
+#endif
+
+// ---- unpipelined strided kernel (gf_apply_vec: accumulate passes) ----
+#ifndef HBEC_WAVES_PER_SIMD
+#define HBEC_WAVES_PER_SIMD 4  // occupancy floor
+#endif
+#ifndef HBEC_TILE_SMALL
+#define HBEC_TILE_SMALL 4  // KiB sub-tiles per wave tile, K <= 2
+#endif
+#ifndef HBEC_TILE_MID
+#define HBEC_TILE_MID 1  // 3 <= K <= 4
+#endif
+#ifndef HBEC_TILE_BIG
+#define HBEC_TILE_BIG 1  // K > 4
+#endif
+
+// ---- register placement of the coefficient tables (gf_device.h) ----
+#ifndef HBEC_ALLVGPR_MIN
+#define HBEC_ALLVGPR_MIN 16  // K*R from which all 5 words live in VGPRs: 8+3 66 -> 73 % (SGPR spills otherwise)
+#endif
+
+// ---- packed short-shard kernels (gf_apply_packed, gf_verify_packed) ----
+#ifndef HBEC_PACKED_U_BIG
+#define HBEC_PACKED_U_BIG 1  // KiB per input per wave tile for K > 4: 70 % vs 57.8 % at 3 KiB
+#endif
+#ifndef HBEC_PACKED_BLOCKS_SMALL
+#define HBEC_PACKED_BLOCKS_SMALL 2  // blocks per CU, K <= 4: +7-10 % over 1 (r02_tune_packed*.jsonl)
+#endif
+#ifndef HBEC_PACKED_BLOCKS_BIG
+#define HBEC_PACKED_BLOCKS_BIG 1
+#endif
+#ifndef HBEC_VERIFY_PACKED_U_SMALL
+#define HBEC_VERIFY_PACKED_U_SMALL 2  // 16-B elements per lane per tile, K <= 4 (r02_verify_packed_tune.jsonl)
+#endif
+#ifndef HBEC_VERIFY_PACKED_U_BIG
+#define HBEC_VERIFY_PACKED_U_BIG 1
+#endif
+#ifndef HBEC_VERIFY_PACKED_BLOCKS_SMALL
+#define HBEC_VERIFY_PACKED_BLOCKS_SMALL 2
+#endif
+#ifndef HBEC_VERIFY_PACKED_BLOCKS_BIG
+#define HBEC_VERIFY_PACKED_BLOCKS_BIG 2
+#endif
+
+// ---- round-2 unaligned kernel (gf_apply_unaligned: 13..16 inputs, S > 2^31) ----
+#ifndef HBEC_UNALIGNED_U
+#define HBEC_UNALIGNED_U 4  // windows per wave tile: u4 > u2, 8 loses 10-20 % (r02_tune_unaligned*.jsonl)
+#endif
+
+// ---- wide kernels (gf_wide: Verify of k > 8, apply of k > 16) ----
+#ifndef HBEC_WIDE_U
+#define HBEC_WIDE_U 2  // windows per tile, each element's tables read once for U columns (10+4 verify 51 -> 55 %)
+#endif
+#ifndef HBEC_WIDE_D
+#define HBEC_WIDE_D 4  // loads in flight per lane (ring depth)
+#endif
+
+// ---- ShardHash (md5.hip) ----
+#ifndef HBEC_MD5_DEPTH
+#define HBEC_MD5_DEPTH 2  // 64-B blocks per load group, two groups ping-ponged: 1 -> 3.85, 2 -> 2.67, 4 -> 2.79 ms
+#endif
+#ifndef HBEC_MD5_DEPTH_LIST
+#define HBEC_MD5_DEPTH_LIST 2
+#endif
+#ifndef HBEC_MD5_PRIO
+#define HBEC_MD5_PRIO 0  // s_setprio of the chain waves beside a co-resident encode
+#endif

@@ -101,15 +101,6 @@ __global__ __launch_bounds__(kPipeBlockThreads, 1) void gf_verify_pipe(PassArgs 
 // (gf_device.h packed_coords), so every lane reads live bytes: K + R loads
 // per 16-B element, the next tile's loads in flight, and each lane flags its
 // own object on a mismatch.
-#ifndef HBEC_VERIFY_PACKED_U_SMALL
-#define HBEC_VERIFY_PACKED_U_SMALL 2  // 16-B elements per lane per tile, K <= 4
-#endif
-#ifndef HBEC_VERIFY_PACKED_U_BIG
-#define HBEC_VERIFY_PACKED_U_BIG 1  // K > 4
-#endif
-#ifndef HBEC_VERIFY_PACKED_BARRIER
-#define HBEC_VERIFY_PACKED_BARRIER 1
-#endif
 __host__ __device__ constexpr int verify_packed_u(int k) {
     return k <= 4 ? HBEC_VERIFY_PACKED_U_SMALL : HBEC_VERIFY_PACKED_U_BIG;
 }
@@ -175,7 +166,7 @@ __global__ __launch_bounds__(kPipeBlockThreads, 1) void gf_verify_packed(PassArg
         packed_coords<U>(nxt, tn < n ? tn : n - 1u, lane, a.n_elems, spo, inv);
         u32x4 y[U][K + R];
         packed_verify_load<K, R, U>(y, a, nxt);
-        if (HBEC_VERIFY_PACKED_BARRIER) __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_barrier();
         packed_check<K, R, U>(x, a, tb, cur, t, t < n ? a.n_elems : 0u, lane, flags);
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -284,12 +275,6 @@ int is_verify_packed_shape(int k, int r, uint64_t shard_len) {
 
 int verify_packed_tile_elems(int k) { return verify_packed_u(k) * 64; }
 
-#ifndef HBEC_VERIFY_PACKED_BLOCKS_SMALL
-#define HBEC_VERIFY_PACKED_BLOCKS_SMALL 2
-#endif
-#ifndef HBEC_VERIFY_PACKED_BLOCKS_BIG
-#define HBEC_VERIFY_PACKED_BLOCKS_BIG 2
-#endif
 
 hipError_t verify_packed_occupancy(int k, int r, int* blocks_per_cu) {
     const void* fn = verify_packed_kernel(k, r);

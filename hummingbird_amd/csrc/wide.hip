@@ -28,14 +28,8 @@ namespace hbec {
 
 constexpr uint32_t kWideStore = 62;             // compared columns per 64-lane window
 constexpr uint32_t kWideWin = kWideStore * 16;  // shard bytes per window
-#ifndef HBEC_WIDE_U
-#define HBEC_WIDE_U 2  // windows per tile: each element's tables are read once for U columns (10+4 verify 51 -> 55 %, r3b7)
-#endif
 constexpr int kWideU = HBEC_WIDE_U;
 constexpr uint32_t kWideTile = kWideU * kWideWin;  // shard bytes per tile
-#ifndef HBEC_WIDE_D
-#define HBEC_WIDE_D 4  // loads in flight per lane (ring depth)
-#endif
 constexpr int kWideD = HBEC_WIDE_D;
 
 // LDS per element j of a tile (inputs 0..K-1, then stored parity K..K+R-1):

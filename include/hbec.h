@@ -30,6 +30,22 @@
 extern "C" {
 #endif
 
+/* Environment.  The library reads these variables once, at first use; every
+ * other setting is a compiled constant (hummingbird_amd/csrc/tuning.h).
+ *
+ *   variable                    default  meaning
+ *   HBEC_HOST_RINGS             8        host-path staging rings per device (callers beyond wait)
+ *   HBEC_HOST_SLOT_MB           64       input bytes per ring slot (3 slots per ring)
+ *   HBEC_HOST_THREADS           16       copy threads of a ring (capped by the host's cores;
+ *                                        OMP_NUM_THREADS when set)
+ *   HBEC_HASH_ARENA_MB          1024     device hash arena per ring for encode + ShardHash
+ *   HBEC_ZEROCOPY               1        0: stage pinned stripes through the ring too
+ *   HBEC_COALESCE               1        0: no grouping of concurrent per-call pinned calls
+ *   HBEC_PERCALL_CONCURRENCY    16       per-call pageable applies at once (0: no limit)
+ *   HBEC_BATCHER_WORKERS        2        batcher worker threads (1..8)
+ *   HBEC_BATCHER_MD5_WORKERS    4        batcher workers for encode + ShardHash groups (0..16)
+ */
+
 /* ABI version.  2: hbec_ec_shard_length's data_shards became int64_t (Go's
  * int, as parseECScheme returns it); it was int in version 1, so a caller
  * compiled against a version-1 header must be rebuilt (a 32-bit argument
@@ -111,11 +127,10 @@ int hbec_verify_databuf(hbec_codec* codec, const uint8_t* databuf, size_t shard_
  * stripes (the *_databuf entries, and hbec_encode / hbec_reconstruct when
  * the shard pointers are one buffer's consecutive slots) in pinned,
  * device-mapped memory (hbec_host_alloc) are coalesced: while at most
- * HBEC_COALESCE_DIRECT (16) such calls are inside the library each runs alone;
- * beyond that, a call that finds
- * fewer than HBEC_COALESCE_INFLIGHT (2) groups in flight codes itself plus
- * every queued call of the same (device, codec, op, erasure pattern) with
- * one zero-copy launch (up to HBEC_COALESCE_MB, 256 MiB); a lone call runs
+ * 16 such calls are inside the library each runs alone; beyond that, a call
+ * that finds fewer than 2 groups in flight codes itself plus every queued
+ * call of the same (device, codec, op, erasure pattern) with one zero-copy
+ * launch (up to 256 MiB); a lone call runs
  * at once.  Pageable stripes run per call (their staging copies parallel on
  * the callers' threads), at most HBEC_PERCALL_CONCURRENCY (16; 0 = no limit)
  * at once, the rest waiting in arrival order.  HBEC_COALESCE=0 turns the
@@ -130,7 +145,7 @@ int hbec_coalesce_stats(uint64_t* groups, uint64_t* calls);
  * outputs are separate slices): every output byte is written exactly once,
  * but a byte that is also an input of another object or column may be read
  * before or after that write.  Batches are split into launches of at most
- * 2^20 tiles (HBEC_CHUNK_TILES) of whole objects.
+ * 2^20 tiles of whole objects.
  * ------------------------------------------------------------------------- */
 typedef struct {
     void* base;
@@ -256,7 +271,7 @@ int hbec_reconstruct_plan(hbec_codec* codec, const hbec_plan* plan, const uint8_
  * Zero-copy: stripes in pinned, device-mapped host memory are coded IN PLACE
  * by the GPU over PCIe — no staging copies, no CPU gather/scatter — at any
  * alignment and shard length (unaligned ones through the unaligned kernel;
- * HBEC_ZC_UNALIGNED=0 stages those, HBEC_ZEROCOPY=0 stages every stripe).
+ * HBEC_ZEROCOPY=0 stages every stripe).
  * hbec_host_alloc memory qualifies on every device; memory pinned elsewhere
  * (hipHostMalloc, hipHostRegister) on the device it was pinned for.  Not for
  * hbec_encode_host_md5. */
@@ -293,8 +308,7 @@ int hbec_reconstruct_host_devices(hbec_codec* codec, const hbec_stripe* stripes,
  * hash arena as it goes (no staging copy, nothing read twice over PCIe) — at
  * any alignment and shard length (the mirrored gf_odd plan kernel when a
  * stripe is not 16-B aligned or S % 16 != 0; k > 12: the outputs are read
- * back once after the last pass); HBEC_MD5_ZEROCOPY=0 sends them through the
- * ring instead.  Otherwise the
+ * back once after the last pass).  Otherwise the
  * whole batch takes the staging ring.  hbec_host_md5_stats: calls since load
  * that took each way. */
 int hbec_encode_host_md5(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n_stripes, uint8_t* digests);

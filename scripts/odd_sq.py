@@ -15,6 +15,8 @@ Shapes (ecSplit databufs, device-resident, 2048 objects by default):
   r83   8+3 reconstruct {0,1}          gf_odd<8,2,0>
   v83   8+3 Verify                     gf_odd<8,3,2>
   o104  10+4, S = 104 858              gf_odd<10,4,0>
+  r104  10+4 reconstruct {0,1}         gf_odd<10,2,0>
+  o124  12+4, S = 87 389               gf_odd<12,4,0>
   p124  12+4 object plan, S = 87 392   gf_odd_plan<12,4,...>
   v328  32+8 Verify, S = 32 768 + 3    gf_wide<8,...> verify
 One JSON line per shape (median ms, % of 8 TB/s on the algorithmic bytes);
@@ -77,7 +79,7 @@ def main():
     for name in names:
         k, m, s, op = {"a42": (4, 2, MiB // 4, "enc"), "o42": (4, 2, 262143, "enc"), "v42": (4, 2, 262143, "ver"), "r42": (4, 2, 262143, "rec"), "a83": (8, 3, MiB // 8, "enc"),
                        "o83": (8, 3, 131071, "enc"), "r83": (8, 3, 131071, "rec"), "v83": (8, 3, 131071, "ver"),
-                       "o104": (10, 4, 104858, "enc"), "p124": (12, 4, 87392, "plan"),
+                       "o104": (10, 4, 104858, "enc"), "o124": (12, 4, 87389, "enc"), "r104": (10, 4, 104858, "rec"), "p124": (12, 4, 87392, "plan"),
                        "v328": (32, 8, 32771, "ver")}[name]
         enc = RS.New(k, m)
         row = {"lib": os.environ.get("HBEC_LIB", "default"), "label": os.environ.get("AB_LABEL", ""), "round": int(os.environ.get("AB_ROUND", "0")),

@@ -23,194 +23,39 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 OUTDIR = ROOT / "tune_build"
 
-BASE = ["HBEC_VGPR_TABLES=1", "HBEC_XOR3=1"]
-T1 = BASE + ["HBEC_TILE_MID=1"]
-T2 = BASE + ["HBEC_TILE_MID=2"]
-T4 = BASE + ["HBEC_TILE_MID=4"]
-P = T1 + ["HBEC_USE_PIPE=1"]
+# Build-time variants override a tuning.h constant (-D); runtime variants set
+# a tune_knob environment variable, which only a tuning build reads, so every
+# variant is built with HBEC_TUNE=1.  The product values are in tuning.h.
 VARIANTS = {
     "cur": ([], {}),
     # packed kernel (short shards, e.g. 8+3 of 4 KiB objects)
     "pk_vec": ([], {"HBEC_PACKED": "0"}),
+    "pk_u2": (["HBEC_PACKED_U_BIG=2"], {}),
+    "pk_sb1": (["HBEC_PACKED_BLOCKS_SMALL=1"], {}),
+    "pk_sb3": (["HBEC_PACKED_BLOCKS_SMALL=3"], {}),
+    "pk_max2k": ([], {"HBEC_PACKED_MAX_SHARD": "2048"}),
     # packed verify (short shards): run scripts/bench_small.py with HBEC_LIB=tune_build/<name>/libhbec.so
     "vp_u1": (["HBEC_VERIFY_PACKED_U_SMALL=1"], {}),
     "vp_u4": (["HBEC_VERIFY_PACKED_U_SMALL=4"], {}),
     "vp_b1": (["HBEC_VERIFY_PACKED_BLOCKS_SMALL=1", "HBEC_VERIFY_PACKED_BLOCKS_BIG=1"], {}),
-    "vp_b3": (["HBEC_VERIFY_PACKED_BLOCKS_SMALL=3", "HBEC_VERIFY_PACKED_BLOCKS_BIG=2"], {}),
-    "vp_ub2": (["HBEC_VERIFY_PACKED_U_BIG=2"], {}),
-    "vp_nobar": (["HBEC_VERIFY_PACKED_BARRIER=0"], {}),
-    "md5d2": (["HBEC_MD5_DEPTH=2"], {}),
     "md5d4": (["HBEC_MD5_DEPTH=4"], {}),
-    "md5d8": (["HBEC_MD5_DEPTH=8"], {}),
-    "md5d4np": (["HBEC_MD5_DEPTH=4", "HBEC_MD5_PINGPONG=0"], {}),
-    "ch128k": ([], {"HBEC_CHUNK_TILES": str(128 << 10)}),
     "ch256k": ([], {"HBEC_CHUNK_TILES": str(256 << 10)}),
-    "ch512k": ([], {"HBEC_CHUNK_TILES": str(512 << 10)}),
-    "ch1m": ([], {"HBEC_CHUNK_TILES": str(1 << 20)}),
-    "ch2m": ([], {"HBEC_CHUNK_TILES": str(2 << 20)}),
     "ch4m": ([], {"HBEC_CHUNK_TILES": str(4 << 20)}),
-    "chinf": ([], {"HBEC_CHUNK_TILES": str(1 << 40)}),
-    "pk_s4": (["HBEC_PACKED_SLEEP_BIG=4"], {}),
-    "pk_s8": (["HBEC_PACKED_SLEEP_BIG=8"], {}),
-    "pk_u1": (["HBEC_PACKED_U_BIG=1"], {}),
-    "pk_u2": (["HBEC_PACKED_U_BIG=2"], {}),
-    "pk_u1s8": (["HBEC_PACKED_U_BIG=1", "HBEC_PACKED_SLEEP_BIG=8"], {}),
-    "pk_u2s4": (["HBEC_PACKED_U_BIG=2", "HBEC_PACKED_SLEEP_BIG=4"], {}),
-    "pk_nobar": (["HBEC_PACKED_BARRIER=0"], {}),
-    "pk_sb1": (["HBEC_PACKED_BLOCKS_SMALL=1"], {}),
-    "pk_sb3": (["HBEC_PACKED_BLOCKS_SMALL=3"], {}),
-    "pk_sb4": (["HBEC_PACKED_BLOCKS_SMALL=4"], {}),
-    "pk_sb2s4": (["HBEC_PACKED_SLEEP=4"], {}),
-    "pk_sb2nb": (["HBEC_PACKED_BARRIER=0"], {}),
-    "pk_max2k": ([], {"HBEC_PACKED_MAX_SHARD": "2048"}),
-    "pk_max2k_sb1": (["HBEC_PACKED_BLOCKS_SMALL=1"], {"HBEC_PACKED_MAX_SHARD": "2048"}),
-    "pk_max512k": ([], {"HBEC_PACKED_MAX_SHARD": "524288"}),
-    "pk_max512k_sb1": (["HBEC_PACKED_BLOCKS_SMALL=1"], {"HBEC_PACKED_MAX_SHARD": "524288"}),
-    "pk_u3": (["HBEC_PACKED_U_BIG=3"], {}),
-    "pk_u3nb": (["HBEC_PACKED_U_BIG=3", "HBEC_PACKED_BARRIER=0"], {}),
-    "pk_u1s2": (["HBEC_PACKED_SLEEP_BIG=2"], {}),
-    "pk_u1s4": (["HBEC_PACKED_SLEEP_BIG=4"], {}),
-    "pk_sl0": (["HBEC_PACKED_SLEEP=0"], {}),
-    "pk_sl4": (["HBEC_PACKED_SLEEP=4"], {}),
-    "pk_sl12": (["HBEC_PACKED_SLEEP=12"], {}),
-    "pk_nb_sl0": (["HBEC_PACKED_BARRIER=0", "HBEC_PACKED_SLEEP=0"], {}),
-    "pk_b2": ([], {"HBEC_BLOCKS_PER_CU": "2"}),
-    "pk_u1b2": (["HBEC_PACKED_U_BIG=1"], {"HBEC_BLOCKS_PER_CU": "2"}),
-    "pk_u1b4": (["HBEC_PACKED_U_BIG=1"], {"HBEC_BLOCKS_PER_CU": "4"}),
-    "d": ([], {}),
-    # GF-free twin of the shipped kernel: same loop, loads, stores, pacing and
-    # barrier; the field multiply replaced by a plain XOR (parity differs by design)
-    "gfnone": (["HBEC_GF_NONE=1"], {}),
-    "v2": (["HBEC_PIPE_V2=1"], {}),
-    "v2all": (["HBEC_PIPE_V2_MAXK=16"], {}),
-    "v2all_l16": (["HBEC_PIPE_V2_MAXK=16", "HBEC_PIPE_LOADS=16"], {}),
-    "v2all_nobar": (["HBEC_PIPE_V2_MAXK=16", "HBEC_PIPE_BARRIER=0"], {}),
-    "v2u2": (["HBEC_PIPE_V2_MAXK=16", "HBEC_PIPE_U_BIG=2"], {}),
-    "v2u1": (["HBEC_PIPE_V2_MAXK=16", "HBEC_PIPE_U_BIG=1"], {}),
-    "v2u2s4": (["HBEC_PIPE_V2_MAXK=16", "HBEC_PIPE_U_BIG=2", "HBEC_PIPE2_SLEEP_BIG=4"], {}),
-    "v2u2s8": (["HBEC_PIPE_V2_MAXK=16", "HBEC_PIPE_U_BIG=2", "HBEC_PIPE2_SLEEP_BIG=8"], {}),
-    "v2u1s8": (["HBEC_PIPE_V2_MAXK=16", "HBEC_PIPE_U_BIG=1", "HBEC_PIPE2_SLEEP_BIG=8"], {}),
-    "v2all_l24": (["HBEC_PIPE_V2_MAXK=16", "HBEC_PIPE_LOADS=24"], {}),
-    "v1_l16": (["HBEC_PIPE_LOADS=16"], {}),
-    "v2s0": (["HBEC_PIPE_V2=1", "HBEC_PIPE_SLEEP=0"], {}),
-    "u2s6": (["HBEC_PIPE_LOADS=8"], {}),
-    "u2s10": (["HBEC_PIPE_LOADS=8", "HBEC_PIPE_SLEEP=10"], {}),
-    "u2s14": (["HBEC_PIPE_LOADS=8", "HBEC_PIPE_SLEEP=14"], {}),
-    "b2s6": ([], {"HBEC_BLOCKS_PER_CU": "2"}),
-    "b2s12": (["HBEC_PIPE_SLEEP=12"], {"HBEC_BLOCKS_PER_CU": "2"}),
-    "sl0": (["HBEC_PIPE_SLEEP=0"], {}),
-    "sl1": (["HBEC_PIPE_SLEEP=1"], {}),
-    "sl2": (["HBEC_PIPE_SLEEP=2"], {}),
-    "sl3": (["HBEC_PIPE_SLEEP=3"], {}),
-    "sl4": (["HBEC_PIPE_SLEEP=4"], {}),
-    "sl8": (["HBEC_PIPE_SLEEP=8"], {}),
-    "sl5": (["HBEC_PIPE_SLEEP=5"], {}),
-    "sl6": (["HBEC_PIPE_SLEEP=6"], {}),
-    "sl7": (["HBEC_PIPE_SLEEP=7"], {}),
-    "sl9": (["HBEC_PIPE_SLEEP=9"], {}),
-    "sl10": (["HBEC_PIPE_SLEEP=10"], {}),
-    "sl12": (["HBEC_PIPE_SLEEP=12"], {}),
-    "sl16": (["HBEC_PIPE_SLEEP=16"], {}),
-    "sl24": (["HBEC_PIPE_SLEEP=24"], {}),
-    "sl32": (["HBEC_PIPE_SLEEP=32"], {}),
-    "xcd1": ([], {}),
-    "head": ([], {}),  # built by hand from the previous commit's kernels.hip
-    "p2old": (["HBEC_PIPE_BARRIER=0", "HBEC_PIPE2_SLEEP=6"], {}),
-    "p2nobar8": (["HBEC_PIPE_BARRIER=0", "HBEC_PIPE2_SLEEP=8"], {}),
-    "p2bar6": (["HBEC_PIPE2_SLEEP=6"], {}),
-    "p2bar10": (["HBEC_PIPE2_SLEEP=10"], {}),
-    "p2bar12": (["HBEC_PIPE2_SLEEP=12"], {}),
-    "bar": (["HBEC_PIPE_BARRIER=1"], {}),
-    "bar_sl0": (["HBEC_PIPE_BARRIER=1", "HBEC_PIPE_SLEEP=0"], {}),
-    "bar_sl3": (["HBEC_PIPE_BARRIER=1", "HBEC_PIPE_SLEEP=3"], {}),
-    "bar_sl8": (["HBEC_PIPE_BARRIER=1", "HBEC_PIPE_SLEEP=8"], {}),
-    "bar2": (["HBEC_PIPE_BARRIER=1"], {}),
-    "gc248": ([], {"HBEC_GRID_CAP": "248"}),
-    "gc240": ([], {"HBEC_GRID_CAP": "240"}),
-    "gc224": ([], {"HBEC_GRID_CAP": "224"}),
-    "gc192": ([], {"HBEC_GRID_CAP": "192"}),
-    "gc160": ([], {"HBEC_GRID_CAP": "160"}),
-    "lds_prod": (["HBEC_GF_LDS=1"], {}),
-    "lds_log": (["HBEC_GF_LDS=2"], {}),
-    "g4c64": (["HBEC_SWZ_G=4", "HBEC_SWZ_C=64"], {}),
-    "g16c16": (["HBEC_SWZ_G=16", "HBEC_SWZ_C=16"], {}),
-    "g16c4": (["HBEC_SWZ_G=16", "HBEC_SWZ_C=4"], {}),
-    "g64c4": (["HBEC_SWZ_G=64", "HBEC_SWZ_C=4"], {}),
-    "g64c1": (["HBEC_SWZ_G=64", "HBEC_SWZ_C=1"], {}),
-    "g8c32": (["HBEC_SWZ_G=8", "HBEC_SWZ_C=32"], {}),
-    "xcd0": (["HBEC_XCD_MAP=0"], {}),
-    "prev": (["HBEC_PIPE_LOADS=16", "HBEC_PIPE_BLOCKS_PER_CU=0"], {}),
-    "cur_b1": ([], {"HBEC_BLOCKS_PER_CU": "1"}),
-    "pl8_b1": (["HBEC_PIPE_LOADS=8"], {"HBEC_BLOCKS_PER_CU": "1"}),
-    "pl4_b1": (["HBEC_PIPE_LOADS=4"], {"HBEC_BLOCKS_PER_CU": "1"}),
-    "pl16_b1": (["HBEC_PIPE_LOADS=16"], {"HBEC_BLOCKS_PER_CU": "1"}),
-    "pl24_b1": (["HBEC_PIPE_LOADS=24"], {"HBEC_BLOCKS_PER_CU": "1"}),
-    "pl32_b1": (["HBEC_PIPE_LOADS=32"], {"HBEC_BLOCKS_PER_CU": "1"}),
-    "pl24_b2": (["HBEC_PIPE_LOADS=24"], {"HBEC_BLOCKS_PER_CU": "2"}),
-    "pl4_t128_b1": (["HBEC_PIPE_LOADS=4", "HBEC_PIPE_BLOCK=128"], {"HBEC_BLOCKS_PER_CU": "1"}),
-    "pl4_t128_b2": (["HBEC_PIPE_LOADS=4", "HBEC_PIPE_BLOCK=128"], {"HBEC_BLOCKS_PER_CU": "2"}),
-    "pl4_t64_b2": (["HBEC_PIPE_LOADS=4", "HBEC_PIPE_BLOCK=64"], {"HBEC_BLOCKS_PER_CU": "2"}),
-    "pl4_t64_b3": (["HBEC_PIPE_LOADS=4", "HBEC_PIPE_BLOCK=64"], {"HBEC_BLOCKS_PER_CU": "3"}),
-    "pl4_t64_b4": (["HBEC_PIPE_LOADS=4", "HBEC_PIPE_BLOCK=64"], {"HBEC_BLOCKS_PER_CU": "4"}),
-    "pl4_t512_b1": (["HBEC_PIPE_LOADS=4", "HBEC_PIPE_BLOCK=512"], {"HBEC_BLOCKS_PER_CU": "1"}),
-    "pl12_b1": (["HBEC_PIPE_LOADS=12"], {"HBEC_BLOCKS_PER_CU": "1"}),
-    "pl8_b1_ldplain": (["HBEC_PIPE_LOADS=8", "HBEC_NT_LOADS=0"], {"HBEC_BLOCKS_PER_CU": "1"}),
-    "pl8_b2": (["HBEC_PIPE_LOADS=8"], {"HBEC_BLOCKS_PER_CU": "2"}),
-    "pl4_b2": (["HBEC_PIPE_LOADS=4"], {"HBEC_BLOCKS_PER_CU": "2"}),
-    "pl4_b4": (["HBEC_PIPE_LOADS=4"], {"HBEC_BLOCKS_PER_CU": "4"}),
-    "av16": (["HBEC_ALLVGPR_MIN=16"], {}),
-    "av16_pl8": (["HBEC_ALLVGPR_MIN=16", "HBEC_PIPE_LOADS=8"], {}),
-    "pl8": (["HBEC_PIPE_LOADS=8"], {}),
-    "av16_pl12": (["HBEC_ALLVGPR_MIN=16", "HBEC_PIPE_LOADS=12"], {}),
-    "pipe": (P, {}),
-    "pipe_b1": (P, {"HBEC_BLOCKS_PER_CU": "1"}),
-    "pipe_b2": (P, {"HBEC_BLOCKS_PER_CU": "2"}),
-    "pipe_b3": (P, {"HBEC_BLOCKS_PER_CU": "3"}),
-    "pipe_ldplain_b1": (P + ["HBEC_NT_LOADS=0"], {"HBEC_BLOCKS_PER_CU": "1"}),
-    "pipe_stplain_b1": (P + ["HBEC_NT_STORES=0"], {"HBEC_BLOCKS_PER_CU": "1"}),
-    "t1_b1": (T1, {"HBEC_BLOCKS_PER_CU": "1"}),
-    "t1_b2": (T1, {"HBEC_BLOCKS_PER_CU": "2"}),
-    "t1_b3": (T1, {"HBEC_BLOCKS_PER_CU": "3"}),
-    "t2_b1": (T2, {"HBEC_BLOCKS_PER_CU": "1"}),
-    "t2_b2": (T2, {"HBEC_BLOCKS_PER_CU": "2"}),
-    "t4_b1": (T4, {"HBEC_BLOCKS_PER_CU": "1"}),
-    "t4_b2": (T4, {"HBEC_BLOCKS_PER_CU": "2"}),
-    "t1": (T1, {}),
-    "t1_w8": (T1 + ["HBEC_WAVES_PER_SIMD=8"], {}),
-    "t1_b4": (T1, {"HBEC_BLOCKS_PER_CU": "4"}),
-    "t1_b6": (T1, {"HBEC_BLOCKS_PER_CU": "6"}),
-    "t1_b16": (T1, {"HBEC_BLOCKS_PER_CU": "16"}),
-    "t1_b64": (T1, {"HBEC_BLOCKS_PER_CU": "64"}),
-    "t1_w8_b16": (T1 + ["HBEC_WAVES_PER_SIMD=8"], {"HBEC_BLOCKS_PER_CU": "16"}),
-    "t1_ldplain": (T1 + ["HBEC_NT_LOADS=0"], {}),
-    "t1_stplain": (T1 + ["HBEC_NT_STORES=0"], {}),
-    "v0_orig": ([], {}),
-    "vt": (["HBEC_VGPR_TABLES=1"], {}),
-    "vt_x3": (BASE, {}),
-    "x3_ldplain": (BASE + ["HBEC_NT_LOADS=0"], {}),
-    "x3_stplain": (BASE + ["HBEC_NT_STORES=0"], {}),
-    "x3_plain": (BASE + ["HBEC_NT_LOADS=0", "HBEC_NT_STORES=0"], {}),
-    "x3_t1": (BASE + ["HBEC_TILE_MID=1"], {}),
-    "x3_t4": (BASE + ["HBEC_TILE_MID=4"], {}),
-    "x3_b2": (BASE, {"HBEC_BLOCKS_PER_CU": "2"}),
-    "x3_b8": (BASE + ["HBEC_WAVES_PER_SIMD=8"], {"HBEC_BLOCKS_PER_CU": "8"}),
-    "x3_w8": (BASE + ["HBEC_WAVES_PER_SIMD=8"], {}),
+    "sleep4": (["HBEC_PIPE2_SLEEP=4"], {}),
+    "sleep12": (["HBEC_PIPE2_SLEEP=12"], {}),
+    "u2big": (["HBEC_PIPE_U_BIG=2"], {}),
+    "b2": ([], {"HBEC_BLOCKS_PER_CU": "2"}),
 }
 
 
 def build(names):
-    import shutil
 
     from hummingbird_amd import build as hb
 
     for n in names:
         defs, _ = VARIANTS[n]
         d = OUTDIR / n
-        if not defs:  # env-only variant: a copy of the product library (its own static state when loaded)
-            d.mkdir(parents=True, exist_ok=True)
-            shutil.copy2(hb.build(verbose=False), d / "libhbec.so")
-        else:
-            hb.build(defs=defs, lib=d / "libhbec.so", objdir=d / "obj", verbose=False)
+        hb.build(defs=["HBEC_TUNE=1"] + list(defs), lib=d / "libhbec.so", objdir=d / "obj", verbose=False)
         print("built", n, flush=True)
 
 

@@ -19,29 +19,14 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 
+# variants override tuning constants of odd_impl.h (-D), built with
+# HBEC_TUNE=1 so runtime tune_knob variables (HBEC_ODD_BPC, ...) are read
 VARIANTS = {
     "base": [],
-    "u2": ["HBEC_ODD_U_SMALL=2"],
-    "uv4": ["HBEC_ODD_U_VERIFY=4"],
-    "nobar": ["HBEC_ODD_BARRIER=0"],
-    "sleep": ["HBEC_ODD_SLEEP=6"],
-    # round 3, second set
-    "aload": ["HBEC_ODD_ALOAD=1"],
-    # "edge" (HBEC_ODD_EDGE_PLAIN=1) and "ntst0" (HBEC_ODD_NT_ST=0): measured in
-    # profiles/r03_tune_odd4.jsonl, rejected, code removed
-    "planu2": ["HBEC_ODD_PLAN_U=2"],
-    "maxk12": ["HBEC_ODD_MAXK=12"],
-    "aload4": ["HBEC_ODD_ALOAD=2"],
-    "wd8": ["HBEC_WIDE_D=8"],
-    "wu2": ["HBEC_WIDE_U=2"],
-    "wu1d8": ["HBEC_WIDE_U=1", "HBEC_WIDE_D=8"],
-    "wd8u2": ["HBEC_WIDE_D=8"],
-    "carry": ["HBEC_ODD_CARRY=1"],
+    "nocarry": ["HBEC_ODD_CARRY=0"],
     "umid2": ["HBEC_ODD_U_MID=2"],
-    "umid3": ["HBEC_ODD_U_MID=3"],
-    "ldstab": ["HBEC_ODD_LDSTAB=1"],
-    "pin": ["HBEC_ODD_PIN=5"],
-    "pinlb2": ["HBEC_ODD_PIN=5", "HBEC_ODD_LB=2"],
+    "uv4": ["HBEC_ODD_U_VERIFY=4"],
+    "planu1": ["HBEC_ODD_PLAN_U=1"],
 }
 
 MiB = 1 << 20
@@ -56,7 +41,7 @@ def build(names=None):
         if names and name not in names:
             continue
         out = ROOT / "tune_build" / f"odd_{name}"
-        Bd.build(defs=defs, lib=out / "libhbec.so", objdir=out / "obj", verbose=False)
+        Bd.build(defs=["HBEC_TUNE=1"] + defs, lib=out / "libhbec.so", objdir=out / "obj", verbose=False)
         print("built", out, flush=True)
 
 

@@ -312,3 +312,19 @@ def test_verify_validation_before_device():
         enc.Verify([np.ones(8, np.uint8)] * 5 + [np.zeros(0, np.uint8)])  # a missing shard is not allowed
     with pytest.raises(RS.ErrShardNoData):
         enc.Verify([np.zeros(0, np.uint8)] * 6)
+
+
+def test_environment_knobs_are_the_documented_table():
+    """The library reads the environment in one place (env_knob, hbec.cpp);
+    the variables it reads in the product build are exactly the table in
+    include/hbec.h (tuning knobs are tune_knob, compiled
+    to their defaults unless HBEC_TUNE=1)."""
+    csrc = ROOT / "hummingbird_amd" / "csrc"
+    src = "\n".join(p.read_text() for p in sorted(csrc.glob("*")) if p.suffix in (".cpp", ".hip", ".h"))
+    assert src.count("getenv(") == 1
+    read = set(re.findall(r'env_(?:knob|size)\("(HBEC_[A-Z0-9_]+)"', src))
+    header = (ROOT / "include" / "hbec.h").read_text()
+    table = header[header.index("/* Environment."):header.index("*/", header.index("/* Environment."))]
+    documented = set(re.findall(r"\*\s+(HBEC_[A-Z0-9_]+)\s+\d", table))
+    assert read == documented, (sorted(read - documented), sorted(documented - read))
+    assert len(documented) <= 10

@@ -509,6 +509,11 @@ def _expected_pool(k, m, pool, layout):
     (4, 2, [MiB, 7, 4096, 1001, MiB + 16, 64, 4097], (1, 3)),
     (10, 4, [4096, 40960, 160], ()),
     (5, 5, [5 * 4096, 5 * 100000, 80], ()),
+    # near-uniform odd sizes: per-object records (gf_odd_planrec + gf_odd_rec)
+    (12, 4, [MiB - i for i in range(1, 9)], (2, 5)),
+    (8, 3, [MiB - 8 * i - 3 for i in range(6)], (0,)),
+    (4, 2, [MiB - 4, MiB - 3, MiB - 1, MiB - 2], (1,)),
+    (20, 4, [20 * 5000 + 1 + i for i in range(5)], (3,)),
 ])
 def test_plan_encode_reconstruct_mixed(k, m, sizes, misalign):
     pool, layout = _stripe_pool(k, m, sizes, misalign=misalign)
@@ -578,6 +583,11 @@ def _object_arenas(k, m, sizes, misalign=()):
     (4, 2, [MiB, 7, 4096, 1001, MiB + 16, 64, 4097], (1, 3)),
     (10, 4, [4096, 40960, 160], ()),
     (5, 5, [5 * 4096, 5 * 100000, 80], ()),
+    # near-uniform odd sizes: per-object records (gf_odd_planrec + gf_odd_rec)
+    (12, 4, [MiB - i for i in range(1, 9)], (2, 5)),
+    (8, 3, [MiB - 8 * i - 3 for i in range(6)], (0,)),
+    (4, 2, [MiB - 4, MiB - 3, MiB - 1, MiB - 2], (1,)),
+    (20, 4, [20 * 5000 + 1 + i for i in range(5)], (3,)),
 ])
 def test_object_plan_encode_reconstruct(k, m, sizes, misalign):
     """hbec_plan_objects: data and parity in separate arenas; every erasure

@@ -154,17 +154,21 @@ def test_unaligned_large_batch_verify():
     assert flags.nonzero().flatten().tolist() == [77]
 
 
-@pytest.mark.parametrize("k,m,n", [(4, 2, 300), (8, 3, 120), (12, 4, 60), (20, 4, 24), (5, 5, 40)])
-def test_plan_random_odd_stripes(k, m, n):
+@pytest.mark.parametrize("k,m,n,lo,hi", [(4, 2, 300, 1, 200_000), (8, 3, 120, 1, 200_000), (12, 4, 60, 1, 200_000),
+                                         (20, 4, 24, 1, 200_000), (5, 5, 40, 1, 200_000),
+                                         (4, 2, 100, 150_000, 150_900), (8, 3, 60, 300_000, 301_000),
+                                         (12, 4, 40, 500_000, 500_100), (20, 4, 12, 400_000, 401_000)])
+def test_plan_random_odd_stripes(k, m, n, lo, hi):
     """Stripe plans whose stripes have random sizes (S % 16 != 0) at random
-    byte offsets: all go through gf_apply_unaligned_plan records in one launch
-    per pass (k = 20: an accumulate pass; m = 5: two output passes).  Encode
-    and Reconstruct of a random erasure set match the oracle; bytes between
-    stripes are untouched."""
+    byte offsets, coded in one launch per pass (k = 20: an accumulate pass;
+    m = 5: two output passes): sizes over [1, 200 000) take per-window
+    records (gf_odd_plan), near-uniform sizes per-stripe records (gf_odd_rec).
+    Encode and Reconstruct of a random erasure set match the oracle; bytes
+    between stripes are untouched."""
     rng = np.random.default_rng(k * 1000 + m * 10 + n)
     layout, off = [], 0
     for _ in range(n):
-        size = int(rng.integers(1, 200_000))
+        size = int(rng.integers(lo, hi))
         s = -(-size // k)
         off += int(rng.integers(1, 40))
         layout.append((off, s))

@@ -76,7 +76,7 @@ def _one(kernels, mangled):
 
 
 def test_odd_plan_kernels_use_no_lds(kernels):
-    plans = {n: k for n, k in kernels.items() if "gf_odd_plan" in n}
+    plans = {n: k for n, k in kernels.items() if "gf_odd_planILi" in n}
     assert len(plans) >= 12 * 4
     bad = {n: k[".group_segment_fixed_size"] for n, k in plans.items() if k[".group_segment_fixed_size"] != 0}
     assert not bad, bad
