@@ -959,8 +959,7 @@ static int wide_launches(const hbec_view* in, int k, const uint8_t* coeffs, int 
         void* d = nullptr;
         int rc = scratch_alloc(blob.size() * 8, stream, &d);
         if (rc) return rc;
-        hipError_t e = hipMemcpyAsync(d, blob.data(), blob.size() * 8, hipMemcpyHostToDevice, stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(stream);  // blob is a host vector of this frame
+        hipError_t e = launch_put_words(d, blob.data(), blob.size() * 8, stream);
         WideArgs a;
         std::memset(&a, 0, sizeof(a));
         a.in_base = static_cast<const uint64_t*>(d);
@@ -982,8 +981,7 @@ static int wide_launches(const hbec_view* in, int k, const uint8_t* coeffs, int 
             if (o0 > 0) {
                 std::vector<uint64_t> base(k);
                 for (int j = 0; j < k; ++j) base[j] = blob[j] + o0 * blob[(size_t)k + j];
-                e = hipMemcpyAsync(d, base.data(), (size_t)k * 8, hipMemcpyHostToDevice, stream);
-                if (e == hipSuccess) e = hipStreamSynchronize(stream);
+                e = launch_put_words(d, base.data(), (size_t)k * 8, stream);
                 if (e != hipSuccess) break;
             }
             e = launch(b, R, o0);

@@ -213,6 +213,10 @@ hipError_t launch_verify_wide(int r, const WideArgs& a, uint32_t* flags, int gri
 uint32_t wide_apply_tiles_per_obj(uint64_t shard_len);
 hipError_t launch_apply_wide(int r, const WideArgs& a, int grid, hipStream_t stream);
 
+// bytes (a multiple of 4) from host src to device dst, stream-ordered through
+// kernel arguments (kPutWordsMax words per launch): src may go away on return
+constexpr uint32_t kPutWordsMax = 960;
+hipError_t launch_put_words(void* dst, const void* src, size_t bytes, hipStream_t stream);
 hipError_t launch_fill(uint8_t* dst, uint64_t n_obj, uint64_t obj_len, uint64_t obj_stride, uint64_t base_seed,
                        uint64_t first, int grid, hipStream_t stream);
 hipError_t vec_occupancy(int k, int r, int pipe, int force_stream, int* blocks_per_cu);

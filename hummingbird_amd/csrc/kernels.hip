@@ -23,6 +23,7 @@
 #include <stdint.h>
 
 #include <cstdlib>
+#include <cstring>
 
 #include "gf_device.h"
 #include "kernels.h"
@@ -962,6 +963,32 @@ hipError_t launch_fill(uint8_t* dst, uint64_t n_obj, uint64_t obj_len, uint64_t 
     hipLaunchKernelGGL(fill_splitmix, dim3(grid), dim3(kBlockThreads), 0, stream, dst, n_obj, obj_len, obj_stride,
                        base_seed, first);
     return hipGetLastError();
+}
+
+// Host words to device memory in stream order, carried in the kernel
+// arguments (which the runtime copies at launch): nothing on the host has to
+// outlive the call and the stream is never synchronised.
+struct PutWords {
+    uint32_t n;
+    uint32_t w[kPutWordsMax];
+};
+__global__ __launch_bounds__(kBlockThreads) void put_words(uint32_t* __restrict__ dst, PutWords a) {
+    for (uint32_t i = threadIdx.x; i < a.n; i += blockDim.x) dst[i] = a.w[i];
+}
+
+hipError_t launch_put_words(void* dst, const void* src, size_t bytes, hipStream_t stream) {
+    if (bytes % 4 != 0) return hipErrorInvalidValue;
+    const uint32_t* w = static_cast<const uint32_t*>(src);
+    uint32_t* d = static_cast<uint32_t*>(dst);
+    for (size_t i = 0, n = bytes / 4; i < n; i += kPutWordsMax) {
+        PutWords a;
+        a.n = (uint32_t)std::min<size_t>(kPutWordsMax, n - i);
+        std::memcpy(a.w, w + i, (size_t)a.n * 4);
+        hipLaunchKernelGGL(put_words, dim3(1), dim3(kBlockThreads), 0, stream, d + i, a);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 hipError_t vec_occupancy(int k, int r, int pipe, int force_stream, int* blocks_per_cu) {

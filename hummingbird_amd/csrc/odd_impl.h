@@ -636,6 +636,35 @@ __host__ __device__ constexpr bool odd_rec_lds(int k) { return k >= HBEC_ODD_LDS
 // right before the input is used and waited for there, so they are neither
 // hoisted out of the loop into VGPRs nor left to the waitcnt pass (which does
 // not see them).  The 3 K products per output dword are folded as in gf_dot.
+// TQ broadcast ds_read_b128 at LDS byte address lt + off and their wait, in
+// ONE asm statement: the outputs are valid where the compiler thinks they are
+// (with the wait in a separate statement the register allocator may copy a
+// destination before the data has landed)
+template <int TQ>
+__device__ __forceinline__ void odd_lds_read_tables(u32x4 (&t)[TQ], uint32_t lt, const int off) {
+    static_assert(TQ >= 2 && TQ <= 5, "R <= 4 outputs: 2..5 quads per input");
+    if constexpr (TQ == 2) {
+        asm volatile("ds_read_b128 %0, %2 offset:%3\n ds_read_b128 %1, %2 offset:%4\n s_waitcnt lgkmcnt(0)"
+                     : "=&v"(t[0]), "=&v"(t[1]) : "v"(lt), "i"(off), "i"(off + 16) : "memory");
+    } else if constexpr (TQ == 3) {
+        asm volatile("ds_read_b128 %0, %3 offset:%4\n ds_read_b128 %1, %3 offset:%5\n"
+                     " ds_read_b128 %2, %3 offset:%6\n s_waitcnt lgkmcnt(0)"
+                     : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]) : "v"(lt), "i"(off), "i"(off + 16), "i"(off + 32)
+                     : "memory");
+    } else if constexpr (TQ == 4) {
+        asm volatile("ds_read_b128 %0, %4 offset:%5\n ds_read_b128 %1, %4 offset:%6\n"
+                     " ds_read_b128 %2, %4 offset:%7\n ds_read_b128 %3, %4 offset:%8\n s_waitcnt lgkmcnt(0)"
+                     : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3])
+                     : "v"(lt), "i"(off), "i"(off + 16), "i"(off + 32), "i"(off + 48) : "memory");
+    } else {
+        asm volatile("ds_read_b128 %0, %5 offset:%6\n ds_read_b128 %1, %5 offset:%7\n"
+                     " ds_read_b128 %2, %5 offset:%8\n ds_read_b128 %3, %5 offset:%9\n"
+                     " ds_read_b128 %4, %5 offset:%10\n s_waitcnt lgkmcnt(0)"
+                     : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3]), "=&v"(t[4])
+                     : "v"(lt), "i"(off), "i"(off + 16), "i"(off + 32), "i"(off + 48), "i"(off + 64) : "memory");
+    }
+}
+
 template <int K, int R>
 __device__ __forceinline__ void gf_dot_lds(u32x4 (&acc)[R], const u32x4 (&x)[K], uint32_t lt) {
     constexpr int TQ = (int)odd_lt_stride(R) / 4;
@@ -643,12 +672,7 @@ __device__ __forceinline__ void gf_dot_lds(u32x4 (&acc)[R], const u32x4 (&x)[K],
 #pragma unroll
     for (int j = 0; j < K; ++j) {
         u32x4 t[TQ];
-#pragma unroll
-        for (int q = 0; q < TQ; ++q)
-            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(t[q]) : "v"(lt), "i"((j * TQ + q) * 16));
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-        for (int q = 0; q < TQ; ++q) asm volatile("" : "+v"(t[q]));
+        odd_lds_read_tables<TQ>(t, lt, j * TQ * 16);
         const bool has = (j & 1) != 0;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -699,6 +723,54 @@ __device__ __forceinline__ void odd_sload(u32x8 (&v)[N], const uint32_t* p) {
 #pragma unroll
     for (int i = 0; i < N; ++i) asm volatile("s_load_dwordx8 %0, %1, %2" : "=s"(v[i]) : "s"(p), "n"(32 * i));
 }
+// odd_sload_now: the loads and their wait in ONE asm statement, for the
+// shapes whose SGPR pressure makes the compiler spill or copy record
+// registers (odd_rec_prefetch false): a copy placed between a split load and
+// its wait would read registers the load has not filled yet.
+template <int N>
+__device__ __forceinline__ void odd_sload_now(u32x8 (&v)[N], const uint32_t* p) {
+    // chunks of <= 4 loads, each with its wait (one asm statement per chunk)
+#pragma unroll
+    for (int i = 0; i < N; i += 4) {
+        const uint32_t* q = p + 8 * i;
+        if (N - i == 1) {
+            asm volatile("s_load_dwordx8 %0, %1, 0\n s_waitcnt lgkmcnt(0)" : "=&s"(v[i]) : "s"(q) : "memory");
+        } else if (N - i == 2) {
+            asm volatile("s_load_dwordx8 %0, %2, 0\n s_load_dwordx8 %1, %2, 32\n s_waitcnt lgkmcnt(0)"
+                         : "=&s"(v[i]), "=&s"(v[i + 1]) : "s"(q) : "memory");
+        } else if (N - i == 3) {
+            asm volatile("s_load_dwordx8 %0, %3, 0\n s_load_dwordx8 %1, %3, 32\n s_load_dwordx8 %2, %3, 64\n"
+                         " s_waitcnt lgkmcnt(0)"
+                         : "=&s"(v[i]), "=&s"(v[i + 1]), "=&s"(v[i + 2]) : "s"(q) : "memory");
+        } else {
+            asm volatile("s_load_dwordx8 %0, %4, 0\n s_load_dwordx8 %1, %4, 32\n s_load_dwordx8 %2, %4, 64\n"
+                         " s_load_dwordx8 %3, %4, 96\n s_waitcnt lgkmcnt(0)"
+                         : "=&s"(v[i]), "=&s"(v[i + 1]), "=&s"(v[i + 2]), "=&s"(v[i + 3]) : "s"(q) : "memory");
+        }
+    }
+}
+
+// Split loads (issued a tile ahead, waited after the next tile's arithmetic)
+// only where the compiler keeps the record registers untouched in between:
+// apply with K R <= 24 and Verify, register-resident tables.  The CPU test
+// tests/test_kernel_resources.py::test_record_loads_unread_before_wait reads
+// every shipped instance's code for such a read.
+#ifndef HBEC_ODD_PREFETCH
+#define HBEC_ODD_PREFETCH 1
+#endif
+template <int K, int R, int MODE>
+__host__ __device__ constexpr bool odd_rec_prefetch() {
+    return HBEC_ODD_PREFETCH != 0 && K < HBEC_ODD_LDS_MINK && (MODE == kOddVerify || (MODE == kOddApply && K * R <= 24));
+}
+template <bool PF, int N>
+__device__ __forceinline__ void odd_rec_sload(u32x8 (&v)[N], const uint32_t* p) {
+    if constexpr (PF) {
+        odd_sload(v, p);
+    } else {
+        odd_sload_now(v, p);
+    }
+}
+
 template <int N>
 __device__ __forceinline__ void odd_swait_pin(u32x8 (&v)[N]) {
 #pragma unroll
@@ -891,6 +963,7 @@ template <int K, int R, int MODE>
 __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE>())) void gf_odd_rec(PassArgs a, uint32_t* flags,
                                                                                         const uint32_t* __restrict__ recs) {
     using RC = OddRec<K, R, MODE>;
+    constexpr bool PF = odd_rec_prefetch<K, R, MODE>();
     constexpr int U = odd_u(K, MODE);
     constexpr bool CARRY = odd_rec_carry(U, MODE);
     constexpr uint32_t SPAN = odd_rec_span(U, MODE);
@@ -946,14 +1019,14 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE>())) void
         tt.obj = q.obj;
         tt.live = q.obj < n_obj;
     };
-    odd_sload(L, rec(p) + RC::FW);
+    odd_rec_sload<PF>(L, rec(p) + RC::FW);
     odd_swait();
     odd_swait_pin(L);
     fill(tx, p);
     odd_rec_load<K, R, U, MODE, CARRY>(X, L, tx.v0, lane);
-    odd_sload(tx.f, rec(p));
+    odd_rec_sload<PF>(tx.f, rec(p));
     p = step(p);
-    odd_sload(L, rec(p) + RC::FW);
+    odd_rec_sload<PF>(L, rec(p) + RC::FW);
     odd_swait();
     odd_swait_pin(L);
     odd_swait_pin(tx.f);
@@ -961,9 +1034,9 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE>())) void
                     const OddRT<K, R, MODE>& tw) {
         fill(tz, p);
         odd_rec_load<K, R, U, MODE, CARRY>(Z, L, tz.v0, lane);
-        odd_sload(tz.f, rec(p));
+        odd_rec_sload<PF>(tz.f, rec(p));
         p = step(p);
-        odd_sload(L, rec(p) + RC::FW);
+        odd_rec_sload<PF>(L, rec(p) + RC::FW);
         // keep the loads ahead of the arithmetic below (left to itself the
         // scheduler sinks most of them below the current tile's selector work)
         if (HBEC_ODD_SCHED && odd_rec_unroll(K, R, MODE)) __builtin_amdgcn_sched_barrier(0);

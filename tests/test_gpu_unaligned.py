@@ -95,13 +95,20 @@ def test_unaligned_every_offset_pair(off_in, off_out):
     assert np.array_equal(got, want)
 
 
-@pytest.mark.parametrize("k,m,obj_len", [(4, 2, (1 << 20) - 4), (4, 2, 1000001), (8, 3, (1 << 20) - 8),
-                                         (6, 3, 1 << 20), (10, 4, 1 << 20), (3, 2, 7)])
-def test_databuf_odd_shards_encode_reconstruct(k, m, obj_len):
+@pytest.mark.parametrize("k,m,obj_len,n", [(4, 2, (1 << 20) - 4, 8), (4, 2, 1000001, 8), (8, 3, (1 << 20) - 8, 8),
+                                           (6, 3, 1 << 20, 8), (10, 4, 1 << 20, 8), (3, 2, 7, 8),
+                                           # several tiles per wave (the record prefetch runs ahead):
+                                           # 12+4 / 11+4 / 9+4 with coefficient tables in LDS, 8+4
+                                           # and 8+3 register-resident, 24+4 with a 12-input
+                                           # accumulate pass
+                                           (12, 4, 12 * 87389, 160), (11, 4, (1 << 20) - 3, 160),
+                                           (9, 4, (1 << 20) + 5, 160), (8, 4, (1 << 20) - 8, 160),
+                                           (8, 3, (1 << 20) - 8, 200), (4, 2, (1 << 20) - 4, 200),
+                                           (24, 4, (1 << 20) - 7, 96)])
+def test_databuf_odd_shards_encode_reconstruct(k, m, obj_len, n):
     """ecSplit databufs of objects whose size gives S % 16 != 0 (shard i at
     i*S, rows of (k+m)*S): Encode against the oracle, then Reconstruct and
     ReconstructData of random erasures restore every shard."""
-    n = 8
     s = -(-obj_len // k)
     rng = np.random.default_rng(obj_len + k)
     rows = torch.empty((n, (k + m) * s), dtype=torch.uint8, device="cuda")
