@@ -169,12 +169,13 @@ static int odd_launches(const PassArgs& a, int K, int R, int mode, bool accumula
                     for (int q = 0; q < 5; ++q) b.tab[r][j][q] = a.tab[r][c1 + j][q];
             }
             const int m = mode == 2 ? 2 : ((accumulate || c1 > 0) ? 1 : 0);
-            const uint64_t tpo = odd_tiles_per_obj(K1, m, shard_len);
+            const bool use_rec = odd_uses_records(K1, R);
+            const uint64_t tpo = odd_tiles_per_obj(K1, m, shard_len, use_rec);
             const uint64_t max_obj = std::max<uint64_t>(1, std::min<uint64_t>((1ull << 31), g_chunk_tiles) / tpo);
             // per-object records of this pass (stream-ordered scratch, freed after its launches)
             uint32_t* recs = nullptr;
             const uint64_t rw = odd_rec_words(K1, R, m);
-            if (odd_uses_records()) {
+            if (use_rec) {
                 rc = scratch_alloc(n_obj * rw * 4, stream, reinterpret_cast<void**>(&recs));
                 if (rc) return rc;
                 PassArgs p = b;

@@ -150,14 +150,15 @@ uint64_t urec_tile_for(int k, bool mirror);  // records read by a k-input pass (
 uint64_t urec_span(uint64_t shard_len);  // 0: no main-kernel records (gf_odd: S <= odd_min_main())
 uint32_t odd_tile_bytes(int k);       // shard bytes per wave tile of the strided kernel
 uint32_t odd_plan_tile_bytes();       // shard bytes per plan record
-uint32_t odd_tiles_per_obj(int k, int mode, uint64_t shard_len);
+uint32_t odd_tiles_per_obj(int k, int mode, uint64_t shard_len, bool records);
 // shards of at most this many bytes are coded by gf_odd_edges alone
 uint64_t odd_min_main();
 // Strided passes code from per-object records (gf_odd_rec): launch_odd_objrec
 // writes odd_rec_words(k, r, mode) words per object of a.n_obj objects into
 // recs (device), before the main launches, whose `recs` point at their first
-// object's record.  Without records (odd_uses_records() false) recs is unused.
-bool odd_uses_records();
+// object's record.  odd_uses_records(k, r): the strided kernel of that shape
+// reads records (launch_odd with recs) rather than the strided bases (recs null).
+bool odd_uses_records(int k, int r);
 uint32_t odd_rec_words(int k, int r, int mode);
 hipError_t launch_odd_objrec(int k, int r, int mode, const PassArgs& a, uint32_t* recs, hipStream_t stream);
 // Plans: the same records for n stripes / objects of orecs (shard lengths

@@ -255,7 +255,7 @@ uint32_t odd_rec_words(int k, int r, int mode) {
     return odd_rec_fw(r, mode) + (uint32_t)((3 * nl + la + 7) & ~7);
 }
 
-bool odd_uses_records() { return HBEC_ODD_REC != 0; }
+bool odd_uses_records(int k, int r) { return odd_use_rec(k, r); }
 
 hipError_t launch_odd_objrec(int k, int r, int mode, const PassArgs& a, uint32_t* recs, hipStream_t stream) {
     if (a.n_obj == 0) return hipSuccess;
@@ -278,10 +278,11 @@ hipError_t launch_odd_planrec(int k, int r, int mode, const UPlanArgs& p, const 
     return hipLaunchKernel((const void*)&gf_odd_planrec, dim3(grid), dim3(kBlockThreads), args, 0, stream);
 }
 
-static const void* odd_kernel(int k, int r, int mode, bool plan, bool mirror = false, bool carry = false) {
-    if (k <= 4) return odd_kernel_range<1, 4>(k, r, mode, plan, mirror, carry);
-    if (k <= 8) return odd_kernel_k58(k, r, mode, plan, mirror);
-    return odd_kernel_k912(k, r, mode, plan, mirror);
+// variant: odd_pick's (plans: carried records; strided: object records)
+static const void* odd_kernel(int k, int r, int mode, bool plan, bool mirror, bool variant) {
+    if (k <= 4) return odd_kernel_range<1, 4>(k, r, mode, plan, mirror, variant);
+    if (k <= 8) return odd_kernel_k58(k, r, mode, plan, mirror, variant);
+    return odd_kernel_k912(k, r, mode, plan, mirror, variant);
 }
 
 #ifndef HBEC_ODD_DEFAULT
@@ -302,7 +303,7 @@ int odd_blocks_per_cu(int mode, int k, int r, bool mirror, bool strided) {
     static const int v = (int)tune_knob("HBEC_ODD_BPC", 0);
     if (v > 0) return v;
     if (mode == kOddVerify) return HBEC_ODD_BPC_VERIFY;
-    if (strided && HBEC_ODD_REC && odd_rec_lds(k)) return 2;  // LDS-table record kernels: 2 waves per SIMD (odd_rec_lb)
+    if (strided && odd_use_rec(k, r) && odd_rec_lds(k)) return 2;  // LDS-table record kernels: 2 waves per SIMD (odd_rec_lb)
     return odd_two_blocks(k, r, mode, mirror) ? 2 : HBEC_ODD_BPC_APPLY;  // launch bounds sized for it (odd_lb)
 }
 
@@ -327,9 +328,9 @@ uint32_t odd_plan_tile_bytes() { return (uint32_t)kOddPlanU * kOddWin; }
 
 // Tiles per shard: enough windows for every output block of the shard, from
 // the frame's first column (c0 >= -32) to position S.
-uint32_t odd_tiles_per_obj(int k, int mode, uint64_t shard_len) {
+uint32_t odd_tiles_per_obj(int k, int mode, uint64_t shard_len, bool records) {
     const uint64_t span = shard_len + 32u;
-    const uint64_t tile = HBEC_ODD_REC ? (uint64_t)odd_rec_span(odd_u(k, mode), mode)
+    const uint64_t tile = records ? (uint64_t)odd_rec_span(odd_u(k, mode), mode)
                           : mode == kOddVerify ? (uint64_t)odd_u(k, mode) * odd_win<kOddVerify>()
                                                : (odd_u(k, mode) == 2 && HBEC_ODD_CARRY ? (uint64_t)(64 + kOddStore) * 16u
                                                                                          : (uint64_t)odd_u(k, mode) * kOddWin);
@@ -341,8 +342,7 @@ bool odd_supported(int k, int r) { return k >= 1 && k <= kOddMaxK && r >= 1 && r
 hipError_t launch_odd(int k, int r, int mode, const PassArgs& a, uint32_t* flags, const uint32_t* recs, int grid,
                       hipStream_t stream) {
     if (!pos32_shard(a.shard_len)) return hipErrorInvalidValue;  // 32-bit shard positions
-    if (HBEC_ODD_REC && !recs) return hipErrorInvalidValue;
-    const void* fn = odd_kernel(k, r, mode, false);
+    const void* fn = odd_kernel(k, r, mode, false, false, recs != nullptr);
     if (!fn) return hipErrorInvalidValue;
     void* args[] = {const_cast<PassArgs*>(&a), &flags, &recs};
     return hipLaunchKernel(fn, dim3(grid), dim3(kPipeBlockThreads), args, 0, stream);

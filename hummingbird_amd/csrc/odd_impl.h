@@ -74,9 +74,6 @@ constexpr uint64_t kOddMinMain = (uint64_t)kOddEdgeSlots;
 #ifndef HBEC_ODD_LDSTAB
 #define HBEC_ODD_LDSTAB 0  // 1: K > 8 read the coefficient tables from LDS per input (fewer VGPRs, more waves)
 #endif
-#ifndef HBEC_ODD_SCHED
-#define HBEC_ODD_SCHED 1  // record kernels: scheduling barrier after the next tile's loads
-#endif
 #ifndef HBEC_ODD_PLAN_U
 #define HBEC_ODD_PLAN_U 2  // windows per plan record (2: odd 4+2 stripe plan 52.9 -> 59.5 %, r03b4)
 #endif
@@ -104,19 +101,13 @@ constexpr int kOddPlanU = HBEC_ODD_PLAN_U;  // plans: windows per record
 __host__ __device__ constexpr bool odd_rec_carry(int u, int mode) {
     return mode == kOddVerify ? (HBEC_ODD_VCARRY != 0 && u >= 2) : (HBEC_ODD_CARRY != 0 && u == 2);
 }
-// unrolled by two (no register copies between tiles) unless two live tile
-// buffers would not fit: the 2-block pinned shapes (10+4: 175 VGPRs spilled)
-#ifndef HBEC_ODD_UNROLL
-#define HBEC_ODD_UNROLL 1
-#endif
-#ifndef HBEC_ODD_LDS_UNROLL
-#define HBEC_ODD_LDS_UNROLL 1
-#endif
-__host__ __device__ constexpr bool odd_two_blocks(int k, int r, int mode, bool mir);
-__host__ __device__ constexpr bool odd_rec_lds(int k);
-__host__ __device__ constexpr bool odd_rec_unroll(int k, int r, int mode) {
-    return HBEC_ODD_UNROLL != 0 && (odd_rec_lds(k) ? HBEC_ODD_LDS_UNROLL != 0 : !odd_two_blocks(k, r, mode, false));
-}
+// Strided batches code from object records (gf_odd_rec) when they carry at
+// least 24 products per column (K R >= 24: 8+3, 10+4, 12+4 encode, 8+3
+// Verify), gf_odd below: the per-tile base arithmetic the records remove only
+// showed where the field arithmetic already filled the issue slots (round-4
+// A/B, profiles/r04_ab_odd.jsonl: 8+3 encode 59.3 -> 64.6 %, 12+4 51.2 ->
+// 57.3 %; 4+2 encode 70.5 vs 67.6 % and 10+2 65.8 vs 60.6 % for gf_odd).
+__host__ __device__ constexpr bool odd_use_rec(int k, int r) { return k * r >= 24; }
 // shard bytes per wave tile of the record kernel
 __host__ __device__ constexpr uint32_t odd_rec_span(int u, int mode) {
     return odd_rec_carry(u, mode) ? (mode == kOddVerify ? (64u * (uint32_t)u - 1u) * 16u : (64u + kOddStore) * 16u)
@@ -1001,10 +992,10 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE>())) void
         return recs + (size_t)__builtin_amdgcn_readfirstlane(p.obj < n_obj ? p.obj : n_obj - 1u) * RC::RW;
     };
     auto v0 = [&](const OddPos& p) { return (p.obj < n_obj ? p.ti : tpo - 1u) * SPAN; };
-    // Unrolled by two over buffers X and Y, so no tile's registers are
-    // copied: each half issues one buffer's loads (tile P, L = its load
-    // record, waited), fetches the next tile's load record into L and P's
-    // finish record, then codes the other buffer's tile.
+    // Each step issues the next tile's loads (P, L = its load record,
+    // waited), fetches the tile after it's load record into L and P's finish
+    // record, codes the current tile, then copies the next tile's registers
+    // over the current ones.
     OddPos p;
     {
         const uint32_t t = wave0 + dw;
@@ -1037,38 +1028,18 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE>())) void
         odd_rec_sload<PF>(tz.f, rec(p));
         p = step(p);
         odd_rec_sload<PF>(L, rec(p) + RC::FW);
-        // keep the loads ahead of the arithmetic below (left to itself the
-        // scheduler sinks most of them below the current tile's selector work)
-        if (HBEC_ODD_SCHED && odd_rec_unroll(K, R, MODE)) __builtin_amdgcn_sched_barrier(0);
         if (MODE == kOddVerify ? HBEC_ODD_VBARRIER : HBEC_ODD_BARRIER) __builtin_amdgcn_s_barrier();
         odd_rec_finish<K, R, U, MODE, CARRY>(W, tw, a.tab, tb, lane, flags, lt);
         odd_swait();
         odd_swait_pin(L);
         odd_swait_pin(tz.f);
     };
-    if constexpr (odd_rec_unroll(K, R, MODE)) {
-        for (uint32_t b0 = wave0 + nw;; b0 += 2u * nw) {  // block-uniform trip count
-            if (b0 >= n) {
-                odd_rec_finish<K, R, U, MODE, CARRY>(X, tx, a.tab, tb, lane, flags, lt);
-                break;
-            }
-            half(Y, ty, X, tx);
-            if (b0 + nw >= n) {
-                odd_rec_finish<K, R, U, MODE, CARRY>(Y, ty, a.tab, tb, lane, flags, lt);
-                break;
-            }
-            half(X, tx, Y, ty);
-        }
-    } else {
-        // one buffer pair, the next tile copied over the current one (the
-        // register-bound shapes, where two live buffers spill)
-        for (uint32_t b0 = wave0 + nw; b0 < n; b0 += nw) {  // block-uniform trip count
-            half(Y, ty, X, tx);
-            X = Y;
-            tx = ty;
-        }
-        odd_rec_finish<K, R, U, MODE, CARRY>(X, tx, a.tab, tb, lane, flags, lt);
+    for (uint32_t b0 = wave0 + nw; b0 < n; b0 += nw) {  // block-uniform trip count
+        half(Y, ty, X, tx);
+        X = Y;
+        tx = ty;
     }
+    odd_rec_finish<K, R, U, MODE, CARRY>(X, tx, a.tab, tb, lane, flags, lt);
 }
 
 template <int K, int R, int MODE, bool MIR = false, bool CARRY = false>
@@ -1080,12 +1051,12 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_lb<K, R, MODE, MIR>())) voi
 // ---------------------------------------------------------------------------
 // launch table: kernel of (K, r, mode, plan?, mirrored?)
 // ---------------------------------------------------------------------------
-#ifndef HBEC_ODD_REC
-#define HBEC_ODD_REC 1  // strided batches: object records (gf_odd_rec) instead of per-tile base arithmetic (gf_odd)
-#endif
+// variant: plans, the carried-record kernel; strided, the object-record
+// kernel (gf_odd_rec) instead of gf_odd
 template <int K, int R, int MODE>
-static const void* odd_pick(bool plan, bool mirror, bool carry) {
-    if (!plan) return HBEC_ODD_REC ? (const void*)&gf_odd_rec<K, R, MODE> : (const void*)&gf_odd<K, R, MODE>;
+static const void* odd_pick(bool plan, bool mirror, bool variant) {
+    const bool carry = variant;
+    if (!plan) return variant ? (const void*)&gf_odd_rec<K, R, MODE> : (const void*)&gf_odd<K, R, MODE>;
     if constexpr (MODE != kOddVerify) {  // plans never verify
         if (mirror) return (const void*)&gf_odd_plan<K, R, MODE, true>;
         if constexpr (HBEC_ODD_CARRY != 0 && odd_plan_u<K>(0) == 2) {
@@ -1112,7 +1083,7 @@ static const void* odd_kernel_k(int r, int mode, bool plan, bool mirror, bool ca
     switch (mode) {
         case kOddApply: return odd_for_r<K, kOddApply>(r, plan, mirror, carry);
         case kOddAcc: return odd_for_r<K, kOddAcc>(r, plan, mirror, carry);
-        case kOddVerify: return plan ? nullptr : odd_for_r<K, kOddVerify>(r, false, false, false);
+        case kOddVerify: return plan ? nullptr : odd_for_r<K, kOddVerify>(r, false, false, carry);
     }
     return nullptr;
 }
@@ -1128,7 +1099,7 @@ static const void* odd_kernel_range(int k, int r, int mode, bool plan, bool mirr
 }
 
 // the other translation units' ranges
-const void* odd_kernel_k58(int k, int r, int mode, bool plan, bool mirror);
-const void* odd_kernel_k912(int k, int r, int mode, bool plan, bool mirror);
+const void* odd_kernel_k58(int k, int r, int mode, bool plan, bool mirror, bool variant);
+const void* odd_kernel_k912(int k, int r, int mode, bool plan, bool mirror, bool variant);
 
 }  // namespace hbec

@@ -4,8 +4,8 @@
 
 namespace hbec {
 
-const void* odd_kernel_k912(int k, int r, int mode, bool plan, bool mirror) {
-    return odd_kernel_range<9, kOddMaxK>(k, r, mode, plan, mirror);
+const void* odd_kernel_k912(int k, int r, int mode, bool plan, bool mirror, bool variant) {
+    return odd_kernel_range<9, kOddMaxK>(k, r, mode, plan, mirror, variant);
 }
 
 }  // namespace hbec

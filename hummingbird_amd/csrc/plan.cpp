@@ -103,6 +103,10 @@ int upload(const std::vector<T>& recs, T** dst, const char* what) {
     return HBEC_OK;
 }
 
+#ifndef HBEC_ODD_PLAN_REC_MINKR
+#define HBEC_ODD_PLAN_REC_MINKR 0
+#endif
+
 // One pass of a plan over per-stripe records: the records (stream-ordered
 // scratch), then gf_odd_rec with the longest stripe's tile count.
 int odd_stripe_rec_pass(int K, int R, int mode, const hbec::UPlanArgs& a, const hbec::OddStripeRecs& o, int cus,
@@ -119,7 +123,7 @@ int odd_stripe_rec_pass(int K, int R, int mode, const hbec::UPlanArgs& a, const 
     hbec::PassArgs c;
     std::memset(&c, 0, sizeof(c));
     std::memcpy(c.tab, a.tab, sizeof(c.tab));
-    const uint64_t tpo = hbec::odd_tiles_per_obj(K, mode, o.s_max);
+    const uint64_t tpo = hbec::odd_tiles_per_obj(K, mode, o.s_max, true);
     c.n_obj = o.n;
     c.shard_len = o.s_max;
     c.tiles_per_obj = (uint32_t)tpo;
@@ -156,13 +160,14 @@ int hbec::launch_unaligned_passes(const URec* recs, uint64_t n_recs, const std::
         // per-stripe records when every stripe's tile count is within 1/32 of
         // the longest one's (the shorter stripes' extra tiles store nothing)
         bool use_orecs = false;
-        if (orecs && orecs->n > 0 && !mirror && hbec::odd_uses_records()) {
+        if (orecs && orecs->n > 0 && !mirror) {
             use_orecs = true;
             for (int c0 = 0; c0 < K_all && use_orecs; c0 += hbec::kOddMaxK) {
                 const int K = std::min(hbec::kOddMaxK, K_all - c0), mode = c0 > 0 ? 1 : 0;
-                const uint64_t t_max = hbec::odd_tiles_per_obj(K, mode, orecs->s_max);
-                const uint64_t t_min = hbec::odd_tiles_per_obj(K, mode, orecs->s_min);
-                use_orecs = t_max * 32 <= t_min * 33 && orecs->n * t_max < (1ull << 31);
+                if (K * std::min(hbec::kMaxR, R_all) < HBEC_ODD_PLAN_REC_MINKR) use_orecs = false;
+                const uint64_t t_max = hbec::odd_tiles_per_obj(K, mode, orecs->s_max, true);
+                const uint64_t t_min = hbec::odd_tiles_per_obj(K, mode, orecs->s_min, true);
+                use_orecs = use_orecs && t_max * 32 <= t_min * 33 && orecs->n * t_max < (1ull << 31);
             }
         }
         // gf_odd_plan: launches of <= 4 outputs x <= kOddMaxK inputs, later input

@@ -49,7 +49,7 @@ def main():
         x.add_(1)
     del x
     row = {"k": k, "m": m, "objects": n,
-           "label": ",".join(f"{v}={os.environ[v]}" for v in sorted(os.environ) if v.startswith("HBEC_MD5")),
+           "label": ",".join(f"{v}={os.environ[v]}" for v in sorted(os.environ) if v.startswith("HBEC_MD5") or v == "HBEC_LIB"),
            "round": int(os.environ.get("AB_ROUND", "0"))}
     row["fused_ms"] = round(timed(lambda: H.encode_md5_views(enc, views, n, S, digests=dig)), 4)
     row["md5_ms"] = round(timed(lambda: H.md5_views(views, n, S, digests=dig)), 4)
