@@ -285,20 +285,11 @@ static const void* odd_kernel(int k, int r, int mode, bool plan, bool mirror, bo
     return odd_kernel_k912(k, r, mode, plan, mirror, variant);
 }
 
-#ifndef HBEC_ODD_DEFAULT
-#define HBEC_ODD_DEFAULT 1
-#endif
 bool odd_enabled() {
-    static const bool on = tune_knob("HBEC_ODD", HBEC_ODD_DEFAULT) != 0;
+    static const bool on = tune_knob("HBEC_ODD", 1) != 0;
     return on;
 }
 
-#ifndef HBEC_ODD_BPC_APPLY
-#define HBEC_ODD_BPC_APPLY 1
-#endif
-#ifndef HBEC_ODD_BPC_VERIFY
-#define HBEC_ODD_BPC_VERIFY 2  // read-only: 4+2 68.5 -> 81 % with 2 blocks per CU (r03_tune_odd3)
-#endif
 int odd_blocks_per_cu(int mode, int k, int r, bool mirror, bool strided) {
     static const int v = (int)tune_knob("HBEC_ODD_BPC", 0);
     if (v > 0) return v;
@@ -314,7 +305,7 @@ uint64_t urec_tile() { return odd_enabled() ? (uint64_t)kOddPlanU * kOddWin : (u
 // windows (mirrored, or K > 4 one window per wave tile).
 uint64_t urec_tile_for(int k, bool mirror) {
     if (!odd_enabled()) return (uint64_t)unaligned_tile_bytes();
-    if (HBEC_ODD_CARRY && !mirror && k <= 4 && kOddPlanU == 2) return (uint64_t)(64 + kOddStore) * 16u;
+    if (!mirror && k <= 4 && kOddPlanU == 2) return (uint64_t)(64 + kOddStore) * 16u;
     return (uint64_t)kOddPlanU * kOddWin;
 }
 uint64_t urec_span(uint64_t shard_len) {
@@ -322,7 +313,7 @@ uint64_t urec_span(uint64_t shard_len) {
     return shard_len > kOddMinMain ? shard_len + 32u : 0u;
 }
 
-uint32_t odd_tile_bytes(int k) { return odd_u(k) == 2 && HBEC_ODD_CARRY ? (64u + kOddStore) * 16u : (uint32_t)odd_u(k) * kOddWin; }
+uint32_t odd_tile_bytes(int k) { return odd_u(k) == 2 ? (64u + kOddStore) * 16u : (uint32_t)odd_u(k) * kOddWin; }
 uint64_t odd_min_main() { return kOddMinMain; }
 uint32_t odd_plan_tile_bytes() { return (uint32_t)kOddPlanU * kOddWin; }
 
@@ -332,7 +323,7 @@ uint32_t odd_tiles_per_obj(int k, int mode, uint64_t shard_len, bool records) {
     const uint64_t span = shard_len + 32u;
     const uint64_t tile = records ? (uint64_t)odd_rec_span(odd_u(k, mode), mode)
                           : mode == kOddVerify ? (uint64_t)odd_u(k, mode) * odd_win<kOddVerify>()
-                                               : (odd_u(k, mode) == 2 && HBEC_ODD_CARRY ? (uint64_t)(64 + kOddStore) * 16u
+                                               : (odd_u(k, mode) == 2 ? (uint64_t)(64 + kOddStore) * 16u
                                                                                          : (uint64_t)odd_u(k, mode) * kOddWin);
     return (uint32_t)((span + tile - 1) / tile);
 }

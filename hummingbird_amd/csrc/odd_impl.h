@@ -15,9 +15,6 @@
 
 namespace hbec {
 
-#ifndef HBEC_ODD_CARRY
-#define HBEC_ODD_CARRY 1  // 2-window apply tiles: window 0 takes window 1's first column, 126 of 128 stored (odd 4+2 65 -> 70 %, r03_tune_carry)
-#endif
 constexpr uint32_t kOddStore = 62;            // blocks stored per 64-lane window
 constexpr uint32_t kOddWin = kOddStore * 16;  // shard bytes per window (992)
 enum : int { kOddApply = 0, kOddAcc = 1, kOddVerify = 2 };
@@ -27,13 +24,14 @@ template <int MODE>
 __host__ __device__ constexpr uint32_t odd_store() { return MODE == kOddVerify ? 63u : kOddStore; }
 template <int MODE>
 __host__ __device__ constexpr uint32_t odd_win() { return odd_store<MODE>() * 16u; }
-// Carry (HBEC_ODD_CARRY, strided apply with 2 windows per wave tile): the
+// Carry (strided apply with 2 windows per wave tile; odd 4+2 65 -> 70 %,
+// r03_tune_carry): the
 // windows are contiguous (columns 0..63 and 64..127 of the tile); window 0
 // gets its lane 63's missing next column from window 1's lane 0 (a readlane
 // + DPP with that value as the out-of-range fill) and stores 64 blocks,
 // window 1 stores 62: 126 of 128 loaded columns instead of 124.
 template <int U, int MODE>
-__host__ __device__ constexpr bool odd_carry() { return HBEC_ODD_CARRY != 0 && U == 2 && MODE != kOddVerify; }
+__host__ __device__ constexpr bool odd_carry() { return U == 2 && MODE != kOddVerify; }
 // first column of window u within a tile, and shard bytes per tile
 template <int U, int MODE, bool CARRY>
 __host__ __device__ constexpr uint32_t odd_wcol(int u) { return CARRY ? 64u * (uint32_t)u : odd_store<MODE>() * (uint32_t)u; }
@@ -44,62 +42,26 @@ constexpr int32_t kOddEdgeSlots = 160;        // edge bytes handled per (shard, 
 // the main kernel runs on shards longer than this (shorter ones: gf_odd_edges only)
 constexpr uint64_t kOddMinMain = (uint64_t)kOddEdgeSlots;
 
-#ifndef HBEC_ODD_SLEEP
-#define HBEC_ODD_SLEEP 0  // x 64 cycles after the next tile's loads
-#endif
-#ifndef HBEC_ODD_BARRIER
-#define HBEC_ODD_BARRIER 1  // apply: one block barrier per tile
-#endif
-#ifndef HBEC_ODD_VBARRIER
-#define HBEC_ODD_VBARRIER 0  // verify: none (8+3 57 -> 66 %, 6+3 63 -> 70 %, profiles/r03_tune_odd3.jsonl)
-#endif
-#ifndef HBEC_ODD_VMIN
-#define HBEC_ODD_VMIN 1  // K*R from which all table words live in VGPRs (1: always)
-#endif
-#ifndef HBEC_ODD_LB
-#define HBEC_ODD_LB 1  // launch_bounds min blocks per CU (register budget)
-#endif
-#ifndef HBEC_ODD_U_SMALL
-#define HBEC_ODD_U_SMALL 2  // windows per wave tile for K <= 4 (0: 4 / K); 2: 4+2 62.5 -> 65 % (r03_tune_odd3)
-#endif
-#ifndef HBEC_ODD_U_MID
-#define HBEC_ODD_U_MID 1  // windows per wave tile for 5 <= K <= 8
-#endif
-#ifndef HBEC_ODD_U_VERIFY
-#define HBEC_ODD_U_VERIFY 0  // windows per wave tile of verify for K <= 4 (0: as apply)
-#endif
-#ifndef HBEC_ODD_ALOAD
-#define HBEC_ODD_ALOAD 0  // 16-B-aligned input loads shifted by realign16: 1 for every K, 2 for K <= 4 (0: dword-aligned loads, 1 DPP)
-#endif
-#ifndef HBEC_ODD_LDSTAB
-#define HBEC_ODD_LDSTAB 0  // 1: K > 8 read the coefficient tables from LDS per input (fewer VGPRs, more waves)
-#endif
-#ifndef HBEC_ODD_PLAN_U
-#define HBEC_ODD_PLAN_U 2  // windows per plan record (2: odd 4+2 stripe plan 52.9 -> 59.5 %, r03b4)
-#endif
+// all coefficient-table words in VGPRs (gf_device.h Tables: v_perm reads one SGPR)
+constexpr int kOddVMin = 1;
 
 // windows per wave tile of the strided kernel: ~4 loads per lane in flight
 // for K <= 4 (as gf_apply_vec_pipe2's 1 KiB x 4 / K), one window above
-__host__ __device__ constexpr int odd_u(int k, int mode = kOddApply) {
-    return (mode == kOddVerify && HBEC_ODD_U_VERIFY > 0 && k <= 4)
-               ? HBEC_ODD_U_VERIFY
-               : (k <= 4 ? (HBEC_ODD_U_SMALL > 0 ? HBEC_ODD_U_SMALL : (4 / k)) : (k <= 8 ? HBEC_ODD_U_MID : 1));
+__host__ __device__ constexpr int odd_u(int k, int = kOddApply) {
+    return k <= 4 ? HBEC_ODD_U_SMALL : (k <= 8 ? HBEC_ODD_U_MID : 1);
 }
-constexpr int kOddPlanU = HBEC_ODD_PLAN_U;  // plans: windows per record
+constexpr int kOddPlanU = HBEC_ODD_PLAN_U;  // plans: windows per record (tuning.h)
 
 // Record kernels (gf_odd_rec): the windows of a wave tile are contiguous
 // columns, and each window but the last takes its lane 63's missing next
 // dword from the following window's lane 0.  Apply / accumulate (U == 2):
 // window 0 stores 64 blocks, window 1 62 (its outputs are realigned, which
-// needs lane l+1's column).  Verify (HBEC_ODD_VCARRY, any U >= 2): windows
+// needs lane l+1's column).  Verify (any U >= 2): windows
 // 0..U-2 compare 64 columns, the last 63, so a tile of 64 U loaded blocks
 // compares 64 U - 1 and neighbouring tiles share one column instead of one
 // per window (odd Verify read 1.067 x its bytes with 63-column windows).
-#ifndef HBEC_ODD_VCARRY
-#define HBEC_ODD_VCARRY 1
-#endif
 __host__ __device__ constexpr bool odd_rec_carry(int u, int mode) {
-    return mode == kOddVerify ? (HBEC_ODD_VCARRY != 0 && u >= 2) : (HBEC_ODD_CARRY != 0 && u == 2);
+    return mode == kOddVerify ? u >= 2 : u == 2;
 }
 // Strided batches code from object records (gf_odd_rec) when they carry at
 // least 24 products per column (K R >= 24: 8+3, 10+4, 12+4 encode, 8+3
@@ -107,7 +69,7 @@ __host__ __device__ constexpr bool odd_rec_carry(int u, int mode) {
 // showed where the field arithmetic already filled the issue slots (round-4
 // A/B, profiles/r04_ab_odd.jsonl: 8+3 encode 59.3 -> 64.6 %, 12+4 51.2 ->
 // 57.3 %; 4+2 encode 70.5 vs 67.6 % and 10+2 65.8 vs 60.6 % for gf_odd).
-__host__ __device__ constexpr bool odd_use_rec(int k, int r) { return k * r >= 24; }
+__host__ __device__ constexpr bool odd_use_rec(int k, int r) { return k * r >= HBEC_ODD_REC_MINKR; }
 // shard bytes per wave tile of the record kernel
 __host__ __device__ constexpr uint32_t odd_rec_span(int u, int mode) {
     return odd_rec_carry(u, mode) ? (mode == kOddVerify ? (64u * (uint32_t)u - 1u) * 16u : (64u + kOddStore) * 16u)
@@ -145,21 +107,14 @@ struct OddIn {
     uint32_t sh;     // the column's first byte within the block (0..3)
 };
 
-// input block alignment of a K-input kernel
-template <int K>
-__host__ __device__ constexpr uint32_t odd_ld_align() {
-    return (HBEC_ODD_ALOAD == 1 || (HBEC_ODD_ALOAD == 2 && K <= 4)) ? 16u : 4u;
-}
-
-template <uint32_t A>
 __device__ __forceinline__ OddIn odd_in(uint64_t base, int32_t S, int32_t c) {
-    const int32_t l4 = (int32_t)((uint32_t)base & (A - 1u));
+    const int32_t l4 = (int32_t)((uint32_t)base & 3u);
     const int32_t t = l4 + c;
     OddIn o;
-    o.base4 = base & ~(uint64_t)(A - 1u);
-    o.sh = (uint32_t)t & (A - 1u);
+    o.base4 = base & ~(uint64_t)3u;
+    o.sh = (uint32_t)t & 3u;
     o.off = t - (int32_t)o.sh;
-    o.lim = ((l4 + S + (int32_t)A - 1) & ~((int32_t)A - 1)) - 16;
+    o.lim = ((l4 + S + 3) & ~3) - 16;
     return o;
 }
 
@@ -169,11 +124,8 @@ __device__ __forceinline__ u32x4 odd_ld(const OddIn& o, int32_t col) {
     return ld16_addr(o.base4 + (uint64_t)(uint32_t)v);
 }
 
-// bytes [sh, sh + 16) of the lane's block and lane l+1's first dword (or,
-// with 16-B-aligned loads, lane l+1's block)
-template <uint32_t A>
+// bytes [sh, sh + 16) of the lane's block and lane l+1's first dword
 __device__ __forceinline__ u32x4 odd_shift_in(const u32x4& v, uint32_t sh) {
-    if constexpr (A == 16u) return realign16(v, lane_next4(v), sh);
     const uint32_t n0 = lane_next(v[0]);
     return u32x4{__builtin_amdgcn_alignbyte(v[1], v[0], sh), __builtin_amdgcn_alignbyte(v[2], v[1], sh),
                  __builtin_amdgcn_alignbyte(v[3], v[2], sh), __builtin_amdgcn_alignbyte(n0, v[3], sh)};
@@ -196,9 +148,7 @@ __device__ __forceinline__ u32x4 lane0(const u32x4& v) {
                  (uint32_t)__builtin_amdgcn_readlane((int)v[2], 0), (uint32_t)__builtin_amdgcn_readlane((int)v[3], 0)};
 }
 
-template <uint32_t A>
 __device__ __forceinline__ u32x4 odd_shift_in_fill(const u32x4& v, uint32_t sh, const u32x4& next0) {
-    if constexpr (A == 16u) return realign16(v, lane_next4_fill(v, next0), sh);
     const uint32_t n0 = lane_next_fill(v[0], next0[0]);
     return u32x4{__builtin_amdgcn_alignbyte(v[1], v[0], sh), __builtin_amdgcn_alignbyte(v[2], v[1], sh),
                  __builtin_amdgcn_alignbyte(v[3], v[2], sh), __builtin_amdgcn_alignbyte(n0, v[3], sh)};
@@ -206,12 +156,10 @@ __device__ __forceinline__ u32x4 odd_shift_in_fill(const u32x4& v, uint32_t sh, 
 
 typedef __attribute__((address_space(1))) uint8_t gu8_t;
 
-// K > 8 with HBEC_ODD_LDSTAB: coefficient tables in LDS (words per input, 16-B padded)
-template <int K>
-__host__ __device__ constexpr bool odd_lds_tables() { return HBEC_ODD_LDSTAB != 0 && K > 8; }
+// coefficient tables in LDS (record kernels, K >= HBEC_ODD_LDS_MINK): words per input, 16-B padded
 __host__ __device__ constexpr uint32_t odd_lt_stride(int r) { return (uint32_t)((r * 5 + 3) & ~3); }
 
-// Pinned outputs (HBEC_ODD_PIN, default on): every output column is
+// Pinned outputs: every output column is
 // materialised right after the field multiply (an empty asm that reads and
 // writes it).  Without it the compiler sinks each output row's products into
 // that row's store branch, r outer and j inner, keeping every input's
@@ -223,15 +171,12 @@ __host__ __device__ constexpr uint32_t odd_lt_stride(int r) { return (uint32_t)(
 // blocks per CU (odd_two_blocks): 10+4 encode 50.0 -> 53.9 %, plans 42.5 ->
 // 50.9 %.  Apply with fewer products (8+3, 6+3, reconstructs) lost 4-8 %
 // pinned, and 12+4 spills.
-#ifndef HBEC_ODD_PIN
-#define HBEC_ODD_PIN 1
-#endif
 __host__ __device__ constexpr bool odd_two_blocks(int k, int r, int mode, bool mir) {
-    return HBEC_ODD_PIN != 0 && !mir && mode == kOddApply && k <= 10 && k * r >= 36;
+    return !mir && mode == kOddApply && k <= 10 && k * r >= 36;
 }
 template <int K, int R, int MODE, bool MIR>
 __host__ __device__ constexpr bool odd_pin_on() {
-    return HBEC_ODD_PIN != 0 && !MIR && ((MODE == kOddVerify && K >= 5 && K <= 8) || odd_two_blocks(K, R, MODE, MIR));
+    return !MIR && ((MODE == kOddVerify && K >= 5 && K <= 8) || odd_two_blocks(K, R, MODE, MIR));
 }
 template <int K, int R, int MODE, bool MIR>
 __device__ __forceinline__ void odd_pin(u32x4 (&acc)[R]) {
@@ -242,7 +187,7 @@ __device__ __forceinline__ void odd_pin(u32x4 (&acc)[R]) {
 }
 
 template <int K, int R, int MODE, bool MIR = false>
-__host__ __device__ constexpr int odd_lb() { return odd_two_blocks(K, R, MODE, MIR) ? 2 : HBEC_ODD_LB; }
+__host__ __device__ constexpr int odd_lb() { return odd_two_blocks(K, R, MODE, MIR) ? 2 : 1; }
 
 // ---- tile sources ----
 // A source names tile t compactly (id(): a few scalars, carried one and two
@@ -347,10 +292,10 @@ __device__ __forceinline__ void odd_load(OddRegs<K, R, U, MODE>& X, const OddTil
     constexpr int NL = OddRegs<K, R, U, MODE>::NL;
     OddIn src[NL];
 #pragma unroll
-    for (int j = 0; j < K; ++j) src[j] = odd_in<odd_ld_align<K>()>(b.in[j], b.S, b.c);
+    for (int j = 0; j < K; ++j) src[j] = odd_in(b.in[j], b.S, b.c);
     if constexpr (MODE == kOddVerify) {
 #pragma unroll
-        for (int r = 0; r < R; ++r) src[K + r] = odd_in<odd_ld_align<K>()>(b.out[r], b.S, b.c);
+        for (int r = 0; r < R; ++r) src[K + r] = odd_in(b.out[r], b.S, b.c);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -385,16 +330,15 @@ __device__ __forceinline__ void odd_st(uint64_t addr, const u32x4& v, bool mine)
 
 template <int K, int R, int U, int MODE, bool MIR = false, bool CARRY = false>
 __device__ __forceinline__ void odd_finish(const OddRegs<K, R, U, MODE>& X, const OddTile<K, R>& b,
-                                           const TabArray& tab, const Tables<K, R, HBEC_ODD_VMIN>& tb, uint32_t lane,
-                                           uint32_t* flags, uint32_t mir = 0, const uint32_t* lt = nullptr) {
-    constexpr int NL = OddRegs<K, R, U, MODE>::NL;
+                                           const TabArray& tab, const Tables<K, R, kOddVMin>& tb, uint32_t lane,
+                                           uint32_t* flags, uint32_t mir = 0) {
     uint32_t sh[K + (MODE == kOddVerify ? R : 0)];
 #pragma unroll
-    for (int j = 0; j < K; ++j) sh[j] = __builtin_amdgcn_readfirstlane(((uint32_t)b.in[j] + (uint32_t)b.c) & (odd_ld_align<K>() - 1u));
+    for (int j = 0; j < K; ++j) sh[j] = __builtin_amdgcn_readfirstlane(((uint32_t)b.in[j] + (uint32_t)b.c) & 3u);
     if constexpr (MODE == kOddVerify) {
 #pragma unroll
         for (int r = 0; r < R; ++r)
-            sh[K + r] = __builtin_amdgcn_readfirstlane(((uint32_t)b.out[r] + (uint32_t)b.c) & (odd_ld_align<K>() - 1u));
+            sh[K + r] = __builtin_amdgcn_readfirstlane(((uint32_t)b.out[r] + (uint32_t)b.c) & 3u);
     }
     const int32_t S = b.S;
     const int32_t hi = S - kOddGuard - 16;  // last block start the main kernel stores / compares
@@ -408,13 +352,13 @@ __device__ __forceinline__ void odd_finish(const OddRegs<K, R, U, MODE>& X, cons
         u32x4 x1[K], x0[K], acc1[R], acc0[R];
 #pragma unroll
         for (int j = 0; j < K; ++j) {
-            x1[j] = odd_shift_in<odd_ld_align<K>()>(X.x[1][j], sh[j]);
-            x0[j] = odd_shift_in_fill<odd_ld_align<K>()>(X.x[0][j], sh[j], lane0(X.x[1][j]));
+            x1[j] = odd_shift_in(X.x[1][j], sh[j]);
+            x0[j] = odd_shift_in_fill(X.x[0][j], sh[j], lane0(X.x[1][j]));
         }
 #pragma unroll
         for (int r = 0; r < R; ++r) acc1[r] = acc0[r] = u32x4{0, 0, 0, 0};
-        gf_dot<K, R, HBEC_ODD_VMIN>(acc1, x1, tab, tb);
-        gf_dot<K, R, HBEC_ODD_VMIN>(acc0, x0, tab, tb);
+        gf_dot<K, R, kOddVMin>(acc1, x1, tab, tb);
+        gf_dot<K, R, kOddVMin>(acc0, x0, tab, tb);
         odd_pin<K, R, MODE, MIR>(acc1);
         odd_pin<K, R, MODE, MIR>(acc0);
 #pragma unroll
@@ -442,40 +386,11 @@ __device__ __forceinline__ void odd_finish(const OddRegs<K, R, U, MODE>& X, cons
         const int32_t cpos = b.c + (int32_t)(u * odd_win<MODE>()) + 16 * (int32_t)lane;  // this lane's column
         u32x4 x[K];
 #pragma unroll
-        for (int j = 0; j < K; ++j) x[j] = odd_shift_in<odd_ld_align<K>()>(X.x[u][j], sh[j]);
+        for (int j = 0; j < K; ++j) x[j] = odd_shift_in(X.x[u][j], sh[j]);
         u32x4 acc[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) acc[r] = u32x4{0, 0, 0, 0};
-        if constexpr (odd_lds_tables<K>()) {
-            // tables of input j: R x 5 words at lt + j * odd_lt_stride(R), broadcast LDS reads
-#pragma unroll
-            for (int j = 0; j < K; ++j) {
-                uint32_t z = 0;
-                // LDSTAB 2: an opaque offset per input keeps each input's table
-                // reads inside the tile (hoisted out of the loop they sit in
-                // VGPRs again, 200 of them at 10+4)
-                if constexpr (HBEC_ODD_LDSTAB >= 2) asm volatile("" : "+v"(z)::"memory");
-                const u32x4* tp = reinterpret_cast<const u32x4*>(lt + z + j * odd_lt_stride(R));
-                uint32_t tw[(R * 5 + 3) & ~3];
-#pragma unroll
-                for (int q = 0; q < (R * 5 + 3) / 4; ++q) {
-                    const u32x4 v = tp[q];
-                    tw[4 * q] = v[0];
-                    tw[4 * q + 1] = v[1];
-                    tw[4 * q + 2] = v[2];
-                    tw[4 * q + 3] = v[3];
-                }
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const Sel sx = selectors(x[j][e]);
-#pragma unroll
-                    for (int r = 0; r < R; ++r)
-                        acc[r][e] ^= gf_mul_sel(sx, tw[5 * r], tw[5 * r + 1], tw[5 * r + 2], tw[5 * r + 3], tw[5 * r + 4]);
-                }
-            }
-        } else {
-            gf_dot<K, R, HBEC_ODD_VMIN>(acc, x, tab, tb);
-        }
+        gf_dot<K, R, kOddVMin>(acc, x, tab, tb);
         odd_pin<K, R, MODE, MIR>(acc);
         if constexpr (MIR && MODE != kOddVerify) {
             // mirror: every arena slot is 16-B aligned, so column i's arena
@@ -504,7 +419,7 @@ __device__ __forceinline__ void odd_finish(const OddRegs<K, R, U, MODE>& X, cons
             const bool mine = b.live != 0u && lane < odd_store<MODE>() && cpos >= kOddGuard && cpos <= hi;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                const u32x4 df = odd_shift_in<odd_ld_align<K>()>(X.x[u][K + r], sh[K + r]) ^ acc[r];
+                const u32x4 df = odd_shift_in(X.x[u][K + r], sh[K + r]) ^ acc[r];
                 bad |= mine && (df[0] | df[1] | df[2] | df[3]) != 0u;
             }
         } else {
@@ -535,17 +450,7 @@ __device__ __forceinline__ void odd_body(const Src& src, uint32_t n, const TabAr
     const uint32_t wave0 = __builtin_amdgcn_readfirstlane(xcd_block() * WPB);  // the block's first wave
     const uint32_t dw = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (wave0 >= n) return;  // whole blocks only: the loop below has block barriers
-    const Tables<K, R, HBEC_ODD_VMIN> tb = load_tables<K, R, HBEC_ODD_VMIN>(tab);
-    __shared__ __attribute__((aligned(16))) uint32_t lt[odd_lds_tables<K>() ? K * odd_lt_stride(R) : 4];
-    if constexpr (odd_lds_tables<K>()) {
-        // whole blocks reach this point (the early return above is per block)
-        const uint32_t ts = odd_lt_stride(R);
-        for (uint32_t i = threadIdx.x; i < (uint32_t)K * ts; i += blockDim.x) {
-            const uint32_t j = i / ts, w = i - j * ts;
-            lt[i] = w < (uint32_t)(R * 5) ? tab[w / 5][j][w % 5] : 0u;
-        }
-        __syncthreads();
-    }
+    const Tables<K, R, kOddVMin> tb = load_tables<K, R, kOddVMin>(tab);
     typename Src::Id cur = src.id(wave0 + dw, n);
     OddRegs<K, R, U, MODE> X;
     {
@@ -561,13 +466,14 @@ __device__ __forceinline__ void odd_body(const Src& src, uint32_t n, const TabAr
             src.at(b, nxt);
             odd_load<K, R, U, MODE, Src::kCarry>(Y, b, lane);
         }
-        if (HBEC_ODD_SLEEP > 0) __builtin_amdgcn_s_sleep(HBEC_ODD_SLEEP);
-        if (MODE == kOddVerify ? HBEC_ODD_VBARRIER : HBEC_ODD_BARRIER) __builtin_amdgcn_s_barrier();
+        // one block barrier per tile for apply; none for Verify (8+3 57 -> 66 %,
+        // 6+3 63 -> 70 %, profiles/r03_tune_odd3.jsonl)
+        if constexpr (MODE != kOddVerify) __builtin_amdgcn_s_barrier();
         const typename Src::Id after = src.id(b0 + dw + nw, n);
         {
             OddTile<K, R> b;
             src.at(b, cur);
-            odd_finish<K, R, U, MODE, MIR, Src::kCarry>(X, b, tab, tb, lane, flags, mir, lt);
+            odd_finish<K, R, U, MODE, MIR, Src::kCarry>(X, b, tab, tb, lane, flags, mir);
         }
         X = Y;
         cur = nxt;
@@ -575,7 +481,7 @@ __device__ __forceinline__ void odd_body(const Src& src, uint32_t n, const TabAr
     }
     OddTile<K, R> b;
     src.at(b, cur);
-    odd_finish<K, R, U, MODE, MIR, Src::kCarry>(X, b, tab, tb, lane, flags, mir, lt);
+    odd_finish<K, R, U, MODE, MIR, Src::kCarry>(X, b, tab, tb, lane, flags, mir);
 }
 
 template <int K, int R, int MODE>
@@ -617,9 +523,6 @@ __host__ __device__ constexpr uint32_t odd_rec_wcol(int u) { return CARRY ? 64u 
 // LDS, one input at a time, instead of holding all 5 K R words in VGPRs
 // (12+4: 240 words; the register-resident kernel spilled 134 SGPRs and ran
 // at 40 % of 8 TB/s).
-#ifndef HBEC_ODD_LDS_MINK
-#define HBEC_ODD_LDS_MINK 9
-#endif
 __host__ __device__ constexpr bool odd_rec_lds(int k) { return k >= HBEC_ODD_LDS_MINK; }
 
 // acc[r] ^= XOR_j C[r][j] x[j], input j's R tables (5 words each) at LDS byte
@@ -746,12 +649,9 @@ __device__ __forceinline__ void odd_sload_now(u32x8 (&v)[N], const uint32_t* p) 
 // apply with K R <= 24 and Verify, register-resident tables.  The CPU test
 // tests/test_kernel_resources.py::test_record_loads_unread_before_wait reads
 // every shipped instance's code for such a read.
-#ifndef HBEC_ODD_PREFETCH
-#define HBEC_ODD_PREFETCH 1
-#endif
 template <int K, int R, int MODE>
 __host__ __device__ constexpr bool odd_rec_prefetch() {
-    return HBEC_ODD_PREFETCH != 0 && K < HBEC_ODD_LDS_MINK && (MODE == kOddVerify || (MODE == kOddApply && K * R <= 24));
+    return !odd_rec_lds(K) && (MODE == kOddVerify || (MODE == kOddApply && K * R <= 24));
 }
 template <bool PF, int N>
 __device__ __forceinline__ void odd_rec_sload(u32x8 (&v)[N], const uint32_t* p) {
@@ -821,7 +721,7 @@ __device__ __forceinline__ void odd_rec_pin(u32x4 (&acc)[R]) {
 
 template <int K, int R, int U, int MODE, bool CARRY>
 __device__ __forceinline__ void odd_rec_finish(const OddRegs<K, R, U, MODE>& X, const OddRT<K, R, MODE>& t,
-                                               const TabArray& tab, const Tables<K, R, HBEC_ODD_VMIN>& tb,
+                                               const TabArray& tab, const Tables<K, R, kOddVMin>& tb,
                                                uint32_t lane, uint32_t* flags, uint32_t lt) {
     constexpr int NL = OddRec<K, R, MODE>::NL;
     const uint32_t shp = odd_w(t.f, 0), dlp = odd_w(t.f, 1);
@@ -848,18 +748,18 @@ __device__ __forceinline__ void odd_rec_finish(const OddRegs<K, R, U, MODE>& X, 
             u32x4 x[K];
 #pragma unroll
             for (int j = 0; j < K; ++j)
-                x[j] = u + 1 < U ? odd_shift_in_fill<4u>(X.x[u][j], sh[j], lane0(X.x[u + 1 < U ? u + 1 : u][j]))
-                                 : odd_shift_in<4u>(X.x[u][j], sh[j]);
+                x[j] = u + 1 < U ? odd_shift_in_fill(X.x[u][j], sh[j], lane0(X.x[u + 1 < U ? u + 1 : u][j]))
+                                 : odd_shift_in(X.x[u][j], sh[j]);
             u32x4 acc[R];
 #pragma unroll
             for (int r = 0; r < R; ++r) acc[r] = u32x4{0, 0, 0, 0};
-            gf_dot<K, R, HBEC_ODD_VMIN>(acc, x, tab, tb);
+            gf_dot<K, R, kOddVMin>(acc, x, tab, tb);
             odd_rec_pin<K, R, MODE>(acc);
             const bool mine = t.live != 0u && (u + 1 < U || lane < 63u) && (v - odd_w(t.f, 2)) <= odd_w(t.f, 3);
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                const u32x4 st = u + 1 < U ? odd_shift_in_fill<4u>(X.x[u][K + r], sh[K + r], lane0(X.x[u + 1 < U ? u + 1 : u][K + r]))
-                                           : odd_shift_in<4u>(X.x[u][K + r], sh[K + r]);
+                const u32x4 st = u + 1 < U ? odd_shift_in_fill(X.x[u][K + r], sh[K + r], lane0(X.x[u + 1 < U ? u + 1 : u][K + r]))
+                                           : odd_shift_in(X.x[u][K + r], sh[K + r]);
                 const u32x4 df = st ^ acc[r];
                 bad |= mine && (df[0] | df[1] | df[2] | df[3]) != 0u;
             }
@@ -873,13 +773,13 @@ __device__ __forceinline__ void odd_rec_finish(const OddRegs<K, R, U, MODE>& X, 
         u32x4 x1[K], x0[K], acc1[R], acc0[R];
 #pragma unroll
         for (int j = 0; j < K; ++j) {
-            x1[j] = odd_shift_in<4u>(X.x[1][j], sh[j]);
-            x0[j] = odd_shift_in_fill<4u>(X.x[0][j], sh[j], lane0(X.x[1][j]));
+            x1[j] = odd_shift_in(X.x[1][j], sh[j]);
+            x0[j] = odd_shift_in_fill(X.x[0][j], sh[j], lane0(X.x[1][j]));
         }
 #pragma unroll
         for (int r = 0; r < R; ++r) acc1[r] = acc0[r] = u32x4{0, 0, 0, 0};
-        gf_dot<K, R, HBEC_ODD_VMIN>(acc1, x1, tab, tb);
-        gf_dot<K, R, HBEC_ODD_VMIN>(acc0, x0, tab, tb);
+        gf_dot<K, R, kOddVMin>(acc1, x1, tab, tb);
+        gf_dot<K, R, kOddVMin>(acc0, x0, tab, tb);
         odd_rec_pin<K, R, MODE>(acc1);
         odd_rec_pin<K, R, MODE>(acc0);
         const uint32_t v0 = t.v0 + 16u * lane, v1 = v0 + 1024u;
@@ -905,21 +805,21 @@ __device__ __forceinline__ void odd_rec_finish(const OddRegs<K, R, U, MODE>& X, 
         const uint32_t v = t.v0 + 16u * odd_rec_wcol<U, MODE, CARRY>(u) + 16u * lane;  // this lane's column
         u32x4 x[K];
 #pragma unroll
-        for (int j = 0; j < K; ++j) x[j] = odd_shift_in<4u>(X.x[u][j], sh[j]);
+        for (int j = 0; j < K; ++j) x[j] = odd_shift_in(X.x[u][j], sh[j]);
         u32x4 acc[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) acc[r] = u32x4{0, 0, 0, 0};
         if constexpr (odd_rec_lds(K)) {
             gf_dot_lds<K, R>(acc, x, lt);
         } else {
-            gf_dot<K, R, HBEC_ODD_VMIN>(acc, x, tab, tb);
+            gf_dot<K, R, kOddVMin>(acc, x, tab, tb);
         }
         odd_rec_pin<K, R, MODE>(acc);
         if constexpr (MODE == kOddVerify) {
             const bool mine = t.live != 0u && lane < odd_store<MODE>() && (v - odd_w(t.f, 2)) <= odd_w(t.f, 3);
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                const u32x4 df = odd_shift_in<4u>(X.x[u][K + r], sh[K + r]) ^ acc[r];
+                const u32x4 df = odd_shift_in(X.x[u][K + r], sh[K + r]) ^ acc[r];
                 bad |= mine && (df[0] | df[1] | df[2] | df[3]) != 0u;
             }
         } else {
@@ -958,7 +858,6 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE>())) void
     constexpr int U = odd_u(K, MODE);
     constexpr bool CARRY = odd_rec_carry(U, MODE);
     constexpr uint32_t SPAN = odd_rec_span(U, MODE);
-    static_assert(odd_ld_align<K>() == 4u, "records hold dword-aligned block bases");
     constexpr uint32_t WPB = kPipeBlockThreads / 64;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t nw = gridDim.x * WPB;
@@ -977,7 +876,7 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE>())) void
         __syncthreads();
     }
     const uint32_t lt = (uint32_t)reinterpret_cast<uintptr_t>(&ltab[0]);  // LDS offset (low half of the flat address)
-    const Tables<K, R, HBEC_ODD_VMIN> tb = load_tables<K, R, HBEC_ODD_VMIN>(a.tab);
+    const Tables<K, R, kOddVMin> tb = load_tables<K, R, kOddVMin>(a.tab);
     const uint32_t qq = nw / tpo, rr = nw - qq * tpo;
     auto step = [&](OddPos p) {
         p.ti += rr;
@@ -1028,7 +927,7 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE>())) void
         odd_rec_sload<PF>(tz.f, rec(p));
         p = step(p);
         odd_rec_sload<PF>(L, rec(p) + RC::FW);
-        if (MODE == kOddVerify ? HBEC_ODD_VBARRIER : HBEC_ODD_BARRIER) __builtin_amdgcn_s_barrier();
+        if constexpr (MODE != kOddVerify) __builtin_amdgcn_s_barrier();
         odd_rec_finish<K, R, U, MODE, CARRY>(W, tw, a.tab, tb, lane, flags, lt);
         odd_swait();
         odd_swait_pin(L);
@@ -1059,7 +958,7 @@ static const void* odd_pick(bool plan, bool mirror, bool variant) {
     if (!plan) return variant ? (const void*)&gf_odd_rec<K, R, MODE> : (const void*)&gf_odd<K, R, MODE>;
     if constexpr (MODE != kOddVerify) {  // plans never verify
         if (mirror) return (const void*)&gf_odd_plan<K, R, MODE, true>;
-        if constexpr (HBEC_ODD_CARRY != 0 && odd_plan_u<K>(0) == 2) {
+        if constexpr (odd_plan_u<K>(0) == 2) {
             if (carry) return (const void*)&gf_odd_plan<K, R, MODE, false, true>;
         }
         return (const void*)&gf_odd_plan<K, R, MODE>;

@@ -103,10 +103,6 @@ int upload(const std::vector<T>& recs, T** dst, const char* what) {
     return HBEC_OK;
 }
 
-#ifndef HBEC_ODD_PLAN_REC_MINKR
-#define HBEC_ODD_PLAN_REC_MINKR 0
-#endif
-
 // One pass of a plan over per-stripe records: the records (stream-ordered
 // scratch), then gf_odd_rec with the longest stripe's tile count.
 int odd_stripe_rec_pass(int K, int R, int mode, const hbec::UPlanArgs& a, const hbec::OddStripeRecs& o, int cus,

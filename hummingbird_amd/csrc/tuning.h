@@ -87,6 +87,32 @@
 #define HBEC_WIDE_D 4  // loads in flight per lane (ring depth)
 #endif
 
+// ---- odd-shard kernels (gf_odd / gf_odd_rec / gf_odd_plan, odd_impl.h) ----
+#ifndef HBEC_ODD_U_SMALL
+#define HBEC_ODD_U_SMALL 2  // windows per wave tile for K <= 4: 4+2 62.5 -> 65 % over 4 / K (r03_tune_odd3)
+#endif
+#ifndef HBEC_ODD_U_MID
+#define HBEC_ODD_U_MID 1  // 5 <= K <= 8 (one window above 8)
+#endif
+#ifndef HBEC_ODD_PLAN_U
+#define HBEC_ODD_PLAN_U 2  // windows per plan record: odd 4+2 stripe plan 52.9 -> 59.5 % (r03b4)
+#endif
+#ifndef HBEC_ODD_REC_MINKR
+#define HBEC_ODD_REC_MINKR 24  // strided batches: object records (gf_odd_rec) from K R >= 24 (r04_ab_odd)
+#endif
+#ifndef HBEC_ODD_LDS_MINK
+#define HBEC_ODD_LDS_MINK 9  // record kernels: coefficient tables in LDS from K = 9 (12+4 encode 51 -> 57 %; from K = 5, 8+3 lost 5 %)
+#endif
+#ifndef HBEC_ODD_PLAN_REC_MINKR
+#define HBEC_ODD_PLAN_REC_MINKR 0  // plans: per-stripe records (gf_odd_planrec + gf_odd_rec) from K R >= this
+#endif
+#ifndef HBEC_ODD_BPC_APPLY
+#define HBEC_ODD_BPC_APPLY 1  // blocks per CU of the strided / plan apply grids (register-bound shapes: odd_two_blocks)
+#endif
+#ifndef HBEC_ODD_BPC_VERIFY
+#define HBEC_ODD_BPC_VERIFY 2  // read-only: 4+2 68.5 -> 81 % with 2 blocks per CU (r03_tune_odd3)
+#endif
+
 // ---- ShardHash (md5.hip) ----
 #ifndef HBEC_MD5_DEPTH
 #define HBEC_MD5_DEPTH 2  // 64-B blocks per load group, two groups ping-ponged: 1 -> 3.85, 2 -> 2.67, 4 -> 2.79 ms

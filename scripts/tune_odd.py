@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """A/B of gf_odd (odd.hip) build variants on odd shard lengths: one variant
-library per process (HBEC_LIB), processes alternated by scripts/tune_odd.sh.
+library per process (HBEC_LIB), processes alternated as scripts/ab_odd.sh does.
 
     python scripts/tune_odd.py build v1,v2        # CPU: tune_build/odd_<v>/libhbec.so
     HBEC_LIB=tune_build/odd_<v>/libhbec.so python scripts/tune_odd.py run <v> [round]
@@ -19,14 +19,14 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 
-# variants override tuning constants of odd_impl.h (-D), built with
+# variants override the odd-kernel constants of tuning.h (-D), built with
 # HBEC_TUNE=1 so runtime tune_knob variables (HBEC_ODD_BPC, ...) are read
 VARIANTS = {
     "base": [],
-    "nocarry": ["HBEC_ODD_CARRY=0"],
     "umid2": ["HBEC_ODD_U_MID=2"],
-    "uv4": ["HBEC_ODD_U_VERIFY=4"],
     "planu1": ["HBEC_ODD_PLAN_U=1"],
+    "rec16": ["HBEC_ODD_REC_MINKR=16"],
+    "lds5": ["HBEC_ODD_LDS_MINK=5"],
 }
 
 MiB = 1 << 20
