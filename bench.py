@@ -100,7 +100,7 @@ def gather_ranks(pg, values, device):
 # its device helpers): a PMC summary is only reported as this run's traffic
 # when it was collected on exactly these sources.
 KERNEL_SOURCES = ("hummingbird_amd/csrc/kernels.hip", "hummingbird_amd/csrc/gf_device.h",
-                  "hummingbird_amd/csrc/kernels.h")
+                  "hummingbird_amd/csrc/kernels.h", "hummingbird_amd/csrc/tuning.h")
 
 
 def kernel_sources_sha256(sources=KERNEL_SOURCES) -> str:
@@ -115,7 +115,8 @@ def kernel_sources_sha256(sources=KERNEL_SOURCES) -> str:
 # 10+4 and gf_odd_edges): their traffic is reported only from a PMC summary
 # collected on exactly these sources (pmc_summary.py records both hashes).
 ODD_SOURCES = ("hummingbird_amd/csrc/odd.hip", "hummingbird_amd/csrc/odd_impl.h", "hummingbird_amd/csrc/gf_device.h",
-               "hummingbird_amd/csrc/kernels.h", "hummingbird_amd/csrc/odd_k58.hip", "hummingbird_amd/csrc/odd_k912.hip")
+               "hummingbird_amd/csrc/kernels.h", "hummingbird_amd/csrc/odd_k58.hip", "hummingbird_amd/csrc/odd_k912.hip",
+               "hummingbird_amd/csrc/tuning.h")
 
 
 def load_pmc(prefix_glob="profiles/r[0-9][0-9]_pmc.json"):

@@ -197,7 +197,7 @@ static int odd_launches(const PassArgs& a, int K, int R, int mode, bool accumula
                 c.tiles_per_obj = (uint32_t)tpo;
                 c.n_tiles = (uint32_t)(no * tpo);
                 const uint64_t want = (c.n_tiles + 3) / 4;
-                const uint64_t cap = (uint64_t)cus * (uint64_t)odd_blocks_per_cu(m, K1, R, false, true);
+                const uint64_t cap = (uint64_t)cus * (uint64_t)odd_blocks_per_cu(m, K1, R, false, use_rec);
                 int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, cap));
                 if (g_grid_cap > 0) grid = std::min(grid, g_grid_cap);
                 hipError_t e = launch_odd(K1, R, m, c, flags ? flags + o0 : nullptr, recs ? recs + o0 * rw : nullptr, grid,

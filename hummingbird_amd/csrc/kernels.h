@@ -140,8 +140,8 @@ __host__ __device__ constexpr bool pos32_shard(uint64_t shard_len) { return shar
 // gf_apply_unaligned family instead, for A/B)
 bool odd_enabled();
 // 4-wave blocks per CU of a gf_odd launch (mode 0 apply, 1 accumulate, 2
-// verify; K, R of the pass; strided: a gf_odd_rec launch)
-int odd_blocks_per_cu(int mode, int k, int r, bool mirror = false, bool strided = false);
+// verify; K, R of the pass; records: a gf_odd_rec launch)
+int odd_blocks_per_cu(int mode, int k, int r, bool mirror = false, bool records = false);
 bool odd_supported(int k, int r);
 // Unaligned plan records (URec) of one stripe / object: p0 = 0, tile, 2*tile,
 // ... while p0 < urec_span(S), for whichever kernel family codes them.

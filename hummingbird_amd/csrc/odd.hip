@@ -290,11 +290,11 @@ bool odd_enabled() {
     return on;
 }
 
-int odd_blocks_per_cu(int mode, int k, int r, bool mirror, bool strided) {
+int odd_blocks_per_cu(int mode, int k, int r, bool mirror, bool records) {
     static const int v = (int)tune_knob("HBEC_ODD_BPC", 0);
     if (v > 0) return v;
     if (mode == kOddVerify) return HBEC_ODD_BPC_VERIFY;
-    if (strided && odd_use_rec(k, r) && odd_rec_lds(k)) return 2;  // LDS-table record kernels: 2 waves per SIMD (odd_rec_lb)
+    if (records && odd_rec_two_blocks(k, r, mode)) return 2;  // launch bounds sized for it (odd_rec_lb)
     return odd_two_blocks(k, r, mode, mirror) ? 2 : HBEC_ODD_BPC_APPLY;  // launch bounds sized for it (odd_lb)
 }
 

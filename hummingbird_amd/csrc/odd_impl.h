@@ -524,6 +524,11 @@ __host__ __device__ constexpr uint32_t odd_rec_wcol(int u) { return CARRY ? 64u 
 // (12+4: 240 words; the register-resident kernel spilled 134 SGPRs and ran
 // at 40 % of 8 TB/s).
 __host__ __device__ constexpr bool odd_rec_lds(int k) { return k >= HBEC_ODD_LDS_MINK; }
+// record kernels run 2 waves per SIMD with LDS tables (and, HBEC_ODD_REC_LB2,
+// register-table apply shapes of K R >= 24)
+__host__ __device__ constexpr bool odd_rec_two_blocks(int k, int r, int mode) {
+    return odd_rec_lds(k) || (HBEC_ODD_REC_LB2 != 0 && mode == kOddApply && k * r >= 24);
+}
 
 // acc[r] ^= XOR_j C[r][j] x[j], input j's R tables (5 words each) at LDS byte
 // address lt + 4 j odd_lt_stride(R): broadcast ds_read_b128 issued by asm
@@ -848,7 +853,7 @@ struct OddPos {
 
 // LDS-table record kernels fit 2 blocks per CU (2 waves per SIMD)
 template <int K, int R, int MODE>
-__host__ __device__ constexpr int odd_rec_lb() { return odd_rec_lds(K) ? 2 : odd_lb<K, R, MODE>(); }
+__host__ __device__ constexpr int odd_rec_lb() { return odd_rec_two_blocks(K, R, MODE) ? 2 : odd_lb<K, R, MODE>(); }
 
 template <int K, int R, int MODE>
 __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE>())) void gf_odd_rec(PassArgs a, uint32_t* flags,

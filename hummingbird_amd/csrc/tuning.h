@@ -106,6 +106,9 @@
 #ifndef HBEC_ODD_PLAN_REC_MINKR
 #define HBEC_ODD_PLAN_REC_MINKR 0  // plans: per-stripe records (gf_odd_planrec + gf_odd_rec) from K R >= this
 #endif
+#ifndef HBEC_ODD_REC_LB2
+#define HBEC_ODD_REC_LB2 0  // experiment: 8+3-class record apply kernels at 2 waves per SIMD
+#endif
 #ifndef HBEC_ODD_BPC_APPLY
 #define HBEC_ODD_BPC_APPLY 1  // blocks per CU of the strided / plan apply grids (register-bound shapes: odd_two_blocks)
 #endif

@@ -29,15 +29,15 @@ for s in "$@"; do
     bench) step bench 600 python bench.py --steps 50 --warmup 10 ;;
     prof)
       mkdir -p "$OUT/prof"
-      (cd /tmp && step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --steps 50 --warmup 10 --no-cpu-baseline --no-host-path --no-small --config5-objects 0) || exit $?
+      (cd /tmp && step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --steps 50 --warmup 10 --no-cpu-baseline --no-host-path --config5-objects 0) || exit $?
       ;;
     pmcfetch)
       mkdir -p "$OUT/pmc_fetch"
-      (cd /tmp && step pmcfetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --no-host-path --no-small --config5-objects 0) || exit $?
+      (cd /tmp && step pmcfetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --no-host-path --config5-objects 0) || exit $?
       ;;
     pmcwrite)
       mkdir -p "$OUT/pmc_write"
-      (cd /tmp && step pmcwrite 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o run -- python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --no-host-path --no-small --config5-objects 0) || exit $?
+      (cd /tmp && step pmcwrite 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o run -- python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --no-host-path --config5-objects 0) || exit $?
       ;;
     cfgprof)
       mkdir -p "$OUT/cfgprof"
