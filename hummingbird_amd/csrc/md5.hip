@@ -135,10 +135,9 @@ struct Md5Args {
 
 
 template <bool ALIGNED, int D>
-__global__ __launch_bounds__(64) void md5_chains(Md5Args a) {
-    if (HBEC_MD5_PRIO > 0) __builtin_amdgcn_s_setprio(HBEC_MD5_PRIO);
+__global__ __launch_bounds__(HBEC_MD5_BLOCK) void md5_chains(Md5Args a) {
     const uint32_t v = blockIdx.y;
-    const uint64_t o = (uint64_t)blockIdx.x * 64u + threadIdx.x;
+    const uint64_t o = (uint64_t)blockIdx.x * HBEC_MD5_BLOCK + threadIdx.x;
     if (o >= a.n_obj) return;
     const uint8_t* p = a.base[v] + o * a.stride[v];
     const uint64_t chain = o * a.chain_stride + a.view0 + v;
@@ -385,11 +384,11 @@ hipError_t launch_md5(const void* const* bases, const uint64_t* strides, int n_v
     a.chain_stride = chain_stride;
     a.view0 = view0;
     a.flags = flags;
-    const dim3 grid((unsigned)((n_obj + 63) / 64), (unsigned)n_views);
+    const dim3 grid((unsigned)((n_obj + HBEC_MD5_BLOCK - 1) / HBEC_MD5_BLOCK), (unsigned)n_views);
     if (aligned)
-        hipLaunchKernelGGL((md5_chains<true, HBEC_MD5_DEPTH>), grid, dim3(64), 0, stream, a);
+        hipLaunchKernelGGL((md5_chains<true, HBEC_MD5_DEPTH>), grid, dim3(HBEC_MD5_BLOCK), 0, stream, a);
     else
-        hipLaunchKernelGGL((md5_chains<false, 1>), grid, dim3(64), 0, stream, a);
+        hipLaunchKernelGGL((md5_chains<false, 1>), grid, dim3(HBEC_MD5_BLOCK), 0, stream, a);
     return hipGetLastError();
 }
 

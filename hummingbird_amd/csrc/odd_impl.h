@@ -524,54 +524,32 @@ __host__ __device__ constexpr uint32_t odd_rec_wcol(int u) { return CARRY ? 64u 
 // (12+4: 240 words; the register-resident kernel spilled 134 SGPRs and ran
 // at 40 % of 8 TB/s).
 __host__ __device__ constexpr bool odd_rec_lds(int k) { return k >= HBEC_ODD_LDS_MINK; }
-// record kernels run 2 waves per SIMD with LDS tables (and, HBEC_ODD_REC_LB2,
-// register-table apply shapes of K R >= 24)
-__host__ __device__ constexpr bool odd_rec_two_blocks(int k, int r, int mode) {
-    return odd_rec_lds(k) || (HBEC_ODD_REC_LB2 != 0 && mode == kOddApply && k * r >= 24);
-}
+// record kernels run 2 waves per SIMD with LDS tables; the register-table
+// ones at 1 (8+3 encode at 2 waves per SIMD, 256 VGPRs with 40 B of spill:
+// 66.8 -> 59.3 %, profiles/r04_ab_odd.jsonl batch I)
+__host__ __device__ constexpr bool odd_rec_two_blocks(int k, int, int) { return odd_rec_lds(k); }
 
 // acc[r] ^= XOR_j C[r][j] x[j], input j's R tables (5 words each) at LDS byte
-// address lt + 4 j odd_lt_stride(R): broadcast ds_read_b128 issued by asm
-// right before the input is used and waited for there, so they are neither
-// hoisted out of the loop into VGPRs nor left to the waitcnt pass (which does
-// not see them).  The 3 K products per output dword are folded as in gf_dot.
-// TQ broadcast ds_read_b128 at LDS byte address lt + off and their wait, in
-// ONE asm statement: the outputs are valid where the compiler thinks they are
-// (with the wait in a separate statement the register allocator may copy a
-// destination before the data has landed)
-template <int TQ>
-__device__ __forceinline__ void odd_lds_read_tables(u32x4 (&t)[TQ], uint32_t lt, const int off) {
-    static_assert(TQ >= 2 && TQ <= 5, "R <= 4 outputs: 2..5 quads per input");
-    if constexpr (TQ == 2) {
-        asm volatile("ds_read_b128 %0, %2 offset:%3\n ds_read_b128 %1, %2 offset:%4\n s_waitcnt lgkmcnt(0)"
-                     : "=&v"(t[0]), "=&v"(t[1]) : "v"(lt), "i"(off), "i"(off + 16) : "memory");
-    } else if constexpr (TQ == 3) {
-        asm volatile("ds_read_b128 %0, %3 offset:%4\n ds_read_b128 %1, %3 offset:%5\n"
-                     " ds_read_b128 %2, %3 offset:%6\n s_waitcnt lgkmcnt(0)"
-                     : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]) : "v"(lt), "i"(off), "i"(off + 16), "i"(off + 32)
-                     : "memory");
-    } else if constexpr (TQ == 4) {
-        asm volatile("ds_read_b128 %0, %4 offset:%5\n ds_read_b128 %1, %4 offset:%6\n"
-                     " ds_read_b128 %2, %4 offset:%7\n ds_read_b128 %3, %4 offset:%8\n s_waitcnt lgkmcnt(0)"
-                     : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3])
-                     : "v"(lt), "i"(off), "i"(off + 16), "i"(off + 32), "i"(off + 48) : "memory");
-    } else {
-        asm volatile("ds_read_b128 %0, %5 offset:%6\n ds_read_b128 %1, %5 offset:%7\n"
-                     " ds_read_b128 %2, %5 offset:%8\n ds_read_b128 %3, %5 offset:%9\n"
-                     " ds_read_b128 %4, %5 offset:%10\n s_waitcnt lgkmcnt(0)"
-                     : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3]), "=&v"(t[4])
-                     : "v"(lt), "i"(off), "i"(off + 16), "i"(off + 32), "i"(off + 48), "i"(off + 64) : "memory");
-    }
-}
-
+// address lt + 4 j odd_lt_stride(R), read by broadcast ds_read_b128 the
+// compiler schedules and waits for (lgkmcnt(N), a few inputs ahead).  The
+// base goes through an empty asm once per window, so the reads cannot be
+// hoisted out of the tile loop into VGPRs (where the tables came from: 12+4
+// held 240 table words and spilled).  The 3 K products per output dword are
+// folded as in gf_dot.  (Reads issued by asm with a wait per input were
+// 0.5-2 % slower: r04_ab_odd.jsonl batch J.)
 template <int K, int R>
 __device__ __forceinline__ void gf_dot_lds(u32x4 (&acc)[R], const u32x4 (&x)[K], uint32_t lt) {
     constexpr int TQ = (int)odd_lt_stride(R) / 4;
     uint32_t pend[4][R];
+    typedef __attribute__((address_space(3))) const u32x4 lds_q;
+    uint32_t z = lt;
+    asm volatile("" : "+v"(z));  // opaque per window: the reads stay in the tile loop
+    lds_q* tp = reinterpret_cast<lds_q*>(static_cast<uintptr_t>(z));
 #pragma unroll
     for (int j = 0; j < K; ++j) {
         u32x4 t[TQ];
-        odd_lds_read_tables<TQ>(t, lt, j * TQ * 16);
+#pragma unroll
+        for (int q = 0; q < TQ; ++q) t[q] = tp[j * TQ + q];
         const bool has = (j & 1) != 0;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {

@@ -92,7 +92,7 @@
 #define HBEC_ODD_U_SMALL 2  // windows per wave tile for K <= 4: 4+2 62.5 -> 65 % over 4 / K (r03_tune_odd3)
 #endif
 #ifndef HBEC_ODD_U_MID
-#define HBEC_ODD_U_MID 1  // 5 <= K <= 8 (one window above 8)
+#define HBEC_ODD_U_MID 1  // 5 <= K <= 8 (one window above 8); 2 / 3 windows: 8+3 encode 66.8 -> 58.8 / 55.2 % (r04_ab_odd I)
 #endif
 #ifndef HBEC_ODD_PLAN_U
 #define HBEC_ODD_PLAN_U 2  // windows per plan record: odd 4+2 stripe plan 52.9 -> 59.5 % (r03b4)
@@ -105,9 +105,6 @@
 #endif
 #ifndef HBEC_ODD_PLAN_REC_MINKR
 #define HBEC_ODD_PLAN_REC_MINKR 0  // plans: per-stripe records (gf_odd_planrec + gf_odd_rec) from K R >= this
-#endif
-#ifndef HBEC_ODD_REC_LB2
-#define HBEC_ODD_REC_LB2 0  // experiment: 8+3-class record apply kernels at 2 waves per SIMD
 #endif
 #ifndef HBEC_ODD_BPC_APPLY
 #define HBEC_ODD_BPC_APPLY 1  // blocks per CU of the strided / plan apply grids (register-bound shapes: odd_two_blocks)
@@ -123,6 +120,7 @@
 #ifndef HBEC_MD5_DEPTH_LIST
 #define HBEC_MD5_DEPTH_LIST 2
 #endif
-#ifndef HBEC_MD5_PRIO
-#define HBEC_MD5_PRIO 0  // s_setprio of the chain waves beside a co-resident encode
+// (s_setprio 3 on the chain waves beside the encode: encode + ShardHash 3.14 -> 3.39 ms, profiles/r04_md5_pipe.jsonl)
+#ifndef HBEC_MD5_BLOCK
+#define HBEC_MD5_BLOCK 64  // chains (lanes) per block: one wave
 #endif
