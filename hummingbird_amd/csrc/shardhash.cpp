@@ -106,45 +106,6 @@ int side_stream_get(int dev, hipStream_t* s) {
     return HBEC_OK;
 }
 
-// CU-partitioned pipeline (tuning builds, HBEC_MD5_CUMASK = n > 0): the MD5
-// chains on a stream masked to n CUs, the encode segments on a stream masked
-// to the others, so no chain wave shares a SIMD with an encode wave.
-// HBEC_MD5_CUMAP: 0 = the n lowest CU ids, 1 = ids spread evenly.
-struct MaskedPair {
-    hipStream_t md5 = nullptr, enc = nullptr;
-    int enc_cus = 0;
-};
-std::map<int, MaskedPair> g_masked;
-
-int masked_pair(int dev, int n_md5, MaskedPair* out) {
-    std::lock_guard<std::mutex> g(g_side_mu);
-    auto it = g_masked.find(dev);
-    if (it != g_masked.end()) {
-        *out = it->second;
-        return HBEC_OK;
-    }
-    int cus = 0;
-    hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (e != hipSuccess) return hip_fail(e, "hipDeviceGetAttribute");
-    n_md5 = std::min(n_md5, cus - 1);
-    const int map = (int)tune_knob("HBEC_MD5_CUMAP", 0);
-    std::vector<uint32_t> m5((size_t)(cus + 31) / 32, 0u), me(m5.size(), 0u);
-    int taken = 0;
-    for (int i = 0; i < cus; ++i) {
-        const bool md5 = map == 0 ? i < n_md5 : ((long long)(i + 1) * n_md5 / cus) != ((long long)i * n_md5 / cus);
-        if (md5) ++taken;
-        (md5 ? m5 : me)[(size_t)i / 32] |= 1u << (i % 32);
-    }
-    MaskedPair p;
-    p.enc_cus = cus - taken;
-    e = hipExtStreamCreateWithCUMask(&p.md5, (uint32_t)m5.size(), m5.data());
-    if (e == hipSuccess) e = hipExtStreamCreateWithCUMask(&p.enc, (uint32_t)me.size(), me.data());
-    if (e != hipSuccess) return hip_fail(e, "hipExtStreamCreateWithCUMask");
-    g_masked[dev] = p;
-    *out = p;
-    return HBEC_OK;
-}
-
 void side_stream_put(int dev, hipStream_t s) {
     std::lock_guard<std::mutex> g(g_side_mu);
     g_side_free.emplace_back(dev, s);
@@ -587,17 +548,8 @@ int hbec_encode_md5_batch(hbec_codec* codec, const hbec_view* views, uint64_t n_
         void* state = nullptr;
         e = hipMallocFromPoolAsync(&state, (size_t)n * n_objects * md5_state_bytes(), pool, main);
         if (e != hipSuccess) return hip_fail(e, "hipMallocFromPoolAsync");
-        hipStream_t side, enc_stream = main;
-        static const int cumask = (int)tune_knob("HBEC_MD5_CUMASK", 0);
-        MaskedPair mp;
-        if (cumask > 0) {
-            rc = masked_pair(dev, cumask, &mp);
-            side = mp.md5;
-            enc_stream = mp.enc;
-            if (!rc) rc = order_after(enc_stream, main);  // inputs ready, state allocated
-        } else {
-            rc = side_stream_get(dev, &side);
-        }
+        hipStream_t side;
+        rc = side_stream_get(dev, &side);
         if (rc) {
             hipFreeAsync(state, main);
             return rc;
@@ -609,20 +561,19 @@ int hbec_encode_md5_batch(hbec_codec* codec, const hbec_view* views, uint64_t n_
             const uint64_t want = (off == 0 && head > 0) ? std::min(head, seg) : seg;
             const uint64_t len = std::min(want, shard_len - off);
             for (int i = 0; i < n; ++i) sv[i] = hbec_view{static_cast<uint8_t*>(views[i].base) + off, views[i].obj_stride};
-            set_thread_grid_cap(cumask > 0 ? mp.enc_cus : (off > 0 ? enc_grid : 0));
-            rc = hbec_encode_batch(codec, sv.data(), n_objects, len, enc_stream);
+            set_thread_grid_cap(off > 0 ? enc_grid : 0);
+            rc = hbec_encode_batch(codec, sv.data(), n_objects, len, hip_stream);
             set_thread_grid_cap(0);
             if (rc) break;
-            rc = order_after(side, enc_stream);  // segment encoded (and, first time, state allocated)
+            rc = order_after(side, main);  // segment encoded (and, first time, state allocated)
             if (rc) break;
             const uint32_t flags = (off == 0 ? kInit : 0u) | (off + len == shard_len ? kFinal : 0u);
             rc = md5_step(sv.data(), n, n_objects, len, off, flags, state, d_digests, side);
             off += len;
         }
-        int rc2 = order_after(main, side);  // caller's stream: digests ready
-        if (cumask > 0 && !rc2) rc2 = order_after(main, enc_stream);
+        const int rc2 = order_after(main, side);  // caller's stream: digests ready
         hipFreeAsync(state, main);
-        if (cumask <= 0) side_stream_put(dev, side);
+        side_stream_put(dev, side);
         return rc ? rc : rc2;
     });
 }

@@ -122,5 +122,5 @@
 #endif
 // (s_setprio 3 on the chain waves beside the encode: encode + ShardHash 3.14 -> 3.39 ms, profiles/r04_md5_pipe.jsonl)
 #ifndef HBEC_MD5_BLOCK
-#define HBEC_MD5_BLOCK 64  // chains (lanes) per block: one wave
+#define HBEC_MD5_BLOCK 64  // chains (lanes) per block: one wave (4-wave blocks: ShardHash alone 2.55 -> 3.45 ms, r04_md5_pipe.jsonl)
 #endif
