@@ -52,17 +52,13 @@ __host__ __device__ constexpr int odd_u(int k, int = kOddApply) {
 }
 constexpr int kOddPlanU = HBEC_ODD_PLAN_U;  // plans: windows per record (tuning.h)
 
-// Record kernels (gf_odd_rec): the windows of a wave tile are contiguous
-// columns, and each window but the last takes its lane 63's missing next
-// dword from the following window's lane 0.  Apply / accumulate (U == 2):
-// window 0 stores 64 blocks, window 1 62 (its outputs are realigned, which
-// needs lane l+1's column).  Verify (any U >= 2): windows
-// 0..U-2 compare 64 columns, the last 63, so a tile of 64 U loaded blocks
-// compares 64 U - 1 and neighbouring tiles share one column instead of one
-// per window (odd Verify read 1.067 x its bytes with 63-column windows).
-__host__ __device__ constexpr bool odd_rec_carry(int u, int mode) {
-    return mode == kOddVerify ? u >= 2 : u == 2;
-}
+// Record kernels (gf_odd_rec), apply / accumulate with 2 windows per wave
+// tile (K <= 4, plans): the carry of gf_odd, window 0 stores 64 blocks,
+// window 1 62.  (A chained Verify of the same kind, 64 U - 1 columns per
+// tile, read less but ran slower than gf_odd's 63-column windows at 4+2:
+// 74.5 vs 76.6 %, profiles/r04_ab_odd.jsonl batch F; Verify records are used
+// from K R >= 24, one window per tile.)
+__host__ __device__ constexpr bool odd_rec_carry(int u, int mode) { return mode != kOddVerify && u == 2; }
 // Strided batches code from object records (gf_odd_rec) when they carry at
 // least 24 products per column (K R >= 24: 8+3, 10+4, 12+4 encode, 8+3
 // Verify), gf_odd below: the per-tile base arithmetic the records remove only
@@ -72,8 +68,7 @@ __host__ __device__ constexpr bool odd_rec_carry(int u, int mode) {
 __host__ __device__ constexpr bool odd_use_rec(int k, int r) { return k * r >= HBEC_ODD_REC_MINKR; }
 // shard bytes per wave tile of the record kernel
 __host__ __device__ constexpr uint32_t odd_rec_span(int u, int mode) {
-    return odd_rec_carry(u, mode) ? (mode == kOddVerify ? (64u * (uint32_t)u - 1u) * 16u : (64u + kOddStore) * 16u)
-                                  : (uint32_t)u * (mode == kOddVerify ? 63u : kOddStore) * 16u;
+    return odd_rec_carry(u, mode) ? (64u + kOddStore) * 16u : (uint32_t)u * (mode == kOddVerify ? 63u : kOddStore) * 16u;
 }
 
 // One tile, wave-uniform.  Positions are 32-bit: the host sends shards of
@@ -721,38 +716,8 @@ __device__ __forceinline__ void odd_rec_finish(const OddRegs<K, R, U, MODE>& X, 
     auto q_addr = [&](int r, uint32_t v) {
         return ((uint64_t)odd_w(t.f, 4 + 4 * r) | ((uint64_t)odd_w(t.f, 5 + 4 * r) << 32)) + v;
     };
-    if constexpr (CARRY && MODE == kOddVerify) {
-        // chained windows: window u < U-1 compares all 64 columns (lane 63
-        // borrows window u+1's first dword), the last window 63
-        bool bad = false;
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t v = t.v0 + 16u * 64u * (uint32_t)u + 16u * lane;
-            u32x4 x[K];
-#pragma unroll
-            for (int j = 0; j < K; ++j)
-                x[j] = u + 1 < U ? odd_shift_in_fill(X.x[u][j], sh[j], lane0(X.x[u + 1 < U ? u + 1 : u][j]))
-                                 : odd_shift_in(X.x[u][j], sh[j]);
-            u32x4 acc[R];
-#pragma unroll
-            for (int r = 0; r < R; ++r) acc[r] = u32x4{0, 0, 0, 0};
-            gf_dot<K, R, kOddVMin>(acc, x, tab, tb);
-            odd_rec_pin<K, R, MODE>(acc);
-            const bool mine = t.live != 0u && (u + 1 < U || lane < 63u) && (v - odd_w(t.f, 2)) <= odd_w(t.f, 3);
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const u32x4 st = u + 1 < U ? odd_shift_in_fill(X.x[u][K + r], sh[K + r], lane0(X.x[u + 1 < U ? u + 1 : u][K + r]))
-                                           : odd_shift_in(X.x[u][K + r], sh[K + r]);
-                const u32x4 df = st ^ acc[r];
-                bad |= mine && (df[0] | df[1] | df[2] | df[3]) != 0u;
-            }
-        }
-        if (__any(bad)) {
-            if (lane == 0u) atomicOr(flags + t.obj, 1u);
-        }
-        return;
-    } else if constexpr (CARRY) {
-        static_assert(U == 2, "apply carry: 2 windows");
+    if constexpr (CARRY) {
+        static_assert(U == 2 && MODE != kOddVerify, "apply carry: 2 windows");
         u32x4 x1[K], x0[K], acc1[R], acc0[R];
 #pragma unroll
         for (int j = 0; j < K; ++j) {
