@@ -169,7 +169,9 @@ static int odd_launches(const PassArgs& a, int K, int R, int mode, bool accumula
                     for (int q = 0; q < 5; ++q) b.tab[r][j][q] = a.tab[r][c1 + j][q];
             }
             const int m = mode == 2 ? 2 : ((accumulate || c1 > 0) ? 1 : 0);
-            const bool use_rec = odd_uses_records(K1, R);
+            // Verify stays on gf_odd: the record kernel's 8+3 Verify ran at the
+            // same speed and read 1.11 x its bytes (gf_odd 1.02 x; r04_pmc.json)
+            const bool use_rec = m != 2 && odd_uses_records(K1, R);
             const uint64_t tpo = odd_tiles_per_obj(K1, m, shard_len, use_rec);
             const uint64_t max_obj = std::max<uint64_t>(1, std::min<uint64_t>((1ull << 31), g_chunk_tiles) / tpo);
             // per-object records of this pass (stream-ordered scratch, freed after its launches)
