@@ -170,7 +170,7 @@ static int odd_launches(const PassArgs& a, int K, int R, int mode, bool accumula
             }
             const int m = mode == 2 ? 2 : ((accumulate || c1 > 0) ? 1 : 0);
             // Verify stays on gf_odd: the record kernel's 8+3 Verify ran at the
-            // same speed and read 1.11 x its bytes (gf_odd 1.02 x; r04_pmc.json)
+            // same speed with the same traffic (1.11 vs 1.10 x, bench.py's leg)
             const bool use_rec = m != 2 && odd_uses_records(K1, R);
             const uint64_t tpo = odd_tiles_per_obj(K1, m, shard_len, use_rec);
             const uint64_t max_obj = std::max<uint64_t>(1, std::min<uint64_t>((1ull << 31), g_chunk_tiles) / tpo);
