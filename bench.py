@@ -466,8 +466,6 @@ def odd_leg(k, m, n, obj_len, first, reps=20, settle=40, pmc=None):
     if pmc is not None:
         kern = pmc.get("kernels", {})
         for name, (r, mode) in (("encode", (m, 0)), ("reconstruct", (2, 0)), ("verify", (m, 2))):
-            if name == "verify" and k > 8:
-                continue  # k > 8 Verify is gf_wide
             kname, t = _odd_kernel_traffic(kern, k, r, mode)
             te = kern.get("gf_odd_edges<2>" if name == "verify" else "gf_odd_edges<0>", {}).get("hbm_bytes_per_launch")
             if t is not None:

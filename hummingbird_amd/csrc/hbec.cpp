@@ -169,9 +169,10 @@ static int odd_launches(const PassArgs& a, int K, int R, int mode, bool accumula
                     for (int q = 0; q < 5; ++q) b.tab[r][j][q] = a.tab[r][c1 + j][q];
             }
             const int m = mode == 2 ? 2 : ((accumulate || c1 > 0) ? 1 : 0);
-            // Verify stays on gf_odd: the record kernel's 8+3 Verify ran at the
-            // same speed with the same traffic (1.11 vs 1.10 x, bench.py's leg)
-            const bool use_rec = m != 2 && odd_uses_records(K1, R);
+            // Verify with register tables (K <= 8) stays on gf_odd: the record
+            // kernel's 8+3 Verify ran at the same speed with the same traffic
+            // (1.11 vs 1.10 x, bench.py's leg); K > 8 needs its LDS tables
+            const bool use_rec = (m != 2 || K1 > 8) && odd_uses_records(K1, R);
             const uint64_t tpo = odd_tiles_per_obj(K1, m, shard_len, use_rec);
             const uint64_t max_obj = std::max<uint64_t>(1, std::min<uint64_t>((1ull << 31), g_chunk_tiles) / tpo);
             // per-object records of this pass (stream-ordered scratch, freed after its launches)
@@ -1128,8 +1129,10 @@ static int verify_views(hbec_codec* c, const hbec_view* views, uint64_t n_obj, u
         }
         return HBEC_OK;
     }
-    // k <= 8: gf_odd verify; above, gf_verify_wide (10+4 53 vs 55 %, 12+4 41 vs 54 %, r3b7)
-    if (odd_enabled() && k <= 8 && pos32_shard(shard_len)) {
+    // k <= 12: gf_odd verify (9 <= k <= 12: the record kernel with LDS tables,
+    // 10+4 54.1 -> 64.5 %, 12+4 45.7 -> 53.6 % over gf_verify_wide,
+    // profiles/r04_ab_odd.jsonl batch N); above, gf_verify_wide
+    if (odd_enabled() && k <= kOddMaxK && pos32_shard(shard_len)) {
         // any alignment: recompute and compare in one pass (gf_odd verify), <= 4 rows per launch
         int dev = 0;
         int rc = current_device(&dev);

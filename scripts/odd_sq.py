@@ -80,7 +80,7 @@ def main():
         k, m, s, op = {"a42": (4, 2, MiB // 4, "enc"), "o42": (4, 2, 262143, "enc"), "v42": (4, 2, 262143, "ver"), "r42": (4, 2, 262143, "rec"), "a83": (8, 3, MiB // 8, "enc"),
                        "o83": (8, 3, 131071, "enc"), "r83": (8, 3, 131071, "rec"), "v83": (8, 3, 131071, "ver"),
                        "o104": (10, 4, 104858, "enc"), "o124": (12, 4, 87389, "enc"), "r104": (10, 4, 104858, "rec"), "p124": (12, 4, 87392, "plan"), "p42": (4, 2, 262143, "plan"), "p83": (8, 3, 131071, "plan"), "p104": (10, 4, 104858, "plan"),
-                       "v328": (32, 8, 32771, "ver")}[name]
+                       "v328": (32, 8, 32771, "ver"), "v104": (10, 4, 104858, "ver"), "v124": (12, 4, 87389, "ver")}[name]
         enc = RS.New(k, m)
         row = {"lib": os.environ.get("HBEC_LIB", "default"), "label": os.environ.get("AB_LABEL", ""), "round": int(os.environ.get("AB_ROUND", "0")),
                "shape": name, "k": k, "m": m, "S": s, "n": n, "op": op}

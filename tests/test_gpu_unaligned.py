@@ -258,17 +258,22 @@ def test_host_pinned_odd_stripes_zero_copy(k, m):
     hb.free()
 
 
-@pytest.mark.parametrize("k,m,s,off", [(4, 2, 1001, 3), (8, 3, 131071, 0), (6, 3, 17, 5), (10, 4, 104858, 1),
-                                       (16, 6, 2015, 9), (17, 3, 333, 2), (3, 2, 1, 15),
-                                       # gf_verify_wide (k > 8, k > 16 included)
-                                       (20, 4, 52429, 3), (32, 8, 32768, 0), (32, 8, 4097, 7), (20, 4, 31, 1),
-                                       (12, 9, 1000, 2), (9, 1, 48, 0), (64, 4, 16387, 5)])
-def test_unaligned_verify_flags_exactly(k, m, s, off):
-    """Encoder.Verify over unaligned views (gf_odd verify for k <= 8,
-    gf_verify_wide above: one read-only pass for any k): clean codewords
-    from the oracle are not flagged; a flipped first / last / middle byte of
-    a parity shard, or of a data shard, flags exactly that object."""
-    n = 12
+@pytest.mark.parametrize("k,m,s,off,n", [(4, 2, 1001, 3, 12), (8, 3, 131071, 0, 12), (6, 3, 17, 5, 12),
+                                         (10, 4, 104858, 1, 12), (16, 6, 2015, 9, 12), (17, 3, 333, 2, 12),
+                                         (3, 2, 1, 15, 12),
+                                         # gf_verify_wide (k > 12)
+                                         (20, 4, 52429, 3, 12), (32, 8, 32768, 0, 12), (32, 8, 4097, 7, 12),
+                                         (20, 4, 31, 1, 12), (12, 9, 1000, 2, 12), (9, 1, 48, 0, 12),
+                                         (64, 4, 16387, 5, 12),
+                                         # record kernel with LDS tables, several tiles per wave
+                                         (10, 4, 104858, 7, 160), (12, 4, 87389, 2, 160), (11, 3, 95325, 9, 96),
+                                         (9, 2, 116509, 0, 96)])
+def test_unaligned_verify_flags_exactly(k, m, s, off, n):
+    """Encoder.Verify over unaligned views (gf_odd verify for k <= 8, the
+    record kernel for 9 <= k <= 12, gf_verify_wide above: one read-only pass
+    for any k): clean codewords from the oracle are not flagged; a flipped
+    first / last / middle byte of a parity shard, or of a data shard, flags
+    exactly that object."""
     rng = np.random.default_rng(k * 1000 + s)
     row = (k + m) * s + 5
     buf = rng.integers(0, 256, off + n * row + 16, dtype=np.uint8)
