@@ -92,10 +92,10 @@ struct URec;
 // passes accumulate).  sel_k > 0: object records (indices >= sel_k are
 // parity, base b).  max_blocks > 0 caps the grid (zero-copy over PCIe).
 // erecs: gf_odd's one edge record per stripe (guard-band bytes; none for the round-2 kernels).
-// orecs: one record per stripe longer than odd_min_main() (shortest s_min,
-// longest s_max bytes): unmirrored passes then code from per-stripe records
-// (gf_odd_rec, every stripe given the longest one's tile count) when that
-// wastes few tiles, instead of recs.
+// orecs: n_orec_cls classes of per-stripe records (stripes longer than
+// odd_min_main(), shortest s_min, longest s_max bytes per class): unmirrored
+// passes code from them (gf_odd_rec, one launch per class, every stripe given
+// its class's longest tile count) when that wastes few tiles, instead of recs.
 struct OddStripeRecs {
     const URec* recs = nullptr;
     uint64_t n = 0, s_min = 0, s_max = 0;
@@ -104,6 +104,6 @@ int launch_unaligned_passes(const URec* recs, uint64_t n_recs, const std::vector
                             const std::vector<int>& out_idx, const std::vector<uint8_t>& rows, int sel_k,
                             hipStream_t stream, int max_blocks = 0, const URec* erecs = nullptr,
                             uint64_t n_erecs = 0, bool mirror = false, bool round2 = false,
-                            const OddStripeRecs* orecs = nullptr);
+                            const OddStripeRecs* orecs = nullptr, int n_orec_cls = 0);
 
 }  // namespace hbec

@@ -46,8 +46,9 @@ struct hbec_plan {
     hbec::URec* d_brecs = nullptr;
     uint64_t n_brecs = 0;
     // gf_odd_rec: one record per stripe / object with a main-kernel part
+    // classes of near-equal tile counts, one gf_odd_rec launch per class and pass
     hbec::URec* d_orecs = nullptr;
-    hbec::OddStripeRecs orecs;
+    std::vector<hbec::OddStripeRecs> orec_cls;
 };
 
 namespace {
@@ -78,14 +79,44 @@ void add_urecs(std::vector<hbec::URec>& recs, std::vector<hbec::URec>& erecs, st
     if (span > 0) orecs.push_back({ua, ub, s, 0});
 }
 
-void set_orecs(hbec_plan* p, const std::vector<hbec::URec>& orecs) {
-    p->orecs.recs = p->d_orecs;
-    p->orecs.n = orecs.size();
-    p->orecs.s_min = p->orecs.s_max = 0;
-    for (size_t i = 0; i < orecs.size(); ++i) {
-        const uint64_t s = orecs[i].shard_len;
-        p->orecs.s_min = i ? std::min(p->orecs.s_min, s) : s;
-        p->orecs.s_max = std::max(p->orecs.s_max, s);
+// Per-stripe record classes: the stripes sorted by length and cut into runs
+// whose tile counts (992-B windows) stay within 1/32 of the run's shortest;
+// more than kOddRecClasses runs: no record path (orecs cleared).
+#ifndef HBEC_ODD_REC_CLASSES
+#define HBEC_ODD_REC_CLASSES 8
+#endif
+constexpr size_t kOddRecClasses = HBEC_ODD_REC_CLASSES;
+
+uint64_t rec_tiles(uint64_t s) { return (s + 32u + 991u) / 992u; }
+
+std::vector<std::pair<size_t, size_t>> group_orecs(std::vector<hbec::URec>& orecs) {
+    std::stable_sort(orecs.begin(), orecs.end(),
+                     [](const hbec::URec& x, const hbec::URec& y) { return x.shard_len < y.shard_len; });
+    std::vector<std::pair<size_t, size_t>> cls;
+    for (size_t i = 0; i < orecs.size();) {
+        const uint64_t t0 = rec_tiles(orecs[i].shard_len);
+        size_t j = i + 1;
+        while (j < orecs.size() && rec_tiles(orecs[j].shard_len) * 32 <= t0 * 33) ++j;
+        cls.emplace_back(i, j - i);
+        i = j;
+        if (cls.size() > kOddRecClasses) {
+            orecs.clear();
+            cls.clear();
+            break;
+        }
+    }
+    return cls;
+}
+
+void set_orecs(hbec_plan* p, const std::vector<hbec::URec>& orecs, const std::vector<std::pair<size_t, size_t>>& cls) {
+    p->orec_cls.clear();
+    for (const auto& c : cls) {
+        hbec::OddStripeRecs o;
+        o.recs = p->d_orecs + c.first;
+        o.n = c.second;
+        o.s_min = orecs[c.first].shard_len;
+        o.s_max = orecs[c.first + c.second - 1].shard_len;
+        p->orec_cls.push_back(o);
     }
 }
 
@@ -142,7 +173,7 @@ int odd_stripe_rec_pass(int K, int R, int mode, const hbec::UPlanArgs& a, const 
 int hbec::launch_unaligned_passes(const URec* recs, uint64_t n_recs, const std::vector<int>& in_idx,
                                   const std::vector<int>& out_idx, const std::vector<uint8_t>& rows, int sel_k,
                                   hipStream_t stream, int max_blocks, const URec* erecs, uint64_t n_erecs,
-                                  bool mirror, bool round2, const OddStripeRecs* orecs) {
+                                  bool mirror, bool round2, const OddStripeRecs* orecs, int n_orec_cls) {
     const int K_all = (int)in_idx.size(), R_all = (int)out_idx.size();
     if ((n_recs == 0 && n_erecs == 0) || R_all == 0) return HBEC_OK;
     if (mirror && (!hbec::odd_enabled() || sel_k > 0 || round2))
@@ -153,17 +184,18 @@ int hbec::launch_unaligned_passes(const URec* recs, uint64_t n_recs, const std::
     e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (e != hipSuccess) return hip_fail(e, "hipDeviceGetAttribute");
     if (hbec::odd_enabled() && !round2) {
-        // per-stripe records when every stripe's tile count is within 1/32 of
-        // the longest one's (the shorter stripes' extra tiles store nothing)
-        bool use_orecs = false;
-        if (orecs && orecs->n > 0 && !mirror) {
-            use_orecs = true;
+        // per-stripe records, one launch per class of stripes whose tile
+        // counts are within 1/32 of the class's longest (the shorter stripes'
+        // extra tiles store nothing), when every class passes for every pass
+        bool use_orecs = orecs && n_orec_cls > 0 && !mirror;
+        for (int c = 0; c < n_orec_cls && use_orecs; ++c) {
+            const OddStripeRecs& o = orecs[c];
             for (int c0 = 0; c0 < K_all && use_orecs; c0 += hbec::kOddMaxK) {
                 const int K = std::min(hbec::kOddMaxK, K_all - c0), mode = c0 > 0 ? 1 : 0;
                 if (K * std::min(hbec::kMaxR, R_all) < HBEC_ODD_PLAN_REC_MINKR) use_orecs = false;
-                const uint64_t t_max = hbec::odd_tiles_per_obj(K, mode, orecs->s_max, true);
-                const uint64_t t_min = hbec::odd_tiles_per_obj(K, mode, orecs->s_min, true);
-                use_orecs = use_orecs && t_max * 32 <= t_min * 33 && orecs->n * t_max < (1ull << 31);
+                const uint64_t t_max = hbec::odd_tiles_per_obj(K, mode, o.s_max, true);
+                const uint64_t t_min = hbec::odd_tiles_per_obj(K, mode, o.s_min, true);
+                use_orecs = use_orecs && t_max * 32 <= t_min * 33 && o.n * t_max < (1ull << 31);
             }
         }
         // gf_odd_plan: launches of <= 4 outputs x <= kOddMaxK inputs, later input
@@ -208,8 +240,10 @@ int hbec::launch_unaligned_passes(const URec* recs, uint64_t n_recs, const std::
                 const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, cap));
                 const int mode = c0 > 0 ? 1 : 0;
                 if (use_orecs) {
-                    int rc = odd_stripe_rec_pass(K, R, mode, a, *orecs, cus, max_blocks, stream);
-                    if (rc) return rc;
+                    for (int c = 0; c < n_orec_cls; ++c) {
+                        int rc = odd_stripe_rec_pass(K, R, mode, a, orecs[c], cus, max_blocks, stream);
+                        if (rc) return rc;
+                    }
                 } else if (n_recs > 0) {
                     e = hbec::launch_odd_plan(K, R, mode, a, grid, stream);
                     if (e != hipSuccess) return hip_fail(e, "launch gf_odd_plan");
@@ -384,7 +418,8 @@ int run_plan(const hbec_plan* p, const std::vector<int>& in_idx, const std::vect
     // with k > 8 every object is in the unaligned records (hbec_plan_objects)
     const int sel_k = p->objects ? p->k : 0;
     int rc = hbec::launch_unaligned_passes(p->d_urecs, p->n_urecs, in_idx, out_idx, rows, sel_k, stream, 0,
-                                           p->d_erecs, p->n_erecs, false, false, &p->orecs);
+                                           p->d_erecs, p->n_erecs, false, false, p->orec_cls.data(),
+                                           (int)p->orec_cls.size());
     if (rc || p->n_brecs == 0) return rc;
     return hbec::launch_unaligned_passes(p->d_brecs, p->n_brecs, in_idx, out_idx, rows, sel_k, stream, 0, nullptr, 0,
                                          false, true);
@@ -444,6 +479,7 @@ int hbec_plan_stripes(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n,
         int urc = upload(urecs, &p->d_urecs, "plan unaligned records");
         if (!urc) urc = upload(erecs, &p->d_erecs, "plan edge records");
         if (!urc) urc = upload(brecs, &p->d_brecs, "plan large-shard records");
+        const auto cls = group_orecs(orecs);
         if (!urc) urc = upload(orecs, &p->d_orecs, "plan stripe records");
         if (urc) {
             if (p->d_tiles) (void)hipFree(p->d_tiles);
@@ -452,7 +488,7 @@ int hbec_plan_stripes(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n,
             if (p->d_brecs) (void)hipFree(p->d_brecs);
             return urc;
         }
-        set_orecs(p.get(), orecs);
+        set_orecs(p.get(), orecs, cls);
         p->n_urecs = urecs.size();
         p->n_erecs = erecs.size();
         p->n_brecs = brecs.size();
@@ -519,6 +555,7 @@ int hbec_plan_objects(hbec_codec* codec, const hbec_object* objects, uint64_t n,
         int urc = upload(urecs, &p->d_urecs, "plan unaligned records");
         if (!urc) urc = upload(erecs, &p->d_erecs, "plan edge records");
         if (!urc) urc = upload(brecs, &p->d_brecs, "plan large-shard records");
+        const auto cls = group_orecs(orecs);
         if (!urc) urc = upload(orecs, &p->d_orecs, "plan stripe records");
         if (urc) {
             if (p->d_tiles) (void)hipFree(p->d_tiles);
@@ -527,7 +564,7 @@ int hbec_plan_objects(hbec_codec* codec, const hbec_object* objects, uint64_t n,
             if (p->d_brecs) (void)hipFree(p->d_brecs);
             return urc;
         }
-        set_orecs(p.get(), orecs);
+        set_orecs(p.get(), orecs, cls);
         p->n_urecs = urecs.size();
         p->n_erecs = erecs.size();
         p->n_brecs = brecs.size();

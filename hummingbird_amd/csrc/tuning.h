@@ -98,7 +98,7 @@
 #define HBEC_ODD_PLAN_U 2  // windows per plan record: odd 4+2 stripe plan 52.9 -> 59.5 % (r03b4)
 #endif
 #ifndef HBEC_ODD_REC_MINKR
-#define HBEC_ODD_REC_MINKR 24  // strided batches: object records (gf_odd_rec) from K R >= 24 (r04_ab_odd)
+#define HBEC_ODD_REC_MINKR 18  // strided batches: object records (gf_odd_rec) from K R >= 18, R >= 3 above K = 8 (r04_ab_odd F, G, Q2)
 #endif
 #ifndef HBEC_ODD_LDS_MINK
 #define HBEC_ODD_LDS_MINK 9  // record kernels: coefficient tables in LDS from K = 9 (12+4 encode 51 -> 57 %; from K = 5, 8+3 lost 5 %)

@@ -80,11 +80,37 @@ def main():
         k, m, s, op = {"a42": (4, 2, MiB // 4, "enc"), "o42": (4, 2, 262143, "enc"), "v42": (4, 2, 262143, "ver"), "r42": (4, 2, 262143, "rec"), "a83": (8, 3, MiB // 8, "enc"),
                        "o83": (8, 3, 131071, "enc"), "r83": (8, 3, 131071, "rec"), "v83": (8, 3, 131071, "ver"),
                        "o104": (10, 4, 104858, "enc"), "o124": (12, 4, 87389, "enc"), "r104": (10, 4, 104858, "rec"), "p124": (12, 4, 87392, "plan"), "p42": (4, 2, 262143, "plan"), "p83": (8, 3, 131071, "plan"), "p104": (10, 4, 104858, "plan"),
-                       "v328": (32, 8, 32771, "ver"), "v104": (10, 4, 104858, "ver"), "v124": (12, 4, 87389, "ver")}[name]
+                       "v328": (32, 8, 32771, "ver"), "v104": (10, 4, 104858, "ver"), "v124": (12, 4, 87389, "ver"),
+                       "o63": (6, 3, 174763, "enc"), "o73": (7, 3, 149797, "enc"), "o62": (6, 2, 174763, "enc"), "c42": (4, 2, 262143, "cplan"), "c83": (8, 3, 131071, "cplan"), "c104": (10, 4, 104858, "cplan")}[name]
         enc = RS.New(k, m)
         row = {"lib": os.environ.get("HBEC_LIB", "default"), "label": os.environ.get("AB_LABEL", ""), "round": int(os.environ.get("AB_ROUND", "0")),
                "shape": name, "k": k, "m": m, "S": s, "n": n, "op": op}
-        if op == "plan":
+        if op == "cplan":
+            # object plan of two size classes, alternating: ~4 KiB and ~1 MiB objects, odd S
+            sizes = [s if i % 2 else max(17, s // 256 + 7) for i in range(n)]
+            d = torch.empty(sum(k * x for x in sizes), dtype=torch.uint8, device="cuda")
+            B.fill_splitmix(d.view(1, -1), d.numel())
+            par = torch.empty(sum(m * x for x in sizes), dtype=torch.uint8, device="cuda")
+            objs, do, po = [], 0, 0
+            for x in sizes:
+                objs.append((d.data_ptr() + do, par.data_ptr() + po, x))
+                do += k * x
+                po += m * x
+            plan = B.StripePlan(enc, objects=objs)
+            ms = timeit(plan.encode)
+            nb = sum((k + m) * x for x in sizes)
+            plan.encode()
+            flags = torch.zeros(1, dtype=torch.int32, device="cuda")
+            ok = True
+            for (a_, b_, x) in objs[:64]:
+                views = [(a_ + j * x, 0) for j in range(k)] + [(b_ + r * x, 0) for r in range(m)]
+                flags.zero_()
+                B.verify_views(enc, views, 1, x, flags)
+                ok = ok and int(flags.item()) == 0
+            torch.cuda.synchronize()
+            row["ok"] = ok
+            del plan, d, par
+        elif op == "plan":
             d = torch.empty((n, k * s), dtype=torch.uint8, device="cuda")
             B.fill_splitmix(d, k * s)
             par = torch.empty((n, m * s), dtype=torch.uint8, device="cuda")

@@ -104,6 +104,7 @@ def test_unaligned_every_offset_pair(off_in, off_out):
                                            (12, 4, 12 * 87389, 160), (11, 4, (1 << 20) - 3, 160),
                                            (9, 4, (1 << 20) + 5, 160), (8, 4, (1 << 20) - 8, 160),
                                            (8, 3, (1 << 20) - 8, 200), (4, 2, (1 << 20) - 4, 200),
+                                           (6, 3, (1 << 20) + 3, 160), (7, 3, (1 << 20) - 5, 120),
                                            (24, 4, (1 << 20) - 7, 96)])
 def test_databuf_odd_shards_encode_reconstruct(k, m, obj_len, n):
     """ecSplit databufs of objects whose size gives S % 16 != 0 (shard i at
@@ -191,6 +192,47 @@ def test_plan_random_odd_stripes(k, m, n, lo, hi):
     plan = B.StripePlan(enc, [(dev.data_ptr() + o, s) for o, s in layout])
     assert plan.info()["n_fallback"] == sum(1 for o, s in layout if (dev.data_ptr() + o) % 16 or s % 16)
     plan.encode()
+    torch.cuda.synchronize()
+    got = dev.cpu().numpy()
+    assert np.array_equal(got, want), np.flatnonzero(got != want)[:8]
+    lost = sorted(rng.choice(k + m, size=m, replace=False).tolist())
+    damaged = torch.from_numpy(want.copy()).cuda()
+    for o, s in layout:
+        for i in lost:
+            damaged[o + i * s:o + (i + 1) * s] = 0xEE
+    B.StripePlan(enc, [(damaged.data_ptr() + o, s) for o, s in layout]).reconstruct(
+        [0 if i in lost else 1 for i in range(k + m)])
+    torch.cuda.synchronize()
+    assert np.array_equal(damaged.cpu().numpy(), want), lost
+
+
+@pytest.mark.parametrize("k,m,clusters", [(4, 2, ((3000, 3100), (300_000, 300_900))),
+                                          (8, 3, ((5000, 5100), (1 << 20, (1 << 20) + 500), (1, 900))),
+                                          (12, 4, ((60_000, 60_400), (600_000, 601_000))),
+                                          (20, 4, ((40_000, 40_500), (400_000, 400_800)))])
+def test_plan_clustered_odd_stripes(k, m, clusters):
+    """Stripe plans whose odd-sized stripes fall into a few size classes
+    (small and large objects, plus a class of tiny stripes that only the edge
+    kernel codes): one per-stripe-record launch per class, stripes of the
+    classes interleaved in the plan.  Encode and Reconstruct against the
+    oracle; bytes between stripes untouched."""
+    rng = np.random.default_rng(k * 7 + m)
+    layout, off = [], 0
+    for i in range(48):
+        lo, hi = clusters[i % len(clusters)]
+        s = -(-int(rng.integers(lo, hi)) // k)
+        off += int(rng.integers(1, 40))
+        layout.append((off, s))
+        off += (k + m) * s
+    pool = rng.integers(0, 256, off + 64, dtype=np.uint8)
+    mat = CO.build_matrix(k, m)[k:]
+    want = pool.copy()
+    for o, s in layout:
+        for r, p in enumerate(CO.apply(mat, [want[o + j * s:o + (j + 1) * s] for j in range(k)])):
+            want[o + (k + r) * s:o + (k + r + 1) * s] = p
+    dev = torch.from_numpy(pool).cuda()
+    enc = RS.New(k, m)
+    B.StripePlan(enc, [(dev.data_ptr() + o, s) for o, s in layout]).encode()
     torch.cuda.synchronize()
     got = dev.cpu().numpy()
     assert np.array_equal(got, want), np.flatnonzero(got != want)[:8]
