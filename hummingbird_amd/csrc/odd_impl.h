@@ -796,15 +796,6 @@ struct OddPos {
     uint32_t obj, ti;
 };
 
-// experiment: register-table apply kernels with 5 <= K <= 8 keep two tiles of
-// loads in flight (HBEC_ODD_REC_DEPTH2)
-#ifndef HBEC_ODD_REC_DEPTH2
-#define HBEC_ODD_REC_DEPTH2 0
-#endif
-__host__ __device__ constexpr bool odd_rec_depth2(int k, int mode) {
-    return HBEC_ODD_REC_DEPTH2 != 0 && mode == kOddApply && k >= 5 && !odd_rec_lds(k);
-}
-
 // LDS-table record kernels fit 2 blocks per CU (2 waves per SIMD)
 template <int K, int R, int MODE>
 __host__ __device__ constexpr int odd_rec_lb() { return odd_rec_two_blocks(K, R, MODE) ? 2 : odd_lb<K, R, MODE>(); }
@@ -892,37 +883,12 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE>())) void
         odd_swait_pin(L);
         odd_swait_pin(tz.f);
     };
-    if constexpr (odd_rec_depth2(K, MODE)) {
-        // two tiles ahead: X and Y loaded before the loop, each step issues
-        // tile p + 2 into Z while X is coded
-        OddRT<K, R, MODE> tz;
-        OddRegs<K, R, U, MODE> Z;
-        fill(ty, p);
-        odd_rec_load<K, R, U, MODE, CARRY>(Y, L, ty.v0, lane);
-        odd_rec_sload<PF>(ty.f, rec(p));
-        p = step(p);
-        odd_rec_sload<PF>(L, rec(p) + RC::FW);
-        odd_swait();
-        odd_swait_pin(L);
-        odd_swait_pin(ty.f);
-        uint32_t b0 = wave0 + 2u * nw;
-        for (; b0 < n; b0 += nw) {  // block-uniform trip count
-            half(Z, tz, X, tx);
-            X = Y;
-            tx = ty;
-            Y = Z;
-            ty = tz;
-        }
-        odd_rec_finish<K, R, U, MODE, CARRY>(X, tx, a.tab, tb, lane, flags, lt);
-        if (b0 - nw < n) odd_rec_finish<K, R, U, MODE, CARRY>(Y, ty, a.tab, tb, lane, flags, lt);
-    } else {
-        for (uint32_t b0 = wave0 + nw; b0 < n; b0 += nw) {  // block-uniform trip count
-            half(Y, ty, X, tx);
-            X = Y;
-            tx = ty;
-        }
-        odd_rec_finish<K, R, U, MODE, CARRY>(X, tx, a.tab, tb, lane, flags, lt);
+    for (uint32_t b0 = wave0 + nw; b0 < n; b0 += nw) {  // block-uniform trip count
+        half(Y, ty, X, tx);
+        X = Y;
+        tx = ty;
     }
+    odd_rec_finish<K, R, U, MODE, CARRY>(X, tx, a.tab, tb, lane, flags, lt);
 }
 
 template <int K, int R, int MODE, bool MIR = false, bool CARRY = false>
