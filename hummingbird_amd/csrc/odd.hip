@@ -322,7 +322,8 @@ uint32_t odd_plan_tile_bytes() { return (uint32_t)kOddPlanU * kOddWin; }
 uint32_t odd_tiles_per_obj(int k, int mode, uint64_t shard_len, bool records) {
     const uint64_t span = shard_len + 32u;
     const uint64_t tile = records ? (uint64_t)odd_rec_span(odd_u(k, mode), mode)
-                          : mode == kOddVerify ? (uint64_t)odd_u(k, mode) * odd_win<kOddVerify>()
+                          : mode == kOddVerify ? (odd_u(k, mode) >= 2 ? (uint64_t)(64u * odd_u(k, mode) - 1u) * 16u
+                                                                      : (uint64_t)odd_win<kOddVerify>())
                                                : (odd_u(k, mode) == 2 ? (uint64_t)(64 + kOddStore) * 16u
                                                                                          : (uint64_t)odd_u(k, mode) * kOddWin);
     return (uint32_t)((span + tile - 1) / tile);

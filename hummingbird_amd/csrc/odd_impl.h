@@ -24,19 +24,27 @@ template <int MODE>
 __host__ __device__ constexpr uint32_t odd_store() { return MODE == kOddVerify ? 63u : kOddStore; }
 template <int MODE>
 __host__ __device__ constexpr uint32_t odd_win() { return odd_store<MODE>() * 16u; }
-// Carry (strided apply with 2 windows per wave tile; odd 4+2 65 -> 70 %,
+// Carry (strided apply with 2 windows per wave tile, Verify below; odd 4+2 65 -> 70 %,
 // r03_tune_carry): the
 // windows are contiguous (columns 0..63 and 64..127 of the tile); window 0
 // gets its lane 63's missing next column from window 1's lane 0 (a readlane
 // + DPP with that value as the out-of-range fill) and stores 64 blocks,
 // window 1 stores 62: 126 of 128 loaded columns instead of 124.
+// Verify tiles of U >= 2 windows are chained the same way: window u < U-1
+// compares all 64 of its columns (lane 63 borrows window u+1's first dword),
+// the last 63, so a tile of 64 U loaded blocks compares 64 U - 1 and the
+// 64-B lines a tile touches are its own (4+2 Verify with 4 chained windows:
+// 1.060 -> 1.024 x its bytes, 80.1 -> 81.3 %; 63-column windows re-read a
+// line at every window boundary; profiles/r04_ab_odd.jsonl batch V).
 template <int U, int MODE>
-__host__ __device__ constexpr bool odd_carry() { return U == 2 && MODE != kOddVerify; }
+__host__ __device__ constexpr bool odd_carry() { return MODE == kOddVerify ? U >= 2 : U == 2; }
 // first column of window u within a tile, and shard bytes per tile
 template <int U, int MODE, bool CARRY>
 __host__ __device__ constexpr uint32_t odd_wcol(int u) { return CARRY ? 64u * (uint32_t)u : odd_store<MODE>() * (uint32_t)u; }
 template <int U, int MODE, bool CARRY>
-__host__ __device__ constexpr uint32_t odd_tile_span() { return CARRY ? (64u + kOddStore) * 16u : U * odd_win<MODE>(); }
+__host__ __device__ constexpr uint32_t odd_tile_span() {
+    return CARRY ? (MODE == kOddVerify ? (64u * U - 1u) * 16u : (64u + kOddStore) * 16u) : U * odd_win<MODE>();
+}
 constexpr int32_t kOddGuard = 48;             // bytes at each end left to gf_odd_edges
 constexpr int32_t kOddEdgeSlots = 160;        // edge bytes handled per (shard, output): 80 head + 80 tail
 // the main kernel runs on shards longer than this (shorter ones: gf_odd_edges only)
@@ -47,8 +55,8 @@ constexpr int kOddVMin = 1;
 
 // windows per wave tile of the strided kernel: ~4 loads per lane in flight
 // for K <= 4 (as gf_apply_vec_pipe2's 1 KiB x 4 / K), one window above
-__host__ __device__ constexpr int odd_u(int k, int = kOddApply) {
-    return k <= 4 ? HBEC_ODD_U_SMALL : (k <= 8 ? HBEC_ODD_U_MID : 1);
+__host__ __device__ constexpr int odd_u(int k, int mode = kOddApply) {
+    return (mode == kOddVerify && k <= 4) ? HBEC_ODD_U_VERIFY : (k <= 4 ? HBEC_ODD_U_SMALL : (k <= 8 ? HBEC_ODD_U_MID : 1));
 }
 constexpr int kOddPlanU = HBEC_ODD_PLAN_U;  // plans: windows per record (tuning.h)
 
@@ -343,7 +351,36 @@ __device__ __forceinline__ void odd_finish(const OddRegs<K, R, U, MODE>& X, cons
     uint32_t dl[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) dl[r] = __builtin_amdgcn_readfirstlane((16u - (((uint32_t)b.out[r] + (uint32_t)b.c) & 15u)) & 15u);
-    if constexpr (CARRY) {
+    if constexpr (CARRY && MODE == kOddVerify) {
+        // chained windows: window u < U-1 compares all 64 columns (lane 63
+        // borrows window u+1's first dword), the last window 63
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int32_t cpos = b.c + 16 * 64 * u + 16 * (int32_t)lane;
+            u32x4 x[K];
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+                x[j] = u + 1 < U ? odd_shift_in_fill(X.x[u][j], sh[j], lane0(X.x[u + 1 < U ? u + 1 : u][j]))
+                                 : odd_shift_in(X.x[u][j], sh[j]);
+            u32x4 acc[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) acc[r] = u32x4{0, 0, 0, 0};
+            gf_dot<K, R, kOddVMin>(acc, x, tab, tb);
+            odd_pin<K, R, MODE, MIR>(acc);
+            const bool mine = b.live != 0u && (u + 1 < U || lane < 63u) && cpos >= kOddGuard && cpos <= hi;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const u32x4 st = u + 1 < U ? odd_shift_in_fill(X.x[u][K + r], sh[K + r], lane0(X.x[u + 1 < U ? u + 1 : u][K + r]))
+                                           : odd_shift_in(X.x[u][K + r], sh[K + r]);
+                const u32x4 df = st ^ acc[r];
+                bad |= mine && (df[0] | df[1] | df[2] | df[3]) != 0u;
+            }
+        }
+        if (__any(bad)) {
+            if (lane == 0u) atomicOr(flags + b.obj, 1u);
+        }
+        return;
+    } else if constexpr (CARRY) {
         static_assert(U == 2 && MODE != kOddVerify && !MIR, "carry: strided apply / accumulate, 2 windows");
         // window 1 first: its lane 0 feeds window 0's lane 63
         u32x4 x1[K], x0[K], acc1[R], acc0[R];

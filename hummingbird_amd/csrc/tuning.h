@@ -94,6 +94,9 @@
 #ifndef HBEC_ODD_U_MID
 #define HBEC_ODD_U_MID 1  // 5 <= K <= 8 (one window above 8); 2 / 3 windows: 8+3 encode 66.8 -> 58.8 / 55.2 % (r04_ab_odd I)
 #endif
+#ifndef HBEC_ODD_U_VERIFY
+#define HBEC_ODD_U_VERIFY 4  // chained Verify windows per tile, K <= 4: 4+2 80.1 -> 81.3 %, traffic 1.060 -> 1.024 x (r04_ab_odd V)
+#endif
 #ifndef HBEC_ODD_PLAN_U
 #define HBEC_ODD_PLAN_U 2  // windows per plan record: odd 4+2 stripe plan 52.9 -> 59.5 % (r03b4)
 #endif
