@@ -12,4 +12,4 @@ cp $OUT/r04_pmc.json profiles/r04_pmc.json
 timeout -k 10 500 python bench.py > $OUT/r4l_bench.json 2> $OUT/r4l_bench.err || exit 1
 tail -c 400 $OUT/r4l_bench.json
 bash scripts/gpu_run.sh prof || exit 1
-bash scripts/r4_sq.sh r4final o42,v42,o83,v83,r83,o104,v104,o124,p42,p124 > gpurun_out/r4final_sq.log 2>&1 || exit 1
+bash scripts/r4_sq.sh r4final o42,v42,o63,o83,v83,r83,o104,v104,o124,p42,p124 > gpurun_out/r4final_sq.log 2>&1 || exit 1

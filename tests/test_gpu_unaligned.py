@@ -307,6 +307,8 @@ def test_host_pinned_odd_stripes_zero_copy(k, m):
                                          (20, 4, 52429, 3, 12), (32, 8, 32768, 0, 12), (32, 8, 4097, 7, 12),
                                          (20, 4, 31, 1, 12), (12, 9, 1000, 2, 12), (9, 1, 48, 0, 12),
                                          (64, 4, 16387, 5, 12),
+                                         # chained 4-window Verify tiles (K <= 4), several tiles per wave
+                                         (4, 2, 262143, 5, 160), (2, 2, 100003, 1, 96), (3, 1, 4081, 11, 200),
                                          # record kernel with LDS tables, several tiles per wave
                                          (10, 4, 104858, 7, 160), (12, 4, 87389, 2, 160), (11, 3, 95325, 9, 96),
                                          (9, 2, 116509, 0, 96)])
