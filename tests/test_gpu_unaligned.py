@@ -311,7 +311,9 @@ def test_host_pinned_odd_stripes_zero_copy(k, m):
                                          (4, 2, 262143, 5, 160), (2, 2, 100003, 1, 96), (3, 1, 4081, 11, 200),
                                          # record kernel with LDS tables, several tiles per wave
                                          (10, 4, 104858, 7, 160), (12, 4, 87389, 2, 160), (11, 3, 95325, 9, 96),
-                                         (9, 2, 116509, 0, 96)])
+                                         (9, 2, 116509, 0, 96),
+                                         # 9 <= k <= 12 with R <= 2: gf_odd's register-table Verify
+                                         (9, 1, 30001, 3, 64), (11, 2, 50001, 4, 64), (12, 1, 7777, 1, 64)])
 def test_unaligned_verify_flags_exactly(k, m, s, off, n):
     """Encoder.Verify over unaligned views (gf_odd verify for k <= 8, the
     record kernel for 9 <= k <= 12, gf_verify_wide above: one read-only pass
