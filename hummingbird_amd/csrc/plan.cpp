@@ -134,15 +134,19 @@ int upload(const std::vector<T>& recs, T** dst, const char* what) {
     return HBEC_OK;
 }
 
-// One pass of a plan over per-stripe records: the records (stream-ordered
-// scratch), then gf_odd_rec with the longest stripe's tile count.
-int odd_stripe_rec_pass(int K, int R, int mode, const hbec::UPlanArgs& a, const hbec::OddStripeRecs& o, int cus,
-                        int max_blocks, hipStream_t stream) {
+// One pass of a plan over per-stripe records: the records of every class in
+// one launch (the classes are consecutive runs of the same record array;
+// stream-ordered scratch), then one gf_odd_rec launch per class with that
+// class's longest tile count.
+int odd_stripe_rec_pass(int K, int R, int mode, const hbec::UPlanArgs& a, const hbec::OddStripeRecs* cls,
+                        int n_cls, int cus, int max_blocks, hipStream_t stream) {
     const uint64_t rw = hbec::odd_rec_words(K, R, mode);
+    uint64_t n_all = 0;
+    for (int c = 0; c < n_cls; ++c) n_all += cls[c].n;
     uint32_t* recs = nullptr;
-    int rc = hbec::scratch_alloc(o.n * rw * 4, stream, reinterpret_cast<void**>(&recs));
+    int rc = hbec::scratch_alloc(n_all * rw * 4, stream, reinterpret_cast<void**>(&recs));
     if (rc) return rc;
-    hipError_t e = hbec::launch_odd_planrec(K, R, mode, a, o.recs, (uint32_t)o.n, recs, stream);
+    hipError_t e = hbec::launch_odd_planrec(K, R, mode, a, cls[0].recs, (uint32_t)n_all, recs, stream);
     if (e != hipSuccess) {
         hbec::scratch_free(recs, stream);
         return hip_fail(e, "launch gf_odd_planrec");
@@ -150,16 +154,21 @@ int odd_stripe_rec_pass(int K, int R, int mode, const hbec::UPlanArgs& a, const 
     hbec::PassArgs c;
     std::memset(&c, 0, sizeof(c));
     std::memcpy(c.tab, a.tab, sizeof(c.tab));
-    const uint64_t tpo = hbec::odd_tiles_per_obj(K, mode, o.s_max, true);
-    c.n_obj = o.n;
-    c.shard_len = o.s_max;
-    c.tiles_per_obj = (uint32_t)tpo;
-    c.n_tiles = (uint32_t)(o.n * tpo);
-    const uint64_t want = (c.n_tiles + 3) / 4;
-    uint64_t cap = (uint64_t)cus * (uint64_t)hbec::odd_blocks_per_cu(mode, K, R, false, true);
-    if (max_blocks > 0) cap = std::min<uint64_t>(cap, (uint64_t)max_blocks);
-    const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, cap));
-    e = hbec::launch_odd(K, R, mode, c, nullptr, recs, grid, stream);
+    uint64_t first = 0;
+    for (int k = 0; k < n_cls && e == hipSuccess; ++k) {
+        const hbec::OddStripeRecs& o = cls[k];
+        const uint64_t tpo = hbec::odd_tiles_per_obj(K, mode, o.s_max, true);
+        c.n_obj = o.n;
+        c.shard_len = o.s_max;
+        c.tiles_per_obj = (uint32_t)tpo;
+        c.n_tiles = (uint32_t)(o.n * tpo);
+        const uint64_t want = (c.n_tiles + 3) / 4;
+        uint64_t cap = (uint64_t)cus * (uint64_t)hbec::odd_blocks_per_cu(mode, K, R, false, true);
+        if (max_blocks > 0) cap = std::min<uint64_t>(cap, (uint64_t)max_blocks);
+        const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, cap));
+        e = hbec::launch_odd(K, R, mode, c, nullptr, recs + first * rw, grid, stream);
+        first += o.n;
+    }
     hbec::scratch_free(recs, stream);
     if (e != hipSuccess) return hip_fail(e, "launch gf_odd_rec (plan)");
     return HBEC_OK;
@@ -240,10 +249,8 @@ int hbec::launch_unaligned_passes(const URec* recs, uint64_t n_recs, const std::
                 const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, cap));
                 const int mode = c0 > 0 ? 1 : 0;
                 if (use_orecs) {
-                    for (int c = 0; c < n_orec_cls; ++c) {
-                        int rc = odd_stripe_rec_pass(K, R, mode, a, orecs[c], cus, max_blocks, stream);
-                        if (rc) return rc;
-                    }
+                    int rc = odd_stripe_rec_pass(K, R, mode, a, orecs, n_orec_cls, cus, max_blocks, stream);
+                    if (rc) return rc;
                 } else if (n_recs > 0) {
                     e = hbec::launch_odd_plan(K, R, mode, a, grid, stream);
                     if (e != hipSuccess) return hip_fail(e, "launch gf_odd_plan");
