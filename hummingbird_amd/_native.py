@@ -107,6 +107,7 @@ _SIG = [
     ("hbec_set_force_stream", C.c_int, [C.c_int]),
     ("hbec_kernel_info", C.c_int,
      [C.c_int, C.c_int, C.c_uint64, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    ("hbec_odd_path_stats", C.c_int, [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     ("hbec_ec_shard_length", C.c_int64, [C.c_int64, C.c_int64]),
     ("hbec_ec_split", C.c_int, [C.c_int, C.c_int, READ_FN, _P, C.c_int, C.c_int64, WRITE_FN, C.POINTER(_P)]),
     ("hbec_ec_reconstruct", C.c_int,
@@ -147,6 +148,10 @@ def lib():
         except OSError as e:  # pragma: no cover - depends on the host
             raise NativeLibraryError(f"cannot load {LIB_PATH}: {e}") from e
         for name, res, args in _SIG:
+            # an explicitly chosen library (HBEC_LIB: an older build in an
+            # interleaved A/B) may lack newer entry points; they raise on use
+            if "HBEC_LIB" in os.environ and not hasattr(h, name):
+                continue
             fn = getattr(h, name)
             fn.restype = res
             fn.argtypes = args

@@ -147,5 +147,13 @@ def kernel_info(k: int, r: int, shard_len: int):
     return {"tile_bytes": tb.value, "kind": KERNEL_KINDS[kind.value], "blocks_per_cu": bpc.value}
 
 
+def odd_path_stats():
+    """Launches since load of the odd-shard main kernels, by family:
+    bit-plane (compiled encode XOR networks), table-multiply records, strided."""
+    b, r, s = C.c_uint64(), C.c_uint64(), C.c_uint64()
+    check(N.lib().hbec_odd_path_stats(C.byref(b), C.byref(r), C.byref(s)))
+    return {"bitplane": b.value, "records": r.value, "strided": s.value}
+
+
 def set_force_stream(on: bool) -> None:
     N.lib().hbec_set_force_stream(1 if on else 0)

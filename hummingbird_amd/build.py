@@ -20,8 +20,8 @@ LIB = PKG / "libhbec.so"
 ROOT = PKG.parent
 INCLUDE = ROOT / "include"
 
-SOURCES = ["odd_k912.hip", "odd_k58.hip", "kernels.hip", "odd.hip", "wide.hip", "stripes.hip", "verify.hip", "md5.hip", "shardhash.cpp", "hbec.cpp", "ecutils.cpp", "plan.cpp", "hostpath.cpp", "batcher.cpp", "coalesce.cpp"]
-HEADERS = ["kernels.h", "gf256.h", "internal.h", "gf_device.h", "pool.h", "odd_impl.h", "tuning.h"]
+SOURCES = ["odd_k912.hip", "odd_k58.hip", "odd_bp.hip", "kernels.hip", "odd.hip", "wide.hip", "stripes.hip", "verify.hip", "md5.hip", "shardhash.cpp", "hbec.cpp", "ecutils.cpp", "plan.cpp", "hostpath.cpp", "batcher.cpp", "coalesce.cpp"]
+HEADERS = ["kernels.h", "gf256.h", "internal.h", "gf_device.h", "pool.h", "odd_impl.h", "tuning.h", "xor_sched.h"]
 ARCH = os.environ.get("HBEC_OFFLOAD_ARCH", "gfx950")
 
 
@@ -81,7 +81,23 @@ def build(force: bool = False, verbose: bool = True, defs=(), lib: Path | None =
         else:
             run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(lib), *map(str, objs),
                  "-lpthread"])
+        check_isa(lib)
     return lib
+
+
+def check_isa(lib: Path) -> None:
+    """Refuse a library whose record kernels touch an SGPR a hand-issued
+    scalar load is still filling (isa_check.py; round 4's 12+4 fault).  The
+    rejected library is moved aside, so nothing loads it."""
+    from hummingbird_amd import isa_check
+
+    n, bad = isa_check.check_library(lib, arch=ARCH)
+    if n == 0 or bad:
+        rej = Path(str(lib) + ".rejected")
+        lib.replace(rej)
+        detail = "; ".join(f"{k}: {v[:2]}" for k, v in list(bad.items())[:4]) or "no record kernels found"
+        raise RuntimeError(f"{lib.name} refused ({len(bad)} of {n} record kernels read scalar-load "
+                           f"destinations before their wait; moved to {rej.name}): {detail}")
 
 
 ASAN_DIR = PKG / "build_asan"

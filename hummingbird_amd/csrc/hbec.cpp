@@ -172,8 +172,10 @@ static int odd_launches(const PassArgs& a, int K, int R, int mode, bool accumula
             // Verify with register tables (K <= 8) stays on gf_odd: the record
             // kernel's 8+3 Verify ran at the same speed with the same traffic
             // (1.11 vs 1.10 x, bench.py's leg); K > 8 needs its LDS tables
-            const bool use_rec = (m != 2 || K1 > 8) && odd_uses_records(K1, R);
-            const uint64_t tpo = odd_tiles_per_obj(K1, m, shard_len, use_rec);
+            // fixed encode matrices of a compiled shape: the bit-plane record kernel
+            const int xs = odd_bp_schedule(K1, R, m, b.tab);
+            const bool use_rec = xs >= 0 || ((m != 2 || K1 > 8) && odd_uses_records(K1, R));
+            const uint64_t tpo = odd_tiles_per_obj(K1, m, shard_len, use_rec, xs);
             const uint64_t max_obj = std::max<uint64_t>(1, std::min<uint64_t>((1ull << 31), g_chunk_tiles) / tpo);
             // per-object records of this pass (stream-ordered scratch, freed after its launches)
             uint32_t* recs = nullptr;
@@ -199,12 +201,13 @@ static int odd_launches(const PassArgs& a, int K, int R, int mode, bool accumula
                 c.shard_len = shard_len;
                 c.tiles_per_obj = (uint32_t)tpo;
                 c.n_tiles = (uint32_t)(no * tpo);
-                const uint64_t want = (c.n_tiles + 3) / 4;
-                const uint64_t cap = (uint64_t)cus * (uint64_t)odd_blocks_per_cu(m, K1, R, false, use_rec);
+                const uint64_t wpb = odd_waves_per_block(xs);
+                const uint64_t want = (c.n_tiles + wpb - 1) / wpb;
+                const uint64_t cap = (uint64_t)cus * (uint64_t)odd_blocks_per_cu(m, K1, R, false, use_rec, xs);
                 int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, cap));
                 if (g_grid_cap > 0) grid = std::min(grid, g_grid_cap);
                 hipError_t e = launch_odd(K1, R, m, c, flags ? flags + o0 : nullptr, recs ? recs + o0 * rw : nullptr, grid,
-                                          stream);
+                                          stream, xs);
                 if (e != hipSuccess) {
                     scratch_free(recs, stream);
                     return hip_fail(e, "launch gf_odd");

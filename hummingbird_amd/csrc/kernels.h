@@ -141,7 +141,7 @@ __host__ __device__ constexpr bool pos32_shard(uint64_t shard_len) { return shar
 bool odd_enabled();
 // 4-wave blocks per CU of a gf_odd launch (mode 0 apply, 1 accumulate, 2
 // verify; K, R of the pass; records: a gf_odd_rec launch)
-int odd_blocks_per_cu(int mode, int k, int r, bool mirror = false, bool records = false);
+int odd_blocks_per_cu(int mode, int k, int r, bool mirror = false, bool records = false, int xs = -1);
 bool odd_supported(int k, int r);
 // Unaligned plan records (URec) of one stripe / object: p0 = 0, tile, 2*tile,
 // ... while p0 < urec_span(S), for whichever kernel family codes them.
@@ -150,7 +150,14 @@ uint64_t urec_tile_for(int k, bool mirror);  // records read by a k-input pass (
 uint64_t urec_span(uint64_t shard_len);  // 0: no main-kernel records (gf_odd: S <= odd_min_main())
 uint32_t odd_tile_bytes(int k);       // shard bytes per wave tile of the strided kernel
 uint32_t odd_plan_tile_bytes();       // shard bytes per plan record
-uint32_t odd_tiles_per_obj(int k, int mode, uint64_t shard_len, bool records);
+// xs >= 0: the bit-plane record kernel of schedule xs (odd_bp_schedule)
+uint32_t odd_tiles_per_obj(int k, int mode, uint64_t shard_len, bool records, int xs = -1);
+// Bit-plane record kernels (xor_sched.h): the schedule whose fixed coefficient
+// matrix equals this pass's tables (the encode parity rows of a compiled
+// (k, m); mode 0 apply only), or -1 for the v_perm table kernels.
+int odd_bp_schedule(int k, int r, int mode, const uint32_t (*tab)[kMaxK][5]);
+// waves per block of a gf_odd / gf_odd_rec launch (xs: odd_bp_schedule)
+uint32_t odd_waves_per_block(int xs);
 // shards of at most this many bytes are coded by gf_odd_edges alone
 uint64_t odd_min_main();
 // Strided passes code from per-object records (gf_odd_rec): launch_odd_objrec
@@ -166,7 +173,7 @@ hipError_t launch_odd_objrec(int k, int r, int mode, const PassArgs& a, uint32_t
 hipError_t launch_odd_planrec(int k, int r, int mode, const UPlanArgs& p, const URec* orecs, uint32_t n,
                               uint32_t* recs, hipStream_t stream);
 hipError_t launch_odd(int k, int r, int mode, const PassArgs& a, uint32_t* flags, const uint32_t* recs, int grid,
-                      hipStream_t stream);
+                      hipStream_t stream, int xs = -1);
 // the guard-band bytes of every shard (after the main launches of a pass;
 // k <= kMaxK inputs, a.n_obj objects; verify flags mismatching objects)
 hipError_t launch_odd_edges(int k, int r, int mode, const PassArgs& a, uint32_t* flags, hipStream_t stream);

@@ -44,6 +44,8 @@
 //
 // This unit: K <= 4 kernels, the edge / mirror-copy kernels and the host
 // launchers; the templates are in odd_impl.h.
+#include <atomic>
+
 #include "odd_impl.h"
 
 namespace hbec {
@@ -250,6 +252,8 @@ __global__ __launch_bounds__(kBlockThreads) void gf_odd_planrec(UPlanArgs p, con
 
 static uint32_t odd_rec_fw(int r, int mode) { return (uint32_t)((4 + 4 * (mode == kOddVerify ? 0 : r) + 7) & ~7); }
 
+uint32_t odd_waves_per_block(int xs) { return xs >= 0 ? (uint32_t)HBEC_ODD_BP_WPB : kPipeBlockThreads / 64; }
+
 uint32_t odd_rec_words(int k, int r, int mode) {
     const int nl = k + (mode == kOddVerify ? r : 0), la = mode == kOddAcc ? 4 * r : 0;
     return odd_rec_fw(r, mode) + (uint32_t)((3 * nl + la + 7) & ~7);
@@ -290,9 +294,10 @@ bool odd_enabled() {
     return on;
 }
 
-int odd_blocks_per_cu(int mode, int k, int r, bool mirror, bool records) {
+int odd_blocks_per_cu(int mode, int k, int r, bool mirror, bool records, int xs) {
     static const int v = (int)tune_knob("HBEC_ODD_BPC", 0);
     if (v > 0) return v;
+    if (xs >= 0) return HBEC_ODD_BP_BPC;  // launch bounds sized for it (odd_rec_lb)
     if (mode == kOddVerify) return HBEC_ODD_BPC_VERIFY;
     if (records && odd_rec_two_blocks(k, r, mode)) return 2;  // launch bounds sized for it (odd_rec_lb)
     return odd_two_blocks(k, r, mode, mirror) ? 2 : HBEC_ODD_BPC_APPLY;  // launch bounds sized for it (odd_lb)
@@ -319,9 +324,10 @@ uint32_t odd_plan_tile_bytes() { return (uint32_t)kOddPlanU * kOddWin; }
 
 // Tiles per shard: enough windows for every output block of the shard, from
 // the frame's first column (c0 >= -32) to position S.
-uint32_t odd_tiles_per_obj(int k, int mode, uint64_t shard_len, bool records) {
+uint32_t odd_tiles_per_obj(int k, int mode, uint64_t shard_len, bool records, int xs) {
     const uint64_t span = shard_len + 32u;
-    const uint64_t tile = records ? (uint64_t)odd_rec_span(odd_u(k, mode), mode)
+    const uint64_t tile = xs >= 0 ? (uint64_t)odd_rec_span(odd_bp_u(), mode)
+                          : records ? (uint64_t)odd_rec_span(odd_u(k, mode), mode)
                           : mode == kOddVerify ? (odd_u(k, mode) >= 2 ? (uint64_t)(64u * odd_u(k, mode) - 1u) * 16u
                                                                       : (uint64_t)odd_win<kOddVerify>())
                                                : (odd_u(k, mode) == 2 ? (uint64_t)(64 + kOddStore) * 16u
@@ -331,9 +337,33 @@ uint32_t odd_tiles_per_obj(int k, int mode, uint64_t shard_len, bool records) {
 
 bool odd_supported(int k, int r) { return k >= 1 && k <= kOddMaxK && r >= 1 && r <= kMaxR; }
 
+int odd_bp_schedule(int k, int r, int mode, const uint32_t (*tab)[kMaxK][5]) {
+    static const bool on = tune_knob("HBEC_ODD_BP", 1) != 0;
+    if (!on || mode != kOddApply || k > kOddMaxK || r > kMaxR) return -1;
+    for (int i = 0; i < kXorShapeCount; ++i) {
+        const XorShape& x = kXorShapes[i];
+        if (x.k != k || x.R != r) continue;
+        bool eq = true;
+        for (int q = 0; q < r && eq; ++q)
+            for (int j = 0; j < k && eq; ++j) eq = ((tab[q][j][0] >> 8) & 0xFFu) == x.coef[q][j];  // t[0] byte 1 = c * 1
+        if (eq) return i;
+    }
+    return -1;
+}
+
+std::atomic<uint64_t> g_odd_launches[3];  // bit-plane, record, strided (hbec_odd_path_stats)
+
 hipError_t launch_odd(int k, int r, int mode, const PassArgs& a, uint32_t* flags, const uint32_t* recs, int grid,
-                      hipStream_t stream) {
+                      hipStream_t stream, int xs) {
     if (!pos32_shard(a.shard_len)) return hipErrorInvalidValue;  // 32-bit shard positions
+    g_odd_launches[xs >= 0 ? 0 : (recs ? 1 : 2)].fetch_add(1, std::memory_order_relaxed);
+    if (xs >= 0) {
+        if (!recs || mode != kOddApply || xs >= kXorShapeCount || kXorShapes[xs].k != k || kXorShapes[xs].R != r)
+            return hipErrorInvalidValue;
+        const void* fn = odd_kernel_bp(xs);
+        void* args[] = {const_cast<PassArgs*>(&a), &flags, &recs};
+        return hipLaunchKernel(fn, dim3(grid), dim3(64 * HBEC_ODD_BP_WPB), args, 0, stream);
+    }
     const void* fn = odd_kernel(k, r, mode, false, false, recs != nullptr);
     if (!fn) return hipErrorInvalidValue;
     void* args[] = {const_cast<PassArgs*>(&a), &flags, &recs};
@@ -363,6 +393,7 @@ hipError_t launch_odd_edges_plan(int k, int r, int mode, const UPlanArgs& p, con
 }
 
 hipError_t launch_odd_plan(int k, int r, int mode, const UPlanArgs& p, int grid, hipStream_t stream) {
+    g_odd_launches[2].fetch_add(1, std::memory_order_relaxed);
     const void* fn = odd_kernel(k, r, mode, true, p.mirror != 0, p.carry != 0);
     if (!fn) return hipErrorInvalidValue;
     const URec* recs = p.recs;
@@ -383,3 +414,10 @@ hipError_t launch_odd_mirror_copy(const URec* erecs, uint32_t n_erecs, const Mir
 uint64_t odd_mirror_pitch_host(uint64_t shard_len) { return odd_mirror_pitch(shard_len); }
 
 }  // namespace hbec
+
+extern "C" int hbec_odd_path_stats(uint64_t* bitplane, uint64_t* records, uint64_t* strided) {
+    if (bitplane) *bitplane = hbec::g_odd_launches[0].load();
+    if (records) *records = hbec::g_odd_launches[1].load();
+    if (strided) *strided = hbec::g_odd_launches[2].load();
+    return 0;
+}

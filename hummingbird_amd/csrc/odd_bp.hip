@@ -1,0 +1,18 @@
+// odd_bp.hip — bit-plane record kernels (gf_odd_rec<K, R, 0, XS>, odd_impl.h):
+// one instance per compiled encode schedule of xor_sched.h, in their own unit
+// so the build compiles them in parallel with the table kernels.
+#include <utility>
+
+#include "odd_impl.h"
+
+namespace hbec {
+
+template <int... I>
+static const void* odd_bp_pick(int xs, std::integer_sequence<int, I...>) {
+    static const void* const fns[] = {(const void*)&gf_odd_rec<XorNet<I>::K, XorNet<I>::R, kOddApply, I>...};
+    return xs >= 0 && xs < (int)sizeof...(I) ? fns[xs] : nullptr;
+}
+
+const void* odd_kernel_bp(int xs) { return odd_bp_pick(xs, std::make_integer_sequence<int, kXorShapeCount>{}); }
+
+}  // namespace hbec

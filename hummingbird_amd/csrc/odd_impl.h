@@ -9,9 +9,11 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "gf_device.h"
 #include "kernels.h"
+#include "xor_sched.h"
 
 namespace hbec {
 
@@ -146,6 +148,27 @@ __device__ __forceinline__ uint32_t lane_next_fill(uint32_t v, uint32_t fill) {
 __device__ __forceinline__ u32x4 lane_next4_fill(const u32x4& v, const u32x4& fill) {
     return u32x4{lane_next_fill(v[0], fill[0]), lane_next_fill(v[1], fill[1]), lane_next_fill(v[2], fill[2]),
                  lane_next_fill(v[3], fill[3])};
+}
+
+// Lane l gets v0's lane l+1, lane 63 gets v1's lane 0 (the carry of two
+// contiguous windows): DPP wave_rol:1 of v1 as the out-of-range fill of a
+// wave_shl:1 of v0.  Two VALU moves; replaces a v_readlane whose SGPR result
+// the next DPP move waits for (an issue stall per dword at one wave per SIMD).
+__device__ __forceinline__ uint32_t lane_next_carry(uint32_t v0, uint32_t v1) {
+    const int rot = __builtin_amdgcn_update_dpp(0, (int)v1, 0x134, 0xF, 0xF, false);  // wave_rol:1
+    return (uint32_t)__builtin_amdgcn_update_dpp(rot, (int)v0, 0x130, 0xF, 0xF, false);
+}
+
+__device__ __forceinline__ u32x4 lane_next4_carry(const u32x4& v0, const u32x4& v1) {
+    return u32x4{lane_next_carry(v0[0], v1[0]), lane_next_carry(v0[1], v1[1]), lane_next_carry(v0[2], v1[2]),
+                 lane_next_carry(v0[3], v1[3])};
+}
+
+// odd_shift_in of window 0 with window 1 (v1) supplying lane 63's neighbour
+__device__ __forceinline__ u32x4 odd_shift_in_carry(const u32x4& v, uint32_t sh, const u32x4& v1) {
+    const uint32_t n0 = lane_next_carry(v[0], v1[0]);
+    return u32x4{__builtin_amdgcn_alignbyte(v[1], v[0], sh), __builtin_amdgcn_alignbyte(v[2], v[1], sh),
+                 __builtin_amdgcn_alignbyte(v[3], v[2], sh), __builtin_amdgcn_alignbyte(n0, v[3], sh)};
 }
 
 __device__ __forceinline__ u32x4 lane0(const u32x4& v) {
@@ -360,7 +383,7 @@ __device__ __forceinline__ void odd_finish(const OddRegs<K, R, U, MODE>& X, cons
             u32x4 x[K];
 #pragma unroll
             for (int j = 0; j < K; ++j)
-                x[j] = u + 1 < U ? odd_shift_in_fill(X.x[u][j], sh[j], lane0(X.x[u + 1 < U ? u + 1 : u][j]))
+                x[j] = u + 1 < U ? odd_shift_in_carry(X.x[u][j], sh[j], X.x[u + 1 < U ? u + 1 : u][j])
                                  : odd_shift_in(X.x[u][j], sh[j]);
             u32x4 acc[R];
 #pragma unroll
@@ -370,7 +393,7 @@ __device__ __forceinline__ void odd_finish(const OddRegs<K, R, U, MODE>& X, cons
             const bool mine = b.live != 0u && (u + 1 < U || lane < 63u) && cpos >= kOddGuard && cpos <= hi;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                const u32x4 st = u + 1 < U ? odd_shift_in_fill(X.x[u][K + r], sh[K + r], lane0(X.x[u + 1 < U ? u + 1 : u][K + r]))
+                const u32x4 st = u + 1 < U ? odd_shift_in_carry(X.x[u][K + r], sh[K + r], X.x[u + 1 < U ? u + 1 : u][K + r])
                                            : odd_shift_in(X.x[u][K + r], sh[K + r]);
                 const u32x4 df = st ^ acc[r];
                 bad |= mine && (df[0] | df[1] | df[2] | df[3]) != 0u;
@@ -387,7 +410,7 @@ __device__ __forceinline__ void odd_finish(const OddRegs<K, R, U, MODE>& X, cons
 #pragma unroll
         for (int j = 0; j < K; ++j) {
             x1[j] = odd_shift_in(X.x[1][j], sh[j]);
-            x0[j] = odd_shift_in_fill(X.x[0][j], sh[j], lane0(X.x[1][j]));
+            x0[j] = odd_shift_in_carry(X.x[0][j], sh[j], X.x[1][j]);
         }
 #pragma unroll
         for (int r = 0; r < R; ++r) acc1[r] = acc0[r] = u32x4{0, 0, 0, 0};
@@ -399,7 +422,7 @@ __device__ __forceinline__ void odd_finish(const OddRegs<K, R, U, MODE>& X, cons
         for (int r = 0; r < R; ++r) {
             u32x4 b0 = acc0[r], b1 = acc1[r];
             if (dl[r] != 0u) {  // wave-uniform (never r = 0)
-                b0 = realign16(acc0[r], lane_next4_fill(acc0[r], lane0(acc1[r])), dl[r]);
+                b0 = realign16(acc0[r], lane_next4_carry(acc0[r], acc1[r]), dl[r]);
                 b1 = realign16(acc1[r], lane_next4(acc1[r]), dl[r]);
             }
             const int32_t q0 = b.c + 16 * (int32_t)lane + (int32_t)dl[r];
@@ -612,6 +635,68 @@ __device__ __forceinline__ void gf_dot_lds(u32x4 (&acc)[R], const u32x4 (&x)[K],
     }
 }
 
+// ---------------------------------------------------------------------------
+// Bit-plane field multiply for fixed coefficient matrices (the encode parity
+// rows, xor_sched.h).  A lane's two 16-B columns of an input (the carried
+// 2-window tile) are 8 dwords; an in-register 8 x 8 bit transpose within each
+// byte lane turns them into 8 planes (plane b, bit 8 L + d = bit b of byte L
+// of dword d), so multiplying every byte by a constant is a fixed XOR of
+// planes, and the whole (8R x 8K) bit matrix of a pass is the straight-line
+// network XorNet<XS>.  The same transpose (an involution) turns the 8R output
+// planes back into bytes.  Per 32 bytes of every input: 48 K + 48 R transpose
+// instructions plus the network (10+4: 672 + 272) against 8 K (5 + 4.5 R) for
+// the v_perm tables (10+4: 1840), and no coefficient tables in registers or LDS.
+// ---------------------------------------------------------------------------
+// a <-> b delta swap of one transpose stage: a's bits (m << s) take b's bits
+// m, b's bits m take a's bits (m << s) (two shifts, two v_bitop3 selects)
+__device__ __forceinline__ void bp_swap(uint32_t& a, uint32_t& b, uint32_t s, uint32_t m) {
+    const uint32_t hi = m << s;
+    const uint32_t na = (a & ~hi) | ((b << s) & hi);
+    const uint32_t nb = (b & ~m) | ((a >> s) & m);
+    a = na;
+    b = nb;
+}
+
+// 8 x 8 bit transpose within every byte lane of d[0..7]: bit b of byte L of
+// d[w] <-> bit w of byte L of d[b]
+__device__ __forceinline__ void bp_transpose8(uint32_t (&d)[8]) {
+#pragma unroll
+    for (int w = 0; w < 4; ++w) bp_swap(d[w], d[w + 4], 4u, 0x0F0F0F0Fu);
+#pragma unroll
+    for (int w = 0; w < 8; w += 4) {
+        bp_swap(d[w], d[w + 2], 2u, 0x33333333u);
+        bp_swap(d[w + 1], d[w + 3], 2u, 0x33333333u);
+    }
+#pragma unroll
+    for (int w = 0; w < 8; w += 2) bp_swap(d[w], d[w + 1], 1u, 0x55555555u);
+}
+
+// acc0 / acc1 = C x0 / C x1 (two columns per lane, fresh accumulators)
+template <int XS, int K, int R>
+__device__ __forceinline__ void bp_dot2(u32x4 (&acc0)[R], u32x4 (&acc1)[R], const u32x4 (&x0)[K],
+                                        const u32x4 (&x1)[K]) {
+    static_assert(XorNet<XS>::K == K && XorNet<XS>::R == R, "schedule shape");
+    uint32_t p[8 * K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        uint32_t d[8] = {x0[j][0], x0[j][1], x0[j][2], x0[j][3], x1[j][0], x1[j][1], x1[j][2], x1[j][3]};
+        bp_transpose8(d);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) p[8 * j + b] = d[b];
+    }
+    uint32_t o[8 * R];
+    XorNet<XS>::run(p, o);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        uint32_t d[8];
+#pragma unroll
+        for (int b = 0; b < 8; ++b) d[b] = o[8 * r + b];
+        bp_transpose8(d);
+        acc0[r] = u32x4{d[0], d[1], d[2], d[3]};
+        acc1[r] = u32x4{d[4], d[5], d[6], d[7]};
+    }
+}
+
 template <int K, int R, int MODE>
 struct OddRec {
     static constexpr int NL = K + (MODE == kOddVerify ? R : 0);
@@ -736,9 +821,9 @@ __device__ __forceinline__ void odd_rec_pin(u32x4 (&acc)[R]) {
     }
 }
 
-template <int K, int R, int U, int MODE, bool CARRY>
+template <int K, int R, int U, int MODE, bool CARRY, int XS = -1, class TB = Tables<K, R, kOddVMin>>
 __device__ __forceinline__ void odd_rec_finish(const OddRegs<K, R, U, MODE>& X, const OddRT<K, R, MODE>& t,
-                                               const TabArray& tab, const Tables<K, R, kOddVMin>& tb,
+                                               const TabArray& tab, const TB& tb,
                                                uint32_t lane, uint32_t* flags, uint32_t lt) {
     constexpr int NL = OddRec<K, R, MODE>::NL;
     const uint32_t shp = odd_w(t.f, 0), dlp = odd_w(t.f, 1);
@@ -761,20 +846,24 @@ __device__ __forceinline__ void odd_rec_finish(const OddRegs<K, R, U, MODE>& X, 
 #pragma unroll
         for (int j = 0; j < K; ++j) {
             x1[j] = odd_shift_in(X.x[1][j], sh[j]);
-            x0[j] = odd_shift_in_fill(X.x[0][j], sh[j], lane0(X.x[1][j]));
+            x0[j] = odd_shift_in_carry(X.x[0][j], sh[j], X.x[1][j]);
         }
+        if constexpr (XS >= 0) {
+            bp_dot2<XS, K, R>(acc0, acc1, x0, x1);
+        } else {
 #pragma unroll
-        for (int r = 0; r < R; ++r) acc1[r] = acc0[r] = u32x4{0, 0, 0, 0};
-        gf_dot<K, R, kOddVMin>(acc1, x1, tab, tb);
-        gf_dot<K, R, kOddVMin>(acc0, x0, tab, tb);
-        odd_rec_pin<K, R, MODE>(acc1);
-        odd_rec_pin<K, R, MODE>(acc0);
+            for (int r = 0; r < R; ++r) acc1[r] = acc0[r] = u32x4{0, 0, 0, 0};
+            gf_dot<K, R, kOddVMin>(acc1, x1, tab, tb);
+            gf_dot<K, R, kOddVMin>(acc0, x0, tab, tb);
+            odd_rec_pin<K, R, MODE>(acc1);
+            odd_rec_pin<K, R, MODE>(acc0);
+        }
         const uint32_t v0 = t.v0 + 16u * lane, v1 = v0 + 1024u;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             u32x4 b0 = acc0[r], b1 = acc1[r];
             if (dl[r] != 0u) {  // wave-uniform (never r = 0)
-                b0 = realign16(acc0[r], lane_next4_fill(acc0[r], lane0(acc1[r])), dl[r]);
+                b0 = realign16(acc0[r], lane_next4_carry(acc0[r], acc1[r]), dl[r]);
                 b1 = realign16(acc1[r], lane_next4(acc1[r]), dl[r]);
             }
             if constexpr (MODE == kOddAcc) {
@@ -785,45 +874,46 @@ __device__ __forceinline__ void odd_rec_finish(const OddRegs<K, R, U, MODE>& X, 
             odd_st(q_addr(r, v1), b1, st_mask(r, v1, kOddStore));
         }
         return;
-    }
-    bool bad = false;
+    } else {
+        bool bad = false;
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const uint32_t v = t.v0 + 16u * odd_rec_wcol<U, MODE, CARRY>(u) + 16u * lane;  // this lane's column
-        u32x4 x[K];
+        for (int u = 0; u < U; ++u) {
+            const uint32_t v = t.v0 + 16u * odd_rec_wcol<U, MODE, CARRY>(u) + 16u * lane;  // this lane's column
+            u32x4 x[K];
 #pragma unroll
-        for (int j = 0; j < K; ++j) x[j] = odd_shift_in(X.x[u][j], sh[j]);
-        u32x4 acc[R];
+            for (int j = 0; j < K; ++j) x[j] = odd_shift_in(X.x[u][j], sh[j]);
+            u32x4 acc[R];
 #pragma unroll
-        for (int r = 0; r < R; ++r) acc[r] = u32x4{0, 0, 0, 0};
-        if constexpr (odd_rec_lds(K)) {
-            gf_dot_lds<K, R>(acc, x, lt);
-        } else {
-            gf_dot<K, R, kOddVMin>(acc, x, tab, tb);
+            for (int r = 0; r < R; ++r) acc[r] = u32x4{0, 0, 0, 0};
+            if constexpr (odd_rec_lds(K)) {
+                gf_dot_lds<K, R>(acc, x, lt);
+            } else {
+                gf_dot<K, R, kOddVMin>(acc, x, tab, tb);
+            }
+            odd_rec_pin<K, R, MODE>(acc);
+            if constexpr (MODE == kOddVerify) {
+                const bool mine = t.live != 0u && lane < odd_store<MODE>() && (v - odd_w(t.f, 2)) <= odd_w(t.f, 3);
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const u32x4 df = odd_shift_in(X.x[u][K + r], sh[K + r]) ^ acc[r];
+                    bad |= mine && (df[0] | df[1] | df[2] | df[3]) != 0u;
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    u32x4 blk = acc[r];
+                    if (dl[r] != 0u) blk = realign16(acc[r], lane_next4(acc[r]), dl[r]);  // wave-uniform (never r = 0)
+                    if constexpr (MODE == kOddAcc) blk ^= X.x[u][K + r];
+                    odd_st(q_addr(r, v), blk, st_mask(r, v, kOddStore));
+                }
+            }
         }
-        odd_rec_pin<K, R, MODE>(acc);
         if constexpr (MODE == kOddVerify) {
-            const bool mine = t.live != 0u && lane < odd_store<MODE>() && (v - odd_w(t.f, 2)) <= odd_w(t.f, 3);
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const u32x4 df = odd_shift_in(X.x[u][K + r], sh[K + r]) ^ acc[r];
-                bad |= mine && (df[0] | df[1] | df[2] | df[3]) != 0u;
-            }
-        } else {
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                u32x4 blk = acc[r];
-                if (dl[r] != 0u) blk = realign16(acc[r], lane_next4(acc[r]), dl[r]);  // wave-uniform (never r = 0)
-                if constexpr (MODE == kOddAcc) blk ^= X.x[u][K + r];
-                odd_st(q_addr(r, v), blk, st_mask(r, v, kOddStore));
+            if (__any(bad)) {
+                if (lane == 0u) atomicOr(flags + t.obj, 1u);
             }
         }
-    }
-    if constexpr (MODE == kOddVerify) {
-        if (__any(bad)) {
-            if (lane == 0u) atomicOr(flags + t.obj, 1u);
-        }
-    }
+    }  // !CARRY
 }
 
 // A wave's tiles t0, t0 + nw, ...: (object, tile in object), stepped by
@@ -833,27 +923,40 @@ struct OddPos {
     uint32_t obj, ti;
 };
 
-// LDS-table record kernels fit 2 blocks per CU (2 waves per SIMD)
+// LDS-table record kernels fit 2 blocks per CU (2 waves per SIMD); the
+// bit-plane kernels (XS >= 0) HBEC_ODD_BP_BPC (tuning.h)
+template <int K, int R, int MODE, int XS = -1>
+__host__ __device__ constexpr int odd_rec_lb() {
+    return XS >= 0 ? HBEC_ODD_BP_BPC : (odd_rec_two_blocks(K, R, MODE) ? 2 : odd_lb<K, R, MODE>());
+}
+// Bit-plane record kernels: the carried 2-window tile (both columns of a
+// lane form one 32-byte plane group), apply only
+__host__ __device__ constexpr int odd_bp_u() { return 2; }
+// split record loads only without SGPR spills (K R <= 24, as odd_rec_prefetch:
+// 8+4 / 10+4 / 12+4 spill 1-21 SGPRs into VGPR lanes)
 template <int K, int R, int MODE>
-__host__ __device__ constexpr int odd_rec_lb() { return odd_rec_two_blocks(K, R, MODE) ? 2 : odd_lb<K, R, MODE>(); }
+__host__ __device__ constexpr bool odd_bp_prefetch() { return HBEC_ODD_BP_PF != 0 && K * R <= 24; }
 
-template <int K, int R, int MODE>
-__global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE>())) void gf_odd_rec(PassArgs a, uint32_t* flags,
-                                                                                        const uint32_t* __restrict__ recs) {
+template <int K, int R, int MODE, int XS = -1>
+__global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE, XS>())) void gf_odd_rec(PassArgs a, uint32_t* flags,
+                                                                                            const uint32_t* __restrict__ recs) {
     using RC = OddRec<K, R, MODE>;
-    constexpr bool PF = odd_rec_prefetch<K, R, MODE>();
-    constexpr int U = odd_u(K, MODE);
+    constexpr bool BP = XS >= 0;
+    static_assert(!BP || MODE == kOddApply, "bit-plane records: apply");
+    constexpr bool PF = BP ? odd_bp_prefetch<K, R, MODE>() : odd_rec_prefetch<K, R, MODE>();
+    constexpr int U = BP ? odd_bp_u() : odd_u(K, MODE);
     constexpr bool CARRY = odd_rec_carry(U, MODE);
+    constexpr bool LDS = !BP && odd_rec_lds(K);
     constexpr uint32_t SPAN = odd_rec_span(U, MODE);
-    constexpr uint32_t WPB = kPipeBlockThreads / 64;
+    constexpr uint32_t WPB = BP ? (uint32_t)HBEC_ODD_BP_WPB : kPipeBlockThreads / 64;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t nw = gridDim.x * WPB;
     const uint32_t n = a.n_tiles, tpo = a.tiles_per_obj, n_obj = (uint32_t)a.n_obj;
     const uint32_t wave0 = __builtin_amdgcn_readfirstlane(xcd_block() * WPB);
     const uint32_t dw = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (wave0 >= n) return;  // whole blocks only: the loop below has block barriers
-    __shared__ __attribute__((aligned(16))) uint32_t ltab[odd_rec_lds(K) ? K * odd_lt_stride(R) : 4];
-    if constexpr (odd_rec_lds(K)) {
+    __shared__ __attribute__((aligned(16))) uint32_t ltab[LDS ? K * odd_lt_stride(R) : 4];
+    if constexpr (LDS) {
         // whole blocks reach this point (the early return above is per block)
         const uint32_t ts = odd_lt_stride(R);
         for (uint32_t i = threadIdx.x; i < (uint32_t)K * ts; i += blockDim.x) {
@@ -863,7 +966,9 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE>())) void
         __syncthreads();
     }
     const uint32_t lt = (uint32_t)reinterpret_cast<uintptr_t>(&ltab[0]);  // LDS offset (low half of the flat address)
-    const Tables<K, R, kOddVMin> tb = load_tables<K, R, kOddVMin>(a.tab);
+    using TB = std::conditional_t<BP, Tables<1, 1, kOddVMin>, Tables<K, R, kOddVMin>>;
+    TB tb{};
+    if constexpr (!BP) tb = load_tables<K, R, kOddVMin>(a.tab);
     const uint32_t qq = nw / tpo, rr = nw - qq * tpo;
     auto step = [&](OddPos p) {
         p.ti += rr;
@@ -914,8 +1019,9 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE>())) void
         odd_rec_sload<PF>(tz.f, rec(p));
         p = step(p);
         odd_rec_sload<PF>(L, rec(p) + RC::FW);
+        if constexpr (BP && HBEC_ODD_BP_SLEEP > 0) __builtin_amdgcn_s_sleep(HBEC_ODD_BP_SLEEP);
         if constexpr (MODE != kOddVerify) __builtin_amdgcn_s_barrier();
-        odd_rec_finish<K, R, U, MODE, CARRY>(W, tw, a.tab, tb, lane, flags, lt);
+        odd_rec_finish<K, R, U, MODE, CARRY, XS>(W, tw, a.tab, tb, lane, flags, lt);
         odd_swait();
         odd_swait_pin(L);
         odd_swait_pin(tz.f);
@@ -925,7 +1031,7 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE>())) void
         X = Y;
         tx = ty;
     }
-    odd_rec_finish<K, R, U, MODE, CARRY>(X, tx, a.tab, tb, lane, flags, lt);
+    odd_rec_finish<K, R, U, MODE, CARRY, XS>(X, tx, a.tab, tb, lane, flags, lt);
 }
 
 template <int K, int R, int MODE, bool MIR = false, bool CARRY = false>
@@ -983,6 +1089,9 @@ static const void* odd_kernel_range(int k, int r, int mode, bool plan, bool mirr
         return odd_kernel_range<K0 + 1, K1>(k, r, mode, plan, mirror, carry);
     }
 }
+
+// bit-plane record kernel of kXorShapes[xs] (odd_bp.hip), mode 0
+const void* odd_kernel_bp(int xs);
 
 // the other translation units' ranges
 const void* odd_kernel_k58(int k, int r, int mode, bool plan, bool mirror, bool variant);

@@ -154,19 +154,21 @@ int odd_stripe_rec_pass(int K, int R, int mode, const hbec::UPlanArgs& a, const 
     hbec::PassArgs c;
     std::memset(&c, 0, sizeof(c));
     std::memcpy(c.tab, a.tab, sizeof(c.tab));
+    const int xs = hbec::odd_bp_schedule(K, R, mode, a.tab);
     uint64_t first = 0;
     for (int k = 0; k < n_cls && e == hipSuccess; ++k) {
         const hbec::OddStripeRecs& o = cls[k];
-        const uint64_t tpo = hbec::odd_tiles_per_obj(K, mode, o.s_max, true);
+        const uint64_t tpo = hbec::odd_tiles_per_obj(K, mode, o.s_max, true, xs);
         c.n_obj = o.n;
         c.shard_len = o.s_max;
         c.tiles_per_obj = (uint32_t)tpo;
         c.n_tiles = (uint32_t)(o.n * tpo);
-        const uint64_t want = (c.n_tiles + 3) / 4;
-        uint64_t cap = (uint64_t)cus * (uint64_t)hbec::odd_blocks_per_cu(mode, K, R, false, true);
+        const uint64_t wpb = hbec::odd_waves_per_block(xs);
+        const uint64_t want = (c.n_tiles + wpb - 1) / wpb;
+        uint64_t cap = (uint64_t)cus * (uint64_t)hbec::odd_blocks_per_cu(mode, K, R, false, true, xs);
         if (max_blocks > 0) cap = std::min<uint64_t>(cap, (uint64_t)max_blocks);
         const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, cap));
-        e = hbec::launch_odd(K, R, mode, c, nullptr, recs + first * rw, grid, stream);
+        e = hbec::launch_odd(K, R, mode, c, nullptr, recs + first * rw, grid, stream, xs);
         first += o.n;
     }
     hbec::scratch_free(recs, stream);

@@ -109,6 +109,18 @@
 #ifndef HBEC_ODD_PLAN_REC_MINKR
 #define HBEC_ODD_PLAN_REC_MINKR 0  // plans: per-stripe records (gf_odd_planrec + gf_odd_rec) from K R >= this
 #endif
+#ifndef HBEC_ODD_BP_BPC
+#define HBEC_ODD_BP_BPC 1  // blocks per CU (launch bounds and grid) of the bit-plane record kernels
+#endif
+#ifndef HBEC_ODD_BP_PF
+#define HBEC_ODD_BP_PF 1  // bit-plane record kernels: record loads issued a tile ahead (split load / wait)
+#endif
+#ifndef HBEC_ODD_BP_WPB
+#define HBEC_ODD_BP_WPB 4  // waves per block of the bit-plane record kernels (one block per CU)
+#endif
+#ifndef HBEC_ODD_BP_SLEEP
+#define HBEC_ODD_BP_SLEEP 0  // x 64 cycles after the next tile's loads, bit-plane record kernels
+#endif
 #ifndef HBEC_ODD_BPC_APPLY
 #define HBEC_ODD_BPC_APPLY 1  // blocks per CU of the strided / plan apply grids (register-bound shapes: odd_two_blocks)
 #endif

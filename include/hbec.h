@@ -337,6 +337,12 @@ int hbec_batcher_stats(hbec_batcher* batcher, uint64_t* batches, uint64_t* strip
  * resident blocks per CU used to size the grid. */
 int hbec_set_force_stream(int on);
 int hbec_kernel_info(int k, int r, uint64_t shard_len, int* tile_bytes, int* kind, int* blocks_per_cu);
+/* Launches since load of the odd-shard main kernels (any alignment, k <= 12
+ * per pass): bitplane = the compiled XOR-network kernels of the fixed encode
+ * matrices (xor_sched.h), records = the table-multiply record kernels,
+ * strided = the table-multiply gf_odd / gf_odd_plan kernels.  Any pointer
+ * may be NULL. */
+int hbec_odd_path_stats(uint64_t* bitplane, uint64_t* records, uint64_t* strided);
 
 /* ---------------------------------------------------------------------------
  * ecutils.go stripe loops over io callbacks (objectserver/ecutils.go:14-186,
