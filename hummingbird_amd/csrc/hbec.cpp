@@ -173,7 +173,7 @@ static int odd_launches(const PassArgs& a, int K, int R, int mode, bool accumula
             // kernel's 8+3 Verify ran at the same speed with the same traffic
             // (1.11 vs 1.10 x, bench.py's leg); K > 8 needs its LDS tables
             // fixed encode matrices of a compiled shape: the bit-plane record kernel
-            const int xs = odd_bp_schedule(K1, R, m, b.tab);
+            const int xs = odd_bp_schedule(K1, R, m, b.tab, false);
             const bool use_rec = xs >= 0 || ((m != 2 || K1 > 8) && odd_uses_records(K1, R));
             const uint64_t tpo = odd_tiles_per_obj(K1, m, shard_len, use_rec, xs);
             const uint64_t max_obj = std::max<uint64_t>(1, std::min<uint64_t>((1ull << 31), g_chunk_tiles) / tpo);

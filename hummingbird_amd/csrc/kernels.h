@@ -155,7 +155,7 @@ uint32_t odd_tiles_per_obj(int k, int mode, uint64_t shard_len, bool records, in
 // Bit-plane record kernels (xor_sched.h): the schedule whose fixed coefficient
 // matrix equals this pass's tables (the encode parity rows of a compiled
 // (k, m); mode 0 apply only), or -1 for the v_perm table kernels.
-int odd_bp_schedule(int k, int r, int mode, const uint32_t (*tab)[kMaxK][5]);
+int odd_bp_schedule(int k, int r, int mode, const uint32_t (*tab)[kMaxK][5], bool plan);
 // waves per block of a gf_odd / gf_odd_rec launch (xs: odd_bp_schedule)
 uint32_t odd_waves_per_block(int xs);
 // shards of at most this many bytes are coded by gf_odd_edges alone

@@ -252,7 +252,10 @@ __global__ __launch_bounds__(kBlockThreads) void gf_odd_planrec(UPlanArgs p, con
 
 static uint32_t odd_rec_fw(int r, int mode) { return (uint32_t)((4 + 4 * (mode == kOddVerify ? 0 : r) + 7) & ~7); }
 
-uint32_t odd_waves_per_block(int xs) { return xs >= 0 ? (uint32_t)HBEC_ODD_BP_WPB : kPipeBlockThreads / 64; }
+uint32_t odd_waves_per_block(int xs) {
+    return xs >= 0 && xs < kXorShapeCount ? (uint32_t)odd_bp_wpb(kXorShapes[xs].k, kXorShapes[xs].R)
+                                          : kPipeBlockThreads / 64;
+}
 
 uint32_t odd_rec_words(int k, int r, int mode) {
     const int nl = k + (mode == kOddVerify ? r : 0), la = mode == kOddAcc ? 4 * r : 0;
@@ -337,12 +340,14 @@ uint32_t odd_tiles_per_obj(int k, int mode, uint64_t shard_len, bool records, in
 
 bool odd_supported(int k, int r) { return k >= 1 && k <= kOddMaxK && r >= 1 && r <= kMaxR; }
 
-int odd_bp_schedule(int k, int r, int mode, const uint32_t (*tab)[kMaxK][5]) {
-    static const bool on = tune_knob("HBEC_ODD_BP", 1) != 0;
+int odd_bp_schedule(int k, int r, int mode, const uint32_t (*tab)[kMaxK][5], bool plan) {
+    // tuning builds: HBEC_ODD_BP = 0 none, 1 the measured choice (XorShape
+    // strided / plan), 2 every compiled schedule
+    static const int on = (int)tune_knob("HBEC_ODD_BP", 1);
     if (!on || mode != kOddApply || k > kOddMaxK || r > kMaxR) return -1;
     for (int i = 0; i < kXorShapeCount; ++i) {
         const XorShape& x = kXorShapes[i];
-        if (x.k != k || x.R != r) continue;
+        if (x.k != k || x.R != r || (on == 1 && !(plan ? x.plan : x.strided))) continue;
         bool eq = true;
         for (int q = 0; q < r && eq; ++q)
             for (int j = 0; j < k && eq; ++j) eq = ((tab[q][j][0] >> 8) & 0xFFu) == x.coef[q][j];  // t[0] byte 1 = c * 1
@@ -362,7 +367,7 @@ hipError_t launch_odd(int k, int r, int mode, const PassArgs& a, uint32_t* flags
             return hipErrorInvalidValue;
         const void* fn = odd_kernel_bp(xs);
         void* args[] = {const_cast<PassArgs*>(&a), &flags, &recs};
-        return hipLaunchKernel(fn, dim3(grid), dim3(64 * HBEC_ODD_BP_WPB), args, 0, stream);
+        return hipLaunchKernel(fn, dim3(grid), dim3(64 * odd_waves_per_block(xs)), args, 0, stream);
     }
     const void* fn = odd_kernel(k, r, mode, false, false, recs != nullptr);
     if (!fn) return hipErrorInvalidValue;

@@ -68,7 +68,7 @@ constexpr int kOddPlanU = HBEC_ODD_PLAN_U;  // plans: windows per record (tuning
 // tile, read less but ran slower than gf_odd's 63-column windows at 4+2:
 // 74.5 vs 76.6 %, profiles/r04_ab_odd.jsonl batch F; Verify records are used
 // from K R >= 24, one window per tile.)
-__host__ __device__ constexpr bool odd_rec_carry(int u, int mode) { return mode != kOddVerify && u == 2; }
+__host__ __device__ constexpr bool odd_rec_carry(int u, int mode) { return mode != kOddVerify && u >= 2; }
 // Strided batches code from object records (gf_odd_rec) when they carry at
 // least 18 products per column (6+3, 7+3, 8+3, 10+4, 12+4 encode), and for
 // K > 8 with at least 3 outputs; gf_odd below: the per-tile base arithmetic
@@ -80,7 +80,8 @@ __host__ __device__ constexpr bool odd_rec_carry(int u, int mode) { return mode 
 __host__ __device__ constexpr bool odd_use_rec(int k, int r) { return k * r >= HBEC_ODD_REC_MINKR && (k <= 8 || r >= 3); }
 // shard bytes per wave tile of the record kernel
 __host__ __device__ constexpr uint32_t odd_rec_span(int u, int mode) {
-    return odd_rec_carry(u, mode) ? (64u + kOddStore) * 16u : (uint32_t)u * (mode == kOddVerify ? 63u : kOddStore) * 16u;
+    return odd_rec_carry(u, mode) ? (64u * (uint32_t)(u - 1) + kOddStore) * 16u
+                                  : (uint32_t)u * (mode == kOddVerify ? 63u : kOddStore) * 16u;
 }
 
 // One tile, wave-uniform.  Positions are 32-bit: the host sends shards of
@@ -781,18 +782,22 @@ struct OddRT {  // the finish's scalars of one tile
     uint32_t obj, live;
 };
 
-template <int K, int R, int U, int MODE, bool CARRY>
+template <int K, int R, int U, int MODE, bool CARRY, bool IMAJ = HBEC_ODD_REC_LOAD_ORDER != 0>
 __device__ __forceinline__ void odd_rec_load(OddRegs<K, R, U, MODE>& X, const u32x8 (&l)[OddRec<K, R, MODE>::LW / 8],
                                              uint32_t v0, uint32_t lane) {
     using RC = OddRec<K, R, MODE>;
+    // IMAJ (input-major): a shard's windows back to back, so the column a
+    // tile shares with the next one (its last window's lanes 62-63, the next
+    // tile's window 0) is requested by the two waves at the same point of
+    // their load sequences (odd 8+3 bit-plane reads 1.052 -> 1.015 x its
+    // bytes, 64.6 -> 65.6 %; profiles/r05_ab_bitplane.jsonl)
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
+    for (int jj = 0; jj < RC::NL * U; ++jj) {
+        const int j = IMAJ ? jj / U : jj % RC::NL;
+        const int u = IMAJ ? jj % U : jj / RC::NL;
         const uint32_t v = v0 + 16u * odd_rec_wcol<U, MODE, CARRY>(u) + 16u * lane;
-#pragma unroll
-        for (int j = 0; j < RC::NL; ++j) {
-            const uint64_t b = (uint64_t)odd_w(l, 3 * j) | ((uint64_t)odd_w(l, 3 * j + 1) << 32);
-            X.x[u][j] = ld16_addr(b + __builtin_elementwise_min(v, odd_w(l, 3 * j + 2)));
-        }
+        const uint64_t b = (uint64_t)odd_w(l, 3 * j) | ((uint64_t)odd_w(l, 3 * j + 1) << 32);
+        X.x[u][j] = ld16_addr(b + __builtin_elementwise_min(v, odd_w(l, 3 * j + 2)));
     }
     if constexpr (MODE == kOddAcc) {
         // the old output block each lane will rewrite, clamped into the band
@@ -841,37 +846,40 @@ __device__ __forceinline__ void odd_rec_finish(const OddRegs<K, R, U, MODE>& X, 
         return ((uint64_t)odd_w(t.f, 4 + 4 * r) | ((uint64_t)odd_w(t.f, 5 + 4 * r) << 32)) + v;
     };
     if constexpr (CARRY) {
-        static_assert(U == 2 && MODE != kOddVerify, "apply carry: 2 windows");
-        u32x4 x1[K], x0[K], acc1[R], acc0[R];
+        // U contiguous windows (2, or an even count for the bit-plane
+        // kernels): window u < U - 1 takes its lane 63's missing next column
+        // from window u + 1 and stores all 64 blocks, the last window 62
+        static_assert(MODE != kOddVerify && (U == 2 || (XS >= 0 && U % 2 == 0)), "apply carry windows");
+        u32x4 xw[U][K], acc[U][R];
 #pragma unroll
-        for (int j = 0; j < K; ++j) {
-            x1[j] = odd_shift_in(X.x[1][j], sh[j]);
-            x0[j] = odd_shift_in_carry(X.x[0][j], sh[j], X.x[1][j]);
-        }
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+                xw[u][j] = u + 1 < U ? odd_shift_in_carry(X.x[u][j], sh[j], X.x[u + 1 < U ? u + 1 : u][j])
+                                     : odd_shift_in(X.x[u][j], sh[j]);
         if constexpr (XS >= 0) {
-            bp_dot2<XS, K, R>(acc0, acc1, x0, x1);
+#pragma unroll
+            for (int u = 0; u < U; u += 2) bp_dot2<XS, K, R>(acc[u], acc[u + 1], xw[u], xw[u + 1]);
         } else {
 #pragma unroll
-            for (int r = 0; r < R; ++r) acc1[r] = acc0[r] = u32x4{0, 0, 0, 0};
-            gf_dot<K, R, kOddVMin>(acc1, x1, tab, tb);
-            gf_dot<K, R, kOddVMin>(acc0, x0, tab, tb);
-            odd_rec_pin<K, R, MODE>(acc1);
-            odd_rec_pin<K, R, MODE>(acc0);
+            for (int r = 0; r < R; ++r) acc[1][r] = acc[0][r] = u32x4{0, 0, 0, 0};
+            gf_dot<K, R, kOddVMin>(acc[1], xw[1], tab, tb);
+            gf_dot<K, R, kOddVMin>(acc[0], xw[0], tab, tb);
+            odd_rec_pin<K, R, MODE>(acc[1]);
+            odd_rec_pin<K, R, MODE>(acc[0]);
         }
-        const uint32_t v0 = t.v0 + 16u * lane, v1 = v0 + 1024u;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            u32x4 b0 = acc0[r], b1 = acc1[r];
-            if (dl[r] != 0u) {  // wave-uniform (never r = 0)
-                b0 = realign16(acc0[r], lane_next4_carry(acc0[r], acc1[r]), dl[r]);
-                b1 = realign16(acc1[r], lane_next4(acc1[r]), dl[r]);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                u32x4 bk = acc[u][r];
+                if (dl[r] != 0u)  // wave-uniform (never r = 0)
+                    bk = realign16(acc[u][r], u + 1 < U ? lane_next4_carry(acc[u][r], acc[u + 1 < U ? u + 1 : u][r])
+                                                        : lane_next4(acc[u][r]), dl[r]);
+                if constexpr (MODE == kOddAcc) bk ^= X.x[u][K + r];
+                const uint32_t v = t.v0 + 16u * lane + 1024u * (uint32_t)u;
+                odd_st(q_addr(r, v), bk, st_mask(r, v, u + 1 < U ? 64u : kOddStore));
             }
-            if constexpr (MODE == kOddAcc) {
-                b0 ^= X.x[0][K + r];
-                b1 ^= X.x[1][K + r];
-            }
-            odd_st(q_addr(r, v0), b0, st_mask(r, v0, 64u));
-            odd_st(q_addr(r, v1), b1, st_mask(r, v1, kOddStore));
         }
         return;
     } else {
@@ -931,7 +939,12 @@ __host__ __device__ constexpr int odd_rec_lb() {
 }
 // Bit-plane record kernels: the carried 2-window tile (both columns of a
 // lane form one 32-byte plane group), apply only
-__host__ __device__ constexpr int odd_bp_u() { return 2; }
+__host__ __device__ constexpr int odd_bp_u() { return HBEC_ODD_BP_U; }
+// waves per block (one block per CU): 3 from K R >= 48 (12+4 encode 58.3 ->
+// 62.9 %, 10+4 lost 2-3 points at 3; r05_ab_bitplane.jsonl)
+__host__ __device__ constexpr int odd_bp_wpb(int k, int r) {
+    return k * r >= HBEC_ODD_BP_WPB3_MINKR ? 3 : HBEC_ODD_BP_WPB;
+}
 // split record loads only without SGPR spills (K R <= 24, as odd_rec_prefetch:
 // 8+4 / 10+4 / 12+4 spill 1-21 SGPRs into VGPR lanes)
 template <int K, int R, int MODE>
@@ -947,8 +960,10 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE, XS>())) 
     constexpr int U = BP ? odd_bp_u() : odd_u(K, MODE);
     constexpr bool CARRY = odd_rec_carry(U, MODE);
     constexpr bool LDS = !BP && odd_rec_lds(K);
+    // input-major loads, except the 3-wave bit-plane blocks (12+4: 61.8 % window-major vs 59.2 %)
+    constexpr bool IMAJ = HBEC_ODD_REC_LOAD_ORDER != 0 && !(BP && odd_bp_wpb(K, R) == 3);
     constexpr uint32_t SPAN = odd_rec_span(U, MODE);
-    constexpr uint32_t WPB = BP ? (uint32_t)HBEC_ODD_BP_WPB : kPipeBlockThreads / 64;
+    constexpr uint32_t WPB = BP ? (uint32_t)odd_bp_wpb(K, R) : kPipeBlockThreads / 64;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t nw = gridDim.x * WPB;
     const uint32_t n = a.n_tiles, tpo = a.tiles_per_obj, n_obj = (uint32_t)a.n_obj;
@@ -1005,7 +1020,7 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE, XS>())) 
     odd_swait();
     odd_swait_pin(L);
     fill(tx, p);
-    odd_rec_load<K, R, U, MODE, CARRY>(X, L, tx.v0, lane);
+    odd_rec_load<K, R, U, MODE, CARRY, IMAJ>(X, L, tx.v0, lane);
     odd_rec_sload<PF>(tx.f, rec(p));
     p = step(p);
     odd_rec_sload<PF>(L, rec(p) + RC::FW);
@@ -1015,12 +1030,12 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE, XS>())) 
     auto half = [&](OddRegs<K, R, U, MODE>& Z, OddRT<K, R, MODE>& tz, const OddRegs<K, R, U, MODE>& W,
                     const OddRT<K, R, MODE>& tw) {
         fill(tz, p);
-        odd_rec_load<K, R, U, MODE, CARRY>(Z, L, tz.v0, lane);
+        odd_rec_load<K, R, U, MODE, CARRY, IMAJ>(Z, L, tz.v0, lane);
         odd_rec_sload<PF>(tz.f, rec(p));
         p = step(p);
         odd_rec_sload<PF>(L, rec(p) + RC::FW);
         if constexpr (BP && HBEC_ODD_BP_SLEEP > 0) __builtin_amdgcn_s_sleep(HBEC_ODD_BP_SLEEP);
-        if constexpr (MODE != kOddVerify) __builtin_amdgcn_s_barrier();
+        if constexpr (MODE != kOddVerify && (!BP || HBEC_ODD_BP_BARRIER)) __builtin_amdgcn_s_barrier();
         odd_rec_finish<K, R, U, MODE, CARRY, XS>(W, tw, a.tab, tb, lane, flags, lt);
         odd_swait();
         odd_swait_pin(L);

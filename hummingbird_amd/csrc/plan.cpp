@@ -154,7 +154,7 @@ int odd_stripe_rec_pass(int K, int R, int mode, const hbec::UPlanArgs& a, const 
     hbec::PassArgs c;
     std::memset(&c, 0, sizeof(c));
     std::memcpy(c.tab, a.tab, sizeof(c.tab));
-    const int xs = hbec::odd_bp_schedule(K, R, mode, a.tab);
+    const int xs = hbec::odd_bp_schedule(K, R, mode, a.tab, true);
     uint64_t first = 0;
     for (int k = 0; k < n_cls && e == hipSuccess; ++k) {
         const hbec::OddStripeRecs& o = cls[k];

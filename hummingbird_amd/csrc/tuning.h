@@ -115,11 +115,23 @@
 #ifndef HBEC_ODD_BP_PF
 #define HBEC_ODD_BP_PF 1  // bit-plane record kernels: record loads issued a tile ahead (split load / wait)
 #endif
+#ifndef HBEC_ODD_BP_U
+#define HBEC_ODD_BP_U 2  // windows per wave tile of the bit-plane record kernels (even: column pairs)
+#endif
+#ifndef HBEC_ODD_BP_BARRIER
+#define HBEC_ODD_BP_BARRIER 1  // one block barrier per tile in the bit-plane record kernels
+#endif
 #ifndef HBEC_ODD_BP_WPB
 #define HBEC_ODD_BP_WPB 4  // waves per block of the bit-plane record kernels (one block per CU)
 #endif
+#ifndef HBEC_ODD_BP_WPB3_MINKR
+#define HBEC_ODD_BP_WPB3_MINKR 48  // bit-plane kernels with K R >= this run 3 waves per block
+#endif
 #ifndef HBEC_ODD_BP_SLEEP
 #define HBEC_ODD_BP_SLEEP 0  // x 64 cycles after the next tile's loads, bit-plane record kernels
+#endif
+#ifndef HBEC_ODD_REC_LOAD_ORDER
+#define HBEC_ODD_REC_LOAD_ORDER 1  // record kernels' tile loads: 1 input-major (a shard's windows together), 0 window-major
 #endif
 #ifndef HBEC_ODD_BPC_APPLY
 #define HBEC_ODD_BPC_APPLY 1  // blocks per CU of the strided / plan apply grids (register-bound shapes: odd_two_blocks)

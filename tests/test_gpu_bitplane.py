@@ -46,7 +46,8 @@ def test_bitplane_encode_split_layout(k, m, s):
     before = _bp()
     B.encode_views(enc, iv + ov, n, s)
     torch.cuda.synchronize()
-    assert _bp() > before, "the bit-plane kernel did not run"
+    # strided batches take the bit-plane kernel where it measured faster
+    assert (_bp() > before) == gen_xor.USE[(k, m)][0]
     got = outs.cpu().numpy()
     want = np.full_like(got, GUARD)
     rows = CO.build_matrix(k, m)[k:]
@@ -60,9 +61,9 @@ def test_bitplane_encode_split_layout(k, m, s):
     assert bad.size == 0, f"{bad.size} bytes differ, first at {bad[:8]}"
 
 
-@pytest.mark.parametrize("k,m,obj_len,n", [(8, 3, (1 << 20) - 8, 160), (10, 4, 1 << 20, 160),
+@pytest.mark.parametrize("k,m,obj_len,n", [(9, 3, (1 << 20) - 8, 160), (10, 4, 1 << 20, 160),
                                            (12, 4, 12 * 87389, 128), (6, 3, (1 << 20) + 3, 160),
-                                           (4, 2, (1 << 20) - 4, 64), (8, 4, (1 << 20) - 9, 96)])
+                                           (8, 2, (1 << 20) - 9, 64), (8, 4, (1 << 20) - 9, 96)])
 def test_bitplane_databuf_many_tiles_then_rebuild(k, m, obj_len, n):
     """ecSplit databufs of 1 MiB-class objects (many tiles per wave, so the
     record prefetch runs ahead): Encode against the oracle, then a
@@ -92,13 +93,13 @@ def test_bitplane_databuf_many_tiles_then_rebuild(k, m, obj_len, n):
     assert torch.equal(damaged, rows)
 
 
-@pytest.mark.parametrize("k,m", [(8, 3), (10, 4), (4, 2)])
+@pytest.mark.parametrize("k,m", [km for km in SHAPES if gen_xor.USE[km][1]])
 def test_bitplane_object_plan(k, m):
     """Object plans of near-uniform odd sizes (per-stripe records, one class)
     take the bit-plane kernel too; every parity byte against the oracle."""
     rng = np.random.default_rng(k + m)
-    n = 96
-    sizes = [int(x) for x in rng.integers(150_001, 150_900, n)]
+    n = 64
+    sizes = [int(x) for x in rng.integers(60_001, 60_400, n)]
     d = torch.empty(sum(k * x for x in sizes) + 16, dtype=torch.uint8, device="cuda")
     B.fill_splitmix(d.view(1, -1), d.numel())
     par = torch.full((sum(m * x for x in sizes) + 16,), GUARD, dtype=torch.uint8, device="cuda")
