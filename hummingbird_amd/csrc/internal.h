@@ -92,18 +92,28 @@ struct URec;
 // passes accumulate).  sel_k > 0: object records (indices >= sel_k are
 // parity, base b).  max_blocks > 0 caps the grid (zero-copy over PCIe).
 // erecs: gf_odd's one edge record per stripe (guard-band bytes; none for the round-2 kernels).
-// orecs: n_orec_cls classes of per-stripe records (stripes longer than
-// odd_min_main(), shortest s_min, longest s_max bytes per class): unmirrored
-// passes code from them (gf_odd_rec, one launch per class, every stripe given
-// its class's longest tile count) when that wastes few tiles, instead of recs.
+// orecs: per-stripe records of the stripes longer than odd_min_main()
+// (longest s_max bytes) and their tile lists, one per record-kernel tile span
+// (odd_rec_tile_span): unmirrored passes code from them (gf_odd_rec over the
+// list: one launch per pass whatever the mix of lengths, no idle tiles)
+// instead of recs.
+struct OddTileList {
+    uint32_t span = 0;            // shard bytes per tile
+    const uint32_t* d = nullptr;  // device: {record index, tile in record} per tile
+    uint64_t n = 0;
+};
+constexpr int kOddSpans = 2;  // the record kernels' tile spans: 992 (5 <= K <= 12 tables), 2016 (carried 2 windows)
 struct OddStripeRecs {
     const URec* recs = nullptr;
-    uint64_t n = 0, s_min = 0, s_max = 0;
+    uint64_t n = 0, s_max = 0;
+    OddTileList lists[kOddSpans];
 };
+// the distinct odd_rec_tile_span values of apply / accumulate passes
+void odd_plan_spans(uint32_t (&spans)[kOddSpans]);
 int launch_unaligned_passes(const URec* recs, uint64_t n_recs, const std::vector<int>& in_idx,
                             const std::vector<int>& out_idx, const std::vector<uint8_t>& rows, int sel_k,
                             hipStream_t stream, int max_blocks = 0, const URec* erecs = nullptr,
                             uint64_t n_erecs = 0, bool mirror = false, bool round2 = false,
-                            const OddStripeRecs* orecs = nullptr, int n_orec_cls = 0);
+                            const OddStripeRecs* orecs = nullptr);
 
 }  // namespace hbec

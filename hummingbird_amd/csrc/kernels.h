@@ -48,6 +48,9 @@ struct PassArgs {
     uint32_t n_elems;       // packed path: n_obj * elems_per_obj (< 2^31)
     uint32_t elems_per_obj; // packed path: shard_len / 16
     uint32_t pad_;
+    // record kernels over a plan: n_tiles entries {record index, tile in record}
+    // (u32 pairs; odd_rec_tile_span bytes per tile); null: strided positions
+    const uint32_t* list;
 };
 
 // Packed path (short shards, S < one pipelined tile, e.g. 8+3 of 4 KiB
@@ -156,6 +159,8 @@ uint32_t odd_tiles_per_obj(int k, int mode, uint64_t shard_len, bool records, in
 // matrix equals this pass's tables (the encode parity rows of a compiled
 // (k, m); mode 0 apply only), or -1 for the v_perm table kernels.
 int odd_bp_schedule(int k, int r, int mode, const uint32_t (*tab)[kMaxK][5], bool plan);
+// shard bytes per tile of the record kernel a pass of k inputs launches (xs: odd_bp_schedule)
+uint32_t odd_rec_tile_span(int k, int mode, int xs);
 // waves per block of a gf_odd / gf_odd_rec launch (xs: odd_bp_schedule)
 uint32_t odd_waves_per_block(int xs);
 // shards of at most this many bytes are coded by gf_odd_edges alone

@@ -46,6 +46,7 @@
 // launchers; the templates are in odd_impl.h.
 #include <atomic>
 
+#include "internal.h"
 #include "odd_impl.h"
 
 namespace hbec {
@@ -285,11 +286,12 @@ hipError_t launch_odd_planrec(int k, int r, int mode, const UPlanArgs& p, const 
     return hipLaunchKernel((const void*)&gf_odd_planrec, dim3(grid), dim3(kBlockThreads), args, 0, stream);
 }
 
-// variant: odd_pick's (plans: carried records; strided: object records)
-static const void* odd_kernel(int k, int r, int mode, bool plan, bool mirror, bool variant) {
-    if (k <= 4) return odd_kernel_range<1, 4>(k, r, mode, plan, mirror, variant);
-    if (k <= 8) return odd_kernel_k58(k, r, mode, plan, mirror, variant);
-    return odd_kernel_k912(k, r, mode, plan, mirror, variant);
+// variant: odd_pick's (plans: carried records; strided: object records);
+// list: the record kernel over a plan's tile list
+static const void* odd_kernel(int k, int r, int mode, bool plan, bool mirror, bool variant, bool list = false) {
+    if (k <= 4) return odd_kernel_range<1, 4>(k, r, mode, plan, mirror, variant, list);
+    if (k <= 8) return odd_kernel_k58(k, r, mode, plan, mirror, variant, list);
+    return odd_kernel_k912(k, r, mode, plan, mirror, variant, list);
 }
 
 bool odd_enabled() {
@@ -327,6 +329,18 @@ uint32_t odd_plan_tile_bytes() { return (uint32_t)kOddPlanU * kOddWin; }
 
 // Tiles per shard: enough windows for every output block of the shard, from
 // the frame's first column (c0 >= -32) to position S.
+void odd_plan_spans(uint32_t (&spans)[kOddSpans]) {
+    // table record kernels: 5 <= K <= 12 one 992-B window per tile, K <= 4 the
+    // carried 2-window tile; bit-plane kernels HBEC_ODD_BP_U carried windows
+    static_assert(odd_rec_span(2, kOddApply) == odd_rec_span(HBEC_ODD_BP_U, kOddApply), "two tile spans");
+    spans[0] = odd_rec_span(1, kOddApply);
+    spans[1] = odd_rec_span(2, kOddApply);
+}
+
+uint32_t odd_rec_tile_span(int k, int mode, int xs) {
+    return xs >= 0 ? odd_rec_span(odd_bp_u(), mode) : odd_rec_span(odd_u(k, mode), mode);
+}
+
 uint32_t odd_tiles_per_obj(int k, int mode, uint64_t shard_len, bool records, int xs) {
     const uint64_t span = shard_len + 32u;
     const uint64_t tile = xs >= 0 ? (uint64_t)odd_rec_span(odd_bp_u(), mode)
@@ -365,11 +379,12 @@ hipError_t launch_odd(int k, int r, int mode, const PassArgs& a, uint32_t* flags
     if (xs >= 0) {
         if (!recs || mode != kOddApply || xs >= kXorShapeCount || kXorShapes[xs].k != k || kXorShapes[xs].R != r)
             return hipErrorInvalidValue;
-        const void* fn = odd_kernel_bp(xs);
+        const void* fn = odd_kernel_bp(xs, a.list != nullptr);
         void* args[] = {const_cast<PassArgs*>(&a), &flags, &recs};
         return hipLaunchKernel(fn, dim3(grid), dim3(64 * odd_waves_per_block(xs)), args, 0, stream);
     }
-    const void* fn = odd_kernel(k, r, mode, false, false, recs != nullptr);
+    if (a.list && !recs) return hipErrorInvalidValue;
+    const void* fn = odd_kernel(k, r, mode, false, false, recs != nullptr, a.list != nullptr);
     if (!fn) return hipErrorInvalidValue;
     void* args[] = {const_cast<PassArgs*>(&a), &flags, &recs};
     return hipLaunchKernel(fn, dim3(grid), dim3(kPipeBlockThreads), args, 0, stream);

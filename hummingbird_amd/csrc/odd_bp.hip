@@ -8,11 +8,14 @@
 namespace hbec {
 
 template <int... I>
-static const void* odd_bp_pick(int xs, std::integer_sequence<int, I...>) {
+static const void* odd_bp_pick(int xs, bool list, std::integer_sequence<int, I...>) {
     static const void* const fns[] = {(const void*)&gf_odd_rec<XorNet<I>::K, XorNet<I>::R, kOddApply, I>...};
-    return xs >= 0 && xs < (int)sizeof...(I) ? fns[xs] : nullptr;
+    static const void* const lfns[] = {(const void*)&gf_odd_rec<XorNet<I>::K, XorNet<I>::R, kOddApply, I, true>...};
+    return xs >= 0 && xs < (int)sizeof...(I) ? (list ? lfns[xs] : fns[xs]) : nullptr;
 }
 
-const void* odd_kernel_bp(int xs) { return odd_bp_pick(xs, std::make_integer_sequence<int, kXorShapeCount>{}); }
+const void* odd_kernel_bp(int xs, bool list) {
+    return odd_bp_pick(xs, list, std::make_integer_sequence<int, kXorShapeCount>{});
+}
 
 }  // namespace hbec

@@ -126,10 +126,16 @@ __device__ __forceinline__ OddIn odd_in(uint64_t base, int32_t S, int32_t c) {
     return o;
 }
 
+// plain (L2-retained) 16-B load: Verify tiles share their boundary column
+// with the neighbouring wave's tile, which without a block barrier reads it
+// at another time; a non-temporal fetch is gone from L2 by then
+__device__ __forceinline__ u32x4 ld16_addr_keep(uint64_t addr) { return *reinterpret_cast<gu32x4_c*>(addr); }
+
+template <bool NT = true>
 __device__ __forceinline__ u32x4 odd_ld(const OddIn& o, int32_t col) {
     int32_t v = o.off + 16 * col;
     v = v < 0 ? 0 : (v > o.lim ? o.lim : v);
-    return ld16_addr(o.base4 + (uint64_t)(uint32_t)v);
+    return NT ? ld16_addr(o.base4 + (uint64_t)(uint32_t)v) : ld16_addr_keep(o.base4 + (uint64_t)(uint32_t)v);
 }
 
 // bytes [sh, sh + 16) of the lane's block and lane l+1's first dword
@@ -330,7 +336,7 @@ __device__ __forceinline__ void odd_load(OddRegs<K, R, U, MODE>& X, const OddTil
     for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int j = 0; j < (MODE == kOddAcc ? K : NL); ++j)
-            X.x[u][j] = odd_ld(src[j], (int32_t)(odd_wcol<U, MODE, CARRY>(u) + lane));
+            X.x[u][j] = odd_ld<!(MODE == kOddVerify && HBEC_ODD_VERIFY_KEEP)>(src[j], (int32_t)(odd_wcol<U, MODE, CARRY>(u) + lane));
     if constexpr (MODE == kOddAcc) {
         // the old output block each lane will rewrite: output r's aligned block
         // at q = column + dl_r; lanes that store nothing read one inside the band
@@ -765,6 +771,22 @@ __device__ __forceinline__ void odd_rec_sload(u32x8 (&v)[N], const uint32_t* p) 
     }
 }
 
+// plan tile-list entries {record, tile}: 2-dword scalar loads, issued with
+// the record loads (split where those are split) and waited with them
+typedef uint32_t u32x2s __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void odd_sload_now2(u32x2s& v, const uint32_t* p) {
+    asm volatile("s_load_dwordx2 %0, %1, 0\n s_waitcnt lgkmcnt(0)" : "=&s"(v) : "s"(p) : "memory");
+}
+template <bool PF>
+__device__ __forceinline__ void odd_rec_sload2(u32x2s& v, const uint32_t* p) {
+    if constexpr (PF) {
+        asm volatile("s_load_dwordx2 %0, %1, 0" : "=s"(v) : "s"(p));
+    } else {
+        odd_sload_now2(v, p);
+    }
+}
+__device__ __forceinline__ void odd_swait_pin2(u32x2s& v) { asm volatile("" : "+s"(v)); }
+
 template <int N>
 __device__ __forceinline__ void odd_swait_pin(u32x8 (&v)[N]) {
 #pragma unroll
@@ -797,7 +819,8 @@ __device__ __forceinline__ void odd_rec_load(OddRegs<K, R, U, MODE>& X, const u3
         const int u = IMAJ ? jj % U : jj / RC::NL;
         const uint32_t v = v0 + 16u * odd_rec_wcol<U, MODE, CARRY>(u) + 16u * lane;
         const uint64_t b = (uint64_t)odd_w(l, 3 * j) | ((uint64_t)odd_w(l, 3 * j + 1) << 32);
-        X.x[u][j] = ld16_addr(b + __builtin_elementwise_min(v, odd_w(l, 3 * j + 2)));
+        const uint64_t ad = b + __builtin_elementwise_min(v, odd_w(l, 3 * j + 2));
+        X.x[u][j] = (MODE == kOddVerify && HBEC_ODD_VERIFY_KEEP) ? ld16_addr_keep(ad) : ld16_addr(ad);
     }
     if constexpr (MODE == kOddAcc) {
         // the old output block each lane will rewrite, clamped into the band
@@ -950,7 +973,13 @@ __host__ __device__ constexpr int odd_bp_wpb(int k, int r) {
 template <int K, int R, int MODE>
 __host__ __device__ constexpr bool odd_bp_prefetch() { return HBEC_ODD_BP_PF != 0 && K * R <= 24; }
 
-template <int K, int R, int MODE, int XS = -1>
+// LIST (plans): tile t codes tile list[t].ti of record list[t].rec (one
+// 8-byte entry per tile, plan.cpp build_tile_lists), so stripes of any mix
+// of lengths share one launch with no idle tiles; the strided batches derive
+// (object, tile) from t by division.  A tile's entry is loaded one step
+// before its record loads need it, together with the previous record loads
+// (no extra wait; the build-time check covers these split loads too).
+template <int K, int R, int MODE, int XS = -1, bool LIST = false>
 __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE, XS>())) void gf_odd_rec(PassArgs a, uint32_t* flags,
                                                                                             const uint32_t* __restrict__ recs) {
     using RC = OddRec<K, R, MODE>;
@@ -984,26 +1013,41 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE, XS>())) 
     using TB = std::conditional_t<BP, Tables<1, 1, kOddVMin>, Tables<K, R, kOddVMin>>;
     TB tb{};
     if constexpr (!BP) tb = load_tables<K, R, kOddVMin>(a.tab);
-    const uint32_t qq = nw / tpo, rr = nw - qq * tpo;
+    const uint32_t qq = LIST ? 0u : nw / tpo, rr = LIST ? 0u : nw - qq * tpo;
+    // LIST: p = {record, tile} of the tile the record loads are for, pe the
+    // entry of the tile after it (a scalar load issued with those record
+    // loads and waited with them); tq = p's tile index
+    uint32_t tq = wave0 + dw;
+    u32x2s pe{0u, 0u};
+    auto lentry = [&](uint32_t t) { return a.list + 2u * (t < n ? t : n - 1u); };
     auto step = [&](OddPos p) {
-        p.ti += rr;
-        p.obj += qq;
-        if (p.ti >= tpo) {
-            p.ti -= tpo;
-            p.obj += 1u;
+        if constexpr (LIST) {
+            tq += nw;
+            return OddPos{pe[0], pe[1]};
+        } else {
+            p.ti += rr;
+            p.obj += qq;
+            if (p.ti >= tpo) {
+                p.ti -= tpo;
+                p.obj += 1u;
+            }
+            return p;
         }
-        return p;
     };
     auto rec = [&](const OddPos& p) {
-        return recs + (size_t)__builtin_amdgcn_readfirstlane(p.obj < n_obj ? p.obj : n_obj - 1u) * RC::RW;
+        return recs + (size_t)__builtin_amdgcn_readfirstlane(LIST || p.obj < n_obj ? p.obj : n_obj - 1u) * RC::RW;
     };
-    auto v0 = [&](const OddPos& p) { return (p.obj < n_obj ? p.ti : tpo - 1u) * SPAN; };
+    auto v0 = [&](const OddPos& p) { return (LIST || p.obj < n_obj ? p.ti : tpo - 1u) * SPAN; };
     // Each step issues the next tile's loads (P, L = its load record,
     // waited), fetches the tile after it's load record into L and P's finish
     // record, codes the current tile, then copies the next tile's registers
     // over the current ones.
     OddPos p;
-    {
+    if constexpr (LIST) {
+        odd_sload_now2(pe, lentry(tq));
+        p = OddPos{pe[0], pe[1]};
+        odd_sload_now2(pe, lentry(tq + nw));
+    } else {
         const uint32_t t = wave0 + dw;
         p.obj = t / tpo;
         p.ti = t - p.obj * tpo;
@@ -1014,7 +1058,7 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE, XS>())) 
     auto fill = [&](OddRT<K, R, MODE>& tt, const OddPos& q) {
         tt.v0 = v0(q);
         tt.obj = q.obj;
-        tt.live = q.obj < n_obj;
+        tt.live = LIST ? (tq < n ? 1u : 0u) : (q.obj < n_obj ? 1u : 0u);
     };
     odd_rec_sload<PF>(L, rec(p) + RC::FW);
     odd_swait();
@@ -1024,9 +1068,11 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE, XS>())) 
     odd_rec_sload<PF>(tx.f, rec(p));
     p = step(p);
     odd_rec_sload<PF>(L, rec(p) + RC::FW);
+    if constexpr (LIST) odd_rec_sload2<PF>(pe, lentry(tq + nw));
     odd_swait();
     odd_swait_pin(L);
     odd_swait_pin(tx.f);
+    if constexpr (LIST) odd_swait_pin2(pe);
     auto half = [&](OddRegs<K, R, U, MODE>& Z, OddRT<K, R, MODE>& tz, const OddRegs<K, R, U, MODE>& W,
                     const OddRT<K, R, MODE>& tw) {
         fill(tz, p);
@@ -1034,12 +1080,14 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE, XS>())) 
         odd_rec_sload<PF>(tz.f, rec(p));
         p = step(p);
         odd_rec_sload<PF>(L, rec(p) + RC::FW);
+        if constexpr (LIST) odd_rec_sload2<PF>(pe, lentry(tq + nw));
         if constexpr (BP && HBEC_ODD_BP_SLEEP > 0) __builtin_amdgcn_s_sleep(HBEC_ODD_BP_SLEEP);
         if constexpr (MODE != kOddVerify && (!BP || HBEC_ODD_BP_BARRIER)) __builtin_amdgcn_s_barrier();
         odd_rec_finish<K, R, U, MODE, CARRY, XS>(W, tw, a.tab, tb, lane, flags, lt);
         odd_swait();
         odd_swait_pin(L);
         odd_swait_pin(tz.f);
+        if constexpr (LIST) odd_swait_pin2(pe);
     };
     for (uint32_t b0 = wave0 + nw; b0 < n; b0 += nw) {  // block-uniform trip count
         half(Y, ty, X, tx);
@@ -1061,9 +1109,15 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_lb<K, R, MODE, MIR>())) voi
 // variant: plans, the carried-record kernel; strided, the object-record
 // kernel (gf_odd_rec) instead of gf_odd
 template <int K, int R, int MODE>
-static const void* odd_pick(bool plan, bool mirror, bool variant) {
+static const void* odd_pick(bool plan, bool mirror, bool variant, bool list = false) {
     const bool carry = variant;
-    if (!plan) return variant ? (const void*)&gf_odd_rec<K, R, MODE> : (const void*)&gf_odd<K, R, MODE>;
+    if (!plan) {
+        if constexpr (MODE != kOddVerify) {  // plans never verify
+            if (list) return (const void*)&gf_odd_rec<K, R, MODE, -1, true>;
+        }
+        if (list) return nullptr;
+        return variant ? (const void*)&gf_odd_rec<K, R, MODE> : (const void*)&gf_odd<K, R, MODE>;
+    }
     if constexpr (MODE != kOddVerify) {  // plans never verify
         if (mirror) return (const void*)&gf_odd_plan<K, R, MODE, true>;
         if constexpr (odd_plan_u<K>(0) == 2) {
@@ -1075,41 +1129,43 @@ static const void* odd_pick(bool plan, bool mirror, bool variant) {
 }
 
 template <int K, int MODE>
-static const void* odd_for_r(int r, bool plan, bool mirror, bool carry) {
+static const void* odd_for_r(int r, bool plan, bool mirror, bool carry, bool list) {
     switch (r) {
-        case 1: return odd_pick<K, 1, MODE>(plan, mirror, carry);
-        case 2: return odd_pick<K, 2, MODE>(plan, mirror, carry);
-        case 3: return odd_pick<K, 3, MODE>(plan, mirror, carry);
-        case 4: return odd_pick<K, 4, MODE>(plan, mirror, carry);
+        case 1: return odd_pick<K, 1, MODE>(plan, mirror, carry, list);
+        case 2: return odd_pick<K, 2, MODE>(plan, mirror, carry, list);
+        case 3: return odd_pick<K, 3, MODE>(plan, mirror, carry, list);
+        case 4: return odd_pick<K, 4, MODE>(plan, mirror, carry, list);
     }
     return nullptr;
 }
 
 template <int K>
-static const void* odd_kernel_k(int r, int mode, bool plan, bool mirror, bool carry) {
+static const void* odd_kernel_k(int r, int mode, bool plan, bool mirror, bool carry, bool list) {
     switch (mode) {
-        case kOddApply: return odd_for_r<K, kOddApply>(r, plan, mirror, carry);
-        case kOddAcc: return odd_for_r<K, kOddAcc>(r, plan, mirror, carry);
-        case kOddVerify: return plan ? nullptr : odd_for_r<K, kOddVerify>(r, false, false, carry);
+        case kOddApply: return odd_for_r<K, kOddApply>(r, plan, mirror, carry, list);
+        case kOddAcc: return odd_for_r<K, kOddAcc>(r, plan, mirror, carry, list);
+        case kOddVerify: return (plan || list) ? nullptr : odd_for_r<K, kOddVerify>(r, false, false, carry, false);
     }
     return nullptr;
 }
 
 template <int K0, int K1>
-static const void* odd_kernel_range(int k, int r, int mode, bool plan, bool mirror, bool carry = false) {
+static const void* odd_kernel_range(int k, int r, int mode, bool plan, bool mirror, bool carry = false,
+                                    bool list = false) {
     if constexpr (K0 > K1) {
         return nullptr;
     } else {
-        if (k == K0) return odd_kernel_k<K0>(r, mode, plan, mirror, carry);
-        return odd_kernel_range<K0 + 1, K1>(k, r, mode, plan, mirror, carry);
+        if (k == K0) return odd_kernel_k<K0>(r, mode, plan, mirror, carry, list);
+        return odd_kernel_range<K0 + 1, K1>(k, r, mode, plan, mirror, carry, list);
     }
 }
 
-// bit-plane record kernel of kXorShapes[xs] (odd_bp.hip), mode 0
-const void* odd_kernel_bp(int xs);
+// bit-plane record kernel of kXorShapes[xs] (odd_bp.hip), mode 0; list: the
+// plan tile-list instance
+const void* odd_kernel_bp(int xs, bool list);
 
 // the other translation units' ranges
-const void* odd_kernel_k58(int k, int r, int mode, bool plan, bool mirror, bool variant);
-const void* odd_kernel_k912(int k, int r, int mode, bool plan, bool mirror, bool variant);
+const void* odd_kernel_k58(int k, int r, int mode, bool plan, bool mirror, bool variant, bool list);
+const void* odd_kernel_k912(int k, int r, int mode, bool plan, bool mirror, bool variant, bool list);
 
 }  // namespace hbec

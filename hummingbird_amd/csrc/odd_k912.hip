@@ -4,8 +4,8 @@
 
 namespace hbec {
 
-const void* odd_kernel_k912(int k, int r, int mode, bool plan, bool mirror, bool variant) {
-    return odd_kernel_range<9, kOddMaxK>(k, r, mode, plan, mirror, variant);
+const void* odd_kernel_k912(int k, int r, int mode, bool plan, bool mirror, bool variant, bool list) {
+    return odd_kernel_range<9, kOddMaxK>(k, r, mode, plan, mirror, variant, list);
 }
 
 }  // namespace hbec

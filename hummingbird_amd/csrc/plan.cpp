@@ -45,10 +45,11 @@ struct hbec_plan {
     // them with HBEC_ODD=0: round-2 gf_apply_unaligned_plan records
     hbec::URec* d_brecs = nullptr;
     uint64_t n_brecs = 0;
-    // gf_odd_rec: one record per stripe / object with a main-kernel part
-    // classes of near-equal tile counts, one gf_odd_rec launch per class and pass
+    // gf_odd_rec: one record per stripe / object with a main-kernel part,
+    // and the tile lists the record kernels walk (one per tile span)
     hbec::URec* d_orecs = nullptr;
-    std::vector<hbec::OddStripeRecs> orec_cls;
+    uint32_t* d_lists[hbec::kOddSpans] = {};
+    hbec::OddStripeRecs orecs;
 };
 
 namespace {
@@ -79,45 +80,35 @@ void add_urecs(std::vector<hbec::URec>& recs, std::vector<hbec::URec>& erecs, st
     if (span > 0) orecs.push_back({ua, ub, s, 0});
 }
 
-// Per-stripe record classes: the stripes sorted by length and cut into runs
-// whose tile counts (992-B windows) stay within 1/32 of the run's shortest;
-// more than kOddRecClasses runs: no record path (orecs cleared).
-#ifndef HBEC_ODD_REC_CLASSES
-#define HBEC_ODD_REC_CLASSES 8
-#endif
-constexpr size_t kOddRecClasses = HBEC_ODD_REC_CLASSES;
-
-uint64_t rec_tiles(uint64_t s) { return (s + 32u + 991u) / 992u; }
-
-std::vector<std::pair<size_t, size_t>> group_orecs(std::vector<hbec::URec>& orecs) {
-    std::stable_sort(orecs.begin(), orecs.end(),
-                     [](const hbec::URec& x, const hbec::URec& y) { return x.shard_len < y.shard_len; });
-    std::vector<std::pair<size_t, size_t>> cls;
-    for (size_t i = 0; i < orecs.size();) {
-        const uint64_t t0 = rec_tiles(orecs[i].shard_len);
-        size_t j = i + 1;
-        while (j < orecs.size() && rec_tiles(orecs[j].shard_len) * 32 <= t0 * 33) ++j;
-        cls.emplace_back(i, j - i);
-        i = j;
-        if (cls.size() > kOddRecClasses) {
-            orecs.clear();
-            cls.clear();
-            break;
+// Tile lists of the per-stripe records: for each record-kernel tile span,
+// tile t of stripe e for t < ceil((S_e + 32) / span), stripe by stripe.
+int build_tile_lists(hbec_plan* p, const std::vector<hbec::URec>& orecs) {
+    p->orecs = hbec::OddStripeRecs{};
+    if (orecs.empty()) return HBEC_OK;
+    uint32_t spans[hbec::kOddSpans];
+    hbec::odd_plan_spans(spans);
+    uint64_t s_max = 0;
+    for (const auto& r : orecs) s_max = std::max<uint64_t>(s_max, r.shard_len);
+    for (int i = 0; i < hbec::kOddSpans; ++i) {
+        std::vector<uint32_t> l;
+        for (size_t e = 0; e < orecs.size(); ++e) {
+            const uint64_t nt = (orecs[e].shard_len + 32u + spans[i] - 1) / spans[i];
+            for (uint64_t t = 0; t < nt; ++t) {
+                l.push_back((uint32_t)e);
+                l.push_back((uint32_t)t);
+            }
         }
+        if (l.size() / 2 >= (1ull << 31)) return fail(HBEC_ERR_INVALID_ARG, "plan too large (>= 2^31 record tiles)");
+        hipError_t e = hipMalloc(reinterpret_cast<void**>(&p->d_lists[i]), l.size() * 4);
+        if (e != hipSuccess) return hip_fail(e, "hipMalloc plan tile list");
+        e = hipMemcpy(p->d_lists[i], l.data(), l.size() * 4, hipMemcpyHostToDevice);
+        if (e != hipSuccess) return hip_fail(e, "hipMemcpy plan tile list");
+        p->orecs.lists[i] = hbec::OddTileList{spans[i], p->d_lists[i], l.size() / 2};
     }
-    return cls;
-}
-
-void set_orecs(hbec_plan* p, const std::vector<hbec::URec>& orecs, const std::vector<std::pair<size_t, size_t>>& cls) {
-    p->orec_cls.clear();
-    for (const auto& c : cls) {
-        hbec::OddStripeRecs o;
-        o.recs = p->d_orecs + c.first;
-        o.n = c.second;
-        o.s_min = orecs[c.first].shard_len;
-        o.s_max = orecs[c.first + c.second - 1].shard_len;
-        p->orec_cls.push_back(o);
-    }
+    p->orecs.recs = p->d_orecs;
+    p->orecs.n = orecs.size();
+    p->orecs.s_max = s_max;
+    return HBEC_OK;
 }
 
 template <class T>
@@ -134,19 +125,22 @@ int upload(const std::vector<T>& recs, T** dst, const char* what) {
     return HBEC_OK;
 }
 
-// One pass of a plan over per-stripe records: the records of every class in
-// one launch (the classes are consecutive runs of the same record array;
-// stream-ordered scratch), then one gf_odd_rec launch per class with that
-// class's longest tile count.
-int odd_stripe_rec_pass(int K, int R, int mode, const hbec::UPlanArgs& a, const hbec::OddStripeRecs* cls,
-                        int n_cls, int cus, int max_blocks, hipStream_t stream) {
+// One pass of a plan over per-stripe records: the records of every stripe in
+// one launch (stream-ordered scratch), then one gf_odd_rec launch over the
+// tile list of the span the pass's kernel uses.
+int odd_stripe_rec_pass(int K, int R, int mode, const hbec::UPlanArgs& a, const hbec::OddStripeRecs& o, int cus,
+                        int max_blocks, hipStream_t stream) {
     const uint64_t rw = hbec::odd_rec_words(K, R, mode);
-    uint64_t n_all = 0;
-    for (int c = 0; c < n_cls; ++c) n_all += cls[c].n;
+    const int xs = hbec::odd_bp_schedule(K, R, mode, a.tab, true);
+    const uint32_t span = hbec::odd_rec_tile_span(K, mode, xs);
+    const hbec::OddTileList* tl = nullptr;
+    for (const auto& l : o.lists)
+        if (l.span == span) tl = &l;
+    if (!tl || !tl->d) return fail(HBEC_ERR_INVALID_ARG, "plan has no tile list for this pass");
     uint32_t* recs = nullptr;
-    int rc = hbec::scratch_alloc(n_all * rw * 4, stream, reinterpret_cast<void**>(&recs));
+    int rc = hbec::scratch_alloc(o.n * rw * 4, stream, reinterpret_cast<void**>(&recs));
     if (rc) return rc;
-    hipError_t e = hbec::launch_odd_planrec(K, R, mode, a, cls[0].recs, (uint32_t)n_all, recs, stream);
+    hipError_t e = hbec::launch_odd_planrec(K, R, mode, a, o.recs, (uint32_t)o.n, recs, stream);
     if (e != hipSuccess) {
         hbec::scratch_free(recs, stream);
         return hip_fail(e, "launch gf_odd_planrec");
@@ -154,23 +148,17 @@ int odd_stripe_rec_pass(int K, int R, int mode, const hbec::UPlanArgs& a, const 
     hbec::PassArgs c;
     std::memset(&c, 0, sizeof(c));
     std::memcpy(c.tab, a.tab, sizeof(c.tab));
-    const int xs = hbec::odd_bp_schedule(K, R, mode, a.tab, true);
-    uint64_t first = 0;
-    for (int k = 0; k < n_cls && e == hipSuccess; ++k) {
-        const hbec::OddStripeRecs& o = cls[k];
-        const uint64_t tpo = hbec::odd_tiles_per_obj(K, mode, o.s_max, true, xs);
-        c.n_obj = o.n;
-        c.shard_len = o.s_max;
-        c.tiles_per_obj = (uint32_t)tpo;
-        c.n_tiles = (uint32_t)(o.n * tpo);
-        const uint64_t wpb = hbec::odd_waves_per_block(xs);
-        const uint64_t want = (c.n_tiles + wpb - 1) / wpb;
-        uint64_t cap = (uint64_t)cus * (uint64_t)hbec::odd_blocks_per_cu(mode, K, R, false, true, xs);
-        if (max_blocks > 0) cap = std::min<uint64_t>(cap, (uint64_t)max_blocks);
-        const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, cap));
-        e = hbec::launch_odd(K, R, mode, c, nullptr, recs + first * rw, grid, stream, xs);
-        first += o.n;
-    }
+    c.n_obj = o.n;
+    c.shard_len = o.s_max;
+    c.tiles_per_obj = 1;
+    c.n_tiles = (uint32_t)tl->n;
+    c.list = tl->d;
+    const uint64_t wpb = hbec::odd_waves_per_block(xs);
+    const uint64_t want = (c.n_tiles + wpb - 1) / wpb;
+    uint64_t cap = (uint64_t)cus * (uint64_t)hbec::odd_blocks_per_cu(mode, K, R, false, true, xs);
+    if (max_blocks > 0) cap = std::min<uint64_t>(cap, (uint64_t)max_blocks);
+    const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, cap));
+    e = hbec::launch_odd(K, R, mode, c, nullptr, recs, grid, stream, xs);
     hbec::scratch_free(recs, stream);
     if (e != hipSuccess) return hip_fail(e, "launch gf_odd_rec (plan)");
     return HBEC_OK;
@@ -184,7 +172,7 @@ int odd_stripe_rec_pass(int K, int R, int mode, const hbec::UPlanArgs& a, const 
 int hbec::launch_unaligned_passes(const URec* recs, uint64_t n_recs, const std::vector<int>& in_idx,
                                   const std::vector<int>& out_idx, const std::vector<uint8_t>& rows, int sel_k,
                                   hipStream_t stream, int max_blocks, const URec* erecs, uint64_t n_erecs,
-                                  bool mirror, bool round2, const OddStripeRecs* orecs, int n_orec_cls) {
+                                  bool mirror, bool round2, const OddStripeRecs* orecs) {
     const int K_all = (int)in_idx.size(), R_all = (int)out_idx.size();
     if ((n_recs == 0 && n_erecs == 0) || R_all == 0) return HBEC_OK;
     if (mirror && (!hbec::odd_enabled() || sel_k > 0 || round2))
@@ -195,20 +183,8 @@ int hbec::launch_unaligned_passes(const URec* recs, uint64_t n_recs, const std::
     e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (e != hipSuccess) return hip_fail(e, "hipDeviceGetAttribute");
     if (hbec::odd_enabled() && !round2) {
-        // per-stripe records, one launch per class of stripes whose tile
-        // counts are within 1/32 of the class's longest (the shorter stripes'
-        // extra tiles store nothing), when every class passes for every pass
-        bool use_orecs = orecs && n_orec_cls > 0 && !mirror;
-        for (int c = 0; c < n_orec_cls && use_orecs; ++c) {
-            const OddStripeRecs& o = orecs[c];
-            for (int c0 = 0; c0 < K_all && use_orecs; c0 += hbec::kOddMaxK) {
-                const int K = std::min(hbec::kOddMaxK, K_all - c0), mode = c0 > 0 ? 1 : 0;
-                if (K * std::min(hbec::kMaxR, R_all) < HBEC_ODD_PLAN_REC_MINKR) use_orecs = false;
-                const uint64_t t_max = hbec::odd_tiles_per_obj(K, mode, o.s_max, true);
-                const uint64_t t_min = hbec::odd_tiles_per_obj(K, mode, o.s_min, true);
-                use_orecs = use_orecs && t_max * 32 <= t_min * 33 && o.n * t_max < (1ull << 31);
-            }
-        }
+        // per-stripe records over the plan's tile lists (unmirrored plans)
+        const bool use_orecs = orecs && orecs->n > 0 && !mirror;
         // gf_odd_plan: launches of <= 4 outputs x <= kOddMaxK inputs, later input
         // launches accumulating; one 4-wave block per CU
         for (int r0 = 0; r0 < R_all; r0 += hbec::kMaxR) {
@@ -251,7 +227,7 @@ int hbec::launch_unaligned_passes(const URec* recs, uint64_t n_recs, const std::
                 const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, cap));
                 const int mode = c0 > 0 ? 1 : 0;
                 if (use_orecs) {
-                    int rc = odd_stripe_rec_pass(K, R, mode, a, orecs, n_orec_cls, cus, max_blocks, stream);
+                    int rc = odd_stripe_rec_pass(K, R, mode, a, *orecs, cus, max_blocks, stream);
                     if (rc) return rc;
                 } else if (n_recs > 0) {
                     e = hbec::launch_odd_plan(K, R, mode, a, grid, stream);
@@ -427,8 +403,7 @@ int run_plan(const hbec_plan* p, const std::vector<int>& in_idx, const std::vect
     // with k > 8 every object is in the unaligned records (hbec_plan_objects)
     const int sel_k = p->objects ? p->k : 0;
     int rc = hbec::launch_unaligned_passes(p->d_urecs, p->n_urecs, in_idx, out_idx, rows, sel_k, stream, 0,
-                                           p->d_erecs, p->n_erecs, false, false, p->orec_cls.data(),
-                                           (int)p->orec_cls.size());
+                                           p->d_erecs, p->n_erecs, false, false, &p->orecs);
     if (rc || p->n_brecs == 0) return rc;
     return hbec::launch_unaligned_passes(p->d_brecs, p->n_brecs, in_idx, out_idx, rows, sel_k, stream, 0, nullptr, 0,
                                          false, true);
@@ -488,16 +463,12 @@ int hbec_plan_stripes(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n,
         int urc = upload(urecs, &p->d_urecs, "plan unaligned records");
         if (!urc) urc = upload(erecs, &p->d_erecs, "plan edge records");
         if (!urc) urc = upload(brecs, &p->d_brecs, "plan large-shard records");
-        const auto cls = group_orecs(orecs);
         if (!urc) urc = upload(orecs, &p->d_orecs, "plan stripe records");
+        if (!urc) urc = build_tile_lists(p.get(), orecs);
         if (urc) {
-            if (p->d_tiles) (void)hipFree(p->d_tiles);
-            if (p->d_urecs) (void)hipFree(p->d_urecs);
-            if (p->d_erecs) (void)hipFree(p->d_erecs);
-            if (p->d_brecs) (void)hipFree(p->d_brecs);
+            hbec_plan_free(p.release());
             return urc;
         }
-        set_orecs(p.get(), orecs, cls);
         p->n_urecs = urecs.size();
         p->n_erecs = erecs.size();
         p->n_brecs = brecs.size();
@@ -564,16 +535,12 @@ int hbec_plan_objects(hbec_codec* codec, const hbec_object* objects, uint64_t n,
         int urc = upload(urecs, &p->d_urecs, "plan unaligned records");
         if (!urc) urc = upload(erecs, &p->d_erecs, "plan edge records");
         if (!urc) urc = upload(brecs, &p->d_brecs, "plan large-shard records");
-        const auto cls = group_orecs(orecs);
         if (!urc) urc = upload(orecs, &p->d_orecs, "plan stripe records");
+        if (!urc) urc = build_tile_lists(p.get(), orecs);
         if (urc) {
-            if (p->d_tiles) (void)hipFree(p->d_tiles);
-            if (p->d_urecs) (void)hipFree(p->d_urecs);
-            if (p->d_erecs) (void)hipFree(p->d_erecs);
-            if (p->d_brecs) (void)hipFree(p->d_brecs);
+            hbec_plan_free(p.release());
             return urc;
         }
-        set_orecs(p.get(), orecs, cls);
         p->n_urecs = urecs.size();
         p->n_erecs = erecs.size();
         p->n_brecs = brecs.size();
@@ -589,6 +556,8 @@ void hbec_plan_free(hbec_plan* plan) {
     if (plan->d_erecs) (void)hipFree(plan->d_erecs);
     if (plan->d_brecs) (void)hipFree(plan->d_brecs);
     if (plan->d_orecs) (void)hipFree(plan->d_orecs);
+    for (uint32_t* l : plan->d_lists)
+        if (l) (void)hipFree(l);
     delete plan;
 }
 

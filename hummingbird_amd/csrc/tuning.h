@@ -106,9 +106,6 @@
 #ifndef HBEC_ODD_LDS_MINK
 #define HBEC_ODD_LDS_MINK 9  // record kernels: coefficient tables in LDS from K = 9 (12+4 encode 51 -> 57 %; from K = 5, 8+3 lost 5 %)
 #endif
-#ifndef HBEC_ODD_PLAN_REC_MINKR
-#define HBEC_ODD_PLAN_REC_MINKR 0  // plans: per-stripe records (gf_odd_planrec + gf_odd_rec) from K R >= this
-#endif
 #ifndef HBEC_ODD_BP_BPC
 #define HBEC_ODD_BP_BPC 1  // blocks per CU (launch bounds and grid) of the bit-plane record kernels
 #endif
@@ -132,6 +129,9 @@
 #endif
 #ifndef HBEC_ODD_REC_LOAD_ORDER
 #define HBEC_ODD_REC_LOAD_ORDER 1  // record kernels' tile loads: 1 input-major (a shard's windows together), 0 window-major
+#endif
+#ifndef HBEC_ODD_VERIFY_KEEP
+#define HBEC_ODD_VERIFY_KEEP 0  // odd Verify: 1 = plain (L2-retained) loads instead of non-temporal
 #endif
 #ifndef HBEC_ODD_BPC_APPLY
 #define HBEC_ODD_BPC_APPLY 1  // blocks per CU of the strided / plan apply grids (register-bound shapes: odd_two_blocks)

@@ -9,7 +9,7 @@ for r in 0 1 2; do
     IFS=: read -r lib envs <<< "$spec"
     envarr=()
     [ -n "${envs:-}" ] && IFS=: read -ra envarr <<< "$envs"
-    env "${envarr[@]}" AB_ROUND=$r HBEC_LIB=$lib AB_LABEL="$spec" timeout -k 10 200 python scripts/odd_sq.py 15 2048 "$shapes" >> "$out" 2>> "${out%.jsonl}.err" || exit $?
+    env "${envarr[@]}" AB_ROUND=$r HBEC_LIB=$lib AB_LABEL="$spec" timeout -k 10 200 python scripts/odd_sq.py 15 ${AB_N:-2048} "$shapes" >> "$out" 2>> "${out%.jsonl}.err" || exit $?
   done
 done
 python - "$out" <<'PY'

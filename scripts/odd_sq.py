@@ -81,13 +81,21 @@ def main():
                        "o83": (8, 3, 131071, "enc"), "r83": (8, 3, 131071, "rec"), "v83": (8, 3, 131071, "ver"),
                        "o104": (10, 4, 104858, "enc"), "o124": (12, 4, 87389, "enc"), "r104": (10, 4, 104858, "rec"), "p124": (12, 4, 87392, "plan"), "p42": (4, 2, 262143, "plan"), "p83": (8, 3, 131071, "plan"), "p104": (10, 4, 104858, "plan"),
                        "v328": (32, 8, 32771, "ver"), "v104": (10, 4, 104858, "ver"), "v124": (12, 4, 87389, "ver"),
-                       "v32": (3, 2, 349525, "ver"), "v63": (6, 3, 174763, "ver"), "o63": (6, 3, 174763, "enc"), "o73": (7, 3, 149797, "enc"), "o62": (6, 2, 174763, "enc"), "o82": (8, 2, 131071, "enc"), "o84": (8, 4, 131071, "enc"), "o93": (9, 3, 116509, "enc"), "p63": (6, 3, 174763, "plan"), "p73": (7, 3, 149797, "plan"), "p42b": (4, 2, 262141, "plan"), "c42": (4, 2, 262143, "cplan"), "c83": (8, 3, 131071, "cplan"), "c104": (10, 4, 104858, "cplan")}[name]
+                       "v32": (3, 2, 349525, "ver"), "v63": (6, 3, 174763, "ver"), "o63": (6, 3, 174763, "enc"), "o73": (7, 3, 149797, "enc"), "o62": (6, 2, 174763, "enc"), "o82": (8, 2, 131071, "enc"), "o84": (8, 4, 131071, "enc"), "o93": (9, 3, 116509, "enc"), "p63": (6, 3, 174763, "plan"), "p73": (7, 3, 149797, "plan"), "p42b": (4, 2, 262141, "plan"), "c42": (4, 2, 262143, "cplan"), "c83": (8, 3, 131071, "cplan"), "c104": (10, 4, 104858, "cplan"),
+                       # random sizes (the nursery batch shape): object plans of n objects, S uniform in
+                       # [4 KiB / k, 1 MiB / k], odd
+                       "x42": (4, 2, 0, "rplan"), "x83": (8, 3, 0, "rplan"), "x104": (10, 4, 0, "rplan"), "x124": (12, 4, 0, "rplan")}[name]
         enc = RS.New(k, m)
         row = {"lib": os.environ.get("HBEC_LIB", "default"), "label": os.environ.get("AB_LABEL", ""), "round": int(os.environ.get("AB_ROUND", "0")),
                "shape": name, "k": k, "m": m, "S": s, "n": n, "op": op}
-        if op == "cplan":
+        if op == "rplan":
+            rng = __import__("numpy").random.default_rng(0x48424543 + k * 100 + m)
+            sizes = [int(x) | 1 for x in rng.integers(4096 // k, (1 << 20) // k + 1, n)]
+            row["S"] = "random"
+        if op in ("cplan", "rplan"):
+            if op == "cplan":
+                sizes = [s if i % 2 else max(17, s // 256 + 7) for i in range(n)]
             # object plan of two size classes, alternating: ~4 KiB and ~1 MiB objects, odd S
-            sizes = [s if i % 2 else max(17, s // 256 + 7) for i in range(n)]
             d = torch.empty(sum(k * x for x in sizes), dtype=torch.uint8, device="cuda")
             B.fill_splitmix(d.view(1, -1), d.numel())
             par = torch.empty(sum(m * x for x in sizes), dtype=torch.uint8, device="cuda")
