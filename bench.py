@@ -116,7 +116,7 @@ def kernel_sources_sha256(sources=KERNEL_SOURCES) -> str:
 # collected on exactly these sources (pmc_summary.py records both hashes).
 ODD_SOURCES = ("hummingbird_amd/csrc/odd.hip", "hummingbird_amd/csrc/odd_impl.h", "hummingbird_amd/csrc/gf_device.h",
                "hummingbird_amd/csrc/kernels.h", "hummingbird_amd/csrc/odd_k58.hip", "hummingbird_amd/csrc/odd_k912.hip",
-               "hummingbird_amd/csrc/tuning.h")
+               "hummingbird_amd/csrc/tuning.h", "hummingbird_amd/csrc/odd_bp.hip", "hummingbird_amd/csrc/xor_sched.h")
 
 
 def load_pmc(prefix_glob="profiles/r[0-9][0-9]_pmc.json"):
@@ -420,12 +420,17 @@ def small_objects(n=65536, obj_len=4096, reps=100, settle=200):
     return out
 
 
-def _odd_kernel_traffic(kern, k, r, mode):
+def _odd_kernel_traffic(kern, k, r, mode, plan=False):
     """PMC bytes per launch of the odd-shard kernel coding (k, r, mode), by the
-    name it runs under (gf_odd_rec for strided batches, gf_odd before)."""
-    for name in (f"gf_odd_rec<{k}, {r}, {mode}>", f"gf_odd<{k}, {r}, {mode}>"):
-        if name in kern:
-            return name, kern[name].get("hbm_bytes_per_launch")
+    name it runs under: gf_odd_rec<k, r, mode, XS, LIST> (XS: the bit-plane
+    schedule or -1, LIST: plans' tile-list instance) or gf_odd<k, r, mode>."""
+    pre = (f"gf_odd_rec<{k}, {r}, {mode}, ",)
+    for name, v in sorted(kern.items()):
+        if name.startswith(pre) and name.endswith("true>" if plan else "false>"):
+            return name, v.get("hbm_bytes_per_launch")
+    name = f"gf_odd<{k}, {r}, {mode}>"
+    if not plan and name in kern:
+        return name, kern[name].get("hbm_bytes_per_launch")
     return None, None
 
 
@@ -504,6 +509,74 @@ def odd_objects(n=4096):
     if not fresh:
         out["traffic_note"] = "no PMC summary collected on this tree's odd-kernel sources"
     out["parity_ok"] = out["parity_ok"] and all(v["parity_ok"] for v in out["shapes"].values())
+    return out
+
+
+def random_objects(n=4096, shapes=((4, 2), (8, 3)), reps=20, settle=40):
+    """The nursery stabilizer's batch shape: a scan hands
+    over the oldest nursery objects whatever their sizes (indexdb.go:26,548-557,
+    ecengine.go:583-640), so S = ceil(len / k) (ecutils.go:14-24) takes many
+    values.  n objects with seeded shard lengths uniform in [4 KiB / k,
+    1 MiB / k], odd, as ONE object plan (data arena + parity arena,
+    hbec_plan_objects): per-stripe records over the plan's tile list, one
+    launch per pass.  Encode is timed; every object is then checked with the
+    product's Verify (a different kernel family), and the -m gpu test
+    (tests/test_gpu_random_plan.py) compares every object with the oracle.
+    HBM traffic per launch from the committed PMC summary (main + edge +
+    record kernels) when it was collected on these sources."""
+    pmc_files = sorted(glob.glob(str(ROOT / "profiles/r[0-9][0-9]_pmc.json")))
+    pmc = json.loads(Path(pmc_files[-1]).read_text()) if pmc_files else {}
+    fresh = pmc.get("odd_sources_sha256") == kernel_sources_sha256(ODD_SOURCES)
+    stream = torch.cuda.current_stream()
+    out = {"workload": f"{n} objects, shard length uniform in [4 KiB/k, 1 MiB/k] and odd (seeded), one object "
+                       "plan per shape, Encode, device-resident", "shapes": {}}
+    for k, m in shapes:
+        rng = __import__("numpy").random.default_rng(0x48424543 + 100 * k + m)
+        sizes = [int(x) | 1 for x in rng.integers(4096 // k, (1 << 20) // k + 1, n)]
+        data = torch.empty(sum(k * s for s in sizes), dtype=torch.uint8, device="cuda")
+        B.fill_splitmix(data.view(1, -1), data.numel(), first=11 * k + m)
+        parity = torch.empty(sum(m * s for s in sizes), dtype=torch.uint8, device="cuda")
+        objs, do, po = [], 0, 0
+        for s in sizes:
+            objs.append((data.data_ptr() + do, parity.data_ptr() + po, s))
+            do += k * s
+            po += m * s
+        enc = RS.New(k, m)
+        plan = B.StripePlan(enc, objects=objs)
+        for _ in range(settle):
+            plan.encode()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            plan.encode()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        nbytes = sum((k + m) * s for s in sizes)
+        gbs = nbytes / (ms * 1e-3) / 1e9
+        flags = torch.zeros(1, dtype=torch.int32, device="cuda")
+        bad = 0
+        for (a_, b_, s) in objs:
+            views = [(a_ + j * s, 0) for j in range(k)] + [(b_ + r * s, 0) for r in range(m)]
+            B.verify_views(enc, views, 1, s, flags)
+        torch.cuda.synchronize()
+        bad = int(flags.item())
+        leg = {"objects": n, "bytes": nbytes, "ms": round(ms, 4), "GB_s": round(gbs, 1),
+               "frac": round(gbs / HBM_PEAK_GBS, 4), "parity_ok": bad == 0}
+        if fresh:
+            kern = pmc.get("kernels", {})
+            kname, t = _odd_kernel_traffic(kern, k, m, 0, plan=True)
+            extra = sum((kern.get(x, {}).get("hbm_bytes_per_launch") or 0)
+                        for x in ("gf_odd_edges_plan<0>", "gf_odd_planrec"))
+            if t is not None:
+                leg["kernel"] = kname
+                leg["traffic"] = int(t + extra)
+                leg["traffic_ratio"] = round((t + extra) / nbytes, 4)
+        out["shapes"][f"{k}+{m}"] = leg
+        del plan, data, parity, flags
+        torch.cuda.empty_cache()
+    out["traffic_source"] = os.path.relpath(pmc_files[-1], ROOT) if (pmc_files and fresh) else None
+    out["parity_ok"] = all(v["parity_ok"] for v in out["shapes"].values())
     return out
 
 
@@ -840,6 +913,10 @@ def main(argv=None):
             line["odd_objects"] = odd_objects()
         except Exception as e:  # noqa: BLE001 - reported; never blocks the other ranks
             line["odd_objects"] = {"error": f"{type(e).__name__}: {e}"[:200]}
+        try:
+            line["random_objects"] = random_objects()
+        except Exception as e:  # noqa: BLE001 - reported; never blocks the other ranks
+            line["random_objects"] = {"error": f"{type(e).__name__}: {e}"[:200]}
     if world > 1 and backend == "nccl" and args.split_objects > 0:
         split = batch_split(pg, k, m, obj_len, args.split_objects, world, rank, ctl_device)
         if rank == 0:

@@ -177,20 +177,14 @@ static int odd_launches(const PassArgs& a, int K, int R, int mode, bool accumula
             const bool use_rec = xs >= 0 || ((m != 2 || K1 > 8) && odd_uses_records(K1, R));
             const uint64_t tpo = odd_tiles_per_obj(K1, m, shard_len, use_rec, xs);
             const uint64_t max_obj = std::max<uint64_t>(1, std::min<uint64_t>((1ull << 31), g_chunk_tiles) / tpo);
-            // per-object records of this pass (stream-ordered scratch, freed after its launches)
+            // per-object records of one launch's objects (stream-ordered
+            // scratch of at most max_obj records, rebuilt per launch, freed
+            // after the pass): device memory bounded by the chunk, not the batch
             uint32_t* recs = nullptr;
             const uint64_t rw = odd_rec_words(K1, R, m);
             if (use_rec) {
-                rc = scratch_alloc(n_obj * rw * 4, stream, reinterpret_cast<void**>(&recs));
+                rc = scratch_alloc(std::min(n_obj, max_obj) * rw * 4, stream, reinterpret_cast<void**>(&recs));
                 if (rc) return rc;
-                PassArgs p = b;
-                p.n_obj = n_obj;
-                p.shard_len = shard_len;
-                hipError_t e = launch_odd_objrec(K1, R, m, p, recs, stream);
-                if (e != hipSuccess) {
-                    scratch_free(recs, stream);
-                    return hip_fail(e, "launch gf_odd_objrec");
-                }
             }
             for (uint64_t o0 = 0; o0 < n_obj; o0 += max_obj) {
                 const uint64_t no = std::min(max_obj, n_obj - o0);
@@ -199,6 +193,13 @@ static int odd_launches(const PassArgs& a, int K, int R, int mode, bool accumula
                 for (int r = 0; r < R; ++r) c.out[r] = b.out[r] + o0 * b.out_stride[r];
                 c.n_obj = no;
                 c.shard_len = shard_len;
+                if (use_rec) {
+                    hipError_t e = launch_odd_objrec(K1, R, m, c, recs, stream);
+                    if (e != hipSuccess) {
+                        scratch_free(recs, stream);
+                        return hip_fail(e, "launch gf_odd_objrec");
+                    }
+                }
                 c.tiles_per_obj = (uint32_t)tpo;
                 c.n_tiles = (uint32_t)(no * tpo);
                 const uint64_t wpb = odd_waves_per_block(xs);
@@ -206,8 +207,7 @@ static int odd_launches(const PassArgs& a, int K, int R, int mode, bool accumula
                 const uint64_t cap = (uint64_t)cus * (uint64_t)odd_blocks_per_cu(m, K1, R, false, use_rec, xs);
                 int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, cap));
                 if (g_grid_cap > 0) grid = std::min(grid, g_grid_cap);
-                hipError_t e = launch_odd(K1, R, m, c, flags ? flags + o0 : nullptr, recs ? recs + o0 * rw : nullptr, grid,
-                                          stream, xs);
+                hipError_t e = launch_odd(K1, R, m, c, flags ? flags + o0 : nullptr, recs, grid, stream, xs);
                 if (e != hipSuccess) {
                     scratch_free(recs, stream);
                     return hip_fail(e, "launch gf_odd");
@@ -1019,8 +1019,7 @@ static int verify_wide(const hbec_view* views, int k, int m, const uint8_t* prow
                          });
 }
 
-// Apply of k > 8 inputs at any alignment in one pass (gf_wide apply):
-// HBEC_WIDE_APPLY=0 keeps the round-2 kernels (passes of <= 16 inputs).
+// Apply of k > 16 inputs at any alignment in one pass (gf_wide apply).
 
 static int apply_wide(int rows, int cols, const uint8_t* coeffs, const hbec_view* in, const hbec_view* out,
                       uint64_t n_obj, uint64_t shard_len, hipStream_t stream) {
@@ -1132,10 +1131,14 @@ static int verify_views(hbec_codec* c, const hbec_view* views, uint64_t n_obj, u
         }
         return HBEC_OK;
     }
-    // k <= 12: gf_odd verify (9 <= k <= 12: the record kernel with LDS tables,
-    // 10+4 54.1 -> 64.5 %, 12+4 45.7 -> 53.6 % over gf_verify_wide,
-    // profiles/r04_ab_odd.jsonl batch N); above, gf_verify_wide
-    if (odd_enabled() && k <= kOddMaxK && pos32_shard(shard_len)) {
+    // k <= 8: gf_odd verify; 9 <= k <= 12 with 3 or 4 parity rows: the record
+    // kernel with LDS tables in one pass (10+4 54.1 -> 64.5 %, 12+4 45.7 ->
+    // 53.6 % over gf_verify_wide, profiles/r04_ab_odd.jsonl batch N).  Other
+    // 9 <= k <= 12 shapes (1-2 rows: the register-table gf_odd, m > 4: the
+    // data read once per 4 rows) and k > 12 take gf_verify_wide, one
+    // read-only pass per <= 8 rows.
+    const bool odd_verify = k <= 8 || (k <= kOddMaxK && m >= 3 && m <= kMaxR);
+    if (odd_enabled() && odd_verify && pos32_shard(shard_len)) {
         // any alignment: recompute and compare in one pass (gf_odd verify), <= 4 rows per launch
         int dev = 0;
         int rc = current_device(&dev);

@@ -358,7 +358,7 @@ int zero_copy_blocks_per_cu() {
 }
 
 // Pinned stripes that are not 16-B aligned (or S % 16 != 0): zero-copy through
-// the unaligned kernel (default) or, with HBEC_ZC_UNALIGNED=0, the staged ring.
+// the unaligned kernel (a tuning build's HBEC_ZC_UNALIGNED=0: the staged ring).
 bool zero_copy_unaligned_enabled() {
     static const bool on = hbec::tune_knob("HBEC_ZC_UNALIGNED", 1) != 0;
     return on;

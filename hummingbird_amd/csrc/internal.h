@@ -49,7 +49,7 @@ void scratch_free(void* p, hipStream_t stream);
 // HBEC_ZEROCOPY=0).  The zero-copy host paths code such memory in place.
 uint64_t pinned_device_addr(const void* p, uint64_t len);
 // Pinned stripes at any alignment / shard length are coded in place over PCIe
-// (the gf_odd plan kernel) unless HBEC_ZC_UNALIGNED=0.
+// (the gf_odd plan kernel; a tuning build's HBEC_ZC_UNALIGNED=0 stages them).
 bool zero_copy_any_alignment();
 
 // ShardHash of a list of device chains: records {addr, len, slot, 0} (32 B

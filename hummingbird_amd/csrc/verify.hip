@@ -259,8 +259,8 @@ hipError_t verify_occupancy(int k, int r, int* blocks_per_cu) {
 int verify_tile_bytes(int k) { return verify_u(k) * 1024; }
 
 // Shards shorter than max(one verify tile, 2 KiB) take the packed verify
-// (HBEC_VERIFY_PACKED=0 turns it off for A/B; HBEC_VERIFY_PACKED_MAX_SHARD=B
-// moves the threshold).
+// (tuning builds, HBEC_TUNE=1, only: HBEC_VERIFY_PACKED=0 turns it off for
+// A/B, HBEC_VERIFY_PACKED_MAX_SHARD=B moves the threshold).
 static const bool g_verify_packed_on = tune_knob("HBEC_VERIFY_PACKED", 1) != 0;
 static const uint64_t g_verify_packed_max = (uint64_t)std::max(0LL, tune_knob("HBEC_VERIFY_PACKED_MAX_SHARD", 0));
 
