@@ -302,7 +302,7 @@ bool odd_enabled() {
 int odd_blocks_per_cu(int mode, int k, int r, bool mirror, bool records, int xs) {
     static const int v = (int)tune_knob("HBEC_ODD_BPC", 0);
     if (v > 0) return v;
-    if (xs >= 0) return HBEC_ODD_BP_BPC;  // launch bounds sized for it (odd_rec_lb)
+    if (xs >= 0) return odd_bp_bpc(k, r, mode);  // launch bounds sized for it (odd_rec_lb)
     if (mode == kOddVerify) return HBEC_ODD_BPC_VERIFY;
     if (records && odd_rec_two_blocks(k, r, mode)) return 2;  // launch bounds sized for it (odd_rec_lb)
     return odd_two_blocks(k, r, mode, mirror) ? 2 : HBEC_ODD_BPC_APPLY;  // launch bounds sized for it (odd_lb)
@@ -338,12 +338,13 @@ void odd_plan_spans(uint32_t (&spans)[kOddSpans]) {
 }
 
 uint32_t odd_rec_tile_span(int k, int mode, int xs) {
+    if (xs >= 0 && mode == kOddVerify) return (64u * odd_bp_u() - 1u) * 16u;  // chained windows (VCHAIN)
     return xs >= 0 ? odd_rec_span(odd_bp_u(), mode) : odd_rec_span(odd_u(k, mode), mode);
 }
 
 uint32_t odd_tiles_per_obj(int k, int mode, uint64_t shard_len, bool records, int xs) {
     const uint64_t span = shard_len + 32u;
-    const uint64_t tile = xs >= 0 ? (uint64_t)odd_rec_span(odd_bp_u(), mode)
+    const uint64_t tile = xs >= 0 ? (uint64_t)odd_rec_tile_span(k, mode, xs)
                           : records ? (uint64_t)odd_rec_span(odd_u(k, mode), mode)
                           : mode == kOddVerify ? (odd_u(k, mode) >= 2 ? (uint64_t)(64u * odd_u(k, mode) - 1u) * 16u
                                                                       : (uint64_t)odd_win<kOddVerify>())
@@ -358,10 +359,11 @@ int odd_bp_schedule(int k, int r, int mode, const uint32_t (*tab)[kMaxK][5], boo
     // tuning builds: HBEC_ODD_BP = 0 none, 1 the measured choice (XorShape
     // strided / plan), 2 every compiled schedule
     static const int on = (int)tune_knob("HBEC_ODD_BP", 1);
-    if (!on || mode != kOddApply || k > kOddMaxK || r > kMaxR) return -1;
+    if (!on || mode == kOddAcc || k > kOddMaxK || r > kMaxR) return -1;
     for (int i = 0; i < kXorShapeCount; ++i) {
         const XorShape& x = kXorShapes[i];
-        if (x.k != k || x.R != r || (on == 1 && !(plan ? x.plan : x.strided))) continue;
+        const bool use = mode == kOddVerify ? (!plan && x.verify) : (plan ? x.plan : x.strided);
+        if (x.k != k || x.R != r || (on == 1 && !use)) continue;
         bool eq = true;
         for (int q = 0; q < r && eq; ++q)
             for (int j = 0; j < k && eq; ++j) eq = ((tab[q][j][0] >> 8) & 0xFFu) == x.coef[q][j];  // t[0] byte 1 = c * 1
@@ -377,9 +379,10 @@ hipError_t launch_odd(int k, int r, int mode, const PassArgs& a, uint32_t* flags
     if (!pos32_shard(a.shard_len)) return hipErrorInvalidValue;  // 32-bit shard positions
     g_odd_launches[xs >= 0 ? 0 : (recs ? 1 : 2)].fetch_add(1, std::memory_order_relaxed);
     if (xs >= 0) {
-        if (!recs || mode != kOddApply || xs >= kXorShapeCount || kXorShapes[xs].k != k || kXorShapes[xs].R != r)
+        if (!recs || mode == kOddAcc || xs >= kXorShapeCount || kXorShapes[xs].k != k || kXorShapes[xs].R != r)
             return hipErrorInvalidValue;
-        const void* fn = odd_kernel_bp(xs, a.list != nullptr);
+        const void* fn = odd_kernel_bp(xs, mode, a.list != nullptr);
+        if (!fn) return hipErrorInvalidValue;
         void* args[] = {const_cast<PassArgs*>(&a), &flags, &recs};
         return hipLaunchKernel(fn, dim3(grid), dim3(64 * odd_waves_per_block(xs)), args, 0, stream);
     }

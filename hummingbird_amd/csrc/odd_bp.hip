@@ -14,8 +14,16 @@ static const void* odd_bp_pick(int xs, bool list, std::integer_sequence<int, I..
     return xs >= 0 && xs < (int)sizeof...(I) ? (list ? lfns[xs] : fns[xs]) : nullptr;
 }
 
-const void* odd_kernel_bp(int xs, bool list) {
-    return odd_bp_pick(xs, list, std::make_integer_sequence<int, kXorShapeCount>{});
+template <int... I>
+static const void* odd_bp_verify_pick(int xs, std::integer_sequence<int, I...>) {
+    static const void* const fns[] = {(const void*)&gf_odd_rec<XorNet<I>::K, XorNet<I>::R, kOddVerify, I>...};
+    return xs >= 0 && xs < (int)sizeof...(I) ? fns[xs] : nullptr;
+}
+
+const void* odd_kernel_bp(int xs, int mode, bool list) {
+    if (mode == kOddVerify)
+        return list ? nullptr : odd_bp_verify_pick(xs, std::make_integer_sequence<int, kXorShapeCount>{});
+    return mode == kOddApply ? odd_bp_pick(xs, list, std::make_integer_sequence<int, kXorShapeCount>{}) : nullptr;
 }
 
 }  // namespace hbec

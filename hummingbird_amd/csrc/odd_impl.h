@@ -905,6 +905,34 @@ __device__ __forceinline__ void odd_rec_finish(const OddRegs<K, R, U, MODE>& X, 
             }
         }
         return;
+    } else if constexpr (XS >= 0 && MODE == kOddVerify) {
+        // chained bit-plane Verify (VCHAIN in gf_odd_rec)
+        static_assert(U % 2 == 0, "bit-plane column pairs");
+        u32x4 xw[U][K], acc[U][R];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+                xw[u][j] = u + 1 < U ? odd_shift_in_carry(X.x[u][j], sh[j], X.x[u + 1 < U ? u + 1 : u][j])
+                                     : odd_shift_in(X.x[u][j], sh[j]);
+#pragma unroll
+        for (int u = 0; u < U; u += 2) bp_dot2<XS, K, R>(acc[u], acc[u + 1], xw[u], xw[u + 1]);
+        bool bad = false;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t v = t.v0 + 16u * (64u * (uint32_t)u + lane);
+            const bool mine = t.live != 0u && (u + 1 < U || lane < 63u) && (v - odd_w(t.f, 2)) <= odd_w(t.f, 3);
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const u32x4 st = u + 1 < U ? odd_shift_in_carry(X.x[u][K + r], sh[K + r], X.x[u + 1 < U ? u + 1 : u][K + r])
+                                           : odd_shift_in(X.x[u][K + r], sh[K + r]);
+                const u32x4 df = st ^ acc[u][r];
+                bad |= mine && (df[0] | df[1] | df[2] | df[3]) != 0u;
+            }
+        }
+        if (__any(bad)) {
+            if (lane == 0u) atomicOr(flags + t.obj, 1u);
+        }
     } else {
         bool bad = false;
 #pragma unroll
@@ -956,9 +984,14 @@ struct OddPos {
 
 // LDS-table record kernels fit 2 blocks per CU (2 waves per SIMD); the
 // bit-plane kernels (XS >= 0) HBEC_ODD_BP_BPC (tuning.h)
+// bit-plane Verify: 2 blocks per CU (2 waves per SIMD, the read-only
+// kernels' occupancy) where K R <= 27 fits them in 256 VGPRs
+__host__ __device__ constexpr int odd_bp_bpc(int k, int r, int mode) {
+    return mode == kOddVerify && k * r <= 27 ? HBEC_ODD_BPC_VERIFY : HBEC_ODD_BP_BPC;
+}
 template <int K, int R, int MODE, int XS = -1>
 __host__ __device__ constexpr int odd_rec_lb() {
-    return XS >= 0 ? HBEC_ODD_BP_BPC : (odd_rec_two_blocks(K, R, MODE) ? 2 : odd_lb<K, R, MODE>());
+    return XS >= 0 ? odd_bp_bpc(K, R, MODE) : (odd_rec_two_blocks(K, R, MODE) ? 2 : odd_lb<K, R, MODE>());
 }
 // Bit-plane record kernels: the carried 2-window tile (both columns of a
 // lane form one 32-byte plane group), apply only
@@ -984,14 +1017,18 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE, XS>())) 
                                                                                             const uint32_t* __restrict__ recs) {
     using RC = OddRec<K, R, MODE>;
     constexpr bool BP = XS >= 0;
-    static_assert(!BP || MODE == kOddApply, "bit-plane records: apply");
+    static_assert(!BP || MODE != kOddAcc, "bit-plane records: apply and Verify");
     constexpr bool PF = BP ? odd_bp_prefetch<K, R, MODE>() : odd_rec_prefetch<K, R, MODE>();
     constexpr int U = BP ? odd_bp_u() : odd_u(K, MODE);
     constexpr bool CARRY = odd_rec_carry(U, MODE);
+    // bit-plane Verify: U chained windows (window u < U - 1 compares all 64
+    // columns, lane 63 borrowing window u + 1's first dword; the last 63), so
+    // a tile reads only its own 64-B lines but the one it shares with the next
+    constexpr bool VCHAIN = BP && MODE == kOddVerify;
     constexpr bool LDS = !BP && odd_rec_lds(K);
     // input-major loads, except the 3-wave bit-plane blocks (12+4: 61.8 % window-major vs 59.2 %)
     constexpr bool IMAJ = HBEC_ODD_REC_LOAD_ORDER != 0 && !(BP && odd_bp_wpb(K, R) == 3);
-    constexpr uint32_t SPAN = odd_rec_span(U, MODE);
+    constexpr uint32_t SPAN = VCHAIN ? (64u * U - 1u) * 16u : odd_rec_span(U, MODE);
     constexpr uint32_t WPB = BP ? (uint32_t)odd_bp_wpb(K, R) : kPipeBlockThreads / 64;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t nw = gridDim.x * WPB;
@@ -1064,7 +1101,7 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE, XS>())) 
     odd_swait();
     odd_swait_pin(L);
     fill(tx, p);
-    odd_rec_load<K, R, U, MODE, CARRY, IMAJ>(X, L, tx.v0, lane);
+    odd_rec_load<K, R, U, MODE, CARRY || VCHAIN, IMAJ>(X, L, tx.v0, lane);
     odd_rec_sload<PF>(tx.f, rec(p));
     p = step(p);
     odd_rec_sload<PF>(L, rec(p) + RC::FW);
@@ -1076,13 +1113,18 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE, XS>())) 
     auto half = [&](OddRegs<K, R, U, MODE>& Z, OddRT<K, R, MODE>& tz, const OddRegs<K, R, U, MODE>& W,
                     const OddRT<K, R, MODE>& tw) {
         fill(tz, p);
-        odd_rec_load<K, R, U, MODE, CARRY, IMAJ>(Z, L, tz.v0, lane);
+        odd_rec_load<K, R, U, MODE, CARRY || VCHAIN, IMAJ>(Z, L, tz.v0, lane);
         odd_rec_sload<PF>(tz.f, rec(p));
         p = step(p);
         odd_rec_sload<PF>(L, rec(p) + RC::FW);
         if constexpr (LIST) odd_rec_sload2<PF>(pe, lentry(tq + nw));
         if constexpr (BP && HBEC_ODD_BP_SLEEP > 0) __builtin_amdgcn_s_sleep(HBEC_ODD_BP_SLEEP);
-        if constexpr (MODE != kOddVerify && (!BP || HBEC_ODD_BP_BARRIER)) __builtin_amdgcn_s_barrier();
+        // bit-plane Verify at 2 waves per SIMD: a block barrier per tile keeps
+        // the waves sharing tile-boundary lines together (8+3 77.2 -> 78.4 %,
+        // reads 1.054 -> 1.026 x); at one wave per SIMD it costs 10 points
+        if constexpr ((MODE != kOddVerify && (!BP || HBEC_ODD_BP_BARRIER)) ||
+                      (VCHAIN && HBEC_ODD_BP_VBARRIER && odd_bp_bpc(K, R, MODE) >= 2))
+            __builtin_amdgcn_s_barrier();
         odd_rec_finish<K, R, U, MODE, CARRY, XS>(W, tw, a.tab, tb, lane, flags, lt);
         odd_swait();
         odd_swait_pin(L);
@@ -1162,7 +1204,7 @@ static const void* odd_kernel_range(int k, int r, int mode, bool plan, bool mirr
 
 // bit-plane record kernel of kXorShapes[xs] (odd_bp.hip), mode 0; list: the
 // plan tile-list instance
-const void* odd_kernel_bp(int xs, bool list);
+const void* odd_kernel_bp(int xs, int mode, bool list);
 
 // the other translation units' ranges
 const void* odd_kernel_k58(int k, int r, int mode, bool plan, bool mirror, bool variant, bool list);

@@ -118,6 +118,9 @@
 #ifndef HBEC_ODD_BP_BARRIER
 #define HBEC_ODD_BP_BARRIER 1  // one block barrier per tile in the bit-plane record kernels
 #endif
+#ifndef HBEC_ODD_BP_VBARRIER
+#define HBEC_ODD_BP_VBARRIER 1  // bit-plane Verify at 2 blocks per CU: one block barrier per tile (r05_ab_verify.jsonl)
+#endif
 #ifndef HBEC_ODD_BP_WPB
 #define HBEC_ODD_BP_WPB 4  // waves per block of the bit-plane record kernels (one block per CU)
 #endif

@@ -40,13 +40,14 @@ OUT = Path(__file__).resolve().parent / "csrc" / "xor_sched.h"
 # the issue slots (K * R >= 18 and the BASELINE / hec shapes).
 SHAPES = [(6, 3), (7, 3), (8, 3), (8, 4), (9, 3), (10, 4), (12, 4), (6, 2), (8, 2), (4, 2)]
 # Where the bit-plane kernel is the one launched (interleaved A/Bs against the
-# v_perm table kernels, profiles/r05_ab_bitplane.jsonl): strided batches /
-# plans.  The others keep the table kernels there (their schedule is still
+# v_perm table kernels, profiles/r05_ab_bitplane.jsonl, r05_ab_plans_verify.jsonl):
+# strided batches / plans / Verify (the parity rows are the encode matrix).  The others keep the table kernels there (their schedule is still
 # compiled, so a tuning build can A/B it).
-USE = {  # (k, m): (strided, plan)
-    (6, 3): (True, True), (7, 3): (False, False), (8, 3): (False, True), (8, 4): (True, True),
-    (9, 3): (True, True), (10, 4): (True, True), (12, 4): (True, True), (6, 2): (False, True),
-    (8, 2): (False, True), (4, 2): (False, False),
+USE = {  # (k, m): (strided, plan, verify)
+    (6, 3): (True, True, True), (7, 3): (False, False, True), (8, 3): (False, True, True),
+    (8, 4): (True, True, True), (9, 3): (True, True, True), (10, 4): (True, True, True),
+    (12, 4): (True, True, True), (6, 2): (False, True, True), (8, 2): (False, True, True),
+    (4, 2): (False, False, False),
 }
 
 
@@ -258,7 +259,7 @@ def generate(max_temps: int = 10_000) -> str:
            '',
            'struct XorShape {',
            '    int k, m, r0, R;  // shape, first parity row, rows',
-           '    bool strided, plan;  // launched for strided batches / plans (else the table kernels)',
+           '    bool strided, plan, verify;  // launched for strided batches / plans / Verify (else the table kernels)',
            '    uint8_t coef[4][12];  // C[r][j]',
            '};',
            '']
@@ -289,8 +290,8 @@ def generate(max_temps: int = 10_000) -> str:
                         assert got[8 * r + i] == want, (k, m, r0, r, i)
             body += emit_net(sid, k, m, r0, coef, temps, frows)
             cs = ", ".join("{" + ", ".join(str(c) for c in (cr + [0] * (12 - k))) + "}" for cr in coef)
-            st, pl = (str(x).lower() for x in USE[(k, m)])
-            table.append(f"    {{{k}, {m}, {r0}, {len(coef)}, {st}, {pl}, {{{cs}}}}},  // XorNet<{sid}>")
+            st, pl, ve = (str(x).lower() for x in USE[(k, m)])
+            table.append(f"    {{{k}, {m}, {r0}, {len(coef)}, {st}, {pl}, {ve}, {{{cs}}}}},  // XorNet<{sid}>")
             sid += 1
     foot = ['// XorNet<i> codes kXorShapes[i]',
             f'constexpr int kXorShapeCount = {sid};',

@@ -124,3 +124,45 @@ def test_bitplane_object_plan(k, m):
         do += k * x
         po += m * x
     assert (pn[:5] == GUARD).all() and (pn[po:] == GUARD).all()
+
+
+@pytest.mark.parametrize("k,m,s", [(km[0], km[1], s) for km in SHAPES if gen_xor.USE[km][2]
+                                   for s in (161, 2031, 2033, 20011)])
+def test_bitplane_verify_flags_exactly(k, m, s):
+    """Verify through the chained bit-plane kernel (2 windows per tile, the
+    last column of window 0 borrowing window 1's first dword): oracle
+    codewords at odd offsets pass, and a single flipped byte — anywhere,
+    including next to the 2032-B tile boundaries and the window seam — flags
+    exactly its object."""
+    n = 24
+    rng = np.random.default_rng(7 * k + m + s)
+    off = int(rng.integers(1, 16))
+    pitch = (k + m) * s + 5
+    buf_np = rng.integers(0, 256, off + n * pitch + 16, dtype=np.uint8)
+    rows = CO.build_matrix(k, m)[k:]
+    for o in range(n):
+        b = off + o * pitch
+        par = CO.apply(rows, [buf_np[b + j * s:b + (j + 1) * s] for j in range(k)])
+        for r in range(m):
+            buf_np[b + (k + r) * s:b + (k + r + 1) * s] = par[r]
+    buf = torch.from_numpy(buf_np).cuda()
+    views = [(buf.data_ptr() + off + i * s, pitch) for i in range(k + m)]
+    enc = RS.New(k, m)
+    flags = torch.zeros(n, dtype=torch.int32, device="cuda")
+    before = _bp()
+    B.verify_views(enc, views, n, s, flags)
+    torch.cuda.synchronize()
+    assert _bp() > before, "the bit-plane Verify did not run"
+    assert int(flags.count_nonzero()) == 0
+    # flips: object -> (shard, position)
+    cand = sorted({p for t in range(1, s // 2032 + 2) for p in (2032 * t - 2, 2032 * t - 1, 2032 * t, 2032 * t + 15)
+                   if 0 <= p < s} | {0, s - 1, min(s - 1, 1023), min(s - 1, 1024), min(s - 1, 1008)})
+    hit = {}
+    for o in range(0, n, 2):
+        hit[o] = (int(rng.integers(0, k + m)), cand[(o // 2) % len(cand)])
+    for o, (i, p) in hit.items():
+        buf[off + o * pitch + i * s + p] ^= 0x10
+    flags.zero_()
+    B.verify_views(enc, views, n, s, flags)
+    torch.cuda.synchronize()
+    assert sorted(flags.nonzero().flatten().tolist()) == sorted(hit)

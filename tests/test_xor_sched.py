@@ -57,7 +57,7 @@ def test_committed_header_is_generated():
 def test_header_table_matches_networks():
     text = G.OUT.read_text()
     nets = re.findall(r"struct XorNet<(\d+)> \{\n    static constexpr int K = (\d+), R = (\d+);", text)
-    table = re.findall(r"\{(\d+), (\d+), (\d+), (\d+), (?:true|false), (?:true|false), \{(.*?)\}\},  // XorNet<(\d+)>",
+    table = re.findall(r"\{(\d+), (\d+), (\d+), (\d+), (?:true|false), (?:true|false), (?:true|false), \{(.*?)\}\},  // XorNet<(\d+)>",
                        text)
     assert len(nets) == len(table) == sum((m + 3) // 4 for _, m in G.SHAPES)
     shapes = {int(i): (int(k), int(r)) for i, k, r in nets}
