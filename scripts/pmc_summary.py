@@ -26,6 +26,10 @@ def short(name: str) -> str:
 
 
 def per_kernel(d: Path, counter: str):
+    """{kernel: [(counter value, duration)]} over the launches of the kernel's
+    LARGEST grid: a kernel that bench.py also launches for small checks (e.g.
+    one-object Verify calls after a plan leg) is reported for its bench-size
+    launches, not for the many tiny ones."""
     out = {}
     for f in d.glob("*counter_collection.csv"):
         for row in csv.DictReader(open(f)):
@@ -33,8 +37,12 @@ def per_kernel(d: Path, counter: str):
                 continue
             k = short(row["Kernel_Name"])
             dur = int(row["End_Timestamp"]) - int(row["Start_Timestamp"])
-            out.setdefault(k, []).append((float(row["Counter_Value"]), dur))
-    return out
+            out.setdefault(k, []).append((int(row["Grid_Size"]), float(row["Counter_Value"]), dur))
+    res = {}
+    for k, v in out.items():
+        g = max(x[0] for x in v)
+        res[k] = [(c, t) for gg, c, t in v if gg == g]
+    return res
 
 
 def main():
