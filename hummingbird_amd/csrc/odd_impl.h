@@ -126,16 +126,13 @@ __device__ __forceinline__ OddIn odd_in(uint64_t base, int32_t S, int32_t c) {
     return o;
 }
 
-// plain (L2-retained) 16-B load: Verify tiles share their boundary column
-// with the neighbouring wave's tile, which without a block barrier reads it
-// at another time; a non-temporal fetch is gone from L2 by then
-__device__ __forceinline__ u32x4 ld16_addr_keep(uint64_t addr) { return *reinterpret_cast<gu32x4_c*>(addr); }
-
-template <bool NT = true>
+// (Plain, L2-retained loads for Verify — the neighbouring wave's tile reads
+// the shared boundary column later — cut odd Verify traffic to <= 1.02 x
+// but ran 3-6 points slower: profiles/r05_ab_plans_verify.jsonl batch r5_ab9.)
 __device__ __forceinline__ u32x4 odd_ld(const OddIn& o, int32_t col) {
     int32_t v = o.off + 16 * col;
     v = v < 0 ? 0 : (v > o.lim ? o.lim : v);
-    return NT ? ld16_addr(o.base4 + (uint64_t)(uint32_t)v) : ld16_addr_keep(o.base4 + (uint64_t)(uint32_t)v);
+    return ld16_addr(o.base4 + (uint64_t)(uint32_t)v);
 }
 
 // bytes [sh, sh + 16) of the lane's block and lane l+1's first dword
@@ -336,7 +333,7 @@ __device__ __forceinline__ void odd_load(OddRegs<K, R, U, MODE>& X, const OddTil
     for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int j = 0; j < (MODE == kOddAcc ? K : NL); ++j)
-            X.x[u][j] = odd_ld<!(MODE == kOddVerify && HBEC_ODD_VERIFY_KEEP)>(src[j], (int32_t)(odd_wcol<U, MODE, CARRY>(u) + lane));
+            X.x[u][j] = odd_ld(src[j], (int32_t)(odd_wcol<U, MODE, CARRY>(u) + lane));
     if constexpr (MODE == kOddAcc) {
         // the old output block each lane will rewrite: output r's aligned block
         // at q = column + dl_r; lanes that store nothing read one inside the band
@@ -804,7 +801,7 @@ struct OddRT {  // the finish's scalars of one tile
     uint32_t obj, live;
 };
 
-template <int K, int R, int U, int MODE, bool CARRY, bool IMAJ = HBEC_ODD_REC_LOAD_ORDER != 0>
+template <int K, int R, int U, int MODE, bool CARRY, bool IMAJ = true>
 __device__ __forceinline__ void odd_rec_load(OddRegs<K, R, U, MODE>& X, const u32x8 (&l)[OddRec<K, R, MODE>::LW / 8],
                                              uint32_t v0, uint32_t lane) {
     using RC = OddRec<K, R, MODE>;
@@ -820,7 +817,7 @@ __device__ __forceinline__ void odd_rec_load(OddRegs<K, R, U, MODE>& X, const u3
         const uint32_t v = v0 + 16u * odd_rec_wcol<U, MODE, CARRY>(u) + 16u * lane;
         const uint64_t b = (uint64_t)odd_w(l, 3 * j) | ((uint64_t)odd_w(l, 3 * j + 1) << 32);
         const uint64_t ad = b + __builtin_elementwise_min(v, odd_w(l, 3 * j + 2));
-        X.x[u][j] = (MODE == kOddVerify && HBEC_ODD_VERIFY_KEEP) ? ld16_addr_keep(ad) : ld16_addr(ad);
+        X.x[u][j] = ld16_addr(ad);
     }
     if constexpr (MODE == kOddAcc) {
         // the old output block each lane will rewrite, clamped into the band
@@ -1027,7 +1024,7 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE, XS>())) 
     constexpr bool VCHAIN = BP && MODE == kOddVerify;
     constexpr bool LDS = !BP && odd_rec_lds(K);
     // input-major loads, except the 3-wave bit-plane blocks (12+4: 61.8 % window-major vs 59.2 %)
-    constexpr bool IMAJ = HBEC_ODD_REC_LOAD_ORDER != 0 && !(BP && odd_bp_wpb(K, R) == 3);
+    constexpr bool IMAJ = !(BP && odd_bp_wpb(K, R) == 3);
     constexpr uint32_t SPAN = VCHAIN ? (64u * U - 1u) * 16u : odd_rec_span(U, MODE);
     constexpr uint32_t WPB = BP ? (uint32_t)odd_bp_wpb(K, R) : kPipeBlockThreads / 64;
     const uint32_t lane = threadIdx.x & 63u;
@@ -1118,12 +1115,11 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE, XS>())) 
         p = step(p);
         odd_rec_sload<PF>(L, rec(p) + RC::FW);
         if constexpr (LIST) odd_rec_sload2<PF>(pe, lentry(tq + nw));
-        if constexpr (BP && HBEC_ODD_BP_SLEEP > 0) __builtin_amdgcn_s_sleep(HBEC_ODD_BP_SLEEP);
+        // (s_sleep pacing after these loads: no effect on the bit-plane kernels, r05_ab_bitplane.jsonl r5_ab4)
         // bit-plane Verify at 2 waves per SIMD: a block barrier per tile keeps
         // the waves sharing tile-boundary lines together (8+3 77.2 -> 78.4 %,
         // reads 1.054 -> 1.026 x); at one wave per SIMD it costs 10 points
-        if constexpr ((MODE != kOddVerify && (!BP || HBEC_ODD_BP_BARRIER)) ||
-                      (VCHAIN && HBEC_ODD_BP_VBARRIER && odd_bp_bpc(K, R, MODE) >= 2))
+        if constexpr (MODE != kOddVerify || (VCHAIN && HBEC_ODD_BP_VBARRIER && odd_bp_bpc(K, R, MODE) >= 2))
             __builtin_amdgcn_s_barrier();
         odd_rec_finish<K, R, U, MODE, CARRY, XS>(W, tw, a.tab, tb, lane, flags, lt);
         odd_swait();

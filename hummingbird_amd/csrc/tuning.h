@@ -107,34 +107,22 @@
 #define HBEC_ODD_LDS_MINK 9  // record kernels: coefficient tables in LDS from K = 9 (12+4 encode 51 -> 57 %; from K = 5, 8+3 lost 5 %)
 #endif
 #ifndef HBEC_ODD_BP_BPC
-#define HBEC_ODD_BP_BPC 1  // blocks per CU (launch bounds and grid) of the bit-plane record kernels
+#define HBEC_ODD_BP_BPC 1  // blocks per CU of the bit-plane apply kernels: 2 lost 5-15 points (r05_ab_bitplane r5_ab2/3)
 #endif
 #ifndef HBEC_ODD_BP_PF
-#define HBEC_ODD_BP_PF 1  // bit-plane record kernels: record loads issued a tile ahead (split load / wait)
+#define HBEC_ODD_BP_PF 1  // bit-plane records issued a tile ahead where no SGPR spills (K R <= 24; off: equal, r5_ab2)
 #endif
 #ifndef HBEC_ODD_BP_U
-#define HBEC_ODD_BP_U 2  // windows per wave tile of the bit-plane record kernels (even: column pairs)
-#endif
-#ifndef HBEC_ODD_BP_BARRIER
-#define HBEC_ODD_BP_BARRIER 1  // one block barrier per tile in the bit-plane record kernels
+#define HBEC_ODD_BP_U 2  // carried windows per bit-plane tile (column pairs); 4 lost 1-13 points (r5_ab6)
 #endif
 #ifndef HBEC_ODD_BP_VBARRIER
 #define HBEC_ODD_BP_VBARRIER 1  // bit-plane Verify at 2 blocks per CU: one block barrier per tile (r05_ab_verify.jsonl)
 #endif
 #ifndef HBEC_ODD_BP_WPB
-#define HBEC_ODD_BP_WPB 4  // waves per block of the bit-plane record kernels (one block per CU)
+#define HBEC_ODD_BP_WPB 4  // waves per block of the bit-plane kernels (one block per CU); 2: -7 to -12 (r5_ab5)
 #endif
 #ifndef HBEC_ODD_BP_WPB3_MINKR
-#define HBEC_ODD_BP_WPB3_MINKR 48  // bit-plane kernels with K R >= this run 3 waves per block
-#endif
-#ifndef HBEC_ODD_BP_SLEEP
-#define HBEC_ODD_BP_SLEEP 0  // x 64 cycles after the next tile's loads, bit-plane record kernels
-#endif
-#ifndef HBEC_ODD_REC_LOAD_ORDER
-#define HBEC_ODD_REC_LOAD_ORDER 1  // record kernels' tile loads: 1 input-major (a shard's windows together), 0 window-major
-#endif
-#ifndef HBEC_ODD_VERIFY_KEEP
-#define HBEC_ODD_VERIFY_KEEP 0  // odd Verify: 1 = plain (L2-retained) loads instead of non-temporal
+#define HBEC_ODD_BP_WPB3_MINKR 48  // 3 waves per block from K R = 48: 12+4 58.3 -> 62.9 %, 10+4 -3 (r5_ab5/6)
 #endif
 #ifndef HBEC_ODD_BPC_APPLY
 #define HBEC_ODD_BPC_APPLY 1  // blocks per CU of the strided / plan apply grids (register-bound shapes: odd_two_blocks)
