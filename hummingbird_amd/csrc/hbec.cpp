@@ -1137,7 +1137,15 @@ static int verify_views(hbec_codec* c, const hbec_view* views, uint64_t n_obj, u
     // 9 <= k <= 12 shapes (1-2 rows: the register-table gf_odd, m > 4: the
     // data read once per 4 rows) and k > 12 take gf_verify_wide, one
     // read-only pass per <= 8 rows.
-    const bool odd_verify = k <= 8 || (k <= kOddMaxK && m >= 3 && m <= kMaxR);
+    bool odd_verify = k <= 8 || (k <= kOddMaxK && m >= 3 && m <= kMaxR);
+    if (!odd_verify && k <= kOddMaxK && m <= kMaxR) {
+        // 9 <= k <= 12 with 1-2 rows: the one-pass bit-plane Verify when the
+        // rows have a compiled schedule (10+2, 12+2)
+        uint32_t tab[kMaxR][kMaxK][5];
+        for (int r = 0; r < m; ++r)
+            for (int j = 0; j < k; ++j) perm_table(prow[(size_t)r * k + j], tab[r][j]);
+        odd_verify = odd_bp_schedule(k, m, 2, tab, false) >= 0;
+    }
     if (odd_enabled() && odd_verify && pos32_shard(shard_len)) {
         // any alignment: recompute and compare in one pass (gf_odd verify), <= 4 rows per launch
         int dev = 0;

@@ -38,7 +38,8 @@ OUT = Path(__file__).resolve().parent / "csrc" / "xor_sched.h"
 # (k, m) encode shapes that get a compiled schedule.  Output groups of <= 4
 # rows (kMaxR); k <= kOddMaxK (12).  Chosen where the table multiply fills
 # the issue slots (K * R >= 18 and the BASELINE / hec shapes).
-SHAPES = [(6, 3), (7, 3), (8, 3), (8, 4), (9, 3), (10, 4), (12, 4), (6, 2), (8, 2), (4, 2)]
+SHAPES = [(6, 3), (7, 3), (8, 3), (8, 4), (9, 3), (10, 4), (12, 4), (6, 2), (8, 2), (4, 2),
+          (5, 3), (6, 4), (10, 2), (10, 3), (12, 2), (12, 3)]
 # Where the bit-plane kernel is the one launched (interleaved A/Bs against the
 # v_perm table kernels, profiles/r05_ab_bitplane.jsonl, r05_ab_plans_verify.jsonl):
 # strided batches / plans / Verify (the parity rows are the encode matrix).  The others keep the table kernels there (their schedule is still
@@ -48,6 +49,8 @@ USE = {  # (k, m): (strided, plan, verify)
     (8, 4): (True, True, True), (9, 3): (True, True, True), (10, 4): (True, True, True),
     (12, 4): (True, True, True), (6, 2): (False, True, True), (8, 2): (False, True, True),
     (4, 2): (False, False, False),
+    (5, 3): (True, True, True), (6, 4): (True, True, True), (10, 2): (True, True, True),
+    (10, 3): (True, True, True), (12, 2): (False, True, True), (12, 3): (True, True, True),
 }
 
 

@@ -81,7 +81,7 @@ def main():
                        "o83": (8, 3, 131071, "enc"), "r83": (8, 3, 131071, "rec"), "v83": (8, 3, 131071, "ver"),
                        "o104": (10, 4, 104858, "enc"), "o124": (12, 4, 87389, "enc"), "r104": (10, 4, 104858, "rec"), "p124": (12, 4, 87392, "plan"), "p42": (4, 2, 262143, "plan"), "p83": (8, 3, 131071, "plan"), "p104": (10, 4, 104858, "plan"),
                        "v328": (32, 8, 32771, "ver"), "v104": (10, 4, 104858, "ver"), "v124": (12, 4, 87389, "ver"),
-                       "v32": (3, 2, 349525, "ver"), "v84": (8, 4, 131071, "ver"), "v93": (9, 3, 116509, "ver"), "v73": (7, 3, 149797, "ver"), "v62": (6, 2, 174763, "ver"), "v82": (8, 2, 131071, "ver"), "v63": (6, 3, 174763, "ver"), "o63": (6, 3, 174763, "enc"), "o73": (7, 3, 149797, "enc"), "o62": (6, 2, 174763, "enc"), "o82": (8, 2, 131071, "enc"), "o84": (8, 4, 131071, "enc"), "o93": (9, 3, 116509, "enc"), "p63": (6, 3, 174763, "plan"), "p73": (7, 3, 149797, "plan"), "p42b": (4, 2, 262141, "plan"), "c42": (4, 2, 262143, "cplan"), "c83": (8, 3, 131071, "cplan"), "c104": (10, 4, 104858, "cplan"),
+                       "v32": (3, 2, 349525, "ver"), "o53": (5, 3, 209715, "enc"), "o64": (6, 4, 174763, "enc"), "o102": (10, 2, 104858, "enc"), "o103": (10, 3, 104858, "enc"), "o122": (12, 2, 87389, "enc"), "o123": (12, 3, 87389, "enc"), "v53": (5, 3, 209715, "ver"), "v64": (6, 4, 174763, "ver"), "v102": (10, 2, 104858, "ver"), "v103": (10, 3, 104858, "ver"), "v122": (12, 2, 87389, "ver"), "v123": (12, 3, 87389, "ver"), "p102": (10, 2, 104858, "plan"), "p123": (12, 3, 87389, "plan"), "p64": (6, 4, 174763, "plan"), "v84": (8, 4, 131071, "ver"), "v93": (9, 3, 116509, "ver"), "v73": (7, 3, 149797, "ver"), "v62": (6, 2, 174763, "ver"), "v82": (8, 2, 131071, "ver"), "v63": (6, 3, 174763, "ver"), "o63": (6, 3, 174763, "enc"), "o73": (7, 3, 149797, "enc"), "o62": (6, 2, 174763, "enc"), "o82": (8, 2, 131071, "enc"), "o84": (8, 4, 131071, "enc"), "o93": (9, 3, 116509, "enc"), "p63": (6, 3, 174763, "plan"), "p73": (7, 3, 149797, "plan"), "p42b": (4, 2, 262141, "plan"), "c42": (4, 2, 262143, "cplan"), "c83": (8, 3, 131071, "cplan"), "c104": (10, 4, 104858, "cplan"),
                        # random sizes (the nursery batch shape): object plans of n objects, S uniform in
                        # [4 KiB / k, 1 MiB / k], odd
                        "x42": (4, 2, 0, "rplan"), "x83": (8, 3, 0, "rplan"), "x104": (10, 4, 0, "rplan"), "x124": (12, 4, 0, "rplan")}[name]
