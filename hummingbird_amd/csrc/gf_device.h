@@ -48,6 +48,9 @@ __device__ __forceinline__ u32x4 ld16_addr(uint64_t addr) {
     return __builtin_nontemporal_load(reinterpret_cast<gu32x4_c*>(addr));
 }
 
+// plain (temporal) load: lines another wave reads next stay in L2
+__device__ __forceinline__ u32x4 ld16_addr_t(uint64_t addr) { return *reinterpret_cast<gu32x4_c*>(addr); }
+
 __device__ __forceinline__ void st16_addr(uint64_t addr, u32x4 v) {
     __builtin_nontemporal_store(v, reinterpret_cast<gu32x4*>(addr));
 }

@@ -801,7 +801,7 @@ struct OddRT {  // the finish's scalars of one tile
     uint32_t obj, live;
 };
 
-template <int K, int R, int U, int MODE, bool CARRY, bool IMAJ = true>
+template <int K, int R, int U, int MODE, bool CARRY, bool IMAJ = true, bool TEMP = false>
 __device__ __forceinline__ void odd_rec_load(OddRegs<K, R, U, MODE>& X, const u32x8 (&l)[OddRec<K, R, MODE>::LW / 8],
                                              uint32_t v0, uint32_t lane) {
     using RC = OddRec<K, R, MODE>;
@@ -817,7 +817,7 @@ __device__ __forceinline__ void odd_rec_load(OddRegs<K, R, U, MODE>& X, const u3
         const uint32_t v = v0 + 16u * odd_rec_wcol<U, MODE, CARRY>(u) + 16u * lane;
         const uint64_t b = (uint64_t)odd_w(l, 3 * j) | ((uint64_t)odd_w(l, 3 * j + 1) << 32);
         const uint64_t ad = b + __builtin_elementwise_min(v, odd_w(l, 3 * j + 2));
-        X.x[u][j] = ld16_addr(ad);
+        X.x[u][j] = TEMP ? ld16_addr_t(ad) : ld16_addr(ad);
     }
     if constexpr (MODE == kOddAcc) {
         // the old output block each lane will rewrite, clamped into the band
@@ -1025,6 +1025,11 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE, XS>())) 
     constexpr bool LDS = !BP && odd_rec_lds(K);
     // input-major loads, except the 3-wave bit-plane blocks (12+4: 61.8 % window-major vs 59.2 %)
     constexpr bool IMAJ = !(BP && odd_bp_wpb(K, R) == 3);
+    // input loads with the temporal hint (HBEC_ODD_TEMP): the window-major
+    // strided apply keeps the lines its neighbour tiles share in L2
+    constexpr bool TEMP = MODE == kOddVerify ? (HBEC_ODD_TEMP & 1) != 0
+                                             : MODE == kOddApply && ((HBEC_ODD_TEMP & 2) != 0 ||
+                                                                     ((HBEC_ODD_TEMP & 4) != 0 && !IMAJ && !LIST));
     constexpr uint32_t SPAN = VCHAIN ? (64u * U - 1u) * 16u : odd_rec_span(U, MODE);
     constexpr uint32_t WPB = BP ? (uint32_t)odd_bp_wpb(K, R) : kPipeBlockThreads / 64;
     const uint32_t lane = threadIdx.x & 63u;
@@ -1098,7 +1103,7 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE, XS>())) 
     odd_swait();
     odd_swait_pin(L);
     fill(tx, p);
-    odd_rec_load<K, R, U, MODE, CARRY || VCHAIN, IMAJ>(X, L, tx.v0, lane);
+    odd_rec_load<K, R, U, MODE, CARRY || VCHAIN, IMAJ, TEMP>(X, L, tx.v0, lane);
     odd_rec_sload<PF>(tx.f, rec(p));
     p = step(p);
     odd_rec_sload<PF>(L, rec(p) + RC::FW);
@@ -1110,7 +1115,7 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE, XS>())) 
     auto half = [&](OddRegs<K, R, U, MODE>& Z, OddRT<K, R, MODE>& tz, const OddRegs<K, R, U, MODE>& W,
                     const OddRT<K, R, MODE>& tw) {
         fill(tz, p);
-        odd_rec_load<K, R, U, MODE, CARRY || VCHAIN, IMAJ>(Z, L, tz.v0, lane);
+        odd_rec_load<K, R, U, MODE, CARRY || VCHAIN, IMAJ, TEMP>(Z, L, tz.v0, lane);
         odd_rec_sload<PF>(tz.f, rec(p));
         p = step(p);
         odd_rec_sload<PF>(L, rec(p) + RC::FW);

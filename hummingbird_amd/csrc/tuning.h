@@ -118,6 +118,15 @@
 #ifndef HBEC_ODD_BP_VBARRIER
 #define HBEC_ODD_BP_VBARRIER 1  // bit-plane Verify at 2 blocks per CU: one block barrier per tile (r05_ab_verify.jsonl)
 #endif
+#ifndef HBEC_ODD_TEMP
+// record-kernel input loads with the temporal hint: bit 0 Verify, bit 1 apply,
+// bit 2 window-major strided apply (the 3-wave 12+4 kernel).  4: odd 12+4
+// encode 61.5-62.7 -> 64.3-64.6 %, reads 1.090 -> 1.002 x; the same hint on
+// its plans reads 1.071 -> 1.003 x but runs 61.0 -> 57.1 %, on 8+3 / 10+4
+// apply -2.3 / -0.4, on Verify -5 to -7 points at 1.006 / 1.002 x reads
+// (r05_ab_temp.jsonl, r5_temp / r5_temp2)
+#define HBEC_ODD_TEMP 4
+#endif
 #ifndef HBEC_ODD_BP_WPB
 #define HBEC_ODD_BP_WPB 4  // waves per block of the bit-plane kernels (one block per CU); 2: -7 to -12 (r5_ab5)
 #endif

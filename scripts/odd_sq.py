@@ -77,7 +77,11 @@ def main():
         return int(flags.count_nonzero().item()) == 0
 
     for name in names:
-        k, m, s, op = {"a42": (4, 2, MiB // 4, "enc"), "o42": (4, 2, 262143, "enc"), "v42": (4, 2, 262143, "ver"), "r42": (4, 2, 262143, "rec"), "a83": (8, 3, MiB // 8, "enc"),
+        if name.startswith("c:"):  # custom: c:K:M:S:OP (OP enc / rec / ver / plan)
+            _, k, m, s, op = name.split(":")
+            k, m, s = int(k), int(m), int(s)
+        else:
+          k, m, s, op = {"a42": (4, 2, MiB // 4, "enc"), "o42": (4, 2, 262143, "enc"), "v42": (4, 2, 262143, "ver"), "r42": (4, 2, 262143, "rec"), "a83": (8, 3, MiB // 8, "enc"),
                        "o83": (8, 3, 131071, "enc"), "r83": (8, 3, 131071, "rec"), "v83": (8, 3, 131071, "ver"),
                        "o104": (10, 4, 104858, "enc"), "o124": (12, 4, 87389, "enc"), "r104": (10, 4, 104858, "rec"), "p124": (12, 4, 87392, "plan"), "p42": (4, 2, 262143, "plan"), "p83": (8, 3, 131071, "plan"), "p104": (10, 4, 104858, "plan"),
                        "v328": (32, 8, 32771, "ver"), "v104": (10, 4, 104858, "ver"), "v124": (12, 4, 87389, "ver"),
@@ -118,6 +122,15 @@ def main():
             torch.cuda.synchronize()
             row["ok"] = ok
             del plan, d, par
+        elif op == "dplan":
+            # the databuf layout of "enc" (shard i at row + i S) coded through an object plan
+            rows, views = databuf(k, m, s)
+            plan = B.StripePlan(enc, objects=[(rows.data_ptr() + i * rows.stride(0),
+                                               rows.data_ptr() + i * rows.stride(0) + k * s, s) for i in range(n)])
+            ms = timeit(plan.encode)
+            nb = n * (k + m) * s
+            row["ok"] = check(enc, views, s)
+            del plan, rows, views
         elif op == "plan":
             d = torch.empty((n, k * s), dtype=torch.uint8, device="cuda")
             B.fill_splitmix(d, k * s)
