@@ -138,7 +138,7 @@ class StripePlan:
         check(N.lib().hbec_reconstruct_plan(self.enc.handle, self._h, p, int(data_only), _stream_ptr(stream)))
 
 
-KERNEL_KINDS = {0: "unrolled", 1: "pipelined", 2: "streaming", 3: "packed"}
+KERNEL_KINDS = {0: "unrolled", 1: "pipelined", 2: "streaming", 3: "packed", 4: "records"}
 
 
 def kernel_info(k: int, r: int, shard_len: int):

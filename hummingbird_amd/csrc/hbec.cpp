@@ -234,6 +234,40 @@ static int apply_odd(const PassArgs& a, int K, int R, bool accumulate, uint64_t 
 // Generic pass planner: out[R] (^)= C[R][K] x in[K] over strided views
 // ---------------------------------------------------------------------------
 static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+static bool vec_len(uint64_t v) { return v % 16 == 0; }
+// 16-B-aligned views the record kernels (gf_odd_rec) code faster than the
+// aligned ones, interleaved A/B over 40 shapes (profiles/r05_ab_route.jsonl):
+//  * 9 <= k <= 12 at any pitch: one bit-plane / record pass against the
+//    tables at 1-KiB tiles, encode +2 to +9 points, 12+4 reconstruct +3;
+//  * 5 <= k <= 8 when a base, object stride or S is not a multiple of the
+//    128-B line (+0.4 to +9: the aligned kernels lose 4-10 points there, the
+//    record kernels with their per-tile block barrier do not), or with 4
+//    output rows (6+4 / 8+4 +7 / +10, their plans +22 to +27: the stripe
+//    kernels take 3 rows per pass), as long as a pass is K R <= 24 or has a
+//    compiled bit-plane schedule (7+4 on tables: -8);
+//  * k <= 4, line-aligned 5 <= k <= 8 with <= 3 rows, and short shards
+//    (tuning.h HBEC_REC_ROUTE_MIN_S*) stay on the aligned kernels.
+// Tuning builds: HBEC_REC_ROUTE=0 keeps every 16-B-aligned view there.
+static const int g_rec_route = (int)tune_knob("HBEC_REC_ROUTE", 1);
+bool rec_route(int cols, int rows, uint64_t shard_len, bool line_aligned, bool bitplane) {
+    if (!g_rec_route || !odd_enabled() || cols < 5 || cols > kOddMaxK || !pos32_shard(shard_len)) return false;
+    if (cols > 8) return shard_len >= HBEC_REC_ROUTE_MIN_S_BIG;
+    const int r = std::min(rows, kMaxR);
+    return shard_len >= HBEC_REC_ROUTE_MIN_S && (!line_aligned || r >= 4) && (cols * r <= 24 || bitplane);
+}
+// the first pass's rows (<= kMaxR of `rows`, coefficients row-major with
+// `cols` per row) have a compiled bit-plane schedule
+static bool bitplane_rows(int k, int rows, const uint8_t* coeffs, int cols, bool plan) {
+    if (k > kMaxK) return false;
+    uint32_t tab[kMaxR][kMaxK][5] = {};
+    const int r = std::min(rows, kMaxR);
+    for (int q = 0; q < r; ++q)
+        for (int j = 0; j < k; ++j) tab[q][j][0] = (uint32_t)coeffs[(size_t)q * cols + j] << 8;  // byte 1 = c * 1
+    return odd_bp_schedule(k, r, 0, tab, plan) >= 0;
+}
+static bool line_aligned(const void* p, uint64_t stride) {
+    return (reinterpret_cast<uintptr_t>(p) & 127u) == 0 && stride % 128 == 0;
+}
 
 static int apply_wide(int rows, int cols, const uint8_t* coeffs, const hbec_view* in, const hbec_view* out,
                       uint64_t n_obj, uint64_t shard_len, hipStream_t stream);
@@ -242,9 +276,13 @@ int apply_views(int rows, int cols, const uint8_t* coeffs, const hbec_view* in, 
                 uint64_t n_obj, uint64_t shard_len, hipStream_t stream) {
     if (rows <= 0 || n_obj == 0 || shard_len == 0) return HBEC_OK;
     if (cols <= 0 || !coeffs || !in || !out) return fail(HBEC_ERR_INVALID_ARG, "apply: bad arguments");
-    bool vec = (shard_len % 16) == 0;
-    for (int c = 0; c < cols && vec; ++c) vec = aligned16(in[c].base) && (in[c].obj_stride % 16) == 0;
-    for (int r = 0; r < rows && vec; ++r) vec = aligned16(out[r].base) && (out[r].obj_stride % 16) == 0;
+    bool vec = vec_len(shard_len);
+    for (int c = 0; c < cols && vec; ++c) vec = aligned16(in[c].base) && vec_len(in[c].obj_stride);
+    for (int r = 0; r < rows && vec; ++r) vec = aligned16(out[r].base) && vec_len(out[r].obj_stride);
+    bool line = vec && shard_len % 128 == 0;
+    for (int c = 0; c < cols && line; ++c) line = line_aligned(in[c].base, in[c].obj_stride);
+    for (int r = 0; r < rows && line; ++r) line = line_aligned(out[r].base, out[r].obj_stride);
+    const bool to_rec = vec && rec_route(cols, rows, shard_len, line, bitplane_rows(cols, rows, coeffs, cols, false));
     for (int c = 0; c < cols; ++c)
         if (!in[c].base) return fail(HBEC_ERR_INVALID_ARG, "apply: null input view");
     for (int r = 0; r < rows; ++r)
@@ -303,7 +341,7 @@ int apply_views(int rows, int cols, const uint8_t* coeffs, const hbec_view* in, 
                     hipError_t e = launch_packed(K, R, b, grid, stream);
                     if (e != hipSuccess) return hip_fail(e, "launch gf_apply_packed");
                 }
-            } else if (vec) {
+            } else if (vec && !to_rec) {
                 int cus = 0, per_cu = 0;
                 rc = device_blocks(dev, K, R, is_pipe_shape(K, R, shard_len, force_stream) && c0 == 0, force_stream,
                                    &cus, &per_cu);
@@ -550,6 +588,11 @@ struct hbec_codec {
 };
 
 namespace hbec {
+
+bool plan_rec_route(const hbec_codec* c, uint64_t shard_len, bool line_aligned) {
+    return rec_route(c->k, c->m, shard_len, line_aligned,
+                     c->m > 0 && bitplane_rows(c->k, c->m, c->matrix.data() + (size_t)c->k * c->k, c->k, true));
+}
 
 // Decode rows for a present mask: survivors = first k present shards.
 static int decode_rows(hbec_codec* c, const std::vector<uint8_t>& present, bool data_only,
@@ -1038,8 +1081,8 @@ static int verify_views(hbec_codec* c, const hbec_view* views, uint64_t n_obj, u
                         hipStream_t stream) {
     const int k = c->k, m = c->m;
     if (m == 0 || n_obj == 0 || shard_len == 0) return HBEC_OK;
-    bool vec = (shard_len % 16) == 0;
-    for (int i = 0; i < k + m && vec; ++i) vec = aligned16(views[i].base) && (views[i].obj_stride % 16) == 0;
+    bool vec = vec_len(shard_len);
+    for (int i = 0; i < k + m && vec; ++i) vec = aligned16(views[i].base) && vec_len(views[i].obj_stride);
     const uint8_t* prow = c->matrix.data() + (size_t)k * k;
     if (vec && is_verify_packed_shape(k, m, shard_len)) {
         // short shards: wave tiles across objects (gf_verify_packed)
@@ -1364,15 +1407,19 @@ int hbec_kernel_info(int k, int r, uint64_t shard_len, int* tile_bytes, int* kin
         if (k < 1 || k > kMaxK || r < 1 || r > kMaxR) return fail(HBEC_ERR_INVALID_ARG, "shape out of range");
         const int fs = g_force_stream.load();
         const bool packed = r <= 3 && is_packed_shape(k, r, shard_len, 0, fs);
+        const bool rec = !packed && shard_len % 16 == 0 && rec_route(k, r, shard_len, shard_len % 128 == 0, false);
         const int pipe = packed ? 2 : is_pipe_shape(k, r, shard_len, fs);
-        if (tile_bytes) *tile_bytes = packed ? packed_tile_elems(k) * 16 : vec_tile_bytes(k, r, shard_len, 0, fs);
-        if (kind) *kind = packed ? 3 : (is_streaming_shape(k, r, fs) ? 2 : (pipe ? 1 : 0));
+        if (tile_bytes)
+            *tile_bytes = packed ? packed_tile_elems(k) * 16
+                                 : (rec ? (int)odd_rec_tile_span(k, 0, -1) : vec_tile_bytes(k, r, shard_len, 0, fs));
+        if (kind) *kind = packed ? 3 : (rec ? 4 : (is_streaming_shape(k, r, fs) ? 2 : (pipe ? 1 : 0)));
         if (blocks_per_cu) {
             int dev = 0, cus = 0;
             int rc = current_device(&dev);
             if (rc) return rc;
             rc = device_blocks(dev, k, r, pipe, packed ? 0 : fs, &cus, blocks_per_cu);
             if (rc) return rc;
+            if (rec) *blocks_per_cu = odd_blocks_per_cu(0, k, r, false, true);
             if (g_blocks_per_cu_override > 0) *blocks_per_cu = g_blocks_per_cu_override;
         }
         return HBEC_OK;

@@ -72,6 +72,14 @@ void coalesce_stats(uint64_t* groups, uint64_t* calls);
 // staging slot of the host ring).
 uint64_t host_md5_max_shard(const hbec_codec* codec);
 
+// 16-B-aligned shards of k inputs that the record kernels code faster than
+// the aligned ones (hbec.cpp: 9 <= k <= 12, or 5 <= k <= 8 off the 128-B
+// line or with 4 rows; long enough shards); line_aligned: every base,
+// stride and S % 128 == 0; bitplane: the rows have a compiled schedule
+bool rec_route(int k, int rows, uint64_t shard_len, bool line_aligned, bool bitplane);
+// the same for a plan of the codec's encode rows
+bool plan_rec_route(const hbec_codec* c, uint64_t shard_len, bool line_aligned);
+
 struct TileRec;
 // Grid for a stripes launch of k inputs / r outputs over n_tiles records
 // (one block of 4 waves per CU at most, as the strided kernels).

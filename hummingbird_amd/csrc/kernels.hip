@@ -117,11 +117,12 @@ template <int K, int R, int U>
 __device__ __forceinline__ void load_tile(u32x4 (&x)[U][K], const PassArgs& a, uint64_t obj, uint64_t off0) {
     const uint64_t last = a.shard_len - 16u;
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
+    for (int q = 0; q < U * K; ++q) {
+        const int u = HBEC_PIPE_IMAJ ? q % U : q / K, j = HBEC_PIPE_IMAJ ? q / U : q % K;
         uint64_t off = off0 + (uint64_t)u * 1024u;
         off = off < last ? off : last;
-#pragma unroll
-        for (int j = 0; j < K; ++j) x[u][j] = ld16(a.in[j] + obj * a.in_stride[j] + off);
+        const uint8_t* p = a.in[j] + obj * a.in_stride[j] + off;
+        x[u][j] = HBEC_PIPE_TEMP ? ld16_addr_t(reinterpret_cast<uint64_t>(p)) : ld16(p);
     }
 }
 
@@ -218,11 +219,11 @@ template <int K, int R, int U>
 __device__ __forceinline__ void pipe2_load(u32x4 (&x)[U][K], const PipeTile<K, R>& b, uint32_t lane) {
     const uint64_t last = (uint64_t)b.valid - 16u;
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
+    for (int q = 0; q < U * K; ++q) {
+        const int u = HBEC_PIPE_IMAJ ? q % U : q / K, j = HBEC_PIPE_IMAJ ? q / U : q % K;
         uint64_t off = (uint64_t)lane * 16u + (uint64_t)u * 1024u;
         off = off < last ? off : last;
-#pragma unroll
-        for (int j = 0; j < K; ++j) x[u][j] = ld16_addr(b.in[j] + off);
+        x[u][j] = HBEC_PIPE_TEMP ? ld16_addr_t(b.in[j] + off) : ld16_addr(b.in[j] + off);
     }
 }
 

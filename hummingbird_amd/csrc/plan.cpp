@@ -430,7 +430,9 @@ int hbec_plan_stripes(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n,
             if (s.shard_len == 0) continue;
             if (!s.base) return fail(HBEC_ERR_INVALID_ARG, "stripe with null base");
             p->shard_bytes += s.shard_len;
-            if (!aligned_stripe(s)) {
+            // (aligned stripes the record kernels code faster join them, hbec.cpp rec_route)
+            if (!aligned_stripe(s) ||
+                hbec::plan_rec_route(codec, s.shard_len, (reinterpret_cast<uintptr_t>(s.base) & 127u) == 0 && s.shard_len % 128 == 0)) {
                 p->fallback.push_back(s);
                 add_urecs(urecs, erecs, brecs, orecs, s.base, nullptr, s.shard_len, k);
                 continue;
@@ -495,7 +497,9 @@ int hbec_plan_objects(hbec_codec* codec, const hbec_object* objects, uint64_t n,
             if (o.shard_len == 0) continue;
             if (!o.data || (m > 0 && !o.parity)) return fail(HBEC_ERR_INVALID_ARG, "object with null data or parity");
             p->shard_bytes += o.shard_len;
-            if (!aligned_object(o)) {
+            const bool line = ((reinterpret_cast<uintptr_t>(o.data) | reinterpret_cast<uintptr_t>(o.parity)) & 127u) == 0 &&
+                              o.shard_len % 128 == 0;
+            if (!aligned_object(o) || (k <= hbec::kStripeMaxK && hbec::plan_rec_route(codec, o.shard_len, line))) {
                 p->obj_fallback.push_back(o);
                 add_urecs(urecs, erecs, brecs, orecs, o.data, o.parity, o.shard_len, k);
                 continue;

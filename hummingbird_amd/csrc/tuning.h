@@ -28,6 +28,12 @@
 #ifndef HBEC_PIPE2_SLEEP
 #define HBEC_PIPE2_SLEEP 8  // pipe2 with its block barrier: 6 and 8 tie, 12 loses 4 % (r01_tune_sleep_pipe2)
 #endif
+#ifndef HBEC_PIPE_IMAJ
+#define HBEC_PIPE_IMAJ 0  // pipelined kernels: 1 = a shard's windows back to back (A/B)
+#endif
+#ifndef HBEC_PIPE_TEMP
+#define HBEC_PIPE_TEMP 0  // pipelined kernels: 1 = input loads with the temporal hint (A/B)
+#endif
 #ifndef HBEC_PIPE_V2_MAXK
 #define HBEC_PIPE_V2_MAXK 4  // pipe2 up to K = 4: +1.6 % at 4+2, -7 % at 8+3 (profiles/r01_tune_pipe2.jsonl)
 #endif
@@ -117,6 +123,16 @@
 #endif
 #ifndef HBEC_ODD_BP_VBARRIER
 #define HBEC_ODD_BP_VBARRIER 1  // bit-plane Verify at 2 blocks per CU: one block barrier per tile (r05_ab_verify.jsonl)
+#endif
+// Shortest 16-B-aligned shard apply_views routes to the record kernels
+// (hbec.cpp rec_route), 5 <= k <= 8 / 9 <= k <= 12: 8+3 at 32 KiB 60.8 % on
+// the aligned kernel vs 56.2 %, at 64 KiB 60.6 vs 63.3 %; 10+4 at 16 KiB
+// 53.8 vs 46.8 %, at 32 KiB 54.0 vs 57.1 % (r05_ab_route.jsonl, r5_route2)
+#ifndef HBEC_REC_ROUTE_MIN_S
+#define HBEC_REC_ROUTE_MIN_S 49152
+#endif
+#ifndef HBEC_REC_ROUTE_MIN_S_BIG
+#define HBEC_REC_ROUTE_MIN_S_BIG 24576
 #endif
 #ifndef HBEC_ODD_TEMP
 // record-kernel input loads with the temporal hint: bit 0 Verify, bit 1 apply,

@@ -332,9 +332,10 @@ int hbec_batcher_reconstruct(hbec_batcher* batcher, const hbec_stripe* stripe, c
 int hbec_batcher_stats(hbec_batcher* batcher, uint64_t* batches, uint64_t* stripes);
 
 /* Tuning / introspection: force the runtime-K streaming kernel (0/1), and
- * report what a pass of k inputs -> r outputs over shard_len bytes launches:
- * tile bytes per wave, kind (0 = unrolled, 1 = pipelined, 2 = streaming) and
- * resident blocks per CU used to size the grid. */
+ * report what a pass of k inputs -> r outputs over shard_len bytes of
+ * 128-B-aligned, contiguous shards launches: tile bytes per wave, kind
+ * (0 = unrolled, 1 = pipelined, 2 = streaming, 3 = packed, 4 = the record
+ * kernel gf_odd_rec) and resident blocks per CU used to size the grid. */
 int hbec_set_force_stream(int on);
 int hbec_kernel_info(int k, int r, uint64_t shard_len, int* tile_bytes, int* kind, int* blocks_per_cu);
 /* Launches since load of the odd-shard main kernels (any alignment, k <= 12

@@ -77,7 +77,11 @@ def main():
         return int(flags.count_nonzero().item()) == 0
 
     for name in names:
-        if name.startswith("c:"):  # custom: c:K:M:S:OP (OP enc / rec / ver / plan)
+        if name.startswith("w:"):  # w:K:M:S:DI:DO  inputs at i (S + DI), outputs (own array) at r (S + DO)
+            _, k, m, s, di, do_ = name.split(":")
+            k, m, s, di, do_ = int(k), int(m), int(s), int(di), int(do_)
+            op = "skew"
+        elif name.startswith("c:"):  # custom: c:K:M:S:OP (OP enc / rec / ver / plan)
             _, k, m, s, op = name.split(":")
             k, m, s = int(k), int(m), int(s)
         else:
@@ -122,6 +126,18 @@ def main():
             torch.cuda.synchronize()
             row["ok"] = ok
             del plan, d, par
+        elif op == "skew":
+            din = torch.empty((n, k * (s + di) + 256), dtype=torch.uint8, device="cuda")
+            B.fill_splitmix(din, din.shape[1])
+            dout = torch.empty((n, m * (s + do_) + 256), dtype=torch.uint8, device="cuda")
+            views = [(din.data_ptr() + i * (s + di), din.stride(0)) for i in range(k)] + \
+                    [(dout.data_ptr() + r * (s + do_), dout.stride(0)) for r in range(m)]
+            B.encode_views(enc, views, n, s)
+            ms = timeit(lambda: B.encode_views(enc, views, n, s))
+            nb = n * (k + m) * s
+            row["ok"] = check(enc, views, s)
+            row["DI"], row["DO"] = di, do_
+            del din, dout, views
         elif op == "dplan":
             # the databuf layout of "enc" (shard i at row + i S) coded through an object plan
             rows, views = databuf(k, m, s)

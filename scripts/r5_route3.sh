@@ -1,0 +1,10 @@
+#!/bin/bash
+# The record-kernel route in stripe / object plans: GPU suite, then the
+# product rule against HBEC_REC_ROUTE=0 on plans of 16-B-aligned objects.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out; export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r5_route3_tests.log 2>&1 || { tail -40 gpurun_out/r5_route3_tests.log; exit 1; }
+tail -2 gpurun_out/r5_route3_tests.log
+SH=c:8:3:131088:plan,c:8:3:131088:dplan,c:10:4:131072:dplan,c:12:4:87424:dplan,c:6:4:174768:plan,c:8:4:131088:dplan,c:10:4:131072:plan,c:8:3:131072:dplan,c:8:3:131088:enc,c:10:4:131072:enc
+timeout -k 10 900 bash scripts/ab_odd.sh gpurun_out/r5_route3.jsonl $SH tune_build/va/libhbec.so tune_build/va/libhbec.so:HBEC_REC_ROUTE=0 || exit $?

@@ -25,6 +25,8 @@ from hummingbird_amd import reedsolomon as RS
 from oracle import coracle as CO
 from oracle import oracle as O
 
+import route_rule as R
+
 pytestmark = pytest.mark.gpu
 MiB = 1 << 20
 
@@ -549,7 +551,7 @@ def test_plan_config4_shape_counts():
     info = plan.info()
     tile = info["tile_bytes"]
     assert info["n_tiles"] == sum((s + tile - 1) // tile for _, s, _ in layout)
-    assert info["n_fallback"] == 0
+    assert info["n_fallback"] == sum(R.stripe_on_records(k, m, dev.data_ptr() + o, s) for o, s, _ in layout)
     plan.encode()
     torch.cuda.synchronize()
     assert np.array_equal(dev.cpu().numpy(), _expected_pool(k, m, pool, layout))
@@ -601,7 +603,8 @@ def test_object_plan_encode_reconstruct(k, m, sizes, misalign):
         return [(dt.data_ptr() + o, pt.data_ptr() + po, s) for (o, s, _), po in zip(dl, pl)]
 
     plan = B.StripePlan(enc, objects=objs(d, p))
-    assert plan.info()["n_fallback"] == sum(1 for o, s, _ in dl if o % 16 or s % 16)
+    assert plan.info()["n_fallback"] == sum(R.object_on_records(k, m, d.data_ptr() + o, p.data_ptr() + po, s)
+                                            for (o, s, _), po in zip(dl, pl))
     plan.encode()
     torch.cuda.synchronize()
     assert np.array_equal(p.cpu().numpy(), parity)
@@ -937,15 +940,15 @@ def test_batcher_wide_k(k, m):
 
 @pytest.mark.parametrize("k,m", [(10, 4), (17, 3)])
 def test_stripe_plan_wide_k(k, m):
-    """Stripe plans with k > 8 take the tiled kernel in accumulate passes (no
-    per-stripe fallback)."""
+    """Stripe plans with k > 8: the tiled kernel in accumulate passes, except
+    the stripes the record kernels take (10+4 with S >= 24 KiB, rec_route)."""
     sizes = [k * 1024 * 3, k * 16, MiB // 4 * k, k * 4096]
     pool, layout = _stripe_pool(k, m, sizes)
     want = _expected_pool(k, m, pool, layout)
     dev = torch.from_numpy(pool).cuda()
     enc = RS.New(k, m)
     plan = B.StripePlan(enc, [(dev.data_ptr() + o, s) for o, s, _ in layout])
-    assert plan.info()["n_fallback"] == 0
+    assert plan.info()["n_fallback"] == sum(R.stripe_on_records(k, m, dev.data_ptr() + o, s) for o, s, _ in layout)
     plan.encode()
     torch.cuda.synchronize()
     assert np.array_equal(dev.cpu().numpy(), want)

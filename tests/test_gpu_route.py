@@ -1,0 +1,84 @@
+"""GPU parity of the 16-B-aligned views that apply_views routes to the record
+kernels (csrc/hbec.cpp rec_route): 9 <= k <= 12 at any pitch and
+5 <= k <= 8 when a base, object stride or S is not a multiple of the 128-B
+line; k <= 4 and line-aligned 5 <= k <= 8 stay on the aligned kernels.
+
+ecSplit databufs (shard i at i*S, objectserver/ecutils.go:31-35) at 16-B
+but not 128-B aligned pitches and at 128-B pitches: Encode (ecutils.go:59)
+and Reconstruct of two data shards (ecutils.go:111) against the oracle, byte
+for byte, and the route taken read from hbec_odd_path_stats.
+"""
+import numpy as np
+import pytest
+import torch
+
+from hummingbird_amd import batch as B
+from hummingbird_amd import reedsolomon as RS
+from oracle import coracle as CO
+
+import route_rule as R
+
+pytestmark = pytest.mark.gpu
+
+
+def _odd_launches():
+    return sum(B.odd_path_stats().values())
+
+
+def _routed(k, m, s, base):
+    from hummingbird_amd import gen_xor
+    return R.rec_route(k, s, base, rows=m, bitplane=gen_xor.USE.get((k, m), (False,))[0])
+
+
+def test_route_rule_thresholds():
+    """the mirror reads tuning.h: 24 KiB for 9 <= k <= 12, 48 KiB off the line for 5 <= k <= 8"""
+    assert (R.MIN_S_BIG, R.MIN_S) == (24576, 49152)
+
+
+@pytest.mark.parametrize("k,m,s,off", [(8, 3, 49168, 0), (8, 3, 49152, 16), (8, 3, 49152, 0), (6, 4, 49200, 0),
+                                       (5, 3, 61456, 48), (7, 3, 8208, 0), (9, 3, 24592, 0), (10, 4, 24576, 0),
+                                       (12, 4, 32768, 0), (12, 3, 26640, 32), (10, 2, 24560, 0), (4, 2, 65552, 0),
+                                       (4, 2, 65536, 0), (8, 4, 65552, 0), (8, 3, 4112, 0), (8, 4, 65536, 0),
+                                       (6, 4, 49152, 0), (7, 4, 65536, 0), (7, 4, 65552, 0), (6, 6, 49152, 0)])
+def test_aligned_views_route_and_parity(k, m, s, off):
+    n = max(3, min(48, 3_000_000 // ((k + m) * s)))
+    pitch = (k + m) * s
+    buf = torch.empty(off + n * pitch + 64, dtype=torch.uint8, device="cuda")
+    B.fill_splitmix(buf.view(1, -1), buf.numel())
+    base = buf.data_ptr() + off
+    views = [(base + i * s, pitch) for i in range(k + m)]
+    enc = RS.New(k, m)
+    before = _odd_launches()
+    B.encode_views(enc, views, n, s)
+    torch.cuda.synchronize()
+    assert (_odd_launches() > before) == _routed(k, m, s, base), "route"
+    got = buf.cpu().numpy()
+    rows = CO.build_matrix(k, m)[k:]
+    for o in range(n):
+        b = off + o * pitch
+        want = CO.apply(rows, [got[b + j * s:b + (j + 1) * s] for j in range(k)])
+        for r in range(m):
+            assert np.array_equal(got[b + (k + r) * s:b + (k + r + 1) * s], want[r]), (o, r)
+    # two data shards lost: rebuilt in place from the first k survivors
+    ref = buf.clone()
+    for o in range(n):
+        buf[off + o * pitch:off + o * pitch + 2 * s] = 0xA5
+    before = _odd_launches()
+    B.reconstruct_views(enc, views, [0, 0] + [1] * (k + m - 2), n, s)
+    torch.cuda.synchronize()
+    assert (_odd_launches() > before) == R.rec_route(k, s, base, rows=2), "route (reconstruct)"
+    assert torch.equal(buf, ref)
+    flags = torch.zeros(n, dtype=torch.int32, device="cuda")
+    B.verify_views(enc, views, n, s, flags)
+    torch.cuda.synchronize()
+    assert int(flags.count_nonzero()) == 0
+
+
+def test_kernel_info_reports_the_route():
+    assert B.kernel_info(4, 2, 1 << 18)["kind"] == "pipelined"
+    assert B.kernel_info(8, 3, 1 << 17)["kind"] == "pipelined"
+    assert B.kernel_info(8, 3, (1 << 17) + 16)["kind"] == "records"
+    assert B.kernel_info(8, 3, 4096 + 16)["kind"] == "pipelined"
+    assert B.kernel_info(10, 4, 1 << 17)["kind"] == "records"
+    assert B.kernel_info(10, 4, 1 << 14)["kind"] == "streaming"  # the aligned k > 8 kernel
+    assert B.kernel_info(8, 3, 512)["kind"] == "packed"

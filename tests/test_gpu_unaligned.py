@@ -17,6 +17,8 @@ from hummingbird_amd import batch as B
 from hummingbird_amd import reedsolomon as RS
 from oracle import coracle as CO
 
+import route_rule as R
+
 pytestmark = pytest.mark.gpu
 GUARD = 0xA5
 
@@ -190,7 +192,7 @@ def test_plan_random_odd_stripes(k, m, n, lo, hi):
     dev = torch.from_numpy(pool).cuda()
     enc = RS.New(k, m)
     plan = B.StripePlan(enc, [(dev.data_ptr() + o, s) for o, s in layout])
-    assert plan.info()["n_fallback"] == sum(1 for o, s in layout if (dev.data_ptr() + o) % 16 or s % 16)
+    assert plan.info()["n_fallback"] == sum(R.stripe_on_records(k, m, dev.data_ptr() + o, s) for o, s in layout)
     plan.encode()
     torch.cuda.synchronize()
     got = dev.cpu().numpy()
