@@ -1130,7 +1130,21 @@ static int verify_views(hbec_codec* c, const hbec_view* views, uint64_t n_obj, u
         }
         return HBEC_OK;
     }
-    if (vec && verify_supported(k, m)) {
+    // 16-B-aligned Verify stays on gf_verify_pipe (2-4 points ahead of the
+    // record kernels from 5+3 to 8+3 at any pitch) except where its tables
+    // run out of issue slots: K R > 24 with a compiled bit-plane Verify
+    // (8+4: 59.8-62.1 -> 74.3-75.5 %, profiles/r05_ab_route.jsonl r5_vroute).
+    // Tuning builds: HBEC_VERIFY_ROUTE=0 keeps them all there.
+    static const bool verify_route = tune_knob("HBEC_VERIFY_ROUTE", 1) != 0;
+    bool v_to_rec = vec && verify_route && odd_enabled() && k >= 5 && k <= 8 && m <= kMaxR && k * m > 24 &&
+                    shard_len >= HBEC_REC_ROUTE_MIN_S && pos32_shard(shard_len);
+    if (v_to_rec) {
+        uint32_t tab[kMaxR][kMaxK][5] = {};
+        for (int r = 0; r < m; ++r)
+            for (int j = 0; j < k; ++j) tab[r][j][0] = (uint32_t)prow[(size_t)r * k + j] << 8;  // byte 1 = c * 1
+        v_to_rec = odd_bp_schedule(k, m, 2, tab, false) >= 0;
+    }
+    if (vec && verify_supported(k, m) && !v_to_rec) {
         PassArgs a;
         std::memset(&a, 0, sizeof(a));
         for (int j = 0; j < k; ++j) {

@@ -69,9 +69,21 @@ def test_aligned_views_route_and_parity(k, m, s, off):
     assert (_odd_launches() > before) == R.rec_route(k, s, base, rows=2), "route (reconstruct)"
     assert torch.equal(buf, ref)
     flags = torch.zeros(n, dtype=torch.int32, device="cuda")
+    before = _odd_launches()
     B.verify_views(enc, views, n, s, flags)
     torch.cuda.synchronize()
     assert int(flags.count_nonzero()) == 0
+    # Verify: gf_verify_pipe (k <= 8, m <= 4) except past K R = 24 with a
+    # compiled bit-plane Verify (8+4); everything else on the odd kernels
+    from hummingbird_amd import gen_xor
+    v_rec = 5 <= k <= 8 and k * m > 24 and m <= 4 and s >= R.MIN_S and gen_xor.USE.get((k, m), (0, 0, 0))[2]
+    assert (_odd_launches() > before) == (bool(v_rec) or 9 <= k <= 12 or m > 4), "route (Verify)"
+    # a flipped parity byte is caught on either route
+    buf[off + (n - 1) * pitch + k * s + s // 2] ^= 1
+    flags.zero_()
+    B.verify_views(enc, views, n, s, flags)
+    torch.cuda.synchronize()
+    assert flags.nonzero().flatten().tolist() == [n - 1]
 
 
 def test_kernel_info_reports_the_route():
