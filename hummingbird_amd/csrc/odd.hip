@@ -107,35 +107,41 @@ __device__ __forceinline__ bool odd_edge_pos(int32_t S, uint64_t out_frame, int3
     return *pos >= qmax + 16;
 }
 
-__device__ __forceinline__ uint32_t odd_edge_byte(const TabArray& tab, int r, int K, const uint64_t* in, int32_t p) {
-    uint32_t v = 0;
-    for (int j = 0; j < K; ++j) {
-        const uint32_t x = *reinterpret_cast<const gu8_t*>(in[j] + (uint64_t)p);
-        const uint32_t* t = tab[r][j];
-        v ^= gf_mul_sel(selectors(x), t[0], t[1], t[2], t[3], t[4]);
-    }
-    return v & 0xFFu;
-}
-
+// One edge position p of every output of a pass: the K input bytes are
+// loaded once and their selectors shared by the R outputs (the table words
+// tab[r][j] are wave-uniform: scalar loads); output r is coded, stored or
+// compared only where position p is in r's guard band (odd_edge_pos on r's
+// frame).  MODE: apply, accumulate (out ^= ...), verify (flag the object).
 template <int MODE>
-__global__ __launch_bounds__(kBlockThreads) void gf_odd_edges(PassArgs a, int K, int R, uint32_t* flags) {
-    const uint64_t per_obj = (uint64_t)R * kOddEdgeSlots;
-    const uint64_t total = a.n_obj * per_obj;
-    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < total; v += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t obj = v / per_obj;
-        const uint32_t rs = (uint32_t)(v - obj * per_obj);
-        const int r = (int)(rs / kOddEdgeSlots);
-        const int32_t slot = (int32_t)(rs - (uint32_t)r * kOddEdgeSlots);
-        uint64_t in[kMaxK];
-        for (int j = 0; j < K; ++j) in[j] = reinterpret_cast<uint64_t>(a.in[j]) + obj * a.in_stride[j];
-        const uint64_t out = reinterpret_cast<uint64_t>(a.out[r]) + obj * a.out_stride[r];
-        const uint64_t frame = MODE == kOddVerify ? reinterpret_cast<uint64_t>(a.out[0]) + obj * a.out_stride[0] : out;
-        int32_t p;
-        if (!odd_edge_pos((int32_t)a.shard_len, frame, slot, &p)) continue;
-        uint32_t val = odd_edge_byte(a.tab, r, K, in, p);
-        gu8_t* d = reinterpret_cast<gu8_t*>(out + (uint64_t)p);
+__device__ __forceinline__ void odd_edge_all(const TabArray& tab, int K, int R, const uint64_t* in, const uint64_t* out,
+                                             uint64_t vframe, int32_t S, int32_t slot, uint32_t* flag) {
+    bool act[kMaxR];
+    int32_t pos[kMaxR];
+    bool any = false;
+    for (int r = 0; r < R; ++r) {
+        act[r] = odd_edge_pos(S, MODE == kOddVerify ? vframe : out[r], slot, &pos[r]);
+        any |= act[r];
+    }
+    if (!any) return;
+    // every active output's position is the same byte of the shard: the
+    // guard band differs per output only in where it ends
+    int32_t p = 0;
+    for (int r = 0; r < R; ++r)
+        if (act[r]) p = pos[r];
+    uint32_t v[kMaxR] = {0u, 0u, 0u, 0u};
+    for (int j = 0; j < K; ++j) {
+        const Sel s = selectors(*reinterpret_cast<const gu8_t*>(in[j] + (uint64_t)p));
+        for (int r = 0; r < R; ++r) {
+            const uint32_t* t = tab[r][j];
+            v[r] ^= gf_mul_sel(s, t[0], t[1], t[2], t[3], t[4]);
+        }
+    }
+    for (int r = 0; r < R; ++r) {
+        if (!act[r]) continue;
+        gu8_t* d = reinterpret_cast<gu8_t*>(out[r] + (uint64_t)p);
+        uint32_t val = v[r] & 0xFFu;
         if (MODE == kOddVerify) {
-            if (val != *d) atomicOr(flags + obj, 1u);
+            if (val != *d) atomicOr(flag, 1u);
         } else {
             if (MODE == kOddAcc) val ^= *d;
             *d = (uint8_t)val;
@@ -143,28 +149,44 @@ __global__ __launch_bounds__(kBlockThreads) void gf_odd_edges(PassArgs a, int K,
     }
 }
 
+// one thread per (object, edge slot), all R outputs; 32-bit index math when
+// the launch has < 2^32 threads (always, for < 26 M objects)
+template <int MODE>
+__global__ __launch_bounds__(kBlockThreads) void gf_odd_edges(PassArgs a, int K, int R, uint32_t* flags) {
+    const uint64_t total = a.n_obj * (uint64_t)kOddEdgeSlots;
+    const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < total; v += step) {
+        uint64_t obj;
+        int32_t slot;
+        if (total < (1ull << 32)) {
+            const uint32_t o = (uint32_t)v / (uint32_t)kOddEdgeSlots;
+            obj = o;
+            slot = (int32_t)((uint32_t)v - o * (uint32_t)kOddEdgeSlots);
+        } else {
+            obj = v / (uint64_t)kOddEdgeSlots;
+            slot = (int32_t)(v - obj * (uint64_t)kOddEdgeSlots);
+        }
+        uint64_t in[kMaxK], out[kMaxR];
+        for (int j = 0; j < K; ++j) in[j] = reinterpret_cast<uint64_t>(a.in[j]) + obj * a.in_stride[j];
+        for (int r = 0; r < R; ++r) out[r] = reinterpret_cast<uint64_t>(a.out[r]) + obj * a.out_stride[r];
+        odd_edge_all<MODE>(a.tab, K, R, in, out, out[0], (int32_t)a.shard_len, slot, flags + obj);
+    }
+}
+
 // plans: one edge record per stripe / object (URec, p0 unused)
 template <int MODE>
 __global__ __launch_bounds__(kBlockThreads) void gf_odd_edges_plan(UPlanArgs p, const URec* __restrict__ erecs,
                                                                   uint32_t n_erecs, int K, int R) {
-    const uint64_t per = (uint64_t)R * kOddEdgeSlots;
-    const uint64_t total = (uint64_t)n_erecs * per;
+    const uint64_t total = (uint64_t)n_erecs * kOddEdgeSlots;
     for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < total; v += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t e = v / per;
-        const uint32_t rs = (uint32_t)(v - e * per);
-        const int r = (int)(rs / kOddEdgeSlots);
-        const int32_t slot = (int32_t)(rs - (uint32_t)r * kOddEdgeSlots);
+        const uint32_t e = (uint32_t)(v / (uint64_t)kOddEdgeSlots);
+        const int32_t slot = (int32_t)(v - (uint64_t)e * kOddEdgeSlots);
         const URec rec = erecs[e];
         const uint64_t S = rec.shard_len;
-        uint64_t in[kMaxK];
+        uint64_t in[kMaxK], out[kMaxR];
         for (int j = 0; j < K; ++j) in[j] = (((p.in_sel >> j) & 1u) ? rec.b : rec.a) + (uint64_t)p.in_idx[j] * S;
-        const uint64_t out = (((p.out_sel >> r) & 1u) ? rec.b : rec.a) + (uint64_t)p.out_idx[r] * S;
-        int32_t q;
-        if (!odd_edge_pos((int32_t)S, out, slot, &q)) continue;
-        uint32_t val = odd_edge_byte(p.tab, r, K, in, q);
-        gu8_t* d = reinterpret_cast<gu8_t*>(out + (uint64_t)q);
-        if (MODE == kOddAcc) val ^= *d;
-        *d = (uint8_t)val;
+        for (int r = 0; r < R; ++r) out[r] = (((p.out_sel >> r) & 1u) ? rec.b : rec.a) + (uint64_t)p.out_idx[r] * S;
+        odd_edge_all<MODE>(p.tab, K, R, in, out, out[0], (int32_t)S, slot, nullptr);
     }
 }
 
@@ -396,7 +418,7 @@ hipError_t launch_odd(int k, int r, int mode, const PassArgs& a, uint32_t* flags
 hipError_t launch_odd_edges(int k, int r, int mode, const PassArgs& a, uint32_t* flags, hipStream_t stream) {
     if (k < 1 || k > kMaxK || r < 1 || r > kMaxR || a.n_obj == 0) return a.n_obj == 0 ? hipSuccess : hipErrorInvalidValue;
     if (!pos32_shard(a.shard_len)) return hipErrorInvalidValue;
-    const uint64_t total = a.n_obj * (uint64_t)r * kOddEdgeSlots;
+    const uint64_t total = a.n_obj * (uint64_t)kOddEdgeSlots;
     const int grid = (int)std::min<uint64_t>((total + kBlockThreads - 1) / kBlockThreads, 4096);
     const void* fn = mode == kOddVerify ? (const void*)&gf_odd_edges<kOddVerify>
                                         : (mode == kOddAcc ? (const void*)&gf_odd_edges<kOddAcc> : (const void*)&gf_odd_edges<kOddApply>);
@@ -408,7 +430,7 @@ hipError_t launch_odd_edges_plan(int k, int r, int mode, const UPlanArgs& p, con
                                  hipStream_t stream) {
     if (n_erecs == 0) return hipSuccess;
     if (k < 1 || k > kMaxK || r < 1 || r > kMaxR || mode == kOddVerify) return hipErrorInvalidValue;
-    const uint64_t total = (uint64_t)n_erecs * (uint64_t)r * kOddEdgeSlots;
+    const uint64_t total = (uint64_t)n_erecs * (uint64_t)kOddEdgeSlots;
     const int grid = (int)std::min<uint64_t>((total + kBlockThreads - 1) / kBlockThreads, 4096);
     const void* fn = mode == kOddAcc ? (const void*)&gf_odd_edges_plan<kOddAcc> : (const void*)&gf_odd_edges_plan<kOddApply>;
     void* args[] = {const_cast<UPlanArgs*>(&p), &erecs, &n_erecs, &k, &r};
