@@ -218,7 +218,8 @@ static int odd_launches(const PassArgs& a, int K, int R, int mode, bool accumula
     }
     // the guard-band bytes of every shard, all K inputs of the pass at once
     // (on a second stream beside the main kernel this ran 0.6-3 points
-    // slower: the scattered edge lines disturb the main stream, r05_ab_edges.jsonl)
+    // slower, the scattered edge lines disturbing the main stream; before the
+    // main kernel, within +-1: r05_ab_edges.jsonl)
     PassArgs g = a;
     g.n_obj = n_obj;
     g.shard_len = shard_len;
