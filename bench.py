@@ -472,7 +472,9 @@ def odd_leg(k, m, n, obj_len, first, reps=20, settle=40, pmc=None):
         kern = pmc.get("kernels", {})
         for name, (r, mode) in (("encode", (m, 0)), ("reconstruct", (2, 0)), ("verify", (m, 2))):
             kname, t = _odd_kernel_traffic(kern, k, r, mode)
-            te = kern.get("gf_odd_edges<2>" if name == "verify" else "gf_odd_edges<0>", {}).get("hbm_bytes_per_launch")
+            # (the edge kernel of a batch of >= kOddEdgeSplitObjs objects: one thread per slot, all outputs)
+            te = kern.get("gf_odd_edges<2, false>" if name == "verify" else "gf_odd_edges<0, false>", {}).get(
+                "hbm_bytes_per_launch")
             if t is not None:
                 out[name]["kernel"] = kname
                 out[name]["traffic"] = int(t + (te or 0))
@@ -567,7 +569,7 @@ def random_objects(n=4096, shapes=((4, 2), (8, 3)), reps=20, settle=40):
             kern = pmc.get("kernels", {})
             kname, t = _odd_kernel_traffic(kern, k, m, 0, plan=True)
             extra = sum((kern.get(x, {}).get("hbm_bytes_per_launch") or 0)
-                        for x in ("gf_odd_edges_plan<0>", "gf_odd_planrec"))
+                        for x in ("gf_odd_edges_plan<0, false>", "gf_odd_planrec"))
             if t is not None:
                 leg["kernel"] = kname
                 leg["traffic"] = int(t + extra)

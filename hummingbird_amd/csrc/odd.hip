@@ -113,12 +113,13 @@ __device__ __forceinline__ bool odd_edge_pos(int32_t S, uint64_t out_frame, int3
 // compared only where position p is in r's guard band (odd_edge_pos on r's
 // frame).  MODE: apply, accumulate (out ^= ...), verify (flag the object).
 template <int MODE>
-__device__ __forceinline__ void odd_edge_all(const TabArray& tab, int K, int R, const uint64_t* in, const uint64_t* out,
-                                             uint64_t vframe, int32_t S, int32_t slot, uint32_t* flag) {
-    bool act[kMaxR];
+__device__ __forceinline__ void odd_edge_all(const TabArray& tab, int K, int r0, int R, const uint64_t* in,
+                                             const uint64_t* out, uint64_t vframe, int32_t S, int32_t slot,
+                                             uint32_t* flag) {
+    bool act[kMaxR] = {false, false, false, false};
     int32_t pos[kMaxR];
     bool any = false;
-    for (int r = 0; r < R; ++r) {
+    for (int r = r0; r < R; ++r) {
         act[r] = odd_edge_pos(S, MODE == kOddVerify ? vframe : out[r], slot, &pos[r]);
         any |= act[r];
     }
@@ -126,17 +127,17 @@ __device__ __forceinline__ void odd_edge_all(const TabArray& tab, int K, int R, 
     // every active output's position is the same byte of the shard: the
     // guard band differs per output only in where it ends
     int32_t p = 0;
-    for (int r = 0; r < R; ++r)
+    for (int r = r0; r < R; ++r)
         if (act[r]) p = pos[r];
     uint32_t v[kMaxR] = {0u, 0u, 0u, 0u};
     for (int j = 0; j < K; ++j) {
         const Sel s = selectors(*reinterpret_cast<const gu8_t*>(in[j] + (uint64_t)p));
-        for (int r = 0; r < R; ++r) {
+        for (int r = r0; r < R; ++r) {
             const uint32_t* t = tab[r][j];
             v[r] ^= gf_mul_sel(s, t[0], t[1], t[2], t[3], t[4]);
         }
     }
-    for (int r = 0; r < R; ++r) {
+    for (int r = r0; r < R; ++r) {
         if (!act[r]) continue;
         gu8_t* d = reinterpret_cast<gu8_t*>(out[r] + (uint64_t)p);
         uint32_t val = v[r] & 0xFFu;
@@ -149,44 +150,54 @@ __device__ __forceinline__ void odd_edge_all(const TabArray& tab, int K, int R, 
     }
 }
 
-// one thread per (object, edge slot), all R outputs; 32-bit index math when
-// the launch has < 2^32 threads (always, for < 26 M objects)
-template <int MODE>
+// one thread per (object, edge slot) for all R outputs, or (split: calls of
+// few objects, where latency and not lines bound the kernel) per (object,
+// output, slot); 32-bit index math below 2^32 threads (< 6 M objects)
+template <int MODE, bool SPLIT>
 __global__ __launch_bounds__(kBlockThreads) void gf_odd_edges(PassArgs a, int K, int R, uint32_t* flags) {
-    const uint64_t total = a.n_obj * (uint64_t)kOddEdgeSlots;
+    const uint32_t groups = SPLIT ? (uint32_t)R : 1u;  // (a constant divisor when not split)
+    const uint64_t per = (uint64_t)groups * kOddEdgeSlots;
+    const uint64_t total = a.n_obj * per;
     const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < total; v += step) {
         uint64_t obj;
-        int32_t slot;
+        uint32_t rs;
         if (total < (1ull << 32)) {
-            const uint32_t o = (uint32_t)v / (uint32_t)kOddEdgeSlots;
+            const uint32_t o = (uint32_t)v / (uint32_t)per;
             obj = o;
-            slot = (int32_t)((uint32_t)v - o * (uint32_t)kOddEdgeSlots);
+            rs = (uint32_t)v - o * (uint32_t)per;
         } else {
-            obj = v / (uint64_t)kOddEdgeSlots;
-            slot = (int32_t)(v - obj * (uint64_t)kOddEdgeSlots);
+            obj = v / per;
+            rs = (uint32_t)(v - obj * per);
         }
+        const uint32_t g = rs / (uint32_t)kOddEdgeSlots;
+        const int32_t slot = (int32_t)(rs - g * (uint32_t)kOddEdgeSlots);
         uint64_t in[kMaxK], out[kMaxR];
         for (int j = 0; j < K; ++j) in[j] = reinterpret_cast<uint64_t>(a.in[j]) + obj * a.in_stride[j];
         for (int r = 0; r < R; ++r) out[r] = reinterpret_cast<uint64_t>(a.out[r]) + obj * a.out_stride[r];
-        odd_edge_all<MODE>(a.tab, K, R, in, out, out[0], (int32_t)a.shard_len, slot, flags + obj);
+        odd_edge_all<MODE>(a.tab, K, SPLIT ? (int)g : 0, SPLIT ? (int)g + 1 : R, in, out, out[0],
+                           (int32_t)a.shard_len, slot, flags + obj);
     }
 }
 
 // plans: one edge record per stripe / object (URec, p0 unused)
-template <int MODE>
+template <int MODE, bool SPLIT>
 __global__ __launch_bounds__(kBlockThreads) void gf_odd_edges_plan(UPlanArgs p, const URec* __restrict__ erecs,
                                                                   uint32_t n_erecs, int K, int R) {
-    const uint64_t total = (uint64_t)n_erecs * kOddEdgeSlots;
+    const uint64_t per = (uint64_t)(SPLIT ? R : 1) * kOddEdgeSlots;
+    const uint64_t total = (uint64_t)n_erecs * per;
     for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < total; v += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t e = (uint32_t)(v / (uint64_t)kOddEdgeSlots);
-        const int32_t slot = (int32_t)(v - (uint64_t)e * kOddEdgeSlots);
+        const uint32_t e = (uint32_t)(v / per);
+        const uint32_t rs = (uint32_t)(v - (uint64_t)e * per);
+        const uint32_t g = rs / (uint32_t)kOddEdgeSlots;
+        const int32_t slot = (int32_t)(rs - g * (uint32_t)kOddEdgeSlots);
         const URec rec = erecs[e];
         const uint64_t S = rec.shard_len;
         uint64_t in[kMaxK], out[kMaxR];
         for (int j = 0; j < K; ++j) in[j] = (((p.in_sel >> j) & 1u) ? rec.b : rec.a) + (uint64_t)p.in_idx[j] * S;
         for (int r = 0; r < R; ++r) out[r] = (((p.out_sel >> r) & 1u) ? rec.b : rec.a) + (uint64_t)p.out_idx[r] * S;
-        odd_edge_all<MODE>(p.tab, K, R, in, out, out[0], (int32_t)S, slot, nullptr);
+        odd_edge_all<MODE>(p.tab, K, SPLIT ? (int)g : 0, SPLIT ? (int)g + 1 : R, in, out, out[0], (int32_t)S, slot,
+                           nullptr);
     }
 }
 
@@ -418,10 +429,18 @@ hipError_t launch_odd(int k, int r, int mode, const PassArgs& a, uint32_t* flags
 hipError_t launch_odd_edges(int k, int r, int mode, const PassArgs& a, uint32_t* flags, hipStream_t stream) {
     if (k < 1 || k > kMaxK || r < 1 || r > kMaxR || a.n_obj == 0) return a.n_obj == 0 ? hipSuccess : hipErrorInvalidValue;
     if (!pos32_shard(a.shard_len)) return hipErrorInvalidValue;
-    const uint64_t total = a.n_obj * (uint64_t)kOddEdgeSlots;
+    // few objects: a thread per output too (shorter per-thread chains); many:
+    // the K input bytes once for every output (fewer line touches: 16384 short
+    // 8+3 objects 59.6 -> 52.4 us, r05_edges_*_kernel_stats.csv)
+    const bool split = a.n_obj < kOddEdgeSplitObjs;
+    const uint64_t total = a.n_obj * (uint64_t)(split ? r : 1) * kOddEdgeSlots;
     const int grid = (int)std::min<uint64_t>((total + kBlockThreads - 1) / kBlockThreads, 4096);
-    const void* fn = mode == kOddVerify ? (const void*)&gf_odd_edges<kOddVerify>
-                                        : (mode == kOddAcc ? (const void*)&gf_odd_edges<kOddAcc> : (const void*)&gf_odd_edges<kOddApply>);
+    const void* fn = split ? (mode == kOddVerify ? (const void*)&gf_odd_edges<kOddVerify, true>
+                                                 : (mode == kOddAcc ? (const void*)&gf_odd_edges<kOddAcc, true>
+                                                                    : (const void*)&gf_odd_edges<kOddApply, true>))
+                           : (mode == kOddVerify ? (const void*)&gf_odd_edges<kOddVerify, false>
+                                                 : (mode == kOddAcc ? (const void*)&gf_odd_edges<kOddAcc, false>
+                                                                    : (const void*)&gf_odd_edges<kOddApply, false>));
     void* args[] = {const_cast<PassArgs*>(&a), &k, &r, &flags};
     return hipLaunchKernel(fn, dim3(grid), dim3(kBlockThreads), args, 0, stream);
 }
@@ -430,9 +449,13 @@ hipError_t launch_odd_edges_plan(int k, int r, int mode, const UPlanArgs& p, con
                                  hipStream_t stream) {
     if (n_erecs == 0) return hipSuccess;
     if (k < 1 || k > kMaxK || r < 1 || r > kMaxR || mode == kOddVerify) return hipErrorInvalidValue;
-    const uint64_t total = (uint64_t)n_erecs * (uint64_t)kOddEdgeSlots;
+    const bool split = n_erecs < kOddEdgeSplitObjs;
+    const uint64_t total = (uint64_t)n_erecs * (uint64_t)(split ? r : 1) * kOddEdgeSlots;
     const int grid = (int)std::min<uint64_t>((total + kBlockThreads - 1) / kBlockThreads, 4096);
-    const void* fn = mode == kOddAcc ? (const void*)&gf_odd_edges_plan<kOddAcc> : (const void*)&gf_odd_edges_plan<kOddApply>;
+    const void* fn = split ? (mode == kOddAcc ? (const void*)&gf_odd_edges_plan<kOddAcc, true>
+                                              : (const void*)&gf_odd_edges_plan<kOddApply, true>)
+                           : (mode == kOddAcc ? (const void*)&gf_odd_edges_plan<kOddAcc, false>
+                                              : (const void*)&gf_odd_edges_plan<kOddApply, false>);
     void* args[] = {const_cast<UPlanArgs*>(&p), &erecs, &n_erecs, &k, &r};
     return hipLaunchKernel(fn, dim3(grid), dim3(kBlockThreads), args, 0, stream);
 }
