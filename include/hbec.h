@@ -335,7 +335,10 @@ int hbec_batcher_stats(hbec_batcher* batcher, uint64_t* batches, uint64_t* strip
  * report what a pass of k inputs -> r outputs over shard_len bytes of
  * 128-B-aligned, contiguous shards launches: tile bytes per wave, kind
  * (0 = unrolled, 1 = pipelined, 2 = streaming, 3 = packed, 4 = the record
- * kernel gf_odd_rec) and resident blocks per CU used to size the grid. */
+ * kernel gf_odd_rec) and resident blocks per CU used to size the grid.  The
+ * route to the record kernels is reported for coefficient tables; rows with
+ * a compiled bit-plane schedule (8+4, 6+4 encode) may take it where this
+ * reports an aligned kind (hbec.cpp rec_route). */
 int hbec_set_force_stream(int on);
 int hbec_kernel_info(int k, int r, uint64_t shard_len, int* tile_bytes, int* kind, int* blocks_per_cu);
 /* Launches since load of the odd-shard main kernels (any alignment, k <= 12
