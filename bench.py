@@ -473,7 +473,7 @@ def odd_leg(k, m, n, obj_len, first, reps=20, settle=40, pmc=None):
         for name, (r, mode) in (("encode", (m, 0)), ("reconstruct", (2, 0)), ("verify", (m, 2))):
             kname, t = _odd_kernel_traffic(kern, k, r, mode)
             # (the edge kernel of a batch of >= kOddEdgeSplitObjs objects: one thread per slot, all outputs)
-            te = kern.get("gf_odd_edges<2, false>" if name == "verify" else "gf_odd_edges<0, false>", {}).get(
+            te = kern.get("gf_odd_edges<2, false, 128>" if name == "verify" else "gf_odd_edges<0, false, 128>", {}).get(
                 "hbm_bytes_per_launch")
             if t is not None:
                 out[name]["kernel"] = kname

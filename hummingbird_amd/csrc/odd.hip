@@ -90,8 +90,14 @@ __global__ __launch_bounds__(kBlockThreads) void gf_odd_mirror_copy(const URec* 
 // verify mode the compared columns are output 0's blocks for every r.  K <= 16
 // inputs, R <= 4 outputs per launch (one pass of apply_views).
 // ---------------------------------------------------------------------------
+// SLOTS per shard: kOddEdgeSlots (shards of any length; all of a shard of
+// S <= kOddMinMain), or kOddEdgeSlotsLong for S > kOddMinMain: the head
+// [0, qmin) and tail [qmax + 16, S) lie in [0, 64) and [S - 64, S)
+// (qmin <= G + 15, qmax >= S - G - 31), so each 64-lane wave then codes
+// exactly one end of one shard
+template <int SLOTS = kOddEdgeSlots>
 __device__ __forceinline__ bool odd_edge_pos(int32_t S, uint64_t out_frame, int32_t slot, int32_t* pos) {
-    if (S <= kOddEdgeSlots) {
+    if (SLOTS == kOddEdgeSlots && S <= kOddEdgeSlots) {
         *pos = slot;
         return slot < S;
     }
@@ -99,11 +105,11 @@ __device__ __forceinline__ bool odd_edge_pos(int32_t S, uint64_t out_frame, int3
     const int32_t qmin = kOddGuard + e;
     const int32_t top = S - kOddGuard - 16;
     const int32_t qmax = top - ((top - e) & 15);
-    if (slot < kOddEdgeSlots / 2) {
+    if (slot < SLOTS / 2) {
         *pos = slot;
         return slot < qmin;
     }
-    *pos = S - kOddEdgeSlots + slot;
+    *pos = S - SLOTS + slot;
     return *pos >= qmax + 16;
 }
 
@@ -112,7 +118,7 @@ __device__ __forceinline__ bool odd_edge_pos(int32_t S, uint64_t out_frame, int3
 // tab[r][j] are wave-uniform: scalar loads); output r is coded, stored or
 // compared only where position p is in r's guard band (odd_edge_pos on r's
 // frame).  MODE: apply, accumulate (out ^= ...), verify (flag the object).
-template <int MODE>
+template <int MODE, int SLOTS = kOddEdgeSlots>
 __device__ __forceinline__ void odd_edge_all(const TabArray& tab, int K, int r0, int R, const uint64_t* in,
                                              const uint64_t* out, uint64_t vframe, int32_t S, int32_t slot,
                                              uint32_t* flag) {
@@ -120,7 +126,7 @@ __device__ __forceinline__ void odd_edge_all(const TabArray& tab, int K, int r0,
     int32_t pos[kMaxR];
     bool any = false;
     for (int r = r0; r < R; ++r) {
-        act[r] = odd_edge_pos(S, MODE == kOddVerify ? vframe : out[r], slot, &pos[r]);
+        act[r] = odd_edge_pos<SLOTS>(S, MODE == kOddVerify ? vframe : out[r], slot, &pos[r]);
         any |= act[r];
     }
     if (!any) return;
@@ -153,10 +159,10 @@ __device__ __forceinline__ void odd_edge_all(const TabArray& tab, int K, int r0,
 // one thread per (object, edge slot) for all R outputs, or (split: calls of
 // few objects, where latency and not lines bound the kernel) per (object,
 // output, slot); 32-bit index math below 2^32 threads (< 6 M objects)
-template <int MODE, bool SPLIT>
+template <int MODE, bool SPLIT, int SLOTS>
 __global__ __launch_bounds__(kBlockThreads) void gf_odd_edges(PassArgs a, int K, int R, uint32_t* flags) {
     const uint32_t groups = SPLIT ? (uint32_t)R : 1u;  // (a constant divisor when not split)
-    const uint64_t per = (uint64_t)groups * kOddEdgeSlots;
+    const uint64_t per = (uint64_t)groups * SLOTS;
     const uint64_t total = a.n_obj * per;
     const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < total; v += step) {
@@ -170,12 +176,12 @@ __global__ __launch_bounds__(kBlockThreads) void gf_odd_edges(PassArgs a, int K,
             obj = v / per;
             rs = (uint32_t)(v - obj * per);
         }
-        const uint32_t g = rs / (uint32_t)kOddEdgeSlots;
-        const int32_t slot = (int32_t)(rs - g * (uint32_t)kOddEdgeSlots);
+        const uint32_t g = rs / (uint32_t)SLOTS;
+        const int32_t slot = (int32_t)(rs - g * (uint32_t)SLOTS);
         uint64_t in[kMaxK], out[kMaxR];
         for (int j = 0; j < K; ++j) in[j] = reinterpret_cast<uint64_t>(a.in[j]) + obj * a.in_stride[j];
         for (int r = 0; r < R; ++r) out[r] = reinterpret_cast<uint64_t>(a.out[r]) + obj * a.out_stride[r];
-        odd_edge_all<MODE>(a.tab, K, SPLIT ? (int)g : 0, SPLIT ? (int)g + 1 : R, in, out, out[0],
+        odd_edge_all<MODE, SLOTS>(a.tab, K, SPLIT ? (int)g : 0, SPLIT ? (int)g + 1 : R, in, out, out[0],
                            (int32_t)a.shard_len, slot, flags + obj);
     }
 }
@@ -433,14 +439,17 @@ hipError_t launch_odd_edges(int k, int r, int mode, const PassArgs& a, uint32_t*
     // the K input bytes once for every output (fewer line touches: 16384 short
     // 8+3 objects 59.6 -> 52.4 us, r05_edges_*_kernel_stats.csv)
     const bool split = a.n_obj < kOddEdgeSplitObjs;
-    const uint64_t total = a.n_obj * (uint64_t)(split ? r : 1) * kOddEdgeSlots;
+    const bool lng = a.shard_len > kOddMinMain;  // 64 + 64 slots: one shard end per wave
+    const uint64_t total = a.n_obj * (uint64_t)(split ? r : 1) * (uint64_t)(lng ? kOddEdgeSlotsLong : kOddEdgeSlots);
     const int grid = (int)std::min<uint64_t>((total + kBlockThreads - 1) / kBlockThreads, 4096);
-    const void* fn = split ? (mode == kOddVerify ? (const void*)&gf_odd_edges<kOddVerify, true>
-                                                 : (mode == kOddAcc ? (const void*)&gf_odd_edges<kOddAcc, true>
-                                                                    : (const void*)&gf_odd_edges<kOddApply, true>))
-                           : (mode == kOddVerify ? (const void*)&gf_odd_edges<kOddVerify, false>
-                                                 : (mode == kOddAcc ? (const void*)&gf_odd_edges<kOddAcc, false>
-                                                                    : (const void*)&gf_odd_edges<kOddApply, false>));
+    const void* fns[3][2][2] = {
+        {{(const void*)&gf_odd_edges<kOddApply, false, kOddEdgeSlots>, (const void*)&gf_odd_edges<kOddApply, false, kOddEdgeSlotsLong>},
+         {(const void*)&gf_odd_edges<kOddApply, true, kOddEdgeSlots>, (const void*)&gf_odd_edges<kOddApply, true, kOddEdgeSlotsLong>}},
+        {{(const void*)&gf_odd_edges<kOddAcc, false, kOddEdgeSlots>, (const void*)&gf_odd_edges<kOddAcc, false, kOddEdgeSlotsLong>},
+         {(const void*)&gf_odd_edges<kOddAcc, true, kOddEdgeSlots>, (const void*)&gf_odd_edges<kOddAcc, true, kOddEdgeSlotsLong>}},
+        {{(const void*)&gf_odd_edges<kOddVerify, false, kOddEdgeSlots>, (const void*)&gf_odd_edges<kOddVerify, false, kOddEdgeSlotsLong>},
+         {(const void*)&gf_odd_edges<kOddVerify, true, kOddEdgeSlots>, (const void*)&gf_odd_edges<kOddVerify, true, kOddEdgeSlotsLong>}}};
+    const void* fn = fns[mode][split ? 1 : 0][lng ? 1 : 0];
     void* args[] = {const_cast<PassArgs*>(&a), &k, &r, &flags};
     return hipLaunchKernel(fn, dim3(grid), dim3(kBlockThreads), args, 0, stream);
 }

@@ -49,6 +49,7 @@ __host__ __device__ constexpr uint32_t odd_tile_span() {
 }
 constexpr int32_t kOddGuard = 48;             // bytes at each end left to gf_odd_edges
 constexpr int32_t kOddEdgeSlots = 160;        // edge bytes handled per (shard, output): 80 head + 80 tail
+constexpr int32_t kOddEdgeSlotsLong = 128;    // the same for S > kOddMinMain: 64 head + 64 tail
 // gf_odd_edges: a thread per (object, output, slot) below this many objects
 // (latency-bound launches), per (object, slot) for every output above
 constexpr uint64_t kOddEdgeSplitObjs = 1024;
