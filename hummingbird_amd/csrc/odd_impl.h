@@ -75,13 +75,15 @@ constexpr int kOddPlanU = HBEC_ODD_PLAN_U;  // plans: windows per record (tuning
 __host__ __device__ constexpr bool odd_rec_carry(int u, int mode) { return mode != kOddVerify && u >= 2; }
 // Strided batches code from object records (gf_odd_rec) when they carry at
 // least 18 products per column (6+3, 7+3, 8+3, 10+4, 12+4 encode), and for
-// K > 8 with at least 3 outputs; gf_odd below: the per-tile base arithmetic
+// K > 8 from 24 (3-4 outputs, and 12 x 2: tuning.h); gf_odd below: the per-tile base arithmetic
 // the records remove only showed where the field arithmetic already filled
 // the issue slots (round-4 A/B, profiles/r04_ab_odd.jsonl: 6+3 encode 62.9 ->
 // 66.9 %, 7+3 55.2 -> 60.5 %, 8+3 59.3 -> 64.5 %, 12+4 51.2 -> 57.3 %; for
 // gf_odd: 4+2 encode 70.5 vs 67.6 %, 6+2 68.4 vs 67.4 %, 8+2 66.2 vs 65.0 %,
 // 10+2 65.8 vs 60.6 %, the last against the LDS-table record kernel).
-__host__ __device__ constexpr bool odd_use_rec(int k, int r) { return k * r >= HBEC_ODD_REC_MINKR && (k <= 8 || r >= 3); }
+__host__ __device__ constexpr bool odd_use_rec(int k, int r) {
+    return k * r >= HBEC_ODD_REC_MINKR && (k <= 8 || k * r >= HBEC_ODD_REC_BIGK_MINKR);
+}
 // shard bytes per wave tile of the record kernel
 __host__ __device__ constexpr uint32_t odd_rec_span(int u, int mode) {
     return odd_rec_carry(u, mode) ? (64u * (uint32_t)(u - 1) + kOddStore) * 16u
