@@ -136,9 +136,8 @@
 #endif
 #ifndef HBEC_ODD_REC_BIGK_MINKR
 // 9 <= k <= 12: the record kernel (LDS tables) from K R >= 24, i.e. every
-// 3-4-output pass and 12 x 2 (12+4 reconstruct {0,1} 53.3 -> 57.4 % on one
-// box, 63.3 -> 62.4 % on another: r05_ab_rr2.jsonl, r05_ab_regress.jsonl);
-// 9-11 inputs x 2 outputs stay on gf_odd (10+4 reconstruct 66.2 vs 58.3 %,
+// 3-4-output pass and 12 x 2 (12+4 reconstruct {0,1} 53.3 -> 57.4 %); 9-11
+// inputs x 2 outputs stay on gf_odd (10+4 reconstruct 66.2 vs 58.3 %,
 // 9+3 66.8 vs 60.1 %, 10+2 66.7 vs 61.1 %; r05_ab_rr2.jsonl)
 #define HBEC_ODD_REC_BIGK_MINKR 24
 #endif
