@@ -6,12 +6,13 @@ KERNEL_SOURCES / ODD_SOURCES, including tuning.h): an edit to any of them
 after the last `scripts/r5_final.sh first` silently drops those fields from
 the driver's bench line.  This test makes that visible before the round ends.
 """
-
 import bench
+
 
 def test_headline_pmc_summary_is_fresh():
     data, path, why = bench.load_pmc()
     assert data is not None, why
+
 
 def test_odd_pmc_summary_is_fresh():
     data, path, why = bench.load_pmc()
