@@ -569,7 +569,7 @@ def random_objects(n=4096, shapes=((4, 2), (8, 3)), reps=20, settle=40):
             kern = pmc.get("kernels", {})
             kname, t = _odd_kernel_traffic(kern, k, m, 0, plan=True)
             extra = sum((kern.get(x, {}).get("hbm_bytes_per_launch") or 0)
-                        for x in ("gf_odd_edges_plan<0, false>", "gf_odd_planrec"))
+                        for x in ("gf_odd_edges_plan<0, false, 128>", "gf_odd_planrec"))
             if t is not None:
                 leg["kernel"] = kname
                 leg["traffic"] = int(t + extra)

@@ -115,6 +115,7 @@ struct OddStripeRecs {
     const URec* recs = nullptr;
     uint64_t n = 0, s_max = 0;
     OddTileList lists[kOddSpans];
+    bool edges_long = false;  // every edge record's S > kOddMinMain (64 + 64 edge slots)
 };
 // the distinct odd_rec_tile_span values of apply / accumulate passes
 void odd_plan_spans(uint32_t (&spans)[kOddSpans]);

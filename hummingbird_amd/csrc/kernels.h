@@ -185,8 +185,9 @@ hipError_t launch_odd_edges(int k, int r, int mode, const PassArgs& a, uint32_t*
 // plan records: URec.p0 = first window * 992 (records cover positions [0, S + 32)),
 // only for stripes longer than odd_min_main(); plus one edge record per stripe
 hipError_t launch_odd_plan(int k, int r, int mode, const UPlanArgs& p, int grid, hipStream_t stream);
+// lng: every record's S > kOddMinMain (the 64 + 64-slot kernel)
 hipError_t launch_odd_edges_plan(int k, int r, int mode, const UPlanArgs& p, const URec* erecs, uint32_t n_erecs,
-                                 hipStream_t stream);
+                                 hipStream_t stream, bool lng = false);
 // Mirrored plans: copy shard bytes the main kernel does not mirror (the guard
 // band, full = 0; whole shards, full = 1) from each edge record's stripe
 // (rec.a) to its arena (rec.b), for shards idx[0 .. n_idx).

@@ -187,23 +187,23 @@ __global__ __launch_bounds__(kBlockThreads) void gf_odd_edges(PassArgs a, int K,
 }
 
 // plans: one edge record per stripe / object (URec, p0 unused)
-template <int MODE, bool SPLIT>
+template <int MODE, bool SPLIT, int SLOTS>
 __global__ __launch_bounds__(kBlockThreads) void gf_odd_edges_plan(UPlanArgs p, const URec* __restrict__ erecs,
                                                                   uint32_t n_erecs, int K, int R) {
-    const uint64_t per = (uint64_t)(SPLIT ? R : 1) * kOddEdgeSlots;
+    const uint64_t per = (uint64_t)(SPLIT ? R : 1) * SLOTS;
     const uint64_t total = (uint64_t)n_erecs * per;
     for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < total; v += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t e = (uint32_t)(v / per);
         const uint32_t rs = (uint32_t)(v - (uint64_t)e * per);
-        const uint32_t g = rs / (uint32_t)kOddEdgeSlots;
-        const int32_t slot = (int32_t)(rs - g * (uint32_t)kOddEdgeSlots);
+        const uint32_t g = rs / (uint32_t)SLOTS;
+        const int32_t slot = (int32_t)(rs - g * (uint32_t)SLOTS);
         const URec rec = erecs[e];
         const uint64_t S = rec.shard_len;
         uint64_t in[kMaxK], out[kMaxR];
         for (int j = 0; j < K; ++j) in[j] = (((p.in_sel >> j) & 1u) ? rec.b : rec.a) + (uint64_t)p.in_idx[j] * S;
         for (int r = 0; r < R; ++r) out[r] = (((p.out_sel >> r) & 1u) ? rec.b : rec.a) + (uint64_t)p.out_idx[r] * S;
-        odd_edge_all<MODE>(p.tab, K, SPLIT ? (int)g : 0, SPLIT ? (int)g + 1 : R, in, out, out[0], (int32_t)S, slot,
-                           nullptr);
+        odd_edge_all<MODE, SLOTS>(p.tab, K, SPLIT ? (int)g : 0, SPLIT ? (int)g + 1 : R, in, out, out[0], (int32_t)S,
+                                  slot, nullptr);
     }
 }
 
@@ -455,16 +455,18 @@ hipError_t launch_odd_edges(int k, int r, int mode, const PassArgs& a, uint32_t*
 }
 
 hipError_t launch_odd_edges_plan(int k, int r, int mode, const UPlanArgs& p, const URec* erecs, uint32_t n_erecs,
-                                 hipStream_t stream) {
+                                 hipStream_t stream, bool lng) {
     if (n_erecs == 0) return hipSuccess;
     if (k < 1 || k > kMaxK || r < 1 || r > kMaxR || mode == kOddVerify) return hipErrorInvalidValue;
     const bool split = n_erecs < kOddEdgeSplitObjs;
-    const uint64_t total = (uint64_t)n_erecs * (uint64_t)(split ? r : 1) * kOddEdgeSlots;
+    const uint64_t total = (uint64_t)n_erecs * (uint64_t)(split ? r : 1) * (uint64_t)(lng ? kOddEdgeSlotsLong : kOddEdgeSlots);
     const int grid = (int)std::min<uint64_t>((total + kBlockThreads - 1) / kBlockThreads, 4096);
-    const void* fn = split ? (mode == kOddAcc ? (const void*)&gf_odd_edges_plan<kOddAcc, true>
-                                              : (const void*)&gf_odd_edges_plan<kOddApply, true>)
-                           : (mode == kOddAcc ? (const void*)&gf_odd_edges_plan<kOddAcc, false>
-                                              : (const void*)&gf_odd_edges_plan<kOddApply, false>);
+    const void* fns[2][2][2] = {
+        {{(const void*)&gf_odd_edges_plan<kOddApply, false, kOddEdgeSlots>, (const void*)&gf_odd_edges_plan<kOddApply, false, kOddEdgeSlotsLong>},
+         {(const void*)&gf_odd_edges_plan<kOddApply, true, kOddEdgeSlots>, (const void*)&gf_odd_edges_plan<kOddApply, true, kOddEdgeSlotsLong>}},
+        {{(const void*)&gf_odd_edges_plan<kOddAcc, false, kOddEdgeSlots>, (const void*)&gf_odd_edges_plan<kOddAcc, false, kOddEdgeSlotsLong>},
+         {(const void*)&gf_odd_edges_plan<kOddAcc, true, kOddEdgeSlots>, (const void*)&gf_odd_edges_plan<kOddAcc, true, kOddEdgeSlotsLong>}}};
+    const void* fn = fns[mode == kOddAcc ? 1 : 0][split ? 1 : 0][lng ? 1 : 0];
     void* args[] = {const_cast<UPlanArgs*>(&p), &erecs, &n_erecs, &k, &r};
     return hipLaunchKernel(fn, dim3(grid), dim3(kBlockThreads), args, 0, stream);
 }

@@ -234,7 +234,8 @@ int hbec::launch_unaligned_passes(const URec* recs, uint64_t n_recs, const std::
                     if (e != hipSuccess) return hip_fail(e, "launch gf_odd_plan");
                 }
                 // guard-band bytes of every stripe, this pass's inputs
-                e = hbec::launch_odd_edges_plan(K, R, c0 > 0 ? 1 : 0, a, erecs, (uint32_t)n_erecs, stream);
+                e = hbec::launch_odd_edges_plan(K, R, c0 > 0 ? 1 : 0, a, erecs, (uint32_t)n_erecs, stream,
+                                                orecs && orecs->edges_long);
                 if (e != hipSuccess) return hip_fail(e, "launch gf_odd_edges_plan");
             }
         }
@@ -473,6 +474,8 @@ int hbec_plan_stripes(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n,
         }
         p->n_urecs = urecs.size();
         p->n_erecs = erecs.size();
+        p->orecs.edges_long = std::all_of(erecs.begin(), erecs.end(),
+                                          [](const hbec::URec& e) { return e.shard_len > hbec::odd_min_main(); });
         p->n_brecs = brecs.size();
         *out = p.release();
         return HBEC_OK;
@@ -547,6 +550,8 @@ int hbec_plan_objects(hbec_codec* codec, const hbec_object* objects, uint64_t n,
         }
         p->n_urecs = urecs.size();
         p->n_erecs = erecs.size();
+        p->orecs.edges_long = std::all_of(erecs.begin(), erecs.end(),
+                                          [](const hbec::URec& e) { return e.shard_len > hbec::odd_min_main(); });
         p->n_brecs = brecs.size();
         *out = p.release();
         return HBEC_OK;

@@ -20,5 +20,5 @@ def test_odd_pmc_summary_is_fresh():
     assert data.get("odd_sources_sha256") == bench.kernel_sources_sha256(bench.ODD_SOURCES), (
         f"{path} was collected on other odd-kernel sources: rerun scripts/r5_final.sh first")
     # the odd legs read these kernels' bytes from it
-    for name in ("gf_odd_edges<0, false, 128>", "gf_odd_edges<2, false, 128>", "gf_odd_edges_plan<0, false>"):
+    for name in ("gf_odd_edges<0, false, 128>", "gf_odd_edges<2, false, 128>", "gf_odd_edges_plan<0, false, 128>"):
         assert name in data["kernels"], name
