@@ -7,6 +7,8 @@ rebuilt shard and every Verify flag is checked against the oracle
 27,59,111), so whichever kernel a case lands on — packed, pipelined,
 streaming, gf_odd, gf_odd_rec tables or bit-plane, gf_wide — it must agree.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -33,7 +35,8 @@ def _case(seed):
     return k, m, s, off, pad, rng
 
 
-@pytest.mark.parametrize("seed", range(96))
+# HBEC_FUZZ_SEEDS widens a one-off run (2000 seeds: profiles/r05_gpu_fuzz_route.txt)
+@pytest.mark.parametrize("seed", range(int(os.environ.get("HBEC_FUZZ_SEEDS", "96"))))
 def test_fuzz_routes_against_oracle(seed):
     k, m, s, off, pad, rng = _case(seed)
     n = max(2, min(12, 2_500_000 // ((k + m) * s)))
