@@ -81,7 +81,7 @@ def main():
             _, k, m, s, di, do_ = name.split(":")
             k, m, s, di, do_ = int(k), int(m), int(s), int(di), int(do_)
             op = "skew"
-        elif name.startswith("c:"):  # custom: c:K:M:S:OP (OP enc / rec / ver / plan)
+        elif name.startswith("c:"):  # custom: c:K:M:S:OP (OP enc / rec / ver / plan / dplan / dplanp)
             _, k, m, s, op = name.split(":")
             k, m, s = int(k), int(m), int(s)
         else:
@@ -138,11 +138,14 @@ def main():
             row["ok"] = check(enc, views, s)
             row["DI"], row["DO"] = di, do_
             del din, dout, views
-        elif op == "dplan":
-            # the databuf layout of "enc" (shard i at row + i S) coded through an object plan
+        elif op in ("dplan", "dplanp"):
+            # the databuf layout of "enc" (shard i at row + i S) coded through an object plan;
+            # dplanp: objects listed in the order 0, n/2, 1, n/2 + 1, ... (concurrent waves
+            # on rows half the batch apart)
             rows, views = databuf(k, m, s)
+            order = list(range(n)) if op == "dplan" else [i // 2 + (n // 2) * (i % 2) for i in range(n)]
             plan = B.StripePlan(enc, objects=[(rows.data_ptr() + i * rows.stride(0),
-                                               rows.data_ptr() + i * rows.stride(0) + k * s, s) for i in range(n)])
+                                               rows.data_ptr() + i * rows.stride(0) + k * s, s) for i in order])
             ms = timeit(plan.encode)
             nb = n * (k + m) * s
             row["ok"] = check(enc, views, s)
