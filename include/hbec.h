@@ -253,6 +253,10 @@ typedef struct {
 } hbec_object;
 int hbec_plan_objects(hbec_codec* codec, const hbec_object* objects, uint64_t n_objects, hbec_plan** out);
 void hbec_plan_free(hbec_plan* plan);
+/* n_tiles / tile_bytes: the aligned stripes' tile records; n_fallback: the
+ * stripes (objects with k <= 8) coded by the any-alignment record kernels
+ * instead — unaligned ones, and aligned ones those kernels code faster
+ * (hbec.cpp rec_route). */
 int hbec_plan_info(const hbec_plan* plan, uint64_t* n_tiles, int* tile_bytes, uint64_t* n_fallback,
                    uint64_t* shard_bytes);
 /* Encode every stripe of the plan (parity shards k..k+m-1 written). */
