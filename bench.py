@@ -18,11 +18,13 @@ data-path collective; torch.distributed carries only the barrier and the
 max-time reduction.
 
 Extra objects on the JSON line: `roofline` (dominant kernel = the
-gf_apply_vec_pipe2<4,2> kernel that both ops launch; achieved = algorithmic bytes per
-launch / its HIP-event-timed average launch duration on the launch stream;
-traffic = PMC HBM bytes per launch from the committed rocprofv3 summary
-profiles/*_pmc.json, used only when that file was collected on the kernel
-sources being run -- same sha256 -- else null), `cpu_baseline`
+gf_apply_vec_pipe2<4,2> kernel that both ops launch, as `dispatches_per_op`
+dispatches of 1024 objects each (tuning.h HBEC_VEC_CHUNK_TILES); achieved =
+algorithmic bytes per op / the op's HIP-event-timed average duration on the
+launch stream, i.e. the summed dispatch times plus the gaps between them;
+traffic = PMC HBM bytes per dispatch from the committed rocprofv3 summary
+profiles/*_pmc.json times the dispatches per op, used only when that file was
+collected on the kernel sources being run -- same sha256 -- else null), `cpu_baseline`
 (oracle/gf_oracle.c's AVX2 port of klauspost's algorithm over the host cores
 on a bounded sample, rank 0 at N=1) and `config5` (BASELINE configs[4]: a
 65 536 x 1 MiB 4+2 batch partitioned contiguously over the N ranks, encoded
@@ -117,6 +119,16 @@ def kernel_sources_sha256(sources=KERNEL_SOURCES) -> str:
 ODD_SOURCES = ("hummingbird_amd/csrc/odd.hip", "hummingbird_amd/csrc/odd_impl.h", "hummingbird_amd/csrc/gf_device.h",
                "hummingbird_amd/csrc/kernels.h", "hummingbird_amd/csrc/odd_k58.hip", "hummingbird_amd/csrc/odd_k912.hip",
                "hummingbird_amd/csrc/tuning.h", "hummingbird_amd/csrc/odd_bp.hip", "hummingbird_amd/csrc/xor_sched.h")
+
+
+def vec_chunk_tiles() -> int:
+    """Tiles per launch of the aligned strided kernels (tuning.h
+    HBEC_VEC_CHUNK_TILES): a batch runs as launches of whole objects."""
+    for line in (ROOT / "hummingbird_amd/csrc/tuning.h").read_text().splitlines():
+        parts = line.split()
+        if len(parts) >= 3 and parts[0] == "#define" and parts[1] == "HBEC_VEC_CHUNK_TILES":
+            return int(parts[2])
+    raise RuntimeError("HBEC_VEC_CHUNK_TILES not in tuning.h")
 
 
 def load_pmc(prefix_glob="profiles/r[0-9][0-9]_pmc.json"):
@@ -582,6 +594,147 @@ def random_objects(n=4096, shapes=((4, 2), (8, 3)), reps=20, settle=40):
     return out
 
 
+def _plan_traffic(kern, k, r, paths):
+    """PMC bytes per launch of a plan pass's record kernel (the bit-plane or
+    the table instance, by which one the pass launched: `paths` is
+    B.odd_path_stats() after minus before) plus its record and edge kernels."""
+    names = sorted(x for x in kern if x.startswith(f"gf_odd_rec<{k}, {r}, 0, ") and x.endswith("true>"))
+    bp = [x for x in names if not x.startswith(f"gf_odd_rec<{k}, {r}, 0, -1,")]
+    tab = [x for x in names if x.startswith(f"gf_odd_rec<{k}, {r}, 0, -1,")]
+    pick = bp if paths[0] > 0 else tab
+    if len(pick) != 1:
+        return None, None
+    extra = sum((kern.get(x, {}).get("hbm_bytes_per_launch") or 0)
+                for x in ("gf_odd_edges_plan<0, false, 128>", "gf_odd_planrec"))
+    t = kern[pick[0]].get("hbm_bytes_per_launch")
+    return pick[0], None if t is None else t + extra
+
+
+def mid_objects(n=16384, shapes=((4, 2), (8, 3)), reps=20, settle=40):
+    """Mid-size objects, the size class most object stores hold (VERDICT r05
+    item 1): n objects with lengths log-uniform in [8 KiB, 128 KiB] (seeded),
+    S = ceil(len / k) (ecutils.go:14-24) forced odd, so every shard sits at an
+    odd offset.  Per shape, the same objects in two layouts, one plan each:
+    ecSplit databufs back to back (hbec_plan_stripes: shard i at base + i S,
+    ecutils.go:31-35) and an object plan (data arena + parity arena,
+    hbec_plan_objects).  Encode is timed over `reps` launches after `settle`;
+    every 16th object is then checked with the product's Verify, and the -m
+    gpu tests compare such plans with the oracle byte for byte.  `aligned_32k`:
+    the same n objects at exactly 32 KiB, 8+3 (S = 4096), as a strided batch
+    (the packed kernel), Encode / Reconstruct {0,1,2} / Verify.  HBM traffic
+    per launch from the committed PMC summary when it was collected on these
+    sources."""
+    import numpy as np
+
+    pmc_files = sorted(glob.glob(str(ROOT / "profiles/r[0-9][0-9]_pmc.json")))
+    pmc = json.loads(Path(pmc_files[-1]).read_text()) if pmc_files else {}
+    fresh = pmc.get("odd_sources_sha256") == kernel_sources_sha256(ODD_SOURCES)
+    kern = pmc.get("kernels", {}) if fresh else {}
+    stream = torch.cuda.current_stream()
+
+    def timed(fn):
+        for _ in range(settle):
+            fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            fn()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps
+
+    out = {"workload": f"{n} objects of log-uniform length in [8 KiB, 128 KiB], S = ceil(len/k) forced odd, "
+                       "device-resident, Encode; ecSplit databufs (stripe plan) and data + parity arenas "
+                       "(object plan)", "shapes": {}}
+    for k, m in shapes:
+        rng = np.random.default_rng(0x4D494430 + 100 * k + m)
+        lens = np.exp(rng.uniform(np.log(8 << 10), np.log(128 << 10), n))
+        sizes = [int(-(-int(x) // k)) | 1 for x in lens]
+        nbytes = sum((k + m) * s for s in sizes)
+        enc = RS.New(k, m)
+        legs = {}
+        for layout in ("databuf", "object_plan"):
+            if layout == "databuf":
+                arena = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+                B.fill_splitmix(arena.view(1, -1), arena.numel(), first=31 * k + m)
+                stripes, off = [], 0
+                for s in sizes:
+                    stripes.append((arena.data_ptr() + off, s))
+                    off += (k + m) * s
+                plan = B.StripePlan(enc, stripes=stripes)
+                views_of = [([(b + j * s, 0) for j in range(k + m)], s) for b, s in stripes]
+                keep = (arena,)
+            else:
+                data = torch.empty(sum(k * s for s in sizes), dtype=torch.uint8, device="cuda")
+                B.fill_splitmix(data.view(1, -1), data.numel(), first=37 * k + m)
+                parity = torch.empty(sum(m * s for s in sizes), dtype=torch.uint8, device="cuda")
+                objs, do, po = [], 0, 0
+                for s in sizes:
+                    objs.append((data.data_ptr() + do, parity.data_ptr() + po, s))
+                    do += k * s
+                    po += m * s
+                plan = B.StripePlan(enc, objects=objs)
+                views_of = [([(a + j * s, 0) for j in range(k)] + [(b + r * s, 0) for r in range(m)], s)
+                            for a, b, s in objs]
+                keep = (data, parity)
+            p0 = B.odd_path_stats()
+            plan.encode()
+            torch.cuda.synchronize()
+            p1 = B.odd_path_stats()
+            paths = [p1[x] - p0[x] for x in ("bitplane", "records", "strided")]
+            ms = timed(plan.encode)
+            gbs = nbytes / (ms * 1e-3) / 1e9
+            flags = torch.zeros(1, dtype=torch.int32, device="cuda")
+            for views, s in views_of[::16]:
+                B.verify_views(enc, views, 1, s, flags)
+            torch.cuda.synchronize()
+            leg = {"objects": n, "bytes": nbytes, "ms": round(ms, 4), "GB_s": round(gbs, 1),
+                   "frac": round(gbs / HBM_PEAK_GBS, 4), "parity_ok": int(flags.item()) == 0,
+                   "launches": {"bitplane": paths[0], "records": paths[1], "strided": paths[2]}}
+            if kern:
+                kname, t = _plan_traffic(kern, k, m, paths)
+                if t is not None:
+                    leg["kernel"] = kname
+                    leg["traffic"] = int(t)
+                    leg["traffic_ratio"] = round(t / nbytes, 4)
+            legs[layout] = leg
+            del plan, keep, flags
+            torch.cuda.empty_cache()
+        out["shapes"][f"{k}+{m}"] = legs
+    # exact 32 KiB 8+3 objects (aligned S = 4096): a strided batch
+    k, m, s = 8, 3, 4096
+    enc = RS.New(k, m)
+    objs = torch.empty((n, k * s), dtype=torch.uint8, device="cuda")
+    B.fill_splitmix(objs, k * s, first=41)
+    par = torch.empty((n, m * s), dtype=torch.uint8, device="cuda")
+    rebuilt = torch.empty((n, m * s), dtype=torch.uint8, device="cuda")
+    flags = torch.zeros(n, dtype=torch.int32, device="cuda")
+    views = B.shard_views(objs, k, s) + B.shard_views(par, m, s)
+    rv = list(views)
+    for slot in range(m):
+        rv[slot] = (rebuilt.data_ptr() + slot * s, rebuilt.stride(0))
+    present = [0] * m + [1] * k
+    al = {"workload": f"{n} x 32 KiB objects, 8+3 (S = 4096), strided batch", "shard_bytes": s,
+          "kernel_kind": B.kernel_info(k, m, s)["kind"]}
+    for name, fn in (("encode", lambda: B.encode_views(enc, views, n, s)),
+                     ("reconstruct", lambda: B.reconstruct_views(enc, rv, present, n, s)),
+                     ("verify", lambda: B.verify_views(enc, views, n, s, flags))):
+        ms = timed(fn)
+        gbs = n * (k + m) * s / (ms * 1e-3) / 1e9
+        al[name] = {"ms": round(ms, 4), "GB_s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
+    ok = int(flags.count_nonzero()) == 0
+    for slot in range(m):
+        ok = ok and torch.equal(rebuilt[:, slot * s:(slot + 1) * s], objs[:, slot * s:(slot + 1) * s])
+    al["parity_ok"] = bool(ok)
+    out["aligned_32k"] = al
+    del objs, par, rebuilt, flags
+    torch.cuda.empty_cache()
+    out["traffic_source"] = os.path.relpath(pmc_files[-1], ROOT) if (pmc_files and fresh) else None
+    out["parity_ok"] = al["parity_ok"] and all(v["parity_ok"] for legs in out["shapes"].values()
+                                               for v in legs.values())
+    return out
+
+
 def config4(n=4096, reps=20, settle=40):
     """BASELINE configs[3]: 8+3 Encode + Reconstruct{0,1,2} of n objects of
     4 KiB or 1 MiB (p = 0.5 each, by the splitmix64 byte stream of the base
@@ -833,14 +986,19 @@ def main(argv=None):
 
     line = None
     if rank == 0:
-        launch_bytes = w.enc_bytes  # == rec_bytes for 2 erasures
-        avg_launch_ms = (enc_ms + rec_ms) / 2
-        achieved = launch_bytes / (avg_launch_ms * 1e-3) / 1e9
-        pmc, pmc_file, pmc_reject = load_pmc()
-        traffic = None
-        if pmc and KERNEL_NAME in pmc.get("kernels", {}):
-            traffic = pmc["kernels"][KERNEL_NAME].get("hbm_bytes_per_launch")
+        op_bytes = w.enc_bytes  # == rec_bytes for 2 erasures
+        avg_op_ms = (enc_ms + rec_ms) / 2
+        achieved = op_bytes / (avg_op_ms * 1e-3) / 1e9
         info = B.kernel_info(k, m, w.s)
+        # each op is `disp` dispatches of the kernel, whole objects each
+        tpo = -(-w.s // info["tile_bytes"])
+        per_disp = max(1, vec_chunk_tiles() // tpo)
+        disp = -(-n // per_disp)
+        pmc, pmc_file, pmc_reject = load_pmc()
+        traffic = traffic_disp = None
+        if pmc and KERNEL_NAME in pmc.get("kernels", {}):
+            traffic_disp = pmc["kernels"][KERNEL_NAME].get("hbm_bytes_per_launch")
+            traffic = None if traffic_disp is None else traffic_disp * disp
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -871,9 +1029,14 @@ def main(argv=None):
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "kernel": KERNEL_NAME,
-                "bytes_per_launch": launch_bytes,
-                "encode_ms_per_launch": round(enc_ms, 4),
-                "reconstruct_ms_per_launch": round(rec_ms, 4),
+                "bytes_per_op": op_bytes,
+                "dispatches_per_op": disp,
+                "objects_per_dispatch": min(per_disp, n),
+                "bytes_per_dispatch": op_bytes // disp,
+                "traffic_per_dispatch": traffic_disp,
+                "encode_ms_per_op": round(enc_ms, 4),
+                "reconstruct_ms_per_op": round(rec_ms, 4),
+                "ms_per_dispatch": round(avg_op_ms / disp, 4),
                 "traffic_source": pmc_file if traffic is not None else None,
                 "traffic_note": pmc_reject,
                 "kernel_sources_sha256": kernel_sources_sha256(),
@@ -881,8 +1044,8 @@ def main(argv=None):
                 "blocks_per_cu": info["blocks_per_cu"],
                 # N > 1: each rank's own launches (the fields above use the max over ranks)
                 "per_rank": None if per_rank is None else [
-                    {"rank": r, "encode_ms_per_launch": round(e, 4), "reconstruct_ms_per_launch": round(c, 4),
-                     "frac": round(launch_bytes / ((e + c) / 2 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+                    {"rank": r, "encode_ms_per_op": round(e, 4), "reconstruct_ms_per_op": round(c, 4),
+                     "frac": round(op_bytes / ((e + c) / 2 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
                     for r, (e, c) in enumerate(per_rank)],
             },
             "object_data_gib_s": round(value * k / (k + m), 2),
@@ -919,6 +1082,10 @@ def main(argv=None):
             line["random_objects"] = random_objects()
         except Exception as e:  # noqa: BLE001 - reported; never blocks the other ranks
             line["random_objects"] = {"error": f"{type(e).__name__}: {e}"[:200]}
+        try:
+            line["mid_objects"] = mid_objects()
+        except Exception as e:  # noqa: BLE001 - reported; never blocks the other ranks
+            line["mid_objects"] = {"error": f"{type(e).__name__}: {e}"[:200]}
     if world > 1 and backend == "nccl" and args.split_objects > 0:
         split = batch_split(pg, k, m, obj_len, args.split_objects, world, rank, ctl_device)
         if rank == 0:

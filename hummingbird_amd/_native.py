@@ -105,6 +105,7 @@ _SIG = [
     ("hbec_batcher_reconstruct", C.c_int, [_P, C.POINTER(Stripe), _U8P, C.c_int]),
     ("hbec_batcher_stats", C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     ("hbec_set_force_stream", C.c_int, [C.c_int]),
+    ("hbec_set_odd_chunk_tiles", C.c_int, [C.c_uint64]),
     ("hbec_kernel_info", C.c_int,
      [C.c_int, C.c_int, C.c_uint64, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     ("hbec_odd_path_stats", C.c_int, [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),

@@ -155,5 +155,10 @@ def odd_path_stats():
     return {"bitplane": b.value, "records": r.value, "strided": s.value}
 
 
+def set_odd_chunk_tiles(tiles: int) -> None:
+    """Test hook: odd-shard strided launches of at most `tiles` tiles (0 = default)."""
+    N.lib().hbec_set_odd_chunk_tiles(int(tiles))
+
+
 def set_force_stream(on: bool) -> None:
     N.lib().hbec_set_force_stream(1 if on else 0)

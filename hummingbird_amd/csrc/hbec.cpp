@@ -81,6 +81,18 @@ static const uint64_t g_chunk_tiles = [] {
     const long long v = tune_knob("HBEC_CHUNK_TILES", 0);
     return (uint64_t)(v > 0 ? v : (1ll << 20));
 }();
+// test hook (hbec_set_odd_chunk_tiles): the odd strided kernels' launch size
+static std::atomic<uint64_t> g_odd_chunk_override{0};
+static uint64_t odd_chunk_tiles() {
+    const uint64_t v = g_odd_chunk_override.load(std::memory_order_relaxed);
+    return v ? v : g_chunk_tiles;
+}
+// the aligned strided (vec / pipelined) kernels' launches (tuning.h
+// HBEC_VEC_CHUNK_TILES; a tuning build's HBEC_CHUNK_TILES overrides both)
+static const uint64_t g_vec_chunk_tiles = [] {
+    const long long v = tune_knob("HBEC_VEC_CHUNK_TILES", tune_knob("HBEC_CHUNK_TILES", 0));
+    return (uint64_t)(v > 0 ? v : HBEC_VEC_CHUNK_TILES);
+}();
 
 // ---------------------------------------------------------------------------
 // Per-device facts (CU count, occupancy per kernel shape)
@@ -158,6 +170,10 @@ static int odd_launches(const PassArgs& a, int K, int R, int mode, bool accumula
     int cus = 0;
     int rc = cu_count(dev, &cus);
     if (rc) return rc;
+    // the main kernel codes the guard band too (HBEC_ODD_EDGE_FUSE): one
+    // apply launch group whose shards span >= 2 tiles (the edge tiles are
+    // each shard's first and last)
+    bool fused = false;
     if (shard_len > odd_min_main()) {
         for (int c1 = 0; c1 < K; c1 += kOddMaxK) {
             const int K1 = std::min(kOddMaxK, K - c1);
@@ -176,7 +192,7 @@ static int odd_launches(const PassArgs& a, int K, int R, int mode, bool accumula
             const int xs = odd_bp_schedule(K1, R, m, b.tab, false);
             const bool use_rec = xs >= 0 || ((m != 2 || K1 > 8) && odd_uses_records(K1, R));
             const uint64_t tpo = odd_tiles_per_obj(K1, m, shard_len, use_rec, xs);
-            const uint64_t max_obj = std::max<uint64_t>(1, std::min<uint64_t>((1ull << 31), g_chunk_tiles) / tpo);
+            const uint64_t max_obj = std::max<uint64_t>(1, std::min<uint64_t>((1ull << 31), odd_chunk_tiles()) / tpo);
             // per-object records of one launch's objects (stream-ordered
             // scratch of at most max_obj records, rebuilt per launch, freed
             // after the pass): device memory bounded by the chunk, not the batch
@@ -202,6 +218,9 @@ static int odd_launches(const PassArgs& a, int K, int R, int mode, bool accumula
                 }
                 c.tiles_per_obj = (uint32_t)tpo;
                 c.n_tiles = (uint32_t)(no * tpo);
+                c.fuse = odd_edge_fuse(K1, R, m, use_rec, xs) && K <= kOddMaxK && tpo >= 2 &&
+                                 shard_len < (1ull << 30) ? 1u : 0u;
+                fused = c.fuse != 0u;
                 const uint64_t wpb = odd_waves_per_block(xs);
                 const uint64_t want = (c.n_tiles + wpb - 1) / wpb;
                 const uint64_t cap = (uint64_t)cus * (uint64_t)odd_blocks_per_cu(m, K1, R, false, use_rec, xs);
@@ -220,6 +239,7 @@ static int odd_launches(const PassArgs& a, int K, int R, int mode, bool accumula
     // (on a second stream beside the main kernel this ran 0.6-3 points
     // slower, the scattered edge lines disturbing the main stream; before the
     // main kernel, within +-1: r05_ab_edges.jsonl)
+    if (fused) return HBEC_OK;
     PassArgs g = a;
     g.n_obj = n_obj;
     g.shard_len = shard_len;
@@ -285,7 +305,9 @@ int apply_views(int rows, int cols, const uint8_t* coeffs, const hbec_view* in, 
     bool line = vec && shard_len % 128 == 0;
     for (int c = 0; c < cols && line; ++c) line = line_aligned(in[c].base, in[c].obj_stride);
     for (int r = 0; r < rows && line; ++r) line = line_aligned(out[r].base, out[r].obj_stride);
-    const bool to_rec = vec && rec_route(cols, rows, shard_len, line, bitplane_rows(cols, rows, coeffs, cols, false));
+    // the schedule match only where it can change the route (rec_route with and without it differ)
+    const bool to_rec = vec && rec_route(cols, rows, shard_len, line, true) &&
+                        (rec_route(cols, rows, shard_len, line, false) || bitplane_rows(cols, rows, coeffs, cols, false));
     for (int c = 0; c < cols; ++c)
         if (!in[c].base) return fail(HBEC_ERR_INVALID_ARG, "apply: null input view");
     for (int r = 0; r < rows; ++r)
@@ -351,8 +373,8 @@ int apply_views(int rows, int cols, const uint8_t* coeffs, const hbec_view* in, 
                 if (rc) return rc;
                 const uint64_t tile = (uint64_t)vec_tile_bytes(K, R, shard_len, c0 > 0, force_stream);
                 const uint64_t tpo = (shard_len + tile - 1) / tile;
-                // keep n_tiles < 2^31 (and <= g_chunk_tiles) per launch: split the batch by objects
-                const uint64_t max_obj = std::max<uint64_t>(1, std::min<uint64_t>((1ull << 31), g_chunk_tiles) / tpo);
+                // keep n_tiles < 2^31 (and <= g_vec_chunk_tiles) per launch: split the batch by objects
+                const uint64_t max_obj = std::max<uint64_t>(1, std::min<uint64_t>((1ull << 31), g_vec_chunk_tiles) / tpo);
                 for (uint64_t o0 = 0; o0 < n_obj; o0 += max_obj) {
                     const uint64_t no = std::min(max_obj, n_obj - o0);
                     PassArgs b = a;
@@ -588,13 +610,13 @@ struct hbec_codec {
     std::vector<uint8_t> matrix;  // (k+m) x k
     std::mutex mu;
     std::map<std::vector<int>, std::vector<uint8_t>> inv_cache;  // survivors -> inv(sub)
+    bool bp_plan = false;  // the parity rows have a compiled bit-plane plan schedule (set by hbec_new)
 };
 
 namespace hbec {
 
 bool plan_rec_route(const hbec_codec* c, uint64_t shard_len, bool line_aligned) {
-    return rec_route(c->k, c->m, shard_len, line_aligned,
-                     c->m > 0 && bitplane_rows(c->k, c->m, c->matrix.data() + (size_t)c->k * c->k, c->k, true));
+    return rec_route(c->k, c->m, shard_len, line_aligned, c->bp_plan);  // once per stripe: no per-call matching
 }
 
 // Decode rows for a present mask: survivors = first k present shards.
@@ -834,6 +856,7 @@ int hbec_new(int data_shards, int parity_shards, hbec_codec** out) {
         c->k = data_shards;
         c->m = parity_shards;
         if (!build_matrix(c->k, c->m, c->matrix)) return fail(HBEC_ERR_SINGULAR, "matrix is singular");
+        c->bp_plan = c->m > 0 && hbec::bitplane_rows(c->k, c->m, c->matrix.data() + (size_t)c->k * c->k, c->k, true);
         *out = c.release();
         return HBEC_OK;
     });
@@ -1410,6 +1433,11 @@ int hbec_coalesce_stats(uint64_t* groups, uint64_t* calls) {
         coalesce_stats(groups, calls);
         return HBEC_OK;
     });
+}
+
+int hbec_set_odd_chunk_tiles(uint64_t tiles) {
+    g_odd_chunk_override.store(tiles, std::memory_order_relaxed);
+    return HBEC_OK;
 }
 
 int hbec_set_force_stream(int on) {

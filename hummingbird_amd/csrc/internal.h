@@ -107,7 +107,7 @@ struct URec;
 // instead of recs.
 struct OddTileList {
     uint32_t span = 0;            // shard bytes per tile
-    const uint32_t* d = nullptr;  // device: {record index, tile in record} per tile
+    const uint32_t* d = nullptr;  // device: {record index, tile in record, S, edge flags} per tile
     uint64_t n = 0;
 };
 constexpr int kOddSpans = 2;  // the record kernels' tile spans: 992 (5 <= K <= 12 tables), 2016 (carried 2 windows)
@@ -116,6 +116,7 @@ struct OddStripeRecs {
     uint64_t n = 0, s_max = 0;
     OddTileList lists[kOddSpans];
     bool edges_long = false;  // every edge record's S > kOddMinMain (64 + 64 edge slots)
+    uint64_t n_short_edges = 0;  // edge records of S <= kOddMinMain (listed first): the fused passes' edge launch
 };
 // the distinct odd_rec_tile_span values of apply / accumulate passes
 void odd_plan_spans(uint32_t (&spans)[kOddSpans]);

@@ -25,6 +25,7 @@ inline long long tune_knob(const char* name, long long dflt) {
 }
 
 constexpr int kMaxK = 16;         // inputs per kernel pass
+constexpr uint32_t kOddListWords = 4;  // words per plan tile-list entry (PassArgs::list)
 constexpr int kMaxR = 4;          // outputs per kernel pass
 constexpr int kBlockThreads = 256;
 constexpr int kPipeBlockThreads = HBEC_PIPE_BLOCK;  // pipelined kernel block size
@@ -47,9 +48,10 @@ struct PassArgs {
     uint32_t accumulate;    // 1: out ^= result (passes 2.. over >kMaxK inputs)
     uint32_t n_elems;       // packed path: n_obj * elems_per_obj (< 2^31)
     uint32_t elems_per_obj; // packed path: shard_len / 16
-    uint32_t pad_;
-    // record kernels over a plan: n_tiles entries {record index, tile in record}
-    // (u32 pairs; odd_rec_tile_span bytes per tile); null: strided positions
+    uint32_t fuse;          // odd strided apply: bit 0 = code the guard band in the main kernel (HBEC_ODD_EDGE_FUSE)
+    // record kernels over a plan: n_tiles entries {record index, tile in
+    // record, S, edge flags} (kOddListWords u32 each; odd_rec_tile_span bytes
+    // per tile); null: strided positions
     const uint32_t* list;
 };
 
@@ -155,9 +157,13 @@ uint32_t odd_tile_bytes(int k);       // shard bytes per wave tile of the stride
 uint32_t odd_plan_tile_bytes();       // shard bytes per plan record
 // xs >= 0: the bit-plane record kernel of schedule xs (odd_bp_schedule)
 uint32_t odd_tiles_per_obj(int k, int mode, uint64_t shard_len, bool records, int xs = -1);
+// tiles of `tile` stored bytes per shard of shard_len > odd_min_main() bytes
+uint64_t odd_frame_tiles(uint64_t shard_len, uint64_t tile);
 // Bit-plane record kernels (xor_sched.h): the schedule whose fixed coefficient
 // matrix equals this pass's tables (the encode parity rows of a compiled
-// (k, m); mode 0 apply only), or -1 for the v_perm table kernels.
+// (k, m)) for apply (mode 0: strided or plan, XorShape strided / plan flags)
+// and Verify (mode 2, strided: XorShape verify), or -1 for the v_perm table
+// kernels (accumulate passes always).
 int odd_bp_schedule(int k, int r, int mode, const uint32_t (*tab)[kMaxK][5], bool plan);
 // shard bytes per tile of the record kernel a pass of k inputs launches (xs: odd_bp_schedule)
 uint32_t odd_rec_tile_span(int k, int mode, int xs);
@@ -179,6 +185,10 @@ hipError_t launch_odd_planrec(int k, int r, int mode, const UPlanArgs& p, const 
                               uint32_t* recs, hipStream_t stream);
 hipError_t launch_odd(int k, int r, int mode, const PassArgs& a, uint32_t* flags, const uint32_t* recs, int grid,
                       hipStream_t stream, int xs = -1);
+// a strided pass of this shape codes the guard band inside its main kernel
+// when PassArgs::fuse is set (HBEC_ODD_EDGE_FUSE: apply passes; records:
+// the gf_odd_rec kernel, else gf_odd)
+bool odd_edge_fuse(int k, int r, int mode, bool records, int xs, bool list = false);
 // the guard-band bytes of every shard (after the main launches of a pass;
 // k <= kMaxK inputs, a.n_obj objects; verify flags mismatching objects)
 hipError_t launch_odd_edges(int k, int r, int mode, const PassArgs& a, uint32_t* flags, hipStream_t stream);

@@ -822,8 +822,14 @@ int packed_tile_elems(int k) { return packed_u(k) * 64; }
 // it is the only full-lane kernel (8+3 @ 4 KiB: 70 % vs 7 % of 8 TB/s); for
 // K <= 4 it also beats gf_apply_vec_pipe2 up to S = 1 KiB (4+2 @ 4 KiB:
 // 72.6 % vs 69.3 %), while at S = 256 KiB it loses (68-72 % vs 74 %)
-// (profiles/r02_tune_packed3_*.jsonl).
+// (profiles/r02_tune_packed3_*.jsonl).  5 <= K <= 8 up to S = 32 KiB
+// (HBEC_PACKED_MAX_BIG): the pipelined kernel's 3 KiB tiles leave most of a
+// tile idle when S mod 3 KiB is small, packed tiles never do; 16 384 8+3
+// objects at S = 4 / 8 / 12 / 16 / 32 KiB 50.5 / 56.5 / 67.2 / 67.7 / 74.8 %
+// -> 71.0 / 56.2 / 67.7 / 72.5 / 75.4 % (profiles/r06_ab_packed.jsonl); 4+2
+// loses at 8-16 KiB (69.9 -> 67.9, 72.8 -> 70.4 %) and keeps one tile.
 static uint64_t packed_max_shard(int k) {
+    if (k > 4) return HBEC_PACKED_MAX_BIG;
     const uint64_t tile = (uint64_t)pipe_u(k) * 1024u;
     return tile > 2048u ? tile : 2048u;
 }

@@ -221,8 +221,8 @@ __device__ __forceinline__ int32_t floor16(int32_t x) { return x & ~15; }
 template <class InB, class OutB>
 __device__ __forceinline__ void odd_rec_write(int K, int R, int mode, int32_t S, InB in_b, OutB out_b, uint32_t* f,
                                               uint32_t* l) {
-    // frame: output 0's 16-B grid, first column at c0 in [0, 16)
-    const int32_t c0 = (int32_t)((0u - (uint32_t)out_b(0)) & 15u);
+    // frame: output 0's 16-B grid, first column at c0 in [kOddFrame, kOddFrame + 16)
+    const int32_t c0 = (int32_t)((0u - (uint32_t)out_b(0)) & 15u) + kOddFrame;
     const int32_t hi = S - kOddGuard - 16;  // last block start stored / compared
     const bool main = S > kOddMinMain;
     const int NL = K + (mode == kOddVerify ? R : 0), NO = mode == kOddVerify ? 0 : R;
@@ -233,7 +233,10 @@ __device__ __forceinline__ void odd_rec_write(int K, int R, int mode, int32_t S,
         const uint64_t base = (b & ~(uint64_t)3) + (uint64_t)(t0 & ~3);
         l[3 * s] = (uint32_t)base;
         l[3 * s + 1] = (uint32_t)(base >> 32);
-        l[3 * s + 2] = main ? (uint32_t)(S - 16 - (t0 & ~3)) : 0u;  // blocks end inside the shard's dwords
+        // blocks end inside the shard's dwords; the low 2 bits (S mod 4 in the
+        // exact limit: the clamp moves by < 4 B, below every stored column)
+        // carry base mod 4 for the fused guard band (gf_odd_rec EDGE)
+        l[3 * s + 2] = main ? (((uint32_t)(S - 16 - (t0 & ~3)) & ~3u) | (uint32_t)(b & 3u)) : 0u;
         shp |= ((uint32_t)t0 & 3u) << (2 * s);
     }
     for (int r = 0; r < NO; ++r) {
@@ -258,7 +261,7 @@ __device__ __forceinline__ void odd_rec_write(int K, int R, int mode, int32_t S,
     int32_t vlo = ceil16(kOddGuard - c0), vtop = floor16(hi - c0);
     if (!main) vlo = -16, vtop = -32;
     f[0] = shp;
-    f[1] = dlp;
+    f[1] = dlp | ((uint32_t)c0 << 16);  // frame start C for the fused guard band
     f[2] = (uint32_t)vlo;
     f[3] = (uint32_t)(vtop >= vlo ? vtop - vlo : 0);
 }
@@ -366,8 +369,7 @@ uint32_t odd_tile_bytes(int k) { return odd_u(k) == 2 ? (64u + kOddStore) * 16u 
 uint64_t odd_min_main() { return kOddMinMain; }
 uint32_t odd_plan_tile_bytes() { return (uint32_t)kOddPlanU * kOddWin; }
 
-// Tiles per shard: enough windows for every output block of the shard, from
-// the frame's first column (c0 >= -32) to position S.
+// The record kernels' tile spans (plan tile lists, odd_frame_tiles).
 void odd_plan_spans(uint32_t (&spans)[kOddSpans]) {
     // table record kernels: 5 <= K <= 12 one 992-B window per tile, K <= 4 the
     // carried 2-window tile; bit-plane kernels HBEC_ODD_BP_U carried windows
@@ -381,18 +383,30 @@ uint32_t odd_rec_tile_span(int k, int mode, int xs) {
     return xs >= 0 ? odd_rec_span(odd_bp_u(), mode) : odd_rec_span(odd_u(k, mode), mode);
 }
 
+// Tiles per shard of S > kOddMinMain bytes: every block stored (compared)
+// lies at V <= S - 64 - kOddFrame in the frame (column V at position
+// kOddFrame + (-out0 mod 16) + V), and a tile stores `tile` bytes of V.
+uint64_t odd_frame_tiles(uint64_t shard_len, uint64_t tile) {
+    const uint64_t last = shard_len - (uint64_t)(kOddGuard + 16 + kOddFrame);  // S > kOddMinMain: positive
+    return last / tile + 1u;
+}
+
 uint32_t odd_tiles_per_obj(int k, int mode, uint64_t shard_len, bool records, int xs) {
-    const uint64_t span = shard_len + 32u;
     const uint64_t tile = xs >= 0 ? (uint64_t)odd_rec_tile_span(k, mode, xs)
                           : records ? (uint64_t)odd_rec_span(odd_u(k, mode), mode)
                           : mode == kOddVerify ? (odd_u(k, mode) >= 2 ? (uint64_t)(64u * odd_u(k, mode) - 1u) * 16u
                                                                       : (uint64_t)odd_win<kOddVerify>())
                                                : (odd_u(k, mode) == 2 ? (uint64_t)(64 + kOddStore) * 16u
                                                                                          : (uint64_t)odd_u(k, mode) * kOddWin);
-    return (uint32_t)((span + tile - 1) / tile);
+    return (uint32_t)odd_frame_tiles(shard_len, tile);
 }
 
 bool odd_supported(int k, int r) { return k >= 1 && k <= kOddMaxK && r >= 1 && r <= kMaxR; }
+
+bool odd_edge_fuse(int k, int r, int mode, bool records, int xs, bool list) {
+    static const bool on = tune_knob("HBEC_ODD_EDGE_FUSE", 1) != 0;  // tuning builds: 0 = the separate edge launch
+    return on && (records ? odd_rec_edge(k, r, mode, xs, list) : odd_strided_edge(k, r, mode));
+}
 
 int odd_bp_schedule(int k, int r, int mode, const uint32_t (*tab)[kMaxK][5], bool plan) {
     // tuning builds: HBEC_ODD_BP = 0 none, 1 the measured choice (XorShape

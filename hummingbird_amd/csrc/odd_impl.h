@@ -109,7 +109,15 @@ struct OddTile {
 // hash-arena pitch of a mirrored stripe: shard i at arena + i * P (16-B aligned)
 __host__ __device__ __forceinline__ uint64_t odd_mirror_pitch(uint64_t S) { return (S + 31u) & ~(uint64_t)15; }
 
-__device__ __forceinline__ int32_t odd_c0(uint64_t out0) { return (int32_t)((16u - ((uint32_t)out0 & 15u)) & 15u) - 32; }
+// Frame offset: column 0 of a shard sits at position kOddFrame + (-out0 mod 16)
+// in [32, 48), so the first block any output stores (position >= kOddGuard)
+// is covered by column 0 or 1 and no column lies before the shard; a shard's
+// tiles then only have to reach the last stored block (<= S - 64):
+// odd_frame_tiles (round 6: one tile fewer per shard for about 1 size in
+// 16 at S = 4 KiB; the old frame started 32 B before the shard and its tiles
+// ran to S + 32).
+constexpr int32_t kOddFrame = 32;
+__device__ __forceinline__ int32_t odd_c0(uint64_t out0) { return (int32_t)((16u - ((uint32_t)out0 & 15u)) & 15u) + kOddFrame; }
 
 // One shard's dword-aligned 16-B blocks for one tile: lane column col's block
 // starts off + 16 col bytes after base4, clamped into the shard's dwords
@@ -194,6 +202,61 @@ __device__ __forceinline__ u32x4 odd_shift_in_fill(const u32x4& v, uint32_t sh, 
 
 typedef __attribute__((address_space(1))) uint8_t gu8_t;
 
+// ---- guard-band bytes inside the main kernels (HBEC_ODD_EDGE_FUSE) ----
+// A strided apply pass of shards longer than one tile codes each shard's
+// head [0, 64) and tail [S - 64, S) in the tile that starts / ends the shard:
+// lane l takes position l (head) or S - 64 + l (tail), loads the K input
+// bytes with that tile's loads (so they come from the lines the tile reads,
+// and the next tile's loads stay in flight behind them), multiplies them
+// with the tile and stores the output bytes of the guard band next to the
+// tile's 16-B blocks (the L2 merges them into the same lines).  Every tile
+// issues the K byte loads, the other tiles from their own first column, so
+// the number of loads in flight is the same on every path (a
+// load under a branch made the compiler wait for the NEXT tile's loads at
+// every finish).  Edge flags (wave-uniform): 1 first tile, 2 last tile;
+// the host fuses only when every shard has >= 2 tiles (never both).
+__device__ __forceinline__ uint32_t ld_u8(uint64_t addr) { return *reinterpret_cast<const gu8_t*>(addr); }
+__device__ __forceinline__ void st_u8(uint64_t addr, uint32_t v) { *reinterpret_cast<gu8_t*>(addr) = (uint8_t)v; }
+
+// lane offset of an edge tile's byte (0 on the others)
+__device__ __forceinline__ uint32_t odd_edge_off(uint32_t flags, uint32_t S, uint32_t lane) {
+    return flags == 0u ? 0u : ((flags & 1u) ? lane : S - 64u + lane);
+}
+
+// the output bytes of an edge word: output r at shard base o; the main
+// kernel stores positions [h, t) of output r
+__device__ __forceinline__ void odd_edge_store(uint64_t o, uint32_t v, uint32_t flags, uint32_t S, uint32_t lane,
+                                               uint32_t h, uint32_t t, bool live) {
+    const uint32_t p = odd_edge_off(flags, S, lane);
+    if (live && ((flags & 1u) ? p < h : p >= t)) st_u8(o + p, v);
+}
+
+// acc[r] = XOR_j C[r][j] * x[j] for one dword per input (register tables)
+template <int K, int R, int VMIN>
+__device__ __forceinline__ void gf_dot1(uint32_t (&acc)[R], const uint32_t (&x)[K], const TabArray& tab,
+                                        const Tables<K, R, VMIN>& tb) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = 0u;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        const Sel sx = selectors(x[j]);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            uint32_t h1, h3, h4;
+            if constexpr (Tables<K, R, VMIN>::kAllV) {
+                h1 = tb.hi[r][j][0];
+                h3 = tb.hi[r][j][1];
+                h4 = tb.hi[r][j][2];
+            } else {
+                h1 = tab[r][j][1];
+                h3 = tab[r][j][3];
+                h4 = tab[r][j][4];
+            }
+            acc[r] = xor3(acc[r], perm(h1, tb.lo0[r][j], sx.s0), perm(h3, tb.lo2[r][j], sx.s1)) ^ perm(h4, h4, sx.s2);
+        }
+    }
+}
+
 // coefficient tables in LDS (record kernels, K >= HBEC_ODD_LDS_MINK): words per input, 16-B padded
 __host__ __device__ constexpr uint32_t odd_lt_stride(int r) { return (uint32_t)((r * 5 + 3) & ~3); }
 
@@ -211,6 +274,12 @@ __host__ __device__ constexpr uint32_t odd_lt_stride(int r) { return (uint32_t)(
 // pinned, and 12+4 spills.
 __host__ __device__ constexpr bool odd_two_blocks(int k, int r, int mode, bool mir) {
     return !mir && mode == kOddApply && k <= 10 && k * r >= 36;
+}
+// gf_odd strided apply codes the guard band in the main kernel
+// (HBEC_ODD_EDGE_FUSE), except the register-bound 2-block pinned instances
+// (9+4 / 10+4 spilled with it; strided 10+4 takes the record kernels)
+__host__ __device__ constexpr bool odd_strided_edge(int k, int r, int mode) {
+    return HBEC_ODD_EDGE_FUSE != 0 && mode == kOddApply && !odd_two_blocks(k, r, mode, false);
 }
 template <int K, int R, int MODE, bool MIR>
 __host__ __device__ constexpr bool odd_pin_on() {
@@ -240,7 +309,13 @@ template <int K, int R, int U, int MODE>
 struct OddStrided {
     using Id = OddIdS;
     static constexpr bool kCarry = odd_carry<U, MODE>();
+    // apply passes code the guard band in the shard's first / last tile
+    static constexpr bool kEdge = odd_strided_edge(K, R, MODE);
     const PassArgs& a;
+    __device__ __forceinline__ uint32_t edge(const Id& i) const {
+        return (a.fuse & 1u) != 0u && i.live != 0u
+                   ? (i.ti == 0u ? 1u : (i.ti + 1u == a.tiles_per_obj ? 2u : 0u)) : 0u;
+    }
     __device__ __forceinline__ Id id(uint32_t t, uint32_t n) const {
         const uint32_t tt = t < n ? t : n - 1u;
         const uint32_t tpo = a.tiles_per_obj;
@@ -280,6 +355,8 @@ __host__ __device__ constexpr int odd_plan_u(int) {
 template <int K, int R, bool MIR = false, bool CARRY = false>
 struct OddPlan {
     using Id = OddIdP;
+    static constexpr bool kEdge = false;  // plans: gf_odd_edges_plan
+    __device__ __forceinline__ uint32_t edge(const Id&) const { return 0u; }
     // CARRY: the records hold one carried 2-window tile each (2016 B,
     // urec_tile_for); otherwise 2 x 992 B windows
     static constexpr bool kCarry = CARRY;
@@ -323,6 +400,7 @@ struct OddRegs {
     // accumulate mode the old output blocks (with the inputs, one tile ahead)
     static constexpr int NL = K + (MODE == kOddVerify || MODE == kOddAcc ? R : 0);
     u32x4 x[U][NL];
+    uint32_t e[K];  // guard-band bytes (edge tiles of fused apply passes; unused otherwise)
 };
 
 template <int K, int R, int U, int MODE, bool CARRY = false>
@@ -366,10 +444,21 @@ __device__ __forceinline__ void odd_st(uint64_t addr, const u32x4& v, bool mine)
     if (mine) st16_addr(addr, v);
 }
 
-template <int K, int R, int U, int MODE, bool MIR = false, bool CARRY = false>
+template <int K, int R, int U, int MODE, bool MIR = false, bool CARRY = false, bool EDGE = false>
 __device__ __forceinline__ void odd_finish(const OddRegs<K, R, U, MODE>& X, const OddTile<K, R>& b,
                                            const TabArray& tab, const Tables<K, R, kOddVMin>& tb, uint32_t lane,
-                                           uint32_t* flags, uint32_t mir = 0) {
+                                           uint32_t* flags, uint32_t mir = 0, uint32_t edge = 0) {
+    if (EDGE && edge != 0u) {  // fused guard band (wave-uniform): the bands of gf_odd_edges
+        uint32_t acc[R];
+        gf_dot1<K, R, kOddVMin>(acc, X.e, tab, tb);
+        const uint32_t S = (uint32_t)b.S, top = S - (uint32_t)kOddGuard - 16u;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint32_t e = (16u - ((uint32_t)b.out[r] & 15u)) & 15u;  // output r's aligned positions = e mod 16
+            const uint32_t qmax = top - ((top - e) & 15u);
+            odd_edge_store(b.out[r], acc[r], edge, S, lane, (uint32_t)kOddGuard + e, qmax + 16u, true);
+        }
+    }
     uint32_t sh[K + (MODE == kOddVerify ? R : 0)];
 #pragma unroll
     for (int j = 0; j < K; ++j) sh[j] = __builtin_amdgcn_readfirstlane(((uint32_t)b.in[j] + (uint32_t)b.c) & 3u);
@@ -518,12 +607,23 @@ __device__ __forceinline__ void odd_body(const Src& src, uint32_t n, const TabAr
     const uint32_t dw = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (wave0 >= n) return;  // whole blocks only: the loop below has block barriers
     const Tables<K, R, kOddVMin> tb = load_tables<K, R, kOddVMin>(tab);
+    // fused guard band: every tile issues the K edge byte loads (an edge
+    // tile from its shards, the others from one hot line), so the loads in
+    // flight do not depend on the path (odd_edge_off)
+    auto edge_load = [&](OddRegs<K, R, U, MODE>& Z, const OddTile<K, R>& b, const typename Src::Id& i) {
+        if constexpr (Src::kEdge) {
+            const uint32_t fl = src.edge(i), eo = odd_edge_off(fl, (uint32_t)b.S, lane);
+#pragma unroll
+            for (int j = 0; j < K; ++j) Z.e[j] = ld_u8(b.in[j] + (fl != 0u ? (uint64_t)eo : (uint64_t)(uint32_t)b.c));
+        }
+    };
     typename Src::Id cur = src.id(wave0 + dw, n);
     OddRegs<K, R, U, MODE> X;
     {
         OddTile<K, R> b;
         src.at(b, cur);
         odd_load<K, R, U, MODE, Src::kCarry>(X, b, lane);
+        edge_load(X, b, cur);
     }
     typename Src::Id nxt = src.id(wave0 + dw + nw, n);
     for (uint32_t b0 = wave0 + nw; b0 < n; b0 += nw) {  // block-uniform trip count
@@ -532,6 +632,7 @@ __device__ __forceinline__ void odd_body(const Src& src, uint32_t n, const TabAr
             OddTile<K, R> b;
             src.at(b, nxt);
             odd_load<K, R, U, MODE, Src::kCarry>(Y, b, lane);
+            edge_load(Y, b, nxt);
         }
         // one block barrier per tile for apply; none for Verify (8+3 57 -> 66 %,
         // 6+3 63 -> 70 %, profiles/r03_tune_odd3.jsonl)
@@ -540,7 +641,7 @@ __device__ __forceinline__ void odd_body(const Src& src, uint32_t n, const TabAr
         {
             OddTile<K, R> b;
             src.at(b, cur);
-            odd_finish<K, R, U, MODE, MIR, Src::kCarry>(X, b, tab, tb, lane, flags, mir);
+            odd_finish<K, R, U, MODE, MIR, Src::kCarry, Src::kEdge>(X, b, tab, tb, lane, flags, mir, src.edge(cur));
         }
         X = Y;
         cur = nxt;
@@ -548,7 +649,7 @@ __device__ __forceinline__ void odd_body(const Src& src, uint32_t n, const TabAr
     }
     OddTile<K, R> b;
     src.at(b, cur);
-    odd_finish<K, R, U, MODE, MIR, Src::kCarry>(X, b, tab, tb, lane, flags, mir);
+    odd_finish<K, R, U, MODE, MIR, Src::kCarry, Src::kEdge>(X, b, tab, tb, lane, flags, mir, src.edge(cur));
 }
 
 template <int K, int R, int MODE>
@@ -591,6 +692,16 @@ __host__ __device__ constexpr uint32_t odd_rec_wcol(int u) { return CARRY ? 64u 
 // (12+4: 240 words; the register-resident kernel spilled 134 SGPRs and ran
 // at 40 % of 8 TB/s).
 __host__ __device__ constexpr bool odd_rec_lds(int k) { return k >= HBEC_ODD_LDS_MINK; }
+// record kernels (strided and plan tile lists) that code the guard band
+// (HBEC_ODD_EDGE_FUSE): apply, register tables or bit-plane (the LDS-table kernels, K >= 9, spilled
+// 15-211 VGPRs with it and keep the gf_odd_edges launch)
+// (4 x 4 tables over a plan's tile list spilled a pending tile-list entry
+// register with it: isa_check.py refused the library; that instance keeps
+// the gf_odd_edges_plan launch)
+__host__ __device__ constexpr bool odd_rec_edge(int k, int r, int mode, int xs, bool list) {
+    return HBEC_ODD_EDGE_FUSE != 0 && mode == kOddApply && (xs >= 0 || !odd_rec_lds(k)) &&
+           !(list && xs < 0 && k == 4 && r == 4);
+}
 // record kernels run 2 waves per SIMD with LDS tables; the register-table
 // ones at 1 (8+3 encode at 2 waves per SIMD, 256 VGPRs with 40 B of spill:
 // 66.8 -> 59.3 %, profiles/r04_ab_odd.jsonl batch I)
@@ -642,6 +753,37 @@ __device__ __forceinline__ void gf_dot_lds(u32x4 (&acc)[R], const u32x4 (&x)[K],
         for (int e = 0; e < 4; ++e)
 #pragma unroll
             for (int r = 0; r < R; ++r) acc[r][e] ^= pend[e][r];
+    }
+}
+
+// gf_dot1 with the tables in LDS (gf_dot_lds layout): edge words of the
+// LDS-table and bit-plane record kernels
+template <int K, int R>
+__device__ __forceinline__ void gf_dot_lds1(uint32_t (&acc)[R], const uint32_t (&x)[K], uint32_t lt) {
+    constexpr int TQ = (int)odd_lt_stride(R) / 4;
+    typedef __attribute__((address_space(3))) const u32x4 lds_q;
+    uint32_t z = lt;
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = 0u;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        // one input's tables at a time: the address of input j depends on the
+        // products of input j - 1 (an empty asm), so the reads are neither
+        // hoisted out of the tile loop nor batched while both tiles' columns
+        // are live (the bit-plane 8+3 kernel held 76 more VGPRs otherwise)
+        asm volatile("" : "+v"(z) : "v"(acc[0]));
+        lds_q* tp = reinterpret_cast<lds_q*>(static_cast<uintptr_t>(z));
+        u32x4 t[TQ];
+#pragma unroll
+        for (int q = 0; q < TQ; ++q) t[q] = tp[j * TQ + q];
+        const Sel sx = selectors(x[j]);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint32_t p0 = perm(t[(5 * r + 1) / 4][(5 * r + 1) % 4], t[(5 * r) / 4][(5 * r) % 4], sx.s0);
+            const uint32_t p1 = perm(t[(5 * r + 3) / 4][(5 * r + 3) % 4], t[(5 * r + 2) / 4][(5 * r + 2) % 4], sx.s1);
+            const uint32_t h4 = t[(5 * r + 4) / 4][(5 * r + 4) % 4];
+            acc[r] = xor3(acc[r], p0, p1) ^ perm(h4, h4, sx.s2);
+        }
     }
 }
 
@@ -776,14 +918,15 @@ __device__ __forceinline__ void odd_rec_sload(u32x8 (&v)[N], const uint32_t* p) 
 
 // plan tile-list entries {record, tile}: 2-dword scalar loads, issued with
 // the record loads (split where those are split) and waited with them
-typedef uint32_t u32x2s __attribute__((ext_vector_type(2)));
+// (4-dword entries {record, tile, S, edge flags}: plan.cpp build_tile_lists)
+typedef uint32_t u32x2s __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void odd_sload_now2(u32x2s& v, const uint32_t* p) {
-    asm volatile("s_load_dwordx2 %0, %1, 0\n s_waitcnt lgkmcnt(0)" : "=&s"(v) : "s"(p) : "memory");
+    asm volatile("s_load_dwordx4 %0, %1, 0\n s_waitcnt lgkmcnt(0)" : "=&s"(v) : "s"(p) : "memory");
 }
 template <bool PF>
 __device__ __forceinline__ void odd_rec_sload2(u32x2s& v, const uint32_t* p) {
     if constexpr (PF) {
-        asm volatile("s_load_dwordx2 %0, %1, 0" : "=s"(v) : "s"(p));
+        asm volatile("s_load_dwordx4 %0, %1, 0" : "=s"(v) : "s"(p));
     } else {
         odd_sload_now2(v, p);
     }
@@ -805,7 +948,12 @@ struct OddRT {  // the finish's scalars of one tile
     u32x8 f[OddRec<K, R, MODE>::FW / 8];
     uint32_t v0;  // ti * span
     uint32_t obj, live;
+    // fused guard band: bits 30-31 the edge flags (1 first tile of its shard,
+    // 2 last), bits 0-29 the shard length (the host fuses only S < 2^30)
+    uint32_t edge;
 };
+__device__ __forceinline__ uint32_t odd_eflags(uint32_t e) { return e >> 30; }
+__device__ __forceinline__ uint32_t odd_elen(uint32_t e) { return e & 0x3FFFFFFFu; }
 
 template <int K, int R, int U, int MODE, bool CARRY, bool IMAJ = true, bool TEMP = false>
 __device__ __forceinline__ void odd_rec_load(OddRegs<K, R, U, MODE>& X, const u32x8 (&l)[OddRec<K, R, MODE>::LW / 8],
@@ -978,11 +1126,37 @@ __device__ __forceinline__ void odd_rec_finish(const OddRegs<K, R, U, MODE>& X, 
     }  // !CARRY
 }
 
+// the fused guard band of an edge tile (gf_odd_rec EDGE)
+template <int K, int R, int U, int MODE, int XS, class TB>
+__device__ __forceinline__ void odd_rec_edges(const OddRegs<K, R, U, MODE>& X, const OddRT<K, R, MODE>& t,
+                                              const TabArray& tab, const TB& tb, uint32_t lane, uint32_t lt) {
+    {
+        if (t.edge != 0u) {  // wave-uniform: the tile starts or ends its shard
+            const uint32_t fl = odd_eflags(t.edge), S = odd_elen(t.edge);
+            uint32_t acc[R];
+            if constexpr (XS >= 0 || odd_rec_lds(K)) {
+                gf_dot_lds1<K, R>(acc, X.e, lt);
+            } else {
+                gf_dot1<K, R, kOddVMin>(acc, X.e, tab, tb);
+            }
+            const uint32_t w1 = odd_w(t.f, 1), c = w1 >> 16;  // frame start C (record word 1, bits 16..)
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const uint32_t d = (w1 >> (4 * r)) & 15u;
+                const uint64_t q = (uint64_t)odd_w(t.f, 4 + 4 * r) | ((uint64_t)odd_w(t.f, 5 + 4 * r) << 32);
+                const uint32_t h = c + d + odd_w(t.f, 6 + 4 * r), e = h + odd_w(t.f, 7 + 4 * r) + 16u;
+                odd_edge_store(q - (uint64_t)(c + d), acc[r], fl, S, lane, h, e, true);
+            }
+        }
+    }
+}
+
 // A wave's tiles t0, t0 + nw, ...: (object, tile in object), stepped by
 // (qq, rr) = divmod(nw, tpo).  Stand-in tiles past the end (obj >= n_obj)
 // load the last tile and store nothing.
 struct OddPos {
     uint32_t obj, ti;
+    uint32_t se;  // plans (LIST): the stripe's S | edge flags << 30; bit 29: edge bytes only (no main stores)
 };
 
 // LDS-table record kernels fit 2 blocks per CU (2 waves per SIMD); the
@@ -1036,6 +1210,9 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE, XS>())) 
     constexpr bool TEMP = MODE == kOddVerify ? (HBEC_ODD_TEMP & 1) != 0
                                              : MODE == kOddApply && ((HBEC_ODD_TEMP & 2) != 0 ||
                                                                      ((HBEC_ODD_TEMP & 4) != 0 && !IMAJ && !LIST));
+    // apply: the guard-band bytes in the shard's first / last tile
+    // (HBEC_ODD_EDGE_FUSE; plans: the tile list's entry flags)
+    constexpr bool EDGE = odd_rec_edge(K, R, MODE, XS, LIST);
     constexpr uint32_t SPAN = VCHAIN ? (64u * U - 1u) * 16u : odd_rec_span(U, MODE);
     constexpr uint32_t WPB = BP ? (uint32_t)odd_bp_wpb(K, R) : kPipeBlockThreads / 64;
     const uint32_t lane = threadIdx.x & 63u;
@@ -1044,8 +1221,10 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE, XS>())) 
     const uint32_t wave0 = __builtin_amdgcn_readfirstlane(xcd_block() * WPB);
     const uint32_t dw = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (wave0 >= n) return;  // whole blocks only: the loop below has block barriers
-    __shared__ __attribute__((aligned(16))) uint32_t ltab[LDS ? K * odd_lt_stride(R) : 4];
-    if constexpr (LDS) {
+    // LDS tables: the LDS-table kernels, and the bit-plane kernels' edge words
+    constexpr bool LDST = LDS || (EDGE && BP);
+    __shared__ __attribute__((aligned(16))) uint32_t ltab[LDST ? K * odd_lt_stride(R) : 4];
+    if constexpr (LDST) {
         // whole blocks reach this point (the early return above is per block)
         const uint32_t ts = odd_lt_stride(R);
         for (uint32_t i = threadIdx.x; i < (uint32_t)K * ts; i += blockDim.x) {
@@ -1064,11 +1243,11 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE, XS>())) 
     // loads and waited with them); tq = p's tile index
     uint32_t tq = wave0 + dw;
     u32x2s pe{0u, 0u};
-    auto lentry = [&](uint32_t t) { return a.list + 2u * (t < n ? t : n - 1u); };
+    auto lentry = [&](uint32_t t) { return a.list + kOddListWords * (t < n ? t : n - 1u); };
     auto step = [&](OddPos p) {
         if constexpr (LIST) {
             tq += nw;
-            return OddPos{pe[0], pe[1]};
+            return OddPos{pe[0], pe[1], pe[2]};
         } else {
             p.ti += rr;
             p.obj += qq;
@@ -1090,26 +1269,60 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE, XS>())) 
     OddPos p;
     if constexpr (LIST) {
         odd_sload_now2(pe, lentry(tq));
-        p = OddPos{pe[0], pe[1]};
+        p = OddPos{pe[0], pe[1], pe[2]};
         odd_sload_now2(pe, lentry(tq + nw));
     } else {
         const uint32_t t = wave0 + dw;
         p.obj = t / tpo;
         p.ti = t - p.obj * tpo;
+        p.se = 0u;
     }
     u32x8 L[RC::LW / 8];
     OddRT<K, R, MODE> tx, ty;
     OddRegs<K, R, U, MODE> X, Y;
+    // strided: every shard has >= 2 tiles when the host fuses; plans: the
+    // entry's flags (a one-tile stripe has two entries, head and tail, the
+    // second with bit 2: its main stores are the first entry's)
+    const bool fuse = (a.fuse & 1u) != 0u;
     auto fill = [&](OddRT<K, R, MODE>& tt, const OddPos& q) {
         tt.v0 = v0(q);
         tt.obj = q.obj;
-        tt.live = LIST ? (tq < n ? 1u : 0u) : (q.obj < n_obj ? 1u : 0u);
+        if constexpr (LIST) {
+            const bool in = tq < n;
+            tt.live = in && (q.se & (1u << 29)) == 0u ? 1u : 0u;
+            tt.edge = EDGE && fuse && in ? (q.se & ~(1u << 29)) : 0u;
+        } else {
+            tt.live = q.obj < n_obj ? 1u : 0u;
+            const uint32_t fl = q.ti == 0u ? 1u : (q.ti + 1u == tpo ? 2u : 0u);
+            tt.edge = EDGE && fuse && tt.live && fl ? (fl << 30) | (uint32_t)a.shard_len : 0u;
+        }
+    };
+    // EDGE: the shard base of loaded shard j is B_j + lim_j + 16 - (S & ~3)
+    // (record: B = base + C rounded down to a dword, lim = S - 16 - (C +
+    // (base & 3) rounded down) with base & 3 in its low 2 bits)
+    auto edge_load = [&](OddRegs<K, R, U, MODE>& Z, const OddRT<K, R, MODE>& tz) {
+        if constexpr (EDGE) {
+            const uint32_t fl = odd_eflags(tz.edge), S = odd_elen(tz.edge), s4 = S & ~3u;
+            const uint32_t eo = odd_edge_off(fl, S, lane);
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                // other tiles: the byte at the tile's first column of shard j
+                // (a line the tile's own loads fetch; one line for every wave
+                // of the launch made an L2 hot spot: -10 to -15 points)
+                const uint64_t bj = (uint64_t)odd_w(L, 3 * j) | ((uint64_t)odd_w(L, 3 * j + 1) << 32);
+                const uint32_t lim = odd_w(L, 3 * j + 2);
+                const uint64_t off = fl != 0u ? (uint64_t)(int64_t)(int32_t)(lim + 16u - s4 + eo)
+                                                   : (uint64_t)(tz.v0 < lim ? tz.v0 : lim);
+                Z.e[j] = ld_u8(bj + off);
+            }
+        }
     };
     odd_rec_sload<PF>(L, rec(p) + RC::FW);
     odd_swait();
     odd_swait_pin(L);
     fill(tx, p);
     odd_rec_load<K, R, U, MODE, CARRY || VCHAIN, IMAJ, TEMP>(X, L, tx.v0, lane);
+    edge_load(X, tx);
     odd_rec_sload<PF>(tx.f, rec(p));
     p = step(p);
     odd_rec_sload<PF>(L, rec(p) + RC::FW);
@@ -1122,6 +1335,7 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE, XS>())) 
                     const OddRT<K, R, MODE>& tw) {
         fill(tz, p);
         odd_rec_load<K, R, U, MODE, CARRY || VCHAIN, IMAJ, TEMP>(Z, L, tz.v0, lane);
+        edge_load(Z, tz);
         odd_rec_sload<PF>(tz.f, rec(p));
         p = step(p);
         odd_rec_sload<PF>(L, rec(p) + RC::FW);
@@ -1132,7 +1346,12 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE, XS>())) 
         // reads 1.054 -> 1.026 x); at one wave per SIMD it costs 10 points
         if constexpr (MODE != kOddVerify || (VCHAIN && HBEC_ODD_BP_VBARRIER && odd_bp_bpc(K, R, MODE) >= 2))
             __builtin_amdgcn_s_barrier();
+        // the guard band before the tile's columns with register tables, after
+        // them with LDS tables (fewer registers in each case: table 8+3 18 vs
+        // 39 AGPRs, bit-plane 8+3 205 vs 256 + 30 VGPRs)
+        if constexpr (EDGE && XS < 0) odd_rec_edges<K, R, U, MODE, XS>(W, tw, a.tab, tb, lane, lt);
         odd_rec_finish<K, R, U, MODE, CARRY, XS>(W, tw, a.tab, tb, lane, flags, lt);
+        if constexpr (EDGE && XS >= 0) odd_rec_edges<K, R, U, MODE, XS>(W, tw, a.tab, tb, lane, lt);
         odd_swait();
         odd_swait_pin(L);
         odd_swait_pin(tz.f);
@@ -1143,7 +1362,9 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE, XS>())) 
         X = Y;
         tx = ty;
     }
+    if constexpr (EDGE && XS < 0) odd_rec_edges<K, R, U, MODE, XS>(X, tx, a.tab, tb, lane, lt);
     odd_rec_finish<K, R, U, MODE, CARRY, XS>(X, tx, a.tab, tb, lane, flags, lt);
+    if constexpr (EDGE && XS >= 0) odd_rec_edges<K, R, U, MODE, XS>(X, tx, a.tab, tb, lane, lt);
 }
 
 template <int K, int R, int MODE, bool MIR = false, bool CARRY = false>

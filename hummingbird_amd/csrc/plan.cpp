@@ -81,7 +81,12 @@ void add_urecs(std::vector<hbec::URec>& recs, std::vector<hbec::URec>& erecs, st
 }
 
 // Tile lists of the per-stripe records: for each record-kernel tile span,
-// tile t of stripe e for t < ceil((S_e + 32) / span), stripe by stripe.
+// tile t of stripe e for t < odd_frame_tiles(S_e, span), stripe by stripe,
+// as {e, t, S_e | flags << 30, 0} (kernels.h kOddListWords): flag 1 the
+// stripe's first tile, 2 its last (apply passes code the guard band there,
+// HBEC_ODD_EDGE_FUSE; bits 0-29 hold S when S < 2^30, else the stripe's edges
+// go to gf_odd_edges_plan).  A one-tile stripe has two entries, {e, 0, S | 1 <<
+// 30} and {e, 0, S | 2 << 30 | 1 << 29}: bit 29 = guard-band bytes only.
 int build_tile_lists(hbec_plan* p, const std::vector<hbec::URec>& orecs) {
     p->orecs = hbec::OddStripeRecs{};
     if (orecs.empty()) return HBEC_OK;
@@ -92,18 +97,25 @@ int build_tile_lists(hbec_plan* p, const std::vector<hbec::URec>& orecs) {
     for (int i = 0; i < hbec::kOddSpans; ++i) {
         std::vector<uint32_t> l;
         for (size_t e = 0; e < orecs.size(); ++e) {
-            const uint64_t nt = (orecs[e].shard_len + 32u + spans[i] - 1) / spans[i];
-            for (uint64_t t = 0; t < nt; ++t) {
+            const uint64_t S = orecs[e].shard_len;
+            const uint64_t nt = hbec::odd_frame_tiles(S, spans[i]);
+            const bool small = S < (1ull << 30);
+            auto put = [&](uint64_t t, uint32_t fl, uint32_t only) {
                 l.push_back((uint32_t)e);
                 l.push_back((uint32_t)t);
-            }
+                l.push_back(small && fl ? (uint32_t)S | (fl << 30) | only : 0u);
+                l.push_back(0u);
+            };
+            for (uint64_t t = 0; t < nt; ++t) put(t, t == 0 ? 1u : (t + 1 == nt ? 2u : 0u), 0u);
+            if (nt == 1 && small) put(0, 2u, 1u << 29);
         }
-        if (l.size() / 2 >= (1ull << 31)) return fail(HBEC_ERR_INVALID_ARG, "plan too large (>= 2^31 record tiles)");
+        if (l.size() / hbec::kOddListWords >= (1ull << 31))
+            return fail(HBEC_ERR_INVALID_ARG, "plan too large (>= 2^31 record tiles)");
         hipError_t e = hipMalloc(reinterpret_cast<void**>(&p->d_lists[i]), l.size() * 4);
         if (e != hipSuccess) return hip_fail(e, "hipMalloc plan tile list");
         e = hipMemcpy(p->d_lists[i], l.data(), l.size() * 4, hipMemcpyHostToDevice);
         if (e != hipSuccess) return hip_fail(e, "hipMemcpy plan tile list");
-        p->orecs.lists[i] = hbec::OddTileList{spans[i], p->d_lists[i], l.size() / 2};
+        p->orecs.lists[i] = hbec::OddTileList{spans[i], p->d_lists[i], l.size() / hbec::kOddListWords};
     }
     p->orecs.recs = p->d_orecs;
     p->orecs.n = orecs.size();
@@ -129,7 +141,7 @@ int upload(const std::vector<T>& recs, T** dst, const char* what) {
 // one launch (stream-ordered scratch), then one gf_odd_rec launch over the
 // tile list of the span the pass's kernel uses.
 int odd_stripe_rec_pass(int K, int R, int mode, const hbec::UPlanArgs& a, const hbec::OddStripeRecs& o, int cus,
-                        int max_blocks, hipStream_t stream) {
+                        int max_blocks, hipStream_t stream, bool one_pass, bool* fused) {
     const uint64_t rw = hbec::odd_rec_words(K, R, mode);
     const int xs = hbec::odd_bp_schedule(K, R, mode, a.tab, true);
     const uint32_t span = hbec::odd_rec_tile_span(K, mode, xs);
@@ -153,6 +165,10 @@ int odd_stripe_rec_pass(int K, int R, int mode, const hbec::UPlanArgs& a, const 
     c.tiles_per_obj = 1;
     c.n_tiles = (uint32_t)tl->n;
     c.list = tl->d;
+    // the record kernel codes the guard band of the stripes it covers (the
+    // tile list's edge flags) when this pass's inputs are all of them
+    *fused = one_pass && o.s_max < (1ull << 30) && hbec::odd_edge_fuse(K, R, mode, true, xs, true);
+    c.fuse = *fused ? 1u : 0u;
     const uint64_t wpb = hbec::odd_waves_per_block(xs);
     const uint64_t want = (c.n_tiles + wpb - 1) / wpb;
     uint64_t cap = (uint64_t)cus * (uint64_t)hbec::odd_blocks_per_cu(mode, K, R, false, true, xs);
@@ -226,16 +242,20 @@ int hbec::launch_unaligned_passes(const URec* recs, uint64_t n_recs, const std::
                 if (max_blocks > 0) cap = std::min<uint64_t>(cap, (uint64_t)max_blocks);
                 const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, cap));
                 const int mode = c0 > 0 ? 1 : 0;
+                bool fused = false;
                 if (use_orecs) {
-                    int rc = odd_stripe_rec_pass(K, R, mode, a, *orecs, cus, max_blocks, stream);
+                    int rc = odd_stripe_rec_pass(K, R, mode, a, *orecs, cus, max_blocks, stream, K == K_all, &fused);
                     if (rc) return rc;
                 } else if (n_recs > 0) {
                     e = hbec::launch_odd_plan(K, R, mode, a, grid, stream);
                     if (e != hipSuccess) return hip_fail(e, "launch gf_odd_plan");
                 }
-                // guard-band bytes of every stripe, this pass's inputs
-                e = hbec::launch_odd_edges_plan(K, R, c0 > 0 ? 1 : 0, a, erecs, (uint32_t)n_erecs, stream,
-                                                orecs && orecs->edges_long);
+                // guard-band bytes of every stripe, this pass's inputs (fused:
+                // only the stripes of S <= odd_min_main(), which have no main
+                // tiles; the edge records list them first)
+                const uint64_t ne = fused ? orecs->n_short_edges : n_erecs;
+                e = hbec::launch_odd_edges_plan(K, R, c0 > 0 ? 1 : 0, a, erecs, (uint32_t)ne, stream,
+                                                !fused && orecs && orecs->edges_long);
                 if (e != hipSuccess) return hip_fail(e, "launch gf_odd_edges_plan");
             }
         }
@@ -463,6 +483,11 @@ int hbec_plan_stripes(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n,
                 return hip_fail(e, "hipMemcpy plan tiles");
             }
         }
+        // edge records of the stripes with no main tiles (S <= odd_min_main()) first
+        const auto short_end = std::stable_partition(erecs.begin(), erecs.end(), [](const hbec::URec& e) {
+            return e.shard_len <= hbec::odd_min_main();
+        });
+        const uint64_t n_short = (uint64_t)(short_end - erecs.begin());
         int urc = upload(urecs, &p->d_urecs, "plan unaligned records");
         if (!urc) urc = upload(erecs, &p->d_erecs, "plan edge records");
         if (!urc) urc = upload(brecs, &p->d_brecs, "plan large-shard records");
@@ -474,8 +499,8 @@ int hbec_plan_stripes(hbec_codec* codec, const hbec_stripe* stripes, uint64_t n,
         }
         p->n_urecs = urecs.size();
         p->n_erecs = erecs.size();
-        p->orecs.edges_long = std::all_of(erecs.begin(), erecs.end(),
-                                          [](const hbec::URec& e) { return e.shard_len > hbec::odd_min_main(); });
+        p->orecs.edges_long = n_short == 0;
+        p->orecs.n_short_edges = n_short;
         p->n_brecs = brecs.size();
         *out = p.release();
         return HBEC_OK;
@@ -539,6 +564,11 @@ int hbec_plan_objects(hbec_codec* codec, const hbec_object* objects, uint64_t n,
                 return hip_fail(e, "hipMemcpy plan tiles");
             }
         }
+        // edge records of the stripes with no main tiles (S <= odd_min_main()) first
+        const auto short_end = std::stable_partition(erecs.begin(), erecs.end(), [](const hbec::URec& e) {
+            return e.shard_len <= hbec::odd_min_main();
+        });
+        const uint64_t n_short = (uint64_t)(short_end - erecs.begin());
         int urc = upload(urecs, &p->d_urecs, "plan unaligned records");
         if (!urc) urc = upload(erecs, &p->d_erecs, "plan edge records");
         if (!urc) urc = upload(brecs, &p->d_brecs, "plan large-shard records");
@@ -550,8 +580,8 @@ int hbec_plan_objects(hbec_codec* codec, const hbec_object* objects, uint64_t n,
         }
         p->n_urecs = urecs.size();
         p->n_erecs = erecs.size();
-        p->orecs.edges_long = std::all_of(erecs.begin(), erecs.end(),
-                                          [](const hbec::URec& e) { return e.shard_len > hbec::odd_min_main(); });
+        p->orecs.edges_long = n_short == 0;
+        p->orecs.n_short_edges = n_short;
         p->n_brecs = brecs.size();
         *out = p.release();
         return HBEC_OK;

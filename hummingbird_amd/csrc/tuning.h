@@ -34,6 +34,14 @@
 #ifndef HBEC_PIPE_TEMP
 #define HBEC_PIPE_TEMP 0  // pipelined kernels: 1 = input loads with the temporal hint (A/B)
 #endif
+#ifndef HBEC_VEC_CHUNK_TILES
+// tiles per launch of the aligned strided kernels (a batch splits into
+// launches of whole objects): 256 Ki tiles ran the 4096 x 1 MiB 4+2 encode
+// 72.9 -> 73.8 % and reconstruct {0,1} 70.6 -> 71.5 % against 1 Mi
+// (profiles/r05_ab_grid.jsonl, HBEC_CHUNK_TILES=262144); the other kernels
+// keep HBEC_CHUNK_TILES' 1 Mi
+#define HBEC_VEC_CHUNK_TILES 262144
+#endif
 #ifndef HBEC_PIPE_V2_MAXK
 #define HBEC_PIPE_V2_MAXK 4  // pipe2 up to K = 4: +1.6 % at 4+2, -7 % at 8+3 (profiles/r01_tune_pipe2.jsonl)
 #endif
@@ -60,6 +68,9 @@
 // ---- packed short-shard kernels (gf_apply_packed, gf_verify_packed) ----
 #ifndef HBEC_PACKED_U_BIG
 #define HBEC_PACKED_U_BIG 1  // KiB per input per wave tile for K > 4: 70 % vs 57.8 % at 3 KiB
+#endif
+#ifndef HBEC_PACKED_MAX_BIG
+#define HBEC_PACKED_MAX_BIG 32784  // 5 <= K <= 8: packed below this S (exclusive), 8+3 @ 32 KiB objects 50.5 -> 71 % (r06_ab_packed)
 #endif
 #ifndef HBEC_PACKED_BLOCKS_SMALL
 #define HBEC_PACKED_BLOCKS_SMALL 2  // blocks per CU, K <= 4: +7-10 % over 1 (r02_tune_packed*.jsonl)
@@ -161,6 +172,13 @@
 #endif
 #ifndef HBEC_ODD_BPC_VERIFY
 #define HBEC_ODD_BPC_VERIFY 2  // read-only: 4+2 68.5 -> 81 % with 2 blocks per CU (r03_tune_odd3)
+#endif
+
+#ifndef HBEC_ODD_EDGE_FUSE
+// strided apply passes code each shard's guard-band bytes (head [0, 64),
+// tail [S - 64, S)) inside the main kernel, in the shard's first / last
+// tile, instead of the second gf_odd_edges launch (round 6)
+#define HBEC_ODD_EDGE_FUSE 1
 #endif
 
 // ---- ShardHash (md5.hip) ----

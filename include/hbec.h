@@ -344,6 +344,11 @@ int hbec_batcher_stats(hbec_batcher* batcher, uint64_t* batches, uint64_t* strip
  * a compiled bit-plane schedule (8+4, 6+4 encode) may take it where this
  * reports an aligned kind (hbec.cpp rec_route). */
 int hbec_set_force_stream(int on);
+/* Test hook: tiles per launch of the odd-shard strided kernels (0 = the
+ * default 1 Mi), so a test can make a small batch cross launch boundaries:
+ * each launch rebuilds its objects' records (gf_odd_objrec) and offsets its
+ * bases by its first object.  Process-wide; not for production use. */
+int hbec_set_odd_chunk_tiles(uint64_t tiles);
 int hbec_kernel_info(int k, int r, uint64_t shard_len, int* tile_bytes, int* kind, int* blocks_per_cu);
 /* Launches since load of the odd-shard main kernels (any alignment, k <= 12
  * per pass): bitplane = the compiled XOR-network kernels of the fixed encode

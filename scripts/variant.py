@@ -14,7 +14,7 @@ sys.path.insert(0, str(ROOT))
 from hummingbird_amd import build as hb  # noqa: E402
 
 args = sys.argv[1:]
-units = ["odd_bp.hip", "odd.hip"]
+units = ["all"]  # every unit: a -D that one unit reads and another does not would build an ODR-inconsistent hybrid
 if "--units" in args:
     i = args.index("--units")
     units = args[i + 1].split(",")

@@ -2,9 +2,9 @@
 
 hummingbird_amd/build.py build_asan() builds libhbec with the sanitizers on
 the host code only (device code is not instrumented; this pool runs no GPU
-ASan) plus the C driver tests/native/host_asan.c.  The CPU test runs the
-host-only entry points; the GPU test drives the staging ring, zero-copy,
-multi-device split, per-call staging, batcher and ecutils loops."""
+ASan) plus the C driver tests/native/host_asan.c.  The test runs the
+host-only entry points.  (A GPU variant existed until round 5; the sanitizer
+build does not travel to the GPU box, so it could only ever skip there.)"""
 import os
 import subprocess
 
@@ -27,9 +27,3 @@ def test_host_asan_cpu():
     assert out.returncode == 0, out.stderr[-4000:]
     assert "host_asan cpu ok" in out.stdout
 
-
-@pytest.mark.gpu
-def test_host_asan_gpu():
-    out = subprocess.run([_exe(), "gpu"], capture_output=True, text=True, env=ENV, timeout=110)
-    assert out.returncode == 0, out.stderr[-4000:]
-    assert "host_asan gpu ok" in out.stdout

@@ -22,7 +22,11 @@ import route_rule as R
 pytestmark = pytest.mark.gpu
 
 _S_CHOICES = [R.MIN_S_BIG - 16, R.MIN_S_BIG, R.MIN_S - 16, R.MIN_S, R.MIN_S + 16, R.MIN_S + 128, R.MIN_S + 1,
-              R.MIN_S + 8, 65536, 65536 + 16, 98304 + 80, 3072, 4096 + 16, 24576 + 128]
+              R.MIN_S + 8, 65536, 65536 + 16, 98304 + 80, 3072, 4096 + 16, 24576 + 128,
+              # round 6: the packed limit of 5 <= k <= 8 (32 KiB), odd mid-size shards (fused guard
+              # band), and either side of one and two tiles per shard (992-B and 2016-B tiles:
+              # the guard band is fused from two tiles up)
+              32768, 32784, 4095, 8191, 16383, 161, 1087, 1088, 1089, 2111, 2112, 2113]
 
 
 def _case(seed):

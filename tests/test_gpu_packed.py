@@ -22,13 +22,16 @@ def _gpu():
 
 
 SHAPES = [(1, 1), (2, 1), (3, 2), (4, 2), (5, 3), (8, 3), (6, 2)]
-LENS = [16, 48, 96, 256, 512, 1008, 1024, 1040, 2032, 3056]
+# 5 <= K <= 8 up to 32 KiB since round 6: both sides of the old 3 KiB limit,
+# of the pipelined kernel's 3 KiB tiles and of the new 32 KiB limit
+LENS = [16, 48, 96, 256, 512, 1008, 1024, 1040, 2032, 3056, 3072, 4096, 4112, 6160, 8192, 12304, 16384, 32768, 32784]
 
 
 def _packed(k, s):
     """The dispatch rule of kernels.hip is_packed_shape (no device needed at
-    collection): S < 2 KiB for K <= 4, S < 3 KiB for 5 <= K <= 8."""
-    return s % 16 == 0 and s < (2048 if k <= 4 else 3072)
+    collection): S < 2 KiB for K <= 4, S <= 32 KiB for 5 <= K <= 8
+    (tuning.h HBEC_PACKED_MAX_BIG)."""
+    return s % 16 == 0 and s < (2048 if k <= 4 else 32784)
 
 
 def _cases():
@@ -41,6 +44,8 @@ def _cases():
 @pytest.mark.parametrize("k,m,s", list(_cases()))
 @pytest.mark.parametrize("n", [1, 7, 333])
 def test_packed_encode_matches_oracle(k, m, s, n):
+    if s > 4096 and n == 333:
+        n = 37  # the oracle's time, not coverage: 37 objects still span many tiles
     pad = 48  # object rows longer than k*S: the views' strides differ from S
     objs = torch.empty((n, k * s + pad), dtype=torch.uint8, device="cuda")
     B.fill_splitmix(objs, k * s + pad, first=k * 1000 + s)
@@ -58,7 +63,8 @@ def test_packed_encode_matches_oracle(k, m, s, n):
     assert (got[:, m * s:] == 0xC5).all()  # nothing written past the last shard
 
 
-@pytest.mark.parametrize("k,m,s", [(8, 3, 512), (4, 2, 1024), (4, 2, 48), (3, 2, 2032), (8, 3, 3056)])
+@pytest.mark.parametrize("k,m,s", [(8, 3, 512), (4, 2, 1024), (4, 2, 48), (3, 2, 2032), (8, 3, 3056), (8, 3, 4096),
+                                   (6, 3, 12304), (8, 3, 32768)])
 def test_packed_reconstruct_three_arrays(k, m, s):
     n = 501
     enc = RS.New(k, m)
@@ -82,7 +88,10 @@ def test_packed_kernel_is_selected_for_short_shards():
     assert B.kernel_info(8, 3, 512)["kind"] == "packed"
     assert B.kernel_info(4, 2, 1024)["kind"] == "packed"
     assert B.kernel_info(4, 2, 2048)["kind"] == "pipelined"
-    assert B.kernel_info(8, 3, 3072)["kind"] == "pipelined"
+    assert B.kernel_info(8, 3, 3072)["kind"] == "packed"
+    assert B.kernel_info(8, 3, 32768)["kind"] == "packed"
+    assert B.kernel_info(8, 3, 32784)["kind"] == "pipelined"
+    assert B.kernel_info(8, 4, 4096)["kind"] != "packed"  # no 4-row packed instance
 
 
 def _verify_packed(k, s):

@@ -90,7 +90,43 @@ def test_kernel_info_reports_the_route():
     assert B.kernel_info(4, 2, 1 << 18)["kind"] == "pipelined"
     assert B.kernel_info(8, 3, 1 << 17)["kind"] == "pipelined"
     assert B.kernel_info(8, 3, (1 << 17) + 16)["kind"] == "records"
-    assert B.kernel_info(8, 3, 4096 + 16)["kind"] == "pipelined"
+    assert B.kernel_info(8, 3, 4096 + 16)["kind"] == "packed"  # 5 <= k <= 8 packed to 32 KiB (round 6)
+    assert B.kernel_info(8, 3, 32768 + 16)["kind"] == "pipelined"
     assert B.kernel_info(10, 4, 1 << 17)["kind"] == "records"
     assert B.kernel_info(10, 4, 1 << 14)["kind"] == "streaming"  # the aligned k > 8 kernel
     assert B.kernel_info(8, 3, 512)["kind"] == "packed"
+
+
+@pytest.mark.parametrize("k,m,s", [(10, 5, 24577), (9, 6, 8193), (12, 5, 32768), (11, 8, 4099)])
+def test_verify_wide_route_9_12_more_than_4_rows(k, m, s):
+    """Verify of 9 <= k <= 12 with m > 4 parity rows takes
+    gf_verify_wide (one read-only pass per <= 8 rows, hbec.cpp verify_views),
+    not the odd kernels: oracle parity passes clean, and single-byte flips in
+    the first and last parity row and in a data shard flag exactly their
+    objects."""
+    n = 9
+    pitch = (k + m) * s + 16
+    buf = torch.empty(n * pitch + 64, dtype=torch.uint8, device="cuda")
+    B.fill_splitmix(buf.view(1, -1), buf.numel(), first=k * 100 + m)
+    host = buf.cpu().numpy()
+    rows = CO.build_matrix(k, m)[k:]
+    for o in range(n):
+        b = 3 + o * pitch
+        want = CO.apply(rows, [host[b + j * s:b + (j + 1) * s] for j in range(k)])
+        for r in range(m):
+            host[b + (k + r) * s:b + (k + r + 1) * s] = want[r]
+    buf.copy_(torch.from_numpy(host))
+    views = [(buf.data_ptr() + 3 + i * s, pitch) for i in range(k + m)]
+    enc = RS.New(k, m)
+    flags = torch.zeros(n, dtype=torch.int32, device="cuda")
+    before = _odd_launches()
+    B.verify_views(enc, views, n, s, flags)
+    torch.cuda.synchronize()
+    assert _odd_launches() == before, "m > 4 rows: gf_verify_wide"
+    assert int(flags.count_nonzero()) == 0
+    hits = {1: (k, 0), 4: (k + m - 1, s - 1), 7: (k // 2, s // 2)}  # object: (shard, byte)
+    for o, (i, p) in hits.items():
+        buf[3 + o * pitch + i * s + p] ^= 0x11
+    B.verify_views(enc, views, n, s, flags)
+    torch.cuda.synchronize()
+    assert flags.nonzero().flatten().tolist() == sorted(hits)

@@ -3,7 +3,7 @@
 bench.py reports `roofline.traffic` and the odd legs' `traffic` only from a
 PMC summary collected on exactly the sources it hashes (bench.py
 KERNEL_SOURCES / ODD_SOURCES, including tuning.h): an edit to any of them
-after the last `scripts/r5_final.sh first` silently drops those fields from
+after the last `scripts/final.sh first` silently drops those fields from
 the driver's bench line.  This test makes that visible before the round ends.
 """
 import bench
@@ -18,7 +18,7 @@ def test_odd_pmc_summary_is_fresh():
     data, path, why = bench.load_pmc()
     assert data is not None, why
     assert data.get("odd_sources_sha256") == bench.kernel_sources_sha256(bench.ODD_SOURCES), (
-        f"{path} was collected on other odd-kernel sources: rerun scripts/r5_final.sh first")
+        f"{path} was collected on other odd-kernel sources: rerun scripts/final.sh first")
     # the odd legs read these kernels' bytes from it
     for name in ("gf_odd_edges<0, false, 128>", "gf_odd_edges<2, false, 128>", "gf_odd_edges_plan<0, false, 128>"):
         assert name in data["kernels"], name
