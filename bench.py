@@ -432,18 +432,37 @@ def small_objects(n=65536, obj_len=4096, reps=100, settle=200):
     return out
 
 
-def _odd_kernel_traffic(kern, k, r, mode, plan=False):
-    """PMC bytes per launch of the odd-shard kernel coding (k, r, mode), by the
-    name it runs under: gf_odd_rec<k, r, mode, XS, LIST> (XS: the bit-plane
-    schedule or -1, LIST: plans' tile-list instance) or gf_odd<k, r, mode>."""
-    pre = (f"gf_odd_rec<{k}, {r}, {mode}, ",)
-    for name, v in sorted(kern.items()):
-        if name.startswith(pre) and name.endswith("true>" if plan else "false>"):
-            return name, v.get("hbm_bytes_per_launch")
-    name = f"gf_odd<{k}, {r}, {mode}>"
-    if not plan and name in kern:
-        return name, kern[name].get("hbm_bytes_per_launch")
-    return None, None
+def _route_delta(fn):
+    """Run fn once and return which odd-shard kernel families it launched
+    (B.odd_path_stats() after minus before)."""
+    p0 = B.odd_path_stats()
+    fn()
+    torch.cuda.synchronize()
+    p1 = B.odd_path_stats()
+    return {x: p1[x] - p0[x] for x in p1}
+
+
+def _odd_kernel_traffic(kern, k, r, mode, paths, plan=False):
+    """PMC bytes per launch of the odd-shard kernel that coded (k, r, mode),
+    chosen by the route the leg actually took (`paths`, from _route_delta):
+    the bit-plane instance gf_odd_rec<k, r, mode, XS, LIST> (XS >= 0), the
+    table record instance (XS = -1), or the strided gf_odd<k, r, mode>; LIST =
+    plans' tile-list instance.  None when the summary holds no instance, or
+    more than one, of the family that ran."""
+    pre = f"gf_odd_rec<{k}, {r}, {mode}, "
+    tail = "true>" if plan else "false>"
+    recs = sorted(x for x in kern if x.startswith(pre) and x.endswith(tail))
+    if paths.get("bitplane", 0) > 0:
+        pick = [x for x in recs if not x.startswith(pre + "-1,")]
+    elif paths.get("records", 0) > 0:
+        pick = [x for x in recs if x.startswith(pre + "-1,")]
+    elif paths.get("strided", 0) > 0 and not plan:
+        pick = [x for x in (f"gf_odd<{k}, {r}, {mode}>",) if x in kern]
+    else:
+        pick = []
+    if len(pick) != 1:
+        return None, None
+    return pick[0], kern[pick[0]].get("hbm_bytes_per_launch")
 
 
 def odd_leg(k, m, n, obj_len, first, reps=20, settle=40, pmc=None):
@@ -468,8 +487,10 @@ def odd_leg(k, m, n, obj_len, first, reps=20, settle=40, pmc=None):
                        "device-resident", "shard_bytes": s}
     for _ in range(settle):
         ops["encode"]()
+    routes = {}
     for name, fn in ops.items():
-        for _ in range(3):
+        routes[name] = _route_delta(fn)
+        for _ in range(2):
             fn()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
@@ -479,14 +500,19 @@ def odd_leg(k, m, n, obj_len, first, reps=20, settle=40, pmc=None):
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / reps
         gbs = nbytes[name] / (ms * 1e-3) / 1e9
-        out[name] = {"ms": round(ms, 4), "GB_s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
+        out[name] = {"ms": round(ms, 4), "GB_s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
+                     "edges": "fused" if routes[name]["fused"] > 0 else "separate launch"}
     if pmc is not None:
         kern = pmc.get("kernels", {})
         for name, (r, mode) in (("encode", (m, 0)), ("reconstruct", (2, 0)), ("verify", (m, 2))):
-            kname, t = _odd_kernel_traffic(kern, k, r, mode)
-            # (the edge kernel of a batch of >= kOddEdgeSplitObjs objects: one thread per slot, all outputs)
-            te = kern.get("gf_odd_edges<2, false, 128>" if name == "verify" else "gf_odd_edges<0, false, 128>", {}).get(
-                "hbm_bytes_per_launch")
+            kname, t = _odd_kernel_traffic(kern, k, r, mode, routes[name])
+            # the edge kernel when the guard bands took their own launch (a
+            # batch of >= kOddEdgeSplitObjs objects: one thread per slot, all outputs)
+            te = 0
+            if routes[name]["edges"] > 0:
+                te = kern.get("gf_odd_edges<2, false, 128>" if name == "verify" else "gf_odd_edges<0, false, 128>",
+                              {}).get("hbm_bytes_per_launch")
+                t = None if te is None else t
             if t is not None:
                 out[name]["kernel"] = kname
                 out[name]["traffic"] = int(t + (te or 0))
@@ -557,6 +583,7 @@ def random_objects(n=4096, shapes=((4, 2), (8, 3)), reps=20, settle=40):
             po += m * s
         enc = RS.New(k, m)
         plan = B.StripePlan(enc, objects=objs)
+        paths = _route_delta(plan.encode)
         for _ in range(settle):
             plan.encode()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -577,15 +604,13 @@ def random_objects(n=4096, shapes=((4, 2), (8, 3)), reps=20, settle=40):
         bad = int(flags.item())
         leg = {"objects": n, "bytes": nbytes, "ms": round(ms, 4), "GB_s": round(gbs, 1),
                "frac": round(gbs / HBM_PEAK_GBS, 4), "parity_ok": bad == 0}
+        leg["edges"] = "fused" if paths["fused"] > 0 else "separate launch"
         if fresh:
-            kern = pmc.get("kernels", {})
-            kname, t = _odd_kernel_traffic(kern, k, m, 0, plan=True)
-            extra = sum((kern.get(x, {}).get("hbm_bytes_per_launch") or 0)
-                        for x in ("gf_odd_edges_plan<0, false, 128>", "gf_odd_planrec"))
+            kname, t = _plan_traffic(pmc.get("kernels", {}), k, m, paths)
             if t is not None:
                 leg["kernel"] = kname
-                leg["traffic"] = int(t + extra)
-                leg["traffic_ratio"] = round((t + extra) / nbytes, 4)
+                leg["traffic"] = int(t)
+                leg["traffic_ratio"] = round(t / nbytes, 4)
         out["shapes"][f"{k}+{m}"] = leg
         del plan, data, parity, flags
         torch.cuda.empty_cache()
@@ -595,19 +620,18 @@ def random_objects(n=4096, shapes=((4, 2), (8, 3)), reps=20, settle=40):
 
 
 def _plan_traffic(kern, k, r, paths):
-    """PMC bytes per launch of a plan pass's record kernel (the bit-plane or
-    the table instance, by which one the pass launched: `paths` is
-    B.odd_path_stats() after minus before) plus its record and edge kernels."""
-    names = sorted(x for x in kern if x.startswith(f"gf_odd_rec<{k}, {r}, 0, ") and x.endswith("true>"))
-    bp = [x for x in names if not x.startswith(f"gf_odd_rec<{k}, {r}, 0, -1,")]
-    tab = [x for x in names if x.startswith(f"gf_odd_rec<{k}, {r}, 0, -1,")]
-    pick = bp if paths[0] > 0 else tab
-    if len(pick) != 1:
+    """PMC bytes per launch of a plan pass: the record kernel of the family
+    that ran (`paths`, from _route_delta), the per-stripe record writer, and
+    the guard-band kernel when the bands took their own launch."""
+    kname, t = _odd_kernel_traffic(kern, k, r, 0, paths, plan=True)
+    if t is None:
         return None, None
-    extra = sum((kern.get(x, {}).get("hbm_bytes_per_launch") or 0)
-                for x in ("gf_odd_edges_plan<0, false, 128>", "gf_odd_planrec"))
-    t = kern[pick[0]].get("hbm_bytes_per_launch")
-    return pick[0], None if t is None else t + extra
+    extra = [kern.get("gf_odd_planrec", {}).get("hbm_bytes_per_launch")]
+    if paths["edges"] > 0:
+        extra.append(kern.get("gf_odd_edges_plan<0, false, 128>", {}).get("hbm_bytes_per_launch"))
+    if any(x is None for x in extra):
+        return None, None
+    return kname, t + sum(extra)
 
 
 def mid_objects(n=16384, shapes=((4, 2), (8, 3)), reps=20, settle=40):
@@ -677,11 +701,7 @@ def mid_objects(n=16384, shapes=((4, 2), (8, 3)), reps=20, settle=40):
                 views_of = [([(a + j * s, 0) for j in range(k)] + [(b + r * s, 0) for r in range(m)], s)
                             for a, b, s in objs]
                 keep = (data, parity)
-            p0 = B.odd_path_stats()
-            plan.encode()
-            torch.cuda.synchronize()
-            p1 = B.odd_path_stats()
-            paths = [p1[x] - p0[x] for x in ("bitplane", "records", "strided")]
+            paths = _route_delta(plan.encode)
             ms = timed(plan.encode)
             gbs = nbytes / (ms * 1e-3) / 1e9
             flags = torch.zeros(1, dtype=torch.int32, device="cuda")
@@ -690,7 +710,7 @@ def mid_objects(n=16384, shapes=((4, 2), (8, 3)), reps=20, settle=40):
             torch.cuda.synchronize()
             leg = {"objects": n, "bytes": nbytes, "ms": round(ms, 4), "GB_s": round(gbs, 1),
                    "frac": round(gbs / HBM_PEAK_GBS, 4), "parity_ok": int(flags.item()) == 0,
-                   "launches": {"bitplane": paths[0], "records": paths[1], "strided": paths[2]}}
+                   "launches": paths}
             if kern:
                 kname, t = _plan_traffic(kern, k, m, paths)
                 if t is not None:

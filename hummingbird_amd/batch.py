@@ -149,10 +149,14 @@ def kernel_info(k: int, r: int, shard_len: int):
 
 def odd_path_stats():
     """Launches since load of the odd-shard main kernels, by family:
-    bit-plane (compiled encode XOR networks), table-multiply records, strided."""
+    bit-plane (compiled encode XOR networks), table-multiply records, strided;
+    and the guard bands: separate edge-kernel launches (`edges`) and main
+    launches that coded their own (`fused`)."""
     b, r, s = C.c_uint64(), C.c_uint64(), C.c_uint64()
     check(N.lib().hbec_odd_path_stats(C.byref(b), C.byref(r), C.byref(s)))
-    return {"bitplane": b.value, "records": r.value, "strided": s.value}
+    e, f = C.c_uint64(), C.c_uint64()
+    check(N.lib().hbec_odd_edge_stats(C.byref(e), C.byref(f)))
+    return {"bitplane": b.value, "records": r.value, "strided": s.value, "edges": e.value, "fused": f.value}
 
 
 def set_odd_chunk_tiles(tiles: int) -> None:

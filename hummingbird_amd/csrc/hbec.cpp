@@ -218,7 +218,7 @@ static int odd_launches(const PassArgs& a, int K, int R, int mode, bool accumula
                 }
                 c.tiles_per_obj = (uint32_t)tpo;
                 c.n_tiles = (uint32_t)(no * tpo);
-                c.fuse = odd_edge_fuse(K1, R, m, use_rec, xs) && K <= kOddMaxK && tpo >= 2 &&
+                c.fuse = odd_edge_fuse(K1, R, m, use_rec, xs, false, shard_len) && K <= kOddMaxK && tpo >= 2 &&
                                  shard_len < (1ull << 30) ? 1u : 0u;
                 fused = c.fuse != 0u;
                 const uint64_t wpb = odd_waves_per_block(xs);

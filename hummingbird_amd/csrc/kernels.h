@@ -185,10 +185,10 @@ hipError_t launch_odd_planrec(int k, int r, int mode, const UPlanArgs& p, const 
                               uint32_t* recs, hipStream_t stream);
 hipError_t launch_odd(int k, int r, int mode, const PassArgs& a, uint32_t* flags, const uint32_t* recs, int grid,
                       hipStream_t stream, int xs = -1);
-// a strided pass of this shape codes the guard band inside its main kernel
-// when PassArgs::fuse is set (HBEC_ODD_EDGE_FUSE: apply passes; records:
-// the gf_odd_rec kernel, else gf_odd)
-bool odd_edge_fuse(int k, int r, int mode, bool records, int xs, bool list = false);
+// a pass of this shape whose shards are at most max_s bytes codes the guard
+// band inside its main kernel when PassArgs::fuse is set (HBEC_ODD_EDGE_FUSE,
+// HBEC_ODD_EDGE_MAX_S: apply passes; records: the gf_odd_rec kernel, else gf_odd)
+bool odd_edge_fuse(int k, int r, int mode, bool records, int xs, bool list, uint64_t max_s);
 // the guard-band bytes of every shard (after the main launches of a pass;
 // k <= kMaxK inputs, a.n_obj objects; verify flags mismatching objects)
 hipError_t launch_odd_edges(int k, int r, int mode, const PassArgs& a, uint32_t* flags, hipStream_t stream);

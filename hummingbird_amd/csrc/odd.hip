@@ -403,9 +403,10 @@ uint32_t odd_tiles_per_obj(int k, int mode, uint64_t shard_len, bool records, in
 
 bool odd_supported(int k, int r) { return k >= 1 && k <= kOddMaxK && r >= 1 && r <= kMaxR; }
 
-bool odd_edge_fuse(int k, int r, int mode, bool records, int xs, bool list) {
+bool odd_edge_fuse(int k, int r, int mode, bool records, int xs, bool list, uint64_t max_s) {
     static const bool on = tune_knob("HBEC_ODD_EDGE_FUSE", 1) != 0;  // tuning builds: 0 = the separate edge launch
-    return on && (records ? odd_rec_edge(k, r, mode, xs, list) : odd_strided_edge(k, r, mode));
+    static const uint64_t lim = (uint64_t)tune_knob("HBEC_ODD_EDGE_MAX_S", HBEC_ODD_EDGE_MAX_S);
+    return on && max_s <= lim && (records ? odd_rec_edge(k, r, mode, xs, list) : odd_strided_edge(k, r, mode));
 }
 
 int odd_bp_schedule(int k, int r, int mode, const uint32_t (*tab)[kMaxK][5], bool plan) {
@@ -426,11 +427,13 @@ int odd_bp_schedule(int k, int r, int mode, const uint32_t (*tab)[kMaxK][5], boo
 }
 
 std::atomic<uint64_t> g_odd_launches[3];  // bit-plane, record, strided (hbec_odd_path_stats)
+std::atomic<uint64_t> g_odd_edge_launches[2];  // guard-band launches, main launches coding them (hbec_odd_edge_stats)
 
 hipError_t launch_odd(int k, int r, int mode, const PassArgs& a, uint32_t* flags, const uint32_t* recs, int grid,
                       hipStream_t stream, int xs) {
     if (!pos32_shard(a.shard_len)) return hipErrorInvalidValue;  // 32-bit shard positions
     g_odd_launches[xs >= 0 ? 0 : (recs ? 1 : 2)].fetch_add(1, std::memory_order_relaxed);
+    if (a.fuse) g_odd_edge_launches[1].fetch_add(1, std::memory_order_relaxed);
     if (xs >= 0) {
         if (!recs || mode == kOddAcc || xs >= kXorShapeCount || kXorShapes[xs].k != k || kXorShapes[xs].R != r)
             return hipErrorInvalidValue;
@@ -464,6 +467,7 @@ hipError_t launch_odd_edges(int k, int r, int mode, const PassArgs& a, uint32_t*
         {{(const void*)&gf_odd_edges<kOddVerify, false, kOddEdgeSlots>, (const void*)&gf_odd_edges<kOddVerify, false, kOddEdgeSlotsLong>},
          {(const void*)&gf_odd_edges<kOddVerify, true, kOddEdgeSlots>, (const void*)&gf_odd_edges<kOddVerify, true, kOddEdgeSlotsLong>}}};
     const void* fn = fns[mode][split ? 1 : 0][lng ? 1 : 0];
+    g_odd_edge_launches[0].fetch_add(1, std::memory_order_relaxed);
     void* args[] = {const_cast<PassArgs*>(&a), &k, &r, &flags};
     return hipLaunchKernel(fn, dim3(grid), dim3(kBlockThreads), args, 0, stream);
 }
@@ -481,6 +485,7 @@ hipError_t launch_odd_edges_plan(int k, int r, int mode, const UPlanArgs& p, con
         {{(const void*)&gf_odd_edges_plan<kOddAcc, false, kOddEdgeSlots>, (const void*)&gf_odd_edges_plan<kOddAcc, false, kOddEdgeSlotsLong>},
          {(const void*)&gf_odd_edges_plan<kOddAcc, true, kOddEdgeSlots>, (const void*)&gf_odd_edges_plan<kOddAcc, true, kOddEdgeSlotsLong>}}};
     const void* fn = fns[mode == kOddAcc ? 1 : 0][split ? 1 : 0][lng ? 1 : 0];
+    g_odd_edge_launches[0].fetch_add(1, std::memory_order_relaxed);
     void* args[] = {const_cast<UPlanArgs*>(&p), &erecs, &n_erecs, &k, &r};
     return hipLaunchKernel(fn, dim3(grid), dim3(kBlockThreads), args, 0, stream);
 }
@@ -512,5 +517,11 @@ extern "C" int hbec_odd_path_stats(uint64_t* bitplane, uint64_t* records, uint64
     if (bitplane) *bitplane = hbec::g_odd_launches[0].load();
     if (records) *records = hbec::g_odd_launches[1].load();
     if (strided) *strided = hbec::g_odd_launches[2].load();
+    return 0;
+}
+
+extern "C" int hbec_odd_edge_stats(uint64_t* edge_launches, uint64_t* fused_launches) {
+    if (edge_launches) *edge_launches = hbec::g_odd_edge_launches[0].load();
+    if (fused_launches) *fused_launches = hbec::g_odd_edge_launches[1].load();
     return 0;
 }

@@ -215,7 +215,13 @@ typedef __attribute__((address_space(1))) uint8_t gu8_t;
 // load under a branch made the compiler wait for the NEXT tile's loads at
 // every finish).  Edge flags (wave-uniform): 1 first tile, 2 last tile;
 // the host fuses only when every shard has >= 2 tiles (never both).
-__device__ __forceinline__ uint32_t ld_u8(uint64_t addr) { return *reinterpret_cast<const gu8_t*>(addr); }
+// The edge bytes are loaded as their aligned dwords and extracted in the
+// finish (odd_edge_byte): a byte load's value reached the loop's back edge as
+// a masked copy (v_and 0xff) that waited for every load in flight, the next
+// tile's included (8+3 records 60 -> 43 %).
+typedef __attribute__((address_space(1))) const uint32_t gu32_c;
+__device__ __forceinline__ uint32_t ld_dw(uint64_t addr) { return *reinterpret_cast<gu32_c*>(addr & ~(uint64_t)3); }
+__device__ __forceinline__ uint32_t odd_edge_byte(uint32_t dw, uint32_t addr_lo) { return dw >> (8u * (addr_lo & 3u)); }
 __device__ __forceinline__ void st_u8(uint64_t addr, uint32_t v) { *reinterpret_cast<gu8_t*>(addr) = (uint8_t)v; }
 
 // lane offset of an edge tile's byte (0 on the others)
@@ -276,10 +282,11 @@ __host__ __device__ constexpr bool odd_two_blocks(int k, int r, int mode, bool m
     return !mir && mode == kOddApply && k <= 10 && k * r >= 36;
 }
 // gf_odd strided apply codes the guard band in the main kernel
-// (HBEC_ODD_EDGE_FUSE), except the register-bound 2-block pinned instances
-// (9+4 / 10+4 spilled with it; strided 10+4 takes the record kernels)
+// (HBEC_ODD_EDGE_FUSE) for K <= 4, R <= 3; above (and 2..4 x 4), the extra edge words made the
+// allocator copy the whole next tile at the loop's back edge (a vmcnt(0)
+// per tile in gf_odd<8,2,0>; the 2-block pinned 9+4 / 10+4 spilled)
 __host__ __device__ constexpr bool odd_strided_edge(int k, int r, int mode) {
-    return HBEC_ODD_EDGE_FUSE != 0 && mode == kOddApply && !odd_two_blocks(k, r, mode, false);
+    return (HBEC_ODD_EDGE_FUSE & 1) != 0 && mode == kOddApply && k <= 4 && r <= 3 && !odd_two_blocks(k, r, mode, false);
 }
 template <int K, int R, int MODE, bool MIR>
 __host__ __device__ constexpr bool odd_pin_on() {
@@ -400,7 +407,6 @@ struct OddRegs {
     // accumulate mode the old output blocks (with the inputs, one tile ahead)
     static constexpr int NL = K + (MODE == kOddVerify || MODE == kOddAcc ? R : 0);
     u32x4 x[U][NL];
-    uint32_t e[K];  // guard-band bytes (edge tiles of fused apply passes; unused otherwise)
 };
 
 template <int K, int R, int U, int MODE, bool CARRY = false>
@@ -444,13 +450,17 @@ __device__ __forceinline__ void odd_st(uint64_t addr, const u32x4& v, bool mine)
     if (mine) st16_addr(addr, v);
 }
 
-template <int K, int R, int U, int MODE, bool MIR = false, bool CARRY = false, bool EDGE = false>
-__device__ __forceinline__ void odd_finish(const OddRegs<K, R, U, MODE>& X, const OddTile<K, R>& b,
-                                           const TabArray& tab, const Tables<K, R, kOddVMin>& tb, uint32_t lane,
-                                           uint32_t* flags, uint32_t mir = 0, uint32_t edge = 0) {
-    if (EDGE && edge != 0u) {  // fused guard band (wave-uniform): the bands of gf_odd_edges
-        uint32_t acc[R];
-        gf_dot1<K, R, kOddVMin>(acc, X.e, tab, tb);
+// gf_odd's fused guard band of one tile (edge: its flags, wave-uniform): the
+// bands of gf_odd_edges, from the edge words e[] loaded with the tile
+template <int K, int R>
+__device__ __forceinline__ void odd_edges(const uint32_t (&e)[K], const OddTile<K, R>& b, const TabArray& tab,
+                                          const Tables<K, R, kOddVMin>& tb, uint32_t lane, uint32_t edge) {
+    {
+        uint32_t acc[R], x[K];
+        const uint32_t p = odd_edge_off(edge, (uint32_t)b.S, lane);
+#pragma unroll
+        for (int j = 0; j < K; ++j) x[j] = odd_edge_byte(e[j], (uint32_t)b.in[j] + p);
+        gf_dot1<K, R, kOddVMin>(acc, x, tab, tb);
         const uint32_t S = (uint32_t)b.S, top = S - (uint32_t)kOddGuard - 16u;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
@@ -459,6 +469,12 @@ __device__ __forceinline__ void odd_finish(const OddRegs<K, R, U, MODE>& X, cons
             odd_edge_store(b.out[r], acc[r], edge, S, lane, (uint32_t)kOddGuard + e, qmax + 16u, true);
         }
     }
+}
+
+template <int K, int R, int U, int MODE, bool MIR = false, bool CARRY = false>
+__device__ __forceinline__ void odd_finish(const OddRegs<K, R, U, MODE>& X, const OddTile<K, R>& b,
+                                           const TabArray& tab, const Tables<K, R, kOddVMin>& tb, uint32_t lane,
+                                           uint32_t* flags, uint32_t mir = 0) {
     uint32_t sh[K + (MODE == kOddVerify ? R : 0)];
 #pragma unroll
     for (int j = 0; j < K; ++j) sh[j] = __builtin_amdgcn_readfirstlane(((uint32_t)b.in[j] + (uint32_t)b.c) & 3u);
@@ -607,23 +623,46 @@ __device__ __forceinline__ void odd_body(const Src& src, uint32_t n, const TabAr
     const uint32_t dw = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (wave0 >= n) return;  // whole blocks only: the loop below has block barriers
     const Tables<K, R, kOddVMin> tb = load_tables<K, R, kOddVMin>(tab);
-    // fused guard band: every tile issues the K edge byte loads (an edge
-    // tile from its shards, the others from one hot line), so the loads in
-    // flight do not depend on the path (odd_edge_off)
-    auto edge_load = [&](OddRegs<K, R, U, MODE>& Z, const OddTile<K, R>& b, const typename Src::Id& i) {
+    // Fused guard band: a tile's K edge words are loaded right before its
+    // columns and coded after the previous tile's finish, in the same loop
+    // step, so they never cross the loop's back edge (a loop-carried copy
+    // waited for the next tile's loads: 8+3 60 -> 43 %).  Only edge tiles
+    // issue them (HBEC_ODD_EDGE_COND): issued before the tile's column loads,
+    // a skipped branch leaves the count the previous tile's columns are
+    // waited with unchanged (LLVM keeps the shortest distance of the two
+    // paths), and the extra load instructions of every other tile cost
+    // 2-4 points (r06_ab_fuse.jsonl).
+    auto edge_load = [&](uint32_t (&e)[K], const OddTile<K, R>& b, const typename Src::Id& i) {
         if constexpr (Src::kEdge) {
             const uint32_t fl = src.edge(i), eo = odd_edge_off(fl, (uint32_t)b.S, lane);
+            if (HBEC_ODD_EDGE_COND == 0 || fl != 0u) {
 #pragma unroll
-            for (int j = 0; j < K; ++j) Z.e[j] = ld_u8(b.in[j] + (fl != 0u ? (uint64_t)eo : (uint64_t)(uint32_t)b.c));
+                for (int j = 0; j < K; ++j) e[j] = ld_dw(b.in[j] + (fl != 0u ? (uint64_t)eo : (uint64_t)(uint32_t)b.c));
+            }
+        }
+    };
+    auto edge_code = [&](const uint32_t (&e)[K], const typename Src::Id& i) {
+        if constexpr (Src::kEdge) {
+            const uint32_t fl = src.edge(i);
+            if (fl != 0u) {
+                OddTile<K, R> b;
+                src.at(b, i);
+                odd_edges<K, R>(e, b, tab, tb, lane, fl);
+            }
         }
     };
     typename Src::Id cur = src.id(wave0 + dw, n);
     OddRegs<K, R, U, MODE> X;
+    // the edge words are carried through the loop unchanged by non-edge
+    // tiles (an undefined value on that path was materialised as zeros,
+    // each write waiting for the loads in flight: vmcnt(0) per tile)
+    uint32_t e[K] = {};
     {
         OddTile<K, R> b;
         src.at(b, cur);
+        edge_load(e, b, cur);
         odd_load<K, R, U, MODE, Src::kCarry>(X, b, lane);
-        edge_load(X, b, cur);
+        edge_code(e, cur);
     }
     typename Src::Id nxt = src.id(wave0 + dw + nw, n);
     for (uint32_t b0 = wave0 + nw; b0 < n; b0 += nw) {  // block-uniform trip count
@@ -631,8 +670,8 @@ __device__ __forceinline__ void odd_body(const Src& src, uint32_t n, const TabAr
         {
             OddTile<K, R> b;
             src.at(b, nxt);
+            edge_load(e, b, nxt);
             odd_load<K, R, U, MODE, Src::kCarry>(Y, b, lane);
-            edge_load(Y, b, nxt);
         }
         // one block barrier per tile for apply; none for Verify (8+3 57 -> 66 %,
         // 6+3 63 -> 70 %, profiles/r03_tune_odd3.jsonl)
@@ -641,15 +680,16 @@ __device__ __forceinline__ void odd_body(const Src& src, uint32_t n, const TabAr
         {
             OddTile<K, R> b;
             src.at(b, cur);
-            odd_finish<K, R, U, MODE, MIR, Src::kCarry, Src::kEdge>(X, b, tab, tb, lane, flags, mir, src.edge(cur));
+            odd_finish<K, R, U, MODE, MIR, Src::kCarry>(X, b, tab, tb, lane, flags, mir);
         }
+        edge_code(e, nxt);
         X = Y;
         cur = nxt;
         nxt = after;
     }
     OddTile<K, R> b;
     src.at(b, cur);
-    odd_finish<K, R, U, MODE, MIR, Src::kCarry, Src::kEdge>(X, b, tab, tb, lane, flags, mir, src.edge(cur));
+    odd_finish<K, R, U, MODE, MIR, Src::kCarry>(X, b, tab, tb, lane, flags, mir);
 }
 
 template <int K, int R, int MODE>
@@ -693,14 +733,15 @@ __host__ __device__ constexpr uint32_t odd_rec_wcol(int u) { return CARRY ? 64u 
 // at 40 % of 8 TB/s).
 __host__ __device__ constexpr bool odd_rec_lds(int k) { return k >= HBEC_ODD_LDS_MINK; }
 // record kernels (strided and plan tile lists) that code the guard band
-// (HBEC_ODD_EDGE_FUSE): apply, register tables or bit-plane (the LDS-table kernels, K >= 9, spilled
+// (HBEC_ODD_EDGE_FUSE bit 2; off: 8+3 / 10+4 records lost 3-4.5 points
+// with it, the 8+3 / 4+2 plans 3, r06_ab_fuse.jsonl): apply, register tables or bit-plane (the LDS-table kernels, K >= 9, spilled
 // 15-211 VGPRs with it and keep the gf_odd_edges launch)
-// (4 x 4 tables over a plan's tile list spilled a pending tile-list entry
-// register with it: isa_check.py refused the library; that instance keeps
-// the gf_odd_edges_plan launch)
+// (Three tile-list instances spilled a pending scalar-load register into a
+// VGPR lane with it — 4 x 4 tables, bit-plane 6+4 and 12+2 — and
+// isa_check.py refused the library: they keep the gf_odd_edges_plan launch.)
 __host__ __device__ constexpr bool odd_rec_edge(int k, int r, int mode, int xs, bool list) {
-    return HBEC_ODD_EDGE_FUSE != 0 && mode == kOddApply && (xs >= 0 || !odd_rec_lds(k)) &&
-           !(list && xs < 0 && k == 4 && r == 4);
+    return (HBEC_ODD_EDGE_FUSE & 2) != 0 && mode == kOddApply && (xs >= 0 || !odd_rec_lds(k)) &&
+           !(list && ((xs < 0 && k == 4 && r == 4) || (xs >= 0 && ((k == 6 && r == 4) || (k == 12 && r == 2)))));
 }
 // record kernels run 2 waves per SIMD with LDS tables; the register-table
 // ones at 1 (8+3 encode at 2 waves per SIMD, 256 VGPRs with 40 B of spill:
@@ -1127,19 +1168,23 @@ __device__ __forceinline__ void odd_rec_finish(const OddRegs<K, R, U, MODE>& X, 
 }
 
 // the fused guard band of an edge tile (gf_odd_rec EDGE)
-template <int K, int R, int U, int MODE, int XS, class TB>
-__device__ __forceinline__ void odd_rec_edges(const OddRegs<K, R, U, MODE>& X, const OddRT<K, R, MODE>& t,
+template <int K, int R, int MODE, int XS, class TB>
+__device__ __forceinline__ void odd_rec_edges(const uint32_t (&e)[K], const OddRT<K, R, MODE>& t,
                                               const TabArray& tab, const TB& tb, uint32_t lane, uint32_t lt) {
     {
         if (t.edge != 0u) {  // wave-uniform: the tile starts or ends its shard
             const uint32_t fl = odd_eflags(t.edge), S = odd_elen(t.edge);
-            uint32_t acc[R];
-            if constexpr (XS >= 0 || odd_rec_lds(K)) {
-                gf_dot_lds1<K, R>(acc, X.e, lt);
-            } else {
-                gf_dot1<K, R, kOddVMin>(acc, X.e, tab, tb);
-            }
             const uint32_t w1 = odd_w(t.f, 1), c = w1 >> 16;  // frame start C (record word 1, bits 16..)
+            // input j's byte at position p: its base mod 4 is (t0 - C) mod 4, t0 mod 4 the packed shift
+            const uint32_t shp = odd_w(t.f, 0), p = odd_edge_off(fl, S, lane);
+            uint32_t acc[R], x[K];
+#pragma unroll
+            for (int j = 0; j < K; ++j) x[j] = odd_edge_byte(e[j], (shp >> (2 * j)) - c + p);
+            if constexpr (XS >= 0 || odd_rec_lds(K)) {
+                gf_dot_lds1<K, R>(acc, x, lt);
+            } else {
+                gf_dot1<K, R, kOddVMin>(acc, x, tab, tb);
+            }
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const uint32_t d = (w1 >> (4 * r)) & 15u;
@@ -1300,10 +1345,16 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE, XS>())) 
     // EDGE: the shard base of loaded shard j is B_j + lim_j + 16 - (S & ~3)
     // (record: B = base + C rounded down to a dword, lim = S - 16 - (C +
     // (base & 3) rounded down) with base & 3 in its low 2 bits)
-    auto edge_load = [&](OddRegs<K, R, U, MODE>& Z, const OddRT<K, R, MODE>& tz) {
+    // Fused guard band: a tile's K edge words are loaded right before its
+    // columns and coded at the end of the same step (its finish record has
+    // arrived by then), after the previous tile's finish: they never cross
+    // the loop's back edge (a loop-carried copy waited for the next tile's
+    // loads: 8+3 60 -> 43 %)
+    auto edge_load = [&](uint32_t (&e)[K], const OddRT<K, R, MODE>& tz) {
         if constexpr (EDGE) {
             const uint32_t fl = odd_eflags(tz.edge), S = odd_elen(tz.edge), s4 = S & ~3u;
             const uint32_t eo = odd_edge_off(fl, S, lane);
+            if (HBEC_ODD_EDGE_COND != 0 && fl == 0u) return;  // edge tiles only (as odd_body)
 #pragma unroll
             for (int j = 0; j < K; ++j) {
                 // other tiles: the byte at the tile's first column of shard j
@@ -1313,7 +1364,7 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE, XS>())) 
                 const uint32_t lim = odd_w(L, 3 * j + 2);
                 const uint64_t off = fl != 0u ? (uint64_t)(int64_t)(int32_t)(lim + 16u - s4 + eo)
                                                    : (uint64_t)(tz.v0 < lim ? tz.v0 : lim);
-                Z.e[j] = ld_u8(bj + off);
+                e[j] = ld_dw(bj + off);
             }
         }
     };
@@ -1321,8 +1372,12 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE, XS>())) 
     odd_swait();
     odd_swait_pin(L);
     fill(tx, p);
+    // the edge words are carried through the loop unchanged by non-edge
+    // tiles (an undefined value on that path was materialised as zeros,
+    // each write waiting for the loads in flight: vmcnt(0) per tile)
+    uint32_t ex[K] = {};
+    edge_load(ex, tx);
     odd_rec_load<K, R, U, MODE, CARRY || VCHAIN, IMAJ, TEMP>(X, L, tx.v0, lane);
-    edge_load(X, tx);
     odd_rec_sload<PF>(tx.f, rec(p));
     p = step(p);
     odd_rec_sload<PF>(L, rec(p) + RC::FW);
@@ -1331,11 +1386,13 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE, XS>())) 
     odd_swait_pin(L);
     odd_swait_pin(tx.f);
     if constexpr (LIST) odd_swait_pin2(pe);
+    if constexpr (EDGE) odd_rec_edges<K, R, MODE, XS>(ex, tx, a.tab, tb, lane, lt);
     auto half = [&](OddRegs<K, R, U, MODE>& Z, OddRT<K, R, MODE>& tz, const OddRegs<K, R, U, MODE>& W,
                     const OddRT<K, R, MODE>& tw) {
         fill(tz, p);
+        uint32_t (&ez)[K] = ex;
+        edge_load(ez, tz);
         odd_rec_load<K, R, U, MODE, CARRY || VCHAIN, IMAJ, TEMP>(Z, L, tz.v0, lane);
-        edge_load(Z, tz);
         odd_rec_sload<PF>(tz.f, rec(p));
         p = step(p);
         odd_rec_sload<PF>(L, rec(p) + RC::FW);
@@ -1346,25 +1403,19 @@ __global__ __launch_bounds__(kPipeBlockThreads, (odd_rec_lb<K, R, MODE, XS>())) 
         // reads 1.054 -> 1.026 x); at one wave per SIMD it costs 10 points
         if constexpr (MODE != kOddVerify || (VCHAIN && HBEC_ODD_BP_VBARRIER && odd_bp_bpc(K, R, MODE) >= 2))
             __builtin_amdgcn_s_barrier();
-        // the guard band before the tile's columns with register tables, after
-        // them with LDS tables (fewer registers in each case: table 8+3 18 vs
-        // 39 AGPRs, bit-plane 8+3 205 vs 256 + 30 VGPRs)
-        if constexpr (EDGE && XS < 0) odd_rec_edges<K, R, U, MODE, XS>(W, tw, a.tab, tb, lane, lt);
         odd_rec_finish<K, R, U, MODE, CARRY, XS>(W, tw, a.tab, tb, lane, flags, lt);
-        if constexpr (EDGE && XS >= 0) odd_rec_edges<K, R, U, MODE, XS>(W, tw, a.tab, tb, lane, lt);
         odd_swait();
         odd_swait_pin(L);
         odd_swait_pin(tz.f);
         if constexpr (LIST) odd_swait_pin2(pe);
+        if constexpr (EDGE) odd_rec_edges<K, R, MODE, XS>(ez, tz, a.tab, tb, lane, lt);
     };
     for (uint32_t b0 = wave0 + nw; b0 < n; b0 += nw) {  // block-uniform trip count
         half(Y, ty, X, tx);
         X = Y;
         tx = ty;
     }
-    if constexpr (EDGE && XS < 0) odd_rec_edges<K, R, U, MODE, XS>(X, tx, a.tab, tb, lane, lt);
     odd_rec_finish<K, R, U, MODE, CARRY, XS>(X, tx, a.tab, tb, lane, flags, lt);
-    if constexpr (EDGE && XS >= 0) odd_rec_edges<K, R, U, MODE, XS>(X, tx, a.tab, tb, lane, lt);
 }
 
 template <int K, int R, int MODE, bool MIR = false, bool CARRY = false>

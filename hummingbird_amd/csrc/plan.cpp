@@ -167,7 +167,7 @@ int odd_stripe_rec_pass(int K, int R, int mode, const hbec::UPlanArgs& a, const 
     c.list = tl->d;
     // the record kernel codes the guard band of the stripes it covers (the
     // tile list's edge flags) when this pass's inputs are all of them
-    *fused = one_pass && o.s_max < (1ull << 30) && hbec::odd_edge_fuse(K, R, mode, true, xs, true);
+    *fused = one_pass && o.s_max < (1ull << 30) && hbec::odd_edge_fuse(K, R, mode, true, xs, true, o.s_max);
     c.fuse = *fused ? 1u : 0u;
     const uint64_t wpb = hbec::odd_waves_per_block(xs);
     const uint64_t want = (c.n_tiles + wpb - 1) / wpb;

@@ -175,10 +175,25 @@
 #endif
 
 #ifndef HBEC_ODD_EDGE_FUSE
-// strided apply passes code each shard's guard-band bytes (head [0, 64),
-// tail [S - 64, S)) inside the main kernel, in the shard's first / last
-// tile, instead of the second gf_odd_edges launch (round 6)
+// apply passes that code each shard's guard-band bytes (head [0, 64), tail
+// [S - 64, S)) inside the main kernel, in the shard's first / last tile,
+// instead of the second gf_odd_edges launch (round 6); bit 1: gf_odd
+// (K <= 4, R <= 3), bit 2: the record kernels (compiled but slower:
+// odd_impl.h odd_rec_edge)
 #define HBEC_ODD_EDGE_FUSE 1
+#endif
+#ifndef HBEC_ODD_EDGE_MAX_S
+// ... for shards of at most this many bytes.  No limit: 4+2 S = 4095 47.0 ->
+// 57.2-58.5 %, 6143 54.6 -> 61.2, 12287 60.7 -> 62.5, 16383 / 24575 +1.3 to
+// +1.9 (one box) and -1.6 (another), 1 MiB +-0.5; 2+1 / 3+2 at S = 4095
+// +10 / +13 points (r06_ab_fuse.jsonl)
+#define HBEC_ODD_EDGE_MAX_S 0xFFFFFFFFull
+#endif
+#ifndef HBEC_ODD_EDGE_COND
+// fused guard band: 1 = only a shard's first / last tile issues the K
+// edge-word loads; 0 = every tile (the others from their own first column),
+// so the loads in flight do not depend on the path
+#define HBEC_ODD_EDGE_COND 0
 #endif
 
 // ---- ShardHash (md5.hip) ----

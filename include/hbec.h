@@ -357,6 +357,13 @@ int hbec_kernel_info(int k, int r, uint64_t shard_len, int* tile_bytes, int* kin
  * may be NULL. */
 int hbec_odd_path_stats(uint64_t* bitplane, uint64_t* records, uint64_t* strided);
 
+/* Odd-shard guard bands (the <= 64 head and tail bytes of each shard the main
+ * kernels' 16-B frame does not store): launches since load of the separate
+ * guard-band kernels (gf_odd_edges / gf_odd_edges_plan), and main-kernel
+ * launches that coded their guard bands themselves (the fused route, round 6).
+ * Either pointer may be NULL. */
+int hbec_odd_edge_stats(uint64_t* edge_launches, uint64_t* fused_launches);
+
 /* ---------------------------------------------------------------------------
  * ecutils.go stripe loops over io callbacks (objectserver/ecutils.go:14-186,
  * objectserver/ecobj.go:82-98, :814-824).

@@ -19,6 +19,9 @@ def test_odd_pmc_summary_is_fresh():
     assert data is not None, why
     assert data.get("odd_sources_sha256") == bench.kernel_sources_sha256(bench.ODD_SOURCES), (
         f"{path} was collected on other odd-kernel sources: rerun scripts/final.sh first")
-    # the odd legs read these kernels' bytes from it
-    for name in ("gf_odd_edges<0, false, 128>", "gf_odd_edges<2, false, 128>", "gf_odd_edges_plan<0, false, 128>"):
+    # the odd legs read these kernels' bytes from it (apply passes code their
+    # guard bands inside the main kernel since round 6; Verify keeps the
+    # separate guard-band launch)
+    for name in ("gf_odd_edges<2, false, 128>", "gf_odd_planrec"):
         assert name in data["kernels"], name
+    assert any(x.startswith("gf_odd_rec<") for x in data["kernels"])
