@@ -22,7 +22,8 @@ pytestmark = pytest.mark.gpu
 
 
 def _odd_launches():
-    return sum(B.odd_path_stats().values())
+    p = B.odd_path_stats()
+    return p["bitplane"] + p["records"] + p["strided"]
 
 
 def _routed(k, m, s, base):
@@ -130,3 +131,48 @@ def test_verify_wide_route_9_12_more_than_4_rows(k, m, s):
     B.verify_views(enc, views, n, s, flags)
     torch.cuda.synchronize()
     assert flags.nonzero().flatten().tolist() == sorted(hits)
+
+
+# Round 6: gf_odd (k <= 4, <= 3 outputs) codes each shard's guard band (the
+# <= 64 head and tail bytes outside its 16-B frame) in the shard's first and
+# last tile (tuning.h HBEC_ODD_EDGE_FUSE); shards of one frame tile, the
+# record kernels and Verify keep the gf_odd_edges launch.
+@pytest.mark.parametrize("k,m,s,fused", [(4, 2, 4095, True), (3, 2, 8191, True), (2, 1, 100003, True),
+                                         (1, 3, 6001, True), (4, 3, 2301, True), (4, 2, 2047, False),
+                                         (8, 3, 8191, False), (10, 4, 8193, False)])
+def test_guard_band_fused_route_and_parity(k, m, s, fused):
+    n = 37
+    pitch = (k + m) * s + 3
+    buf = torch.empty(5 + n * pitch + 64, dtype=torch.uint8, device="cuda")
+    B.fill_splitmix(buf.view(1, -1), buf.numel(), first=s)
+    ref = buf.clone()
+    views = [(buf.data_ptr() + 5 + i * s, pitch) for i in range(k + m)]
+    enc = RS.New(k, m)
+    p0 = B.odd_path_stats()
+    B.encode_views(enc, views, n, s)
+    torch.cuda.synchronize()
+    p1 = B.odd_path_stats()
+    assert (p1["fused"] > p0["fused"], p1["edges"] > p0["edges"]) == (fused, not fused)
+    got = buf.cpu().numpy()
+    rows = CO.build_matrix(k, m)[k:]
+    for o in range(n):
+        b = 5 + o * pitch
+        want = CO.apply(rows, [got[b + j * s:b + (j + 1) * s] for j in range(k)])
+        for r in range(m):
+            assert np.array_equal(got[b + (k + r) * s:b + (k + r + 1) * s], want[r]), (o, r)
+    # nothing outside the shards changed (the guard-band stores are byte-exact)
+    refh = ref.cpu().numpy()
+    gaps = [(0, 5)] + [(5 + o * pitch + (k + m) * s, 5 + (o + 1) * pitch) for o in range(n)]
+    gaps.append((5 + n * pitch, refh.size))
+    for a, e in gaps:
+        assert np.array_equal(got[a:e], refh[a:e])
+    # two shards lost and rebuilt (gf_odd with 2 outputs when k <= 4)
+    keep = buf.clone()
+    lost = [0, k] if k > 1 else [0, 1]
+    for o in range(n):
+        for i in lost:
+            a = 5 + o * pitch + i * s
+            buf[a:a + s] = 0xA5
+    B.reconstruct_views(enc, views, [0 if i in lost else 1 for i in range(k + m)], n, s)
+    torch.cuda.synchronize()
+    assert torch.equal(buf, keep)
