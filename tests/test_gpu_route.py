@@ -166,9 +166,9 @@ def test_guard_band_fused_route_and_parity(k, m, s, fused):
     gaps.append((5 + n * pitch, refh.size))
     for a, e in gaps:
         assert np.array_equal(got[a:e], refh[a:e])
-    # two shards lost and rebuilt (gf_odd with 2 outputs when k <= 4)
+    # min(2, m) shards lost and rebuilt (gf_odd again for k <= 4)
     keep = buf.clone()
-    lost = [0, k] if k > 1 else [0, 1]
+    lost = ([0, k] if k > 1 else [0, 1])[:m]
     for o in range(n):
         for i in lost:
             a = 5 + o * pitch + i * s
