@@ -15,9 +15,12 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 ROOT = Path(__file__).resolve().parents[1]
-DEADLINE_S = 90
+# the child computes the oracle for 16 threads on the box's CPU share: 20-40 s
+# on most boxes, 90+ on one slow box in round 6 (its whole suite ran 3x slower)
+DEADLINE_S = 150
 
 
+@pytest.mark.timeout(170)
 def test_more_callers_than_rings_finish_and_match_oracle():
     env = dict(os.environ, HBEC_HOST_RINGS="2")
     p = subprocess.run([sys.executable, str(ROOT / "tests" / "ring_stress.py"), "16", "6"], env=env,
