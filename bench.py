@@ -146,6 +146,30 @@ def load_pmc(prefix_glob="profiles/r[0-9][0-9]_pmc.json"):
     return data, rel, None
 
 
+# PMC attribution: before each leg that quotes PMC traffic, one fill_splitmix
+# launch of exactly PMC_MARK_BLOCKS + i blocks (i = the leg's index in
+# PMC_LEGS) marks where that leg's dispatches begin, so scripts/pmc_summary.py
+# can give each leg the bytes of its own launches (two legs launching the same
+# kernel, e.g. the random-size and mid-size plans, are no longer averaged)
+PMC_LEGS = ("odd_objects", "random_objects", "mid_objects")
+PMC_MARK_BLOCKS = 9001
+_mark_buf = []
+
+
+def pmc_mark(leg):
+    i = PMC_LEGS.index(leg)
+    if not _mark_buf:
+        _mark_buf.append(torch.empty((1, (PMC_MARK_BLOCKS + len(PMC_LEGS)) * 2048), dtype=torch.uint8, device="cuda"))
+    nb = (PMC_MARK_BLOCKS + i) * 2048  # 256 threads x 8 B per block
+    B.fill_splitmix(_mark_buf[0][:, :nb], nb)
+
+
+def pmc_kernels(pmc, leg):
+    """The per-kernel PMC bytes of one leg's own launches (pmc_summary.py
+    `legs`); {} when the summary predates the markers."""
+    return (pmc or {}).get("legs", {}).get(leg, {})
+
+
 class Workload:
     """4+2 batch resident in HBM: objs [n, 1 MiB], parity [n, 512 KiB],
     rebuilt [n, 512 KiB] (reconstruct target for the erased shards 0,1)."""
@@ -465,7 +489,7 @@ def _odd_kernel_traffic(kern, k, r, mode, paths, plan=False):
     return pick[0], kern[pick[0]].get("hbm_bytes_per_launch")
 
 
-def odd_leg(k, m, n, obj_len, first, reps=20, settle=40, pmc=None):
+def odd_leg(k, m, n, obj_len, first, reps=20, settle=40, kern=None):
     """One odd-shard shape: n ecSplit databufs of obj_len-byte objects,
     device-resident: Encode, Reconstruct of shards {0,1} in place, Verify.
     Rebuilt shards must equal the originals and Verify must pass every object."""
@@ -502,8 +526,7 @@ def odd_leg(k, m, n, obj_len, first, reps=20, settle=40, pmc=None):
         gbs = nbytes[name] / (ms * 1e-3) / 1e9
         out[name] = {"ms": round(ms, 4), "GB_s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
                      "edges": "fused" if routes[name]["fused"] > 0 else "separate launch"}
-    if pmc is not None:
-        kern = pmc.get("kernels", {})
+    if kern:
         for name, (r, mode) in (("encode", (m, 0)), ("reconstruct", (2, 0)), ("verify", (m, 2))):
             kname, t = _odd_kernel_traffic(kern, k, r, mode, routes[name])
             # the edge kernel when the guard bands took their own launch (a
@@ -542,9 +565,11 @@ def odd_objects(n=4096):
     pmc_files = sorted(glob.glob(str(ROOT / "profiles/r[0-9][0-9]_pmc.json")))
     pmc = json.loads(Path(pmc_files[-1]).read_text()) if pmc_files else {}
     fresh = pmc.get("odd_sources_sha256") == kernel_sources_sha256(ODD_SOURCES)
-    out = odd_leg(4, 2, n, (1 << 20) - 4, 1 << 21, pmc=pmc if fresh else None)
-    out["shapes"] = {"8+3": odd_leg(8, 3, n, (1 << 20) - 8, 1 << 22, pmc=pmc if fresh else None),
-                     "10+4": odd_leg(10, 4, n, 1 << 20, 1 << 23, pmc=pmc if fresh else None)}
+    kern = pmc_kernels(pmc, "odd_objects") if fresh else None
+    pmc_mark("odd_objects")
+    out = odd_leg(4, 2, n, (1 << 20) - 4, 1 << 21, kern=kern)
+    out["shapes"] = {"8+3": odd_leg(8, 3, n, (1 << 20) - 8, 1 << 22, kern=kern),
+                     "10+4": odd_leg(10, 4, n, 1 << 20, 1 << 23, kern=kern)}
     out["traffic_source"] = os.path.relpath(pmc_files[-1], ROOT) if (pmc_files and fresh) else None
     if not fresh:
         out["traffic_note"] = "no PMC summary collected on this tree's odd-kernel sources"
@@ -570,6 +595,8 @@ def random_objects(n=4096, shapes=((4, 2), (8, 3)), reps=20, settle=40):
     stream = torch.cuda.current_stream()
     out = {"workload": f"{n} objects, shard length uniform in [4 KiB/k, 1 MiB/k] and odd (seeded), one object "
                        "plan per shape, Encode, device-resident", "shapes": {}}
+    kern = pmc_kernels(pmc, "random_objects") if fresh else {}
+    pmc_mark("random_objects")
     for k, m in shapes:
         rng = __import__("numpy").random.default_rng(0x48424543 + 100 * k + m)
         sizes = [int(x) | 1 for x in rng.integers(4096 // k, (1 << 20) // k + 1, n)]
@@ -605,8 +632,8 @@ def random_objects(n=4096, shapes=((4, 2), (8, 3)), reps=20, settle=40):
         leg = {"objects": n, "bytes": nbytes, "ms": round(ms, 4), "GB_s": round(gbs, 1),
                "frac": round(gbs / HBM_PEAK_GBS, 4), "parity_ok": bad == 0}
         leg["edges"] = "fused" if paths["fused"] > 0 else "separate launch"
-        if fresh:
-            kname, t = _plan_traffic(pmc.get("kernels", {}), k, m, paths)
+        if kern:
+            kname, t = _plan_traffic(kern, k, m, paths)
             if t is not None:
                 leg["kernel"] = kname
                 leg["traffic"] = int(t)
@@ -653,7 +680,8 @@ def mid_objects(n=16384, shapes=((4, 2), (8, 3)), reps=20, settle=40):
     pmc_files = sorted(glob.glob(str(ROOT / "profiles/r[0-9][0-9]_pmc.json")))
     pmc = json.loads(Path(pmc_files[-1]).read_text()) if pmc_files else {}
     fresh = pmc.get("odd_sources_sha256") == kernel_sources_sha256(ODD_SOURCES)
-    kern = pmc.get("kernels", {}) if fresh else {}
+    kern = pmc_kernels(pmc, "mid_objects") if fresh else {}
+    pmc_mark("mid_objects")
     stream = torch.cuda.current_stream()
 
     def timed(fn):

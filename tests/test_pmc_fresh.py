@@ -25,3 +25,6 @@ def test_odd_pmc_summary_is_fresh():
     for name in ("gf_odd_edges<2, false, 128>", "gf_odd_planrec"):
         assert name in data["kernels"], name
     assert any(x.startswith("gf_odd_rec<") for x in data["kernels"])
+    # each odd leg's bytes come from its own launches (bench.py leg markers)
+    for leg in bench.PMC_LEGS:
+        assert any(x.startswith("gf_odd") for x in data.get("legs", {}).get(leg, {})), leg
