@@ -111,7 +111,9 @@ struct OddTileList {
     uint64_t n = 0;
 };
 constexpr int kOddSpans = 2;  // the record kernels' tile spans: 992 (5 <= K <= 12 tables), 2016 (carried 2 windows)
+struct OddRecCache;  // a plan's built pass records (plan.cpp)
 struct OddStripeRecs {
+    OddRecCache* cache = nullptr;  // owned by the plan
     const URec* recs = nullptr;
     uint64_t n = 0, s_max = 0;
     OddTileList lists[kOddSpans];

@@ -50,6 +50,31 @@ struct hbec_plan {
     hbec::URec* d_orecs = nullptr;
     uint32_t* d_lists[hbec::kOddSpans] = {};
     hbec::OddStripeRecs orecs;
+    std::unique_ptr<hbec::OddRecCache> rec_cache;
+};
+
+// The gf_odd_rec records of a plan pass depend only on the plan's stripes and
+// on which shards the pass reads and writes, not on its coefficients: a
+// plan keeps those it built (the encode pass, recurring erasure patterns)
+// instead of rebuilding them on every call (gf_odd_planrec: 13-15 us of a
+// 16384-stripe 8+3 plan's 250 us, r6_trace_mid).  Built on the first
+// caller's stream; a caller on another stream waits for that build's event.
+struct hbec::OddRecCache {
+    static constexpr size_t kMaxEntries = 16;
+    struct Entry {
+        std::vector<uint32_t> key;
+        uint32_t* d = nullptr;
+        hipEvent_t ev = nullptr;
+        hipStream_t stream = nullptr;
+    };
+    std::mutex mu;
+    std::vector<Entry> entries;
+    ~OddRecCache() {
+        for (auto& x : entries) {
+            if (x.ev) (void)hipEventDestroy(x.ev);
+            if (x.d) (void)hipFree(x.d);
+        }
+    }
 };
 
 namespace {
@@ -117,6 +142,8 @@ int build_tile_lists(hbec_plan* p, const std::vector<hbec::URec>& orecs) {
         if (e != hipSuccess) return hip_fail(e, "hipMemcpy plan tile list");
         p->orecs.lists[i] = hbec::OddTileList{spans[i], p->d_lists[i], l.size() / hbec::kOddListWords};
     }
+    p->rec_cache = std::make_unique<hbec::OddRecCache>();
+    p->orecs.cache = p->rec_cache.get();
     p->orecs.recs = p->d_orecs;
     p->orecs.n = orecs.size();
     p->orecs.s_max = s_max;
@@ -150,12 +177,51 @@ int odd_stripe_rec_pass(int K, int R, int mode, const hbec::UPlanArgs& a, const 
         if (l.span == span) tl = &l;
     if (!tl || !tl->d) return fail(HBEC_ERR_INVALID_ARG, "plan has no tile list for this pass");
     uint32_t* recs = nullptr;
-    int rc = hbec::scratch_alloc(o.n * rw * 4, stream, reinterpret_cast<void**>(&recs));
-    if (rc) return rc;
-    hipError_t e = hbec::launch_odd_planrec(K, R, mode, a, o.recs, (uint32_t)o.n, recs, stream);
-    if (e != hipSuccess) {
-        hbec::scratch_free(recs, stream);
-        return hip_fail(e, "launch gf_odd_planrec");
+    bool cached = false;
+    hipError_t e = hipSuccess;
+    if (o.cache) {
+        std::vector<uint32_t> key{(uint32_t)K, (uint32_t)R, (uint32_t)mode, a.in_sel, a.out_sel};
+        key.insert(key.end(), a.in_idx, a.in_idx + K);
+        key.insert(key.end(), a.out_idx, a.out_idx + R);
+        std::lock_guard<std::mutex> lk(o.cache->mu);
+        for (const auto& x : o.cache->entries) {
+            if (x.key != key) continue;
+            if (x.stream != stream) {
+                e = hipStreamWaitEvent(stream, x.ev, 0);
+                if (e != hipSuccess) return hip_fail(e, "hipStreamWaitEvent (plan records)");
+            }
+            recs = x.d;
+            cached = true;
+        }
+        if (!cached && o.cache->entries.size() < hbec::OddRecCache::kMaxEntries) {
+            hbec::OddRecCache::Entry x;
+            x.key = std::move(key);
+            x.stream = stream;
+            if (hipMalloc(reinterpret_cast<void**>(&x.d), o.n * rw * 4) == hipSuccess) {
+                e = hbec::launch_odd_planrec(K, R, mode, a, o.recs, (uint32_t)o.n, x.d, stream);
+                if (e == hipSuccess) e = hipEventCreateWithFlags(&x.ev, hipEventDisableTiming);
+                if (e == hipSuccess) e = hipEventRecord(x.ev, stream);
+                if (e != hipSuccess) {
+                    if (x.ev) (void)hipEventDestroy(x.ev);
+                    (void)hipFree(x.d);
+                    return hip_fail(e, "launch gf_odd_planrec (plan records)");
+                }
+                recs = x.d;
+                cached = true;
+                o.cache->entries.push_back(std::move(x));
+            } else {
+                (void)hipGetLastError();  // HBM full: per-call scratch records below
+            }
+        }
+    }
+    if (!cached) {
+        int rc = hbec::scratch_alloc(o.n * rw * 4, stream, reinterpret_cast<void**>(&recs));
+        if (rc) return rc;
+        e = hbec::launch_odd_planrec(K, R, mode, a, o.recs, (uint32_t)o.n, recs, stream);
+        if (e != hipSuccess) {
+            hbec::scratch_free(recs, stream);
+            return hip_fail(e, "launch gf_odd_planrec");
+        }
     }
     hbec::PassArgs c;
     std::memset(&c, 0, sizeof(c));
@@ -175,7 +241,7 @@ int odd_stripe_rec_pass(int K, int R, int mode, const hbec::UPlanArgs& a, const 
     if (max_blocks > 0) cap = std::min<uint64_t>(cap, (uint64_t)max_blocks);
     const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, cap));
     e = hbec::launch_odd(K, R, mode, c, nullptr, recs, grid, stream, xs);
-    hbec::scratch_free(recs, stream);
+    if (!cached) hbec::scratch_free(recs, stream);
     if (e != hipSuccess) return hip_fail(e, "launch gf_odd_rec (plan)");
     return HBEC_OK;
 }
