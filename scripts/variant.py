@@ -5,6 +5,7 @@ are copied from the product build).
 
     python scripts/variant.py NAME DEF[=VAL] ... [--units odd_bp.hip,odd.hip]
 """
+import json
 import shutil
 import sys
 from pathlib import Path
@@ -30,4 +31,7 @@ for u in (hb.SOURCES if units == ["all"] else units):
 lib = ROOT / "tune_build" / name / "libhbec.so"
 lib.unlink(missing_ok=True)
 hb.build(verbose=False, defs=defs, lib=lib, objdir=od)
+# what this variant is: its -D definitions and the units rebuilt with them
+rebuilt = list(hb.SOURCES) if units == ["all"] else units
+(lib.parent / "variant.json").write_text(json.dumps({"defs": defs, "units_rebuilt": [str(u) for u in rebuilt]}, indent=1) + "\n")
 print(lib)
