@@ -110,6 +110,7 @@ _SIG = [
      [C.c_int, C.c_int, C.c_uint64, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     ("hbec_odd_path_stats", C.c_int, [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     ("hbec_odd_edge_stats", C.c_int, [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    ("hbec_odd_record_cache", C.c_int, [C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     ("hbec_ec_shard_length", C.c_int64, [C.c_int64, C.c_int64]),
     ("hbec_ec_split", C.c_int, [C.c_int, C.c_int, READ_FN, _P, C.c_int, C.c_int64, WRITE_FN, C.POINTER(_P)]),
     ("hbec_ec_reconstruct", C.c_int,

@@ -159,6 +159,14 @@ def odd_path_stats():
     return {"bitplane": b.value, "records": r.value, "strided": s.value, "edges": e.value, "fused": f.value}
 
 
+def odd_record_cache(clear: bool = False):
+    """(cached view sets, calls that reused one) of the strided record
+    passes' record cache; clear=True drops it (test hook, device synchronised)."""
+    e, h = C.c_uint64(), C.c_uint64()
+    check(N.lib().hbec_odd_record_cache(1 if clear else 0, C.byref(e), C.byref(h)))
+    return e.value, h.value
+
+
 def set_odd_chunk_tiles(tiles: int) -> None:
     """Test hook: odd-shard strided launches of at most `tiles` tiles (0 = default)."""
     N.lib().hbec_set_odd_chunk_tiles(int(tiles))

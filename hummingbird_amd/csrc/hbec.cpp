@@ -160,6 +160,93 @@ static int cu_count(int dev, int* cus) {
     return HBEC_OK;
 }
 
+// Per-object records of a strided record pass depend only on the views (bases
+// and strides), the object count, S and the pass shape, never on the data or
+// the coefficients.  Views coded again (a service reusing its batch buffers,
+// bench loops) get the records built the first time instead of a
+// gf_odd_objrec launch per call (10 us of a 16 384-object 8+3 call).  A key
+// is cached on its second sighting, so one-off views (per-call entries) never
+// allocate; at most kObjRecMax entries / kObjRecMaxBytes, never evicted (a
+// full cache codes new views with per-call scratch records).  Built on the
+// first caller's stream; another stream waits for the build's event.
+namespace {
+struct ObjRecCache {
+    struct Entry {
+        std::vector<uint64_t> key;
+        uint32_t* d = nullptr;
+        hipEvent_t ev = nullptr;
+        hipStream_t stream = nullptr;
+    };
+    std::mutex mu;
+    std::vector<Entry> entries;
+    std::deque<std::vector<uint64_t>> seen;  // keys seen once
+    uint64_t bytes = 0, hits = 0;
+};
+constexpr size_t kObjRecMax = 16, kObjRecSeen = 64;
+constexpr uint64_t kObjRecMaxBytes = 64ull << 20;
+ObjRecCache& objrec_cache() {
+    static ObjRecCache* c = new ObjRecCache;  // process lifetime (no teardown against the HIP runtime)
+    return *c;
+}
+}  // namespace
+
+// *out = the cached records of this launch's views, or nullptr (build them)
+static int objrec_cached(const PassArgs& c, int K, int R, int m, int dev, uint64_t rw, hipStream_t stream,
+                         uint32_t** out) {
+    *out = nullptr;
+    static const bool on = tune_knob("HBEC_ODD_REC_CACHE", 1) != 0;  // tuning builds: 0 = rebuild every call
+    if (!on) return HBEC_OK;
+    std::vector<uint64_t> key{(uint64_t)dev, (uint64_t)K, (uint64_t)R, (uint64_t)m, c.n_obj, c.shard_len};
+    for (int j = 0; j < K; ++j) {
+        key.push_back(reinterpret_cast<uintptr_t>(c.in[j]));
+        key.push_back(c.in_stride[j]);
+    }
+    for (int r = 0; r < R; ++r) {
+        key.push_back(reinterpret_cast<uintptr_t>(c.out[r]));
+        key.push_back(c.out_stride[r]);
+    }
+    ObjRecCache& C = objrec_cache();
+    std::lock_guard<std::mutex> lk(C.mu);
+    for (const auto& x : C.entries) {
+        if (x.key != key) continue;
+        if (x.stream != stream) {
+            hipError_t e = hipStreamWaitEvent(stream, x.ev, 0);
+            if (e != hipSuccess) return hip_fail(e, "hipStreamWaitEvent (object records)");
+        }
+        *out = x.d;
+        ++C.hits;
+        return HBEC_OK;
+    }
+    const auto it = std::find(C.seen.begin(), C.seen.end(), key);
+    if (it == C.seen.end()) {
+        C.seen.push_back(std::move(key));
+        if (C.seen.size() > kObjRecSeen) C.seen.pop_front();
+        return HBEC_OK;
+    }
+    C.seen.erase(it);
+    const uint64_t bytes = c.n_obj * rw * 4;
+    if (C.entries.size() >= kObjRecMax || C.bytes + bytes > kObjRecMaxBytes) return HBEC_OK;
+    ObjRecCache::Entry x;
+    x.key = std::move(key);
+    x.stream = stream;
+    if (hipMalloc(reinterpret_cast<void**>(&x.d), bytes) != hipSuccess) {
+        (void)hipGetLastError();  // HBM full: scratch records
+        return HBEC_OK;
+    }
+    hipError_t e = launch_odd_objrec(K, R, m, c, x.d, stream);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&x.ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(x.ev, stream);
+    if (e != hipSuccess) {
+        if (x.ev) (void)hipEventDestroy(x.ev);
+        (void)hipFree(x.d);
+        return hip_fail(e, "launch gf_odd_objrec (cached)");
+    }
+    C.bytes += bytes;
+    *out = x.d;
+    C.entries.push_back(std::move(x));
+    return HBEC_OK;
+}
+
 // One pass of a (K <= kMaxK inputs, R <= kMaxR outputs) over strided views at
 // any alignment, as launches of <= kOddMaxK inputs: the first accumulates
 // only when `accumulate`, the later ones always.  mode 2 (verify) flags
@@ -196,12 +283,8 @@ static int odd_launches(const PassArgs& a, int K, int R, int mode, bool accumula
             // per-object records of one launch's objects (stream-ordered
             // scratch of at most max_obj records, rebuilt per launch, freed
             // after the pass): device memory bounded by the chunk, not the batch
-            uint32_t* recs = nullptr;
+            uint32_t* recs = nullptr;  // scratch, allocated when a launch's records are not cached
             const uint64_t rw = odd_rec_words(K1, R, m);
-            if (use_rec) {
-                rc = scratch_alloc(std::min(n_obj, max_obj) * rw * 4, stream, reinterpret_cast<void**>(&recs));
-                if (rc) return rc;
-            }
             for (uint64_t o0 = 0; o0 < n_obj; o0 += max_obj) {
                 const uint64_t no = std::min(max_obj, n_obj - o0);
                 PassArgs c = b;
@@ -209,11 +292,24 @@ static int odd_launches(const PassArgs& a, int K, int R, int mode, bool accumula
                 for (int r = 0; r < R; ++r) c.out[r] = b.out[r] + o0 * b.out_stride[r];
                 c.n_obj = no;
                 c.shard_len = shard_len;
+                uint32_t* lrecs = nullptr;
                 if (use_rec) {
-                    hipError_t e = launch_odd_objrec(K1, R, m, c, recs, stream);
-                    if (e != hipSuccess) {
-                        scratch_free(recs, stream);
-                        return hip_fail(e, "launch gf_odd_objrec");
+                    rc = objrec_cached(c, K1, R, m, dev, rw, stream, &lrecs);
+                    if (rc) {
+                        if (recs) scratch_free(recs, stream);
+                        return rc;
+                    }
+                    if (!lrecs) {
+                        if (!recs) {
+                            rc = scratch_alloc(std::min(n_obj, max_obj) * rw * 4, stream, reinterpret_cast<void**>(&recs));
+                            if (rc) return rc;
+                        }
+                        hipError_t e = launch_odd_objrec(K1, R, m, c, recs, stream);
+                        if (e != hipSuccess) {
+                            scratch_free(recs, stream);
+                            return hip_fail(e, "launch gf_odd_objrec");
+                        }
+                        lrecs = recs;
                     }
                 }
                 c.tiles_per_obj = (uint32_t)tpo;
@@ -226,13 +322,13 @@ static int odd_launches(const PassArgs& a, int K, int R, int mode, bool accumula
                 const uint64_t cap = (uint64_t)cus * (uint64_t)odd_blocks_per_cu(m, K1, R, false, use_rec, xs);
                 int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, cap));
                 if (g_grid_cap > 0) grid = std::min(grid, g_grid_cap);
-                hipError_t e = launch_odd(K1, R, m, c, flags ? flags + o0 : nullptr, recs, grid, stream, xs);
+                hipError_t e = launch_odd(K1, R, m, c, flags ? flags + o0 : nullptr, lrecs, grid, stream, xs);
                 if (e != hipSuccess) {
-                    scratch_free(recs, stream);
+                    if (recs) scratch_free(recs, stream);
                     return hip_fail(e, "launch gf_odd");
                 }
             }
-            scratch_free(recs, stream);
+            if (recs) scratch_free(recs, stream);
         }
     }
     // the guard-band bytes of every shard, all K inputs of the pass at once
@@ -1472,3 +1568,25 @@ int hbec_kernel_info(int k, int r, uint64_t shard_len, int* tile_bytes, int* kin
 }
 
 }  // extern "C"
+
+extern "C" int hbec_odd_record_cache(int clear, uint64_t* entries, uint64_t* hits) {
+    return hbec::guarded("hbec_odd_record_cache", [&]() -> int {
+        ObjRecCache& C = objrec_cache();
+        std::lock_guard<std::mutex> lk(C.mu);
+        if (clear) {
+            hipError_t e = hipDeviceSynchronize();
+            if (e != hipSuccess) return hip_fail(e, "hipDeviceSynchronize (record cache)");
+            for (auto& x : C.entries) {
+                if (x.ev) (void)hipEventDestroy(x.ev);
+                if (x.d) (void)hipFree(x.d);
+            }
+            C.entries.clear();
+            C.seen.clear();
+            C.bytes = 0;
+            C.hits = 0;
+        }
+        if (entries) *entries = C.entries.size();
+        if (hits) *hits = C.hits;
+        return HBEC_OK;
+    });
+}

@@ -364,6 +364,13 @@ int hbec_odd_path_stats(uint64_t* bitplane, uint64_t* records, uint64_t* strided
  * Either pointer may be NULL. */
 int hbec_odd_edge_stats(uint64_t* edge_launches, uint64_t* fused_launches);
 
+/* The per-object records of strided record passes (gf_odd_rec) are kept for
+ * views coded again (cached on a view set's second sighting; at most 16 sets,
+ * 64 MiB).  Reports the cached sets and the calls that reused one; clear != 0
+ * (a test hook: no call may be in flight on any stream) synchronises the
+ * device and drops them.  Either pointer may be NULL. */
+int hbec_odd_record_cache(int clear, uint64_t* entries, uint64_t* hits);
+
 /* ---------------------------------------------------------------------------
  * ecutils.go stripe loops over io callbacks (objectserver/ecutils.go:14-186,
  * objectserver/ecobj.go:82-98, :814-824).

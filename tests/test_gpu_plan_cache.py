@@ -67,3 +67,55 @@ def test_plan_records_reused_across_calls_patterns_and_streams(k, m):
         plan.reconstruct(present)
         torch.cuda.synchronize()
         assert torch.equal(data, keep_d) and torch.equal(parity, keep_p), lost
+
+
+# Strided record passes keep the per-object records of views they code again
+# (hbec.cpp objrec_cached: cached on a key's second sighting), chunked
+# launches included (hbec_set_odd_chunk_tiles).
+@pytest.mark.parametrize("k,m,s,chunk", [(8, 3, 8191, 0), (10, 4, 8193, 0), (8, 3, 8191, 60)])
+def test_strided_records_reused_across_calls_and_streams(k, m, s, chunk):
+    n = 40
+    pitch = (k + m) * s + 9
+    buf = torch.empty(3 + n * pitch + 64, dtype=torch.uint8, device="cuda")
+    views = [(buf.data_ptr() + 3 + i * s, pitch) for i in range(k + m)]
+    enc = RS.New(k, m)
+    rows = CO.build_matrix(k, m)[k:]
+    side = torch.cuda.Stream()
+    B.set_odd_chunk_tiles(chunk)
+    B.odd_record_cache(clear=True)
+    try:
+        for rep in range(4):
+            B.fill_splitmix(buf.view(1, -1), buf.numel(), first=500 + rep)
+            p0 = B.odd_path_stats()
+            if rep == 2:
+                torch.cuda.synchronize()
+                with torch.cuda.stream(side):
+                    B.encode_views(enc, views, n, s, stream=side)
+                side.synchronize()
+            else:
+                B.encode_views(enc, views, n, s)
+            torch.cuda.synchronize()
+            p1 = B.odd_path_stats()
+            launches = sum(p1[x] - p0[x] for x in ("bitplane", "records", "strided"))
+            got = buf.cpu().numpy()
+            for o in range(n):
+                b = 3 + o * pitch
+                want = CO.apply(rows, [got[b + j * s:b + (j + 1) * s] for j in range(k)])
+                for r in range(m):
+                    assert np.array_equal(got[b + (k + r) * s:b + (k + r + 1) * s], want[r]), (rep, o, r)
+        entries, hits = B.odd_record_cache()
+        assert launches >= (2 if chunk else 1)
+        assert entries == launches and hits == 2 * launches, (entries, hits)  # built on call 2, reused on 3 and 4
+        flags = torch.zeros(n, dtype=torch.int32, device="cuda")
+        for rep in range(3):  # Verify's own records, cached from the second call
+            flags.zero_()
+            hit = {5 + rep: (k, 1), 30 - rep: (1, s - 2)}
+            for o, (i, p) in hit.items():
+                buf[3 + o * pitch + i * s + p] ^= 0x11
+            B.verify_views(enc, views, n, s, flags)
+            torch.cuda.synchronize()
+            assert flags.nonzero().flatten().tolist() == sorted(hit), rep
+            for o, (i, p) in hit.items():
+                buf[3 + o * pitch + i * s + p] ^= 0x11
+    finally:
+        B.set_odd_chunk_tiles(0)
